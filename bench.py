@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Headline benchmark: wall-clock SVM training time to tol=1e-3 on the MNIST
+even/odd shape (60000 x 784, RBF, C=10, gamma=0.25) — BASELINE.json's metric.
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+One "step" = one complete training run from alpha = 0 to convergence: state
+init, the resident Gram shard (MFMA GEMM) and the device-resident SMO loop —
+the reference's timed region (svmTrainMain.cpp:206-314) plus the kernel-row
+work it does inside that loop.  X upload / |x|^2 / cache allocation (the
+reference's untimed setup, svmTrainMain.cpp:194-202) happen once, before.
+W untimed warmup runs, then K timed runs bracketed by barrier + device sync;
+the per-run time is the MAX over ranks.  Data: synthetic MNIST-shape (no
+dataset or network on the box), identical on every rank (seeded).
+Strong scaling: the problem is fixed, ranks split the rows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_1GPU_S = 137.0   # README.md:23 (1x GTX 780)
+BASELINE_MULTI_S = 46.0   # README.md:23 (10 GPUs, OpenMPI over Ethernet)
+METRIC = "wall-clock training time (s) to tol=1e-3, MNIST even-odd RBF, at 1/2/4/8 MI355X"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--data", default="mnist", help="synthetic generator (mnist = BASELINE headline shape)")
+    ap.add_argument("--samples", type=int, default=60000)
+    ap.add_argument("--features", type=int, default=784)
+    ap.add_argument("--C", type=float, default=10.0)
+    ap.add_argument("--gamma", type=float, default=0.25)
+    ap.add_argument("--eps", type=float, default=1e-3)
+    ap.add_argument("--max-iter", type=int, default=150000)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cache-lines", type=int, default=0)
+    ap.add_argument("--x-mode", default="auto")
+    ap.add_argument("--graph-block", type=int, default=64)
+    ap.add_argument("--comm", default="auto", help="auto | rccl | gloo")
+    ap.add_argument("--device", default="auto", help="auto | cuda | cpu")
+    ap.add_argument("--no-accuracy", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from dpsvm_amd import SVCConfig
+    from dpsvm_amd._native import load
+    from dpsvm_amd.parallel import init_distributed, make_comm, shutdown
+    from dpsvm_amd.utils.datasets import synthetic
+
+    C = load()
+    ctx = init_distributed(device=a.device)
+    on_gpu = ctx.device.startswith("cuda")
+    if ctx.world != a.gpus and ctx.rank == 0:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
+    n_ranks = ctx.world
+
+    X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
+    cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines,
+                    x_mode=a.x_mode, graph_block=a.graph_block)
+    params = cfg.to_native(X.shape[1])
+    comm = make_comm(ctx, a.comm)
+
+    def barrier():
+        if n_ranks > 1:
+            dist.barrier()
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    if on_gpu:
+        solver = C.GpuSolver(params, comm, ctx.local_rank)
+        info = solver.setup(X, X.shape[0], y)
+        run = lambda: solver.solve()  # noqa: E731
+    else:
+        info = {"device_name": "cpu", "x_replicated": True, "cache_lines": 0}
+        run = lambda: C.solve_cpu(X, y, params, comm if n_ranks > 1 else None)  # noqa: E731
+
+    for _ in range(a.warmup):
+        run()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    results = [run() for _ in range(a.steps)]
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    per_run = elapsed / max(1, a.steps)
+    solve_s = [r[1]["t_solve"] for r in results]
+    t = torch.tensor([per_run, max(solve_s), min(solve_s)], dtype=torch.float64)
+    if n_ranks > 1:
+        t[2] = -t[2]
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t[2] = -t[2]
+    per_run, solve_max, solve_min = t.tolist()
+    alpha, res = results[-1]
+    acc = None
+    if not a.no_accuracy and on_gpu:
+        acc = float(solver.train_accuracy(alpha, res["b"]))
+    nsv = int((alpha > 0).sum())
+
+    if ctx.rank == 0:
+        base = BASELINE_1GPU_S if n_ranks == 1 else BASELINE_MULTI_S
+        out = {
+            "metric": METRIC,
+            "value": round(per_run, 6),
+            "unit": "s",
+            "n_gpus": n_ranks,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(per_run * 1000.0, 3),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": round(per_run / base, 6),
+            "speedup_vs_baseline": round(base / per_run, 2),
+            "baseline_s": base,
+            "dtype": "fp32",
+            "data": f"synthetic {a.data}-shape {a.samples}x{a.features} (seed {a.seed}; pixel-like [0,1] features, random +/-1 labels)",
+            "config": {
+                "model": f"RBF C-SVM, modified SMO (C={a.C:g}, gamma={a.gamma:g}, tol={a.eps:g})",
+                "global_batch": a.samples,
+                "seq_len": a.features,
+                "parallelism": f"dp{n_ranks}",
+            },
+            "iterations": int(res["iters"]),
+            "converged": bool(res["converged"]),
+            "n_sv": nsv,
+            "b": res["b"],
+            "train_accuracy": acc,
+            "smo_loop_s_min": round(solve_min, 6),
+            "smo_loop_s_max": round(solve_max, 6),
+            "iters_per_s": round(res["iters"] / max(solve_max, 1e-9), 1),
+            "device": info.get("device_name", ""),
+            "x_replicated": bool(info.get("x_replicated", True)),
+            "cache_lines": int(info.get("cache_lines", 0)),
+            "comm": getattr(comm, "name", "local"),
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    del comm
+    shutdown(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

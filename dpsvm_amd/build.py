@@ -1,0 +1,167 @@
+"""Build the native core for MI355X (gfx950) in-tree.
+
+Products (all git-ignored, shipped to the GPU box with the snapshot):
+  dpsvm_amd/_C<EXT_SUFFIX>   pybind11 module (solver, kernels, comm, I/O)
+  bin/svmTrain               distributed trainer CLI  (reference: svmTrainMain.cpp)
+  bin/svmTest                predictor CLI            (reference: seq_test.cpp / Makefile:104)
+  bin/svmSeq                 CPU trainer CLI          (reference: seq.cpp)
+  bin/dpsvm_unit             native unit tests (CTest-style, run by pytest)
+
+Usage:  python -m dpsvm_amd.build [-j N] [--force] [--debug] [--asan]
+Everything is compiled by hipcc (ROCm 7.2) with --offload-arch=gfx950; .cpp files
+are host-only C++20, .hip files carry the device code.  Incremental: an object
+is rebuilt when its source or any header under csrc/ is newer.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build"
+BIN = ROOT / "bin"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+
+LIB_SOURCES = [
+    "io/csv.cpp",
+    "io/model_io.cpp",
+    "io/synth.cpp",
+    "comm/comm_host.cpp",
+    "comm/comm_rccl.cpp",
+    "solver/smo_cpu.cpp",
+    "solver/checkpoint.cpp",
+    "solver/smo_gpu.hip",
+    "kernels/smo_kernels.hip",
+    "kernels/rbf_gemm.hip",
+]
+CLI = {
+    "svmTrain": "cli/svm_train.cpp",
+    "svmTest": "cli/svm_test.cpp",
+    "svmSeq": "cli/svm_seq.cpp",
+    "dpsvm_unit": "cli/unit_tests.cpp",
+}
+BINDINGS = "python/bindings.cpp"
+
+
+def hipcc() -> str:
+    p = ROCM / "bin" / "hipcc"
+    return str(p) if p.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def module_path() -> Path:
+    return PKG / ("_C" + ext_suffix())
+
+
+def _headers_mtime() -> float:
+    m = 0.0
+    for p in CSRC.rglob("*"):
+        if p.suffix in (".hpp", ".h", ".cuh"):
+            m = max(m, p.stat().st_mtime)
+    return m
+
+
+def _flags(debug: bool, asan: bool) -> list[str]:
+    f = ["-std=c++20", "-fPIC", f"-I{CSRC / 'include'}", f"-I{CSRC}", f"-I{ROCM / 'include'}",
+         "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
+    f += ["-O0", "-g"] if debug else ["-O3"]
+    if asan:
+        # host-only sanitizer: GPU ASan/xnack+ is not available on this pool
+        f += ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+    return f
+
+
+def _compile(src: Path, obj: Path, flags: list[str], extra: list[str], force: bool, hdr_m: float) -> str:
+    if (not force and obj.exists() and obj.stat().st_mtime >= src.stat().st_mtime
+            and obj.stat().st_mtime >= hdr_m):
+        return f"up-to-date {src.name}"
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    if src.suffix == ".hip":
+        cmd = [hipcc(), "-x", "hip", f"--offload-arch={ARCH}"] + flags + extra + ["-c", str(src), "-o", str(obj)]
+    else:
+        cmd = [hipcc(), "-x", "c++", "-D__HIP_PLATFORM_AMD__"] + flags + extra + ["-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return f"compiled {src.name}"
+
+
+def _link(out: Path, objs: list[Path], shared: bool, flags: list[str]) -> None:
+    out.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [hipcc(), f"--offload-arch={ARCH}"] + [str(o) for o in objs] + ["-o", str(out)]
+    if shared:
+        cmd += ["-shared"]
+    cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lpthread", f"-Wl,-rpath,{ROCM / 'lib'}"]
+    cmd += [x for x in flags if x.startswith("-Xarch_host") or x.startswith("-fsanitize")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {out}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build(jobs: int | None = None, force: bool = False, debug: bool = False, asan: bool = False,
+          verbose: bool = False, clis: bool = True) -> Path:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    flags = _flags(debug, asan)
+    tag = ("dbg" if debug else "rel") + ("-asan" if asan else "")
+    objdir = BUILD / tag
+    hdr_m = _headers_mtime()
+    import pybind11
+
+    py_inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    tasks = [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in LIB_SOURCES]
+    tasks.append((CSRC / BINDINGS, objdir / "bindings.o", py_inc + ["-fvisibility=hidden"]))
+    if clis:
+        tasks += [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in CLI.values()]
+    with ThreadPoolExecutor(jobs) as ex:
+        futs = [ex.submit(_compile, s, o, flags, e, force, hdr_m) for s, o, e in tasks]
+        for f in futs:
+            msg = f.result()
+            if verbose:
+                print(msg, flush=True)
+    lib_objs = [objdir / (s.replace("/", "_") + ".o") for s in LIB_SOURCES]
+    mod = module_path() if not (debug or asan) else objdir / ("_C" + ext_suffix())
+    newest = max(o.stat().st_mtime for o in lib_objs + [objdir / "bindings.o"])
+    if force or not mod.exists() or mod.stat().st_mtime < newest:
+        _link(mod, lib_objs + [objdir / "bindings.o"], True, flags)
+        if verbose:
+            print(f"linked {mod}")
+    if clis:
+        bindir = BIN if not (debug or asan) else objdir / "bin"
+        for name, src in CLI.items():
+            o = objdir / (src.replace("/", "_") + ".o")
+            out = bindir / name
+            if force or not out.exists() or out.stat().st_mtime < max(newest, o.stat().st_mtime):
+                _link(out, lib_objs + [o], False, flags)
+                if verbose:
+                    print(f"linked {out}")
+    return mod
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-only AddressSanitizer build (build/<tag>/bin)")
+    ap.add_argument("--no-cli", action="store_true")
+    ap.add_argument("-q", "--quiet", action="store_true")
+    a = ap.parse_args(argv)
+    mod = build(a.jobs, a.force, a.debug, a.asan, verbose=not a.quiet, clis=not a.no_cli)
+    print(f"dpsvm_amd native build OK ({ARCH}): {mod}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

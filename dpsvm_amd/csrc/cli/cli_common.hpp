@@ -1,0 +1,226 @@
+// Shared CLI plumbing: option parsing, data loading, metrics JSON.
+// Flag surface follows the reference (svmTrainMain.cpp:22-136, seq.cpp:47-155,
+// seq_test.cpp:36-124); new flags are long-only.
+#pragma once
+
+#include <getopt.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/io.hpp"
+#include "dpsvm/solver.hpp"
+
+namespace dpsvm {
+namespace cli {
+
+struct Options {
+  int num_att = -1;
+  int64_t num_ex = -1;
+  std::string file, model;
+  SolverParams p;
+  bool gamma_set = false;
+  bool legacy_gamma = false;  // integer 1/d like the reference (== 0 for d > 1)
+  // new
+  int gpus = 1;               // one GPU per rank (threads, ncclCommInitAll)
+  int ranks = 0;              // simulated ranks on one device (ThreadComm)
+  int device = 0;
+  bool cpu = false;
+  std::string synthetic;      // generator name instead of -f
+  uint64_t seed = 0;
+  std::string metrics_json;
+  std::string resume;
+  int precision = 9;
+  bool legacy_model = false;  // write/read the seq format (no b line)
+  bool quiet = false;
+  bool skip_accuracy = false;
+};
+
+inline void usage_train(const char* prog, bool seq) {
+  std::cerr << "   Command Line (" << prog << "):\n\n"
+               "   -a/--num-att        :  [REQUIRED] The number of attributes /features\n"
+               "   -x/--num-ex         :  [REQUIRED] The number of training examples\n"
+               "   -f/--file-path      :  [REQUIRED] Path to the training file (or --synthetic)\n"
+               "   -c/--cost           :  Parameter c of the SVM (default 1)\n"
+               "   -g/--gamma          :  Parameter gamma of the radial basis function: exp(-gamma*|u-v|^2)\n"
+               "                          (default: 1.0/num-att; --legacy-gamma: integer 1/num-att)\n"
+               "   -e/--epsilon        :  Tolerance of termination criterion (default 0.001)\n"
+               "   -n/--max-iter       :  Maximum number of iterations (default 150,000)\n"
+               "   -m/--model          :  [REQUIRED] Path of model to be saved\n";
+  if (!seq) std::cerr << "   -s/--cache-size     :  Size of cache (num cache lines; default: fill HBM)\n";
+  std::cerr << "\n   MI355X extensions:\n"
+               "   -p/--gpus N         :  ranks = GPUs of this node (RCCL over xGMI)\n"
+               "   --ranks N           :  simulate N ranks on one device (in-process comm)\n"
+               "   --cpu               :  CPU solver\n"
+               "   --device N          :  GPU for a single-rank run\n"
+               "   --synthetic NAME    :  mnist | mnist-parity | adult | covtype | blobs | uniform\n"
+               "   --seed N            :  synthetic seed (default 0)\n"
+               "   --clip MODE         :  independent (reference) | box (LIBSVM joint box)\n"
+               "   --cache-mb MB       :  device cache budget\n"
+               "   --x-mode MODE       :  auto | replicated | partitioned\n"
+               "   --spec N            :  speculative kernel rows per X pass (LRU mode, default 14)\n"
+               "   --graph-block N     :  SMO iterations per hipGraph (default 64); --no-graph\n"
+               "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
+               "   --metrics-json PATH :  run summary\n"
+               "   --log-every N       :  progress line every N iterations\n"
+               "   --precision N       :  model-file significant digits (reference: 6; default 9)\n"
+               "   --legacy-model      :  write the seq model format (no b line)\n"
+               "   --skip-accuracy     :  do not compute the training accuracy\n";
+  exit(-1);
+}
+
+inline Options parse_train(int argc, char** argv, bool seq) {
+  Options o;
+  enum {
+    OPT_RANKS = 1000, OPT_CPU, OPT_DEVICE, OPT_SYN, OPT_SEED, OPT_CLIP, OPT_CMB, OPT_XMODE, OPT_SPEC,
+    OPT_GB, OPT_NOGRAPH, OPT_CK, OPT_CKE, OPT_RESUME, OPT_METRICS, OPT_LOG, OPT_PREC, OPT_LEGM,
+    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE
+  };
+  static struct option longopts[] = {
+      {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
+      {"cost", required_argument, 0, 'c'},        {"gamma", required_argument, 0, 'g'},
+      {"file-path", required_argument, 0, 'f'},   {"epsilon", required_argument, 0, 'e'},
+      {"max-iter", required_argument, 0, 'n'},    {"model", required_argument, 0, 'm'},
+      {"cache-size", required_argument, 0, 's'},  {"gpus", required_argument, 0, 'p'},
+      {"ranks", required_argument, 0, OPT_RANKS}, {"cpu", no_argument, 0, OPT_CPU},
+      {"device", required_argument, 0, OPT_DEVICE}, {"synthetic", required_argument, 0, OPT_SYN},
+      {"seed", required_argument, 0, OPT_SEED},   {"clip", required_argument, 0, OPT_CLIP},
+      {"cache-mb", required_argument, 0, OPT_CMB}, {"x-mode", required_argument, 0, OPT_XMODE},
+      {"spec", required_argument, 0, OPT_SPEC},   {"graph-block", required_argument, 0, OPT_GB},
+      {"no-graph", no_argument, 0, OPT_NOGRAPH},  {"checkpoint", required_argument, 0, OPT_CK},
+      {"checkpoint-every", required_argument, 0, OPT_CKE}, {"resume", required_argument, 0, OPT_RESUME},
+      {"metrics-json", required_argument, 0, OPT_METRICS}, {"log-every", required_argument, 0, OPT_LOG},
+      {"precision", required_argument, 0, OPT_PREC}, {"legacy-model", no_argument, 0, OPT_LEGM},
+      {"legacy-gamma", no_argument, 0, OPT_LEGG}, {"quiet", no_argument, 0, OPT_QUIET},
+      {"skip-accuracy", no_argument, 0, OPT_SKIPACC}, {"verbose", no_argument, 0, OPT_VERBOSE},
+      {0, 0, 0, 0}};
+  while (true) {
+    int idx = 0;
+    int c = getopt_long(argc, argv, seq ? "a:x:c:g:f:e:n:m:p:" : "a:x:c:g:f:e:n:m:s:p:", longopts, &idx);
+    if (c == -1) break;
+    switch (c) {
+      case 'a': o.num_att = atoi(optarg); break;
+      case 'x': o.num_ex = atoll(optarg); break;
+      case 'c': o.p.C = (float)atof(optarg); break;
+      case 'g': o.p.gamma = (float)atof(optarg); o.gamma_set = true; break;
+      case 'f': o.file = optarg; break;
+      case 'e': o.p.eps = (float)atof(optarg); break;
+      case 'n': o.p.max_iter = atoll(optarg); break;
+      case 'm': o.model = optarg; break;
+      case 's': o.p.cache_lines = atoll(optarg); break;
+      case 'p': o.gpus = atoi(optarg); break;
+      case OPT_RANKS: o.ranks = atoi(optarg); break;
+      case OPT_CPU: o.cpu = true; break;
+      case OPT_DEVICE: o.device = atoi(optarg); break;
+      case OPT_SYN: o.synthetic = optarg; break;
+      case OPT_SEED: o.seed = strtoull(optarg, nullptr, 10); break;
+      case OPT_CLIP:
+        if (std::string(optarg) == "box") o.p.clip = ClipMode::Box;
+        else if (std::string(optarg) == "independent") o.p.clip = ClipMode::Independent;
+        else usage_train(argv[0], seq);
+        break;
+      case OPT_CMB: o.p.cache_mb = atof(optarg); break;
+      case OPT_XMODE: {
+        std::string v = optarg;
+        o.p.x_mode = v == "replicated" ? 1 : v == "partitioned" ? 2 : 0;
+        break;
+      }
+      case OPT_SPEC: o.p.spec_rows = atoi(optarg); break;
+      case OPT_GB: o.p.graph_block = atoi(optarg); break;
+      case OPT_NOGRAPH: o.p.use_graph = false; break;
+      case OPT_CK: o.p.checkpoint_path = optarg; break;
+      case OPT_CKE: o.p.checkpoint_every = atoll(optarg); break;
+      case OPT_RESUME: o.resume = optarg; break;
+      case OPT_METRICS: o.metrics_json = optarg; break;
+      case OPT_LOG: o.p.log_every = atoi(optarg); break;
+      case OPT_PREC: o.precision = atoi(optarg); break;
+      case OPT_LEGM: o.legacy_model = true; break;
+      case OPT_LEGG: o.legacy_gamma = true; break;
+      case OPT_QUIET: o.quiet = true; break;
+      case OPT_SKIPACC: o.skip_accuracy = true; break;
+      case OPT_VERBOSE: o.p.verbose = true; break;
+      default:
+        std::cerr << "\nERROR: Unknown option: -" << (char)c << "\n";
+        usage_train(argv[0], seq);
+    }
+  }
+  if ((o.file.empty() && o.synthetic.empty()) || o.model.empty()) {
+    std::cerr << "Enter a valid file name\n";
+    usage_train(argv[0], seq);
+  }
+  if (o.num_att <= 0 || o.num_ex <= 0) {
+    std::cerr << "Missing a required parameter, or invalid parameter\n";
+    usage_train(argv[0], seq);
+  }
+  if (!o.gamma_set || o.p.gamma < 0) {
+    // reference: `1 / num_attributes` in int arithmetic
+    o.p.gamma = o.legacy_gamma ? (float)(1 / o.num_att) : 1.0f / (float)o.num_att;
+  }
+  if (o.p.cache_lines == 1) o.p.cache_lines = 2;  // two lines in flight
+  return o;
+}
+
+inline Dataset load_data(const Options& o, int64_t row0 = 0, int64_t rows = -1) {
+  if (!o.synthetic.empty())
+    return make_synthetic(synth_from_name(o.synthetic), o.num_ex, o.num_att, o.seed, row0, rows);
+  if (rows >= 0) return read_csv_rows(o.file, row0, rows, o.num_att);
+  return read_csv(o.file, o.num_ex, o.num_att);
+}
+
+inline std::string json_escape(const std::string& s) {
+  std::string r;
+  for (char c : s) {
+    if (c == '"' || c == '\\') r += '\\';
+    r += c;
+  }
+  return r;
+}
+
+inline void write_metrics(const std::string& path, const Options& o, const SolveResult& r, int64_t n, int d,
+                          int64_t nsv, double acc, const std::string& backend, const std::string& device,
+                          double t_load) {
+  FILE* fp = fopen(path.c_str(), "w");
+  if (!fp) {
+    std::cerr << "cannot write metrics " << path << "\n";
+    return;
+  }
+  fprintf(fp,
+          "{\"backend\": \"%s\", \"device\": \"%s\", \"world\": %d, \"n\": %lld, \"d\": %d, \"C\": %g, "
+          "\"gamma\": %g, \"eps\": %g, \"clip\": \"%s\", \"iterations\": %lld, \"status\": %d, "
+          "\"converged\": %s, \"b\": %.9g, \"b_hi\": %.9g, \"b_lo\": %.9g, \"n_sv\": %lld, "
+          "\"train_accuracy\": %.9g, \"t_load_s\": %.6f, \"t_setup_s\": %.6f, \"t_solve_s\": %.6f, "
+          "\"iters_per_s\": %.3f, \"cache_lines\": %lld, \"cache_hits\": %lld, \"cache_misses\": %lld, "
+          "\"rows_computed\": %lld, \"x_passes\": %lld, \"spec_rows\": %lld, \"data\": \"%s\"}\n",
+          backend.c_str(), json_escape(device).c_str(), r.world, (long long)n, d, o.p.C, o.p.gamma, o.p.eps,
+          o.p.clip == ClipMode::Box ? "box" : "independent", (long long)r.iters, r.status,
+          r.converged() ? "true" : "false", r.b, r.b_hi, r.b_lo, (long long)nsv, acc, t_load, r.t_setup,
+          r.t_solve, r.t_solve > 0 ? r.iters / r.t_solve : 0.0, (long long)r.cache_lines,
+          (long long)r.cache_hits, (long long)r.cache_misses, (long long)r.rows_computed,
+          (long long)r.x_passes, (long long)r.spec_rows,
+          json_escape(o.synthetic.empty() ? o.file : "synthetic:" + o.synthetic).c_str());
+  fclose(fp);
+}
+
+inline void print_outcome(const SolveResult& r, float eps) {
+  std::cout << "TOTAL TIME TAKEN in seconds: " << r.t_solve << "\n";
+  if (r.status == 2 || (r.status != 1 && gap_open(r.b_hi, r.b_lo, eps))) {
+    std::cout << "Could not converge in " << r.iters << " iterations. SVM training has been stopped\n";
+  } else {
+    std::cout << "Converged at iteration number: " << r.iters << "\n";
+  }
+  if (r.status == 4) std::cout << "WARNING: non-finite b_hi/b_lo encountered; training stopped\n";
+  std::cout << "b: " << r.b << "\n";
+}
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace cli
+}  // namespace dpsvm

@@ -1,0 +1,40 @@
+// svmSeq — CPU trainer (reference: seq.cpp, the single-threaded CBLAS SMO).
+// Same flags (no -s); writes the dpsvm model format (with b) unless
+// --legacy-model, and applies b in the training accuracy.
+#include <iostream>
+
+#include "cli_common.hpp"
+
+using namespace dpsvm;
+
+int main(int argc, char** argv) {
+  cli::Options o = cli::parse_train(argc, argv, true);
+  try {
+    const double tl0 = cli::now_s();
+    Dataset ds = cli::load_data(o);
+    const double t_load = cli::now_s() - tl0;
+    std::cout << "Populated Data from input file\n";
+    std::unique_ptr<Checkpoint> resume;
+    if (!o.resume.empty()) resume = std::make_unique<Checkpoint>(read_checkpoint(o.resume));
+    ProgressFn prog = [](const Progress& p) {
+      std::cout << "Current iteration number: " << p.iter << "  b_hi " << p.b_hi << "  b_lo " << p.b_lo << "\n";
+    };
+    SolveResult r = solve_cpu(ds, o.p, nullptr, resume.get(), prog);
+    cli::print_outcome(r, o.p.eps);
+    Model mdl = make_model(ds, r.alpha, r.b, o.p.gamma);
+    double acc = -1;
+    if (!o.skip_accuracy) {
+      auto dec = decision_cpu(mdl, ds.x.data(), ds.n, ds.d);
+      acc = accuracy_from_decision(dec, ds.y.data(), ds.n);
+      std::cout << "Training accuracy: " << acc << "\n";
+    }
+    write_model(o.model, mdl, o.precision, o.legacy_model);
+    std::cout << "Training model has been saved to the file " << o.model << "\n";
+    if (!o.metrics_json.empty())
+      cli::write_metrics(o.metrics_json, o, r, ds.n, ds.d, mdl.nsv(), acc, "cpu", "cpu", t_load);
+    return 0;
+  } catch (const std::exception& e) {
+    std::cerr << "svmSeq: " << e.what() << "\n";
+    return 1;
+  }
+}

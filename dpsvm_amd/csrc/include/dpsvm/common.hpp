@@ -1,0 +1,225 @@
+// dpsvm_amd — MI355X-native distributed RBF C-SVM trainer (modified SMO).
+//
+// Shared host/device definitions: error checking, parameters, order-preserving
+// selection keys and the solver result record.
+//
+// Behavioural reference: farshid83/dpsvm
+//   - algorithm / stop test / alpha update: svmTrainMain.cpp:235-310
+//   - I-set classification:                  svmTrain.cu:41-95
+//   - defaults (eps 1e-3, C 1, 150000 iters): svmTrainMain.cpp:60-136
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#if defined(__HIPCC__)
+#define DPSVM_HD __host__ __device__ __forceinline__
+#else
+#define DPSVM_HD inline
+#endif
+
+namespace dpsvm {
+
+// ---------------------------------------------------------------------------
+// Errors
+// ---------------------------------------------------------------------------
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+[[noreturn]] inline void fail(const std::string& msg) { throw Error(msg); }
+
+#define DPSVM_CHECK(cond, msg)                                                   \
+  do {                                                                           \
+    if (!(cond)) ::dpsvm::fail(std::string("dpsvm: ") + (msg) + " [" __FILE__ ":" + \
+                               std::to_string(__LINE__) + "]");                  \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Parameters
+// ---------------------------------------------------------------------------
+enum class ClipMode : int {
+  Independent = 0,  // reference behaviour: both alphas clipped to [0,C] separately
+                    // (svmTrainMain.cpp:294-295)
+  Box = 1,          // LIBSVM-style joint [L,H] box, keeps sum(alpha*y) = 0
+};
+
+struct SolverParams {
+  float C = 1.0f;
+  float gamma = -1.0f;        // <0 -> 1/d (reference uses integer 1/d == 0)
+  float eps = 1e-3f;          // stop when !(b_lo > b_hi + 2 eps)
+  int64_t max_iter = 150000;
+  ClipMode clip = ClipMode::Independent;
+  float tau = 1e-12f;         // eta floor
+  // kernel-row cache
+  int64_t cache_lines = 0;    // explicit number of lines (0 = auto)
+  double cache_mb = 0.0;      // explicit size in MiB (0 = auto)
+  double cache_frac = 0.80;   // auto: fraction of free HBM used for lines
+  int64_t host_cache_lines = 0;  // pinned host spill tier (lines); 0 = off
+  // X-pass batching: extra speculative kernel rows computed on a miss
+  int spec_rows = 14;
+  // execution
+  int graph_block = 64;       // SMO iterations captured per hipGraph
+  bool use_graph = true;
+  int x_mode = 0;             // 0 auto, 1 replicated, 2 partitioned
+  int log_every = 0;
+  bool verbose = false;
+  // checkpoint
+  int64_t checkpoint_every = 0;
+  std::string checkpoint_path;
+  // debugging
+  bool sync_debug = false;    // device sync + error check after every launch
+};
+
+// Per-run result, gathered on every rank.
+struct SolveResult {
+  std::vector<float> alpha;   // length n (global)
+  float b = 0.f, b_hi = 0.f, b_lo = 0.f;
+  int64_t iters = 0;
+  int status = 0;             // 1 converged, 2 max_iter, 3 no violating pair, 4 non-finite
+  double t_setup = 0.0, t_solve = 0.0;
+  int64_t cache_hits = 0, cache_misses = 0, rows_computed = 0, x_passes = 0;
+  int64_t host_hits = 0, spec_rows = 0;
+  int64_t cache_lines = 0, host_cache_lines = 0;
+  int world = 1;
+  bool converged() const { return status == 1; }
+};
+
+// ---------------------------------------------------------------------------
+// Order-preserving selection keys.
+//
+// A key packs (f, global index) into one u64 so that an unsigned min over keys
+// picks the smallest f and, on ties, the lowest global index (SURVEY Q15:
+// deterministic on every rank).  b_lo = max f over I_low is encoded with -f.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kKeyNone = ~0ull;
+
+DPSVM_HD uint32_t f32_bits(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return u;
+}
+DPSVM_HD float bits_f32(uint32_t u) {
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+DPSVM_HD uint32_t f32_order(float f) {
+  uint32_t u = f32_bits(f);
+  if (u == 0x80000000u) u = 0u;  // -0 == +0
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+DPSVM_HD float order_f32(uint32_t o) {
+  uint32_t u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  return bits_f32(u);
+}
+DPSVM_HD uint64_t make_key(float f, uint32_t idx) {
+  return ((uint64_t)f32_order(f) << 32) | (uint64_t)idx;
+}
+DPSVM_HD float key_value(uint64_t k) { return order_f32((uint32_t)(k >> 32)); }
+DPSVM_HD uint32_t key_index(uint64_t k) { return (uint32_t)(k & 0xffffffffu); }
+
+// I_up / I_low membership (svmTrain.cu:56-91; seq.cpp:469-493).
+DPSVM_HD bool in_up(float a, float y, float C) {
+  if (a == 0.0f) return y == 1.0f;
+  if (a == C) return y != 1.0f;
+  return true;
+}
+DPSVM_HD bool in_low(float a, float y, float C) {
+  if (a == 0.0f) return y != 1.0f;
+  if (a == C) return y == 1.0f;
+  return true;
+}
+
+DPSVM_HD float clip01(float v, float lo, float hi) {
+  // reference clip_value (svmTrain.cu:674-682); NaN falls through unchanged
+  if (v < lo) return lo;
+  if (v > hi) return hi;
+  return v;
+}
+
+// One SMO pair update.  Shared by the CPU solver and the device finalize
+// kernel so both paths round identically.  (svmTrainMain.cpp:282-299)
+struct PairUpdate {
+  float a_hi_new, a_lo_new, c_hi, c_lo;
+};
+
+DPSVM_HD PairUpdate pair_update(float a_hi_old, float a_lo_old, float y_hi, float y_lo, float b_hi,
+                                float b_lo, float k_hl, float C, float tau, int clip_mode,
+                                bool same) {
+  float eta = (1.0f + 1.0f) - 2.0f * k_hl;  // K(hi,hi) + K(lo,lo) - 2 K(hi,lo); K(i,i) = 1
+  if (!(eta >= tau)) eta = tau;
+  float s = y_lo * y_hi;
+  float a_lo_new = a_lo_old + (y_lo * (b_hi - b_lo) / eta);
+  float a_hi_new;
+  if (clip_mode == (int)ClipMode::Box && !same) {
+    // Joint box on the line y_hi a_hi + y_lo a_lo = const.  When a_lo hits a
+    // bound that comes from a_hi's own bound, a_hi is set to that bound exactly
+    // (as LIBSVM does) so round-off cannot leave it a hair inside the box,
+    // where it would keep being selected with a zero-length step.
+    float L, H;
+    float hi_at_L, hi_at_H;  // a_hi value implied when a_lo lands on L / H (-1: none)
+    if (y_hi != y_lo) {
+      const float dl = a_lo_old - a_hi_old;
+      L = dl > 0.f ? dl : 0.f;
+      hi_at_L = dl > 0.f ? 0.f : -1.f;
+      H = C + dl < C ? C + dl : C;
+      hi_at_H = C + dl < C ? C : -1.f;
+    } else {
+      const float sm = a_lo_old + a_hi_old;
+      L = sm - C > 0.f ? sm - C : 0.f;
+      hi_at_L = sm - C > 0.f ? C : -1.f;
+      H = sm < C ? sm : C;
+      hi_at_H = sm < C ? 0.f : -1.f;
+    }
+    if (a_lo_new <= L) {
+      a_lo_new = L;
+      a_hi_new = hi_at_L >= 0.f ? hi_at_L : a_hi_old + (s * (a_lo_old - a_lo_new));
+    } else if (a_lo_new >= H) {
+      a_lo_new = H;
+      a_hi_new = hi_at_H >= 0.f ? hi_at_H : a_hi_old + (s * (a_lo_old - a_lo_new));
+    } else {
+      a_hi_new = a_hi_old + (s * (a_lo_old - a_lo_new));  // NaN-safe: NaN falls here
+    }
+    a_hi_new = clip01(a_hi_new, 0.0f, C);  // guards fp round-off only
+  } else {
+    a_hi_new = a_hi_old + (s * (a_lo_old - a_lo_new));
+    a_lo_new = clip01(a_lo_new, 0.0f, C);
+    a_hi_new = clip01(a_hi_new, 0.0f, C);
+  }
+  PairUpdate u;
+  u.a_hi_new = a_hi_new;
+  u.a_lo_new = a_lo_new;
+  u.c_hi = (a_hi_new - a_hi_old) * y_hi;
+  u.c_lo = (a_lo_new - a_lo_old) * y_lo;
+  return u;
+}
+
+// Stop test of the reference do/while tail (svmTrainMain.cpp:310).
+DPSVM_HD bool gap_open(float b_hi, float b_lo, float eps) { return b_lo > (b_hi + (2.0f * eps)); }
+
+inline float resolve_gamma(float gamma, int d) { return gamma < 0.f ? 1.0f / (float)d : gamma; }
+
+// Row padding for device X: multiples of 16 floats (one MFMA k-step of 4 lanes x float4).
+constexpr int kFeatPad = 16;
+inline int pad_features(int d) { return (d + kFeatPad - 1) / kFeatPad * kFeatPad; }
+
+// Balanced contiguous sharding (fixes SURVEY Q9: sizes differ by at most 1).
+// Reference: svmTrainMain.cpp:367-384.
+struct Shard {
+  int64_t offset = 0, size = 0;
+};
+inline Shard shard_of(int64_t n, int rank, int world) {
+  int64_t base = n / world, rem = n % world;
+  Shard s;
+  s.size = base + (rank < rem ? 1 : 0);
+  s.offset = rank * base + (rank < rem ? rank : rem);
+  return s;
+}
+
+}  // namespace dpsvm

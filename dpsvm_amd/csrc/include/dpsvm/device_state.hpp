@@ -1,0 +1,99 @@
+// Device-resident SMO state shared by the HIP kernels and the host driver.
+//
+// One SMO iteration on a rank is a short, host-free kernel chain
+//     [smo_rows]  -> smo_step -> [collective] -> smo_finalize
+// and blocks of iterations are captured into a hipGraph.  The host only polls
+// a status record in pinned host-mapped memory (SURVEY §7.1 design 1).
+// Reference per-iteration path for contrast: svmTrainMain.cpp:235-310 with >=7
+// blocking host<->device round trips (SURVEY §3.1 hot-loop cost structure).
+#pragma once
+
+#include <cstdint>
+
+namespace dpsvm {
+
+constexpr int kNQ = 16;             // kernel rows per X pass (MFMA 16x16x4 N width)
+constexpr int kStepRows = 128;      // rows per step/rows workgroup
+constexpr int kStepThreads = 256;   // 4 waves
+constexpr int kFinThreads = 1024;   // finalize: one workgroup, 16 waves
+constexpr int kRowsKC = 1024;       // k-chunk of query vectors staged in LDS
+
+enum CacheMode : int32_t {
+  kCacheDense = 0,  // whole Gram shard resident: line i == global row i
+  kCacheLRU = 1,    // LRU lines computed on demand by smo_rows
+};
+
+enum DoneCode : int32_t {
+  kRunning = 0,
+  kConverged = 1,
+  kMaxIter = 2,
+  kNoPair = 3,
+  kNonFinite = 4,
+};
+
+// Written by smo_finalize, read by the next iteration's kernels.
+struct alignas(16) SmoCtrl {
+  int32_t iter;        // SMO updates applied so far
+  int32_t done;        // DoneCode of the last finalize (0 = running)
+  int32_t final_applied;  // 1 once the step after `done` applied the last f update
+  int32_t nq;          // rows smo_rows must compute this iteration
+  int32_t i_hi, i_lo;
+  int32_t line_hi, line_lo;  // lines holding K(hi,.) / K(lo,.) for the pending update
+  float c_hi, c_lo;    // (alpha_new - alpha_old) * y, pending f-update coefficients
+  float b_hi, b_lo;    // selection values of the last finalize
+  int32_t q_idx[kNQ];  // global rows to compute
+  int32_t q_line[kNQ]; // destination lines
+  float q_sq[kNQ];     // |x_q|^2
+  const float* q_ptr[kNQ];  // query vectors (device X row, or a gathered record row)
+  // LRU (CacheLRU)
+  int32_t lru_head, lru_tail, lines_used, pad0;
+  // statistics
+  int64_t hits, misses, rows_computed, x_passes, spec_rows, spec_hits;
+};
+
+// Host-mapped status record (pinned, written by finalize thread 0).
+struct alignas(16) SmoStatus {
+  int64_t iter;
+  int32_t done;
+  int32_t seq;
+  float b_hi, b_lo;
+  int64_t hits, misses, rows_computed, x_passes, spec_rows, spec_hits;
+};
+
+// Partitioned-X candidate record: one per rank, all-gathered each iteration.
+// Row payload follows the header: x_hi[dp], x_lo[dp].
+struct alignas(16) CandRecord {
+  uint64_t key_hi, key_lo;
+};
+
+struct SmoArgs {
+  const float* x;        // device X rows [x_rows][dp] (zero padded)
+  const float* xsq;      // [n] global |x|^2
+  const float* y;        // [n] global labels (+1/-1)
+  float* alpha;          // [n] global (replicated, updated identically on every rank)
+  float* f;              // [nl] local gradient
+  float* lines;          // [L][ldl] cache lines (K values)
+  int64_t ldl;           // line stride in floats (>= G*kStepRows)
+  int32_t* slot_of;      // [n] line of a global row or -1 (LRU)
+  int32_t* key_of;       // [L] global row in a line or -1
+  int32_t* lru_prev;     // [L]
+  int32_t* lru_next;     // [L]
+  uint64_t* partials;    // [G][2] per-workgroup selection keys
+  SmoCtrl* ctrl;
+  SmoStatus* status;     // host-mapped
+  const uint8_t* records;  // partitioned: [world][rec_bytes] after all-gather
+  uint8_t* my_record;      // partitioned: this rank's record (all-gather source)
+  int64_t rec_bytes;
+  int64_t n, nl, off;
+  int64_t x_row0;        // global index of device X row 0 (0 replicated, off partitioned)
+  int32_t d, dp, G, L;
+  int32_t world;
+  int32_t cache_mode;    // CacheMode
+  int32_t partitioned;   // 1: X rows only local, query rows travel in records
+  int32_t spec;          // speculative rows per X pass (LRU, replicated)
+  int32_t clip;
+  float C, gamma, eps, tau;
+  int64_t max_iter;
+};
+
+}  // namespace dpsvm

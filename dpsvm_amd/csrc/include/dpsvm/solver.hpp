@@ -1,0 +1,121 @@
+// SMO solvers (CPU oracle + MI355X device-resident), predictors, checkpoints.
+//
+// Reference call stacks: SURVEY §3.1 (GPU/MPI svmTrain), §3.2 (CPU seq),
+// §3.3 (seq_test predictor).
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dpsvm/comm.hpp"
+#include "dpsvm/common.hpp"
+#include "dpsvm/io.hpp"
+
+namespace dpsvm {
+
+struct Progress {
+  int64_t iter;
+  float b_hi, b_lo;
+  double elapsed;
+  int64_t hits, misses;
+};
+using ProgressFn = std::function<void(const Progress&)>;
+
+// Checkpoint: everything needed to continue SMO (alpha, f, iteration, last b's).
+struct Checkpoint {
+  int64_t n = 0;
+  int d = 0;
+  float C = 0, gamma = 0, eps = 0;
+  int clip = 0;
+  int64_t iter = 0;
+  float b_hi = 0, b_lo = 0;
+  std::vector<float> alpha;  // n
+  std::vector<float> f;      // n (may be empty -> recomputed from alpha)
+};
+void write_checkpoint(const std::string& path, const Checkpoint& ck);
+Checkpoint read_checkpoint(const std::string& path);
+
+// ---------------------------------------------------------------------------
+// CPU solver (C10 seq / the no-GPU path and the test oracle).  X is replicated,
+// f and the kernel-row cache are sharded by `comm` (nullptr = one rank).
+// ---------------------------------------------------------------------------
+SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* comm = nullptr,
+                      const Checkpoint* resume = nullptr, const ProgressFn& progress = {});
+
+// Decision values d(x) = sum_sv alpha y K(sv,x) - b  (svmTrain.cu:646-658)
+std::vector<float> decision_cpu(const Model& m, const float* x, int64_t n, int d, int threads = 0);
+// fraction of rows with sign(decision) == y  (>= 0 -> +1)
+double accuracy_from_decision(const std::vector<float>& dec, const float* y, int64_t n);
+
+// ---------------------------------------------------------------------------
+// Device-resident solver (one rank = one GPU).  Implementation: smo_gpu.hip.
+// ---------------------------------------------------------------------------
+struct GpuSetupInfo {
+  int device = 0;
+  std::string device_name;
+  int64_t n = 0, n_local = 0, offset = 0;
+  int d = 0, dp = 0;
+  bool x_replicated = true;
+  int64_t cache_lines = 0, host_cache_lines = 0;
+  int blocks = 0;
+  size_t bytes_device = 0;
+};
+
+class GpuSolver {
+ public:
+  // x: host row-major [n_x][d] where n_x = n (replicated) or the rank's shard
+  // rows (partitioned, x_mode=2).  y: host, global n labels.
+  GpuSolver(const SolverParams& p, Communicator* comm, int device);
+  ~GpuSolver();
+  GpuSolver(const GpuSolver&) = delete;
+  GpuSolver& operator=(const GpuSolver&) = delete;
+
+  GpuSetupInfo setup(const float* x, int64_t n_x_rows, int64_t n, int d, const float* y);
+  SolveResult solve(const Checkpoint* resume = nullptr, const ProgressFn& progress = {});
+  // After solve(): distributed training accuracy (each rank predicts its shard)
+  double train_accuracy(const SolveResult& r);
+  // decision values for rows of a host matrix using the trained SVs (any rank)
+  std::vector<float> decision(const SolveResult& r, const float* x, int64_t n, int d);
+  const GpuSetupInfo& info() const;
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+};
+
+// Stand-alone GPU predictor (svmTest GPU path): model SVs resident on device,
+// decision values of a host or device matrix via the MFMA predict kernel.
+class GpuPredictor {
+ public:
+  GpuPredictor(const Model& m, int device);
+  ~GpuPredictor();
+  std::vector<float> decision(const float* x_host, int64_t n, int d);
+  // device pointers, stream = hipStream_t as void*
+  void decision_device(const float* x_dev, int64_t n, int d, int ld, float* out_dev, void* stream);
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+};
+
+// Low-level kernel entry points exposed for unit tests (device pointers).
+namespace kernels {
+void row_sqnorm(const float* x, int64_t n, int d, int ld, float* out, void* stream);
+// K[q][j] = exp(-gamma * max(|x_j|^2 + |w_q|^2 - 2 x_j.w_q, 0)) for q < nq <= 16
+void rbf_rows(const float* x, const float* xsq, int64_t n, int ld, const float* w, const float* wsq,
+              int nq, float gamma, float* out, int64_t out_ld, void* stream);
+// per-block selection partials over f/alpha/y (keys as in common.hpp)
+void select_partials(const float* f, const float* alpha, const float* y, int64_t n, int64_t offset,
+                     float C, uint64_t* partials, int* blocks_out, void* stream);
+void predict(const float* x, const float* xsq, int64_t n, int ld, const float* sv,
+             const float* svsq, const float* coef, int64_t nsv, int sv_ld, float gamma, float b,
+             float* dec, void* stream);
+int64_t compact_nonzero(const float* alpha, int64_t n, int* idx_out, void* stream);
+}  // namespace kernels
+
+int device_count();
+std::string device_name(int dev);
+
+}  // namespace dpsvm

@@ -1,0 +1,91 @@
+// Wave-64 / workgroup reduction helpers for CDNA4 (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dpsvm/common.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = __shfl_xor(lo, m, 64);
+  hi = __shfl_xor(hi, m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    uint64_t o = shfl_xor_u64(v, m);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// Block-wide min of two u64 keys; result valid in every thread.
+// `scratch` must hold 2*(blockDim/64) u64.
+template <int THREADS>
+__device__ __forceinline__ void block_min2_u64(uint64_t& a, uint64_t& b, uint64_t* scratch) {
+  constexpr int W = THREADS / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_min_u64(a);
+  b = wave_min_u64(b);
+  if (lane == 0) {
+    scratch[wave] = a;
+    scratch[W + wave] = b;
+  }
+  __syncthreads();
+  uint64_t ra = kKeyNone, rb = kKeyNone;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    ra = scratch[w] < ra ? scratch[w] : ra;
+    rb = scratch[W + w] < rb ? scratch[W + w] : rb;
+  }
+  a = ra;
+  b = rb;
+  __syncthreads();
+}
+
+// Deterministic block sum (fixed tree: wave shuffles then waves in order).
+template <int THREADS>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  constexpr int W = THREADS / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wave] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int w = 0; w < W; ++w) r += scratch[w];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float rbf_from_dot(float sq_a, float sq_b, float dot, float gamma) {
+  float d2 = sq_a + sq_b - 2.0f * dot;  // expansion as svmTrain.cu:128-130
+  d2 = d2 > 0.f ? d2 : 0.f;             // clamp
+  return expf(-gamma * d2);
+}
+
+}  // namespace dev
+}  // namespace dpsvm

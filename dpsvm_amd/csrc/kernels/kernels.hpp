@@ -1,0 +1,48 @@
+// Host-side launchers of the HIP kernels (implemented in *.hip under kernels/).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dpsvm/device_state.hpp"
+
+namespace dpsvm {
+namespace launch {
+
+void row_sqnorm(const float* x, int64_t n, int d, int ld, float* out, hipStream_t s);
+void init_f(const float* y, int64_t off, int64_t nl, float* f, hipStream_t s);
+void fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
+
+// One SMO iteration's kernels (see device_state.hpp)
+void smo_rows(const SmoArgs& a, hipStream_t s);
+void smo_step(const SmoArgs& a, hipStream_t s);
+void smo_local_record(const SmoArgs& a, hipStream_t s);
+void smo_finalize(const SmoArgs& a, hipStream_t s);
+size_t smo_rows_lds_bytes(int dp);
+
+// RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
+//   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)
+void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,
+                    const float* Bsq, int64_t N, int ldb, int dp, float gamma, float* out,
+                    int64_t ldo, hipStream_t s);
+// Decision values: dec[i] = sum_j coef[j] K(A_i, B_j) - b   (B = SVs, coef = alpha*y)
+//   partial: scratch [splits][M_pad] (returned by predict_scratch_floats)
+int64_t predict_scratch_floats(int64_t M, int64_t N);
+void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
+                 const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
+                 float b, float* partial, float* dec, const float* y, int32_t* correct,
+                 hipStream_t s);
+
+// SV compaction: idx_out[k] = i for the k-th alpha[i] > 0 (index order)
+// scratch: >= compact_scratch_ints(n) ints; count written to *count_dev
+int64_t compact_scratch_ints(int64_t n);
+void compact_positive(const float* alpha, int64_t n, int32_t* idx_out, int32_t* count_dev,
+                      int32_t* scratch, hipStream_t s);
+// sv[r] = x[idx[r]-x_row0], svsq[r] = xsq[idx[r]], coef[r] = alpha[idx[r]] * y[idx[r]]
+void gather_sv(const float* x, int64_t x_row0, const float* xsq, const float* alpha,
+               const float* y, const int32_t* idx, int64_t nsv, int dp, float* sv, float* svsq,
+               float* coef, hipStream_t s);
+
+}  // namespace launch
+}  // namespace dpsvm

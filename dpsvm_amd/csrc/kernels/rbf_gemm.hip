@@ -1,0 +1,249 @@
+// RBF GEMM on fp32 MFMA (v_mfma_f32_32x32x2_f32: exact f32, 64 FLOP/clk/SIMD).
+//
+// Two fused epilogues over the same LDS-tiled main loop (C = A . B^T):
+//   STORE   : out[i][j] = exp(-g * max(|a_i|^2 + |b_j|^2 - 2 c_ij, 0))
+//             -> the whole resident Gram shard in one launch (dense cache mode)
+//   PREDICT : partial[s][i] = sum_{j in split s} coef_j * exp(...)
+//             -> decision values / training accuracy in one launch.
+//             Replaces the reference's n x (cublasSgemv + thrust::transform_reduce)
+//             launches (svmTrain.cu:633-665, K12/K13).
+//
+// Tiling: 128x128 block tile, BK = 16, 256 threads = 4 waves (2x2), each wave
+// 64x64 = 2x2 MFMA 32x32 tiles (64 accumulator registers).  A/B tiles are
+// staged k-major in LDS (+4 float pad) through registers, double buffered so
+// the next tile's global loads overlap the current tile's 32 MFMAs per wave.
+// Operand maps (32x32x2 f32): A lane l -> (row l&31, k l>>5); B lane l ->
+// (k l>>5, col l&31); C reg r of lane l -> (row (r&3)+8(r>>2)+4(l>>5), col l&31).
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+constexpr int BM = 128, BN = 128, BK = 16, LDP = BM + 4;
+constexpr int GEMM_THREADS = 256;
+
+enum Epi { EPI_STORE = 0, EPI_PREDICT = 1 };
+
+template <int EPI>
+__global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
+    const float* __restrict__ A, const float* __restrict__ Asq, int64_t M, int lda,
+    const float* __restrict__ B, const float* __restrict__ Bsq, int64_t N, int ldb, int dp,
+    float gamma, float* __restrict__ out, int64_t ldo, const float* __restrict__ coef,
+    int n_tiles_per_split) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
+  __shared__ float red[2][BM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t ntiles_total = (N + BN - 1) / BN;
+  int64_t nt_begin, nt_end;
+  if (EPI == EPI_STORE) {
+    nt_begin = blockIdx.y;
+    nt_end = nt_begin + 1;
+  } else {
+    nt_begin = (int64_t)blockIdx.y * n_tiles_per_split;
+    nt_end = nt_begin + n_tiles_per_split;
+    if (nt_end > ntiles_total) nt_end = ntiles_total;
+  }
+  // staging map: 512 float4 per tile, 2 per thread: row r = idx>>2, k4 = idx&3
+  const int r_ld0 = tid >> 2, k4_ld = tid & 3;
+  const int nk = dp / BK;  // dp is a multiple of 16
+
+  float rowacc[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rowacc[i][r] = 0.f;
+
+  for (int64_t nt = nt_begin; nt < nt_end; ++nt) {
+    const int64_t n0 = nt * BN;
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const float* ga0 = A + (m0 + r_ld0) * (int64_t)lda + 4 * k4_ld;
+    const float* ga1 = ga0 + 64 * (int64_t)lda;
+    const float* gb0 = B + (n0 + r_ld0) * (int64_t)ldb + 4 * k4_ld;
+    const float* gb1 = gb0 + 64 * (int64_t)ldb;
+    f4 ra0 = *(const f4*)ga0, ra1 = *(const f4*)ga1;
+    f4 rb0 = *(const f4*)gb0, rb1 = *(const f4*)gb1;
+    auto stage = [&](int buf) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        As[buf][4 * k4_ld + c][r_ld0] = ra0[c];
+        As[buf][4 * k4_ld + c][r_ld0 + 64] = ra1[c];
+        Bs[buf][4 * k4_ld + c][r_ld0] = rb0[c];
+        Bs[buf][4 * k4_ld + c][r_ld0 + 64] = rb1[c];
+      }
+    };
+    __syncthreads();  // previous n-tile's readers are done with buffer 0
+    stage(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        const int koff = (kt + 1) * BK;
+        ra0 = *(const f4*)(ga0 + koff);
+        ra1 = *(const f4*)(ga1 + koff);
+        rb0 = *(const f4*)(gb0 + koff);
+        rb1 = *(const f4*)(gb1 + koff);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        const int kr = 2 * kk + (lane >> 5);
+        const float a0 = As[cur][kr][wm * 64 + (lane & 31)];
+        const float a1 = As[cur][kr][wm * 64 + 32 + (lane & 31)];
+        const float b0 = Bs[cur][kr][wn * 64 + (lane & 31)];
+        const float b1 = Bs[cur][kr][wn * 64 + 32 + (lane & 31)];
+        acc[0][0] = mfma32(a0, b0, acc[0][0]);
+        acc[0][1] = mfma32(a0, b1, acc[0][1]);
+        acc[1][0] = mfma32(a1, b0, acc[1][0]);
+        acc[1][1] = mfma32(a1, b1, acc[1][1]);
+      }
+      if (more) stage(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+
+    // ---- epilogue ----
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
+        const float bsq = Bsq[col];
+        float cf = 0.f;
+        if (EPI == EPI_PREDICT) cf = col < N ? coef[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int64_t row = m0 + wm * 64 + i * 32 + rl;
+          const float kv = rbf_from_dot(Asq[row], bsq, acc[i][j][r], gamma);
+          if (EPI == EPI_STORE) {
+            if (row < M && col < N) out[row * ldo + col] = kv;
+          } else {
+            rowacc[i][r] += cf * kv;
+          }
+        }
+      }
+    }
+  }
+
+  if (EPI == EPI_PREDICT) {
+    // sum over the 32 columns held by lanes with equal (lane>>5), then over wn
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = rowacc[i][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        rowacc[i][r] = v;
+      }
+    if ((lane & 31) == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          red[wn][wm * 64 + i * 32 + rl] = rowacc[i][r];
+        }
+    }
+    __syncthreads();
+    if (tid < BM) {
+      const int64_t row = m0 + tid;
+      // out = partial [splits][ldo], ldo = M_pad
+      out[(int64_t)blockIdx.y * ldo + row] = red[0][tid] + red[1][tid];
+    }
+  }
+}
+
+__global__ void predict_reduce_kernel(const float* partial, int64_t M, int64_t ldp, int splits,
+                                      float b, float* dec, const float* y, int32_t* correct) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = false;
+  if (i < M) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += partial[(int64_t)k * ldp + i];
+    const float v = s - b;  // svmTrain.cu:652
+    if (dec) dec[i] = v;
+    if (y) ok = ((v < 0.f ? -1.f : 1.f) == y[i]);
+  }
+  if (correct) {
+    const uint64_t m = __ballot(ok);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(correct, (int32_t)__popcll(m));
+  }
+}
+
+}  // namespace dev
+
+namespace launch {
+
+static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,
+                    const float* Bsq, int64_t N, int ldb, int dp, float gamma, float* out,
+                    int64_t ldo, hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  DPSVM_CHECK(dp % 16 == 0, "rbf_gemm: dp must be a multiple of 16");
+  const int64_t tm = (M + dev::BM - 1) / dev::BM, tn = (N + dev::BN - 1) / dev::BN;
+  DPSVM_CHECK(tn < 65536, "rbf_gemm_store: N too large for grid.y");
+  dev::rbf_gemm_kernel<dev::EPI_STORE><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
+      A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, out, ldo, nullptr, 1);
+  post_launch("rbf_gemm_store", s);
+}
+
+static int predict_splits(int64_t M, int64_t N) {
+  const int64_t tm = (M + dev::BM - 1) / dev::BM, tn = (N + dev::BN - 1) / dev::BN;
+  int64_t splits = (2048 + tm - 1) / tm;  // aim for >= 2048 workgroups (8 per CU)
+  if (splits > tn) splits = tn;
+  if (splits < 1) splits = 1;
+  if (splits > 4096) splits = 4096;
+  return (int)splits;
+}
+
+int64_t predict_scratch_floats(int64_t M, int64_t N) {
+  return (int64_t)predict_splits(M, std::max<int64_t>(N, 1)) * round_up(std::max<int64_t>(M, 1), dev::BM);
+}
+
+void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
+                 const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
+                 float b, float* partial, float* dec, const float* y, int32_t* correct,
+                 hipStream_t s) {
+  if (M <= 0) return;
+  DPSVM_CHECK(dp % 16 == 0, "rbf_predict: dp must be a multiple of 16");
+  const int64_t ldp = round_up(M, dev::BM);
+  int splits = 1;
+  if (N > 0) {
+    const int64_t tm = ldp / dev::BM, tn = (N + dev::BN - 1) / dev::BN;
+    splits = predict_splits(M, N);
+    const int per = (int)((tn + splits - 1) / splits);
+    splits = (int)((tn + per - 1) / per);
+    dev::rbf_gemm_kernel<dev::EPI_PREDICT><<<dim3((unsigned)tm, (unsigned)splits), dev::GEMM_THREADS, 0, s>>>(
+        A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, partial, ldp, coef, per);
+    post_launch("rbf_predict", s);
+  } else {
+    HIP_CHECK(hipMemsetAsync(partial, 0, sizeof(float) * ldp, s));
+  }
+  dev::predict_reduce_kernel<<<dim3((unsigned)((M + 255) / 256)), 256, 0, s>>>(partial, M, ldp, splits, b,
+                                                                             dec, y, correct);
+  post_launch("predict_reduce", s);
+}
+
+}  // namespace launch
+}  // namespace dpsvm

@@ -1,0 +1,407 @@
+// pybind11 bindings of the native core (module dpsvm_amd._C).
+//
+// Host arrays cross as numpy float32 (zero-copy where C-contiguous); device
+// tensors cross as raw pointers + a hipStream_t handle (torch tensors'
+// data_ptr() / torch.cuda.current_stream().cuda_stream), so this module has
+// no compile-time dependency on torch.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "dpsvm/comm.hpp"
+#include "dpsvm/common.hpp"
+#include "dpsvm/io.hpp"
+#include "dpsvm/solver.hpp"
+
+namespace py = pybind11;
+using namespace dpsvm;
+
+namespace {
+
+using F32 = py::array_t<float, py::array::c_style | py::array::forcecast>;
+
+py::array_t<float> to_np(const std::vector<float>& v) {
+  py::array_t<float> a((py::ssize_t)v.size());
+  if (!v.empty()) memcpy(a.mutable_data(), v.data(), v.size() * 4);
+  return a;
+}
+py::array_t<float> to_np2(const std::vector<float>& v, int64_t rows, int cols) {
+  py::array_t<float> a({(py::ssize_t)rows, (py::ssize_t)cols});
+  if (!v.empty()) memcpy(a.mutable_data(), v.data(), v.size() * 4);
+  return a;
+}
+std::vector<float> from_np(const F32& a) { return std::vector<float>(a.data(), a.data() + a.size()); }
+
+void check_xy(const F32& x, const F32& y, int64_t& n, int& d) {
+  if (x.ndim() != 2) throw py::value_error("x must be 2-D (n, d)");
+  n = x.shape(0);
+  d = (int)x.shape(1);
+  if (y.ndim() != 1 || y.shape(0) != n) throw py::value_error("y must be 1-D with len(y) == x.shape[0]");
+}
+
+// Communicator backed by Python callables (torch.distributed / gloo, tests).
+class CallbackComm final : public Communicator {
+ public:
+  CallbackComm(int rank, int size, py::function ar_min_u64, py::function ar_sum_f64, py::function ar_sum_f32,
+               py::function allgather, py::function broadcast, py::function barrier)
+      : rank_(rank), size_(size), min_(ar_min_u64), sum64_(ar_sum_f64), sum32_(ar_sum_f32),
+        ag_(allgather), bc_(broadcast), bar_(barrier) {}
+  ~CallbackComm() override {
+    py::gil_scoped_acquire g;
+    min_ = py::function(); sum64_ = py::function(); sum32_ = py::function();
+    ag_ = py::function(); bc_ = py::function(); bar_ = py::function();
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  bool device_memory() const override { return false; }
+  std::string name() const override { return "callback"; }
+  void allreduce_min_u64(uint64_t* buf, size_t count, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    py::array_t<uint64_t> a({(py::ssize_t)count}, {8}, buf, py::none());
+    min_(a);
+  }
+  void allreduce_sum_f64(double* buf, size_t count, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    py::array_t<double> a({(py::ssize_t)count}, {8}, buf, py::none());
+    sum64_(a);
+  }
+  void allreduce_sum_f32(float* buf, size_t count, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    py::array_t<float> a({(py::ssize_t)count}, {4}, buf, py::none());
+    sum32_(a);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    py::array_t<uint8_t> s({(py::ssize_t)bytes}, {1}, (const uint8_t*)send, py::none());
+    py::array_t<uint8_t> r({(py::ssize_t)(bytes * size_)}, {1}, (uint8_t*)recv, py::none());
+    // the send block may alias recv: hand Python a copy
+    py::array_t<uint8_t> sc((py::ssize_t)bytes);
+    memcpy(sc.mutable_data(), send, bytes);
+    ag_(sc, r);
+    (void)s;
+  }
+  void broadcast(void* buf, size_t bytes, int root, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    py::array_t<uint8_t> a({(py::ssize_t)bytes}, {1}, (uint8_t*)buf, py::none());
+    bc_(a, root);
+  }
+  void barrier() override {
+    py::gil_scoped_acquire g;
+    bar_();
+  }
+
+ private:
+  int rank_, size_;
+  py::function min_, sum64_, sum32_, ag_, bc_, bar_;
+};
+
+py::dict result_dict(const SolveResult& r) {
+  py::dict d;
+  d["b"] = r.b;
+  d["b_hi"] = r.b_hi;
+  d["b_lo"] = r.b_lo;
+  d["iters"] = r.iters;
+  d["status"] = r.status;
+  d["converged"] = r.converged();
+  d["t_setup"] = r.t_setup;
+  d["t_solve"] = r.t_solve;
+  d["cache_hits"] = r.cache_hits;
+  d["cache_misses"] = r.cache_misses;
+  d["rows_computed"] = r.rows_computed;
+  d["x_passes"] = r.x_passes;
+  d["spec_rows"] = r.spec_rows;
+  d["cache_lines"] = r.cache_lines;
+  d["world"] = r.world;
+  return d;
+}
+
+ProgressFn wrap_progress(py::object cb) {
+  if (cb.is_none()) return {};
+  py::function fn = cb;
+  return [fn](const Progress& p) {
+    py::gil_scoped_acquire g;
+    fn(p.iter, p.b_hi, p.b_lo, p.elapsed, p.hits, p.misses);
+  };
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "dpsvm_amd native core: MI355X modified-SMO RBF C-SVM";
+
+  py::register_exception<Error>(m, "NativeError", PyExc_RuntimeError);
+
+  py::enum_<ClipMode>(m, "ClipMode")
+      .value("independent", ClipMode::Independent)
+      .value("box", ClipMode::Box);
+
+  py::class_<SolverParams>(m, "SolverParams")
+      .def(py::init<>())
+      .def_readwrite("C", &SolverParams::C)
+      .def_readwrite("gamma", &SolverParams::gamma)
+      .def_readwrite("eps", &SolverParams::eps)
+      .def_readwrite("max_iter", &SolverParams::max_iter)
+      .def_readwrite("clip", &SolverParams::clip)
+      .def_readwrite("tau", &SolverParams::tau)
+      .def_readwrite("cache_lines", &SolverParams::cache_lines)
+      .def_readwrite("cache_mb", &SolverParams::cache_mb)
+      .def_readwrite("cache_frac", &SolverParams::cache_frac)
+      .def_readwrite("host_cache_lines", &SolverParams::host_cache_lines)
+      .def_readwrite("spec_rows", &SolverParams::spec_rows)
+      .def_readwrite("graph_block", &SolverParams::graph_block)
+      .def_readwrite("use_graph", &SolverParams::use_graph)
+      .def_readwrite("x_mode", &SolverParams::x_mode)
+      .def_readwrite("log_every", &SolverParams::log_every)
+      .def_readwrite("verbose", &SolverParams::verbose)
+      .def_readwrite("checkpoint_every", &SolverParams::checkpoint_every)
+      .def_readwrite("checkpoint_path", &SolverParams::checkpoint_path)
+      .def_readwrite("sync_debug", &SolverParams::sync_debug);
+
+  py::class_<Checkpoint>(m, "Checkpoint")
+      .def(py::init<>())
+      .def_readwrite("n", &Checkpoint::n)
+      .def_readwrite("d", &Checkpoint::d)
+      .def_readwrite("C", &Checkpoint::C)
+      .def_readwrite("gamma", &Checkpoint::gamma)
+      .def_readwrite("eps", &Checkpoint::eps)
+      .def_readwrite("clip", &Checkpoint::clip)
+      .def_readwrite("iter", &Checkpoint::iter)
+      .def_readwrite("b_hi", &Checkpoint::b_hi)
+      .def_readwrite("b_lo", &Checkpoint::b_lo)
+      .def_property("alpha", [](const Checkpoint& c) { return to_np(c.alpha); },
+                    [](Checkpoint& c, F32 a) { c.alpha = from_np(a); })
+      .def_property("f", [](const Checkpoint& c) { return to_np(c.f); },
+                    [](Checkpoint& c, F32 a) { c.f = from_np(a); });
+  m.def("write_checkpoint", &write_checkpoint, py::arg("path"), py::arg("ck"));
+  m.def("read_checkpoint", &read_checkpoint, py::arg("path"));
+
+  // ---------------- communicators ----------------
+  py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")
+      .def_property_readonly("rank", &Communicator::rank)
+      .def_property_readonly("size", &Communicator::size)
+      .def_property_readonly("name", &Communicator::name)
+      .def_property_readonly("device_memory", &Communicator::device_memory)
+      .def("barrier", [](Communicator& c) { py::gil_scoped_release r; c.barrier(); });
+  m.def("local_comm", []() { return std::shared_ptr<Communicator>(make_local_comm()); });
+  py::class_<ThreadCommGroup, std::shared_ptr<ThreadCommGroup>>(m, "ThreadCommGroup")
+      .def(py::init<int>(), py::arg("world"))
+      .def("comm", [](ThreadCommGroup& g, int r) { return std::shared_ptr<Communicator>(g.comm(r)); });
+  m.def("rccl_unique_id", []() {
+    auto v = rccl_unique_id();
+    return py::bytes((const char*)v.data(), v.size());
+  });
+  m.def("rccl_comm", [](py::bytes uid, int rank, int world, int device) {
+    std::string s = uid;
+    std::vector<uint8_t> v(s.begin(), s.end());
+    py::gil_scoped_release r;
+    return std::shared_ptr<Communicator>(make_rccl_comm(v, rank, world, device));
+  }, py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"));
+  m.def("callback_comm", [](int rank, int size, py::function a, py::function b, py::function c, py::function d,
+                            py::function e, py::function f) {
+    return std::shared_ptr<Communicator>(new CallbackComm(rank, size, a, b, c, d, e, f));
+  });
+
+  // ---------------- data ----------------
+  m.def("read_csv", [](const std::string& path, int64_t n, int d, int threads) {
+    Dataset ds;
+    {
+      py::gil_scoped_release r;
+      ds = read_csv(path, n, d, threads);
+    }
+    return py::make_tuple(to_np2(ds.x, ds.n, ds.d), to_np(ds.y));
+  }, py::arg("path"), py::arg("n") = 0, py::arg("d") = 0, py::arg("threads") = 0);
+  m.def("read_csv_rows", [](const std::string& path, int64_t row0, int64_t rows, int d) {
+    Dataset ds;
+    {
+      py::gil_scoped_release r;
+      ds = read_csv_rows(path, row0, rows, d, 0);
+    }
+    return py::make_tuple(to_np2(ds.x, ds.n, ds.d), to_np(ds.y));
+  });
+  m.def("write_csv", [](const std::string& path, F32 x, F32 y) {
+    Dataset ds;
+    check_xy(x, y, ds.n, ds.d);
+    ds.x = from_np(x);
+    ds.y = from_np(y);
+    py::gil_scoped_release r;
+    write_csv(path, ds);
+  });
+  m.def("read_libsvm", [](const std::string& path, int d, int64_t n) {
+    Dataset ds = read_libsvm(path, d, n);
+    return py::make_tuple(to_np2(ds.x, ds.n, ds.d), to_np(ds.y));
+  }, py::arg("path"), py::arg("d"), py::arg("n") = 0);
+  m.def("make_synthetic", [](const std::string& name, int64_t n, int d, uint64_t seed, int64_t row0,
+                             int64_t rows, float sep) {
+    Dataset ds;
+    {
+      py::gil_scoped_release r;
+      ds = make_synthetic(synth_from_name(name), n, d, seed, row0, rows, sep, 0);
+    }
+    return py::make_tuple(to_np2(ds.x, ds.n, ds.d), to_np(ds.y));
+  }, py::arg("name"), py::arg("n"), py::arg("d") = 0, py::arg("seed") = 0, py::arg("row0") = 0,
+     py::arg("rows") = -1, py::arg("sep") = 2.0f);
+  m.def("synth_default_d", [](const std::string& name) { return synth_default_d(synth_from_name(name)); });
+
+  // ---------------- model ----------------
+  py::class_<Model>(m, "Model")
+      .def(py::init<>())
+      .def_readwrite("gamma", &Model::gamma)
+      .def_readwrite("b", &Model::b)
+      .def_readwrite("d", &Model::d)
+      .def_readwrite("has_b", &Model::has_b)
+      .def_property_readonly("nsv", &Model::nsv)
+      .def_property("alpha", [](const Model& md) { return to_np(md.alpha); },
+                    [](Model& md, F32 a) { md.alpha = from_np(a); })
+      .def_property("y", [](const Model& md) { return to_np(md.y); }, [](Model& md, F32 a) { md.y = from_np(a); })
+      .def_property("x", [](const Model& md) { return to_np2(md.x, md.nsv(), md.d); },
+                    [](Model& md, F32 a) { md.x = from_np(a); });
+  m.def("make_model", [](F32 x, F32 y, F32 alpha, float b, float gamma) {
+    Dataset ds;
+    check_xy(x, y, ds.n, ds.d);
+    ds.x = from_np(x);
+    ds.y = from_np(y);
+    return make_model(ds, from_np(alpha), b, gamma);
+  });
+  m.def("write_model", &write_model, py::arg("path"), py::arg("model"), py::arg("precision") = 9,
+        py::arg("legacy") = false);
+  m.def("read_model", &read_model, py::arg("path"), py::arg("force_legacy") = false);
+  m.def("decision_cpu", [](const Model& md, F32 x, int threads) {
+    if (x.ndim() != 2) throw py::value_error("x must be 2-D");
+    std::vector<float> dec;
+    {
+      py::gil_scoped_release r;
+      dec = decision_cpu(md, x.data(), x.shape(0), (int)x.shape(1), threads);
+    }
+    return to_np(dec);
+  }, py::arg("model"), py::arg("x"), py::arg("threads") = 0);
+
+  // ---------------- solvers ----------------
+  m.def("solve_cpu", [](F32 x, F32 y, const SolverParams& p, std::shared_ptr<Communicator> comm,
+                        const Checkpoint* resume, py::object progress) {
+    Dataset ds;
+    check_xy(x, y, ds.n, ds.d);
+    ds.x = from_np(x);
+    ds.y = from_np(y);
+    for (auto& v : ds.y) v = v > 0 ? 1.f : -1.f;
+    auto prog = wrap_progress(progress);
+    SolveResult r;
+    {
+      py::gil_scoped_release rel;
+      r = solve_cpu(ds, p, comm.get(), resume, prog);
+    }
+    return py::make_tuple(to_np(r.alpha), result_dict(r));
+  }, py::arg("x"), py::arg("y"), py::arg("params"), py::arg("comm") = nullptr, py::arg("resume") = nullptr,
+     py::arg("progress") = py::none());
+
+  py::class_<GpuSolver, std::shared_ptr<GpuSolver>>(m, "GpuSolver")
+      .def(py::init([](const SolverParams& p, std::shared_ptr<Communicator> comm, int device) {
+             // keep the communicator alive as long as the solver
+             auto* s = new GpuSolver(p, comm.get(), device);
+             return std::shared_ptr<GpuSolver>(s, [comm](GpuSolver* q) { delete q; });
+           }),
+           py::arg("params"), py::arg("comm") = nullptr, py::arg("device") = 0)
+      .def("setup", [](GpuSolver& s, F32 x, int64_t n, F32 y) {
+        if (x.ndim() != 2) throw py::value_error("x must be 2-D");
+        if (y.ndim() != 1 || y.shape(0) != n) throw py::value_error("y must have n entries");
+        GpuSetupInfo i;
+        {
+          py::gil_scoped_release r;
+          i = s.setup(x.data(), x.shape(0), n, (int)x.shape(1), y.data());
+        }
+        py::dict d;
+        d["device"] = i.device;
+        d["device_name"] = i.device_name;
+        d["n"] = i.n;
+        d["n_local"] = i.n_local;
+        d["offset"] = i.offset;
+        d["d"] = i.d;
+        d["dp"] = i.dp;
+        d["x_replicated"] = i.x_replicated;
+        d["cache_lines"] = i.cache_lines;
+        d["blocks"] = i.blocks;
+        d["bytes_device"] = i.bytes_device;
+        return d;
+      })
+      .def("solve", [](GpuSolver& s, const Checkpoint* resume, py::object progress) {
+        auto prog = wrap_progress(progress);
+        SolveResult r;
+        {
+          py::gil_scoped_release rel;
+          r = s.solve(resume, prog);
+        }
+        return py::make_tuple(to_np(r.alpha), result_dict(r));
+      }, py::arg("resume") = nullptr, py::arg("progress") = py::none())
+      .def("train_accuracy", [](GpuSolver& s, F32 alpha, float b) {
+        SolveResult r;
+        r.alpha = from_np(alpha);
+        r.b = b;
+        py::gil_scoped_release rel;
+        return s.train_accuracy(r);
+      })
+      .def("decision", [](GpuSolver& s, F32 alpha, float b, F32 x) {
+        SolveResult r;
+        r.alpha = from_np(alpha);
+        r.b = b;
+        std::vector<float> out;
+        {
+          py::gil_scoped_release rel;
+          out = s.decision(r, x.data(), x.shape(0), (int)x.shape(1));
+        }
+        return to_np(out);
+      });
+
+  py::class_<GpuPredictor, std::shared_ptr<GpuPredictor>>(m, "GpuPredictor")
+      .def(py::init<const Model&, int>(), py::arg("model"), py::arg("device") = 0)
+      .def("decision", [](GpuPredictor& p, F32 x) {
+        if (x.ndim() != 2) throw py::value_error("x must be 2-D");
+        std::vector<float> out;
+        {
+          py::gil_scoped_release rel;
+          out = p.decision(x.data(), x.shape(0), (int)x.shape(1));
+        }
+        return to_np(out);
+      })
+      .def("decision_device", [](GpuPredictor& p, uintptr_t x, int64_t n, int d, int ld, uintptr_t out,
+                                 uintptr_t stream) {
+        py::gil_scoped_release rel;
+        p.decision_device((const float*)x, n, d, ld, (float*)out, (void*)stream);
+      });
+
+  // ---------------- kernel test entry points (device pointers) ----------------
+  m.def("k_row_sqnorm", [](uintptr_t x, int64_t n, int d, int ld, uintptr_t out, uintptr_t stream) {
+    kernels::row_sqnorm((const float*)x, n, d, ld, (float*)out, (void*)stream);
+  });
+  m.def("k_rbf_rows", [](uintptr_t x, uintptr_t xsq, int64_t n, int ld, uintptr_t w, uintptr_t wsq, int nq,
+                         float gamma, uintptr_t out, int64_t out_ld, uintptr_t stream) {
+    kernels::rbf_rows((const float*)x, (const float*)xsq, n, ld, (const float*)w, (const float*)wsq, nq, gamma,
+                      (float*)out, out_ld, (void*)stream);
+  });
+  m.def("k_select_partials", [](uintptr_t f, uintptr_t alpha, uintptr_t y, int64_t n, int64_t off, float C,
+                                uintptr_t partials, uintptr_t stream) {
+    int blocks = 0;
+    kernels::select_partials((const float*)f, (const float*)alpha, (const float*)y, n, off, C,
+                             (uint64_t*)partials, &blocks, (void*)stream);
+    return blocks;
+  });
+  m.def("k_predict", [](uintptr_t x, uintptr_t xsq, int64_t n, int ld, uintptr_t sv, uintptr_t svsq,
+                        uintptr_t coef, int64_t nsv, float gamma, float b, uintptr_t dec, uintptr_t stream) {
+    kernels::predict((const float*)x, (const float*)xsq, n, ld, (const float*)sv, (const float*)svsq,
+                     (const float*)coef, nsv, ld, gamma, b, (float*)dec, (void*)stream);
+  });
+  m.def("k_compact", [](uintptr_t alpha, int64_t n, uintptr_t idx, uintptr_t stream) {
+    return kernels::compact_nonzero((const float*)alpha, n, (int*)idx, (void*)stream);
+  });
+  m.def("make_key", [](float f, uint32_t idx) { return make_key(f, idx); });
+  m.def("key_value", [](uint64_t k) { return key_value(k); });
+  m.def("key_index", [](uint64_t k) { return key_index(k); });
+  m.def("pad_features", &pad_features);
+  m.def("shard_of", [](int64_t n, int rank, int world) {
+    Shard s = shard_of(n, rank, world);
+    return py::make_tuple(s.offset, s.size);
+  });
+  m.def("device_count", &device_count);
+  m.def("device_name", &device_name);
+  m.attr("NQ") = 16;
+  m.attr("STEP_ROWS") = 128;
+}

@@ -1,0 +1,297 @@
+"""SVC: the estimator-level API over the native MI355X solver.
+
+Reference capability map (farshid83/dpsvm):
+  fit()                -> svmTrainMain.cpp:142-365 (GPU/MPI trainer) or seq.cpp (CPU)
+  decision_function()  -> svmTrain.cu:633-665 (training accuracy) / seq_test.cpp:187-210
+  save() / load_model()-> svmTrainMain.cpp:386-416 model writer, seq_test.cpp:212-249 reader
+Labels: the reference requires +1/-1 (svmTrain.cu:58,73); any two distinct
+labels are accepted here and mapped (classes_[1] -> +1), like scikit-learn.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Optional
+
+import numpy as np
+
+from .._native import gpu_available, load
+
+
+def _as_f32_2d(X) -> np.ndarray:
+    try:
+        import torch
+
+        if isinstance(X, torch.Tensor):
+            X = X.detach().to("cpu", dtype=torch.float32).numpy()
+    except ImportError:
+        pass
+    X = np.ascontiguousarray(np.asarray(X, dtype=np.float32))
+    if X.ndim != 2:
+        raise ValueError(f"X must be 2-D (n_samples, n_features), got shape {X.shape}")
+    return X
+
+
+def _as_1d(y) -> np.ndarray:
+    try:
+        import torch
+
+        if isinstance(y, torch.Tensor):
+            y = y.detach().cpu().numpy()
+    except ImportError:
+        pass
+    return np.asarray(y).reshape(-1)
+
+
+_CLIP = {"independent": 0, "box": 1}
+_XMODE = {"auto": 0, "replicated": 1, "partitioned": 2}
+
+
+@dataclass
+class SVCConfig:
+    """Solver configuration (mirrors the svmTrain flags)."""
+
+    C: float = 1.0                  # -c (reference default 1)
+    gamma: Optional[float] = None   # -g; None -> 1/d (reference: integer 1/d, Q1)
+    eps: float = 1e-3               # -e
+    max_iter: int = 150000          # -n
+    clip: str = "independent"       # reference clipping; "box" = LIBSVM joint box
+    tau: float = 1e-12              # eta floor (Q4)
+    cache_lines: int = 0            # -s (0 = auto: fill HBM; dense Gram when it fits)
+    cache_mb: float = 0.0
+    cache_frac: float = 0.80
+    spec_rows: int = 14             # speculative rows per X pass (LRU mode)
+    graph_block: int = 64           # SMO iterations per hipGraph
+    use_graph: bool = True
+    x_mode: str = "auto"            # auto | replicated | partitioned
+    log_every: int = 0
+    checkpoint_path: Optional[str] = None
+    checkpoint_every: int = 0
+    device: str = "auto"            # auto | cpu | cuda | cuda:N
+    verbose: bool = False
+
+    def resolved_gamma(self, d: int) -> float:
+        return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
+
+    def to_native(self, d: int):
+        C = load()
+        if self.clip not in _CLIP:
+            raise ValueError(f"clip must be one of {list(_CLIP)}")
+        if self.x_mode not in _XMODE:
+            raise ValueError(f"x_mode must be one of {list(_XMODE)}")
+        if not self.C > 0:
+            raise ValueError("C must be > 0")
+        p = C.SolverParams()
+        p.C = float(self.C)
+        p.gamma = self.resolved_gamma(d)
+        p.eps = float(self.eps)
+        p.max_iter = int(self.max_iter)
+        p.clip = C.ClipMode.box if self.clip == "box" else C.ClipMode.independent
+        p.tau = float(self.tau)
+        p.cache_lines = int(self.cache_lines)
+        p.cache_mb = float(self.cache_mb)
+        p.cache_frac = float(self.cache_frac)
+        p.spec_rows = int(self.spec_rows)
+        p.graph_block = int(self.graph_block)
+        p.use_graph = bool(self.use_graph)
+        p.x_mode = _XMODE[self.x_mode]
+        p.log_every = int(self.log_every)
+        p.verbose = bool(self.verbose)
+        p.checkpoint_every = int(self.checkpoint_every)
+        p.checkpoint_path = self.checkpoint_path or ""
+        return p
+
+    def device_kind(self) -> tuple[str, int]:
+        dev = self.device
+        if dev == "auto":
+            return ("cuda", 0) if gpu_available() else ("cpu", 0)
+        if dev == "cpu":
+            return ("cpu", 0)
+        if dev.startswith("cuda"):
+            idx = int(dev.split(":")[1]) if ":" in dev else 0
+            return ("cuda", idx)
+        raise ValueError(f"unknown device {dev!r}")
+
+
+class SVC:
+    """Binary RBF C-SVM trained by modified SMO on MI355X (or the CPU).
+
+    Attributes after fit: ``alpha_`` (dual variables, len n), ``b_`` (threshold:
+    decision = sum alpha_i y_i K(x_i, x) - b), ``intercept_`` (= -b_),
+    ``support_`` (indices with alpha > 0), ``support_vectors_``, ``dual_coef_``
+    (alpha*y of the SVs), ``n_iter_``, ``status_``, ``fit_time_`` (SMO loop
+    seconds, the reference's timed region), ``stats_`` (cache / pass counters).
+    """
+
+    def __init__(self, C: float = 1.0, gamma: Optional[float] = None, eps: float = 1e-3,
+                 max_iter: int = 150000, device: str = "auto", **kwargs: Any):
+        self.config = SVCConfig(C=C, gamma=gamma, eps=eps, max_iter=max_iter, device=device, **kwargs)
+        self._model = None
+        self._gpu_pred = None
+        self.classes_ = np.array([-1.0, 1.0], dtype=np.float32)
+
+    # ------------------------------------------------------------------ labels
+    def _encode(self, y) -> np.ndarray:
+        y = _as_1d(y)
+        u = np.unique(y)
+        if len(u) > 2:
+            raise ValueError(f"binary classifier: got {len(u)} classes")
+        if len(u) == 2 and set(u.tolist()) <= {-1, 1}:
+            self.classes_ = np.array([-1.0, 1.0], dtype=np.float32)
+            return np.where(y > 0, 1.0, -1.0).astype(np.float32)
+        if len(u) == 1:
+            self.classes_ = np.array([u[0], u[0]])
+            return np.ones(len(y), dtype=np.float32) * (1.0 if (u[0] > 0 if np.isreal(u[0]) else True) else -1.0)
+        self.classes_ = u
+        return np.where(y == u[1], 1.0, -1.0).astype(np.float32)
+
+    def _decode(self, s: np.ndarray) -> np.ndarray:
+        if np.array_equal(self.classes_, np.array([-1.0, 1.0], dtype=np.float32)):
+            return s.astype(np.float32)
+        return np.where(s > 0, self.classes_[-1], self.classes_[0])
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, X, y, comm=None, resume=None, progress: Optional[Callable] = None,
+            rank_rows: Optional[int] = None) -> "SVC":
+        """Train.  ``comm``: a native communicator (see dpsvm_amd.parallel) for
+        multi-rank training; ``resume``: checkpoint path or native Checkpoint."""
+        C = load()
+        X = _as_f32_2d(X)
+        ys = self._encode(y)
+        n, d = X.shape[0], X.shape[1]
+        if rank_rows is None and ys.shape[0] != n:
+            raise ValueError("len(y) != X.shape[0]")
+        cfg = self.config
+        p = cfg.to_native(d)
+        if cfg.log_every and progress is None:
+            def progress(it, bh, bl, el, hits, misses):  # noqa: E306
+                print(f"iter {it}  b_hi {bh:.6g}  b_lo {bl:.6g}  gap {bl - bh:.3g}  "
+                      f"{it / max(el, 1e-9):.0f} it/s  hits {hits} misses {misses}", flush=True)
+        ck = None
+        if resume is not None:
+            ck = C.read_checkpoint(resume) if isinstance(resume, str) else resume
+        kind, dev = cfg.device_kind()
+        self.device_ = f"{kind}:{dev}" if kind == "cuda" else "cpu"
+        t0 = time.perf_counter()
+        if kind == "cuda":
+            solver = C.GpuSolver(p, comm, dev)
+            self.setup_info_ = solver.setup(X, ys.shape[0], ys)
+            alpha, info = solver.solve(ck, progress)
+            self._solver = solver
+        else:
+            if rank_rows is not None:
+                raise ValueError("partitioned X needs the GPU solver")
+            alpha, info = C.solve_cpu(X, ys, p, comm, ck, progress)
+            self._solver = None
+        self.wall_time_ = time.perf_counter() - t0
+        self.alpha_ = alpha
+        self.b_ = float(info["b"])
+        self.intercept_ = -self.b_
+        self.n_iter_ = int(info["iters"])
+        self.status_ = int(info["status"])
+        self.converged_ = bool(info["converged"])
+        self.fit_time_ = float(info["t_solve"])
+        self.setup_time_ = float(info["t_setup"])
+        self.stats_ = dict(info)
+        self.gamma_ = p.gamma
+        self.n_features_in_ = d
+        self._X_train, self._y_train = (X, ys) if rank_rows is None else (None, None)
+        if rank_rows is None:
+            self.support_ = np.nonzero(alpha > 0)[0]
+            self.support_vectors_ = X[self.support_]
+            self.dual_coef_ = (alpha[self.support_] * ys[self.support_]).astype(np.float32)
+            self.n_support_ = int(len(self.support_))
+        self._model = None
+        self._gpu_pred = None
+        return self
+
+    # ------------------------------------------------------------------ model
+    def to_model(self):
+        C = load()
+        if self._model is None:
+            if self._X_train is None:
+                raise RuntimeError("to_model() needs the full training set on this rank")
+            self._model = C.make_model(self._X_train, self._y_train, self.alpha_, self.b_, self.gamma_)
+        return self._model
+
+    def save(self, path: str, precision: int = 9, legacy: bool = False) -> None:
+        """Write the reference text model (gamma, b, then alpha,y,x... per SV)."""
+        load().write_model(path, self.to_model(), precision, legacy)
+
+    # ------------------------------------------------------------------ predict
+    def _predictor(self):
+        if self._gpu_pred is None:
+            kind, dev = self.config.device_kind()
+            if kind == "cuda":
+                self._gpu_pred = load().GpuPredictor(self.to_model(), dev)
+        return self._gpu_pred
+
+    def decision_function(self, X) -> np.ndarray:
+        """sum_sv alpha y K(sv, x) - b  (svmTrain.cu:646-652)."""
+        X = _as_f32_2d(X)
+        if X.shape[1] != self.n_features_in_:
+            raise ValueError(f"X has {X.shape[1]} features, model has {self.n_features_in_}")
+        gp = self._predictor()
+        if gp is not None:
+            return gp.decision(X)
+        return load().decision_cpu(self.to_model(), X, 0)
+
+    def predict(self, X) -> np.ndarray:
+        dec = self.decision_function(X)
+        return self._decode(np.where(dec < 0, -1.0, 1.0))  # d >= 0 -> +1 (svmTrain.cu:654-657)
+
+    def score(self, X, y) -> float:
+        yy = _as_1d(y)
+        return float(np.mean(self.predict(X) == yy))
+
+    def train_accuracy(self) -> float:
+        """Training accuracy computed on device (distributed across ranks)."""
+        if getattr(self, "_solver", None) is not None:
+            return float(self._solver.train_accuracy(self.alpha_, self.b_))
+        return self.score(self._X_train, self._y_train)
+
+    def get_params(self, deep: bool = True) -> dict:
+        return dataclasses.asdict(self.config)
+
+
+class LoadedModel:
+    """A model read from a reference-format file (svmTest path)."""
+
+    def __init__(self, model, device: str = "auto"):
+        self.model = model
+        self.device = device
+        self._gpu = None
+
+    @property
+    def gamma(self) -> float:
+        return self.model.gamma
+
+    @property
+    def b(self) -> float:
+        return self.model.b
+
+    @property
+    def n_support(self) -> int:
+        return self.model.nsv
+
+    def decision_function(self, X) -> np.ndarray:
+        X = _as_f32_2d(X)
+        use_gpu = self.device.startswith("cuda") or (self.device == "auto" and gpu_available())
+        if use_gpu:
+            if self._gpu is None:
+                dev = int(self.device.split(":")[1]) if ":" in self.device else 0
+                self._gpu = load().GpuPredictor(self.model, dev)
+            return self._gpu.decision(X)
+        return load().decision_cpu(self.model, X, 0)
+
+    def predict(self, X) -> np.ndarray:
+        return np.where(self.decision_function(X) < 0, -1.0, 1.0).astype(np.float32)
+
+    def score(self, X, y) -> float:
+        return float(np.mean(self.predict(X) == np.where(_as_1d(y) > 0, 1.0, -1.0)))
+
+
+def load_model(path: str, device: str = "auto", legacy: bool = False) -> LoadedModel:
+    return LoadedModel(load().read_model(path, legacy), device)

@@ -1,0 +1,105 @@
+"""torch-facing wrappers of the individual HIP kernels (device tensors in,
+device tensors out).  Used by the GPU numerics tests, which compare each
+kernel with a plain PyTorch fp32 reference of the same op, and usable as
+building blocks (e.g. an RBF Gram / decision op on torch tensors).
+
+Every wrapper raises if the native extension is missing: there is no silent
+PyTorch fallback on a GPU box.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._native import load
+
+STEP_ROWS = 128
+
+
+def _pad_rows_cols(x: torch.Tensor, row_mult: int = 128, col_mult: int = 16, extra_rows: int = 128):
+    n, d = x.shape
+    dp = (d + col_mult - 1) // col_mult * col_mult
+    rows = (n + row_mult - 1) // row_mult * row_mult + extra_rows
+    out = torch.zeros(rows, dp, device=x.device, dtype=torch.float32)
+    out[:n, :d] = x.to(torch.float32)
+    return out, dp
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def row_sqnorm(x: torch.Tensor) -> torch.Tensor:
+    """|x_i|^2 per row (one wave per row)."""
+    C = load()
+    xp, dp = _pad_rows_cols(x)
+    out = torch.zeros(xp.shape[0], device=x.device, dtype=torch.float32)
+    C.k_row_sqnorm(xp.data_ptr(), x.shape[0], dp, dp, out.data_ptr(), _stream(x))
+    return out[: x.shape[0]]
+
+
+def rbf_rows(x: torch.Tensor, w: torch.Tensor, gamma: float) -> torch.Tensor:
+    """K[q, j] = exp(-gamma |x_j - w_q|^2) for up to 16 query rows w (the
+    smo_rows MFMA 16x16x4 kernel)."""
+    C = load()
+    nq = w.shape[0]
+    if not 1 <= nq <= 16:
+        raise ValueError("1 <= len(w) <= 16")
+    xp, dp = _pad_rows_cols(x)
+    wp, _ = _pad_rows_cols(w)
+    xsq = torch.zeros(xp.shape[0], device=x.device)
+    wsq = torch.zeros(wp.shape[0], device=x.device)
+    C.k_row_sqnorm(xp.data_ptr(), xp.shape[0], dp, dp, xsq.data_ptr(), _stream(x))
+    C.k_row_sqnorm(wp.data_ptr(), wp.shape[0], dp, dp, wsq.data_ptr(), _stream(x))
+    n = x.shape[0]
+    ld = (n + STEP_ROWS - 1) // STEP_ROWS * STEP_ROWS
+    out = torch.zeros(nq, ld, device=x.device)
+    C.k_rbf_rows(xp.data_ptr(), xsq.data_ptr(), n, dp, wp.data_ptr(), wsq.data_ptr(), nq, float(gamma),
+                 out.data_ptr(), ld, _stream(x))
+    return out[:, :n]
+
+
+def select_partials(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: float, offset: int = 0):
+    """Per-workgroup packed (b_hi, I_hi) / (-b_lo, I_lo) keys of smo_step."""
+    C = load()
+    n = f.shape[0]
+    g = (n + STEP_ROWS - 1) // STEP_ROWS
+    part = torch.zeros(2 * g, device=f.device, dtype=torch.int64)
+    a_full = alpha.contiguous().float()
+    blocks = C.k_select_partials(f.contiguous().float().data_ptr(), a_full.data_ptr(),
+                                 y.contiguous().float().data_ptr(), n, offset, float(C_), part.data_ptr(),
+                                 _stream(f))
+    return part.view(-1, 2)[:blocks]
+
+
+def decode_key(k: int):
+    """(value, index) of a packed selection key (python int, may be negative i64)."""
+    C = load()
+    k &= (1 << 64) - 1
+    return C.key_value(k), C.key_index(k)
+
+
+def rbf_decision(x: torch.Tensor, sv: torch.Tensor, coef: torch.Tensor, gamma: float, b: float) -> torch.Tensor:
+    """dec_i = sum_s coef_s exp(-gamma |x_i - sv_s|^2) - b (MFMA 32x32x2 GEMM +
+    fused exp + row reduce)."""
+    C = load()
+    xp, dp = _pad_rows_cols(x)
+    svp, _ = _pad_rows_cols(sv)
+    xsq = torch.zeros(xp.shape[0], device=x.device)
+    svsq = torch.zeros(svp.shape[0], device=x.device)
+    cf = torch.zeros(svp.shape[0], device=x.device)
+    cf[: coef.shape[0]] = coef.float()
+    C.k_row_sqnorm(xp.data_ptr(), xp.shape[0], dp, dp, xsq.data_ptr(), _stream(x))
+    C.k_row_sqnorm(svp.data_ptr(), svp.shape[0], dp, dp, svsq.data_ptr(), _stream(x))
+    dec = torch.zeros(xp.shape[0], device=x.device)
+    C.k_predict(xp.data_ptr(), xsq.data_ptr(), x.shape[0], dp, svp.data_ptr(), svsq.data_ptr(), cf.data_ptr(),
+                sv.shape[0], float(gamma), float(b), dec.data_ptr(), _stream(x))
+    return dec[: x.shape[0]]
+
+
+def compact_positive(alpha: torch.Tensor) -> torch.Tensor:
+    """Indices i with alpha_i > 0, in index order (ballot + scan kernels)."""
+    C = load()
+    a = alpha.contiguous().float()
+    idx = torch.empty(a.shape[0] + 1, device=a.device, dtype=torch.int32)
+    cnt = C.k_compact(a.data_ptr(), a.shape[0], idx.data_ptr(), _stream(a))
+    return idx[:cnt]

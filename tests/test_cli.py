@@ -1,0 +1,91 @@
+"""svmTrain / svmSeq / svmTest CLIs: reference flags, stdout lines, model file."""
+import os
+
+import numpy as np
+
+from conftest import run
+from dpsvm_amd.utils import datasets
+
+
+def _data(tmp_path, n=400):
+    X, y = datasets.synthetic("blobs", n=n, d=5, seed=7, sep=1.5)
+    p = str(tmp_path / "train.csv")
+    datasets.write_csv(p, X, y)
+    return p, X, y
+
+
+def test_svmtrain_cpu_reference_output(tmp_path, bin_dir):
+    p, X, y = _data(tmp_path)
+    m = str(tmp_path / "model.txt")
+    js = str(tmp_path / "metrics.json")
+    r = run([os.path.join(bin_dir, "svmTrain"), "-a", "5", "-x", "400", "-f", p, "-c", "2", "-g", "0.4",
+             "-e", "0.001", "-m", m, "--cpu", "--metrics-json", js])
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    for line in ("Populated Data from input file at node: 0", "SETUP DONE", "TOTAL TIME TAKEN in seconds:",
+                 "Converged at iteration number:", "b: ", "Number of SVs:", "Training accuracy:",
+                 f"Training model has been saved to the file {m}"):
+        assert line in out, (line, out)
+    assert "0\t400" in out  # shard table disp\tsize
+    import json
+
+    met = json.load(open(js))
+    assert met["converged"] and met["n"] == 400 and met["iterations"] > 0
+    lines = open(m).read().strip().split("\n")
+    assert abs(float(lines[0]) - 0.4) < 1e-7 and len(lines) - 2 == met["n_sv"]
+
+
+def test_svmtrain_simulated_ranks_cpu(tmp_path, bin_dir):
+    p, X, y = _data(tmp_path)
+    outs = []
+    for ranks in ("1", "3"):
+        m = str(tmp_path / f"m{ranks}.txt")
+        r = run([os.path.join(bin_dir, "svmTrain"), "-a", "5", "-x", "400", "-f", p, "-c", "2", "-g", "0.4",
+                 "-m", m, "--cpu", "--ranks", ranks])
+        assert r.returncode == 0, r.stderr
+        outs.append(open(m).read())
+    assert outs[0] == outs[1]  # identical model from 1 and 3 ranks
+
+
+def test_svmtrain_usage_errors(tmp_path, bin_dir):
+    r = run([os.path.join(bin_dir, "svmTrain"), "-a", "5", "-x", "10"])
+    assert r.returncode == 255 and "Enter a valid file name" in r.stderr
+    r = run([os.path.join(bin_dir, "svmTrain"), "-f", "x.csv", "-m", "m.txt"])
+    assert r.returncode == 255 and "Missing a required parameter" in r.stderr
+    r = run([os.path.join(bin_dir, "svmTrain"), "--bogus"])
+    assert r.returncode == 255
+
+
+def test_svmseq_and_svmtest(tmp_path, bin_dir):
+    p, X, y = _data(tmp_path)
+    m = str(tmp_path / "model.txt")
+    r = run([os.path.join(bin_dir, "svmSeq"), "-a", "5", "-x", "400", "-f", p, "-c", "2", "-g", "0.4",
+             "-m", m])
+    assert r.returncode == 0, r.stderr
+    assert "Converged at iteration number:" in r.stdout and "Training accuracy:" in r.stdout
+    dec_path = str(tmp_path / "dec.txt")
+    r = run([os.path.join(bin_dir, "svmTest"), "-a", "5", "-x", "400", "-f", p, "-m", m, "--cpu",
+             "--decision-out", dec_path])
+    assert r.returncode == 0, r.stderr
+    for line in ("Populated test data", "Total number of Support Vectors:", "Populated training model",
+                 "Test accuracy:"):
+        assert line in r.stdout
+    acc = float(r.stdout.split("Test accuracy:")[1].split()[0])
+    dec = np.loadtxt(dec_path)
+    assert acc > 0.8 and dec.shape == (400,)
+
+
+def test_svmtrain_synthetic_and_checkpoint_resume(tmp_path, bin_dir):
+    m = str(tmp_path / "m.txt")
+    ck = str(tmp_path / "ck.bin")
+    base = [os.path.join(bin_dir, "svmTrain"), "-a", "4", "-x", "500", "--synthetic", "blobs", "--seed", "3",
+            "-c", "1", "-g", "0.5", "--cpu", "-m", m]
+    r = run(base + ["--skip-accuracy"])
+    full_it = int(r.stdout.split("Converged at iteration number:")[1].split()[0])
+    full_model = open(m).read()
+    r = run(base + ["-n", str(full_it // 2), "--checkpoint", ck, "--checkpoint-every", str(full_it // 4)])
+    assert "Could not converge in" in r.stdout and os.path.exists(ck)
+    r = run(base + ["--resume", ck])
+    assert r.returncode == 0, r.stderr
+    assert f"Converged at iteration number: {full_it}" in r.stdout
+    assert open(m).read() == full_model

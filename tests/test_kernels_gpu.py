@@ -1,0 +1,108 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (GPU only)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dpsvm_amd.ops import kernels
+
+    return kernels
+
+
+def _rbf_ref(x, w, gamma):
+    x64, w64 = x.double(), w.double()
+    d2 = (x64 * x64).sum(1)[None, :] + (w64 * w64).sum(1)[:, None] - 2 * w64 @ x64.T
+    return torch.exp(-gamma * d2.clamp_min(0))
+
+
+def test_native_loaded_from_tree(K, C):
+    import os
+
+    from dpsvm_amd._native import is_loaded_from_tree
+
+    assert is_loaded_from_tree()
+    assert C.device_count() >= 1
+
+
+@pytest.mark.parametrize("n,d", [(1, 3), (300, 17), (4097, 784), (1000, 1100)])
+def test_row_sqnorm(K, n, d):
+    x = torch.rand(n, d, device="cuda")
+    got = K.row_sqnorm(x)
+    ref = (x.double() ** 2).sum(1)
+    assert torch.allclose(got.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("nq", [1, 2, 5, 16])
+@pytest.mark.parametrize("n,d,gamma", [(257, 13, 0.5), (3000, 784, 0.02), (1500, 2100, 0.001)])
+def test_rbf_rows_mfma(K, nq, n, d, gamma):
+    g = torch.Generator(device="cuda").manual_seed(nq * 7 + n)
+    x = torch.rand(n, d, device="cuda", generator=g)
+    w = torch.rand(nq, d, device="cuda", generator=g)
+    w[0] = x[min(3, n - 1)]  # exact self-kernel: K = 1
+    got = K.rbf_rows(x, w, gamma)
+    ref = _rbf_ref(x, w, gamma)
+    assert got.shape == (nq, n)
+    assert torch.allclose(got.double(), ref, rtol=2e-4, atol=2e-5), (got.double() - ref).abs().max()
+    assert abs(float(got[0, min(3, n - 1)]) - 1.0) < 1e-4
+
+
+def test_rbf_rows_asymmetric_operands(K):
+    # integer data: exact f32 arithmetic, catches swapped row/col maps
+    n, d = 200, 32
+    x = torch.randint(0, 3, (n, d), device="cuda").float()
+    w = torch.randint(0, 3, (16, d), device="cuda").float()
+    got = K.rbf_rows(x, w, 0.01)
+    ref = _rbf_ref(x, w, 0.01)
+    assert torch.allclose(got.double(), ref, rtol=1e-5, atol=1e-7)
+
+
+def test_select_partials(K):
+    from dpsvm_amd.ops.kernels import decode_key
+
+    n, C_ = 5000, 2.0
+    g = torch.Generator(device="cuda").manual_seed(0)
+    f = torch.randn(n, device="cuda", generator=g)
+    f[1234] = f[77] = -10.0  # tie across workgroups: lowest index must win
+    y = torch.where(torch.rand(n, device="cuda", generator=g) > 0.5, 1.0, -1.0)
+    a = torch.rand(n, device="cuda", generator=g) * C_
+    a[torch.rand(n, device="cuda", generator=g) < 0.3] = 0.0
+    a[torch.rand(n, device="cuda", generator=g) < 0.2] = C_
+    y[77] = y[1234] = 1.0
+    a[77] = a[1234] = 0.0
+    part = K.select_partials(f, a, y, C_).cpu()
+    kh = min(int(v) & (2**64 - 1) for v in part[:, 0].tolist())
+    kl = min(int(v) & (2**64 - 1) for v in part[:, 1].tolist())
+    up = ((a == 0) & (y == 1)) | ((a == C_) & (y != 1)) | ((a > 0) & (a < C_))
+    lo = ((a == 0) & (y != 1)) | ((a == C_) & (y == 1)) | ((a > 0) & (a < C_))
+    b_hi = float(torch.where(up, f, torch.inf).min())
+    b_lo = float(torch.where(lo, f, -torch.inf).max())
+    vh, ih = decode_key(kh)
+    vl, il = decode_key(kl)
+    assert vh == b_hi and ih == 77
+    assert -vl == b_lo and float(f[il]) == b_lo and bool(lo[il])
+
+
+@pytest.mark.parametrize("n,nsv,d", [(100, 1, 5), (2000, 3000, 784), (5000, 257, 54), (130, 129, 123)])
+def test_rbf_decision_gemm(K, n, nsv, d):
+    g = torch.Generator(device="cuda").manual_seed(n + nsv)
+    x = torch.rand(n, d, device="cuda", generator=g)
+    sv = torch.rand(nsv, d, device="cuda", generator=g)
+    coef = torch.randn(nsv, device="cuda", generator=g)
+    gamma = 1.0 / d
+    got = K.rbf_decision(x, sv, coef, gamma, 0.25)
+    ref = _rbf_ref(sv, x, gamma).T @ coef.double() - 0.25
+    assert torch.allclose(got.double(), ref, rtol=1e-4, atol=1e-4 * (1 + coef.abs().sum().item() / 100))
+
+
+def test_compact(K):
+    a = torch.rand(100003, device="cuda")
+    a[a < 0.7] = 0
+    got = K.compact_positive(a).long()
+    ref = torch.nonzero(a > 0).flatten()
+    assert torch.equal(got, ref)

@@ -1,0 +1,126 @@
+"""Device-resident SMO on MI355X vs the CPU oracle; cache modes; simulated
+multi-rank on one GPU; checkpoint/resume; predictor; bench on GPU."""
+import json
+import os
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from dpsvm_amd import SVC, load_model
+from dpsvm_amd.utils.datasets import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _close(g, c, n):
+    assert g.converged_ and c.converged_
+    assert abs(g.n_iter_ - c.n_iter_) <= max(10, c.n_iter_ // 50)
+    assert abs(g.n_support_ - c.n_support_) <= max(3, c.n_support_ // 100)
+    assert abs(g.b_ - c.b_) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["dense", "lru", "lru_tiny", "partitioned"])
+def test_gpu_matches_cpu(mode):
+    X, y = synthetic("adult", n=4000, seed=3)
+    kw = dict(C=1.0, gamma=0.05, eps=1e-3)
+    cpu = SVC(device="cpu", **kw).fit(X, y)
+    extra = {"dense": {}, "lru": {"cache_lines": 256}, "lru_tiny": {"cache_lines": 2, "spec_rows": 0},
+             "partitioned": {"x_mode": "partitioned"}}[mode]
+    gpu = SVC(device="cuda", **kw, **extra).fit(X, y)
+    _close(gpu, cpu, 4000)
+    if mode == "dense":
+        assert gpu.setup_info_["cache_lines"] == 4000
+    else:
+        assert gpu.stats_["cache_misses"] > 0
+    assert abs(gpu.train_accuracy() - cpu.score(X, y)) < 0.01
+
+
+def test_gpu_box_clip_and_max_iter():
+    X, y = synthetic("blobs", n=3000, d=16, seed=5, sep=1.0)
+    g = SVC(C=1.0, gamma=0.1, clip="box", device="cuda").fit(X, y)
+    assert g.converged_ and abs(float((g.alpha_ * y).sum())) < 1e-2
+    g2 = SVC(C=1.0, gamma=0.1, max_iter=1000, device="cuda").fit(X, y)
+    assert g2.n_iter_ == 1000 and g2.status_ == 2
+    g3 = SVC(C=1.0, gamma=0.1, max_iter=1000, use_graph=False, device="cuda").fit(X, y)
+    assert np.array_equal(g2.alpha_, g3.alpha_)  # graph replay == eager launches
+
+
+def test_simulated_ranks_one_gpu_identical(C):
+    """P ranks as threads sharing the GPU (host-staged collectives) must make
+    bit-identical decisions to one rank."""
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    ref = SVC(**kw).fit(X, y)
+    for world, extra in ((2, {}), (3, {"x_mode": "partitioned"}), (4, {"cache_lines": 64})):
+        g = C.ThreadCommGroup(world)
+        comms = [g.comm(r) for r in range(world)]
+        out = [None] * world
+        errs = []
+
+        def work(r):
+            try:
+                out[r] = SVC(**kw, **extra).fit(X, y, comm=comms[r])
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert not errs, errs
+        for r in range(world):
+            assert out[r].n_iter_ == ref.n_iter_, (world, extra)
+            assert np.array_equal(out[r].alpha_, ref.alpha_)
+
+
+def test_gpu_checkpoint_resume(tmp_path):
+    X, y = synthetic("blobs", n=5000, d=24, seed=9, sep=1.0)
+    full = SVC(C=1.0, gamma=0.05, device="cuda").fit(X, y)
+    ck = str(tmp_path / "ck.bin")
+    part = SVC(C=1.0, gamma=0.05, device="cuda", max_iter=full.n_iter_ // 2, checkpoint_path=ck,
+               checkpoint_every=max(1, full.n_iter_ // 5)).fit(X, y)
+    assert not part.converged_ and os.path.exists(ck)
+    res = SVC(C=1.0, gamma=0.05, device="cuda").fit(X, y, resume=ck)
+    assert res.n_iter_ == full.n_iter_
+    assert np.array_equal(res.alpha_, full.alpha_)
+
+
+def test_gpu_predictor_and_model_file(tmp_path):
+    X, y = synthetic("mnist-parity", n=3000, seed=4)
+    clf = SVC(C=10.0, gamma=0.02, device="cuda").fit(X, y)
+    Xt, yt = synthetic("mnist-parity", n=1000, seed=5)
+    dec_gpu = clf.decision_function(Xt)
+    p = str(tmp_path / "m.txt")
+    clf.save(p)
+    m = load_model(p, device="cpu")
+    dec_cpu = m.decision_function(Xt)
+    assert np.allclose(dec_gpu, dec_cpu, atol=2e-4, rtol=1e-4)
+    assert load_model(p, device="cuda").score(Xt, yt) > 0.9
+
+
+def test_mnist_shape_headline_converges():
+    """The BASELINE config (60000 x 784, C=10, gamma=0.25, tol=1e-3) on one GPU."""
+    X, y = synthetic("mnist", n=60000, seed=0)
+    clf = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
+    assert clf.converged_
+    assert clf.fit_time_ < 30.0
+    assert clf.train_accuracy() > 0.99
+
+
+def test_bench_gpu_small():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--samples", "8000", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
+    assert out["converged"] and out["n_gpus"] == 1 and out["train_accuracy"] > 0.99
