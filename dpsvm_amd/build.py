@@ -42,6 +42,7 @@ LIB_SOURCES = [
     "solver/smo_gpu.hip",
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
+    "kernels/smo_fused.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

@@ -66,6 +66,20 @@ struct alignas(16) CandRecord {
   uint64_t key_hi, key_lo;
 };
 
+// Dense-mode fused iteration (smo_fused): kernel t derives pair t from the
+// partials of kernel t-1 redundantly in every workgroup, so one launch (+ one
+// collective when world > 1) is one SMO iteration.  The record carries pair
+// t's new alphas; they are committed to the alpha array by kernel t+1 (lazy
+// commit avoids a read/write race between workgroups of kernel t).
+struct alignas(16) FusedRec {
+  int32_t i_hi, i_lo;   // pair updated by the producing kernel (-1: none)
+  float a_hi, a_lo;     // its new alphas (a_hi wins when i_hi == i_lo)
+  int32_t iter, done;   // SMO iterations completed; DoneCode
+  float b_hi, b_lo;
+};
+constexpr int kFusedThreads = 256;
+constexpr int kStatusEvery = 32;  // host-mapped status refresh period (iterations)
+
 struct SmoArgs {
   const float* x;        // device X rows [x_rows][dp] (zero padded)
   const float* xsq;      // [n] global |x|^2
@@ -94,6 +108,8 @@ struct SmoArgs {
   int32_t clip;
   float C, gamma, eps, tau;
   int64_t max_iter;
+  int32_t fused_rows;   // rows per workgroup of smo_fused (multiple of kFusedThreads)
+  int32_t fused_G;      // workgroups of smo_fused (same on every rank)
 };
 
 }  // namespace dpsvm

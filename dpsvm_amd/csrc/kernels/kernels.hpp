@@ -20,6 +20,9 @@ void smo_step(const SmoArgs& a, hipStream_t s);
 void smo_local_record(const SmoArgs& a, hipStream_t s);
 void smo_finalize(const SmoArgs& a, hipStream_t s);
 size_t smo_rows_lds_bytes(int dp);
+// dense mode: init (selection only, mode 0) or one fused SMO iteration (mode 1)
+void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out, const FusedRec* r_in,
+               FusedRec* r_out, hipStream_t s);
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)

@@ -72,6 +72,9 @@ struct GpuSolver::Impl {
   SmoStatus* status_h = nullptr;  // host view
   SmoStatus* status_d = nullptr;  // device view
   uint8_t *records = nullptr, *my_record = nullptr;
+  uint64_t* pf = nullptr;  // dense fused mode: two partial buffers [2][2*Gf]
+  FusedRec* rf = nullptr;  // dense fused mode: two records
+  int64_t Gf = 0, RBf = 0;
   // host staging for host-memory communicators
   std::vector<uint64_t> h_partials;
   std::vector<uint8_t> h_records;
@@ -93,7 +96,7 @@ struct GpuSolver::Impl {
     if (graph) (void)hipGraphDestroy(graph);
     for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines,
                       (void*)slot_of, (void*)key_of, (void*)lru_prev, (void*)lru_next,
-                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record})
+                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf})
       if (ptr) (void)hipFree(ptr);
     if (status_h) (void)hipHostFree(status_h);
     for (auto& e : ev)
@@ -124,8 +127,32 @@ struct GpuSolver::Impl {
   }
 
   // one SMO iteration on `stream` (no host synchronisation for device comms)
-  void enqueue_iteration() {
-    if (!dense) launch::smo_rows(args, stream);
+  // dense fused iteration k of a block (k even <-> reads buffer 1, writes 0)
+  void enqueue_fused(int k) {
+    const int wi = k & 1, ri = wi ^ 1;
+    uint64_t* pout = pf + (size_t)wi * 2 * Gf;
+    launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
+    if (world > 1) allreduce_keys(pout, 2 * Gf);
+  }
+
+  void allreduce_keys(uint64_t* buf, int64_t count) {
+    if (comm->device_memory()) {
+      comm->allreduce_min_u64(buf, (size_t)count, stream);
+    } else {
+      if ((int64_t)h_partials.size() < count) h_partials.resize((size_t)count);
+      HIP_CHECK(hipMemcpyAsync(h_partials.data(), buf, 8 * count, hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      comm->allreduce_min_u64(h_partials.data(), (size_t)count, nullptr);
+      HIP_CHECK(hipMemcpyAsync(buf, h_partials.data(), 8 * count, hipMemcpyHostToDevice, stream));
+    }
+  }
+
+  void enqueue_iteration(int k) {
+    if (dense) {
+      enqueue_fused(k);
+      return;
+    }
+    launch::smo_rows(args, stream);
     launch::smo_step(args, stream);
     if (world > 1) {
       if (replicated) {
@@ -161,7 +188,7 @@ struct GpuSolver::Impl {
     if (gexec) return;
     HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
     try {
-      for (int i = 0; i < iters; ++i) enqueue_iteration();
+      for (int i = 0; i < iters; ++i) enqueue_iteration(i);
     } catch (...) {
       hipGraph_t g;
       (void)hipStreamEndCapture(stream, &g);
@@ -182,6 +209,15 @@ struct GpuSolver::Impl {
     ck.clip = (int)p.clip; ck.iter = st.iter; ck.b_hi = st.b_hi; ck.b_lo = st.b_lo;
     ck.alpha.resize((size_t)n);
     HIP_CHECK(hipMemcpy(ck.alpha.data(), alpha, n * 4, hipMemcpyDeviceToHost));
+    if (dense) {
+      // the latest pair's alphas are still pending in the record of the last kernel
+      FusedRec r;
+      HIP_CHECK(hipMemcpy(&r, rf + 1, sizeof(r), hipMemcpyDeviceToHost));
+      if (r.i_hi >= 0) {
+        ck.alpha[r.i_lo] = r.a_lo;
+        ck.alpha[r.i_hi] = r.a_hi;
+      }
+    }
     std::vector<float> floc((size_t)ldl, 0.f), fall((size_t)ldl * world);
     HIP_CHECK(hipMemcpy(floc.data(), f, nl * 4, hipMemcpyDeviceToHost));
     if (world > 1) {
@@ -368,6 +404,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.L = m.dense ? n : std::max<int64_t>(2, std::min<int64_t>(want_lines, n));
   DPSVM_CHECK(m.L * line_bytes <= (double)freeb, "not enough device memory for 2 kernel-row lines");
   m.lines = dmalloc<float>((size_t)m.L * m.ldl, &m.bytes);
+  if (m.dense) {
+    // fused iteration geometry: <= ~256 workgroups, rows per workgroup a multiple of 256
+    const int64_t per = (nl_max + 255) / 256;
+    m.RBf = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
+    m.Gf = std::max<int64_t>(1, (nl_max + m.RBf - 1) / m.RBf);
+    m.pf = dmalloc<uint64_t>((size_t)4 * m.Gf, &m.bytes);
+    m.rf = dmalloc<FusedRec>(2, &m.bytes);
+  }
   if (!m.dense) {
     m.slot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
     m.key_of = dmalloc<int32_t>((size_t)m.L, &m.bytes);
@@ -410,6 +454,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.eps = m.p.eps;
   a.tau = m.p.tau;
   a.max_iter = m.p.max_iter;
+  a.fused_rows = (int32_t)m.RBf;
+  a.fused_G = (int32_t)m.Gf;
 
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
@@ -504,9 +550,22 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
                            m.dp, m.gamma, m.lines, m.ldl, m.stream);
     res.rows_computed = m.n;
     res.x_passes = 1;
+    // fused-iteration seed: record "no pending pair" in buffer 1 + initial keys
+    FusedRec r0;
+    r0.i_hi = r0.i_lo = -1;
+    r0.a_hi = r0.a_lo = 0.f;
+    r0.iter = (int32_t)iter0;
+    r0.done = kRunning;
+    r0.b_hi = b_hi0;
+    r0.b_lo = b_lo0;
+    HIP_CHECK(hipMemcpyAsync(m.rf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
+    uint64_t* p1 = m.pf + 2 * m.Gf;
+    launch::smo_fused(m.args, 0, nullptr, p1, nullptr, nullptr, m.stream);
+    if (m.world > 1) m.allreduce_keys(p1, 2 * m.Gf);
   }
   const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
-  const int B = std::max(1, m.p.graph_block);
+  int B = std::max(1, m.p.graph_block);
+  if (m.dense) B = std::max(2, (B + 1) / 2 * 2);  // ping-pong parity must survive graph replays
   if (graphs) {
     try {
       m.build_graph(B);
@@ -522,7 +581,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     if (m.gexec) {
       HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
     } else {
-      for (int i = 0; i < B; ++i) m.enqueue_iteration();
+      for (int i = 0; i < B; ++i) m.enqueue_iteration(i);
     }
     HIP_CHECK(hipEventRecord(m.ev[blocks & 1], m.stream));
     if (blocks > 0) {

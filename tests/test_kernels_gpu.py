@@ -96,7 +96,7 @@ def test_rbf_decision_gemm(K, n, nsv, d):
     coef = torch.randn(nsv, device="cuda", generator=g)
     gamma = 1.0 / d
     got = K.rbf_decision(x, sv, coef, gamma, 0.25)
-    ref = _rbf_ref(sv, x, gamma).T @ coef.double() - 0.25
+    ref = _rbf_ref(sv, x, gamma) @ coef.double() - 0.25
     assert torch.allclose(got.double(), ref, rtol=1e-4, atol=1e-4 * (1 + coef.abs().sum().item() / 100))
 
 
