@@ -43,6 +43,7 @@ LIB_SOURCES = [
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/smo_fused.hip",
+    "kernels/microbench.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

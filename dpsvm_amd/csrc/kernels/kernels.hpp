@@ -49,3 +49,10 @@ void gather_sv(const float* x, int64_t x_row0, const float* xsq, const float* al
 
 }  // namespace launch
 }  // namespace dpsvm
+
+namespace dpsvm {
+namespace launch {
+// microsecond cost per kernel of a graph-replayed chain of dependent empty kernels
+double launch_floor_us(int blocks, int threads, int chain, int reps);
+}  // namespace launch
+}  // namespace dpsvm

@@ -2,19 +2,23 @@
 // iteration, no finalize kernel and no in-kernel grid synchronisation.
 //
 // Kernel t:
-//   1. every workgroup reads the previous kernel's per-workgroup selection keys
-//      (all-reduced across ranks when world > 1) and reduces them to the same
-//      global pair (i_hi, i_lo, b_hi, b_lo) — redundantly, deterministically;
-//   2. every workgroup computes eta from |x_hi - x_lo|^2 and the alpha update
-//      (identical arithmetic everywhere; common.hpp pair_update);
-//   3. the f update of its own rows from the resident Gram rows K[i_hi][.],
-//      K[i_lo][.] (svmTrain.cu:98-137), I-set classification and the
-//      per-workgroup argmin/argmax keys for iteration t+1;
-//   4. workgroup 0 commits the PREVIOUS pair's alphas (lazy: nobody reads those
-//      two entries from memory in this launch — readers take them from the
-//      record) and publishes this pair's record + the host status.
+//   1. every WAVE reads the previous kernel's per-workgroup selection keys
+//      (all-reduced across ranks when world > 1) and reduces them with wave-64
+//      shuffles to the global pair (i_hi, i_lo, b_hi, b_lo) — redundantly and
+//      deterministically, so no LDS round trip or barrier is needed;
+//   2. every wave computes |x_hi - x_lo|^2 (same shuffle tree everywhere), eta
+//      and the alpha update (common.hpp pair_update, identical arithmetic);
+//   3. the f update of the workgroup's rows from the resident Gram rows
+//      K[i_hi][.], K[i_lo][.] (svmTrain.cu:98-137), I-set classification and
+//      the per-workgroup argmin/argmax keys for iteration t+1 (the only
+//      workgroup barrier of the kernel);
+//   4. workgroup 0 commits the PREVIOUS pair's alphas (lazy: no one reads
+//      those two entries from memory in this launch — readers take them from
+//      the record) and publishes this pair's record and the host status.
+// Latency structure: two dependent global round trips (keys -> Gram rows / x
+// rows), everything row-local is prefetched before the first one.
 // Reference per-iteration path: svmTrainMain.cpp:235-310 (>= 7 blocking host
-// round trips + a TCP Allgather); two kernels + host in the CUDA build.
+// round trips + a TCP Allgather).
 #include <hip/hip_runtime.h>
 
 #include "dpsvm/common.hpp"
@@ -26,6 +30,8 @@
 namespace dpsvm {
 namespace dev {
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void publish_status(SmoStatus* st, int iter, int done, float b_hi, float b_lo) {
   if (!st) return;
   st->iter = iter;
@@ -35,41 +41,84 @@ __device__ __forceinline__ void publish_status(SmoStatus* st, int iter, int done
   __atomic_store_n(&st->seq, iter, __ATOMIC_RELEASE);
 }
 
+__device__ __forceinline__ void commit_pending(const SmoArgs& a, const FusedRec& r) {
+  if (r.i_hi >= 0) {
+    a.alpha[r.i_lo] = r.a_lo;
+    a.alpha[r.i_hi] = r.a_hi;  // hi written last (svmTrainMain.cpp:298-299)
+  }
+}
+
+// per-workgroup min of two keys -> p_out[blockIdx] (the kernel's one barrier)
+__device__ __forceinline__ void store_block_keys(uint64_t kh, uint64_t kl, uint64_t* p_out, uint64_t* scr) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  kh = wave_min_u64(kh);
+  kl = wave_min_u64(kl);
+  if (lane == 0) {
+    scr[wave] = kh;
+    scr[4 + wave] = kl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < kFusedThreads / 64; ++w) {
+      kh = scr[w] < kh ? scr[w] : kh;
+      kl = scr[4 + w] < kl ? scr[4 + w] : kl;
+    }
+    u64x2 v;
+    v.x = kh;
+    v.y = kl;
+    *(u64x2*)(p_out + 2 * blockIdx.x) = v;
+  }
+}
+
 __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int mode,
                                                                   const uint64_t* __restrict__ p_in,
                                                                   uint64_t* __restrict__ p_out,
                                                                   const FusedRec* __restrict__ r_in,
                                                                   FusedRec* __restrict__ r_out) {
-  __shared__ uint64_t kscr[2 * (kFusedThreads / 64)];
-  __shared__ float fscr[kFusedThreads / 64];
-  const int tid = threadIdx.x;
+  static_assert(kFusedThreads == 256, "4 waves assumed");
+  __shared__ uint64_t kscr[8];
+  const int tid = threadIdx.x, lane = tid & 63;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
   const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
+  const int64_t j0 = row0 + tid;
+  const bool has0 = j0 < row_end;
+
+  // ---- prefetch everything row-local (independent of the pair) ----
+  float f0 = 0.f, a0 = 0.f, y0 = 0.f;
+  if (has0) {
+    f0 = a.f[j0];
+    a0 = a.alpha[a.off + j0];
+    y0 = a.y[a.off + j0];
+  }
 
   if (mode == 0) {  // initial selection over the current f / alpha
     uint64_t kh = kKeyNone, kl = kKeyNone;
-    for (int64_t j = row0 + tid; j < row_end; j += kFusedThreads) {
+    for (int64_t j = j0; j < row_end; j += kFusedThreads) {
       const int64_t g = a.off + j;
-      const float fj = a.f[j], av = a.alpha[g], yv = a.y[g];
+      const float fj = j == j0 ? f0 : a.f[j];
+      const float av = j == j0 ? a0 : a.alpha[g];
+      const float yv = j == j0 ? y0 : a.y[g];
       if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); kh = k < kh ? k : kh; }
       if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); kl = k < kl ? k : kl; }
     }
-    block_min2_u64<kFusedThreads>(kh, kl, kscr);
-    if (tid == 0) {
-      p_out[2 * blockIdx.x] = kh;
-      p_out[2 * blockIdx.x + 1] = kl;
-    }
+    store_block_keys(kh, kl, p_out, kscr);
     return;
   }
 
   const FusedRec rin = *r_in;
+  // ---- 1. global pair: every wave reduces all workgroup keys (16-B loads) ----
+  uint64_t kh = kKeyNone, kl = kKeyNone;
+  const u64x2* pk = (const u64x2*)p_in;
+  for (int b = lane; b < a.fused_G; b += 64) {
+    const u64x2 v = pk[b];
+    kh = v.x < kh ? v.x : kh;
+    kl = v.y < kl ? v.y : kl;
+  }
   if (rin.done != kRunning) {
     if (lead) {
-      if (rin.i_hi >= 0) {
-        a.alpha[rin.i_lo] = rin.a_lo;
-        a.alpha[rin.i_hi] = rin.a_hi;
-      }
+      commit_pending(a, rin);
       FusedRec o = rin;
       o.i_hi = o.i_lo = -1;
       *r_out = o;
@@ -77,21 +126,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
     }
     return;
   }
-
-  // ---- 1. global pair (redundant in every workgroup) ----
-  uint64_t kh = kKeyNone, kl = kKeyNone;
-  for (int b = tid; b < a.fused_G; b += kFusedThreads) {
-    const uint64_t h = p_in[2 * b], l = p_in[2 * b + 1];
-    kh = h < kh ? h : kh;
-    kl = l < kl ? l : kl;
-  }
-  block_min2_u64<kFusedThreads>(kh, kl, kscr);
+  kh = wave_min_u64(kh);
+  kl = wave_min_u64(kl);
   if (kh == kKeyNone || kl == kKeyNone) {
     if (lead) {
-      if (rin.i_hi >= 0) {
-        a.alpha[rin.i_lo] = rin.a_lo;
-        a.alpha[rin.i_hi] = rin.a_hi;
-      }
+      commit_pending(a, rin);
       FusedRec o = rin;
       o.i_hi = o.i_lo = -1;
       o.done = kNoPair;
@@ -103,32 +142,29 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   const int i_hi = (int)key_index(kh), i_lo = (int)key_index(kl);
   const float b_hi = key_value(kh), b_lo = -key_value(kl);
 
-  // issue the Gram-row loads of this thread's first row early (dense: line = row)
-  const int64_t j0 = row0 + tid;
+  // ---- 2. second round trip: Gram rows, x rows, pair alphas/labels ----
   const float* line_hi = a.lines + (int64_t)i_hi * a.ldl;
   const float* line_lo = a.lines + (int64_t)i_lo * a.ldl;
-  float kh0 = 0.f, kl0 = 0.f, f0 = 0.f;
-  if (j0 < row_end) {
+  float kh0 = 0.f, kl0 = 0.f;
+  if (has0) {
     kh0 = line_hi[j0];
     kl0 = line_lo[j0];
-    f0 = a.f[j0];
   }
-
-  // ---- 2. eta and the alpha update (identical arithmetic in every workgroup) ----
+  const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];
+  const float al_hi = a.alpha[i_hi], al_lo = a.alpha[i_lo];
   const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
   const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
   float part = 0.f;
-  for (int k = tid; k < a.d; k += kFusedThreads) {
-    const float t = xh[k] - xl[k];
-    part += t * t;
+  for (int k = 4 * lane; k < a.dp; k += 256) {  // dp is a multiple of 16, padding is zero
+    const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
+    const f4 t = h - l;
+    part += (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
   }
-  const float dist2 = block_sum<kFusedThreads>(part, fscr);
-  auto alpha_now = [&](int i) -> float {
-    if (i == rin.i_hi) return rin.a_hi;  // pending commit of the previous pair (hi wins)
-    if (i == rin.i_lo) return rin.a_lo;
-    return a.alpha[i];
-  };
-  const float a_hi_old = alpha_now(i_hi), a_lo_old = alpha_now(i_lo);
+  const float dist2 = wave_sum(part);  // identical tree in every wave -> identical value
+
+  // pending commit of the previous pair overrides memory (hi wins)
+  const float a_hi_old = i_hi == rin.i_hi ? rin.a_hi : (i_hi == rin.i_lo ? rin.a_lo : al_hi);
+  const float a_lo_old = i_lo == rin.i_hi ? rin.a_hi : (i_lo == rin.i_lo ? rin.a_lo : al_lo);
   int done = kRunning;
   float c_hi = 0.f, c_lo = 0.f, a_hi_new = a_hi_old, a_lo_new = a_lo_old;
   const int iter = rin.iter + 1;
@@ -136,8 +172,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
     done = kNonFinite;
   } else {
     const float k_hl = expf(-a.gamma * dist2);
-    const PairUpdate u = pair_update(a_hi_old, a_lo_old, a.y[i_hi], a.y[i_lo], b_hi, b_lo, k_hl, a.C, a.tau,
-                                     a.clip, i_hi == i_lo);
+    const PairUpdate u =
+        pair_update(a_hi_old, a_lo_old, y_hi, y_lo, b_hi, b_lo, k_hl, a.C, a.tau, a.clip, i_hi == i_lo);
     a_hi_new = u.a_hi_new;
     a_lo_new = u.a_lo_new;
     c_hi = u.c_hi;
@@ -148,10 +184,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
 
   // ---- 4. commit previous pair, publish this one ----
   if (lead) {
-    if (rin.i_hi >= 0) {
-      a.alpha[rin.i_lo] = rin.a_lo;
-      a.alpha[rin.i_hi] = rin.a_hi;
-    }
+    commit_pending(a, rin);
     FusedRec o;
     const bool upd = done != kNonFinite;
     o.i_hi = upd ? i_hi : -1;
@@ -167,15 +200,15 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   }
 
   // ---- 3. f update + classification of this workgroup's rows ----
+  const bool upd_f = c_hi != 0.f || c_lo != 0.f;
   uint64_t nh = kKeyNone, nlk = kKeyNone;
   for (int64_t j = j0; j < row_end; j += kFusedThreads) {
-    float fj, khv, klv;
-    if (j == j0) {
-      fj = f0; khv = kh0; klv = kl0;
-    } else {
-      fj = a.f[j]; khv = line_hi[j]; klv = line_lo[j];
-    }
-    if (c_hi != 0.f || c_lo != 0.f) {
+    const bool first = j == j0;
+    const int64_t g = a.off + j;
+    float fj = first ? f0 : a.f[j];
+    if (upd_f) {
+      const float khv = first ? kh0 : line_hi[j];
+      const float klv = first ? kl0 : line_lo[j];
       float delta;
       if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * khv) + (c_lo * klv);
       else if (c_hi != 0.f) delta = c_hi * khv;
@@ -184,24 +217,19 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       a.f[j] = fj;
     }
     if (done == kRunning) {
-      const int64_t g = a.off + j;
       float av;
       if (g == i_hi) av = a_hi_new;
       else if (g == i_lo) av = a_lo_new;
       else if (g == rin.i_hi) av = rin.a_hi;
       else if (g == rin.i_lo) av = rin.a_lo;
-      else av = a.alpha[g];
-      const float yv = a.y[g];
+      else av = first ? a0 : a.alpha[g];
+      const float yv = first ? y0 : a.y[g];
       if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
       if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
     }
   }
   if (done != kRunning) return;  // uniform
-  block_min2_u64<kFusedThreads>(nh, nlk, kscr);
-  if (tid == 0) {
-    p_out[2 * blockIdx.x] = nh;
-    p_out[2 * blockIdx.x + 1] = nlk;
-  }
+  store_block_keys(nh, nlk, p_out, kscr);
 }
 
 }  // namespace dev

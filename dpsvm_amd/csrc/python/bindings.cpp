@@ -13,6 +13,7 @@
 #include "dpsvm/common.hpp"
 #include "dpsvm/io.hpp"
 #include "dpsvm/solver.hpp"
+#include "../kernels/kernels.hpp"
 
 namespace py = pybind11;
 using namespace dpsvm;
@@ -400,6 +401,8 @@ PYBIND11_MODULE(_C, m) {
     Shard s = shard_of(n, rank, world);
     return py::make_tuple(s.offset, s.size);
   });
+  m.def("launch_floor_us", &launch::launch_floor_us, py::arg("blocks") = 256, py::arg("threads") = 256,
+        py::arg("chain") = 64, py::arg("reps") = 50, py::call_guard<py::gil_scoped_release>());
   m.def("device_count", &device_count);
   m.def("device_name", &device_name);
   m.attr("NQ") = 16;
