@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Summarise DPSVM_STAMPS in-kernel timestamps of the fused SMO iteration.
+
+Slots (s_memrealtime, 100 MHz): 0 entry, 1 pair known (first round trip +
+wave reduction), 2 eta/alpha update done (second round trip), 3 row loop done,
+4 keys stored (end).  Workgroup 0 and workgroup G-1 of each iteration.
+Usage: DPSVM_STAMPS=/tmp/st python bench.py ...; python bench/stamps_report.py /tmp/st.rank0
+"""
+import json
+import sys
+
+import numpy as np
+
+RING, SLOTS = 4096, 6
+
+
+def main(path):
+    a = np.fromfile(path, dtype=np.uint64).reshape(RING, 2, SLOTS).astype(np.int64)
+    ok = (a[:, 0, 0] > 0) & (a[:, 0, 4] > 0) & (a[:, 1, 4] > 0)
+    a = a[ok]
+    out = {}
+    for b, name in ((0, "wg0"), (1, "wglast")):
+        d = np.diff(a[:, b, :5], axis=1) * 10.0  # ns
+        out[name] = {
+            "entry->pair_ns": float(np.median(d[:, 0])),
+            "pair->update_ns": float(np.median(d[:, 1])),
+            "update->rows_ns": float(np.median(d[:, 2])),
+            "rows->end_ns": float(np.median(d[:, 3])),
+            "entry->end_ns": float(np.median((a[:, b, 4] - a[:, b, 0]) * 10.0)),
+        }
+    # kernel-to-kernel: entry of iteration t+1 minus end of iteration t (workgroup 0),
+    # only for consecutive ring slots
+    it0 = a[:, 0, 0]
+    nxt = it0[1:] - a[:-1, 0, 4]
+    period = np.diff(it0) * 10.0
+    out["iter_period_ns_median"] = float(np.median(period[period > 0]))
+    out["end_to_next_entry_ns_median"] = float(np.median(nxt[nxt > 0] * 10.0))
+    out["wg_skew_entry_ns_median"] = float(np.median((a[:, 1, 0] - a[:, 0, 0]) * 10.0))
+    out["samples"] = int(len(a))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -110,6 +110,11 @@ struct SmoArgs {
   int64_t max_iter;
   int32_t fused_rows;   // rows per workgroup of smo_fused (multiple of kFusedThreads)
   int32_t fused_G;      // workgroups of smo_fused (same on every rank)
+  // diagnostics (DPSVM_STAMPS): s_memrealtime stamps of workgroups 0 and G-1,
+  // ring of kStampRing iterations x 2 workgroups x kStampSlots
+  uint64_t* stamps;
 };
+constexpr int kStampRing = 4096;
+constexpr int kStampSlots = 6;
 
 }  // namespace dpsvm

@@ -32,6 +32,8 @@ struct Rng {
   }
 };
 
+constexpr uint64_t kTaskSeed = 0x5eed5eedull;
+
 inline uint64_t row_seed(uint64_t seed, uint64_t kind, int64_t row) {
   return mix64(seed * 0x100000001b3ull ^ (kind << 56) ^ mix64((uint64_t)row + 0x51ed27ull));
 }
@@ -114,14 +116,16 @@ Dataset make_synthetic(Synth kind, int64_t n, int d, uint64_t seed, int64_t row0
   if (kind == Synth::MnistParity) {
     side = (int)std::lround(std::sqrt((double)d));
     if (side * side != d) side = 0;
-    protos = digit_prototypes(seed, side ? side : 28);
+    // the "distribution" (prototypes, hidden rules) is fixed; the seed only
+    // picks the samples, so different seeds give train/test splits of one task
+    protos = digit_prototypes(kTaskSeed, side ? side : 28);
   }
   // adult: 14 categorical groups one-hot over 123 columns (a9a layout sizes)
   static const std::array<int, 14> adult_groups = {5, 8, 16, 16, 7, 14, 6, 5, 2, 3, 3, 3, 40, 2};
   // hidden linear rule for adult / covtype labels
   std::vector<float> w(d);
   {
-    Rng r(mix64(seed ^ 0xabcdefull ^ k));
+    Rng r(mix64(kTaskSeed ^ 0xabcdefull ^ k));
     for (int j = 0; j < d; ++j) w[j] = r.normal();
   }
 

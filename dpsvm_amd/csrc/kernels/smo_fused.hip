@@ -84,6 +84,14 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
   const int64_t j0 = row0 + tid;
   const bool has0 = j0 < row_end;
+  // diagnostics only (a.stamps == nullptr in normal runs)
+  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+  const uint64_t ts_entry = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto stamp = [&](int it, int slot, uint64_t v) {
+    if (stamping)
+      a.stamps[((size_t)(it % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots + slot] =
+          v ? v : __builtin_amdgcn_s_memrealtime();
+  };
 
   // ---- prefetch everything row-local (independent of the pair) ----
   float f0 = 0.f, a0 = 0.f, y0 = 0.f;
@@ -141,6 +149,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   }
   const int i_hi = (int)key_index(kh), i_lo = (int)key_index(kl);
   const float b_hi = key_value(kh), b_lo = -key_value(kl);
+  stamp(rin.iter, 0, ts_entry);
+  stamp(rin.iter, 1, 0);
 
   // ---- 2. second round trip: Gram rows, x rows, pair alphas/labels ----
   const float* line_hi = a.lines + (int64_t)i_hi * a.ldl;
@@ -182,6 +192,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
     else if (iter >= a.max_iter) done = kMaxIter;
   }
 
+  stamp(rin.iter, 2, 0);
   // ---- 4. commit previous pair, publish this one ----
   if (lead) {
     commit_pending(a, rin);
@@ -228,8 +239,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
     }
   }
+  stamp(rin.iter, 3, 0);
   if (done != kRunning) return;  // uniform
   store_block_keys(nh, nlk, p_out, kscr);
+  stamp(rin.iter, 4, 0);
 }
 
 }  // namespace dev

@@ -75,6 +75,8 @@ struct GpuSolver::Impl {
   uint64_t* pf = nullptr;  // dense fused mode: two partial buffers [2][2*Gf]
   FusedRec* rf = nullptr;  // dense fused mode: two records
   int64_t Gf = 0, RBf = 0;
+  uint64_t* stamps = nullptr;  // DPSVM_STAMPS diagnostics
+  std::string stamps_path;
   // host staging for host-memory communicators
   std::vector<uint64_t> h_partials;
   std::vector<uint8_t> h_records;
@@ -96,7 +98,7 @@ struct GpuSolver::Impl {
     if (graph) (void)hipGraphDestroy(graph);
     for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines,
                       (void*)slot_of, (void*)key_of, (void*)lru_prev, (void*)lru_next,
-                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf})
+                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)stamps})
       if (ptr) (void)hipFree(ptr);
     if (status_h) (void)hipHostFree(status_h);
     for (auto& e : ev)
@@ -456,6 +458,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.max_iter = m.p.max_iter;
   a.fused_rows = (int32_t)m.RBf;
   a.fused_G = (int32_t)m.Gf;
+  a.stamps = nullptr;
+  if (const char* sp = std::getenv("DPSVM_STAMPS")) {
+    m.stamps_path = std::string(sp) + ".rank" + std::to_string(m.rank);
+    const size_t cnt = (size_t)kStampRing * 2 * kStampSlots;
+    m.stamps = dmalloc<uint64_t>(cnt, &m.bytes);
+    HIP_CHECK(hipMemset(m.stamps, 0, cnt * 8));
+    a.stamps = m.stamps;
+  }
 
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
@@ -626,6 +636,14 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   res.rows_computed += st.rows_computed;
   res.x_passes += st.x_passes;
   res.spec_rows = st.spec_rows;
+  if (m.stamps) {
+    std::vector<uint64_t> h((size_t)kStampRing * 2 * kStampSlots);
+    HIP_CHECK(hipMemcpy(h.data(), m.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* fp = fopen(m.stamps_path.c_str(), "wb")) {
+      fwrite(h.data(), 8, h.size(), fp);
+      fclose(fp);
+    }
+  }
   res.alpha.resize((size_t)m.n);
   HIP_CHECK(hipMemcpy(res.alpha.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
   return res;
