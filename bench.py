@@ -76,6 +76,8 @@ def main(argv=None) -> int:
                     x_mode=a.x_mode, graph_block=a.graph_block)
     params = cfg.to_native(X.shape[1])
     comm = make_comm(ctx, a.comm)
+    if a.comm == "rccl" and n_ranks == 1:
+        params.force_collectives = True  # one-rank RCCL: exercise the collective + graph path
 
     def barrier():
         if n_ranks > 1:

@@ -74,6 +74,7 @@ struct SolverParams {
   std::string checkpoint_path;
   // debugging
   bool sync_debug = false;    // device sync + error check after every launch
+  bool force_collectives = false;  // run the per-iteration collective even at world 1 (tests RCCL/graph paths)
 };
 
 // Per-run result, gathered on every rank.

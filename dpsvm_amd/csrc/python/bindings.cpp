@@ -157,7 +157,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("verbose", &SolverParams::verbose)
       .def_readwrite("checkpoint_every", &SolverParams::checkpoint_every)
       .def_readwrite("checkpoint_path", &SolverParams::checkpoint_path)
-      .def_readwrite("sync_debug", &SolverParams::sync_debug);
+      .def_readwrite("sync_debug", &SolverParams::sync_debug)
+      .def_readwrite("force_collectives", &SolverParams::force_collectives);
 
   py::class_<Checkpoint>(m, "Checkpoint")
       .def(py::init<>())

@@ -134,8 +134,10 @@ struct GpuSolver::Impl {
     const int wi = k & 1, ri = wi ^ 1;
     uint64_t* pout = pf + (size_t)wi * 2 * Gf;
     launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
-    if (world > 1) allreduce_keys(pout, 2 * Gf);
+    if (collectives()) allreduce_keys(pout, 2 * Gf);
   }
+
+  bool collectives() const { return world > 1 || p.force_collectives; }
 
   void allreduce_keys(uint64_t* buf, int64_t count) {
     if (comm->device_memory()) {
@@ -156,7 +158,7 @@ struct GpuSolver::Impl {
     }
     launch::smo_rows(args, stream);
     launch::smo_step(args, stream);
-    if (world > 1) {
+    if (collectives()) {
       if (replicated) {
         if (comm->device_memory()) {
           comm->allreduce_min_u64(partials, 2 * (size_t)G, stream);
@@ -571,7 +573,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     HIP_CHECK(hipMemcpyAsync(m.rf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
     uint64_t* p1 = m.pf + 2 * m.Gf;
     launch::smo_fused(m.args, 0, nullptr, p1, nullptr, nullptr, m.stream);
-    if (m.world > 1) m.allreduce_keys(p1, 2 * m.Gf);
+    if (m.collectives()) m.allreduce_keys(p1, 2 * m.Gf);
   }
   const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
   int B = std::max(1, m.p.graph_block);

@@ -71,6 +71,7 @@ class SVCConfig:
     checkpoint_every: int = 0
     device: str = "auto"            # auto | cpu | cuda | cuda:N
     verbose: bool = False
+    force_collectives: bool = False  # run the per-iteration collective even with one rank (tests)
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -101,6 +102,7 @@ class SVCConfig:
         p.verbose = bool(self.verbose)
         p.checkpoint_every = int(self.checkpoint_every)
         p.checkpoint_path = self.checkpoint_path or ""
+        p.force_collectives = bool(self.force_collectives)
         return p
 
     def device_kind(self) -> tuple[str, int]:

@@ -150,7 +150,9 @@ def rccl_comm(ctx: DistContext):
 
     C = load()
     if ctx.world == 1:
-        return C.local_comm()
+        # a real one-rank RCCL communicator (exercises the collective + graph
+        # capture path on a single GPU; the solver needs force_collectives)
+        return C.rccl_comm(C.rccl_unique_id(), 0, 1, ctx.local_rank)
     obj = [C.rccl_unique_id() if ctx.rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=_host_group())
     return C.rccl_comm(obj[0], ctx.rank, ctx.world, ctx.local_rank)
@@ -158,7 +160,7 @@ def rccl_comm(ctx: DistContext):
 
 def make_comm(ctx: DistContext, kind: str = "auto"):
     """kind: auto (rccl on GPU, gloo on CPU) | rccl | gloo | local."""
-    if ctx.world == 1 or kind == "local":
+    if kind == "local" or (ctx.world == 1 and kind in ("auto", "gloo")):
         return load().local_comm()
     if kind == "auto":
         kind = "rccl" if ctx.device.startswith("cuda") else "gloo"

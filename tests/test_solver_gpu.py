@@ -126,3 +126,18 @@ def test_bench_gpu_small():
     assert r.returncode == 0, r.stderr
     out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
     assert out["converged"] and out["n_gpus"] == 1 and out["train_accuracy"] > 0.99
+
+
+@pytest.mark.parametrize("extra", [{}, {"cache_lines": 128}, {"x_mode": "partitioned"}])
+def test_rccl_one_rank_collective_path(C, extra):
+    """The RCCL collective + hipGraph capture path, exercised on one GPU with a
+    one-rank communicator (force_collectives): identical to the local path."""
+    X, y = synthetic("adult", n=3000, seed=1)
+    kw = dict(C=1.0, gamma=0.05, device="cuda", **extra)
+    ref = SVC(**kw).fit(X, y)
+    comm = C.rccl_comm(C.rccl_unique_id(), 0, 1, 0)
+    assert comm.name == "rccl" and comm.device_memory
+    got = SVC(force_collectives=True, **kw).fit(X, y, comm=comm)
+    assert got.n_iter_ == ref.n_iter_
+    assert np.array_equal(got.alpha_, ref.alpha_)
+    assert abs(got.train_accuracy() - ref.train_accuracy()) < 1e-9
