@@ -44,6 +44,7 @@ LIB_SOURCES = [
     "kernels/rbf_gemm.hip",
     "kernels/smo_fused.hip",
     "kernels/microbench.hip",
+    "kernels/compact.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

@@ -65,6 +65,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --cache-mb MB       :  device cache budget\n"
                "   --x-mode MODE       :  auto | replicated | partitioned\n"
                "   --spec N            :  speculative kernel rows per X pass (LRU mode, default 14)\n"
+               "   --host-cache-lines N:  pinned host spill tier for evicted kernel rows (LRU mode)\n"
                "   --graph-block N     :  SMO iterations per hipGraph (default 64); --no-graph\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
@@ -80,7 +81,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
   enum {
     OPT_RANKS = 1000, OPT_CPU, OPT_DEVICE, OPT_SYN, OPT_SEED, OPT_CLIP, OPT_CMB, OPT_XMODE, OPT_SPEC,
     OPT_GB, OPT_NOGRAPH, OPT_CK, OPT_CKE, OPT_RESUME, OPT_METRICS, OPT_LOG, OPT_PREC, OPT_LEGM,
-    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE
+    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -93,6 +94,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"seed", required_argument, 0, OPT_SEED},   {"clip", required_argument, 0, OPT_CLIP},
       {"cache-mb", required_argument, 0, OPT_CMB}, {"x-mode", required_argument, 0, OPT_XMODE},
       {"spec", required_argument, 0, OPT_SPEC},   {"graph-block", required_argument, 0, OPT_GB},
+      {"host-cache-lines", required_argument, 0, OPT_HOSTC},
       {"no-graph", no_argument, 0, OPT_NOGRAPH},  {"checkpoint", required_argument, 0, OPT_CK},
       {"checkpoint-every", required_argument, 0, OPT_CKE}, {"resume", required_argument, 0, OPT_RESUME},
       {"metrics-json", required_argument, 0, OPT_METRICS}, {"log-every", required_argument, 0, OPT_LOG},
@@ -132,6 +134,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
         break;
       }
       case OPT_SPEC: o.p.spec_rows = atoi(optarg); break;
+      case OPT_HOSTC: o.p.host_cache_lines = atoll(optarg); break;
       case OPT_GB: o.p.graph_block = atoi(optarg); break;
       case OPT_NOGRAPH: o.p.use_graph = false; break;
       case OPT_CK: o.p.checkpoint_path = optarg; break;

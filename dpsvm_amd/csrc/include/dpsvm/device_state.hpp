@@ -20,7 +20,13 @@ constexpr int kRowsKC = 1024;       // k-chunk of query vectors staged in LDS
 
 enum CacheMode : int32_t {
   kCacheDense = 0,  // whole Gram shard resident: line i == global row i
-  kCacheLRU = 1,    // LRU lines computed on demand by smo_rows
+  kCacheLRU = 1,    // CLOCK-replaced lines filled on demand by smo_rows (+ host tier)
+};
+
+// smo_rows per-query operation
+enum RowOp : int32_t {
+  kOpCompute = 0,   // MFMA X pass
+  kOpFetch = 1,     // copy from the pinned host tier (zero-copy PCIe loads)
 };
 
 enum DoneCode : int32_t {
@@ -36,19 +42,24 @@ struct alignas(16) SmoCtrl {
   int32_t iter;        // SMO updates applied so far
   int32_t done;        // DoneCode of the last finalize (0 = running)
   int32_t final_applied;  // 1 once the step after `done` applied the last f update
-  int32_t nq;          // rows smo_rows must compute this iteration
+  int32_t nq;          // rows smo_rows must fill this iteration (compute or fetch)
   int32_t i_hi, i_lo;
   int32_t line_hi, line_lo;  // lines holding K(hi,.) / K(lo,.) for the pending update
   float c_hi, c_lo;    // (alpha_new - alpha_old) * y, pending f-update coefficients
   float b_hi, b_lo;    // selection values of the last finalize
+  int32_t n_compute;   // queries with op kOpCompute (0: no X pass this iteration)
+  int32_t n_spill;     // queries whose victim line must first be copied to the host tier
   int32_t q_idx[kNQ];  // global rows to compute
   int32_t q_line[kNQ]; // destination lines
+  int32_t q_op[kNQ];   // RowOp
+  int32_t q_hsrc[kNQ];   // kOpFetch: host-tier line to copy from
+  int32_t q_hspill[kNQ]; // >= 0: host-tier line receiving the victim's old content
   float q_sq[kNQ];     // |x_q|^2
   const float* q_ptr[kNQ];  // query vectors (device X row, or a gathered record row)
-  // LRU (CacheLRU)
-  int32_t lru_head, lru_tail, lines_used, pad0;
+  // CLOCK hands (device lines, host-tier FIFO)
+  int32_t hand, hhand, pad0, pad1;
   // statistics
-  int64_t hits, misses, rows_computed, x_passes, spec_rows, spec_hits;
+  int64_t hits, misses, rows_computed, x_passes, spec_rows, host_hits, spills;
 };
 
 // Host-mapped status record (pinned, written by finalize thread 0).
@@ -57,7 +68,7 @@ struct alignas(16) SmoStatus {
   int32_t done;
   int32_t seq;
   float b_hi, b_lo;
-  int64_t hits, misses, rows_computed, x_passes, spec_rows, spec_hits;
+  int64_t hits, misses, rows_computed, x_passes, spec_rows, host_hits, spills;
 };
 
 // Partitioned-X candidate record: one per rank, all-gathered each iteration.
@@ -90,8 +101,11 @@ struct SmoArgs {
   int64_t ldl;           // line stride in floats (>= G*kStepRows)
   int32_t* slot_of;      // [n] line of a global row or -1 (LRU)
   int32_t* key_of;       // [L] global row in a line or -1
-  int32_t* lru_prev;     // [L]
-  int32_t* lru_next;     // [L]
+  uint8_t* ref;          // [L] CLOCK reference bits
+  float* hlines;         // [H][ldl] pinned host tier (device-mapped pointer) or nullptr
+  int32_t* hslot_of;     // [n] host-tier line of a global row or -1
+  int32_t* hkey_of;      // [H]
+  int32_t H;             // host-tier lines (0 = off)
   uint64_t* partials;    // [G][2] per-workgroup selection keys
   SmoCtrl* ctrl;
   SmoStatus* status;     // host-mapped

@@ -1,19 +1,27 @@
-// SMO iteration kernels for MI355X (gfx950, wave64).
+// SMO iteration kernels for the kernel-row-cache ("LRU") mode, MI355X (gfx950).
+// (The Gram-resident dense mode uses the single fused kernel in smo_fused.hip.)
 //
-//   smo_rows      LRU cache misses: K rows of up to 16 query vectors over the
-//                 local shard in ONE pass over X, fp32 MFMA 16x16x4 (exact f32),
-//                 query vectors staged in LDS, fused expansion + exp epilogue.
-//                 Replaces the reference's per-miss cublasSgemv x2 on two
-//                 streams (svmTrain.cu:212-249, K3/K4) and the Thrust functor
-//                 that turned dot products into RBF values (K5).
+//   smo_rows      fill this iteration's cache lines: (1) spill victims' old
+//                 contents to the pinned host tier, (2) fetch host-tier hits back
+//                 (zero-copy PCIe loads), (3) ONE X pass computing up to 16 new
+//                 kernel rows on fp32 MFMA 16x16x4 (exact f32), query vectors in
+//                 LDS, fused expansion + exp epilogue.  Replaces the reference's
+//                 per-miss cublasSgemv x2 on two streams (svmTrain.cu:212-249,
+//                 K3/K4) and the functor turning dot products into RBF values (K5).
 //   smo_step      pending f update (svmTrain.cu:98-137) fused with I-set
 //                 classification and the argmin/argmax selection
 //                 (svmTrain.cu:41-95 + 400-483): per-workgroup u64 keys.
-//   smo_finalize  one workgroup: global pair, eta from the two sample rows on
-//                 device (was host CBLAS, svmTrain.cu:696-714), alpha update and
-//                 clip (svmTrainMain.cpp:282-299), stop test, device LRU
-//                 bookkeeping (was host std::map/list, cache.cu:62-105), next
-//                 iteration's row requests, host-mapped status record.
+//   smo_finalize  one workgroup: global pair, eta on device (was host CBLAS,
+//                 svmTrain.cu:696-714), alpha update + clip
+//                 (svmTrainMain.cpp:282-299), stop test, the cache policy and
+//                 next iteration's row requests, host-mapped status record.
+//
+// Cache policy: CLOCK (second chance) instead of the reference's host-side
+// std::map + std::list LRU (cache.cu:62-105, O(L) lookup, host sync every
+// iteration).  Hits set a reference bit (one store); allocating up to 16 lines
+// is ONE parallel pass over a 1024-line window (ballot + prefix ranks), so the
+// policy costs a constant number of dependent global round trips.  Optional
+// pinned host tier = FIFO victim cache (SURVEY §5.7 spill tier).
 #include <hip/hip_runtime.h>
 
 #include "dpsvm/common.hpp"
@@ -52,12 +60,13 @@ __global__ void fill_i32_kernel(int32_t* p, int64_t n, int32_t v) {
 }
 
 // ---------------------------------------------------------------------------
-// smo_rows: K(q, j) for the ctrl->nq requested rows q and every local row j.
-// Grid: G workgroups x 256 threads; each wave owns two 16-row tiles.
-// MFMA 16x16x4 f32 operand map: A lane l -> (row l&15, k l>>4), B lane l ->
-// (k l>>4, query l&15).  Each lane loads a float4 of X (16 contiguous columns
-// per 16 rows and wave-instruction); component c of the float4 feeds MFMA c, a
-// permutation of k that the query operand (LDS, same float4) mirrors.
+// smo_rows
+// Grid: G workgroups x 256 threads, 128 local rows per workgroup; each wave
+// owns two 16-row MFMA tiles.  MFMA 16x16x4 f32 operand map: A lane l ->
+// (row l&15, k l>>4), B lane l -> (k l>>4, query l&15).  Each lane loads a
+// float4 of X (16 contiguous columns per 16 rows and wave-instruction);
+// component c of the float4 feeds MFMA c — a permutation of k that the query
+// operand (LDS, same float4) mirrors.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kStepThreads) void smo_rows_kernel(SmoArgs a) {
   const SmoCtrl* c = a.ctrl;
@@ -65,7 +74,33 @@ __global__ __launch_bounds__(kStepThreads) void smo_rows_kernel(SmoArgs a) {
   if (nq == 0 || (c->done != kRunning && c->final_applied)) return;
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t row0 = (int64_t)blockIdx.x * kStepRows + wave * 32;
+  const int64_t blk_row0 = (int64_t)blockIdx.x * kStepRows;
+
+  // (1) spill the victims' old contents to the host tier, (2) fetch host hits.
+  //     Each workgroup touches only its own 128 rows of every line.
+  if (a.hlines) {
+    const int half = tid >> 7, r = tid & 127;
+    if (c->n_spill > 0) {
+      for (int q = half; q < nq; q += 2) {
+        const int h = c->q_hspill[q];
+        if (h >= 0) {
+          const int64_t col = blk_row0 + r;
+          a.hlines[(int64_t)h * a.ldl + col] = a.lines[(int64_t)c->q_line[q] * a.ldl + col];
+        }
+      }
+      __syncthreads();  // old contents read before any new value lands
+    }
+    for (int q = half; q < nq; q += 2) {
+      if (c->q_op[q] == kOpFetch) {
+        const int64_t col = blk_row0 + r;
+        a.lines[(int64_t)c->q_line[q] * a.ldl + col] = a.hlines[(int64_t)c->q_hsrc[q] * a.ldl + col];
+      }
+    }
+  }
+  if (c->n_compute == 0) return;
+
+  // (3) X pass for the kOpCompute queries
+  const int64_t row0 = blk_row0 + wave * 32;
   const int64_t xbase = a.off - a.x_row0;  // local row -> device X row
   const int dp = a.dp;
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -79,7 +114,7 @@ __global__ __launch_bounds__(kStepThreads) void smo_rows_kernel(SmoArgs a) {
     for (int i = tid; i < kNQ * k4n; i += kStepThreads) {
       const int q = i / k4n, k4 = i - q * k4n;
       f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (q < nq) v = *(const f4*)(c->q_ptr[q] + kc + 4 * k4);
+      if (q < nq && c->q_op[q] == kOpCompute) v = *(const f4*)(c->q_ptr[q] + kc + 4 * k4);
       *(f4*)(wsm + q * ldw + 4 * k4) = v;
     }
     __syncthreads();
@@ -102,7 +137,7 @@ __global__ __launch_bounds__(kStepThreads) void smo_rows_kernel(SmoArgs a) {
   }
   // epilogue: lane holds rows (lane>>4)*4 + r of each tile for query lane&15
   const int q = lane & 15;
-  if (q < nq) {
+  if (q < nq && c->q_op[q] == kOpCompute) {
     const int64_t line = c->q_line[q];
     const float wsq = c->q_sq[q];
     float* out = a.lines + line * a.ldl;
@@ -193,50 +228,8 @@ __global__ __launch_bounds__(256) void smo_local_record_kernel(SmoArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// smo_finalize: one workgroup, identical on every rank.
+// smo_finalize: one workgroup (16 waves), identical on every rank.
 // ---------------------------------------------------------------------------
-struct Lru {
-  int32_t head, tail, used;
-};
-
-__device__ void lru_unlink(const SmoArgs& a, Lru& s, int l) {
-  const int p = a.lru_prev[l], nx = a.lru_next[l];
-  if (p >= 0) a.lru_next[p] = nx; else s.head = nx;
-  if (nx >= 0) a.lru_prev[nx] = p; else s.tail = p;
-}
-__device__ void lru_push_front(const SmoArgs& a, Lru& s, int l) {
-  a.lru_prev[l] = -1;
-  a.lru_next[l] = s.head;
-  if (s.head >= 0) a.lru_prev[s.head] = l;
-  s.head = l;
-  if (s.tail < 0) s.tail = l;
-}
-// returns line; *hit set; on miss the line is (re)assigned to `key` (LRU victim)
-__device__ int lru_get(const SmoArgs& a, Lru& s, int key, bool* hit) {
-  int l = a.slot_of[key];
-  if (l >= 0) {
-    *hit = true;
-    if (s.head != l) {
-      lru_unlink(a, s, l);
-      lru_push_front(a, s, l);
-    }
-    return l;
-  }
-  *hit = false;
-  if (s.used < a.L) {
-    l = s.used++;
-  } else {
-    l = s.tail;
-    lru_unlink(a, s, l);
-    const int old = a.key_of[l];
-    if (old >= 0) a.slot_of[old] = -1;
-  }
-  a.key_of[l] = key;
-  a.slot_of[key] = l;
-  lru_push_front(a, s, l);
-  return l;
-}
-
 __device__ void write_status(const SmoArgs& a, const SmoCtrl* c) {
   SmoStatus* st = a.status;
   if (!st) return;
@@ -249,15 +242,37 @@ __device__ void write_status(const SmoArgs& a, const SmoCtrl* c) {
   st->rows_computed = c->rows_computed;
   st->x_passes = c->x_passes;
   st->spec_rows = c->spec_rows;
-  st->spec_hits = c->spec_hits;
+  st->host_hits = c->host_hits;
+  st->spills = c->spills;
   __atomic_store_n(&st->seq, c->iter, __ATOMIC_RELEASE);
 }
 
+// exclusive prefix rank of `pred` over the workgroup (1024 threads); *total set
+__device__ __forceinline__ int block_rank(bool pred, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(pred);
+  if (lane == 0) wsum[wave] = __popcll(m);
+  __syncthreads();
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kFinThreads / 64; ++w) {
+    before += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return before + __popcll(m & ((1ull << lane) - 1ull));
+}
+
 __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
-  __shared__ uint64_t kscratch[2 * (kFinThreads / 64)];
-  __shared__ float fscratch[kFinThreads / 64];
-  __shared__ int s_nq;
-  __shared__ int32_t s_qidx[kNQ];
+  __shared__ uint64_t kscr[2 * (kFinThreads / 64)];
+  __shared__ float fscr[kFinThreads / 64];
+  __shared__ int wsum[kFinThreads / 64];
+  __shared__ int s_i[32];
+  __shared__ float s_f[4];
+  __shared__ int32_t s_keys[kNQ];
+  __shared__ int32_t s_lines[kNQ];
+  __shared__ int32_t s_hsrc[kNQ];
   SmoCtrl* c = a.ctrl;
   const int tid = threadIdx.x;
   const int done_in = c->done;
@@ -266,6 +281,8 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
     if (tid == 0 && !c->final_applied) {
       c->final_applied = 1;
       c->nq = 0;
+      c->n_compute = 0;
+      c->n_spill = 0;
       c->c_hi = 0.f;
       c->c_lo = 0.f;
       write_status(a, c);
@@ -273,8 +290,8 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
     return;
   }
 
-  // ---- 1. global selection ----
-  uint64_t kh = kKeyNone, kl = kKeyNone;
+  // ---- 1. global selection (+ this thread's partial as a speculation candidate) ----
+  uint64_t kh = kKeyNone, kl = kKeyNone, my_h = kKeyNone, my_l = kKeyNone;
   if (a.partitioned) {
     for (int r = tid; r < a.world; r += kFinThreads) {
       const CandRecord* rec = (const CandRecord*)(a.records + (int64_t)r * a.rec_bytes);
@@ -284,17 +301,22 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
   } else {
     for (int b = tid; b < a.G; b += kFinThreads) {
       const uint64_t h = a.partials[2 * b], l = a.partials[2 * b + 1];
+      if (b == tid) {
+        my_h = h;
+        my_l = l;
+      }
       kh = h < kh ? h : kh;
       kl = l < kl ? l : kl;
     }
   }
-  block_min2_u64<kFinThreads>(kh, kl, kscratch);
-
+  block_min2_u64<kFinThreads>(kh, kl, kscr);
   if (kh == kKeyNone || kl == kKeyNone) {
     if (tid == 0) {
       c->done = kNoPair;
       c->final_applied = 1;
       c->nq = 0;
+      c->n_compute = 0;
+      c->n_spill = 0;
       c->c_hi = c->c_lo = 0.f;
       write_status(a, c);
     }
@@ -322,9 +344,9 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
     const float t = xh[k] - xl[k];
     part += t * t;
   }
-  const float dist2 = block_sum<kFinThreads>(part, fscratch);
+  const float dist2 = block_sum<kFinThreads>(part, fscr);
 
-  // ---- 3. alpha update, stop test, cache requests (one lane) ----
+  // ---- 3. alpha update and stop test (one lane) ----
   if (tid == 0) {
     int done = kRunning;
     float c_hi = 0.f, c_lo = 0.f;
@@ -339,58 +361,195 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
       a.alpha[i_hi] = u.a_hi_new;
       c_hi = u.c_hi;
       c_lo = u.c_lo;
-      const int iter = c->iter + 1;
-      c->iter = iter;
+      c->iter = c->iter + 1;
       if (!gap_open(b_hi, b_lo, a.eps)) done = kConverged;
-      else if (iter >= a.max_iter) done = kMaxIter;
+      else if (c->iter >= a.max_iter) done = kMaxIter;
     }
-    int nq = 0;
-    int line_hi = -1, line_lo = -1;
-    int64_t hits = c->hits, misses = c->misses;
-    if (done != kNonFinite) {
-      if (a.cache_mode == kCacheDense) {
-        if (c_hi != 0.f) { line_hi = i_hi; ++hits; }
-        if (c_lo != 0.f) { line_lo = i_lo; ++hits; }
-      } else {
-        Lru s{c->lru_head, c->lru_tail, c->lines_used};
-        bool hit;
-        if (c_hi != 0.f) {
-          line_hi = lru_get(a, s, i_hi, &hit);
-          if (hit) ++hits;
-          else {
-            ++misses;
-            c->q_idx[nq] = i_hi;
-            c->q_line[nq] = line_hi;
-            c->q_ptr[nq] = xh;
-            c->q_sq[nq] = a.xsq[i_hi];
-            ++nq;
-          }
-        }
-        if (c_lo != 0.f) {
-          if (i_lo == i_hi && line_hi >= 0) {
-            line_lo = line_hi;
-          } else {
-            line_lo = lru_get(a, s, i_lo, &hit);
-            if (hit) ++hits;
-            else {
-              ++misses;
-              c->q_idx[nq] = i_lo;
-              c->q_line[nq] = line_lo;
-              c->q_ptr[nq] = xl;
-              c->q_sq[nq] = a.xsq[i_lo];
-              ++nq;
-            }
-          }
-        }
-        c->lru_head = s.head;
-        c->lru_tail = s.tail;
-        c->lines_used = s.used;
+    s_i[0] = done;
+    s_f[0] = c_hi;
+    s_f[1] = c_lo;
+  }
+  __syncthreads();
+  const int done = s_i[0];
+  const float c_hi = s_f[0], c_lo = s_f[1];
+  if (done == kNonFinite) {
+    if (tid == 0) {
+      c->done = kNonFinite;
+      c->final_applied = 1;
+      c->nq = 0;
+      c->n_compute = 0;
+      c->n_spill = 0;
+      c->c_hi = c->c_lo = 0.f;
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+      write_status(a, c);
+    }
+    return;
+  }
+
+  // ---- 4. rows needed by the pending f update: hits set the CLOCK bit ----
+  if (tid < 2) {
+    int key = -1;
+    if (tid == 0 && c_hi != 0.f) key = i_hi;
+    if (tid == 1 && c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) key = i_lo;
+    int line = -1;
+    if (key >= 0) {
+      line = a.slot_of[key];
+      if (line >= 0) a.ref[line] = 1;
+    }
+    s_i[2 + tid] = key;
+    s_i[4 + tid] = line;
+  }
+  __syncthreads();
+  const int need_hi = s_i[2], need_lo = s_i[3];
+  const int hit_line_hi = s_i[4], hit_line_lo = s_i[5];
+  int m = 0;
+  if (need_hi >= 0 && hit_line_hi < 0) ++m;
+  if (need_lo >= 0 && hit_line_lo < 0) ++m;
+  if (tid == 0) {
+    int k = 0;
+    if (need_hi >= 0 && hit_line_hi < 0) s_keys[k++] = need_hi;
+    if (need_lo >= 0 && hit_line_lo < 0) s_keys[k++] = need_lo;
+  }
+
+  // ---- 5. speculation: the X pass is paid anyway -> add the best uncached
+  //         workgroup winners (parallel cache check, then ordered rounds) ----
+  if (!a.partitioned && a.spec > 0 && m > 0) {
+    const int budget = min(min(a.spec, kNQ - m), max(0, a.L / 2 - m));
+    if (budget > 0) {
+      uint64_t ch = my_h, cl = my_l;
+      if (ch != kKeyNone) {
+        const int idx = (int)key_index(ch);
+        if (idx == i_hi || idx == i_lo || a.slot_of[idx] >= 0) ch = kKeyNone;
       }
-    } else {
-      c_hi = c_lo = 0.f;
+      if (cl != kKeyNone) {
+        const int idx = (int)key_index(cl);
+        if (idx == i_hi || idx == i_lo || a.slot_of[idx] >= 0) cl = kKeyNone;
+      }
+      int cnt = m;  // thread 0's view of the list length
+      if (tid == 0) s_i[6] = m;
+      for (int r = 0; r < (budget + 1) / 2; ++r) {
+        uint64_t bh = ch, bl = cl;
+        block_min2_u64<kFinThreads>(bh, bl, kscr);
+        if (bh == kKeyNone && bl == kKeyNone) break;
+        if (ch == bh) ch = kKeyNone;
+        if (cl == bl) cl = kKeyNone;
+        if (tid == 0) {
+          const uint64_t cand[2] = {bh, bl};
+          for (int s = 0; s < 2; ++s) {
+            if (cand[s] == kKeyNone || cnt >= m + budget) continue;
+            const int idx = (int)key_index(cand[s]);
+            bool dup = false;
+            for (int q = 0; q < cnt; ++q) dup |= s_keys[q] == idx;
+            if (!dup) s_keys[cnt++] = idx;
+          }
+          s_i[6] = cnt;
+        }
+      }
+      __syncthreads();
+      if (s_i[6] > m) m = s_i[6];
+      __syncthreads();
     }
+  }
+  const int M = m;  // lines to allocate (needed misses first, then speculative)
+
+  // ---- 6. CLOCK allocation of M lines in one parallel window scan ----
+  int hand = c->hand;
+  if (M > 0) {
+    const int W = min(kFinThreads, a.L);
+    const int p = (int)(((int64_t)hand + tid) % a.L);
+    const bool in_win = tid < W;
+    const bool pin = p == hit_line_hi || p == hit_line_lo;
+    const int r = in_win ? (int)a.ref[p] : 1;
+    const bool elig = in_win && r == 0 && !pin;
+    int total = 0;
+    const int rank = block_rank(elig, wsum, &total);
+    if (elig && rank < M) s_lines[rank] = p;
+    if (elig && rank == M - 1) s_i[7] = tid;  // cut: position of the M-th victim
+    __syncthreads();
+    const int cut = total >= M ? s_i[7] : W - 1;
+    if (in_win && tid <= cut && r != 0 && !pin) a.ref[p] = 0;  // second chance consumed
+    if (total < M) {
+      // every window line was referenced: take the first unpinned, unchosen ones
+      const bool chosen = elig && rank < M;
+      const bool e2 = in_win && !pin && !chosen;
+      int tot2 = 0;
+      const int r2 = block_rank(e2, wsum, &tot2);
+      if (e2 && total + r2 < M) s_lines[total + r2] = p;
+    }
+    hand = (int)(((int64_t)hand + cut + 1) % a.L);
+    __syncthreads();
+  }
+
+  // ---- 7. install the M keys; host-tier fetch / spill decisions ----
+  // (wave 0, one lane per query; keys are misses, victims are cached rows, so
+  //  no key is both inserted and evicted here)
+  int n_spill = 0, n_fetch = 0;
+  int hhand = c->hhand;
+  if (tid < kNQ) s_hsrc[tid] = (tid < M && a.H > 0) ? a.hslot_of[s_keys[tid]] : -1;
+  __syncthreads();
+  if (tid < 64) {
+    const bool act = tid < M;
+    int l = -1, k = -1, old = -1, hsrc = -1;
+    if (act) {
+      l = s_lines[tid];
+      k = s_keys[tid];
+      old = a.key_of[l];
+      hsrc = s_hsrc[tid];
+    }
+    const bool want_spill = act && a.H > 0 && old >= 0 && a.hslot_of[old] < 0;
+    const uint64_t sm = __ballot(want_spill);
+    const int srank = __popcll(sm & ((1ull << tid) - 1ull));
+    n_spill = __popcll(sm);
+    n_fetch = __popcll(__ballot(hsrc >= 0));
+    int hspill = -1;
+    if (want_spill) {
+      const int hl = (int)(((int64_t)hhand + srank) % a.H);
+      bool clash = false;  // never overwrite a host line this iteration fetches from
+      for (int q = 0; q < M; ++q) clash |= s_hsrc[q] == hl;
+      if (!clash) {
+        const int prev = a.hkey_of[hl];
+        if (prev >= 0) a.hslot_of[prev] = -1;
+        a.hkey_of[hl] = old;
+        a.hslot_of[old] = hl;
+        hspill = hl;
+      }
+    }
+    if (act) {
+      if (old >= 0) a.slot_of[old] = -1;
+      a.key_of[l] = k;
+      a.slot_of[k] = l;
+      a.ref[l] = 1;
+      c->q_idx[tid] = k;
+      c->q_line[tid] = l;
+      c->q_op[tid] = hsrc >= 0 ? kOpFetch : kOpCompute;
+      c->q_hsrc[tid] = hsrc;
+      c->q_hspill[tid] = hspill;
+      c->q_sq[tid] = a.xsq[k];
+      c->q_ptr[tid] = (a.partitioned ? (k == i_hi ? xh : xl) : a.x + ((int64_t)k - a.x_row0) * a.dp);
+    }
+    if (a.H > 0) hhand = (int)(((int64_t)hhand + n_spill) % a.H);
+    if (tid == 0) {
+      s_i[8] = n_spill;
+      s_i[9] = n_fetch;
+    }
+  }
+  __syncthreads();
+
+  // ---- 8. publish the control record ----
+  if (tid == 0) {
+    n_spill = s_i[8];
+    n_fetch = s_i[9];
+    int line_hi = -1, line_lo = -1, q = 0;
+    if (need_hi >= 0) line_hi = hit_line_hi >= 0 ? hit_line_hi : s_lines[q++];
+    if (c_lo != 0.f) {
+      if (i_lo == i_hi && c_hi != 0.f) line_lo = line_hi;
+      else line_lo = hit_line_lo >= 0 ? hit_line_lo : s_lines[q++];
+    }
+    const int n_need = (need_hi >= 0) + (need_lo >= 0);
+    const int n_miss = (need_hi >= 0 && hit_line_hi < 0) + (need_lo >= 0 && hit_line_lo < 0);
     c->done = done;
-    c->final_applied = (done == kNonFinite) ? 1 : 0;
+    c->final_applied = 0;
     c->i_hi = i_hi;
     c->i_lo = i_lo;
     c->c_hi = c_hi;
@@ -399,159 +558,23 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
     c->line_lo = line_lo;
     c->b_hi = b_hi;
     c->b_lo = b_lo;
-    c->hits = hits;
-    c->misses = misses;
-    if (nq > 0) {
-      c->rows_computed += nq;
-      c->x_passes += 1;
-    }
-    c->nq = nq;
-    s_nq = nq;
-    for (int q = 0; q < nq; ++q) s_qidx[q] = c->q_idx[q];
-  }
-  __syncthreads();
-
-  // ---- 4. speculative rows (LRU, replicated X): the X pass is paid anyway,
-  //      so fill the idle MFMA columns with the best uncached block winners ----
-  int nq = s_nq;
-  if (a.cache_mode == kCacheLRU && !a.partitioned && a.spec > 0 && nq > 0) {
-    const int budget = min(min(a.spec, kNQ - nq), a.L / 2 - nq);
-    // each thread holds the partial keys of its blocks (both sides, as copies)
-    int rounds = 0;
-    uint64_t mine_h = kKeyNone, mine_l = kKeyNone;  // min over this thread's untaken keys
-    // thread owns blocks tid, tid+1024, ...; G is typically <= 1024 per rank
-    auto recompute = [&](uint64_t taken_h, uint64_t taken_l) {
-      uint64_t h = kKeyNone, l = kKeyNone;
-      for (int b = tid; b < a.G; b += kFinThreads) {
-        const uint64_t ph = a.partials[2 * b], pl = a.partials[2 * b + 1];
-        if (ph > taken_h && ph < h) h = ph;
-        if (pl > taken_l && pl < l) l = pl;
-      }
-      mine_h = h;
-      mine_l = l;
-    };
-    // keys are distinct; "taken" = every key <= the last selected one on that side
-    uint64_t last_h = kh, last_l = kl;  // the current pair is already handled
-    int added = 0;
-    while (added < budget && rounds < 2 * kNQ) {
-      ++rounds;
-      recompute(last_h, last_l);
-      uint64_t bh = mine_h, bl = mine_l;
-      block_min2_u64<kFinThreads>(bh, bl, kscratch);
-      if (bh == kKeyNone && bl == kKeyNone) break;
-      if (tid == 0) {
-        Lru s{c->lru_head, c->lru_tail, c->lines_used};
-        const uint64_t cand[2] = {bh, bl};
-        for (int side = 0; side < 2 && added < budget; ++side) {
-          if (cand[side] == kKeyNone) continue;
-          const int idx = (int)key_index(cand[side]);
-          if (a.slot_of[idx] >= 0) continue;  // cached already
-          bool dup = false;
-          for (int q = 0; q < s_nq; ++q) dup |= (s_qidx[q] == idx);
-          if (dup) continue;
-          bool hit;
-          const int line = lru_get(a, s, idx, &hit);
-          c->q_idx[s_nq] = idx;
-          c->q_line[s_nq] = line;
-          c->q_ptr[s_nq] = a.x + ((int64_t)idx - a.x_row0) * a.dp;
-          c->q_sq[s_nq] = a.xsq[idx];
-          s_qidx[s_nq] = idx;
-          ++s_nq;
-          ++added;
-        }
-        c->lru_head = s.head;
-        c->lru_tail = s.tail;
-        c->lines_used = s.used;
-      }
-      last_h = bh;
-      last_l = bl;
-      __syncthreads();
-    }
-    if (tid == 0 && added > 0) {
-      c->nq = s_nq;
-      c->rows_computed += added;
-      c->spec_rows += added;
-    }
-  }
-  if (tid == 0) write_status(a, c);
-}
-
-// ---------------------------------------------------------------------------
-// SV compaction (K11 replacement: thrust::remove_if over a 4-zip)
-// ---------------------------------------------------------------------------
-constexpr int kCompactBlock = 1024;
-
-__global__ __launch_bounds__(kCompactBlock) void compact_count_kernel(const float* alpha, int64_t n,
-                                                                      int32_t* counts) {
-  __shared__ int32_t wc[kCompactBlock / 64];
-  const int64_t i = (int64_t)blockIdx.x * kCompactBlock + threadIdx.x;
-  const bool p = i < n && alpha[i] > 0.f;
-  const uint64_t m = __ballot(p);
-  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t s = 0;
-    for (int w = 0; w < kCompactBlock / 64; ++w) s += wc[w];
-    counts[blockIdx.x] = s;
+    c->nq = M;
+    c->n_compute = M - n_fetch;
+    c->n_spill = n_spill;
+    c->hand = hand;
+    c->hhand = hhand;
+    c->hits += n_need - n_miss;
+    c->misses += n_miss;
+    c->rows_computed += M - n_fetch;
+    c->x_passes += (M - n_fetch) > 0 ? 1 : 0;
+    c->spec_rows += M - n_miss;
+    c->host_hits += n_fetch;
+    c->spills += n_spill;
+    write_status(a, c);
   }
 }
 
-__global__ __launch_bounds__(1024) void compact_scan_kernel(int32_t* counts, int nb, int32_t* total) {
-  // single workgroup exclusive scan (sequential chunks per thread + LDS scan)
-  __shared__ int32_t part[1024];
-  const int per = (nb + 1023) / 1024;
-  const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
-  int32_t s = 0;
-  for (int b = b0; b < b1; ++b) s += counts[b];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t run = 0;
-    for (int t = 0; t < 1024; ++t) {
-      int32_t v = part[t];
-      part[t] = run;
-      run += v;
-    }
-    *total = run;
-  }
-  __syncthreads();
-  int32_t run = part[threadIdx.x];
-  for (int b = b0; b < b1; ++b) {
-    int32_t v = counts[b];
-    counts[b] = run;
-    run += v;
-  }
-}
-
-__global__ __launch_bounds__(kCompactBlock) void compact_scatter_kernel(const float* alpha, int64_t n,
-                                                                        const int32_t* offsets,
-                                                                        int32_t* idx_out) {
-  __shared__ int32_t wc[kCompactBlock / 64];
-  const int64_t i = (int64_t)blockIdx.x * kCompactBlock + threadIdx.x;
-  const bool p = i < n && alpha[i] > 0.f;
-  const uint64_t m = __ballot(p);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wc[wave] = __popcll(m);
-  __syncthreads();
-  int32_t base = offsets[blockIdx.x];
-  for (int w = 0; w < wave; ++w) base += wc[w];
-  const int32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-  if (p) idx_out[base + rank] = (int32_t)i;
-}
-
-__global__ void gather_sv_kernel(const float* x, int64_t x_row0, const float* xsq, const float* alpha,
-                                 const float* y, const int32_t* idx, int64_t nsv, int dp, float* sv,
-                                 float* svsq, float* coef) {
-  const int64_t r = blockIdx.x;
-  if (r >= nsv) return;
-  const int64_t g = idx[r];
-  const float* src = x + (g - x_row0) * dp;
-  for (int k = threadIdx.x; k < dp; k += blockDim.x) sv[r * dp + k] = src[k];
-  if (threadIdx.x == 0) {
-    svsq[r] = xsq[g];
-    coef[r] = alpha[g] * y[g];
-  }
-}
+// Dense mode in the 3-kernel pipeline is not used (smo_fused covers it).
 
 }  // namespace dev
 
@@ -602,28 +625,6 @@ void smo_local_record(const SmoArgs& a, hipStream_t s) {
 void smo_finalize(const SmoArgs& a, hipStream_t s) {
   dev::smo_finalize_kernel<<<dim3(1), kFinThreads, 0, s>>>(a);
   post_launch("smo_finalize", s);
-}
-
-int64_t compact_scratch_ints(int64_t n) { return (n + dev::kCompactBlock - 1) / dev::kCompactBlock + 1; }
-
-void compact_positive(const float* alpha, int64_t n, int32_t* idx_out, int32_t* count_dev,
-                      int32_t* scratch, hipStream_t s) {
-  const int nb = (int)((n + dev::kCompactBlock - 1) / dev::kCompactBlock);
-  dev::compact_count_kernel<<<dim3(nb), dev::kCompactBlock, 0, s>>>(alpha, n, scratch);
-  post_launch("compact_count", s);
-  dev::compact_scan_kernel<<<dim3(1), 1024, 0, s>>>(scratch, nb, count_dev);
-  post_launch("compact_scan", s);
-  dev::compact_scatter_kernel<<<dim3(nb), dev::kCompactBlock, 0, s>>>(alpha, n, scratch, idx_out);
-  post_launch("compact_scatter", s);
-}
-
-void gather_sv(const float* x, int64_t x_row0, const float* xsq, const float* alpha,
-               const float* y, const int32_t* idx, int64_t nsv, int dp, float* sv, float* svsq,
-               float* coef, hipStream_t s) {
-  if (nsv <= 0) return;
-  dev::gather_sv_kernel<<<dim3((unsigned)nsv), 256, 0, s>>>(x, x_row0, xsq, alpha, y, idx, nsv, dp,
-                                                           sv, svsq, coef);
-  post_launch("gather_sv", s);
 }
 
 }  // namespace launch

@@ -112,6 +112,8 @@ py::dict result_dict(const SolveResult& r) {
   d["rows_computed"] = r.rows_computed;
   d["x_passes"] = r.x_passes;
   d["spec_rows"] = r.spec_rows;
+  d["host_hits"] = r.host_hits;
+  d["host_cache_lines"] = r.host_cache_lines;
   d["cache_lines"] = r.cache_lines;
   d["world"] = r.world;
   return d;

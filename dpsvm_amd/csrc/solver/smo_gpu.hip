@@ -66,7 +66,11 @@ struct GpuSolver::Impl {
   // device buffers
   float *x = nullptr, *xsq = nullptr, *y = nullptr, *alpha = nullptr, *f = nullptr;
   float* lines = nullptr;
-  int32_t *slot_of = nullptr, *key_of = nullptr, *lru_prev = nullptr, *lru_next = nullptr;
+  int32_t *slot_of = nullptr, *key_of = nullptr;
+  uint8_t* ref = nullptr;  // CLOCK reference bits
+  float *hlines_h = nullptr, *hlines_d = nullptr;  // pinned host tier (host / device view)
+  int32_t *hslot_of = nullptr, *hkey_of = nullptr;
+  int64_t H = 0;
   uint64_t* partials = nullptr;
   SmoCtrl* ctrl = nullptr;
   SmoStatus* status_h = nullptr;  // host view
@@ -97,10 +101,11 @@ struct GpuSolver::Impl {
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
     for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines,
-                      (void*)slot_of, (void*)key_of, (void*)lru_prev, (void*)lru_next,
+                      (void*)slot_of, (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of,
                       (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)stamps})
       if (ptr) (void)hipFree(ptr);
     if (status_h) (void)hipHostFree(status_h);
+    if (hlines_h) (void)hipHostFree(hlines_h);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -122,8 +127,8 @@ struct GpuSolver::Impl {
     c.line_hi = c.line_lo = -1;
     c.b_hi = b_hi;
     c.b_lo = b_lo;
-    c.lru_head = c.lru_tail = -1;
-    c.lines_used = 0;
+    c.hand = 0;
+    c.hhand = 0;
     HIP_CHECK(hipMemcpyAsync(ctrl, &c, sizeof(c), hipMemcpyHostToDevice, stream));
     memset(status_h, 0, sizeof(SmoStatus));
   }
@@ -419,8 +424,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   if (!m.dense) {
     m.slot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
     m.key_of = dmalloc<int32_t>((size_t)m.L, &m.bytes);
-    m.lru_prev = dmalloc<int32_t>((size_t)m.L, &m.bytes);
-    m.lru_next = dmalloc<int32_t>((size_t)m.L, &m.bytes);
+    m.ref = dmalloc<uint8_t>((size_t)m.L, &m.bytes);
+    if (m.p.host_cache_lines > 0) {
+      // pinned host tier: a FIFO victim cache the row kernel spills to and
+      // fetches from with zero-copy PCIe accesses (no host round trip)
+      m.H = m.p.host_cache_lines;
+      HIP_CHECK(hipHostMalloc((void**)&m.hlines_h, (size_t)m.H * m.ldl * 4, hipHostMallocMapped));
+      HIP_CHECK(hipHostGetDevicePointer((void**)&m.hlines_d, m.hlines_h, 0));
+      m.hslot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
+      m.hkey_of = dmalloc<int32_t>((size_t)m.H, &m.bytes);
+    }
   }
 
   SmoArgs& a = m.args;
@@ -433,8 +446,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.ldl = m.ldl;
   a.slot_of = m.slot_of;
   a.key_of = m.key_of;
-  a.lru_prev = m.lru_prev;
-  a.lru_next = m.lru_next;
+  a.ref = m.ref;
+  a.hlines = m.hlines_d;
+  a.hslot_of = m.hslot_of;
+  a.hkey_of = m.hkey_of;
+  a.H = (int32_t)m.H;
   a.partials = m.partials;
   a.ctrl = m.ctrl;
   a.status = m.status_d;
@@ -546,8 +562,11 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   if (!m.dense) {
     launch::fill_i32(m.slot_of, m.n, -1, m.stream);
     launch::fill_i32(m.key_of, m.L, -1, m.stream);
-    launch::fill_i32(m.lru_prev, m.L, -1, m.stream);
-    launch::fill_i32(m.lru_next, m.L, -1, m.stream);
+    HIP_CHECK(hipMemsetAsync(m.ref, 0, m.L, m.stream));
+    if (m.H > 0) {
+      launch::fill_i32(m.hslot_of, m.n, -1, m.stream);
+      launch::fill_i32(m.hkey_of, m.H, -1, m.stream);
+    }
   }
   m.init_ctrl(iter0, b_hi0, b_lo0);
   HIP_CHECK(hipStreamSynchronize(m.stream));
@@ -638,6 +657,8 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   res.rows_computed += st.rows_computed;
   res.x_passes += st.x_passes;
   res.spec_rows = st.spec_rows;
+  res.host_hits = st.host_hits;
+  res.host_cache_lines = m.H;
   if (m.stamps) {
     std::vector<uint64_t> h((size_t)kStampRing * 2 * kStampSlots);
     HIP_CHECK(hipMemcpy(h.data(), m.stamps, h.size() * 8, hipMemcpyDeviceToHost));

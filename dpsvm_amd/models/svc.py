@@ -62,6 +62,7 @@ class SVCConfig:
     cache_lines: int = 0            # -s (0 = auto: fill HBM; dense Gram when it fits)
     cache_mb: float = 0.0
     cache_frac: float = 0.80
+    host_cache_lines: int = 0       # pinned host tier lines (LRU mode; 0 = off)
     spec_rows: int = 14             # speculative rows per X pass (LRU mode)
     graph_block: int = 64           # SMO iterations per hipGraph
     use_graph: bool = True
@@ -94,6 +95,7 @@ class SVCConfig:
         p.cache_lines = int(self.cache_lines)
         p.cache_mb = float(self.cache_mb)
         p.cache_frac = float(self.cache_frac)
+        p.host_cache_lines = int(self.host_cache_lines)
         p.spec_rows = int(self.spec_rows)
         p.graph_block = int(self.graph_block)
         p.use_graph = bool(self.use_graph)

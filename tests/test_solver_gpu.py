@@ -141,3 +141,19 @@ def test_rccl_one_rank_collective_path(C, extra):
     assert got.n_iter_ == ref.n_iter_
     assert np.array_equal(got.alpha_, ref.alpha_)
     assert abs(got.train_accuracy() - ref.train_accuracy()) < 1e-9
+
+
+def test_cache_policies_bitwise_identical():
+    """K(i, j) from the row kernel is bitwise independent of when/where it is
+    computed, so every cache configuration (tiny device cache, speculation,
+    host spill tier) must reproduce the same SMO trajectory exactly."""
+    X, y = synthetic("covtype", n=5000, seed=6)
+    kw = dict(C=4.0, gamma=0.5, device="cuda")
+    ref = SVC(cache_lines=4096, **kw).fit(X, y)
+    tiny = SVC(cache_lines=2, spec_rows=0, **kw).fit(X, y)
+    spill = SVC(cache_lines=24, host_cache_lines=512, **kw).fit(X, y)
+    for other in (tiny, spill):
+        assert other.n_iter_ == ref.n_iter_
+        assert np.array_equal(other.alpha_, ref.alpha_)
+    assert spill.stats_["host_hits"] > 0
+    assert tiny.stats_["cache_misses"] > ref.stats_["cache_misses"]
