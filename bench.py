@@ -28,19 +28,36 @@ BASELINE_1GPU_S = 137.0   # README.md:23 (1x GTX 780)
 BASELINE_MULTI_S = 46.0   # README.md:23 (10 GPUs, OpenMPI over Ethernet)
 METRIC = "wall-clock training time (s) to tol=1e-3, MNIST even-odd RBF, at 1/2/4/8 MI355X"
 
+# BASELINE.json configs (parameters from README.md:23 and Makefile:74-86)
+PRESETS = {
+    "mnist": dict(data="mnist", samples=60000, features=784, C=10.0, gamma=0.25, eps=1e-3, max_iter=150000),
+    "mnist-makefile": dict(data="mnist", samples=60000, features=784, C=10.0, gamma=0.125, eps=0.01,
+                           max_iter=100000),
+    "mnist-parity": dict(data="mnist-parity", samples=60000, features=784, C=10.0, gamma=0.25, eps=1e-3,
+                         max_iter=150000),
+    "adult": dict(data="adult", samples=32561, features=123, C=100.0, gamma=0.5, eps=1e-3, max_iter=150000),
+    "covtype": dict(data="covtype", samples=581012, features=54, C=2048.0, gamma=0.03125, eps=1e-3,
+                    max_iter=3000000),
+    "synthetic-2m": dict(data="uniform", samples=2000000, features=1024, C=1.0, gamma=1.0 / 1024, eps=1e-3,
+                         max_iter=3000000),
+}
+
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--data", default="mnist", help="synthetic generator (mnist = BASELINE headline shape)")
-    ap.add_argument("--samples", type=int, default=60000)
-    ap.add_argument("--features", type=int, default=784)
-    ap.add_argument("--C", type=float, default=10.0)
-    ap.add_argument("--gamma", type=float, default=0.25)
-    ap.add_argument("--eps", type=float, default=1e-3)
-    ap.add_argument("--max-iter", type=int, default=150000)
+    ap.add_argument("--config", default="mnist", choices=sorted(PRESETS),
+                    help="preset (BASELINE.json configs; explicit flags override)")
+    ap.add_argument("--data", default=None, help="synthetic generator (mnist = BASELINE headline shape)")
+    ap.add_argument("--samples", type=int, default=None)
+    ap.add_argument("--features", type=int, default=None)
+    ap.add_argument("--C", type=float, default=None)
+    ap.add_argument("--gamma", type=float, default=None)
+    ap.add_argument("--eps", type=float, default=None)
+    ap.add_argument("--max-iter", type=int, default=None)
+    ap.add_argument("--host-cache-lines", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cache-lines", type=int, default=0)
     ap.add_argument("--x-mode", default="auto")
@@ -49,7 +66,11 @@ def parse(argv=None):
     ap.add_argument("--device", default="auto", help="auto | cuda | cpu")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def main(argv=None) -> int:
@@ -73,7 +94,7 @@ def main(argv=None) -> int:
 
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
     cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines,
-                    x_mode=a.x_mode, graph_block=a.graph_block)
+                    x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines)
     params = cfg.to_native(X.shape[1])
     comm = make_comm(ctx, a.comm)
     if a.comm == "rccl" and n_ranks == 1:
@@ -134,7 +155,8 @@ def main(argv=None) -> int:
             "speedup_vs_baseline": round(base / per_run, 2),
             "baseline_s": base,
             "dtype": "fp32",
-            "data": f"synthetic {a.data}-shape {a.samples}x{a.features} (seed {a.seed}; pixel-like [0,1] features, random +/-1 labels)",
+            "data": f"synthetic {a.data}-shape {a.samples}x{a.features} (seed {a.seed}; "
+                    + ("pixel-like [0,1] features, random +/-1 labels)" if a.data == "mnist" else "generated)"),
             "config": {
                 "model": f"RBF C-SVM, modified SMO (C={a.C:g}, gamma={a.gamma:g}, tol={a.eps:g})",
                 "global_batch": a.samples,
@@ -153,6 +175,7 @@ def main(argv=None) -> int:
             "x_replicated": bool(info.get("x_replicated", True)),
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
+            "preset": a.config,
         }
         line = json.dumps(out)
         print(line, flush=True)

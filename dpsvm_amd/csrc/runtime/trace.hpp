@@ -1,0 +1,80 @@
+// Tracing, fault injection and cross-rank verification hooks.
+//
+//   DPSVM_ROCTX=1        ROCTx ranges around setup / Gram / SMO loop / accuracy
+//                        (visible in rocprofv3 --marker-trace); libroctx64 is
+//                        dlopen'ed so no link dependency exists when unused.
+//   DPSVM_FAULT=nan@K    poison f at the first block boundary at/after SMO
+//                        iteration K (exercises the non-finite abort path).
+//   DPSVM_VERIFY=1       after solve, all-reduce MIN and MAX of an alpha hash;
+//                        ranks that diverged raise an error.
+#pragma once
+
+#include <dlfcn.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+namespace dpsvm {
+namespace trace {
+
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    const char* e = std::getenv("DPSVM_ROCTX");
+    if (!e || e[0] != '1') return;
+    void* h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW);
+    if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW);
+    if (!h) return;
+    push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+    pop = (int (*)())dlsym(h, "roctxRangePop");
+    if (!push || !pop) push = nullptr, pop = nullptr;
+  }
+  static Roctx& get() {
+    static Roctx r;
+    return r;
+  }
+};
+
+class Range {
+ public:
+  explicit Range(const char* name) : on_(Roctx::get().push != nullptr) {
+    if (on_) Roctx::get().push(name);
+  }
+  ~Range() {
+    if (on_) Roctx::get().pop();
+  }
+
+ private:
+  bool on_;
+};
+
+// DPSVM_FAULT=nan@K -> K, else -1
+inline int64_t fault_nan_iter() {
+  const char* e = std::getenv("DPSVM_FAULT");
+  if (!e || strncmp(e, "nan@", 4) != 0) return -1;
+  return atoll(e + 4);
+}
+
+inline bool verify_enabled() {
+  const char* e = std::getenv("DPSVM_VERIFY");
+  return e && e[0] == '1';
+}
+
+// order-sensitive 64-bit hash of float bit patterns (FNV-1a over words)
+inline uint64_t hash_floats(const float* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t u;
+    memcpy(&u, p + i, 4);
+    h ^= u;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+}  // namespace trace
+}  // namespace dpsvm

@@ -22,6 +22,7 @@
 #include "dpsvm/common.hpp"
 #include "dpsvm/solver.hpp"
 #include "../runtime/thread_pool.hpp"
+#include "../runtime/trace.hpp"
 
 namespace dpsvm {
 namespace {
@@ -165,6 +166,8 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
 
   const int T = pool.size();
   std::vector<uint64_t> th_hi(T), th_lo(T);
+  const int64_t fault_iter = trace::fault_nan_iter();
+  trace::Range loop_range("dpsvm/smo_loop_cpu");
   auto t0 = Clock::now();
   int64_t iter = iter0;
   int status = 0;
@@ -237,6 +240,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
       });
     }
     ++iter;
+    if (fault_iter >= 0 && iter == fault_iter && nl > 0) f[0] = std::nanf("");  // DPSVM_FAULT
     const bool open = gap_open(b_hi, b_lo, p.eps);
     if (progress && p.log_every > 0 && iter % p.log_every == 0)
       progress(Progress{iter, b_hi, b_lo, secs_since(t0), res.cache_hits, res.cache_misses});
@@ -261,6 +265,13 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
     if (iter >= p.max_iter) { status = 2; break; }
   }
   res.t_solve = secs_since(t0);
+  if (world > 1 && trace::verify_enabled()) {
+    // cross-rank consistency: every rank must hold bit-identical alphas
+    const uint64_t h = trace::hash_floats(alpha.data(), alpha.size());
+    uint64_t hk[2] = {h, ~h};
+    comm->allreduce_min_u64(hk, 2, nullptr);
+    if (hk[0] != h || ~hk[1] != h) fail("DPSVM_VERIFY: ranks hold different alphas (diverged)");
+  }
   res.iters = iter;
   res.status = status;
   res.b_hi = b_hi;

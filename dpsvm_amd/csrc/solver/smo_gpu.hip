@@ -27,6 +27,7 @@
 #include "dpsvm/solver.hpp"
 #include "../kernels/kernels.hpp"
 #include "../runtime/hip_check.hpp"
+#include "../runtime/trace.hpp"
 
 namespace dpsvm {
 namespace {
@@ -574,8 +575,12 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   res.t_setup = secs_since(ts0);
 
   // ================= timed region: the SMO loop (svmTrainMain.cpp:206-314) =================
+  trace::Range loop_range("dpsvm/solve");
+  const int64_t fault_iter = trace::fault_nan_iter();
+  bool fault_done = false;
   auto t0 = Clock::now();
   if (m.dense) {
+    trace::Range gram_range("dpsvm/gram_gemm");
     // whole Gram shard K[i][j], i over all n rows, j over local rows: one MFMA GEMM
     launch::rbf_gemm_store(m.x, m.xsq, m.n, m.dp, m.x + (size_t)m.off * m.dp, m.xsq + m.off, m.nl, m.dp,
                            m.dp, m.gamma, m.lines, m.ldl, m.stream);
@@ -623,6 +628,12 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
         progress(Progress{st.iter, st.b_hi, st.b_lo, secs_since(t0), st.hits, st.misses});
       }
       if (st.done != kRunning) break;
+      if (fault_iter >= 0 && !fault_done && st.iter >= fault_iter) {
+        // DPSVM_FAULT=nan@K: poison f[0]; lands between two enqueued blocks
+        static const float qnan = std::nanf("");
+        HIP_CHECK(hipMemcpyAsync(m.f, &qnan, 4, hipMemcpyHostToDevice, m.stream));
+        fault_done = true;
+      }
       if (m.p.checkpoint_every > 0 && !m.p.checkpoint_path.empty() &&
           st.iter - last_ck >= m.p.checkpoint_every) {
         // drain the in-flight block, then snapshot (alpha replicated, f gathered)
@@ -646,6 +657,25 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   }
   // ================= end of timed region =================
 
+  if (m.collectives() && trace::verify_enabled()) {
+    // cross-rank consistency: every rank must hold bit-identical alphas
+    std::vector<float> ah((size_t)m.n);
+    HIP_CHECK(hipMemcpy(ah.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
+    const uint64_t h = trace::hash_floats(ah.data(), ah.size());
+    uint64_t hk[2] = {h, ~h};
+    if (m.comm->device_memory()) {
+      size_t tb = 0;
+      uint64_t* dk = dmalloc<uint64_t>(2, &tb);
+      HIP_CHECK(hipMemcpy(dk, hk, 16, hipMemcpyHostToDevice));
+      m.comm->allreduce_min_u64(dk, 2, m.stream);
+      HIP_CHECK(hipMemcpyAsync(hk, dk, 16, hipMemcpyDeviceToHost, m.stream));
+      HIP_CHECK(hipStreamSynchronize(m.stream));
+      (void)hipFree(dk);
+    } else {
+      m.comm->allreduce_min_u64(hk, 2, nullptr);
+    }
+    if (hk[0] != h || ~hk[1] != h) fail("DPSVM_VERIFY: ranks hold different alphas (diverged)");
+  }
   st = m.read_status();
   res.iters = st.iter;
   res.status = st.done;
@@ -951,6 +981,7 @@ void rbf_rows(const float* x, const float* xsq, int64_t n, int ld, const float* 
   SmoCtrl c;
   memset(&c, 0, sizeof(c));
   c.nq = nq;
+  c.n_compute = nq;  // all queries are kOpCompute (0) after the memset
   for (int q = 0; q < nq; ++q) {
     c.q_idx[q] = q;
     c.q_line[q] = q;

@@ -91,3 +91,32 @@ def test_cache_lines_small_same_result():
     assert tiny.n_iter_ == full.n_iter_
     assert np.array_equal(tiny.alpha_, full.alpha_)
     assert tiny.stats_["cache_misses"] > full.stats_["cache_misses"]
+
+
+def test_fault_injection_nonfinite_abort(monkeypatch):
+    """DPSVM_FAULT=nan@K poisons f; the solver must stop with status 4."""
+    X, y = synthetic("blobs", n=400, d=4, seed=3, sep=1.0)
+    monkeypatch.setenv("DPSVM_FAULT", "nan@25")
+    clf = SVC(C=1.0, gamma=0.5, device="cpu").fit(X, y)
+    assert clf.status_ == 4 and not clf.converged_ and clf.n_iter_ == 25
+
+
+def test_verify_ranks_consistent(monkeypatch, C):
+    import threading
+
+    monkeypatch.setenv("DPSVM_VERIFY", "1")
+    X, y = synthetic("blobs", n=300, d=4, seed=3, sep=1.0)
+    g = C.ThreadCommGroup(2)
+    comms = [g.comm(r) for r in range(2)]
+    out, errs = [None, None], []
+
+    def work(r):
+        try:
+            out[r] = SVC(C=1.0, gamma=0.5, device="cpu").fit(X, y, comm=comms[r])
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs and out[0].converged_

@@ -157,3 +157,15 @@ def test_cache_policies_bitwise_identical():
         assert np.array_equal(other.alpha_, ref.alpha_)
     assert spill.stats_["host_hits"] > 0
     assert tiny.stats_["cache_misses"] > ref.stats_["cache_misses"]
+
+
+def test_gpu_fault_injection_and_verify(monkeypatch, C):
+    X, y = synthetic("blobs", n=3000, d=8, seed=3, sep=1.0)
+    monkeypatch.setenv("DPSVM_FAULT", "nan@200")
+    clf = SVC(C=1.0, gamma=0.1, device="cuda", graph_block=16).fit(X, y)
+    assert clf.status_ == 4 and not clf.converged_ and clf.n_iter_ >= 200
+    monkeypatch.delenv("DPSVM_FAULT")
+    monkeypatch.setenv("DPSVM_VERIFY", "1")
+    comm = C.rccl_comm(C.rccl_unique_id(), 0, 1, 0)
+    ok = SVC(C=1.0, gamma=0.1, device="cuda", force_collectives=True).fit(X, y, comm=comm)
+    assert ok.converged_
