@@ -54,6 +54,9 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistContext
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("DPSVM_FORCE_DEVICE"):
+        # testing aid: several ranks share one GPU (e.g. a 1-GPU box rehearsing N > 1)
+        local_rank = int(os.environ["DPSVM_FORCE_DEVICE"])
     use_gpu = (device == "cuda") or (device == "auto" and gpu_available())
     ctx = DistContext(rank=rank, world=world, local_rank=local_rank,
                       device=f"cuda:{local_rank}" if use_gpu else "cpu")
