@@ -173,6 +173,7 @@ def main(argv=None) -> int:
             "iters_per_s": round(res["iters"] / max(solve_max, 1e-9), 1),
             "device": info.get("device_name", ""),
             "x_replicated": bool(info.get("x_replicated", True)),
+            "iteration": info.get("iteration", "cpu"),
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
             "preset": a.config,

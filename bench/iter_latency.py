@@ -4,8 +4,8 @@
 Prints (JSON lines):
   * launch floor: us per kernel of a hipGraph chain of dependent empty kernels
     (the MI355X 'boundary' cost) for several grid sizes;
-  * SMO loop: us per iteration for the dense fused kernel and the LRU
-    (rows + step + finalize) pipeline, on the MNIST-shape headline problem,
+  * SMO loop: us per iteration for the dense fused kernel, the fused cache-mode
+    kernel and the cache-mode rows + step + finalize chain, on the MNIST-shape headline problem,
     for several graph block sizes.
 """
 import argparse
@@ -34,11 +34,13 @@ def main():
         us = C.launch_floor_us(blocks, 256, 64, 50)
         lines.append({"what": "launch_floor", "blocks": blocks, "us_per_kernel": round(us, 3)})
     X, y = synthetic("mnist", n=a.samples, d=a.features, seed=0)
-    for mode, extra in (("dense", {}), ("lru", {"cache_lines": 20000})):
-        for gb in (16, 64, 256):
+    for mode, extra in (("dense", {}), ("lru", {"cache_lines": 20000}), ("lru-chain", {"cache_lines": 20000})):
+        if mode == "lru-chain":
+            os.environ["DPSVM_LRU_KERNELS"] = "3"  # rows/step/finalize chain (A/B)
+        for gb in ((64,) if mode == "lru-chain" else (16, 64, 256)):
             cfg = SVCConfig(C=10.0, gamma=0.25, eps=1e-3, graph_block=gb, **extra)
             s = C.GpuSolver(cfg.to_native(X.shape[1]), None, 0)
-            s.setup(X, X.shape[0], y)
+            si = s.setup(X, X.shape[0], y)
             s.solve()  # warm (graph build, caches)
             t0 = time.perf_counter()
             alpha, info = s.solve()
@@ -47,7 +49,8 @@ def main():
                           "t_solve_s": round(info["t_solve"], 4), "wall_s": round(wall, 4),
                           "us_per_iter": round(1e6 * info["t_solve"] / max(1, info["iters"]), 3),
                           "x_passes": info["x_passes"], "rows_computed": info["rows_computed"],
-                          "misses": info["cache_misses"]})
+                          "misses": info["cache_misses"], "spec_rows": info.get("spec_rows"),
+                          "iteration": si["iteration"]})
             del s
     out = "\n".join(json.dumps(l) for l in lines)
     print(out)

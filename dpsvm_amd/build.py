@@ -45,6 +45,7 @@ LIB_SOURCES = [
     "kernels/smo_fused.hip",
     "kernels/microbench.hip",
     "kernels/compact.hip",
+    "kernels/smo_fused_lru.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

@@ -16,7 +16,7 @@ constexpr int kNQ = 16;             // kernel rows per X pass (MFMA 16x16x4 N wi
 constexpr int kStepRows = 128;      // rows per step/rows workgroup
 constexpr int kStepThreads = 256;   // 4 waves
 constexpr int kFinThreads = 1024;   // finalize: one workgroup, 16 waves
-constexpr int kRowsKC = 1024;       // k-chunk of query vectors staged in LDS
+constexpr int kRowsKC = 1008;       // k-chunk of query vectors staged in LDS (16 x 1012 floats < 64 KiB)
 
 enum CacheMode : int32_t {
   kCacheDense = 0,  // whole Gram shard resident: line i == global row i
@@ -88,6 +88,27 @@ struct alignas(16) FusedRec {
   int32_t iter, done;   // SMO iterations completed; DoneCode
   float b_hi, b_lo;
 };
+// Cache-mode fused iteration (smo_fused_lru): as FusedRec plus the cache
+// decisions of the producing kernel, committed lazily by workgroup 0 of the
+// next launch while every reader applies them as corrections.
+struct alignas(16) FusedCacheRec {
+  int32_t i_hi, i_lo;
+  float a_hi, a_lo;
+  int32_t iter, done;
+  float b_hi, b_lo;
+  int32_t n_new;          // lines (re)assigned by the producing kernel
+  int32_t hand0, span;    // CLOCK window scanned: ref bits cleared except new/hit lines
+  int32_t hand;           // CLOCK hand after the scan
+  int32_t hit_line[2];    // lines hit by the producing kernel (ref set)
+  int32_t hhand, pad0;
+  int32_t line[kNQ];      // assigned lines
+  int32_t key[kNQ];       // their new rows
+  int32_t old[kNQ];       // evicted rows (-1: none)
+  int32_t hline[kNQ];     // host-tier line receiving old[q] (-1: no spill)
+  int32_t hold[kNQ];      // row evicted from that host line (-1)
+  int64_t hits, misses, rows_computed, x_passes, spec_rows, host_hits, spills;
+};
+
 constexpr int kFusedThreads = 256;
 constexpr int kStatusEvery = 32;  // host-mapped status refresh period (iterations)
 

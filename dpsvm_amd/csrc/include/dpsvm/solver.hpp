@@ -61,6 +61,7 @@ struct GpuSetupInfo {
   int64_t cache_lines = 0, host_cache_lines = 0;
   int blocks = 0;
   size_t bytes_device = 0;
+  std::string iteration;  // "fused-dense" | "fused-cache" | "chain" (rows/step/finalize)
 };
 
 class GpuSolver {

@@ -1,0 +1,576 @@
+// Fused SMO iteration for the kernel-row-cache mode (replicated X): ONE launch
+// per iteration, like the dense smo_fused, but the kernel rows come from a
+// CLOCK-managed cache of lines that is filled inside the same launch.
+//
+// Kernel t (every workgroup, redundantly where noted):
+//   1. pair from the previous launch's keys (every wave), eta + alpha update;
+//   2. wave 0 decides the cache actions for this iteration from the cache
+//      state at launch start corrected by the previous launch's pending-commit
+//      record (slot lookups for the two rows, speculative rows from the
+//      workgroup winners, a CLOCK victim scan, host-tier fetch/spill choices)
+//      — identical in every workgroup, so no inter-workgroup communication;
+//   3. every workgroup fills ITS OWN rows of the newly assigned lines: spill the
+//      victims' old segments to the pinned host tier, fetch host-tier hits, and
+//      the X pass for computed rows (fp32 MFMA 16x16x4, query vectors in LDS);
+//      i.e. the reference's cublasSgemv per miss (svmTrain.cu:212-249) becomes a
+//      slice of one distributed X pass inside the iteration kernel;
+//   4. f update from the two lines, classification, keys for iteration t+1;
+//   5. workgroup 0 commits the previous record (alphas + cache metadata) and
+//      publishes this iteration's record.
+// Readers never depend on an entry that the committer writes in the same
+// launch: they apply the previous record as a correction instead.
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+typedef unsigned long long u64x2l __attribute__((ext_vector_type(2)));
+
+
+// ---- state as of the previous launch = memory + pending record ----
+struct View {
+  const SmoArgs& a;
+  const FusedCacheRec& r;
+  __device__ int slot(int k) const {
+    for (int q = 0; q < r.n_new; ++q) {
+      if (r.key[q] == k) return r.line[q];
+      if (r.old[q] == k) return -1;
+    }
+    return a.slot_of[k];
+  }
+  __device__ int key_of(int l) const {
+    for (int q = 0; q < r.n_new; ++q)
+      if (r.line[q] == l) return r.key[q];
+    return a.key_of[l];
+  }
+  __device__ int ref(int l) const {
+    for (int q = 0; q < r.n_new; ++q)
+      if (r.line[q] == l) return 1;
+    if (l == r.hit_line[0] || l == r.hit_line[1]) return 1;
+    if (r.span > 0) {
+      int64_t off = (int64_t)l - r.hand0;
+      if (off < 0) off += a.L;
+      if (off < r.span) return 0;
+    }
+    return a.ref[l];
+  }
+  __device__ int hslot(int k) const {
+    if (a.H == 0) return -1;
+    for (int q = 0; q < r.n_new; ++q) {
+      if (r.hline[q] >= 0 && r.old[q] == k) return r.hline[q];
+      if (r.hline[q] >= 0 && r.hold[q] == k) return -1;
+    }
+    return a.hslot_of[k];
+  }
+  __device__ int hkey(int h) const {
+    for (int q = 0; q < r.n_new; ++q)
+      if (r.hline[q] == h) return r.old[q];
+    return a.hkey_of[h];
+  }
+};
+
+// decisions shared by all waves of a workgroup (LDS)
+struct Plan {
+  int n_new, n_compute, n_fetch, n_spill, n_miss, n_need;
+  int line_hi, line_lo, hit_hi, hit_lo;
+  int hand0, span, hand, hhand;
+  int line[kNQ], key[kNQ], old[kNQ], op[kNQ], hsrc[kNQ], hline[kNQ], hold[kNQ];
+};
+
+__device__ __forceinline__ void publish_status_lru(SmoStatus* st, const FusedCacheRec& o) {
+  if (!st) return;
+  st->iter = o.iter;
+  st->done = o.done;
+  st->b_hi = o.b_hi;
+  st->b_lo = o.b_lo;
+  st->hits = o.hits;
+  st->misses = o.misses;
+  st->rows_computed = o.rows_computed;
+  st->x_passes = o.x_passes;
+  st->spec_rows = o.spec_rows;
+  st->host_hits = o.host_hits;
+  st->spills = o.spills;
+  __atomic_store_n(&st->seq, o.iter, __ATOMIC_RELEASE);
+}
+
+// workgroup 0: apply the previous record to memory (alphas + cache metadata)
+__device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r) {
+  const int tid = threadIdx.x;
+  if (tid == 0 && r.i_hi >= 0) {
+    a.alpha[r.i_lo] = r.a_lo;
+    a.alpha[r.i_hi] = r.a_hi;
+  }
+  // CLOCK window: clear every scanned bit (new and hit lines re-set below)
+  for (int i = tid; i < r.span; i += kFusedThreads) {
+    const int l = (int)(((int64_t)r.hand0 + i) % a.L);
+    a.ref[l] = 0;
+  }
+  __syncthreads();
+  if (tid < 2 && r.hit_line[tid] >= 0) a.ref[r.hit_line[tid]] = 1;
+  if (tid < r.n_new) {
+    const int q = tid;
+    if (r.old[q] >= 0) a.slot_of[r.old[q]] = -1;
+    a.key_of[r.line[q]] = r.key[q];
+    a.slot_of[r.key[q]] = r.line[q];
+    a.ref[r.line[q]] = 1;
+    if (r.hline[q] >= 0) {
+      if (r.hold[q] >= 0) a.hslot_of[r.hold[q]] = -1;
+      a.hkey_of[r.hline[q]] = r.old[q];
+      a.hslot_of[r.old[q]] = r.hline[q];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
+                                                                      const uint64_t* __restrict__ p_in,
+                                                                      uint64_t* __restrict__ p_out,
+                                                                      const FusedCacheRec* __restrict__ r_in,
+                                                                      FusedCacheRec* __restrict__ r_out) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];  // [kNQ][dp+4] query vectors
+  __shared__ uint64_t kscr[8];
+  __shared__ Plan pl;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
+  const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
+  const int64_t j0 = row0 + tid;
+  const bool has0 = j0 < row_end;
+  float f0 = 0.f, a0 = 0.f, y0 = 0.f;
+  if (has0) {
+    f0 = a.f[j0];
+    a0 = a.alpha[a.off + j0];
+    y0 = a.y[a.off + j0];
+  }
+  const FusedCacheRec& rin = *r_in;  // read through the scalar cache (never written this launch)
+  const View view{a, rin};
+
+  // ---- 1. pair (every wave), alpha update ----
+  uint64_t kh = kKeyNone, kl = kKeyNone;
+  const u64x2l* pk = (const u64x2l*)p_in;
+  for (int b = lane; b < a.fused_G; b += 64) {
+    const u64x2l v = pk[b];
+    kh = v.x < kh ? v.x : kh;
+    kl = v.y < kl ? v.y : kl;
+  }
+  if (rin.done != kRunning) {
+    if (blockIdx.x == 0) {
+      commit_record(a, rin);
+      if (tid == 0) {
+        FusedCacheRec o = rin;
+        o.i_hi = o.i_lo = -1;
+        o.n_new = 0;
+        o.span = 0;
+        o.hit_line[0] = o.hit_line[1] = -1;
+        *r_out = o;
+        publish_status_lru(a.status, o);
+      }
+    }
+    return;
+  }
+  kh = wave_min_u64(kh);
+  kl = wave_min_u64(kl);
+  const bool nopair = kh == kKeyNone || kl == kKeyNone;
+  const int i_hi = nopair ? 0 : (int)key_index(kh), i_lo = nopair ? 0 : (int)key_index(kl);
+  const float b_hi = key_value(kh), b_lo = -key_value(kl);
+  int done = kRunning;
+  float c_hi = 0.f, c_lo = 0.f, a_hi_new = 0.f, a_lo_new = 0.f;
+  const int iter = rin.iter + 1;
+  if (nopair) {
+    done = kNoPair;
+  } else {
+    const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
+    const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
+    const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];
+    const float al_hi = a.alpha[i_hi], al_lo = a.alpha[i_lo];
+    float part = 0.f;
+    for (int k = 4 * lane; k < a.dp; k += 256) {
+      const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
+      const f4 t = h - l;
+      part += (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
+    }
+    const float dist2 = wave_sum(part);
+    const float a_hi_old = i_hi == rin.i_hi ? rin.a_hi : (i_hi == rin.i_lo ? rin.a_lo : al_hi);
+    const float a_lo_old = i_lo == rin.i_hi ? rin.a_hi : (i_lo == rin.i_lo ? rin.a_lo : al_lo);
+    a_hi_new = a_hi_old;
+    a_lo_new = a_lo_old;
+    if (!isfinite(b_hi) || !isfinite(b_lo)) {
+      done = kNonFinite;
+    } else {
+      const float k_hl = expf(-a.gamma * dist2);
+      const PairUpdate u =
+          pair_update(a_hi_old, a_lo_old, y_hi, y_lo, b_hi, b_lo, k_hl, a.C, a.tau, a.clip, i_hi == i_lo);
+      a_hi_new = u.a_hi_new;
+      a_lo_new = u.a_lo_new;
+      c_hi = u.c_hi;
+      c_lo = u.c_lo;
+      if (!gap_open(b_hi, b_lo, a.eps)) done = kConverged;
+      else if (iter >= a.max_iter) done = kMaxIter;
+    }
+  }
+
+  // ---- 2. cache plan (wave 0 of every workgroup; identical everywhere) ----
+  if (wave == 0) {
+    const int need_hi = c_hi != 0.f ? i_hi : -1;
+    const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
+    const int hit_hi = need_hi >= 0 ? view.slot(need_hi) : -1;
+    const int hit_lo = need_lo >= 0 ? view.slot(need_lo) : -1;
+    int keys[kNQ];  // uniform, compile-time indexed via unrolled loops below
+    int M = 0;
+    const int miss_hi = need_hi >= 0 && hit_hi < 0, miss_lo = need_lo >= 0 && hit_lo < 0;
+    // misses first (hi before lo), constant register indices only
+    keys[0] = miss_hi ? need_hi : need_lo;
+    keys[1] = need_lo;
+    M = miss_hi + miss_lo;
+    const int n_miss = M;
+    // speculative rows: best uncached workgroup winners (lane holds <= 4 per side)
+    const int budget = M > 0 ? min(min(a.spec, kNQ - M), max(0, a.L / 2 - M)) : 0;
+    if (budget > 0) {
+      uint64_t cand[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = lane + 64 * i;
+        cand[2 * i] = kKeyNone;
+        cand[2 * i + 1] = kKeyNone;
+        if (b < a.fused_G) {
+          const u64x2l v = pk[b];
+          cand[2 * i] = v.x;
+          cand[2 * i + 1] = v.y;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (cand[i] != kKeyNone) {
+          const int idx = (int)key_index(cand[i]);
+          if (idx == i_hi || idx == i_lo || view.slot(idx) >= 0) cand[i] = kKeyNone;
+        }
+      }
+      // up side (even slots) and low side (odd slots) alternate, best first
+      for (int rnd = 0; rnd < budget && M < kNQ; ++rnd) {
+        const int side = rnd & 1;
+        uint64_t best = kKeyNone;
+#pragma unroll
+        for (int i = side; i < 8; i += 2) best = cand[i] < best ? cand[i] : best;
+        best = wave_min_u64(best);
+        if (best == kKeyNone) {
+          // this side is exhausted; try the other next round
+          continue;
+        }
+#pragma unroll
+        for (int i = side; i < 8; i += 2)
+          if (cand[i] == best) cand[i] = kKeyNone;
+        const int idx = (int)key_index(best);
+        bool dup = false;
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) dup |= (q < M && keys[q] == idx);
+        // the same row can win on both sides: keep one copy
+        if (!dup) {
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q)
+            if (q == M) keys[q] = idx;
+          ++M;
+        }
+      }
+    }
+    // CLOCK victim scan over up to 1024 lines from the hand (64 per step)
+    int chosen_line[kNQ];
+    int found = 0, span = 0;
+    const int hand = rin.hand;
+    const int W = min(1024, a.L);
+    if (M > 0) {
+      for (int c0 = 0; c0 < W && found < M; c0 += 64) {
+        const int pos = c0 + lane;
+        const int p = (int)(((int64_t)hand + pos) % a.L);
+        const bool in_w = pos < W;
+        const bool pin = p == hit_hi || p == hit_lo;
+        const bool elig = in_w && !pin && view.ref(p) == 0;
+        const uint64_t m = __ballot(elig);
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        const int take = min(__popcll(m), M - found);
+        // positions of the taken lanes, in order
+#pragma unroll
+        for (int q = 0; q < kNQ; ++q) {
+          const bool mine = elig && rank == q - found && q >= found && q < found + take;
+          const uint64_t who = __ballot(mine);
+          if (who) {
+            const int src = __ffsll((unsigned long long)who) - 1;
+            chosen_line[q] = __shfl(p, src, 64);
+            span = c0 + src + 1;
+          }
+        }
+        found += take;
+      }
+      if (found < M) {
+        // the whole window was referenced (bits now cleared): first unpinned, unchosen lines
+        span = W;
+        for (int c0 = 0; c0 < W && found < M; c0 += 64) {
+          const int pos = c0 + lane;
+          const int p = (int)(((int64_t)hand + pos) % a.L);
+          bool elig = pos < W && p != hit_hi && p != hit_lo;
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) elig &= !(q < found && chosen_line[q] == p);
+          const uint64_t m = __ballot(elig);
+          const int rank = __popcll(m & ((1ull << lane) - 1ull));
+          const int take = min(__popcll(m), M - found);
+#pragma unroll
+          for (int q = 0; q < kNQ; ++q) {
+            const bool mine = elig && rank == q - found && q >= found && q < found + take;
+            const uint64_t who = __ballot(mine);
+            if (who) chosen_line[q] = __shfl(p, __ffsll((unsigned long long)who) - 1, 64);
+          }
+          found += take;
+        }
+      }
+    }
+    // victims and host tier (lane q handles query q)
+    int my_key = -1, my_line = -1, my_old = -1, my_hsrc = -1;
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q)
+      if (lane == q && q < M) {
+        my_key = keys[q];
+        my_line = chosen_line[q];
+      }
+    if (lane < M) {
+      my_old = view.key_of(my_line);
+      my_hsrc = view.hslot(my_key);
+    }
+    const bool want_spill = lane < M && a.H > 0 && my_old >= 0 && view.hslot(my_old) < 0;
+    const uint64_t sm = __ballot(want_spill);
+    const int srank = __popcll(sm & ((1ull << lane) - 1ull));
+    int my_hline = -1, my_hold = -1;
+    const int hl = a.H > 0 ? (int)(((int64_t)rin.hhand + srank) % a.H) : -1;
+    bool clash = false;  // never overwrite a host line this iteration fetches from
+    for (int q = 0; q < M; ++q) clash |= __shfl(my_hsrc, q, 64) == hl;  // all lanes active
+    if (want_spill && !clash && srank < a.H) {  // distinct host lines even when H < kNQ
+      my_hline = hl;
+      my_hold = view.hkey(hl);
+    }
+    const int n_fetch = __popcll(__ballot(lane < M && my_hsrc >= 0));
+    const int n_spill_used = __popcll(__ballot(my_hline >= 0));
+    if (lane < M) {
+      pl.line[lane] = my_line;
+      pl.key[lane] = my_key;
+      pl.old[lane] = my_old;
+      pl.op[lane] = my_hsrc >= 0 ? kOpFetch : kOpCompute;
+      pl.hsrc[lane] = my_hsrc;
+      pl.hline[lane] = my_hline;
+      pl.hold[lane] = my_hold;
+    }
+    if (lane == 0) {
+      pl.n_new = M;
+      pl.n_fetch = n_fetch;
+      pl.n_compute = M - n_fetch;
+      pl.n_spill = n_spill_used;
+      pl.n_miss = n_miss;
+      pl.n_need = (need_hi >= 0) + (need_lo >= 0);
+      pl.hit_hi = hit_hi;
+      pl.hit_lo = hit_lo;
+      pl.line_hi = need_hi >= 0 ? (hit_hi >= 0 ? hit_hi : chosen_line[0]) : -1;
+      if (c_lo != 0.f) {
+        if (i_lo == i_hi && c_hi != 0.f) pl.line_lo = pl.line_hi;
+        else pl.line_lo = hit_lo >= 0 ? hit_lo : (miss_hi ? chosen_line[1] : chosen_line[0]);
+      } else {
+        pl.line_lo = -1;
+      }
+      pl.hand0 = hand;
+      pl.span = M > 0 ? span : 0;
+      pl.hand = M > 0 ? (int)(((int64_t)hand + span) % a.L) : hand;
+      pl.hhand = a.H > 0 ? (int)(((int64_t)rin.hhand + __popcll(sm)) % a.H) : 0;
+    }
+  }
+  __syncthreads();
+  const int n_new = pl.n_new;
+
+  // ---- 3. fill this workgroup's rows of the new lines ----
+  if (n_new > 0 && done != kNonFinite && done != kNoPair) {
+    if (a.hlines) {
+      if (pl.n_spill > 0) {
+        for (int q = 0; q < n_new; ++q) {
+          const int h = pl.hline[q];
+          if (h < 0) continue;
+          const float* src = a.lines + (int64_t)pl.line[q] * a.ldl;
+          float* dst = a.hlines + (int64_t)h * a.ldl;
+          for (int64_t j = row0 + tid; j < row_end; j += kFusedThreads) dst[j] = src[j];
+        }
+        __syncthreads();  // old contents out before new values land
+      }
+      for (int q = 0; q < n_new; ++q) {
+        if (pl.op[q] != kOpFetch) continue;
+        const float* src = a.hlines + (int64_t)pl.hsrc[q] * a.ldl;
+        float* dst = a.lines + (int64_t)pl.line[q] * a.ldl;
+        for (int64_t j = row0 + tid; j < row_end; j += kFusedThreads) dst[j] = src[j];
+      }
+    }
+    if (pl.n_compute > 0) {
+      const int dp = a.dp;
+      const int q = lane & 15;
+      const bool qv = q < n_new && pl.op[q] == kOpCompute;
+      const float wsq = qv ? a.xsq[pl.key[q]] : 0.f;
+      const int64_t xbase = a.off - a.x_row0;
+      // 256 rows per pass: 4 waves x 4 tiles of 16 rows; query vectors staged in
+      // LDS in k-chunks of kRowsKC (same k order as smo_rows: bit-identical rows)
+      for (int64_t r0 = row0; r0 < row_end; r0 += 256) {
+        f4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
+        const float* xr = a.x + (xbase + r0 + wave * 64 + (lane & 15)) * dp + 4 * (lane >> 4);
+        for (int kc = 0; kc < dp; kc += kRowsKC) {
+          const int kcl = min(kRowsKC, dp - kc), ldw = kcl + 4, k4n = kcl >> 2;
+          const bool restage = dp > kRowsKC;  // else the single chunk stays resident
+          if (restage || r0 == row0) {
+            if (restage) __syncthreads();  // previous readers of the staged chunk are done
+            for (int i = tid; i < kNQ * k4n; i += kFusedThreads) {
+              const int qq = i / k4n, k4 = i - qq * k4n;
+              f4 v = {0.f, 0.f, 0.f, 0.f};
+              if (qq < n_new && pl.op[qq] == kOpCompute)
+                v = *(const f4*)(a.x + ((int64_t)pl.key[qq] - a.x_row0) * dp + kc + 4 * k4);
+              *(f4*)(wsm + qq * ldw + 4 * k4) = v;
+            }
+            __syncthreads();
+          }
+          const float* wr = wsm + q * ldw + 4 * (lane >> 4);
+          const float* xk = xr + kc;
+          for (int k0 = 0; k0 < kcl; k0 += 16) {
+            const f4 wv = *(const f4*)(wr + k0);
+            f4 xv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) xv[t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              acc[t] = mfma16(xv[t].x, wv.x, acc[t]);
+              acc[t] = mfma16(xv[t].y, wv.y, acc[t]);
+              acc[t] = mfma16(xv[t].z, wv.z, acc[t]);
+              acc[t] = mfma16(xv[t].w, wv.w, acc[t]);
+            }
+          }
+        }
+        if (qv) {
+          float* out = a.lines + (int64_t)pl.line[q] * a.ldl;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int64_t base = r0 + wave * 64 + t * 16 + (lane >> 4) * 4;
+            f4 kv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) kv[r] = rbf_from_dot(a.xsq[a.off + base + r], wsq, acc[t][r], a.gamma);
+            *(f4*)(out + base) = kv;
+          }
+        }
+      }
+    }
+    __syncthreads();  // this workgroup's new line segments are visible to all its waves
+  }
+
+  // ---- 5. (workgroup 0) commit the previous record, publish this one ----
+  if (blockIdx.x == 0) {
+    commit_record(a, rin);
+    if (tid == 0) {
+      FusedCacheRec o;
+      const bool upd = done != kNonFinite && done != kNoPair;
+      o.i_hi = upd ? i_hi : -1;
+      o.i_lo = upd ? i_lo : -1;
+      o.a_hi = a_hi_new;
+      o.a_lo = a_lo_new;
+      o.iter = upd ? iter : rin.iter;
+      o.done = done;
+      o.b_hi = nopair ? rin.b_hi : b_hi;
+      o.b_lo = nopair ? rin.b_lo : b_lo;
+      o.n_new = upd ? n_new : 0;
+      o.hand0 = pl.hand0;
+      o.span = upd ? pl.span : 0;
+      o.hand = upd ? pl.hand : rin.hand;
+      o.hit_line[0] = upd ? pl.hit_hi : -1;
+      o.hit_line[1] = upd ? pl.hit_lo : -1;
+      o.hhand = upd ? pl.hhand : rin.hhand;
+      for (int q = 0; q < kNQ; ++q) {
+        const bool v = upd && q < n_new;
+        o.line[q] = v ? pl.line[q] : -1;
+        o.key[q] = v ? pl.key[q] : -1;
+        o.old[q] = v ? pl.old[q] : -1;
+        o.hline[q] = v ? pl.hline[q] : -1;
+        o.hold[q] = v ? pl.hold[q] : -1;
+      }
+      o.hits = rin.hits + (upd ? pl.n_need - pl.n_miss : 0);
+      o.misses = rin.misses + (upd ? pl.n_miss : 0);
+      o.rows_computed = rin.rows_computed + (upd ? pl.n_compute : 0);
+      o.x_passes = rin.x_passes + ((upd && pl.n_compute > 0) ? 1 : 0);
+      o.spec_rows = rin.spec_rows + (upd ? n_new - pl.n_miss : 0);
+      o.host_hits = rin.host_hits + (upd ? pl.n_fetch : 0);
+      o.spills = rin.spills + (upd ? pl.n_spill : 0);
+      *r_out = o;
+      if (done != kRunning || iter % kStatusEvery == 0) publish_status_lru(a.status, o);
+    }
+  }
+  if (done == kNonFinite || done == kNoPair) return;
+
+  // ---- 4. f update + classification of this workgroup's rows ----
+  const bool upd_f = c_hi != 0.f || c_lo != 0.f;
+  const float* line_hi = pl.line_hi >= 0 ? a.lines + (int64_t)pl.line_hi * a.ldl : nullptr;
+  const float* line_lo = pl.line_lo >= 0 ? a.lines + (int64_t)pl.line_lo * a.ldl : nullptr;
+  uint64_t nh = kKeyNone, nlk = kKeyNone;
+  for (int64_t j = j0; j < row_end; j += kFusedThreads) {
+    const bool first = j == j0;
+    const int64_t g = a.off + j;
+    float fj = first ? f0 : a.f[j];
+    if (upd_f) {
+      float delta;
+      if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * line_hi[j]) + (c_lo * line_lo[j]);
+      else if (c_hi != 0.f) delta = c_hi * line_hi[j];
+      else delta = c_lo * line_lo[j];
+      fj += delta;
+      a.f[j] = fj;
+    }
+    if (done == kRunning) {
+      float av;
+      if (g == i_hi) av = a_hi_new;
+      else if (g == i_lo) av = a_lo_new;
+      else if (g == rin.i_hi) av = rin.a_hi;
+      else if (g == rin.i_lo) av = rin.a_lo;
+      else av = first ? a0 : a.alpha[g];
+      const float yv = first ? y0 : a.y[g];
+      if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
+      if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
+    }
+  }
+  if (done != kRunning) return;  // uniform
+  nh = wave_min_u64(nh);
+  nlk = wave_min_u64(nlk);
+  if (lane == 0) {
+    kscr[wave] = nh;
+    kscr[4 + wave] = nlk;
+  }
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      nh = kscr[w] < nh ? kscr[w] : nh;
+      nlk = kscr[4 + w] < nlk ? kscr[4 + w] : nlk;
+    }
+    u64x2l v;
+    v.x = nh;
+    v.y = nlk;
+    *(u64x2l*)(p_out + 2 * blockIdx.x) = v;
+  }
+}
+
+}  // namespace dev
+
+namespace launch {
+
+size_t smo_fused_lru_lds_bytes(int dp) { return (size_t)kNQ * ((dp < kRowsKC ? dp : kRowsKC) + 4) * sizeof(float); }
+
+bool smo_fused_lru_supported(int dp) { return dp >= 16 && dp % 16 == 0; }
+
+void smo_fused_lru(const SmoArgs& a, const uint64_t* p_in, uint64_t* p_out, const FusedCacheRec* r_in,
+                   FusedCacheRec* r_out, hipStream_t s) {
+  dev::smo_fused_lru_kernel<<<dim3(a.fused_G), kFusedThreads, smo_fused_lru_lds_bytes(a.dp), s>>>(a, p_in, p_out,
+                                                                                                  r_in, r_out);
+  post_launch("smo_fused_lru", s);
+}
+
+}  // namespace launch
+}  // namespace dpsvm

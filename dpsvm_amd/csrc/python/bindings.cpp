@@ -322,6 +322,7 @@ PYBIND11_MODULE(_C, m) {
         d["d"] = i.d;
         d["dp"] = i.dp;
         d["x_replicated"] = i.x_replicated;
+        d["iteration"] = i.iteration;
         d["cache_lines"] = i.cache_lines;
         d["blocks"] = i.blocks;
         d["bytes_device"] = i.bytes_device;

@@ -79,6 +79,7 @@ struct GpuSolver::Impl {
   uint8_t *records = nullptr, *my_record = nullptr;
   uint64_t* pf = nullptr;  // dense fused mode: two partial buffers [2][2*Gf]
   FusedRec* rf = nullptr;  // dense fused mode: two records
+  FusedCacheRec* rcf = nullptr;  // fused cache mode: two records
   int64_t Gf = 0, RBf = 0;
   uint64_t* stamps = nullptr;  // DPSVM_STAMPS diagnostics
   std::string stamps_path;
@@ -91,6 +92,7 @@ struct GpuSolver::Impl {
   int64_t n = 0, nl = 0, off = 0, x_rows = 0, G = 0, ldl = 0, L = 0;
   int d = 0, dp = 0;
   bool replicated = true, dense = false;
+  bool fused_lru = false;  // cache mode with one fused launch per iteration
   std::vector<float> h_y;
 
   hipGraphExec_t gexec = nullptr;
@@ -103,7 +105,7 @@ struct GpuSolver::Impl {
     if (graph) (void)hipGraphDestroy(graph);
     for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines,
                       (void*)slot_of, (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of,
-                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)stamps})
+                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps})
       if (ptr) (void)hipFree(ptr);
     if (status_h) (void)hipHostFree(status_h);
     if (hlines_h) (void)hipHostFree(hlines_h);
@@ -139,7 +141,10 @@ struct GpuSolver::Impl {
   void enqueue_fused(int k) {
     const int wi = k & 1, ri = wi ^ 1;
     uint64_t* pout = pf + (size_t)wi * 2 * Gf;
-    launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
+    if (fused_lru)
+      launch::smo_fused_lru(args, pf + (size_t)ri * 2 * Gf, pout, rcf + ri, rcf + wi, stream);
+    else
+      launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
     if (collectives()) allreduce_keys(pout, 2 * Gf);
   }
 
@@ -157,8 +162,10 @@ struct GpuSolver::Impl {
     }
   }
 
+  bool fused() const { return dense || fused_lru; }
+
   void enqueue_iteration(int k) {
-    if (dense) {
+    if (fused()) {
       enqueue_fused(k);
       return;
     }
@@ -219,13 +226,26 @@ struct GpuSolver::Impl {
     ck.clip = (int)p.clip; ck.iter = st.iter; ck.b_hi = st.b_hi; ck.b_lo = st.b_lo;
     ck.alpha.resize((size_t)n);
     HIP_CHECK(hipMemcpy(ck.alpha.data(), alpha, n * 4, hipMemcpyDeviceToHost));
-    if (dense) {
-      // the latest pair's alphas are still pending in the record of the last kernel
-      FusedRec r;
-      HIP_CHECK(hipMemcpy(&r, rf + 1, sizeof(r), hipMemcpyDeviceToHost));
-      if (r.i_hi >= 0) {
-        ck.alpha[r.i_lo] = r.a_lo;
-        ck.alpha[r.i_hi] = r.a_hi;
+    if (fused()) {
+      // the latest pair's alphas are still pending in the record of the last
+      // kernel (blocks have even length: the last kernel wrote record 1)
+      // (the record is exact; the host-mapped status refreshes every kStatusEvery)
+      int32_t ih = -1, il = -1;
+      float ah = 0.f, al = 0.f;
+      if (dense) {
+        FusedRec r;
+        HIP_CHECK(hipMemcpy(&r, rf + 1, sizeof(r), hipMemcpyDeviceToHost));
+        ih = r.i_hi; il = r.i_lo; ah = r.a_hi; al = r.a_lo;
+        ck.iter = r.iter; ck.b_hi = r.b_hi; ck.b_lo = r.b_lo;
+      } else {
+        FusedCacheRec r;
+        HIP_CHECK(hipMemcpy(&r, rcf + 1, sizeof(r), hipMemcpyDeviceToHost));
+        ih = r.i_hi; il = r.i_lo; ah = r.a_hi; al = r.a_lo;
+        ck.iter = r.iter; ck.b_hi = r.b_hi; ck.b_lo = r.b_lo;
+      }
+      if (ih >= 0) {
+        ck.alpha[il] = al;
+        ck.alpha[ih] = ah;
       }
     }
     std::vector<float> floc((size_t)ldl, 0.f), fall((size_t)ldl * world);
@@ -313,7 +333,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.off = sh.offset;
   const int64_t nl_max = (n + m.world - 1) / m.world;
   m.G = std::max<int64_t>(1, (nl_max + kStepRows - 1) / kStepRows);
-  m.ldl = m.G * kStepRows;
+  // fused-iteration geometry: <= ~256 workgroups, rows per workgroup a multiple of 256
+  {
+    const int64_t per = (nl_max + 255) / 256;
+    m.RBf = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
+    m.Gf = std::max<int64_t>(1, (nl_max + m.RBf - 1) / m.RBf);
+  }
+  // lines cover every row a kernel may write (the fused X pass writes whole 256-row tiles)
+  m.ldl = std::max<int64_t>(m.G * kStepRows, m.Gf * m.RBf);
 
   // ---- X placement ----
   if (n_x_rows == n) {
@@ -414,13 +441,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.L = m.dense ? n : std::max<int64_t>(2, std::min<int64_t>(want_lines, n));
   DPSVM_CHECK(m.L * line_bytes <= (double)freeb, "not enough device memory for 2 kernel-row lines");
   m.lines = dmalloc<float>((size_t)m.L * m.ldl, &m.bytes);
-  if (m.dense) {
-    // fused iteration geometry: <= ~256 workgroups, rows per workgroup a multiple of 256
-    const int64_t per = (nl_max + 255) / 256;
-    m.RBf = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
-    m.Gf = std::max<int64_t>(1, (nl_max + m.RBf - 1) / m.RBf);
+  // cache mode with replicated X: one fused launch per iteration
+  // (DPSVM_LRU_KERNELS=3 keeps the rows/step/finalize chain, e.g. for A/B runs)
+  const char* lk = std::getenv("DPSVM_LRU_KERNELS");
+  m.fused_lru = !m.dense && m.replicated && launch::smo_fused_lru_supported(m.dp) && !(lk && lk[0] == '3');
+  if (m.fused()) {
     m.pf = dmalloc<uint64_t>((size_t)4 * m.Gf, &m.bytes);
-    m.rf = dmalloc<FusedRec>(2, &m.bytes);
+    if (m.dense) m.rf = dmalloc<FusedRec>(2, &m.bytes);
+    else m.rcf = dmalloc<FusedCacheRec>(2, &m.bytes);
   }
   if (!m.dense) {
     m.slot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
@@ -501,6 +529,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.info.x_replicated = m.replicated;
   m.info.cache_lines = m.L;
   m.info.blocks = (int)m.G;
+  m.info.iteration = m.dense ? "fused-dense" : (m.fused_lru ? "fused-cache" : "chain");
   m.info.bytes_device = m.bytes;
   return m.info;
 }
@@ -579,6 +608,22 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   const int64_t fault_iter = trace::fault_nan_iter();
   bool fault_done = false;
   auto t0 = Clock::now();
+  if (m.fused_lru) {
+    // seed: record "no pending pair, empty cache" in buffer 1 + initial keys
+    FusedCacheRec r0;
+    memset(&r0, 0, sizeof(r0));
+    r0.i_hi = r0.i_lo = -1;
+    r0.iter = (int32_t)iter0;
+    r0.done = kRunning;
+    r0.b_hi = b_hi0;
+    r0.b_lo = b_lo0;
+    r0.hit_line[0] = r0.hit_line[1] = -1;
+    for (int q = 0; q < kNQ; ++q) r0.line[q] = r0.key[q] = r0.old[q] = r0.hline[q] = r0.hold[q] = -1;
+    HIP_CHECK(hipMemcpyAsync(m.rcf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
+    uint64_t* p1 = m.pf + 2 * m.Gf;
+    launch::smo_fused(m.args, 0, nullptr, p1, nullptr, nullptr, m.stream);
+    if (m.collectives()) m.allreduce_keys(p1, 2 * m.Gf);
+  }
   if (m.dense) {
     trace::Range gram_range("dpsvm/gram_gemm");
     // whole Gram shard K[i][j], i over all n rows, j over local rows: one MFMA GEMM
@@ -601,7 +646,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   }
   const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
   int B = std::max(1, m.p.graph_block);
-  if (m.dense) B = std::max(2, (B + 1) / 2 * 2);  // ping-pong parity must survive graph replays
+  if (m.fused()) B = std::max(2, (B + 1) / 2 * 2);  // ping-pong parity must survive graph replays
   if (graphs) {
     try {
       m.build_graph(B);

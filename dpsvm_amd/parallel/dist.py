@@ -64,15 +64,12 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistContext
         torch.cuda.set_device(local_rank)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "cpu:gloo,cuda:nccl" if use_gpu else "gloo"
-        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu:
-            kw["device_id"] = torch.device(f"cuda:{local_rank}")
-        try:
-            dist.init_process_group(**kw)
-        except TypeError:
-            kw.pop("device_id", None)
-            dist.init_process_group(**kw)
+        # lazy NCCL(RCCL) init (no device_id): ranks rehearsing on a shared GPU
+        # (DPSVM_FORCE_DEVICE) only ever touch the gloo side
+        shared_gpu = bool(os.environ.get("DPSVM_FORCE_DEVICE"))
+        backend = "cpu:gloo,cuda:nccl" if (use_gpu and not shared_gpu) else "gloo"
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
         ctx.backend = backend
         ctx.initialized_here = True
     elif dist.is_initialized():

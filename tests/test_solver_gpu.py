@@ -169,3 +169,43 @@ def test_gpu_fault_injection_and_verify(monkeypatch, C):
     comm = C.rccl_comm(C.rccl_unique_id(), 0, 1, 0)
     ok = SVC(C=1.0, gamma=0.1, device="cuda", force_collectives=True).fit(X, y, comm=comm)
     assert ok.converged_
+
+
+@pytest.mark.parametrize("extra", [{"cache_lines": 64}, {"cache_lines": 2, "spec_rows": 0},
+                                   {"cache_lines": 24, "host_cache_lines": 8}])
+def test_fused_cache_iteration_matches_kernel_chain(monkeypatch, extra):
+    """The one-launch cache-mode iteration (smo_fused_lru) and the
+    rows/step/finalize chain compute bit-identical kernel rows, so they must
+    follow the same SMO trajectory (whatever their cache decisions)."""
+    X, y = synthetic("covtype", n=5000, seed=6)
+    kw = dict(C=4.0, gamma=0.5, device="cuda", **extra)
+    fused = SVC(**kw).fit(X, y)
+    assert fused.setup_info_["iteration"] == "fused-cache"
+    monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
+    chain = SVC(**kw).fit(X, y)
+    assert chain.setup_info_["iteration"] == "chain"
+    assert fused.n_iter_ == chain.n_iter_
+    assert np.array_equal(fused.alpha_, chain.alpha_)
+    assert fused.stats_["cache_misses"] > 0
+    if extra.get("host_cache_lines"):
+        assert fused.stats_["host_hits"] > 0
+
+
+def test_fused_cache_wide_features_and_checkpoint(monkeypatch, tmp_path):
+    """d > one LDS k-chunk (multi-chunk X pass) + checkpoint/resume in cache mode."""
+    X, y = synthetic("blobs", n=2500, d=1100, seed=8, sep=1.0)
+    kw = dict(C=1.0, gamma=1.0 / 1100, device="cuda", cache_lines=48)
+    cpu = SVC(C=1.0, gamma=1.0 / 1100, device="cpu").fit(X, y)
+    full = SVC(**kw).fit(X, y)
+    assert full.setup_info_["iteration"] == "fused-cache"
+    _close(full, cpu, 2500)
+    ck = str(tmp_path / "ck.bin")
+    part = SVC(max_iter=full.n_iter_ // 2, checkpoint_path=ck, checkpoint_every=max(1, full.n_iter_ // 4),
+               **kw).fit(X, y)
+    assert not part.converged_
+    res = SVC(**kw).fit(X, y, resume=ck)
+    assert res.n_iter_ == full.n_iter_
+    assert np.array_equal(res.alpha_, full.alpha_)
+    monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
+    chain = SVC(**kw).fit(X, y)
+    assert np.array_equal(chain.alpha_, full.alpha_)
