@@ -35,6 +35,19 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// |x_h - x_l|^2 over dp floats (multiple of 4, zero padded, 16-B aligned) by
+// one wave.  Every kernel that derives eta uses this exact lane mapping and
+// summation tree, so all iteration variants agree bit for bit.
+__device__ __forceinline__ float wave_dist2(const float* xh, const float* xl, int dp, int lane) {
+  float part = 0.f;
+  for (int k = 4 * lane; k < dp; k += 256) {
+    const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
+    const f4 t = h - l;
+    part += (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
+  }
+  return wave_sum(part);
+}
+
 // Block-wide min of two u64 keys; result valid in every thread.
 // `scratch` must hold 2*(blockDim/64) u64.
 template <int THREADS>

@@ -164,13 +164,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   const float al_hi = a.alpha[i_hi], al_lo = a.alpha[i_lo];
   const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
   const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
-  float part = 0.f;
-  for (int k = 4 * lane; k < a.dp; k += 256) {  // dp is a multiple of 16, padding is zero
-    const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
-    const f4 t = h - l;
-    part += (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
-  }
-  const float dist2 = wave_sum(part);  // identical tree in every wave -> identical value
+  const float dist2 = wave_dist2(xh, xl, a.dp, lane);  // identical tree in every wave
 
   // pending commit of the previous pair overrides memory (hi wins)
   const float a_hi_old = i_hi == rin.i_hi ? rin.a_hi : (i_hi == rin.i_lo ? rin.a_lo : al_hi);

@@ -188,13 +188,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
     const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];
     const float al_hi = a.alpha[i_hi], al_lo = a.alpha[i_lo];
-    float part = 0.f;
-    for (int k = 4 * lane; k < a.dp; k += 256) {
-      const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
-      const f4 t = h - l;
-      part += (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
-    }
-    const float dist2 = wave_sum(part);
+    const float dist2 = wave_dist2(xh, xl, a.dp, lane);
     const float a_hi_old = i_hi == rin.i_hi ? rin.a_hi : (i_hi == rin.i_lo ? rin.a_lo : al_hi);
     const float a_lo_old = i_lo == rin.i_hi ? rin.a_hi : (i_lo == rin.i_lo ? rin.a_lo : al_lo);
     a_hi_new = a_hi_old;

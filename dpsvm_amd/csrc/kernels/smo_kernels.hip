@@ -266,7 +266,6 @@ __device__ __forceinline__ int block_rank(bool pred, int* wsum, int* total) {
 
 __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
   __shared__ uint64_t kscr[2 * (kFinThreads / 64)];
-  __shared__ float fscr[kFinThreads / 64];
   __shared__ int wsum[kFinThreads / 64];
   __shared__ int s_i[32];
   __shared__ float s_f[4];
@@ -339,12 +338,8 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
     xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
     xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
   }
-  float part = 0.f;
-  for (int k = tid; k < a.d; k += kFinThreads) {
-    const float t = xh[k] - xl[k];
-    part += t * t;
-  }
-  const float dist2 = block_sum<kFinThreads>(part, fscr);
+  // wave 0 (thread 0 applies the update): same arithmetic as the fused kernels
+  const float dist2 = tid < 64 ? wave_dist2(xh, xl, a.dp, tid) : 0.f;
 
   // ---- 3. alpha update and stop test (one lane) ----
   if (tid == 0) {
