@@ -498,7 +498,7 @@ __global__ __launch_bounds__(kFinThreads) void smo_finalize_kernel(SmoArgs a) {
     n_spill = __popcll(sm);
     n_fetch = __popcll(__ballot(hsrc >= 0));
     int hspill = -1;
-    if (want_spill) {
+    if (want_spill && srank < a.H) {  // distinct host lines even when H < kNQ
       const int hl = (int)(((int64_t)hhand + srank) % a.H);
       bool clash = false;  // never overwrite a host line this iteration fetches from
       for (int q = 0; q < M; ++q) clash |= s_hsrc[q] == hl;
