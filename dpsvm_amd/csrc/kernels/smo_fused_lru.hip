@@ -429,7 +429,44 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
           }
           const float* wr = wsm + q * ldw + 4 * (lane >> 4);
           const float* xk = xr + kc;
-          for (int k0 = 0; k0 < kcl; k0 += 16) {
+          // X loads double-buffered in batches of 4 k-steps x 4 tiles (16 KiB
+          // per wave in flight; one workgroup per CU, so the pass is
+          // HBM-latency bound without deep prefetch).  sched_barrier keeps the
+          // scheduler from sinking the loads back next to their MFMAs.
+          const int nb = kcl >> 6;
+          f4 xa[4][4], xb[4][4];
+          auto load = [&](f4 (&v)[4][4], int k) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int t = 0; t < 4; ++t) v[s][t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k + 16 * s);
+          };
+          auto comp = [&](const f4 (&v)[4][4], int k) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const f4 wv = *(const f4*)(wr + k + 16 * s);
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                acc[t] = mfma16(v[s][t].x, wv.x, acc[t]);
+                acc[t] = mfma16(v[s][t].y, wv.y, acc[t]);
+                acc[t] = mfma16(v[s][t].z, wv.z, acc[t]);
+                acc[t] = mfma16(v[s][t].w, wv.w, acc[t]);
+              }
+            }
+          };
+          if (nb > 0) load(xa, 0);
+          for (int b = 0; b < nb; b += 2) {
+            if (b + 1 < nb) load(xb, (b + 1) * 64);
+            __builtin_amdgcn_sched_barrier(0);
+            comp(xa, b * 64);
+            if (b + 1 < nb) {
+              if (b + 2 < nb) load(xa, (b + 2) * 64);
+              __builtin_amdgcn_sched_barrier(0);
+              comp(xb, (b + 1) * 64);
+            }
+          }
+          int k0 = nb * 64;
+          for (; k0 < kcl; k0 += 16) {
             const f4 wv = *(const f4*)(wr + k0);
             f4 xv[4];
 #pragma unroll
