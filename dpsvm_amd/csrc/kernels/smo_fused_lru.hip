@@ -78,7 +78,7 @@ struct View {
 // decisions shared by all waves of a workgroup (LDS)
 struct Plan {
   int n_new, n_compute, n_fetch, n_spill, n_miss, n_need;
-  int line_hi, line_lo, hit_hi, hit_lo;
+  int line_hi, line_lo, hit_hi, hit_lo, need_hi, miss_hi;
   int hand0, span, hand, hhand;
   int line[kNQ], key[kNQ], old[kNQ], op[kNQ], hsrc[kNQ], hline[kNQ], hold[kNQ];
 };
@@ -97,6 +97,28 @@ __device__ __forceinline__ void publish_status_lru(SmoStatus* st, const FusedCac
   st->host_hits = o.host_hits;
   st->spills = o.spills;
   __atomic_store_n(&st->seq, o.iter, __ATOMIC_RELEASE);
+}
+
+// exclusive prefix sum of v over the workgroup (kFusedThreads); *total = sum
+__device__ __forceinline__ int block_excl_scan(int v, int* total, int* wsum) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kFusedThreads / 64; ++w) {
+    before += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return before + incl - v;
 }
 
 // workgroup 0: apply the previous record to memory (alphas + cache metadata)
@@ -134,6 +156,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
                                                                       FusedCacheRec* __restrict__ r_out) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];  // [kNQ][dp+4] query vectors
   __shared__ uint64_t kscr[8];
+  __shared__ int kscan[kFusedThreads / 64];
   __shared__ Plan pl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
@@ -208,19 +231,18 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     }
   }
 
-  // ---- 2. cache plan (wave 0 of every workgroup; identical everywhere) ----
+  // ---- 2. cache plan (identical in every workgroup) ----
+  // 2a. wave 0: rows the f update needs, their lines, speculative rows
   if (wave == 0) {
     const int need_hi = c_hi != 0.f ? i_hi : -1;
     const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
     const int hit_hi = need_hi >= 0 ? view.slot(need_hi) : -1;
     const int hit_lo = need_lo >= 0 ? view.slot(need_lo) : -1;
-    int keys[kNQ];  // uniform, compile-time indexed via unrolled loops below
-    int M = 0;
     const int miss_hi = need_hi >= 0 && hit_hi < 0, miss_lo = need_lo >= 0 && hit_lo < 0;
-    // misses first (hi before lo), constant register indices only
-    keys[0] = miss_hi ? need_hi : need_lo;
+    int keys[kNQ];  // uniform; constant indices only (unrolled selects)
+    keys[0] = miss_hi ? need_hi : need_lo;  // misses first (hi before lo)
     keys[1] = need_lo;
-    M = miss_hi + miss_lo;
+    int M = miss_hi + miss_lo;
     const int n_miss = M;
     // speculative rows: best uncached workgroup winners (lane holds <= 4 per side)
     const int budget = M > 0 ? min(min(a.spec, kNQ - M), max(0, a.L / 2 - M)) : 0;
@@ -251,10 +273,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
 #pragma unroll
         for (int i = side; i < 8; i += 2) best = cand[i] < best ? cand[i] : best;
         best = wave_min_u64(best);
-        if (best == kKeyNone) {
-          // this side is exhausted; try the other next round
-          continue;
-        }
+        if (best == kKeyNone) continue;  // this side is exhausted
 #pragma unroll
         for (int i = side; i < 8; i += 2)
           if (cand[i] == best) cand[i] = kKeyNone;
@@ -262,8 +281,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
         bool dup = false;
 #pragma unroll
         for (int q = 0; q < kNQ; ++q) dup |= (q < M && keys[q] == idx);
-        // the same row can win on both sides: keep one copy
-        if (!dup) {
+        if (!dup) {  // the same row can win on both sides: keep one copy
 #pragma unroll
           for (int q = 0; q < kNQ; ++q)
             if (q == M) keys[q] = idx;
@@ -271,65 +289,73 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
         }
       }
     }
-    // CLOCK victim scan over up to 1024 lines from the hand (64 per step)
-    int chosen_line[kNQ];
-    int found = 0, span = 0;
-    const int hand = rin.hand;
-    const int W = min(1024, a.L);
-    if (M > 0) {
-      for (int c0 = 0; c0 < W && found < M; c0 += 64) {
-        const int pos = c0 + lane;
-        const int p = (int)(((int64_t)hand + pos) % a.L);
-        const bool in_w = pos < W;
-        const bool pin = p == hit_hi || p == hit_lo;
-        const bool elig = in_w && !pin && view.ref(p) == 0;
-        const uint64_t m = __ballot(elig);
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        const int take = min(__popcll(m), M - found);
-        // positions of the taken lanes, in order
-#pragma unroll
-        for (int q = 0; q < kNQ; ++q) {
-          const bool mine = elig && rank == q - found && q >= found && q < found + take;
-          const uint64_t who = __ballot(mine);
-          if (who) {
-            const int src = __ffsll((unsigned long long)who) - 1;
-            chosen_line[q] = __shfl(p, src, 64);
-            span = c0 + src + 1;
-          }
-        }
-        found += take;
-      }
-      if (found < M) {
-        // the whole window was referenced (bits now cleared): first unpinned, unchosen lines
-        span = W;
-        for (int c0 = 0; c0 < W && found < M; c0 += 64) {
-          const int pos = c0 + lane;
-          const int p = (int)(((int64_t)hand + pos) % a.L);
-          bool elig = pos < W && p != hit_hi && p != hit_lo;
-#pragma unroll
-          for (int q = 0; q < kNQ; ++q) elig &= !(q < found && chosen_line[q] == p);
-          const uint64_t m = __ballot(elig);
-          const int rank = __popcll(m & ((1ull << lane) - 1ull));
-          const int take = min(__popcll(m), M - found);
-#pragma unroll
-          for (int q = 0; q < kNQ; ++q) {
-            const bool mine = elig && rank == q - found && q >= found && q < found + take;
-            const uint64_t who = __ballot(mine);
-            if (who) chosen_line[q] = __shfl(p, __ffsll((unsigned long long)who) - 1, 64);
-          }
-          found += take;
-        }
-      }
-    }
-    // victims and host tier (lane q handles query q)
-    int my_key = -1, my_line = -1, my_old = -1, my_hsrc = -1;
 #pragma unroll
     for (int q = 0; q < kNQ; ++q)
-      if (lane == q && q < M) {
-        my_key = keys[q];
-        my_line = chosen_line[q];
+      if (lane == q && q < M) pl.key[q] = keys[q];
+    if (lane == 0) {
+      pl.n_new = M;
+      pl.n_miss = n_miss;
+      pl.n_need = (need_hi >= 0) + (need_lo >= 0);
+      pl.hit_hi = hit_hi;
+      pl.hit_lo = hit_lo;
+      pl.need_hi = need_hi;
+      pl.miss_hi = miss_hi;
+      pl.span = 0;
+    }
+  }
+  __syncthreads();
+
+  // 2b. all waves: CLOCK victim scan of a window of up to 1024 lines from the
+  //     hand, 4 consecutive positions per thread, one block-wide rank
+  const int M = pl.n_new;  // uniform
+  if (M > 0) {
+    const int hand = rin.hand;
+    const int W = min(1024, a.L);
+    const int pin0 = pl.hit_hi, pin1 = pl.hit_lo;
+    int p[4];
+    bool e[4];
+    bool unp[4];
+    int cnt = 0, cnt2 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pos = 4 * tid + j;
+      p[j] = (int)(((int64_t)hand + pos) % a.L);
+      unp[j] = pos < W && p[j] != pin0 && p[j] != pin1;
+      e[j] = unp[j] && view.ref(p[j]) == 0;
+      cnt += e[j];
+      cnt2 += unp[j] && !e[j];
+    }
+    int total = 0;
+    int r = block_excl_scan(cnt, &total, kscan);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (e[j]) {
+        if (r < M) pl.line[r] = p[j];
+        if (r == M - 1) pl.span = 4 * tid + j + 1;  // second chances consumed up to here
+        ++r;
       }
+    }
+    if (total < M) {  // uniform: the window was (nearly) all referenced
+      int total2 = 0;
+      int r2 = block_excl_scan(cnt2, &total2, kscan);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (unp[j] && !e[j]) {
+          if (total + r2 < M) pl.line[total + r2] = p[j];
+          ++r2;
+        }
+      }
+      if (tid == 0) pl.span = W;
+    }
+    __syncthreads();
+  }
+
+  // 2c. wave 0: victims' rows, host-tier fetch / spill (lane q <-> new line q)
+  if (wave == 0) {
+    int my_key = -1, my_line = -1, my_old = -1, my_hsrc = -1;
     if (lane < M) {
+      my_key = pl.key[lane];
+      my_line = pl.line[lane];
       my_old = view.key_of(my_line);
       my_hsrc = view.hslot(my_key);
     }
@@ -346,9 +372,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     }
     const int n_fetch = __popcll(__ballot(lane < M && my_hsrc >= 0));
     const int n_spill_used = __popcll(__ballot(my_hline >= 0));
+    const int line0 = __shfl(my_line, 0, 64), line1 = __shfl(my_line, 1, 64);
     if (lane < M) {
-      pl.line[lane] = my_line;
-      pl.key[lane] = my_key;
       pl.old[lane] = my_old;
       pl.op[lane] = my_hsrc >= 0 ? kOpFetch : kOpCompute;
       pl.hsrc[lane] = my_hsrc;
@@ -356,24 +381,21 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       pl.hold[lane] = my_hold;
     }
     if (lane == 0) {
-      pl.n_new = M;
       pl.n_fetch = n_fetch;
       pl.n_compute = M - n_fetch;
       pl.n_spill = n_spill_used;
-      pl.n_miss = n_miss;
-      pl.n_need = (need_hi >= 0) + (need_lo >= 0);
-      pl.hit_hi = hit_hi;
-      pl.hit_lo = hit_lo;
-      pl.line_hi = need_hi >= 0 ? (hit_hi >= 0 ? hit_hi : chosen_line[0]) : -1;
+      const int hit_hi = pl.hit_hi, hit_lo = pl.hit_lo;
+      pl.line_hi = pl.need_hi >= 0 ? (hit_hi >= 0 ? hit_hi : line0) : -1;
       if (c_lo != 0.f) {
         if (i_lo == i_hi && c_hi != 0.f) pl.line_lo = pl.line_hi;
-        else pl.line_lo = hit_lo >= 0 ? hit_lo : (miss_hi ? chosen_line[1] : chosen_line[0]);
+        else pl.line_lo = hit_lo >= 0 ? hit_lo : (pl.miss_hi ? line1 : line0);
       } else {
         pl.line_lo = -1;
       }
-      pl.hand0 = hand;
-      pl.span = M > 0 ? span : 0;
-      pl.hand = M > 0 ? (int)(((int64_t)hand + span) % a.L) : hand;
+      const int span = M > 0 ? pl.span : 0;
+      pl.span = span;
+      pl.hand0 = rin.hand;
+      pl.hand = (int)(((int64_t)rin.hand + span) % a.L);
       pl.hhand = a.H > 0 ? (int)(((int64_t)rin.hhand + __popcll(sm)) % a.H) : 0;
     }
   }
