@@ -11,7 +11,31 @@ import sys
 
 import numpy as np
 
-RING, SLOTS = 4096, 6
+RING, SLOTS = 4096, 8
+
+
+LRU_PHASES = ["alpha", "rows_chosen", "victims", "plan", "fill", "commit", "f_update_keys"]
+
+
+def main_lru(path):
+    """smo_fused_lru slots: 0 entry, 1 alpha update, 2 rows chosen, 3 victims,
+    4 plan done, 5 lines filled, 6 commit, 7 end; split by fill time (X pass)."""
+    a = np.fromfile(path, dtype=np.uint64).reshape(RING, 2, SLOTS).astype(np.int64)
+    ok = (a[:, :, 0] > 0).all(1) & (a[:, :, 7] > 0).all(1)
+    a = a[ok]
+    out = {"samples": int(len(a))}
+    for b, name in ((0, "wg0"), (1, "wglast")):
+        d = np.diff(a[:, b, :], axis=1) * 10.0
+        fill = d[:, 4]
+        for tag, sel in (("pass", fill > 3000), ("nopass", fill <= 3000)):
+            if sel.sum() == 0:
+                continue
+            out[f"{name}_{tag}"] = {"n": int(sel.sum()),
+                                    **{ph + "_ns": float(np.median(d[sel, i])) for i, ph in enumerate(LRU_PHASES)},
+                                    "total_ns": float(np.median((a[sel, b, 7] - a[sel, b, 0]) * 10.0))}
+    period = np.diff(a[:, 0, 0]) * 10.0
+    out["iter_period_ns_median"] = float(np.median(period[period > 0]))
+    print(json.dumps(out, indent=1))
 
 
 def main(path):
@@ -41,4 +65,7 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if len(sys.argv) > 2 and sys.argv[2] == "--lru":
+        main_lru(sys.argv[1])
+    else:
+        main(sys.argv[1])

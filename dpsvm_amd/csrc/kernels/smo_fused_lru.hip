@@ -172,6 +172,16 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   }
   const FusedCacheRec& rin = *r_in;  // read through the scalar cache (never written this launch)
   const View view{a, rin};
+  // diagnostics only (a.stamps == nullptr in normal runs): 0 entry, 1 alpha
+  // update, 2 rows chosen, 3 victims, 4 plan done, 5 lines filled, 6 commit, 7 end
+  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+  const uint64_t ts_entry = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
+  const int it_st = rin.iter;
+  auto stamp = [&](int slot) {
+    if (stamping)
+      a.stamps[((size_t)(it_st % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots + slot] =
+          slot == 0 ? ts_entry : __builtin_amdgcn_s_memrealtime();
+  };
 
   // ---- 1. pair (every wave), alpha update ----
   uint64_t kh = kKeyNone, kl = kKeyNone;
@@ -231,6 +241,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     }
   }
 
+  stamp(0);
+  stamp(1);
   // ---- 2. cache plan (identical in every workgroup) ----
   // 2a. wave 0: rows the f update needs, their lines, speculative rows
   if (wave == 0) {
@@ -304,6 +316,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     }
   }
   __syncthreads();
+  stamp(2);
 
   // 2b. all waves: CLOCK victim scan of a window of up to 1024 lines from the
   //     hand, 4 consecutive positions per thread, one block-wide rank
@@ -350,6 +363,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     __syncthreads();
   }
 
+  stamp(3);
   // 2c. wave 0: victims' rows, host-tier fetch / spill (lane q <-> new line q)
   if (wave == 0) {
     int my_key = -1, my_line = -1, my_old = -1, my_hsrc = -1;
@@ -400,6 +414,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     }
   }
   __syncthreads();
+  stamp(4);
   const int n_new = pl.n_new;
 
   // ---- 3. fill this workgroup's rows of the new lines ----
@@ -518,6 +533,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     __syncthreads();  // this workgroup's new line segments are visible to all its waves
   }
 
+  stamp(5);
   // ---- 5. (workgroup 0) commit the previous record, publish this one ----
   if (blockIdx.x == 0) {
     commit_record(a, rin);
@@ -558,6 +574,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       if (done != kRunning || iter % kStatusEvery == 0) publish_status_lru(a.status, o);
     }
   }
+  stamp(6);
   if (done == kNonFinite || done == kNoPair) return;
 
   // ---- 4. f update + classification of this workgroup's rows ----
@@ -608,6 +625,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     v.y = nlk;
     *(u64x2l*)(p_out + 2 * blockIdx.x) = v;
   }
+  stamp(7);
 }
 
 }  // namespace dev
