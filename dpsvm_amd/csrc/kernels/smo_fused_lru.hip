@@ -15,8 +15,8 @@
 //      i.e. the reference's cublasSgemv per miss (svmTrain.cu:212-249) becomes a
 //      slice of one distributed X pass inside the iteration kernel;
 //   4. f update from the two lines, classification, keys for iteration t+1;
-//   5. workgroup 0 commits the previous record (alphas + cache metadata) and
-//      publishes this iteration's record.
+//   5. the last workgroup (fewest rows) commits the previous record (alphas +
+//      cache metadata) and publishes this iteration's record.
 // Readers never depend on an entry that the committer writes in the same
 // launch: they apply the previous record as a correction instead.
 #include <hip/hip_runtime.h>
@@ -34,44 +34,67 @@ typedef unsigned long long u64x2l __attribute__((ext_vector_type(2)));
 
 
 // ---- state as of the previous launch = memory + pending record ----
+// The record's per-line arrays are staged in LDS (broadcast reads) and every
+// lookup is branch-free with the memory load issued first: lookups sit on the
+// serial critical path of every iteration.  Keys and evicted rows of one
+// record are disjoint, lines are distinct, so at most one entry matches.
+struct RecLds {
+  int key[kNQ], old[kNQ], line[kNQ], hline[kNQ], hold[kNQ];
+};
+
 struct View {
   const SmoArgs& a;
-  const FusedCacheRec& r;
+  const RecLds& r;
+  int n, hit0, hit1, hand0, span;
   __device__ int slot(int k) const {
-    for (int q = 0; q < r.n_new; ++q) {
-      if (r.key[q] == k) return r.line[q];
-      if (r.old[q] == k) return -1;
+    int v = a.slot_of[k];
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) {
+      if (q < n) {
+        v = r.key[q] == k ? r.line[q] : v;
+        v = r.old[q] == k ? -1 : v;
+      }
     }
-    return a.slot_of[k];
+    return v;
   }
   __device__ int key_of(int l) const {
-    for (int q = 0; q < r.n_new; ++q)
-      if (r.line[q] == l) return r.key[q];
-    return a.key_of[l];
+    int v = a.key_of[l];
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q)
+      if (q < n) v = r.line[q] == l ? r.key[q] : v;
+    return v;
   }
   __device__ int ref(int l) const {
-    for (int q = 0; q < r.n_new; ++q)
-      if (r.line[q] == l) return 1;
-    if (l == r.hit_line[0] || l == r.hit_line[1]) return 1;
-    if (r.span > 0) {
-      int64_t off = (int64_t)l - r.hand0;
+    int v = a.ref[l];
+    if (span > 0) {
+      int64_t off = (int64_t)l - hand0;
       if (off < 0) off += a.L;
-      if (off < r.span) return 0;
+      if (off < span) v = 0;  // scanned: second chance consumed
     }
-    return a.ref[l];
+    if (l == hit0 || l == hit1) v = 1;
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q)
+      if (q < n) v = r.line[q] == l ? 1 : v;
+    return v;
   }
   __device__ int hslot(int k) const {
     if (a.H == 0) return -1;
-    for (int q = 0; q < r.n_new; ++q) {
-      if (r.hline[q] >= 0 && r.old[q] == k) return r.hline[q];
-      if (r.hline[q] >= 0 && r.hold[q] == k) return -1;
+    int v = a.hslot_of[k];
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) {
+      if (q < n && r.hline[q] >= 0) {
+        v = r.old[q] == k ? r.hline[q] : v;
+        v = r.hold[q] == k ? -1 : v;
+      }
     }
-    return a.hslot_of[k];
+    return v;
   }
   __device__ int hkey(int h) const {
-    for (int q = 0; q < r.n_new; ++q)
-      if (r.hline[q] == h) return r.old[q];
-    return a.hkey_of[h];
+    int v = a.hkey_of[h];
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q)
+      if (q < n) v = r.hline[q] == h ? r.old[q] : v;
+    return v;
   }
 };
 
@@ -121,30 +144,45 @@ __device__ __forceinline__ int block_excl_scan(int v, int* total, int* wsum) {
   return before + incl - v;
 }
 
-// workgroup 0: apply the previous record to memory (alphas + cache metadata)
-__device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r) {
+// one workgroup: apply the previous record to memory (alphas + cache
+// metadata), all threads in parallel and without a barrier: scanned window
+// bits are written once with their final value (1 for new / hit lines).
+__device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const RecLds& rl) {
   const int tid = threadIdx.x;
+  const int n = r.n_new, h0 = r.hit_line[0], h1 = r.hit_line[1];
   if (tid == 0 && r.i_hi >= 0) {
     a.alpha[r.i_lo] = r.a_lo;
     a.alpha[r.i_hi] = r.a_hi;
   }
-  // CLOCK window: clear every scanned bit (new and hit lines re-set below)
   for (int i = tid; i < r.span; i += kFusedThreads) {
     const int l = (int)(((int64_t)r.hand0 + i) % a.L);
-    a.ref[l] = 0;
+    bool keep = l == h0 || l == h1;
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) keep |= q < n && rl.line[q] == l;
+    a.ref[l] = keep ? 1 : 0;
   }
-  __syncthreads();
-  if (tid < 2 && r.hit_line[tid] >= 0) a.ref[r.hit_line[tid]] = 1;
-  if (tid < r.n_new) {
-    const int q = tid;
-    if (r.old[q] >= 0) a.slot_of[r.old[q]] = -1;
-    a.key_of[r.line[q]] = r.key[q];
-    a.slot_of[r.key[q]] = r.line[q];
-    a.ref[r.line[q]] = 1;
-    if (r.hline[q] >= 0) {
-      if (r.hold[q] >= 0) a.hslot_of[r.hold[q]] = -1;
-      a.hkey_of[r.hline[q]] = r.old[q];
-      a.hslot_of[r.old[q]] = r.hline[q];
+  auto outside = [&](int l) {  // set bits of lines the window loop does not touch
+    int64_t off = (int64_t)l - r.hand0;
+    if (off < 0) off += a.L;
+    return off >= r.span;
+  };
+  if (tid < 2) {
+    const int l = tid == 0 ? h0 : h1;
+    if (l >= 0 && outside(l)) a.ref[l] = 1;
+  }
+  if (tid >= 64 && tid < 64 + n) {
+    const int q = tid - 64;
+    const int l = rl.line[q], k = rl.key[q], o = rl.old[q];
+    if (o >= 0) a.slot_of[o] = -1;
+    a.key_of[l] = k;
+    a.slot_of[k] = l;
+    if (outside(l)) a.ref[l] = 1;
+    const int hl = rl.hline[q];
+    if (hl >= 0) {
+      const int ho = rl.hold[q];
+      if (ho >= 0) a.hslot_of[ho] = -1;
+      a.hkey_of[hl] = o;
+      a.hslot_of[o] = hl;
     }
   }
 }
@@ -159,7 +197,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   __shared__ int kscan[kFusedThreads / 64];
   __shared__ Plan pl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool lead = blockIdx.x == 0 && tid == 0;
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
   const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
   const int64_t j0 = row0 + tid;
@@ -171,7 +208,14 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     y0 = a.y[a.off + j0];
   }
   const FusedCacheRec& rin = *r_in;  // read through the scalar cache (never written this launch)
-  const View view{a, rin};
+  __shared__ RecLds rl;
+  if (tid < 5 * kNQ) {
+    const int arr = tid / kNQ, q = tid - arr * kNQ;
+    const int32_t* src = arr == 0 ? rin.key : arr == 1 ? rin.old : arr == 2 ? rin.line : arr == 3 ? rin.hline : rin.hold;
+    int* dst = arr == 0 ? rl.key : arr == 1 ? rl.old : arr == 2 ? rl.line : arr == 3 ? rl.hline : rl.hold;
+    dst[q] = src[q];
+  }
+  const View view{a, rl, rin.n_new, rin.hit_line[0], rin.hit_line[1], rin.hand0, rin.span};
   // diagnostics only (a.stamps == nullptr in normal runs): 0 entry, 1 alpha
   // update, 2 rows chosen, 3 victims, 4 plan done, 5 lines filled, 6 commit, 7 end
   const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
@@ -191,9 +235,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     kh = v.x < kh ? v.x : kh;
     kl = v.y < kl ? v.y : kl;
   }
+  __syncthreads();  // staged record visible (the key loads above are in flight meanwhile)
   if (rin.done != kRunning) {
-    if (blockIdx.x == 0) {
-      commit_record(a, rin);
+    if (blockIdx.x == a.fused_G - 1) {
+      commit_record(a, rin, rl);
       if (tid == 0) {
         FusedCacheRec o = rin;
         o.i_hi = o.i_lo = -1;
@@ -534,12 +579,21 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   }
 
   stamp(5);
-  // ---- 5. (workgroup 0) commit the previous record, publish this one ----
-  if (blockIdx.x == 0) {
-    commit_record(a, rin);
+  // ---- 5. (last workgroup: fewest rows) commit the previous record, publish this one ----
+  if (blockIdx.x == a.fused_G - 1) {
+    commit_record(a, rin, rl);
+    const bool upd = done != kNonFinite && done != kNoPair;
+    if (tid < kNQ) {
+      const int q = tid;
+      const bool v = upd && q < n_new;
+      r_out->line[q] = v ? pl.line[q] : -1;
+      r_out->key[q] = v ? pl.key[q] : -1;
+      r_out->old[q] = v ? pl.old[q] : -1;
+      r_out->hline[q] = v ? pl.hline[q] : -1;
+      r_out->hold[q] = v ? pl.hold[q] : -1;
+    }
     if (tid == 0) {
-      FusedCacheRec o;
-      const bool upd = done != kNonFinite && done != kNoPair;
+      FusedCacheRec o;  // scalar part (arrays written above)
       o.i_hi = upd ? i_hi : -1;
       o.i_lo = upd ? i_lo : -1;
       o.a_hi = a_hi_new;
@@ -555,14 +609,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       o.hit_line[0] = upd ? pl.hit_hi : -1;
       o.hit_line[1] = upd ? pl.hit_lo : -1;
       o.hhand = upd ? pl.hhand : rin.hhand;
-      for (int q = 0; q < kNQ; ++q) {
-        const bool v = upd && q < n_new;
-        o.line[q] = v ? pl.line[q] : -1;
-        o.key[q] = v ? pl.key[q] : -1;
-        o.old[q] = v ? pl.old[q] : -1;
-        o.hline[q] = v ? pl.hline[q] : -1;
-        o.hold[q] = v ? pl.hold[q] : -1;
-      }
       o.hits = rin.hits + (upd ? pl.n_need - pl.n_miss : 0);
       o.misses = rin.misses + (upd ? pl.n_miss : 0);
       o.rows_computed = rin.rows_computed + (upd ? pl.n_compute : 0);
@@ -570,7 +616,13 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       o.spec_rows = rin.spec_rows + (upd ? n_new - pl.n_miss : 0);
       o.host_hits = rin.host_hits + (upd ? pl.n_fetch : 0);
       o.spills = rin.spills + (upd ? pl.n_spill : 0);
-      *r_out = o;
+      r_out->i_hi = o.i_hi; r_out->i_lo = o.i_lo; r_out->a_hi = o.a_hi; r_out->a_lo = o.a_lo;
+      r_out->iter = o.iter; r_out->done = o.done; r_out->b_hi = o.b_hi; r_out->b_lo = o.b_lo;
+      r_out->n_new = o.n_new; r_out->hand0 = o.hand0; r_out->span = o.span; r_out->hand = o.hand;
+      r_out->hit_line[0] = o.hit_line[0]; r_out->hit_line[1] = o.hit_line[1]; r_out->hhand = o.hhand;
+      r_out->hits = o.hits; r_out->misses = o.misses; r_out->rows_computed = o.rows_computed;
+      r_out->x_passes = o.x_passes; r_out->spec_rows = o.spec_rows; r_out->host_hits = o.host_hits;
+      r_out->spills = o.spills;
       if (done != kRunning || iter % kStatusEvery == 0) publish_status_lru(a.status, o);
     }
   }
