@@ -46,8 +46,9 @@ struct View {
   const SmoArgs& a;
   const RecLds& r;
   int n, hit0, hit1, hand0, span;
-  __device__ int slot(int k) const {
-    int v = a.slot_of[k];
+  __device__ int slot(int k) const { return slot_fix(k, a.slot_of[k]); }
+  // v = memory slot_of[k], corrected by the pending record
+  __device__ int slot_fix(int k, int v) const {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       if (q < n) {
@@ -155,7 +156,8 @@ __device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const Re
     a.alpha[r.i_hi] = r.a_hi;
   }
   for (int i = tid; i < r.span; i += kFusedThreads) {
-    const int l = (int)(((int64_t)r.hand0 + i) % a.L);
+    const int ll = r.hand0 + i;  // span <= min(1024, L)
+    const int l = ll >= a.L ? ll - a.L : ll;
     bool keep = l == h0 || l == h1;
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) keep |= q < n && rl.line[q] == l;
@@ -293,8 +295,9 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   if (wave == 0) {
     const int need_hi = c_hi != 0.f ? i_hi : -1;
     const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
-    const int hit_hi = need_hi >= 0 ? view.slot(need_hi) : -1;
-    const int hit_lo = need_lo >= 0 ? view.slot(need_lo) : -1;
+    const int s_hi = a.slot_of[max(need_hi, 0)], s_lo = a.slot_of[max(need_lo, 0)];  // both loads in flight
+    const int hit_hi = need_hi >= 0 ? view.slot_fix(need_hi, s_hi) : -1;
+    const int hit_lo = need_lo >= 0 ? view.slot_fix(need_lo, s_lo) : -1;
     const int miss_hi = need_hi >= 0 && hit_hi < 0, miss_lo = need_lo >= 0 && hit_lo < 0;
     int keys[kNQ];  // uniform; constant indices only (unrolled selects)
     keys[0] = miss_hi ? need_hi : need_lo;  // misses first (hi before lo)
@@ -316,12 +319,16 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
           cand[2 * i + 1] = v.y;
         }
       }
+      // cache check: the 8 slot loads are issued together (branch-free)
+      int cidx[8], cmem[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cidx[i] = cand[i] != kKeyNone ? (int)key_index(cand[i]) : 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cmem[i] = a.slot_of[cidx[i]];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        if (cand[i] != kKeyNone) {
-          const int idx = (int)key_index(cand[i]);
-          if (idx == i_hi || idx == i_lo || view.slot(idx) >= 0) cand[i] = kKeyNone;
-        }
+        const int idx = cidx[i];
+        if (idx == i_hi || idx == i_lo || view.slot_fix(idx, cmem[i]) >= 0) cand[i] = kKeyNone;
       }
       // up side (even slots) and low side (odd slots) alternate, best first
       for (int rnd = 0; rnd < budget && M < kNQ; ++rnd) {
@@ -377,7 +384,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int pos = 4 * tid + j;
-      p[j] = (int)(((int64_t)hand + pos) % a.L);
+      const int pp = hand + pos;  // hand < L; only pos < W <= L is used
+      p[j] = pp >= a.L ? pp - a.L : pp;
       unp[j] = pos < W && p[j] != pin0 && p[j] != pin1;
       e[j] = unp[j] && view.ref(p[j]) == 0;
       cnt += e[j];
