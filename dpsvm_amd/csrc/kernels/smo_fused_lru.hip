@@ -197,6 +197,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   extern __shared__ __attribute__((aligned(16))) float wsm[];  // [kNQ][dp+4] query vectors
   __shared__ uint64_t kscr[8];
   __shared__ int kscan[kFusedThreads / 64];
+  __shared__ __attribute__((aligned(16))) uint64_t sc_hi[kFusedThreads], sc_lo[kFusedThreads];
+  __shared__ int s_ord[2 * kNQ];
   __shared__ Plan pl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
@@ -291,80 +293,74 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   stamp(0);
   stamp(1);
   // ---- 2. cache plan (identical in every workgroup) ----
-  // 2a. wave 0: rows the f update needs, their lines, speculative rows
-  if (wave == 0) {
-    const int need_hi = c_hi != 0.f ? i_hi : -1;
-    const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
-    const int s_hi = a.slot_of[max(need_hi, 0)], s_lo = a.slot_of[max(need_lo, 0)];  // both loads in flight
-    const int hit_hi = need_hi >= 0 ? view.slot_fix(need_hi, s_hi) : -1;
-    const int hit_lo = need_lo >= 0 ? view.slot_fix(need_lo, s_lo) : -1;
-    const int miss_hi = need_hi >= 0 && hit_hi < 0, miss_lo = need_lo >= 0 && hit_lo < 0;
-    int keys[kNQ];  // uniform; constant indices only (unrolled selects)
-    keys[0] = miss_hi ? need_hi : need_lo;  // misses first (hi before lo)
-    keys[1] = need_lo;
-    int M = miss_hi + miss_lo;
-    const int n_miss = M;
-    // speculative rows: best uncached workgroup winners (lane holds <= 4 per side)
-    const int budget = M > 0 ? min(min(a.spec, kNQ - M), max(0, a.L / 2 - M)) : 0;
-    if (budget > 0) {
-      uint64_t cand[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = lane + 64 * i;
-        cand[2 * i] = kKeyNone;
-        cand[2 * i + 1] = kKeyNone;
-        if (b < a.fused_G) {
-          const u64x2l v = pk[b];
-          cand[2 * i] = v.x;
-          cand[2 * i + 1] = v.y;
-        }
-      }
-      // cache check: the 8 slot loads are issued together (branch-free)
-      int cidx[8], cmem[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) cidx[i] = cand[i] != kKeyNone ? (int)key_index(cand[i]) : 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) cmem[i] = a.slot_of[cidx[i]];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int idx = cidx[i];
-        if (idx == i_hi || idx == i_lo || view.slot_fix(idx, cmem[i]) >= 0) cand[i] = kKeyNone;
-      }
-      // up side (even slots) and low side (odd slots) alternate, best first
-      for (int rnd = 0; rnd < budget && M < kNQ; ++rnd) {
-        const int side = rnd & 1;
-        uint64_t best = kKeyNone;
-#pragma unroll
-        for (int i = side; i < 8; i += 2) best = cand[i] < best ? cand[i] : best;
-        best = wave_min_u64(best);
-        if (best == kKeyNone) continue;  // this side is exhausted
-#pragma unroll
-        for (int i = side; i < 8; i += 2)
-          if (cand[i] == best) cand[i] = kKeyNone;
-        const int idx = (int)key_index(best);
-        bool dup = false;
-#pragma unroll
-        for (int q = 0; q < kNQ; ++q) dup |= (q < M && keys[q] == idx);
-        if (!dup) {  // the same row can win on both sides: keep one copy
-#pragma unroll
-          for (int q = 0; q < kNQ; ++q)
-            if (q == M) keys[q] = idx;
-          ++M;
-        }
-      }
+  // 2a. rows the f update needs and their lines (every thread, uniform), then
+  //     speculative rows: the best uncached workgroup winners of each side,
+  //     ranked block-wide (thread b owns workgroup b's two keys; exact top-k
+  //     by counting, no serial reduction rounds), interleaved hi/lo
+  const int need_hi = c_hi != 0.f ? i_hi : -1;
+  const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
+  int hit_hi, hit_lo;
+  {
+    const int s_hi = a.slot_of[max(need_hi, 0)], s_lo = a.slot_of[max(need_lo, 0)];  // both in flight
+    hit_hi = need_hi >= 0 ? view.slot_fix(need_hi, s_hi) : -1;
+    hit_lo = need_lo >= 0 ? view.slot_fix(need_lo, s_lo) : -1;
+  }
+  const int miss_hi = need_hi >= 0 && hit_hi < 0, miss_lo = need_lo >= 0 && hit_lo < 0;
+  const int n_miss = miss_hi + miss_lo;
+  const int budget = n_miss > 0 ? min(min(a.spec, kNQ - n_miss), max(0, a.L / 2 - n_miss)) : 0;
+  if (tid == 0) {
+    pl.key[0] = miss_hi ? need_hi : need_lo;  // misses first (hi before lo)
+    pl.key[1] = need_lo;
+    pl.n_new = n_miss;
+    pl.n_miss = n_miss;
+    pl.n_need = (need_hi >= 0) + (need_lo >= 0);
+    pl.hit_hi = hit_hi;
+    pl.hit_lo = hit_lo;
+    pl.need_hi = need_hi;
+    pl.miss_hi = miss_hi;
+    pl.span = 0;
+  }
+  if (budget > 0) {  // uniform
+    uint64_t ch = kKeyNone, cl = kKeyNone;
+    if (tid < a.fused_G) {
+      const u64x2l v = pk[tid];
+      ch = v.x;
+      cl = v.y;
     }
-#pragma unroll
-    for (int q = 0; q < kNQ; ++q)
-      if (lane == q && q < M) pl.key[q] = keys[q];
-    if (lane == 0) {
-      pl.n_new = M;
-      pl.n_miss = n_miss;
-      pl.n_need = (need_hi >= 0) + (need_lo >= 0);
-      pl.hit_hi = hit_hi;
-      pl.hit_lo = hit_lo;
-      pl.need_hi = need_hi;
-      pl.miss_hi = miss_hi;
-      pl.span = 0;
+    const int ih = ch != kKeyNone ? (int)key_index(ch) : 0;
+    const int il = cl != kKeyNone ? (int)key_index(cl) : 0;
+    const int mh = a.slot_of[ih], ml = a.slot_of[il];
+    if (ih == i_hi || ih == i_lo || view.slot_fix(ih, mh) >= 0) ch = kKeyNone;
+    if (il == i_hi || il == i_lo || view.slot_fix(il, ml) >= 0) cl = kKeyNone;
+    sc_hi[tid] = ch;
+    sc_lo[tid] = cl;
+    if (tid < 2 * kNQ) s_ord[tid] = -1;
+    __syncthreads();
+    int rh = 0, rl = 0, vh = 0, vl = 0;
+    for (int u = 0; u < kFusedThreads; u += 2) {
+      const u64x2l hh = *(const u64x2l*)&sc_hi[u], ll = *(const u64x2l*)&sc_lo[u];
+      rh += (hh.x < ch) + (hh.y < ch);
+      rl += (ll.x < cl) + (ll.y < cl);
+      vh += (hh.x != kKeyNone) + (hh.y != kKeyNone);
+      vl += (ll.x != kKeyNone) + (ll.y != kKeyNone);
+    }
+    int take_h = min(vh, (budget + 1) / 2);
+    const int take_l = min(vl, budget - take_h);
+    take_h = min(vh, budget - take_l);  // an exhausted low side leaves room
+    if (ch != kKeyNone && rh < take_h) s_ord[2 * rh] = ih;
+    __syncthreads();
+    if (cl != kKeyNone && rl < take_l) {
+      bool dup = false;  // a free SV can win on both sides: keep one copy
+      for (int q = 0; q < take_h; ++q) dup |= s_ord[2 * q] == il;
+      if (!dup) s_ord[2 * rl + 1] = il;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int v = lane < 2 * kNQ ? s_ord[lane] : -1;
+      const uint64_t m = __ballot(v >= 0);
+      const int pos = n_miss + __popcll(m & ((1ull << lane) - 1ull));
+      if (v >= 0) pl.key[pos] = v;  // take_h + take_l <= budget <= kNQ - n_miss
+      if (lane == 0) pl.n_new = n_miss + __popcll(m);
     }
   }
   __syncthreads();
