@@ -123,6 +123,13 @@ __device__ __forceinline__ void publish_status_lru(SmoStatus* st, const FusedCac
   __atomic_store_n(&st->seq, o.iter, __ATOMIC_RELEASE);
 }
 
+// lane `src`'s value (the builtin is 32-bit: two halves)
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int src) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, src);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // exclusive prefix sum of v over the workgroup (kFusedThreads); *total = sum
 __device__ __forceinline__ int block_excl_scan(int v, int* total, int* wsum) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -197,7 +204,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   extern __shared__ __attribute__((aligned(16))) float wsm[];  // [kNQ][dp+4] query vectors
   __shared__ uint64_t kscr[8];
   __shared__ int kscan[kFusedThreads / 64];
-  __shared__ __attribute__((aligned(16))) uint64_t sc_hi[kFusedThreads], sc_lo[kFusedThreads];
   __shared__ int s_ord[2 * kNQ];
   __shared__ Plan pl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -294,9 +300,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   stamp(1);
   // ---- 2. cache plan (identical in every workgroup) ----
   // 2a. rows the f update needs and their lines (every thread, uniform), then
-  //     speculative rows: the best uncached workgroup winners of each side,
-  //     ranked block-wide (thread b owns workgroup b's two keys; exact top-k
-  //     by counting, no serial reduction rounds), interleaved hi/lo
+  //     speculative rows (wave 0): the best uncached workgroup winners of
+  //     each side (best per lane, ranked by a readlane sweep), interleaved hi/lo
   const int need_hi = c_hi != 0.f ? i_hi : -1;
   const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
   int hit_hi, hit_lo;
@@ -320,48 +325,71 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     pl.miss_hi = miss_hi;
     pl.span = 0;
   }
-  if (budget > 0) {  // uniform
+  if (budget > 0 && wave == 0) {  // uniform
+    // lane holds workgroups lane + 64 i (i < 4) per side; filter, keep the lane's best
     uint64_t ch = kKeyNone, cl = kKeyNone;
-    if (tid < a.fused_G) {
-      const u64x2l v = pk[tid];
-      ch = v.x;
-      cl = v.y;
+    {
+      uint64_t cand[8];
+      int cidx[8], cmem[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = lane + 64 * i;
+        cand[2 * i] = kKeyNone;
+        cand[2 * i + 1] = kKeyNone;
+        if (b < a.fused_G) {
+          const u64x2l v = pk[b];
+          cand[2 * i] = v.x;
+          cand[2 * i + 1] = v.y;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cidx[i] = cand[i] != kKeyNone ? (int)key_index(cand[i]) : 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cmem[i] = a.slot_of[cidx[i]];  // 8 loads in flight
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int idx = cidx[i];
+        if (idx == i_hi || idx == i_lo || view.slot_fix(idx, cmem[i]) >= 0) cand[i] = kKeyNone;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ch = cand[2 * i] < ch ? cand[2 * i] : ch;
+        cl = cand[2 * i + 1] < cl ? cand[2 * i + 1] : cl;
+      }
     }
-    const int ih = ch != kKeyNone ? (int)key_index(ch) : 0;
-    const int il = cl != kKeyNone ? (int)key_index(cl) : 0;
-    const int mh = a.slot_of[ih], ml = a.slot_of[il];
-    if (ih == i_hi || ih == i_lo || view.slot_fix(ih, mh) >= 0) ch = kKeyNone;
-    if (il == i_hi || il == i_lo || view.slot_fix(il, ml) >= 0) cl = kKeyNone;
-    sc_hi[tid] = ch;
-    sc_lo[tid] = cl;
-    if (tid < 2 * kNQ) s_ord[tid] = -1;
-    __syncthreads();
+    // rank of the lane's best among the 64 lane bests (readlane sweep: VALU/SALU
+    // only, no LDS traffic and no serial reduction rounds)
     int rh = 0, rl = 0, vh = 0, vl = 0;
-    for (int u = 0; u < kFusedThreads; u += 2) {
-      const u64x2l hh = *(const u64x2l*)&sc_hi[u], ll = *(const u64x2l*)&sc_lo[u];
-      rh += (hh.x < ch) + (hh.y < ch);
-      rl += (ll.x < cl) + (ll.y < cl);
-      vh += (hh.x != kKeyNone) + (hh.y != kKeyNone);
-      vl += (ll.x != kKeyNone) + (ll.y != kKeyNone);
+    for (int src = 0; src < 64; ++src) {
+      const uint64_t oh = readlane_u64(ch, src), ol = readlane_u64(cl, src);
+      rh += oh < ch;
+      rl += ol < cl;
+      vh += oh != kKeyNone;
+      vl += ol != kKeyNone;
     }
     int take_h = min(vh, (budget + 1) / 2);
     const int take_l = min(vl, budget - take_h);
     take_h = min(vh, budget - take_l);  // an exhausted low side leaves room
-    if (ch != kKeyNone && rh < take_h) s_ord[2 * rh] = ih;
-    __syncthreads();
-    if (cl != kKeyNone && rl < take_l) {
+    if (lane < 2 * kNQ) s_ord[lane] = -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int ih = ch != kKeyNone ? (int)key_index(ch) : -1;
+    const int il = cl != kKeyNone ? (int)key_index(cl) : -1;
+    if (ih >= 0 && rh < take_h) s_ord[2 * rh] = ih;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (il >= 0 && rl < take_l) {
       bool dup = false;  // a free SV can win on both sides: keep one copy
       for (int q = 0; q < take_h; ++q) dup |= s_ord[2 * q] == il;
       if (!dup) s_ord[2 * rl + 1] = il;
     }
-    __syncthreads();
-    if (wave == 0) {
-      const int v = lane < 2 * kNQ ? s_ord[lane] : -1;
-      const uint64_t m = __ballot(v >= 0);
-      const int pos = n_miss + __popcll(m & ((1ull << lane) - 1ull));
-      if (v >= 0) pl.key[pos] = v;  // take_h + take_l <= budget <= kNQ - n_miss
-      if (lane == 0) pl.n_new = n_miss + __popcll(m);
-    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int v = lane < 2 * kNQ ? s_ord[lane] : -1;
+    const uint64_t m = __ballot(v >= 0);
+    const int pos = n_miss + __popcll(m & ((1ull << lane) - 1ull));
+    if (v >= 0) pl.key[pos] = v;  // take_h + take_l <= budget <= kNQ - n_miss
+    if (lane == 0) pl.n_new = n_miss + __popcll(m);
   }
   __syncthreads();
   stamp(2);
