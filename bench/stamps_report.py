@@ -11,10 +11,12 @@ import sys
 
 import numpy as np
 
-RING, SLOTS = 4096, 8
+RING, SLOTS = 4096, 12
 
 
-LRU_PHASES = ["alpha", "rows_chosen", "victims", "plan", "fill", "commit", "f_update_keys"]
+LRU_ORDER = [0, 1, 8, 9, 10, 2, 3, 4, 5, 6, 7]  # slot order in time
+LRU_PHASES = ["alpha", "need_slots", "spec_cands", "spec_rank", "rows_chosen", "victims", "plan", "fill", "commit",
+              "f_update_keys"]
 
 
 def main_lru(path):
@@ -25,8 +27,12 @@ def main_lru(path):
     a = a[ok]
     out = {"samples": int(len(a))}
     for b, name in ((0, "wg0"), (1, "wglast")):
-        d = np.diff(a[:, b, :], axis=1) * 10.0
-        fill = d[:, 4]
+        t = a[:, b, LRU_ORDER].copy()
+        # slots 9/10 are only stamped in speculating iterations: carry the previous time
+        for c in range(1, t.shape[1]):
+            t[:, c] = np.where(t[:, c] >= t[:, c - 1], t[:, c], t[:, c - 1])
+        d = np.diff(t, axis=1) * 10.0
+        fill = d[:, LRU_PHASES.index("fill")]
         for tag, sel in (("pass", fill > 3000), ("nopass", fill <= 3000)):
             if sel.sum() == 0:
                 continue

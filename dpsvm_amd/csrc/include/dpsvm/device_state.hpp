@@ -150,6 +150,6 @@ struct SmoArgs {
   uint64_t* stamps;
 };
 constexpr int kStampRing = 4096;
-constexpr int kStampSlots = 8;
+constexpr int kStampSlots = 12;
 
 }  // namespace dpsvm

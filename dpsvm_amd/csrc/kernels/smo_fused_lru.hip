@@ -46,8 +46,7 @@ struct View {
   const SmoArgs& a;
   const RecLds& r;
   int n, hit0, hit1, hand0, span;
-  __device__ int slot(int k) const { return slot_fix(k, a.slot_of[k]); }
-  // v = memory slot_of[k], corrected by the pending record
+  // *_fix(x, v): v = the memory value for x, corrected by the pending record
   __device__ int slot_fix(int k, int v) const {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
@@ -58,17 +57,15 @@ struct View {
     }
     return v;
   }
-  __device__ int key_of(int l) const {
-    int v = a.key_of[l];
+  __device__ int key_fix(int l, int v) const {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q)
       if (q < n) v = r.line[q] == l ? r.key[q] : v;
     return v;
   }
-  __device__ int ref(int l) const {
-    int v = a.ref[l];
+  __device__ int ref_fix(int l, int v) const {
     if (span > 0) {
-      int64_t off = (int64_t)l - hand0;
+      int off = l - hand0;
       if (off < 0) off += a.L;
       if (off < span) v = 0;  // scanned: second chance consumed
     }
@@ -78,9 +75,7 @@ struct View {
       if (q < n) v = r.line[q] == l ? 1 : v;
     return v;
   }
-  __device__ int hslot(int k) const {
-    if (a.H == 0) return -1;
-    int v = a.hslot_of[k];
+  __device__ int hslot_fix(int k, int v) const {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       if (q < n && r.hline[q] >= 0) {
@@ -90,13 +85,14 @@ struct View {
     }
     return v;
   }
-  __device__ int hkey(int h) const {
-    int v = a.hkey_of[h];
+  __device__ int hkey_fix(int h, int v) const {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q)
       if (q < n) v = r.hline[q] == h ? r.old[q] : v;
     return v;
   }
+  __device__ int hslot(int k) const { return a.H == 0 ? -1 : hslot_fix(k, a.hslot_of[k]); }
+  __device__ int hkey(int h) const { return hkey_fix(h, a.hkey_of[h]); }
 };
 
 // decisions shared by all waves of a workgroup (LDS)
@@ -123,13 +119,6 @@ __device__ __forceinline__ void publish_status_lru(SmoStatus* st, const FusedCac
   __atomic_store_n(&st->seq, o.iter, __ATOMIC_RELEASE);
 }
 
-// lane `src`'s value (the builtin is 32-bit: two halves)
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int src) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, src);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), src);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // exclusive prefix sum of v over the workgroup (kFusedThreads); *total = sum
 __device__ __forceinline__ int block_excl_scan(int v, int* total, int* wsum) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -152,17 +141,17 @@ __device__ __forceinline__ int block_excl_scan(int v, int* total, int* wsum) {
   return before + incl - v;
 }
 
-// one workgroup: apply the previous record to memory (alphas + cache
-// metadata), all threads in parallel and without a barrier: scanned window
-// bits are written once with their final value (1 for new / hit lines).
-__device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const RecLds& rl) {
-  const int tid = threadIdx.x;
+// Apply the previous record to memory (alphas + cache metadata) with threads
+// ct = 0..nt-1 (nt >= 32) of one workgroup, in parallel and without a barrier:
+// scanned window bits are written once with their final value (1 for new /
+// hit lines).  Readers never need the result in this launch (View).
+__device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const RecLds& rl, int ct, int nt) {
   const int n = r.n_new, h0 = r.hit_line[0], h1 = r.hit_line[1];
-  if (tid == 0 && r.i_hi >= 0) {
+  if (ct == 0 && r.i_hi >= 0) {
     a.alpha[r.i_lo] = r.a_lo;
     a.alpha[r.i_hi] = r.a_hi;
   }
-  for (int i = tid; i < r.span; i += kFusedThreads) {
+  for (int i = ct; i < r.span; i += nt) {
     const int ll = r.hand0 + i;  // span <= min(1024, L)
     const int l = ll >= a.L ? ll - a.L : ll;
     bool keep = l == h0 || l == h1;
@@ -171,16 +160,16 @@ __device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const Re
     a.ref[l] = keep ? 1 : 0;
   }
   auto outside = [&](int l) {  // set bits of lines the window loop does not touch
-    int64_t off = (int64_t)l - r.hand0;
+    int off = l - r.hand0;
     if (off < 0) off += a.L;
     return off >= r.span;
   };
-  if (tid < 2) {
-    const int l = tid == 0 ? h0 : h1;
+  if (ct == 1 || ct == 2) {
+    const int l = ct == 1 ? h0 : h1;
     if (l >= 0 && outside(l)) a.ref[l] = 1;
   }
-  if (tid >= 64 && tid < 64 + n) {
-    const int q = tid - 64;
+  if (ct >= 16 && ct < 16 + n) {
+    const int q = ct - 16;
     const int l = rl.line[q], k = rl.key[q], o = rl.old[q];
     if (o >= 0) a.slot_of[o] = -1;
     a.key_of[l] = k;
@@ -196,6 +185,25 @@ __device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const Re
   }
 }
 
+// lanes holding the t smallest of the wave's values among `valid` lanes
+// (values unique): MSB-first radix select on ballots, uniform SALU control
+__device__ __forceinline__ uint64_t wave_smallest(uint64_t v, int t, uint64_t valid) {
+  uint64_t chosen = 0, active = valid;
+  int need = t;
+  for (int bit = 63; bit >= 0 && need > 0 && active; --bit) {
+    const uint64_t zero = __ballot(((v >> bit) & 1ull) == 0ull) & active;
+    const int nz = __popcll(zero);
+    if (nz <= need) {
+      chosen |= zero;
+      need -= nz;
+      active &= ~zero;
+    } else {
+      active = zero;
+    }
+  }
+  return chosen;
+}
+
 __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
                                                                       const uint64_t* __restrict__ p_in,
                                                                       uint64_t* __restrict__ p_out,
@@ -204,9 +212,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   extern __shared__ __attribute__((aligned(16))) float wsm[];  // [kNQ][dp+4] query vectors
   __shared__ uint64_t kscr[8];
   __shared__ int kscan[kFusedThreads / 64];
-  __shared__ int s_ord[2 * kNQ];
   __shared__ Plan pl;
+  __shared__ RecLds rl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool committer = blockIdx.x == a.fused_G - 1;  // fewest rows
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
   const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
   const int64_t j0 = row0 + tid;
@@ -218,7 +227,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     y0 = a.y[a.off + j0];
   }
   const FusedCacheRec& rin = *r_in;  // read through the scalar cache (never written this launch)
-  __shared__ RecLds rl;
   if (tid < 5 * kNQ) {
     const int arr = tid / kNQ, q = tid - arr * kNQ;
     const int32_t* src = arr == 0 ? rin.key : arr == 1 ? rin.old : arr == 2 ? rin.line : arr == 3 ? rin.hline : rin.hold;
@@ -227,8 +235,9 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   }
   const View view{a, rl, rin.n_new, rin.hit_line[0], rin.hit_line[1], rin.hand0, rin.span};
   // diagnostics only (a.stamps == nullptr in normal runs): 0 entry, 1 alpha
-  // update, 2 rows chosen, 3 victims, 4 plan done, 5 lines filled, 6 commit, 7 end
-  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+  // update, 8 need rows, 9/10 speculation, 2 rows chosen, 3 victims, 4 plan
+  // done, 5 lines filled, 6 commit, 7 end
+  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || committer);
   const uint64_t ts_entry = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
   const int it_st = rin.iter;
   auto stamp = [&](int slot) {
@@ -237,18 +246,52 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
           slot == 0 ? ts_entry : __builtin_amdgcn_s_memrealtime();
   };
 
-  // ---- 1. pair (every wave), alpha update ----
-  uint64_t kh = kKeyNone, kl = kKeyNone;
+  // ---- 0. everything that does not depend on this iteration's pair, in flight
+  //         together: the previous launch's keys (pair + speculation
+  //         candidates), the CLOCK window's bits and owners, candidate slots ----
   const u64x2l* pk = (const u64x2l*)p_in;
-  for (int b = lane; b < a.fused_G; b += 64) {
-    const u64x2l v = pk[b];
-    kh = v.x < kh ? v.x : kh;
-    kl = v.y < kl ? v.y : kl;
+  uint64_t cand[8];  // [2i] up side, [2i+1] low side of workgroup lane + 64 i (fused_G <= 256)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = lane + 64 * i;
+    cand[2 * i] = kKeyNone;
+    cand[2 * i + 1] = kKeyNone;
+    if (b < a.fused_G) {
+      const u64x2l v = pk[b];
+      cand[2 * i] = v.x;
+      cand[2 * i + 1] = v.y;
+    }
   }
-  __syncthreads();  // staged record visible (the key loads above are in flight meanwhile)
+  const int W = min(1024, a.L), hand = rin.hand;
+  int wp[4], wref[4], wkey[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pos = 4 * tid + j;
+    const int pp = hand + pos;  // hand < L; only pos < W <= L is used
+    wp[j] = pp >= a.L ? pp - a.L : pp;
+    wref[j] = 1;
+    wkey[j] = -1;
+    if (pos < W) {
+      wref[j] = a.ref[wp[j]];
+      wkey[j] = a.key_of[wp[j]];
+    }
+  }
+  int cidx[8], cmem[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    cidx[i] = cand[i] != kKeyNone ? (int)key_index(cand[i]) : 0;
+    cmem[i] = wave == 0 ? a.slot_of[cidx[i]] : -1;
+  }
+  uint64_t kh = kKeyNone, kl = kKeyNone;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    kh = cand[2 * i] < kh ? cand[2 * i] : kh;
+    kl = cand[2 * i + 1] < kl ? cand[2 * i + 1] : kl;
+  }
+  __syncthreads();  // staged record visible
   if (rin.done != kRunning) {
-    if (blockIdx.x == a.fused_G - 1) {
-      commit_record(a, rin, rl);
+    if (committer) {
+      commit_record(a, rin, rl, tid, kFusedThreads);
       if (tid == 0) {
         FusedCacheRec o = rin;
         o.i_hi = o.i_lo = -1;
@@ -261,11 +304,15 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     }
     return;
   }
+
+  // ---- 1. pair (every wave), alpha update ----
   kh = wave_min_u64(kh);
   kl = wave_min_u64(kl);
   const bool nopair = kh == kKeyNone || kl == kKeyNone;
   const int i_hi = nopair ? 0 : (int)key_index(kh), i_lo = nopair ? 0 : (int)key_index(kl);
   const float b_hi = key_value(kh), b_lo = -key_value(kl);
+  // the f update may need either row: their slots load with the sample rows
+  const int s_hi = a.slot_of[i_hi], s_lo = a.slot_of[i_lo];
   int done = kRunning;
   float c_hi = 0.f, c_lo = 0.f, a_hi_new = 0.f, a_lo_new = 0.f;
   const int iter = rin.iter + 1;
@@ -295,23 +342,21 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       else if (iter >= a.max_iter) done = kMaxIter;
     }
   }
-
   stamp(0);
   stamp(1);
+
   // ---- 2. cache plan (identical in every workgroup) ----
-  // 2a. rows the f update needs and their lines (every thread, uniform), then
-  //     speculative rows (wave 0): the best uncached workgroup winners of
-  //     each side (best per lane, ranked by a readlane sweep), interleaved hi/lo
+  // 2a. rows the f update needs and their lines (uniform), then speculative
+  //     rows (wave 0): the best uncached workgroup winners, t per side by a
+  //     ballot radix select.  Meanwhile waves 1-3 of the committing workgroup
+  //     apply the previous record.
   const int need_hi = c_hi != 0.f ? i_hi : -1;
   const int need_lo = (c_lo != 0.f && !(i_lo == i_hi && c_hi != 0.f)) ? i_lo : -1;
-  int hit_hi, hit_lo;
-  {
-    const int s_hi = a.slot_of[max(need_hi, 0)], s_lo = a.slot_of[max(need_lo, 0)];  // both in flight
-    hit_hi = need_hi >= 0 ? view.slot_fix(need_hi, s_hi) : -1;
-    hit_lo = need_lo >= 0 ? view.slot_fix(need_lo, s_lo) : -1;
-  }
+  const int hit_hi = need_hi >= 0 ? view.slot_fix(need_hi, s_hi) : -1;
+  const int hit_lo = need_lo >= 0 ? view.slot_fix(need_lo, s_lo) : -1;
   const int miss_hi = need_hi >= 0 && hit_hi < 0, miss_lo = need_lo >= 0 && hit_lo < 0;
   const int n_miss = miss_hi + miss_lo;
+  stamp(8);
   const int budget = n_miss > 0 ? min(min(a.spec, kNQ - n_miss), max(0, a.L / 2 - n_miss)) : 0;
   if (tid == 0) {
     pl.key[0] = miss_hi ? need_hi : need_lo;  // misses first (hi before lo)
@@ -325,93 +370,52 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     pl.miss_hi = miss_hi;
     pl.span = 0;
   }
+  if (committer && wave > 0) commit_record(a, rin, rl, tid - 64, kFusedThreads - 64);
   if (budget > 0 && wave == 0) {  // uniform
-    // lane holds workgroups lane + 64 i (i < 4) per side; filter, keep the lane's best
-    uint64_t ch = kKeyNone, cl = kKeyNone;
-    {
-      uint64_t cand[8];
-      int cidx[8], cmem[8];
+    uint64_t ch = kKeyNone, cl = kKeyNone;  // lane's best uncached candidate per side
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = lane + 64 * i;
-        cand[2 * i] = kKeyNone;
-        cand[2 * i + 1] = kKeyNone;
-        if (b < a.fused_G) {
-          const u64x2l v = pk[b];
-          cand[2 * i] = v.x;
-          cand[2 * i + 1] = v.y;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) cidx[i] = cand[i] != kKeyNone ? (int)key_index(cand[i]) : 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) cmem[i] = a.slot_of[cidx[i]];  // 8 loads in flight
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int idx = cidx[i];
-        if (idx == i_hi || idx == i_lo || view.slot_fix(idx, cmem[i]) >= 0) cand[i] = kKeyNone;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ch = cand[2 * i] < ch ? cand[2 * i] : ch;
-        cl = cand[2 * i + 1] < cl ? cand[2 * i + 1] : cl;
-      }
+    for (int i = 0; i < 8; ++i) {
+      const int idx = cidx[i];
+      const bool ok = cand[i] != kKeyNone && idx != i_hi && idx != i_lo && view.slot_fix(idx, cmem[i]) < 0;
+      if (ok && (i & 1) == 0) ch = cand[i] < ch ? cand[i] : ch;
+      if (ok && (i & 1) == 1) cl = cand[i] < cl ? cand[i] : cl;
     }
-    // rank of the lane's best among the 64 lane bests (readlane sweep: VALU/SALU
-    // only, no LDS traffic and no serial reduction rounds)
-    int rh = 0, rl = 0, vh = 0, vl = 0;
-    for (int src = 0; src < 64; ++src) {
-      const uint64_t oh = readlane_u64(ch, src), ol = readlane_u64(cl, src);
-      rh += oh < ch;
-      rl += ol < cl;
-      vh += oh != kKeyNone;
-      vl += ol != kKeyNone;
-    }
+    stamp(9);
+    const uint64_t valid_h = __ballot(ch != kKeyNone), valid_l = __ballot(cl != kKeyNone);
+    const int vh = __popcll(valid_h), vl = __popcll(valid_l);
     int take_h = min(vh, (budget + 1) / 2);
     const int take_l = min(vl, budget - take_h);
     take_h = min(vh, budget - take_l);  // an exhausted low side leaves room
-    if (lane < 2 * kNQ) s_ord[lane] = -1;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int ih = ch != kKeyNone ? (int)key_index(ch) : -1;
-    const int il = cl != kKeyNone ? (int)key_index(cl) : -1;
-    if (ih >= 0 && rh < take_h) s_ord[2 * rh] = ih;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (il >= 0 && rl < take_l) {
-      bool dup = false;  // a free SV can win on both sides: keep one copy
-      for (int q = 0; q < take_h; ++q) dup |= s_ord[2 * q] == il;
-      if (!dup) s_ord[2 * rl + 1] = il;
+    const uint64_t sel_h = wave_smallest(ch, take_h, valid_h);
+    uint64_t sel_l = wave_smallest(cl, take_l, valid_l);
+    const int ih = (int)key_index(ch), il = (int)key_index(cl);
+    // a free SV can win on both sides: keep one copy
+    bool dup = false;
+    for (uint64_t m = sel_h; m; m &= m - 1) {
+      const int src = __ffsll((unsigned long long)m) - 1;
+      dup |= __builtin_amdgcn_readlane(ih, src) == il;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int v = lane < 2 * kNQ ? s_ord[lane] : -1;
-    const uint64_t m = __ballot(v >= 0);
-    const int pos = n_miss + __popcll(m & ((1ull << lane) - 1ull));
-    if (v >= 0) pl.key[pos] = v;  // take_h + take_l <= budget <= kNQ - n_miss
-    if (lane == 0) pl.n_new = n_miss + __popcll(m);
+    sel_l &= ~__ballot(dup);
+    stamp(10);
+    const uint64_t below = (1ull << lane) - 1ull;
+    if ((sel_h >> lane) & 1ull) pl.key[n_miss + __popcll(sel_h & below)] = ih;
+    if ((sel_l >> lane) & 1ull) pl.key[n_miss + __popcll(sel_h) + __popcll(sel_l & below)] = il;
+    if (lane == 0) pl.n_new = n_miss + __popcll(sel_h) + __popcll(sel_l);
   }
   __syncthreads();
   stamp(2);
 
-  // 2b. all waves: CLOCK victim scan of a window of up to 1024 lines from the
-  //     hand, 4 consecutive positions per thread, one block-wide rank
+  // 2b. all waves: CLOCK victim scan of the window (prefetched bits), 4
+  //     consecutive positions per thread, one block-wide rank
   const int M = pl.n_new;  // uniform
   if (M > 0) {
-    const int hand = rin.hand;
-    const int W = min(1024, a.L);
     const int pin0 = pl.hit_hi, pin1 = pl.hit_lo;
-    int p[4];
-    bool e[4];
-    bool unp[4];
+    bool e[4], unp[4];
     int cnt = 0, cnt2 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int pos = 4 * tid + j;
-      const int pp = hand + pos;  // hand < L; only pos < W <= L is used
-      p[j] = pp >= a.L ? pp - a.L : pp;
-      unp[j] = pos < W && p[j] != pin0 && p[j] != pin1;
-      e[j] = unp[j] && view.ref(p[j]) == 0;
+      unp[j] = 4 * tid + j < W && wp[j] != pin0 && wp[j] != pin1;
+      e[j] = unp[j] && view.ref_fix(wp[j], wref[j]) == 0;
       cnt += e[j];
       cnt2 += unp[j] && !e[j];
     }
@@ -420,7 +424,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (e[j]) {
-        if (r < M) pl.line[r] = p[j];
+        if (r < M) {
+          pl.line[r] = wp[j];
+          pl.old[r] = view.key_fix(wp[j], wkey[j]);
+        }
         if (r == M - 1) pl.span = 4 * tid + j + 1;  // second chances consumed up to here
         ++r;
       }
@@ -431,7 +438,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (unp[j] && !e[j]) {
-          if (total + r2 < M) pl.line[total + r2] = p[j];
+          if (total + r2 < M) {
+            pl.line[total + r2] = wp[j];
+            pl.old[total + r2] = view.key_fix(wp[j], wkey[j]);
+          }
           ++r2;
         }
       }
@@ -441,13 +451,13 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   }
 
   stamp(3);
-  // 2c. wave 0: victims' rows, host-tier fetch / spill (lane q <-> new line q)
+  // 2c. wave 0: host-tier fetch / spill (lane q <-> new line q), f-update lines
   if (wave == 0) {
     int my_key = -1, my_line = -1, my_old = -1, my_hsrc = -1;
     if (lane < M) {
       my_key = pl.key[lane];
       my_line = pl.line[lane];
-      my_old = view.key_of(my_line);
+      my_old = pl.old[lane];
       my_hsrc = view.hslot(my_key);
     }
     const bool want_spill = lane < M && a.H > 0 && my_old >= 0 && view.hslot(my_old) < 0;
@@ -465,7 +475,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     const int n_spill_used = __popcll(__ballot(my_hline >= 0));
     const int line0 = __shfl(my_line, 0, 64), line1 = __shfl(my_line, 1, 64);
     if (lane < M) {
-      pl.old[lane] = my_old;
       pl.op[lane] = my_hsrc >= 0 ? kOpFetch : kOpCompute;
       pl.hsrc[lane] = my_hsrc;
       pl.hline[lane] = my_hline;
@@ -475,11 +484,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       pl.n_fetch = n_fetch;
       pl.n_compute = M - n_fetch;
       pl.n_spill = n_spill_used;
-      const int hit_hi = pl.hit_hi, hit_lo = pl.hit_lo;
-      pl.line_hi = pl.need_hi >= 0 ? (hit_hi >= 0 ? hit_hi : line0) : -1;
+      pl.line_hi = need_hi >= 0 ? (hit_hi >= 0 ? hit_hi : line0) : -1;
       if (c_lo != 0.f) {
         if (i_lo == i_hi && c_hi != 0.f) pl.line_lo = pl.line_hi;
-        else pl.line_lo = hit_lo >= 0 ? hit_lo : (pl.miss_hi ? line1 : line0);
+        else pl.line_lo = hit_lo >= 0 ? hit_lo : (miss_hi ? line1 : line0);
       } else {
         pl.line_lo = -1;
       }
@@ -611,9 +619,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   }
 
   stamp(5);
-  // ---- 5. (last workgroup: fewest rows) commit the previous record, publish this one ----
-  if (blockIdx.x == a.fused_G - 1) {
-    commit_record(a, rin, rl);
+  // ---- 5. (last workgroup: fewest rows) publish this iteration's record ----
+  if (committer) {
     const bool upd = done != kNonFinite && done != kNoPair;
     if (tid < kNQ) {
       const int q = tid;
