@@ -38,10 +38,15 @@ typedef unsigned long long u64x2l __attribute__((ext_vector_type(2)));
 // lookup is branch-free with the memory load issued first: lookups sit on the
 // serial critical path of every iteration.  Keys and evicted rows of one
 // record are disjoint, lines are distinct, so at most one entry matches.
-struct RecLds {
+struct alignas(16) RecLds {
   int key[kNQ], old[kNQ], line[kNQ], hline[kNQ], hold[kNQ];
 };
 
+typedef int i4 __attribute__((ext_vector_type(4)));
+
+// Lookups read the staged arrays as unconditional 16-B vectors (loop-invariant,
+// hoisted by the compiler) and mask entries >= n with selects: no branch ever
+// waits on an LDS round trip inside the loop.
 struct View {
   const SmoArgs& a;
   const RecLds& r;
@@ -49,18 +54,24 @@ struct View {
   // *_fix(x, v): v = the memory value for x, corrected by the pending record
   __device__ int slot_fix(int k, int v) const {
 #pragma unroll
-    for (int q = 0; q < kNQ; ++q) {
-      if (q < n) {
-        v = r.key[q] == k ? r.line[q] : v;
-        v = r.old[q] == k ? -1 : v;
+    for (int q4 = 0; q4 < kNQ; q4 += 4) {
+      const i4 kk = *(const i4*)&r.key[q4], oo = *(const i4*)&r.old[q4], ll = *(const i4*)&r.line[q4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool in = q4 + c < n;
+        v = (in && kk[c] == k) ? ll[c] : v;
+        v = (in && oo[c] == k) ? -1 : v;
       }
     }
     return v;
   }
   __device__ int key_fix(int l, int v) const {
 #pragma unroll
-    for (int q = 0; q < kNQ; ++q)
-      if (q < n) v = r.line[q] == l ? r.key[q] : v;
+    for (int q4 = 0; q4 < kNQ; q4 += 4) {
+      const i4 kk = *(const i4*)&r.key[q4], ll = *(const i4*)&r.line[q4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v = (q4 + c < n && ll[c] == l) ? kk[c] : v;
+    }
     return v;
   }
   __device__ int ref_fix(int l, int v) const {
@@ -71,24 +82,33 @@ struct View {
     }
     if (l == hit0 || l == hit1) v = 1;
 #pragma unroll
-    for (int q = 0; q < kNQ; ++q)
-      if (q < n) v = r.line[q] == l ? 1 : v;
+    for (int q4 = 0; q4 < kNQ; q4 += 4) {
+      const i4 ll = *(const i4*)&r.line[q4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v = (q4 + c < n && ll[c] == l) ? 1 : v;
+    }
     return v;
   }
   __device__ int hslot_fix(int k, int v) const {
 #pragma unroll
-    for (int q = 0; q < kNQ; ++q) {
-      if (q < n && r.hline[q] >= 0) {
-        v = r.old[q] == k ? r.hline[q] : v;
-        v = r.hold[q] == k ? -1 : v;
+    for (int q4 = 0; q4 < kNQ; q4 += 4) {
+      const i4 hl = *(const i4*)&r.hline[q4], oo = *(const i4*)&r.old[q4], ho = *(const i4*)&r.hold[q4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool in = q4 + c < n && hl[c] >= 0;
+        v = (in && oo[c] == k) ? hl[c] : v;
+        v = (in && ho[c] == k) ? -1 : v;
       }
     }
     return v;
   }
   __device__ int hkey_fix(int h, int v) const {
 #pragma unroll
-    for (int q = 0; q < kNQ; ++q)
-      if (q < n) v = r.hline[q] == h ? r.old[q] : v;
+    for (int q4 = 0; q4 < kNQ; q4 += 4) {
+      const i4 hl = *(const i4*)&r.hline[q4], oo = *(const i4*)&r.old[q4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v = (q4 + c < n && hl[c] == h) ? oo[c] : v;
+    }
     return v;
   }
   __device__ int hslot(int k) const { return a.H == 0 ? -1 : hslot_fix(k, a.hslot_of[k]); }
@@ -156,7 +176,11 @@ __device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const Re
     const int l = ll >= a.L ? ll - a.L : ll;
     bool keep = l == h0 || l == h1;
 #pragma unroll
-    for (int q = 0; q < kNQ; ++q) keep |= q < n && rl.line[q] == l;
+    for (int q4 = 0; q4 < kNQ; q4 += 4) {
+      const i4 ll = *(const i4*)&rl.line[q4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) keep |= q4 + c < n && ll[c] == l;
+    }
     a.ref[l] = keep ? 1 : 0;
   }
   auto outside = [&](int l) {  // set bits of lines the window loop does not touch
