@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--x-mode", default="auto")
     ap.add_argument("--graph-block", type=int, default=64)
     ap.add_argument("--comm", default="auto", help="auto | rccl | gloo")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "allreduce", "peer"],
+                    help="per-iteration key exchange of the dense mode (auto: in-kernel xGMI peer exchange "
+                         "when its self test passes, else the communicator all-reduce)")
     ap.add_argument("--device", default="auto", help="auto | cuda | cpu")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--json-out", default=None)
@@ -94,7 +97,8 @@ def main(argv=None) -> int:
 
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
     cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines,
-                    x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines)
+                    x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
+                    exchange=a.exchange)
     params = cfg.to_native(X.shape[1])
     comm = make_comm(ctx, a.comm)
     if a.comm == "rccl" and n_ranks == 1:
@@ -176,6 +180,7 @@ def main(argv=None) -> int:
             "iteration": info.get("iteration", "cpu"),
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
+            "exchange": info.get("exchange", "none"),
             "preset": a.config,
         }
         line = json.dumps(out)

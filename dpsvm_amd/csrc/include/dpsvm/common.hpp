@@ -75,6 +75,11 @@ struct SolverParams {
   // debugging
   bool sync_debug = false;    // device sync + error check after every launch
   bool force_collectives = false;  // run the per-iteration collective even at world 1 (tests RCCL/graph paths)
+  // per-iteration key exchange of the dense fused mode: 0 auto (peer exchange
+  // when world > 1 and its self test passes, else the communicator's
+  // all-reduce), 1 communicator all-reduce, 2 peer exchange (required; also
+  // at world 1 as a loopback, for tests)
+  int exchange = 0;
 };
 
 // Per-run result, gathered on every rank.

@@ -35,6 +35,7 @@ enum DoneCode : int32_t {
   kMaxIter = 2,
   kNoPair = 3,
   kNonFinite = 4,
+  kCommFail = 5,   // peer exchange gave up waiting (a rank stopped or diverged)
 };
 
 // Written by smo_finalize, read by the next iteration's kernels.
@@ -148,7 +149,17 @@ struct SmoArgs {
   // diagnostics (DPSVM_STAMPS): s_memrealtime stamps of workgroups 0 and G-1,
   // ring of kStampRing iterations x 2 workgroups x kStampSlots
   uint64_t* stamps;
+  // peer exchange (dense fused mode, xworld > 0): every workgroup pushes its
+  // two selection keys as tagged granules straight into every rank's receive
+  // buffer (xGMI peer stores); the next launch polls its own buffer until all
+  // tags match.  Layout per rank: [2 parity][xworld * fused_G][4] u64,
+  // granule = tag << 32 | 32-bit half of a key.  Replaces the per-iteration
+  // all-reduce (no collective launch, no host involvement).
+  uint64_t* const* xpeer;  // [xworld] receive buffers (device-accessible)
+  int32_t xrank, xworld;
+  int64_t xtimeout_ticks;  // give-up bound of one poll loop (s_memrealtime, 100 MHz)
 };
+constexpr int kXchGranules = 4;  // per workgroup entry: hi key (2 halves), lo key (2 halves)
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;
 

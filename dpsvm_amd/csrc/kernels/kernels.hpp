@@ -25,9 +25,15 @@ bool smo_fused_lru_supported(int dp);
 size_t smo_fused_lru_lds_bytes(int dp);
 void smo_fused_lru(const SmoArgs& a, const uint64_t* p_in, uint64_t* p_out, const FusedCacheRec* r_in,
                    FusedCacheRec* r_out, hipStream_t s);
-// dense mode: init (selection only, mode 0) or one fused SMO iteration (mode 1)
+// dense mode: init (selection only, mode 0) or one fused SMO iteration (mode 1);
+// xpar: peer-exchange parity this launch publishes (a.xworld > 0)
 void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out, const FusedRec* r_in,
-               FusedRec* r_out, hipStream_t s);
+               FusedRec* r_out, hipStream_t s, int xpar = 0);
+// peer-exchange self test: every rank pushes a tagged granule to every rank and
+// polls its own; *ok = 1 when all arrived within timeout_ticks
+//   (ping slots at u64 offset ping_off of every receive buffer)
+void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uint32_t tag, int64_t timeout_ticks,
+              int32_t* ok, hipStream_t s);
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)

@@ -25,6 +25,7 @@
 #include "dpsvm/device_state.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
+#include "xch.hpp"
 #include "../runtime/hip_check.hpp"
 
 namespace dpsvm {
@@ -48,8 +49,10 @@ __device__ __forceinline__ void commit_pending(const SmoArgs& a, const FusedRec&
   }
 }
 
-// per-workgroup min of two keys -> p_out[blockIdx] (the kernel's one barrier)
-__device__ __forceinline__ void store_block_keys(uint64_t kh, uint64_t kl, uint64_t* p_out, uint64_t* scr) {
+// per-workgroup min of two keys -> p_out[blockIdx], or pushed to every rank
+// (peer exchange, parity xpar, tag) (the kernel's one barrier)
+__device__ __forceinline__ void store_block_keys(const SmoArgs& a, uint64_t kh, uint64_t kl, uint64_t* p_out,
+                                                 uint64_t* scr, int xpar, uint32_t tag) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   kh = wave_min_u64(kh);
   kl = wave_min_u64(kl);
@@ -58,6 +61,17 @@ __device__ __forceinline__ void store_block_keys(uint64_t kh, uint64_t kl, uint6
     scr[4 + wave] = kl;
   }
   __syncthreads();
+  if (a.xworld > 0) {
+    if (wave == 0) {
+#pragma unroll
+      for (int w = 1; w < kFusedThreads / 64; ++w) {
+        kh = scr[w] < kh ? scr[w] : kh;
+        kl = scr[4 + w] < kl ? scr[4 + w] : kl;
+      }
+      xch_push(a, xpar, blockIdx.x, kh, kl, tag, lane);
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int w = 1; w < kFusedThreads / 64; ++w) {
@@ -75,7 +89,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
                                                                   const uint64_t* __restrict__ p_in,
                                                                   uint64_t* __restrict__ p_out,
                                                                   const FusedRec* __restrict__ r_in,
-                                                                  FusedRec* __restrict__ r_out) {
+                                                                  FusedRec* __restrict__ r_out, int xpar) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -111,7 +125,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); kh = k < kh ? k : kh; }
       if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); kl = k < kl ? k : kl; }
     }
-    store_block_keys(kh, kl, p_out, kscr);
+    // peer exchange: the seed's keys carry tag iter0 + 1 (r_in = the seed record)
+    store_block_keys(a, kh, kl, p_out, kscr, xpar, a.xworld > 0 ? (uint32_t)r_in->iter + 1u : 0u);
     return;
   }
 
@@ -119,10 +134,24 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   // ---- 1. global pair: every wave reduces all workgroup keys (16-B loads) ----
   uint64_t kh = kKeyNone, kl = kKeyNone;
   const u64x2* pk = (const u64x2*)p_in;
-  for (int b = lane; b < a.fused_G; b += 64) {
-    const u64x2 v = pk[b];
-    kh = v.x < kh ? v.x : kh;
-    kl = v.y < kl ? v.y : kl;
+  if (a.xworld == 0) {
+    for (int b = lane; b < a.fused_G; b += 64) {
+      const u64x2 v = pk[b];
+      kh = v.x < kh ? v.x : kh;
+      kl = v.y < kl ? v.y : kl;
+    }
+  }
+  if (rin.done == kRunning && a.xworld > 0 && !xch_pull(a, xpar ^ 1, (uint32_t)rin.iter + 1u, kh, kl, lane)) {
+    // a peer stopped publishing: give up (every rank that times out stops the same way)
+    if (lead) {
+      commit_pending(a, rin);
+      FusedRec o = rin;
+      o.i_hi = o.i_lo = -1;
+      o.done = kCommFail;
+      *r_out = o;
+      publish_status(a.status, rin.iter, kCommFail, rin.b_hi, rin.b_lo);
+    }
+    return;
   }
   if (rin.done != kRunning) {
     if (lead) {
@@ -235,17 +264,43 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   }
   stamp(rin.iter, 3, 0);
   if (done != kRunning) return;  // uniform
-  store_block_keys(nh, nlk, p_out, kscr);
+  store_block_keys(a, nh, nlk, p_out, kscr, xpar, (uint32_t)iter + 1u);
   stamp(rin.iter, 4, 0);
+}
+
+__global__ __launch_bounds__(64) void xch_ping_kernel(uint64_t* const* peers, int rank, int world, int64_t ping_off,
+                                                       uint32_t tag, int64_t timeout_ticks, int32_t* ok) {
+  const int lane = threadIdx.x;
+  if (lane < world) xch_store(peers[lane] + ping_off + rank, ((uint64_t)tag << 32) | (uint32_t)rank);
+  const uint64_t* mine = peers[rank] + ping_off;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    const bool good = lane >= world || (uint32_t)(xch_load(mine + lane) >> 32) == tag;
+    if (__all(good)) {
+      if (lane == 0) *ok = 1;
+      return;
+    }
+    if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > timeout_ticks) {
+      if (lane == 0) *ok = 0;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 }  // namespace dev
 
 namespace launch {
 
+void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uint32_t tag, int64_t timeout_ticks,
+              int32_t* ok, hipStream_t s) {
+  dev::xch_ping_kernel<<<1, 64, 0, s>>>(peers, rank, world, ping_off, tag, timeout_ticks, ok);
+  post_launch("xch_ping", s);
+}
+
 void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out, const FusedRec* r_in,
-               FusedRec* r_out, hipStream_t s) {
-  dev::smo_fused_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out);
+               FusedRec* r_out, hipStream_t s, int xpar) {
+  dev::smo_fused_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out, xpar);
   post_launch("smo_fused", s);
 }
 

@@ -264,10 +264,19 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || committer);
   const uint64_t ts_entry = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
   const int it_st = rin.iter;
+  // stamps collect in LDS and are flushed once at the end (a global store
+  // mid-kernel would add its completion wait to the next vmcnt(0))
+  __shared__ uint64_t st_lds[kStampSlots];
   auto stamp = [&](int slot) {
-    if (stamping)
-      a.stamps[((size_t)(it_st % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots + slot] =
-          slot == 0 ? ts_entry : __builtin_amdgcn_s_memrealtime();
+    if (stamping) {
+      if (slot == 0)
+        for (int i = 1; i < kStampSlots; ++i) st_lds[i] = 0;
+      st_lds[slot] = slot == 0 ? ts_entry : __builtin_amdgcn_s_memrealtime();
+      if (slot == 7) {
+        uint64_t* dst = a.stamps + ((size_t)(it_st % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots;
+        for (int i = 0; i < kStampSlots; ++i) dst[i] = st_lds[i];
+      }
+    }
   };
 
   // ---- 0. everything that does not depend on this iteration's pair, in flight
@@ -306,6 +315,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
     cidx[i] = cand[i] != kKeyNone ? (int)key_index(cand[i]) : 0;
     cmem[i] = wave == 0 ? a.slot_of[cidx[i]] : -1;
   }
+  __builtin_amdgcn_sched_barrier(0);  // keep the prefetches here (the scheduler sinks loads to their uses)
   uint64_t kh = kKeyNone, kl = kKeyNone;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -337,6 +347,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   const float b_hi = key_value(kh), b_lo = -key_value(kl);
   // the f update may need either row: their slots load with the sample rows
   const int s_hi = a.slot_of[i_hi], s_lo = a.slot_of[i_lo];
+  __builtin_amdgcn_sched_barrier(0);
   int done = kRunning;
   float c_hi = 0.f, c_lo = 0.f, a_hi_new = 0.f, a_lo_new = 0.f;
   const int iter = rin.iter + 1;

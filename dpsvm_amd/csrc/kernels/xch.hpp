@@ -1,0 +1,82 @@
+// Peer exchange of per-workgroup selection keys (dense fused mode, world > 1):
+// the in-kernel replacement of the per-iteration all-reduce.
+//
+// Each workgroup of launch t pushes its (up, low) keys to every rank as four
+// 8-byte granules {tag, 32-bit half} with system-scope relaxed stores (one
+// aligned store per granule: never torn; the data IS the flag, no fence).
+// Launch t+1 on every rank polls its own receive buffer with system-scope
+// loads until every granule of the parity carries the expected tag, then
+// reduces exactly as from an all-reduced buffer — so every rank derives the
+// same pair.  Tags are the iteration count + 1 (never 0; buffers are zeroed
+// before each solve), parities alternate, and a rank cannot lap a peer: its
+// launch t+2 needs that peer's launch-t+1 keys, which the peer publishes only
+// after it has read the parity t+2 overwrites.
+// Reference: one 16-byte MPI Allgather per iteration (svmTrainMain.cpp:244).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+__device__ __forceinline__ uint64_t* xch_entry(uint64_t* base, int par, const SmoArgs& a, int rank, int b) {
+  return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * kXchGranules;
+}
+
+__device__ __forceinline__ void xch_store(uint64_t* g, uint64_t v) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ uint64_t xch_load(const uint64_t* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// lane p < xworld pushes workgroup b's keys to rank p (parity par)
+__device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, uint64_t kh, uint64_t kl, uint32_t tag,
+                                         int lane) {
+  if (lane < a.xworld) {
+    uint64_t* g = xch_entry(a.xpeer[lane], par, a, a.xrank, b);
+    const uint64_t t = (uint64_t)tag << 32;
+    xch_store(g + 0, t | (kh >> 32));
+    xch_store(g + 1, t | (kh & 0xffffffffull));
+    xch_store(g + 2, t | (kl >> 32));
+    xch_store(g + 3, t | (kl & 0xffffffffull));
+  }
+}
+
+// every lane of the calling wave: min keys over all ranks' workgroups of
+// parity par, polling until every granule carries `tag`; false on give-up
+__device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
+                                         int lane) {
+  const int E = a.xworld * a.fused_G;
+  const uint64_t* base = a.xpeer[a.xrank] + (int64_t)par * E * kXchGranules;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    uint64_t h = kKeyNone, l = kKeyNone;
+    bool ok = true;
+    for (int e = lane; e < E; e += 64) {
+      const uint64_t* g = base + (int64_t)e * kXchGranules;
+      const uint64_t g0 = xch_load(g), g1 = xch_load(g + 1), g2 = xch_load(g + 2), g3 = xch_load(g + 3);
+      ok &= (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag && (uint32_t)(g2 >> 32) == tag &&
+            (uint32_t)(g3 >> 32) == tag;
+      const uint64_t vh = (g0 << 32) | (g1 & 0xffffffffull), vl = (g2 << 32) | (g3 & 0xffffffffull);
+      h = vh < h ? vh : h;
+      l = vl < l ? vl : l;
+    }
+    if (__all(ok)) {
+      kh = h;
+      kl = l;
+      return true;
+    }
+    if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+}  // namespace dev
+}  // namespace dpsvm

@@ -160,7 +160,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("checkpoint_every", &SolverParams::checkpoint_every)
       .def_readwrite("checkpoint_path", &SolverParams::checkpoint_path)
       .def_readwrite("sync_debug", &SolverParams::sync_debug)
-      .def_readwrite("force_collectives", &SolverParams::force_collectives);
+      .def_readwrite("force_collectives", &SolverParams::force_collectives)
+      .def_readwrite("exchange", &SolverParams::exchange);
 
   py::class_<Checkpoint>(m, "Checkpoint")
       .def(py::init<>())
@@ -323,6 +324,7 @@ PYBIND11_MODULE(_C, m) {
         d["dp"] = i.dp;
         d["x_replicated"] = i.x_replicated;
         d["iteration"] = i.iteration;
+        d["exchange"] = i.exchange;
         d["cache_lines"] = i.cache_lines;
         d["blocks"] = i.blocks;
         d["bytes_device"] = i.bytes_device;

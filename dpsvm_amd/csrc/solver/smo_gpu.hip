@@ -23,6 +23,8 @@
 #include <atomic>
 #include <thread>
 
+#include <unistd.h>
+
 #include "dpsvm/device_state.hpp"
 #include "dpsvm/solver.hpp"
 #include "../kernels/kernels.hpp"
@@ -80,6 +82,13 @@ struct GpuSolver::Impl {
   uint64_t* pf = nullptr;  // dense fused mode: two partial buffers [2][2*Gf]
   FusedRec* rf = nullptr;  // dense fused mode: two records
   FusedCacheRec* rcf = nullptr;  // fused cache mode: two records
+  // peer exchange (dense fused mode): own receive buffer (own allocation, IPC
+  // exported), device table of every rank's buffer, IPC mappings to close
+  bool xch = false;
+  uint64_t* xbuf = nullptr;
+  uint64_t** xpeer_d = nullptr;
+  int64_t xregion = 0;  // u64 words of the two key parities (zeroed per solve)
+  std::vector<void*> xopened;
   int64_t Gf = 0, RBf = 0;
   uint64_t* stamps = nullptr;  // DPSVM_STAMPS diagnostics
   std::string stamps_path;
@@ -101,6 +110,9 @@ struct GpuSolver::Impl {
 
   ~Impl() {
     if (device >= 0) (void)hipSetDevice(device);
+    for (void* q : xopened) (void)hipIpcCloseMemHandle(q);
+    if (xbuf) (void)hipFree(xbuf);
+    if (xpeer_d) (void)hipFree(xpeer_d);
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
     for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines,
@@ -144,8 +156,8 @@ struct GpuSolver::Impl {
     if (fused_lru)
       launch::smo_fused_lru(args, pf + (size_t)ri * 2 * Gf, pout, rcf + ri, rcf + wi, stream);
     else
-      launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
-    if (collectives()) allreduce_keys(pout, 2 * Gf);
+      launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream, wi);
+    if (collectives() && !xch) allreduce_keys(pout, 2 * Gf);
   }
 
   bool collectives() const { return world > 1 || p.force_collectives; }
@@ -163,6 +175,114 @@ struct GpuSolver::Impl {
   }
 
   bool fused() const { return dense || fused_lru; }
+
+  // byte all-gather through the communicator (host or device memory)
+  void allgather_bytes(const void* send, void* recv, size_t bytes) {
+    if (world == 1) {
+      memcpy(recv, send, bytes);
+      return;
+    }
+    if (comm->device_memory()) {
+      size_t tb = 0;
+      uint8_t* d = dmalloc<uint8_t>(bytes * (world + 1), &tb);
+      HIP_CHECK(hipMemcpy(d + bytes * world, send, bytes, hipMemcpyHostToDevice));
+      comm->allgather(d + bytes * world, d, bytes, stream);
+      HIP_CHECK(hipMemcpyAsync(recv, d, bytes * world, hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      (void)hipFree(d);
+    } else {
+      comm->allgather(send, recv, bytes, nullptr);
+    }
+  }
+
+  // Peer exchange setup (collective over the communicator): receive buffers,
+  // pointer / IPC-handle all-gather, mapping, and an in-kernel ping that every
+  // rank must pass.  Returns false (everywhere) if any rank failed.
+  bool setup_exchange() {
+    struct alignas(16) XInfo {
+      int64_t pid, device, ok;
+      uint64_t ptr;
+      hipIpcMemHandle_t handle;
+    };
+    XInfo me{};
+    me.pid = (int64_t)getpid();
+    me.device = device;
+    me.ok = 1;
+    const int64_t ping_words = 64;
+    xregion = (int64_t)2 * world * Gf * kXchGranules;
+    try {
+      DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
+      HIP_CHECK(hipMalloc((void**)&xbuf, (size_t)(xregion + ping_words) * 8));  // own allocation: IPC export
+      HIP_CHECK(hipMemset(xbuf, 0, (size_t)(xregion + ping_words) * 8));
+      HIP_CHECK(hipDeviceSynchronize());
+      me.ptr = (uint64_t)xbuf;
+      if (world > 1) HIP_CHECK(hipIpcGetMemHandle(&me.handle, xbuf));
+    } catch (const std::exception& e) {
+      if (p.verbose) fprintf(stderr, "[dpsvm] peer exchange unavailable on rank %d: %s\n", rank, e.what());
+      me.ok = 0;
+    }
+    std::vector<XInfo> all((size_t)world);
+    allgather_bytes(&me, all.data(), sizeof(XInfo));
+    bool ok = true;
+    for (const auto& r : all) ok &= r.ok != 0;
+    std::vector<uint64_t*> ptrs((size_t)world, nullptr);
+    if (ok) {
+      try {
+        for (int r = 0; r < world; ++r) {
+          if (r == rank) {
+            ptrs[r] = xbuf;
+          } else if (all[r].pid == me.pid) {  // rank thread of this process: direct pointer
+            ptrs[r] = (uint64_t*)all[r].ptr;
+            if (all[r].device != device) {
+              const hipError_t e = hipDeviceEnablePeerAccess((int)all[r].device, 0);
+              if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_CHECK(e);
+              (void)hipGetLastError();
+            }
+          } else {  // other process: dmabuf IPC mapping (xGMI peer memory)
+            void* q = nullptr;
+            HIP_CHECK(hipIpcOpenMemHandle(&q, all[r].handle, hipIpcMemLazyEnablePeerAccess));
+            xopened.push_back(q);
+            ptrs[r] = (uint64_t*)q;
+          }
+        }
+        size_t tb = 0;
+        xpeer_d = dmalloc<uint64_t*>((size_t)world, &tb);
+        HIP_CHECK(hipMemcpy(xpeer_d, ptrs.data(), world * sizeof(uint64_t*), hipMemcpyHostToDevice));
+      } catch (const std::exception& e) {
+        if (p.verbose) fprintf(stderr, "[dpsvm] peer mapping failed on rank %d: %s\n", rank, e.what());
+        ok = false;
+      }
+    }
+    // in-kernel self test (a rank that failed above does not ping: the others time out)
+    size_t tb = 0;
+    int32_t* okd = dmalloc<int32_t>(2, &tb);
+    uint64_t* agree = dmalloc<uint64_t>(1, &tb);
+    HIP_CHECK(hipMemset(okd, 0, 8));
+    if (world > 1) comm->barrier();
+    if (ok) launch::xch_ping(xpeer_d, rank, world, xregion, 1u, (int64_t)5e8 /* 5 s */, okd, stream);
+    int32_t okh = 0;
+    HIP_CHECK(hipMemcpyAsync(&okh, okd, 4, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    const uint64_t mine = (ok && okh == 1) ? 0ull : 1ull;  // MIN over ranks of "failed" -> use MAX via complement
+    uint64_t v = ~mine;  // all ok -> every rank holds ~0; any failure -> some rank holds ~1 (smaller)
+    HIP_CHECK(hipMemcpy(agree, &v, 8, hipMemcpyHostToDevice));
+    if (world > 1) allreduce_keys(agree, 1);
+    HIP_CHECK(hipMemcpyAsync(&v, agree, 8, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    (void)hipFree(okd);
+    (void)hipFree(agree);
+    const bool all_ok = v == ~0ull;
+    if (!all_ok) {
+      for (void* q : xopened) (void)hipIpcCloseMemHandle(q);
+      xopened.clear();
+      if (xbuf) (void)hipFree(xbuf);
+      if (xpeer_d) (void)hipFree(xpeer_d);
+      xbuf = nullptr;
+      xpeer_d = nullptr;
+    }
+    if (world > 1) comm->barrier();
+    return all_ok;
+  }
 
   void enqueue_iteration(int k) {
     if (fused()) {
@@ -530,6 +650,26 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.info.cache_lines = m.L;
   m.info.blocks = (int)m.G;
   m.info.iteration = m.dense ? "fused-dense" : (m.fused_lru ? "fused-cache" : "chain");
+  // ---- per-iteration key exchange ----
+  a.xpeer = nullptr;
+  a.xrank = 0;
+  a.xworld = 0;
+  a.xtimeout_ticks = 0;
+  m.xch = false;
+  if (m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) {
+    const bool ok = m.setup_exchange();
+    DPSVM_CHECK(ok || m.p.exchange != 2, "peer exchange requested (exchange=2) but its self test failed");
+    if (ok) {
+      double tmo = 120.0;
+      if (const char* e = std::getenv("DPSVM_XCH_TIMEOUT_S")) tmo = std::max(0.1, atof(e));
+      m.xch = true;
+      a.xpeer = m.xpeer_d;
+      a.xrank = m.rank;
+      a.xworld = m.world;
+      a.xtimeout_ticks = (int64_t)(tmo * 1e8);
+    }
+  }
+  m.info.exchange = m.xch ? "peer" : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
   m.info.bytes_device = m.bytes;
   return m.info;
 }
@@ -599,6 +739,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     }
   }
   m.init_ctrl(iter0, b_hi0, b_lo0);
+  if (m.xch) HIP_CHECK(hipMemsetAsync(m.xbuf, 0, (size_t)m.xregion * 8, m.stream));  // tags restart at iter0 + 1
   HIP_CHECK(hipStreamSynchronize(m.stream));
   if (m.world > 1) m.comm->barrier();
   res.t_setup = secs_since(ts0);
@@ -641,8 +782,8 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     r0.b_lo = b_lo0;
     HIP_CHECK(hipMemcpyAsync(m.rf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
     uint64_t* p1 = m.pf + 2 * m.Gf;
-    launch::smo_fused(m.args, 0, nullptr, p1, nullptr, nullptr, m.stream);
-    if (m.collectives()) m.allreduce_keys(p1, 2 * m.Gf);
+    launch::smo_fused(m.args, 0, nullptr, p1, m.rf + 1, nullptr, m.stream, 1);
+    if (m.collectives() && !m.xch) m.allreduce_keys(p1, 2 * m.Gf);
   }
   const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
   int B = std::max(1, m.p.graph_block);
@@ -724,6 +865,9 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   st = m.read_status();
   res.iters = st.iter;
   res.status = st.done;
+  if (st.done == kCommFail)
+    fail("peer exchange: a rank stopped publishing its selection keys (timeout after iteration " +
+         std::to_string(st.iter) + ")");
   res.b_hi = st.b_hi;
   res.b_lo = st.b_lo;
   res.b = (st.b_lo + st.b_hi) / 2.0f;

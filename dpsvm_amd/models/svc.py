@@ -47,6 +47,7 @@ def _as_1d(y) -> np.ndarray:
 
 _CLIP = {"independent": 0, "box": 1}
 _XMODE = {"auto": 0, "replicated": 1, "partitioned": 2}
+_EXCHANGE = {"auto": 0, "allreduce": 1, "peer": 2}
 
 
 @dataclass
@@ -73,6 +74,7 @@ class SVCConfig:
     device: str = "auto"            # auto | cpu | cuda | cuda:N
     verbose: bool = False
     force_collectives: bool = False  # run the per-iteration collective even with one rank (tests)
+    exchange: str = "auto"          # per-iteration key exchange (dense mode): auto | allreduce | peer
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -105,6 +107,9 @@ class SVCConfig:
         p.checkpoint_every = int(self.checkpoint_every)
         p.checkpoint_path = self.checkpoint_path or ""
         p.force_collectives = bool(self.force_collectives)
+        if self.exchange not in _EXCHANGE:
+            raise ValueError(f"exchange must be one of {list(_EXCHANGE)}")
+        p.exchange = _EXCHANGE[self.exchange]
         return p
 
     def device_kind(self) -> tuple[str, int]:

@@ -209,3 +209,37 @@ def test_fused_cache_wide_features_and_checkpoint(monkeypatch, tmp_path):
     monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
     chain = SVC(**kw).fit(X, y)
     assert np.array_equal(chain.alpha_, full.alpha_)
+
+
+def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
+    """In-kernel peer exchange of the selection keys (dense mode): a one-rank
+    loopback and 2/3 rank threads sharing the GPU must reproduce the local
+    run bit for bit."""
+    monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    ref = SVC(**kw).fit(X, y)
+    assert ref.setup_info_["exchange"] == "none"
+    loop = SVC(exchange="peer", **kw).fit(X, y)
+    assert loop.setup_info_["exchange"] == "peer"
+    assert loop.n_iter_ == ref.n_iter_ and np.array_equal(loop.alpha_, ref.alpha_)
+    for world in (2, 3):
+        g = C.ThreadCommGroup(world)
+        comms = [g.comm(r) for r in range(world)]
+        out = [None] * world
+        errs = []
+
+        def work(r):
+            try:
+                out[r] = SVC(exchange="peer", **kw).fit(X, y, comm=comms[r])
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert not errs, errs
+        for r in range(world):
+            assert out[r].setup_info_["exchange"] == "peer"
+            assert out[r].n_iter_ == ref.n_iter_, world
+            assert np.array_equal(out[r].alpha_, ref.alpha_)
