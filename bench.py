@@ -172,6 +172,7 @@ def main(argv=None) -> int:
             "n_sv": nsv,
             "b": res["b"],
             "train_accuracy": acc,
+            "gram_gemm_s": round(float(res.get("t_gram", 0.0)), 6),
             "smo_loop_s_min": round(solve_min, 6),
             "smo_loop_s_max": round(solve_max, 6),
             "iters_per_s": round(res["iters"] / max(solve_max, 1e-9), 1),

@@ -34,10 +34,14 @@ def main():
         us = C.launch_floor_us(blocks, 256, 64, 50)
         lines.append({"what": "launch_floor", "blocks": blocks, "us_per_kernel": round(us, 3)})
     X, y = synthetic("mnist", n=a.samples, d=a.features, seed=0)
-    for mode, extra in (("dense", {}), ("lru", {"cache_lines": 20000}), ("lru-chain", {"cache_lines": 20000})):
+    modes = (("dense", {"persist": "off"}), ("dense-persist", {"persist": "on"}), ("lru", {"cache_lines": 20000}),
+             ("lru-chain", {"cache_lines": 20000}))
+    for mode, extra in modes:
         if mode == "lru-chain":
             os.environ["DPSVM_LRU_KERNELS"] = "3"  # rows/step/finalize chain (A/B)
         for gb in ((64,) if mode == "lru-chain" else (16, 64, 256)):
+            if mode == "dense-persist":
+                extra = dict(extra, persist_block=gb * 32)
             cfg = SVCConfig(C=10.0, gamma=0.25, eps=1e-3, graph_block=gb, **extra)
             s = C.GpuSolver(cfg.to_native(X.shape[1]), None, 0)
             si = s.setup(X, X.shape[0], y)

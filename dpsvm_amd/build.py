@@ -46,6 +46,7 @@ LIB_SOURCES = [
     "kernels/microbench.hip",
     "kernels/compact.hip",
     "kernels/smo_fused_lru.hip",
+    "kernels/smo_persist.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

@@ -80,6 +80,10 @@ struct SolverParams {
   // all-reduce), 1 communicator all-reduce, 2 peer exchange (required; also
   // at world 1 as a loopback, for tests)
   int exchange = 0;
+  // dense mode iteration engine: 0 auto, 1 one launch per iteration (graphs),
+  // 2 persistent kernel (persist_block iterations per launch)
+  int persist = 0;
+  int persist_block = 2048;
 };
 
 // Per-run result, gathered on every rank.
@@ -89,6 +93,7 @@ struct SolveResult {
   int64_t iters = 0;
   int status = 0;             // 1 converged, 2 max_iter, 3 no violating pair, 4 non-finite
   double t_setup = 0.0, t_solve = 0.0;
+  double t_gram = 0.0;  // device time of the resident Gram GEMM inside t_solve (dense mode)
   int64_t cache_hits = 0, cache_misses = 0, rows_computed = 0, x_passes = 0;
   int64_t host_hits = 0, spec_rows = 0;
   int64_t cache_lines = 0, host_cache_lines = 0;

@@ -25,10 +25,14 @@ bool smo_fused_lru_supported(int dp);
 size_t smo_fused_lru_lds_bytes(int dp);
 void smo_fused_lru(const SmoArgs& a, const uint64_t* p_in, uint64_t* p_out, const FusedCacheRec* r_in,
                    FusedCacheRec* r_out, hipStream_t s);
-// dense mode: init (selection only, mode 0) or one fused SMO iteration (mode 1);
-// xpar: peer-exchange parity this launch publishes (a.xworld > 0)
+// dense mode: init (selection only, mode 0; r_in = the seed record when
+// a.xworld > 0) or one fused SMO iteration (mode 1)
 void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out, const FusedRec* r_in,
-               FusedRec* r_out, hipStream_t s, int xpar = 0);
+               FusedRec* r_out, hipStream_t s);
+// dense mode, persistent: up to `steps` SMO iterations in one launch (every
+// workgroup co-resident; keys exchanged as tagged granules, a.xworld >= 1);
+// st: state record in/out (iteration, done, b_hi, b_lo; no pending pair)
+void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s);
 // peer-exchange self test: every rank pushes a tagged granule to every rank and
 // polls its own; *ok = 1 when all arrived within timeout_ticks
 //   (ping slots at u64 offset ping_off of every receive buffer)

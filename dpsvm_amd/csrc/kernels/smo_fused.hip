@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
                                                                   const uint64_t* __restrict__ p_in,
                                                                   uint64_t* __restrict__ p_out,
                                                                   const FusedRec* __restrict__ r_in,
-                                                                  FusedRec* __restrict__ r_out, int xpar) {
+                                                                  FusedRec* __restrict__ r_out) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -126,7 +126,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); kl = k < kl ? k : kl; }
     }
     // peer exchange: the seed's keys carry tag iter0 + 1 (r_in = the seed record)
-    store_block_keys(a, kh, kl, p_out, kscr, xpar, a.xworld > 0 ? (uint32_t)r_in->iter + 1u : 0u);
+    const uint32_t tag = a.xworld > 0 ? (uint32_t)r_in->iter + 1u : 0u;
+    store_block_keys(a, kh, kl, p_out, kscr, (int)(tag & 1u), tag);
     return;
   }
 
@@ -141,7 +142,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       kl = v.y < kl ? v.y : kl;
     }
   }
-  if (rin.done == kRunning && a.xworld > 0 && !xch_pull(a, xpar ^ 1, (uint32_t)rin.iter + 1u, kh, kl, lane)) {
+  if (rin.done == kRunning && a.xworld > 0 &&
+      !xch_pull(a, (int)(((uint32_t)rin.iter + 1u) & 1u), (uint32_t)rin.iter + 1u, kh, kl, lane)) {
     // a peer stopped publishing: give up (every rank that times out stops the same way)
     if (lead) {
       commit_pending(a, rin);
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   }
   stamp(rin.iter, 3, 0);
   if (done != kRunning) return;  // uniform
-  store_block_keys(a, nh, nlk, p_out, kscr, xpar, (uint32_t)iter + 1u);
+  store_block_keys(a, nh, nlk, p_out, kscr, (int)(((uint32_t)iter + 1u) & 1u), (uint32_t)iter + 1u);
   stamp(rin.iter, 4, 0);
 }
 
@@ -299,8 +301,8 @@ void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uin
 }
 
 void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out, const FusedRec* r_in,
-               FusedRec* r_out, hipStream_t s, int xpar) {
-  dev::smo_fused_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out, xpar);
+               FusedRec* r_out, hipStream_t s) {
+  dev::smo_fused_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out);
   post_launch("smo_fused", s);
 }
 

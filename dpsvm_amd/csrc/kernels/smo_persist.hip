@@ -1,0 +1,228 @@
+// Persistent dense SMO (Gram resident): ONE launch runs up to `steps` SMO
+// iterations.  Every workgroup stays resident (grid <= 256 workgroups of 256
+// threads, one per CU) and keeps its rows' f, alpha and y in registers; the
+// only per-iteration traffic between workgroups is the selection keys,
+// exchanged as tagged granules (xch.hpp) — each workgroup publishes its two
+// keys to every rank, every workgroup polls all of them.  This replaces the
+// kernel boundary (~1.5 us) and the reload of row state of the one-launch-per-
+// iteration kernel (smo_fused.hip) with one all-to-all poll.
+//
+// Iteration t in workgroup b (identical arithmetic to smo_fused.hip, so the
+// two paths are bit-identical):
+//   1. wave 0 polls the keys tagged t (all ranks' workgroups), broadcasts the
+//      minima through LDS (barrier 1);
+//   2. pair (i_hi, i_lo), eta from the two sample rows, alpha update;
+//      alphas of older pairs come from memory, committed by workgroup 0 with
+//      write-through stores that it drains before publishing its keys — so a
+//      workgroup that has seen those keys sees the commit; the previous pair is
+//      still pending and is applied from registers;
+//   3. f update of the own rows from the Gram rows K[i_hi][.], K[i_lo][.],
+//      classification, per-workgroup keys (barrier 2), published tagged t+1.
+// Alpha memory is written only by workgroup 0, thread 0, in program order
+// (commits during the run, the last pair at exit): no write-write race.
+// Reference per-iteration path: svmTrainMain.cpp:235-310.
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "xch.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+constexpr int kPersistMaxRows = 4;  // rows per thread (fused_rows <= 1024)
+
+__device__ __forceinline__ float load_alpha(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_alpha(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
+  static_assert(kFusedThreads == 256, "4 waves assumed");
+  __shared__ uint64_t kscr[8];
+  __shared__ uint64_t pair_s[2];
+  __shared__ int fail_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  const int rpt = a.fused_rows / kFusedThreads;  // rows per thread
+  const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
+  const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
+
+  float f[kPersistMaxRows], al[kPersistMaxRows], yv[kPersistMaxRows];
+  bool has[kPersistMaxRows];
+#pragma unroll
+  for (int k = 0; k < kPersistMaxRows; ++k) {
+    const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
+    has[k] = k < rpt && j < row_end;
+    f[k] = has[k] ? a.f[j] : 0.f;
+    al[k] = has[k] ? a.alpha[a.off + j] : 0.f;
+    yv[k] = has[k] ? a.y[a.off + j] : 0.f;
+  }
+  const FusedRec s0 = *st;
+  if (s0.done != kRunning) return;
+  int t = s0.iter, done = kRunning;
+  float b_hi = s0.b_hi, b_lo = s0.b_lo;
+  int p_hi = -1, p_lo = -1;  // pending pair (applied by every workgroup, committed one iteration later)
+  float pa_hi = 0.f, pa_lo = 0.f;
+
+  for (int step = 0; step < steps; ++step) {
+    // ---- 1. keys tagged t+1 (produced by iteration t) ----
+    const uint32_t tag = (uint32_t)t + 1u;
+    if (wave == 0) {
+      uint64_t kh = kKeyNone, kl = kKeyNone;
+      const bool ok = xch_pull(a, (int)(tag & 1u), tag, kh, kl, lane);
+      if (lane == 0) {
+        pair_s[0] = kh;
+        pair_s[1] = kl;
+        fail_s = ok ? 0 : 1;
+      }
+    }
+    __syncthreads();
+    const uint64_t kh = pair_s[0], kl = pair_s[1];
+    if (fail_s) {
+      done = kCommFail;
+      break;
+    }
+    if (kh == kKeyNone || kl == kKeyNone) {
+      done = kNoPair;
+      break;
+    }
+    const int i_hi = (int)key_index(kh), i_lo = (int)key_index(kl);
+    const float bh = key_value(kh), bl = -key_value(kl);
+
+    // ---- 2. one round trip: Gram rows of the own rows, sample rows, pair state ----
+    const float* line_hi = a.lines + (int64_t)i_hi * a.ldl;
+    const float* line_lo = a.lines + (int64_t)i_lo * a.ldl;
+    float khv[kPersistMaxRows], klv[kPersistMaxRows];
+#pragma unroll
+    for (int k = 0; k < kPersistMaxRows; ++k) {
+      const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
+      khv[k] = has[k] ? line_hi[j] : 0.f;
+      klv[k] = has[k] ? line_lo[j] : 0.f;
+    }
+    const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];
+    const float m_hi = load_alpha(a.alpha + i_hi), m_lo = load_alpha(a.alpha + i_lo);
+    const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
+    const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
+    const float dist2 = wave_dist2(xh, xl, a.dp, lane);  // identical tree in every wave
+    const float a_hi_old = i_hi == p_hi ? pa_hi : (i_hi == p_lo ? pa_lo : m_hi);
+    const float a_lo_old = i_lo == p_hi ? pa_hi : (i_lo == p_lo ? pa_lo : m_lo);
+    float c_hi = 0.f, c_lo = 0.f, a_hi_new = a_hi_old, a_lo_new = a_lo_old;
+    const int iter = t + 1;
+    if (!isfinite(bh) || !isfinite(bl)) {
+      done = kNonFinite;
+    } else {
+      const float k_hl = expf(-a.gamma * dist2);
+      const PairUpdate u =
+          pair_update(a_hi_old, a_lo_old, y_hi, y_lo, bh, bl, k_hl, a.C, a.tau, a.clip, i_hi == i_lo);
+      a_hi_new = u.a_hi_new;
+      a_lo_new = u.a_lo_new;
+      c_hi = u.c_hi;
+      c_lo = u.c_lo;
+      if (!gap_open(bh, bl, a.eps)) done = kConverged;
+      else if (iter >= a.max_iter) done = kMaxIter;
+    }
+    b_hi = bh;
+    b_lo = bl;
+    if (done == kNonFinite) break;
+
+    // commit the pending pair (write-through; drained before this workgroup publishes)
+    if (lead && p_hi >= 0) {
+      store_alpha(a.alpha + p_lo, pa_lo);
+      store_alpha(a.alpha + p_hi, pa_hi);  // hi written last (svmTrainMain.cpp:298-299)
+    }
+    p_hi = i_hi;
+    p_lo = i_lo;
+    pa_hi = a_hi_new;
+    pa_lo = a_lo_new;
+    t = iter;
+
+    // ---- 3. f update + classification of the own rows ----
+    const bool upd_f = c_hi != 0.f || c_lo != 0.f;
+    uint64_t nh = kKeyNone, nlk = kKeyNone;
+#pragma unroll
+    for (int k = 0; k < kPersistMaxRows; ++k) {
+      if (!has[k]) continue;
+      const int64_t g = a.off + row0 + tid + (int64_t)k * kFusedThreads;
+      if (upd_f) {
+        float delta;
+        if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * khv[k]) + (c_lo * klv[k]);
+        else if (c_hi != 0.f) delta = c_hi * khv[k];
+        else delta = c_lo * klv[k];
+        f[k] += delta;
+      }
+      if (g == i_lo) al[k] = a_lo_new;
+      if (g == i_hi) al[k] = a_hi_new;  // hi wins when i_hi == i_lo
+      if (in_up(al[k], yv[k], a.C)) { const uint64_t key = make_key(f[k], (uint32_t)g); nh = key < nh ? key : nh; }
+      if (in_low(al[k], yv[k], a.C)) { const uint64_t key = make_key(-f[k], (uint32_t)g); nlk = key < nlk ? key : nlk; }
+    }
+    if (done != kRunning) break;  // uniform: the last update is applied, no keys needed
+
+    nh = wave_min_u64(nh);
+    nlk = wave_min_u64(nlk);
+    if (lane == 0) {
+      kscr[wave] = nh;
+      kscr[4 + wave] = nlk;
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int w = 1; w < kFusedThreads / 64; ++w) {
+        nh = kscr[w] < nh ? kscr[w] : nh;
+        nlk = kscr[4 + w] < nlk ? kscr[4 + w] : nlk;
+      }
+      // the alpha commit above (thread 0 of this wave) lands before the keys
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t otag = (uint32_t)t + 1u;
+      xch_push(a, (int)(otag & 1u), blockIdx.x, nh, nlk, otag, lane);
+    }
+  }
+
+  // ---- exit: own rows' f back to memory; workgroup 0 commits the last pair and the state ----
+#pragma unroll
+  for (int k = 0; k < kPersistMaxRows; ++k) {
+    const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
+    if (has[k]) a.f[j] = f[k];
+  }
+  if (lead) {
+    if (p_hi >= 0) {
+      store_alpha(a.alpha + p_lo, pa_lo);
+      store_alpha(a.alpha + p_hi, pa_hi);
+    }
+    FusedRec o;
+    o.i_hi = o.i_lo = -1;
+    o.a_hi = o.a_lo = 0.f;
+    o.iter = t;
+    o.done = done;
+    o.b_hi = b_hi;
+    o.b_lo = b_lo;
+    *st = o;
+    if (a.status) {
+      SmoStatus* s = a.status;
+      s->iter = t;
+      s->done = done;
+      s->b_hi = b_hi;
+      s->b_lo = b_lo;
+      __atomic_store_n(&s->seq, t, __ATOMIC_RELEASE);
+    }
+  }
+}
+
+}  // namespace dev
+
+namespace launch {
+
+void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {
+  DPSVM_CHECK(a.xworld >= 1 && a.fused_G <= 256 && a.fused_rows <= dev::kPersistMaxRows * kFusedThreads,
+              "persistent SMO needs the key exchange and <= 256 resident workgroups");
+  dev::smo_persist_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, st, steps);
+  post_launch("smo_persist", s);
+}
+
+}  // namespace launch
+}  // namespace dpsvm

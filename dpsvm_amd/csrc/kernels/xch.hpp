@@ -8,7 +8,7 @@
 // loads until every granule of the parity carries the expected tag, then
 // reduces exactly as from an all-reduced buffer — so every rank derives the
 // same pair.  Tags are the iteration count + 1 (never 0; buffers are zeroed
-// before each solve), parities alternate, and a rank cannot lap a peer: its
+// before each solve); keys tagged T live in parity T & 1, and a rank cannot lap a peer: its
 // launch t+2 needs that peer's launch-t+1 keys, which the peer publishes only
 // after it has read the parity t+2 overwrites.
 // Reference: one 16-byte MPI Allgather per iteration (svmTrainMain.cpp:244).

@@ -107,6 +107,7 @@ py::dict result_dict(const SolveResult& r) {
   d["converged"] = r.converged();
   d["t_setup"] = r.t_setup;
   d["t_solve"] = r.t_solve;
+  d["t_gram"] = r.t_gram;
   d["cache_hits"] = r.cache_hits;
   d["cache_misses"] = r.cache_misses;
   d["rows_computed"] = r.rows_computed;
@@ -161,7 +162,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("checkpoint_path", &SolverParams::checkpoint_path)
       .def_readwrite("sync_debug", &SolverParams::sync_debug)
       .def_readwrite("force_collectives", &SolverParams::force_collectives)
-      .def_readwrite("exchange", &SolverParams::exchange);
+      .def_readwrite("exchange", &SolverParams::exchange)
+      .def_readwrite("persist", &SolverParams::persist)
+      .def_readwrite("persist_block", &SolverParams::persist_block);
 
   py::class_<Checkpoint>(m, "Checkpoint")
       .def(py::init<>())

@@ -22,15 +22,11 @@
 #include "dpsvm/common.hpp"
 #include "dpsvm/solver.hpp"
 #include "../runtime/thread_pool.hpp"
+#include "../runtime/timer.hpp"
 #include "../runtime/trace.hpp"
 
 namespace dpsvm {
 namespace {
-
-using Clock = std::chrono::steady_clock;
-double secs_since(Clock::time_point t0) {
-  return std::chrono::duration<double>(Clock::now() - t0).count();
-}
 
 inline float dot_f32(const float* a, const float* b, int d) {
   // 4 partial sums (vectorisable); order fixed per row -> shard-invariant

@@ -29,15 +29,12 @@
 #include "dpsvm/solver.hpp"
 #include "../kernels/kernels.hpp"
 #include "../runtime/hip_check.hpp"
+#include "../runtime/timer.hpp"
 #include "../runtime/trace.hpp"
 
 namespace dpsvm {
 namespace {
 
-using Clock = std::chrono::steady_clock;
-double secs_since(Clock::time_point t0) {
-  return std::chrono::duration<double>(Clock::now() - t0).count();
-}
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
 template <class T>
@@ -85,6 +82,7 @@ struct GpuSolver::Impl {
   // peer exchange (dense fused mode): own receive buffer (own allocation, IPC
   // exported), device table of every rank's buffer, IPC mappings to close
   bool xch = false;
+  bool persist = false;  // dense mode: persistent kernel, persist_block iterations per launch
   uint64_t* xbuf = nullptr;
   uint64_t** xpeer_d = nullptr;
   int64_t xregion = 0;  // u64 words of the two key parities (zeroed per solve)
@@ -156,7 +154,7 @@ struct GpuSolver::Impl {
     if (fused_lru)
       launch::smo_fused_lru(args, pf + (size_t)ri * 2 * Gf, pout, rcf + ri, rcf + wi, stream);
     else
-      launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream, wi);
+      launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
     if (collectives() && !xch) allreduce_keys(pout, 2 * Gf);
   }
 
@@ -656,9 +654,17 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.xworld = 0;
   a.xtimeout_ticks = 0;
   m.xch = false;
-  if (m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) {
+  bool want_persist = false;
+  if (m.dense && m.replicated) {
+    const char* pe = std::getenv("DPSVM_PERSIST");
+    int mode = m.p.persist;
+    if (pe && pe[0]) mode = pe[0] == '1' ? 2 : 1;
+    want_persist = mode == 2;
+  }
+  if (m.dense && ((m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || want_persist)) {
     const bool ok = m.setup_exchange();
-    DPSVM_CHECK(ok || m.p.exchange != 2, "peer exchange requested (exchange=2) but its self test failed");
+    DPSVM_CHECK(ok || (m.p.exchange != 2 && m.p.persist != 2),
+                "peer exchange requested (exchange=2 / persist=2) but its self test failed");
     if (ok) {
       double tmo = 120.0;
       if (const char* e = std::getenv("DPSVM_XCH_TIMEOUT_S")) tmo = std::max(0.1, atof(e));
@@ -670,6 +676,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     }
   }
   m.info.exchange = m.xch ? "peer" : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
+  m.persist = want_persist && m.xch;
+  if (m.persist) m.info.iteration = "persistent-dense";
   m.info.bytes_device = m.bytes;
   return m.info;
 }
@@ -749,6 +757,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   const int64_t fault_iter = trace::fault_nan_iter();
   bool fault_done = false;
   auto t0 = Clock::now();
+  EventTimer gram_timer;
   if (m.fused_lru) {
     // seed: record "no pending pair, empty cache" in buffer 1 + initial keys
     FusedCacheRec r0;
@@ -768,8 +777,10 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   if (m.dense) {
     trace::Range gram_range("dpsvm/gram_gemm");
     // whole Gram shard K[i][j], i over all n rows, j over local rows: one MFMA GEMM
+    gram_timer.start(m.stream);
     launch::rbf_gemm_store(m.x, m.xsq, m.n, m.dp, m.x + (size_t)m.off * m.dp, m.xsq + m.off, m.nl, m.dp,
                            m.dp, m.gamma, m.lines, m.ldl, m.stream);
+    gram_timer.stop(m.stream);
     res.rows_computed = m.n;
     res.x_passes = 1;
     // fused-iteration seed: record "no pending pair" in buffer 1 + initial keys
@@ -782,13 +793,14 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     r0.b_lo = b_lo0;
     HIP_CHECK(hipMemcpyAsync(m.rf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
     uint64_t* p1 = m.pf + 2 * m.Gf;
-    launch::smo_fused(m.args, 0, nullptr, p1, m.rf + 1, nullptr, m.stream, 1);
+    launch::smo_fused(m.args, 0, nullptr, p1, m.rf + 1, nullptr, m.stream);
     if (m.collectives() && !m.xch) m.allreduce_keys(p1, 2 * m.Gf);
   }
   const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
   int B = std::max(1, m.p.graph_block);
   if (m.fused()) B = std::max(2, (B + 1) / 2 * 2);  // ping-pong parity must survive graph replays
-  if (graphs) {
+  if (m.persist) B = std::max(1, m.p.persist_block);
+  if (graphs && !m.persist) {
     try {
       m.build_graph(B);
     } catch (const std::exception& e) {
@@ -800,7 +812,9 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   int64_t last_ck = iter0, last_log = iter0;
   SmoStatus st{};
   while (true) {
-    if (m.gexec) {
+    if (m.persist) {
+      launch::smo_persist(m.args, m.rf + 1, B, m.stream);
+    } else if (m.gexec) {
       HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
     } else {
       for (int i = 0; i < B; ++i) m.enqueue_iteration(i);
@@ -837,6 +851,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   m.wait_event(m.ev[blocks & 1]);  // the overshoot block (early-exit kernels)
   HIP_CHECK(hipStreamSynchronize(m.stream));
   res.t_solve = secs_since(t0);
+  if (m.dense) res.t_gram = gram_timer.seconds();
   if (m.p.checkpoint_every > 0 && !m.p.checkpoint_path.empty()) {
     st = m.read_status();
     if (st.done == kMaxIter) m.snapshot(st);  // resumable continuation point

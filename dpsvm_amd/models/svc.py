@@ -48,6 +48,7 @@ def _as_1d(y) -> np.ndarray:
 _CLIP = {"independent": 0, "box": 1}
 _XMODE = {"auto": 0, "replicated": 1, "partitioned": 2}
 _EXCHANGE = {"auto": 0, "allreduce": 1, "peer": 2}
+_PERSIST = {"auto": 0, "off": 1, "on": 2}
 
 
 @dataclass
@@ -75,6 +76,8 @@ class SVCConfig:
     verbose: bool = False
     force_collectives: bool = False  # run the per-iteration collective even with one rank (tests)
     exchange: str = "auto"          # per-iteration key exchange (dense mode): auto | allreduce | peer
+    persist: str = "auto"           # dense-mode engine: auto | off (one launch per iteration) | on (persistent)
+    persist_block: int = 2048       # SMO iterations per persistent launch
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -110,6 +113,10 @@ class SVCConfig:
         if self.exchange not in _EXCHANGE:
             raise ValueError(f"exchange must be one of {list(_EXCHANGE)}")
         p.exchange = _EXCHANGE[self.exchange]
+        if self.persist not in _PERSIST:
+            raise ValueError(f"persist must be one of {list(_PERSIST)}")
+        p.persist = _PERSIST[self.persist]
+        p.persist_block = int(self.persist_block)
         return p
 
     def device_kind(self) -> tuple[str, int]:

@@ -243,3 +243,39 @@ def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
             assert out[r].setup_info_["exchange"] == "peer"
             assert out[r].n_iter_ == ref.n_iter_, world
             assert np.array_equal(out[r].alpha_, ref.alpha_)
+
+
+@pytest.mark.parametrize("block", [2048, 37])
+def test_persistent_engine_matches_fused(monkeypatch, C, block):
+    """Persistent dense kernel (keys exchanged in-kernel, row state in
+    registers) == one launch per iteration, bit for bit; also across launches
+    of an odd block length, with 2 rank threads, and with a checkpoint."""
+    monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    ref = SVC(persist="off", **kw).fit(X, y)
+    got = SVC(persist="on", persist_block=block, **kw).fit(X, y)
+    assert got.setup_info_["iteration"] == "persistent-dense"
+    assert got.n_iter_ == ref.n_iter_ and got.status_ == ref.status_
+    assert np.array_equal(got.alpha_, ref.alpha_)
+    assert got.b_ == ref.b_
+    g = C.ThreadCommGroup(2)
+    comms = [g.comm(r) for r in range(2)]
+    out = [None, None]
+    errs = []
+
+    def work(r):
+        try:
+            out[r] = SVC(persist="on", persist_block=block, **kw).fit(X, y, comm=comms[r])
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs, errs
+    for r in range(2):
+        assert out[r].n_iter_ == ref.n_iter_ and np.array_equal(out[r].alpha_, ref.alpha_)
+    m = SVC(persist="on", persist_block=block, max_iter=1000, **kw).fit(X, y)
+    m_ref = SVC(persist="off", max_iter=1000, **kw).fit(X, y)
+    assert m.n_iter_ == 1000 and m.status_ == 2 and np.array_equal(m.alpha_, m_ref.alpha_)
