@@ -294,6 +294,12 @@ __global__ __launch_bounds__(64) void xch_ping_kernel(uint64_t* const* peers, in
 
 namespace launch {
 
+void preload_fused_kernels() {
+  hipFuncAttributes at;
+  HIP_CHECK(hipFuncGetAttributes(&at, (const void*)dev::smo_fused_kernel));
+  HIP_CHECK(hipFuncGetAttributes(&at, (const void*)dev::xch_ping_kernel));
+}
+
 void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uint32_t tag, int64_t timeout_ticks,
               int32_t* ok, hipStream_t s) {
   dev::xch_ping_kernel<<<1, 64, 0, s>>>(peers, rank, world, ping_off, tag, timeout_ticks, ok);

@@ -217,6 +217,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
 
 namespace launch {
 
+void preload_persist_kernel() {
+  hipFuncAttributes at;
+  HIP_CHECK(hipFuncGetAttributes(&at, (const void*)dev::smo_persist_kernel));
+}
+
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {
   DPSVM_CHECK(a.xworld >= 1 && a.fused_G <= 256 && a.fused_rows <= dev::kPersistMaxRows * kFusedThreads,
               "persistent SMO needs the key exchange and <= 256 resident workgroups");

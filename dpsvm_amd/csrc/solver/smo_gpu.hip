@@ -87,6 +87,7 @@ struct GpuSolver::Impl {
   uint64_t** xpeer_d = nullptr;
   int64_t xregion = 0;  // u64 words of the two key parities (zeroed per solve)
   std::vector<void*> xopened;
+  std::string xch_diag;
   int64_t Gf = 0, RBf = 0;
   uint64_t* stamps = nullptr;  // DPSVM_STAMPS diagnostics
   std::string stamps_path;
@@ -210,6 +211,8 @@ struct GpuSolver::Impl {
     xregion = (int64_t)2 * world * Gf * kXchGranules;
     try {
       DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
+      launch::preload_fused_kernels();
+      launch::preload_persist_kernel();
       HIP_CHECK(hipMalloc((void**)&xbuf, (size_t)(xregion + ping_words) * 8));  // own allocation: IPC export
       HIP_CHECK(hipMemset(xbuf, 0, (size_t)(xregion + ping_words) * 8));
       HIP_CHECK(hipDeviceSynchronize());
@@ -261,7 +264,8 @@ struct GpuSolver::Impl {
     int32_t okh = 0;
     HIP_CHECK(hipMemcpyAsync(&okh, okd, 4, hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
-    const uint64_t mine = (ok && okh == 1) ? 0ull : 1ull;  // MIN over ranks of "failed" -> use MAX via complement
+    xch_diag = "rank " + std::to_string(rank) + ": mapped=" + std::to_string((int)ok) + " ping=" + std::to_string(okh);
+    const uint64_t mine = (ok && okh == 1) ? 0ull : 1ull;
     uint64_t v = ~mine;  // all ok -> every rank holds ~0; any failure -> some rank holds ~1 (smaller)
     HIP_CHECK(hipMemcpy(agree, &v, 8, hipMemcpyHostToDevice));
     if (world > 1) allreduce_keys(agree, 1);
@@ -664,7 +668,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   if (m.dense && ((m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || want_persist)) {
     const bool ok = m.setup_exchange();
     DPSVM_CHECK(ok || (m.p.exchange != 2 && m.p.persist != 2),
-                "peer exchange requested (exchange=2 / persist=2) but its self test failed");
+                "peer exchange requested (exchange=2 / persist=2) but its self test failed (" + m.xch_diag + ")");
     if (ok) {
       double tmo = 120.0;
       if (const char* e = std::getenv("DPSVM_XCH_TIMEOUT_S")) tmo = std::max(0.1, atof(e));
