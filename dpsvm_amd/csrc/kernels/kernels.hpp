@@ -36,8 +36,8 @@ void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s);
 // load the code objects of the kernels that spin on other ranks/workgroups
 // BEFORE any of them runs: a first launch that loads its code object while a
 // peer's spinning kernel occupies the device can stall behind it
-void preload_fused_kernels();
-void preload_persist_kernel();
+void preload_fused_kernels(hipStream_t s);
+void preload_persist_kernel(hipStream_t s);
 // peer-exchange self test: every rank pushes a tagged granule to every rank and
 // polls its own; *ok = 1 when all arrived within timeout_ticks
 //   (ping slots at u64 offset ping_off of every receive buffer)

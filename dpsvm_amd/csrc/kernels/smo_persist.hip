@@ -217,9 +217,20 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
 
 namespace launch {
 
-void preload_persist_kernel() {
-  hipFuncAttributes at;
-  HIP_CHECK(hipFuncGetAttributes(&at, (const void*)dev::smo_persist_kernel));
+void preload_persist_kernel(hipStream_t s) {
+  // trivial launch (no rows, state "done"): loads the code object and exits
+  FusedRec* st = nullptr;
+  HIP_CHECK(hipMalloc((void**)&st, sizeof(FusedRec)));
+  FusedRec h{};
+  h.done = kConverged;
+  HIP_CHECK(hipMemcpyAsync(st, &h, sizeof(h), hipMemcpyHostToDevice, s));
+  SmoArgs z{};
+  z.fused_G = 1;
+  z.fused_rows = kFusedThreads;
+  dev::smo_persist_kernel<<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipGetLastError());
+  (void)hipFree(st);
 }
 
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {

@@ -211,8 +211,8 @@ struct GpuSolver::Impl {
     xregion = (int64_t)2 * world * Gf * kXchGranules;
     try {
       DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
-      launch::preload_fused_kernels();
-      launch::preload_persist_kernel();
+      launch::preload_fused_kernels(stream);
+      launch::preload_persist_kernel(stream);
       HIP_CHECK(hipMalloc((void**)&xbuf, (size_t)(xregion + ping_words) * 8));  // own allocation: IPC export
       HIP_CHECK(hipMemset(xbuf, 0, (size_t)(xregion + ping_words) * 8));
       HIP_CHECK(hipDeviceSynchronize());
