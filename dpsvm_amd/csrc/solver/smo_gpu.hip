@@ -226,6 +226,14 @@ struct GpuSolver::Impl {
     allgather_bytes(&me, all.data(), sizeof(XInfo));
     bool ok = true;
     for (const auto& r : all) ok &= r.ok != 0;
+    for (int r = 0; r < world; ++r) {
+      // rank threads of one process on one device: their streams may share a
+      // hardware queue, so one spinning kernel can block the other's forever
+      if (r != rank && all[r].pid == me.pid && all[r].device == me.device) {
+        ok = false;
+        xch_diag = "ranks " + std::to_string(rank) + " and " + std::to_string(r) + " share a device in one process";
+      }
+    }
     std::vector<uint64_t*> ptrs((size_t)world, nullptr);
     if (ok) {
       try {
@@ -264,7 +272,8 @@ struct GpuSolver::Impl {
     int32_t okh = 0;
     HIP_CHECK(hipMemcpyAsync(&okh, okd, 4, hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
-    xch_diag = "rank " + std::to_string(rank) + ": mapped=" + std::to_string((int)ok) + " ping=" + std::to_string(okh);
+    if (xch_diag.empty())
+      xch_diag = "rank " + std::to_string(rank) + ": mapped=" + std::to_string((int)ok) + " ping=" + std::to_string(okh);
     const uint64_t mine = (ok && okh == 1) ? 0ull : 1ull;
     uint64_t v = ~mine;  // all ok -> every rank holds ~0; any failure -> some rank holds ~1 (smaller)
     HIP_CHECK(hipMemcpy(agree, &v, 8, hipMemcpyHostToDevice));

@@ -1,0 +1,33 @@
+"""Worker for test_peer_exchange_two_processes_one_gpu (launched by
+torch.distributed.run): train with the in-kernel peer exchange, write the
+result digest to <out>.rank<r>.json."""
+import hashlib
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(out: str, engine: str) -> int:
+    import torch  # noqa: F401
+    from dpsvm_amd import SVC
+    from dpsvm_amd.parallel import init_distributed, make_comm, shutdown
+    from dpsvm_amd.utils.datasets import synthetic
+
+    ctx = init_distributed(device="cuda")
+    comm = make_comm(ctx, "gloo")
+    X, y = synthetic("covtype", n=6000, seed=2)
+    clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer",
+              persist="on" if engine == "persistent" else "off", persist_block=257).fit(X, y, comm=comm)
+    rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
+           "iters": int(clf.n_iter_), "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
+    with open(f"{out}.rank{ctx.rank}.json", "w") as f:
+        json.dump(rec, f)
+    del comm
+    shutdown(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1], sys.argv[2]))

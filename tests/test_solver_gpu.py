@@ -213,8 +213,9 @@ def test_fused_cache_wide_features_and_checkpoint(monkeypatch, tmp_path):
 
 def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
     """In-kernel peer exchange of the selection keys (dense mode): a one-rank
-    loopback and 2/3 rank threads sharing the GPU must reproduce the local
-    run bit for bit."""
+    loopback reproduces the local run bit for bit; rank threads sharing one
+    device in one process fall back to the all-reduce (their streams may share
+    a hardware queue) with identical results."""
     monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
     X, y = synthetic("covtype", n=6000, seed=2)
     kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
@@ -223,33 +224,31 @@ def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
     loop = SVC(exchange="peer", **kw).fit(X, y)
     assert loop.setup_info_["exchange"] == "peer"
     assert loop.n_iter_ == ref.n_iter_ and np.array_equal(loop.alpha_, ref.alpha_)
-    for world in (2, 3):
-        g = C.ThreadCommGroup(world)
-        comms = [g.comm(r) for r in range(world)]
-        out = [None] * world
-        errs = []
+    g = C.ThreadCommGroup(2)
+    comms = [g.comm(r) for r in range(2)]
+    out = [None, None]
+    errs = []
 
-        def work(r):
-            try:
-                out[r] = SVC(exchange="peer", **kw).fit(X, y, comm=comms[r])
-            except Exception as e:  # pragma: no cover
-                errs.append(e)
+    def work(r):
+        try:
+            out[r] = SVC(**kw).fit(X, y, comm=comms[r])
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
 
-        ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
-        [t.start() for t in ts]
-        [t.join() for t in ts]
-        assert not errs, errs
-        for r in range(world):
-            assert out[r].setup_info_["exchange"] == "peer"
-            assert out[r].n_iter_ == ref.n_iter_, world
-            assert np.array_equal(out[r].alpha_, ref.alpha_)
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs, errs
+    for r in range(2):
+        assert out[r].setup_info_["exchange"] == "allreduce"
+        assert out[r].n_iter_ == ref.n_iter_ and np.array_equal(out[r].alpha_, ref.alpha_)
 
 
 @pytest.mark.parametrize("block", [2048, 37])
-def test_persistent_engine_matches_fused(monkeypatch, C, block):
+def test_persistent_engine_matches_fused(monkeypatch, block):
     """Persistent dense kernel (keys exchanged in-kernel, row state in
     registers) == one launch per iteration, bit for bit; also across launches
-    of an odd block length, with 2 rank threads, and with a checkpoint."""
+    of an odd block length and at max_iter."""
     monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
     X, y = synthetic("covtype", n=6000, seed=2)
     kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
@@ -259,23 +258,29 @@ def test_persistent_engine_matches_fused(monkeypatch, C, block):
     assert got.n_iter_ == ref.n_iter_ and got.status_ == ref.status_
     assert np.array_equal(got.alpha_, ref.alpha_)
     assert got.b_ == ref.b_
-    g = C.ThreadCommGroup(2)
-    comms = [g.comm(r) for r in range(2)]
-    out = [None, None]
-    errs = []
-
-    def work(r):
-        try:
-            out[r] = SVC(persist="on", persist_block=block, **kw).fit(X, y, comm=comms[r])
-        except Exception as e:  # pragma: no cover
-            errs.append(e)
-
-    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
-    [t.start() for t in ts]
-    [t.join() for t in ts]
-    assert not errs, errs
-    for r in range(2):
-        assert out[r].n_iter_ == ref.n_iter_ and np.array_equal(out[r].alpha_, ref.alpha_)
     m = SVC(persist="on", persist_block=block, max_iter=1000, **kw).fit(X, y)
     m_ref = SVC(persist="off", max_iter=1000, **kw).fit(X, y)
     assert m.n_iter_ == 1000 and m.status_ == 2 and np.array_equal(m.alpha_, m_ref.alpha_)
+
+
+@pytest.mark.parametrize("engine", ["fused", "persistent"])
+def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
+    """Two ranks as two processes sharing the GPU (gloo bootstrap, IPC-mapped
+    receive buffers): in-kernel exchange, bit-identical to one rank."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="30", DPSVM_VERIFY="1")
+    out = tmp_path / "mp"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + (engine == "persistent")),
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(f"{out}.rank{k}.json")) for k in range(2)]
+    X, y = synthetic("covtype", n=6000, seed=2)
+    ref = SVC(C=4.0, gamma=0.5, eps=1e-3, device="cuda").fit(X, y)
+    for k in range(2):
+        assert res[k]["exchange"] == "peer"
+        assert res[k]["iters"] == ref.n_iter_
+        assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
