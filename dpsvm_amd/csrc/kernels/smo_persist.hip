@@ -75,7 +75,9 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     const uint32_t tag = (uint32_t)t + 1u;
     if (wave == 0) {
       uint64_t kh = kKeyNone, kl = kKeyNone;
-      const bool ok = xch_pull(a, (int)(tag & 1u), tag, kh, kl, lane);
+      const bool ok = xch_pull(a, (int)(tag & 1u), tag, kh, kl, lane);  // per-lane minima
+      kh = wave_min_u64(kh);
+      kl = wave_min_u64(kl);
       if (lane == 0) {
         pair_s[0] = kh;
         pair_s[1] = kl;

@@ -49,8 +49,9 @@ __device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, uint6
   }
 }
 
-// every lane of the calling wave: min keys over all ranks' workgroups of
-// parity par, polling until every granule carries `tag`; false on give-up
+// every lane of the calling wave: min keys over ITS entries (lane, lane + 64,
+// ...) of all ranks' workgroups of parity par, polling until every granule
+// carries `tag` (the caller reduces across the wave); false on give-up
 __device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
                                          int lane) {
   const int E = a.xworld * a.fused_G;
