@@ -277,11 +277,11 @@ __global__ __launch_bounds__(64) void xch_ping_kernel(uint64_t* const* peers, in
     if (lane == 0) *ok = 1;
     return;
   }
-  if (lane < world) xch_store(peers[lane] + ping_off + rank, ((uint64_t)tag << 32) | (uint32_t)rank);
+  if (lane < world) xch_store<true>(peers[lane] + ping_off + rank, ((uint64_t)tag << 32) | (uint32_t)rank);
   const uint64_t* mine = peers[rank] + ping_off;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
-    const bool good = lane >= world || (uint32_t)(xch_load(mine + lane) >> 32) == tag;
+    const bool good = lane >= world || (uint32_t)(xch_load<true>(mine + lane) >> 32) == tag;
     if (__all(good)) {
       if (lane == 0) *ok = 1;
       return;

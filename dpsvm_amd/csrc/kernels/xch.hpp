@@ -28,32 +28,35 @@ __device__ __forceinline__ uint64_t* xch_entry(uint64_t* base, int par, const Sm
   return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * kXchGranules;
 }
 
+// system scope across GPUs (xGMI peer memory), agent scope within one GPU
+template <bool kSys>
 __device__ __forceinline__ void xch_store(uint64_t* g, uint64_t v) {
-  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if constexpr (kSys) __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <bool kSys>
 __device__ __forceinline__ uint64_t xch_load(const uint64_t* g) {
-  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if constexpr (kSys) return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// lane p < xworld pushes workgroup b's keys to rank p (parity par)
-__device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, uint64_t kh, uint64_t kl, uint32_t tag,
-                                         int lane) {
+template <bool kSys>
+__device__ __forceinline__ void xch_push_t(const SmoArgs& a, int par, int b, uint64_t kh, uint64_t kl, uint32_t tag,
+                                           int lane) {
   if (lane < a.xworld) {
     uint64_t* g = xch_entry(a.xpeer[lane], par, a, a.xrank, b);
     const uint64_t t = (uint64_t)tag << 32;
-    xch_store(g + 0, t | (kh >> 32));
-    xch_store(g + 1, t | (kh & 0xffffffffull));
-    xch_store(g + 2, t | (kl >> 32));
-    xch_store(g + 3, t | (kl & 0xffffffffull));
+    xch_store<kSys>(g + 0, t | (kh >> 32));
+    xch_store<kSys>(g + 1, t | (kh & 0xffffffffull));
+    xch_store<kSys>(g + 2, t | (kl >> 32));
+    xch_store<kSys>(g + 3, t | (kl & 0xffffffffull));
   }
 }
 
-// every lane of the calling wave: min keys over ITS entries (lane, lane + 64,
-// ...) of all ranks' workgroups of parity par, polling until every granule
-// carries `tag` (the caller reduces across the wave); false on give-up
-__device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
-                                         int lane) {
+template <bool kSys>
+__device__ __forceinline__ bool xch_pull_t(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
+                                           int lane) {
   const int E = a.xworld * a.fused_G;
   const uint64_t* base = a.xpeer[a.xrank] + (int64_t)par * E * kXchGranules;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -62,7 +65,8 @@ __device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag
     bool ok = true;
     for (int e = lane; e < E; e += 64) {
       const uint64_t* g = base + (int64_t)e * kXchGranules;
-      const uint64_t g0 = xch_load(g), g1 = xch_load(g + 1), g2 = xch_load(g + 2), g3 = xch_load(g + 3);
+      const uint64_t g0 = xch_load<kSys>(g), g1 = xch_load<kSys>(g + 1), g2 = xch_load<kSys>(g + 2),
+                     g3 = xch_load<kSys>(g + 3);
       ok &= (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag && (uint32_t)(g2 >> 32) == tag &&
             (uint32_t)(g3 >> 32) == tag;
       const uint64_t vh = (g0 << 32) | (g1 & 0xffffffffull), vl = (g2 << 32) | (g3 & 0xffffffffull);
@@ -77,6 +81,21 @@ __device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag
     if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
     __builtin_amdgcn_s_sleep(1);
   }
+}
+
+// lane p < xworld pushes workgroup b's keys to rank p (parity par)
+__device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, uint64_t kh, uint64_t kl, uint32_t tag,
+                                         int lane) {
+  if (a.xworld > 1) xch_push_t<true>(a, par, b, kh, kl, tag, lane);
+  else xch_push_t<false>(a, par, b, kh, kl, tag, lane);
+}
+
+// every lane of the calling wave: min keys over ITS entries (lane, lane + 64,
+// ...) of all ranks' workgroups of parity par, polling until every granule
+// carries `tag` (the caller reduces across the wave); false on give-up
+__device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
+                                         int lane) {
+  return a.xworld > 1 ? xch_pull_t<true>(a, par, tag, kh, kl, lane) : xch_pull_t<false>(a, par, tag, kh, kl, lane);
 }
 
 }  // namespace dev

@@ -672,7 +672,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     const char* pe = std::getenv("DPSVM_PERSIST");
     int mode = m.p.persist;
     if (pe && pe[0]) mode = pe[0] == '1' ? 2 : 1;
-    want_persist = mode == 2;
+    // auto: persistent unless the exchange is pinned to the communicator all-reduce
+    // (and unless a test forces the per-iteration collective path or eager launches)
+    want_persist = mode == 2 || (mode == 0 && m.p.exchange != 1 && m.p.use_graph && !m.p.force_collectives);
   }
   if (m.dense && ((m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || want_persist)) {
     const bool ok = m.setup_exchange();
