@@ -67,6 +67,9 @@ def parse(argv=None):
                     help="per-iteration key exchange of the dense mode (auto: in-kernel xGMI peer exchange "
                          "when its self test passes, else the communicator all-reduce)")
     ap.add_argument("--device", default="auto", help="auto | cuda | cpu")
+    ap.add_argument("--persist", default="auto", choices=["auto", "off", "on"],
+                    help="dense-mode engine: persistent kernel (auto/on) or one launch per iteration (off)")
+    ap.add_argument("--persist-block", type=int, default=2048)
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
@@ -98,7 +101,7 @@ def main(argv=None) -> int:
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
     cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines,
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
-                    exchange=a.exchange)
+                    exchange=a.exchange, persist=a.persist, persist_block=a.persist_block)
     params = cfg.to_native(X.shape[1])
     comm = make_comm(ctx, a.comm)
     if a.comm == "rccl" and n_ranks == 1:

@@ -67,6 +67,9 @@ inline void usage_train(const char* prog, bool seq) {
                "   --spec N            :  speculative kernel rows per X pass (LRU mode, default 14)\n"
                "   --host-cache-lines N:  pinned host spill tier for evicted kernel rows (LRU mode)\n"
                "   --graph-block N     :  SMO iterations per hipGraph (default 64); --no-graph\n"
+               "   --persist MODE      :  dense engine: auto | off (one launch/iteration) | on (persistent)\n"
+               "   --persist-block N   :  SMO iterations per persistent launch (default 2048)\n"
+               "   --exchange MODE     :  per-iteration keys: auto | allreduce | peer (in-kernel, xGMI)\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
                "   --log-every N       :  progress line every N iterations\n"
@@ -81,7 +84,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
   enum {
     OPT_RANKS = 1000, OPT_CPU, OPT_DEVICE, OPT_SYN, OPT_SEED, OPT_CLIP, OPT_CMB, OPT_XMODE, OPT_SPEC,
     OPT_GB, OPT_NOGRAPH, OPT_CK, OPT_CKE, OPT_RESUME, OPT_METRICS, OPT_LOG, OPT_PREC, OPT_LEGM,
-    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC
+    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -101,6 +104,8 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"precision", required_argument, 0, OPT_PREC}, {"legacy-model", no_argument, 0, OPT_LEGM},
       {"legacy-gamma", no_argument, 0, OPT_LEGG}, {"quiet", no_argument, 0, OPT_QUIET},
       {"skip-accuracy", no_argument, 0, OPT_SKIPACC}, {"verbose", no_argument, 0, OPT_VERBOSE},
+      {"persist", required_argument, 0, OPT_PERSIST}, {"persist-block", required_argument, 0, OPT_PBLOCK},
+      {"exchange", required_argument, 0, OPT_XCH},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -148,6 +153,19 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_QUIET: o.quiet = true; break;
       case OPT_SKIPACC: o.skip_accuracy = true; break;
       case OPT_VERBOSE: o.p.verbose = true; break;
+      case OPT_PERSIST: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "off" && v != "on") usage_train(argv[0], seq);
+        o.p.persist = v == "on" ? 2 : v == "off" ? 1 : 0;
+        break;
+      }
+      case OPT_PBLOCK: o.p.persist_block = atoi(optarg); break;
+      case OPT_XCH: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "allreduce" && v != "peer") usage_train(argv[0], seq);
+        o.p.exchange = v == "peer" ? 2 : v == "allreduce" ? 1 : 0;
+        break;
+      }
       default:
         std::cerr << "\nERROR: Unknown option: -" << (char)c << "\n";
         usage_train(argv[0], seq);
