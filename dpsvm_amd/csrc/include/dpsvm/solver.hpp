@@ -62,7 +62,7 @@ struct GpuSetupInfo {
   int blocks = 0;
   size_t bytes_device = 0;
   std::string iteration;  // "fused-dense" | "fused-cache" | "chain" (rows/step/finalize)
-  std::string exchange;   // per-iteration key exchange: "none" | "allreduce" | "peer"
+  std::string exchange;   // per-iteration key exchange: "none" | "allreduce" | "peer" | "loopback" (1 rank)
 };
 
 class GpuSolver {

@@ -690,7 +690,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       a.xtimeout_ticks = (int64_t)(tmo * 1e8);
     }
   }
-  m.info.exchange = m.xch ? "peer" : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
+  m.info.exchange = m.xch ? (m.world > 1 ? "peer" : "loopback")
+                          : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
   m.persist = want_persist && m.xch;
   if (m.persist) m.info.iteration = "persistent-dense";
   m.info.bytes_device = m.bytes;

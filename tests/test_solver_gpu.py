@@ -162,7 +162,7 @@ def test_cache_policies_bitwise_identical():
 def test_gpu_fault_injection_and_verify(monkeypatch, C):
     X, y = synthetic("blobs", n=3000, d=8, seed=3, sep=1.0)
     monkeypatch.setenv("DPSVM_FAULT", "nan@200")
-    clf = SVC(C=1.0, gamma=0.1, device="cuda", graph_block=16).fit(X, y)
+    clf = SVC(C=1.0, gamma=0.1, device="cuda", graph_block=16, persist_block=16).fit(X, y)
     assert clf.status_ == 4 and not clf.converged_ and clf.n_iter_ >= 200
     monkeypatch.delenv("DPSVM_FAULT")
     monkeypatch.setenv("DPSVM_VERIFY", "1")
@@ -219,10 +219,10 @@ def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
     monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
     X, y = synthetic("covtype", n=6000, seed=2)
     kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
-    ref = SVC(**kw).fit(X, y)
+    ref = SVC(persist="off", **kw).fit(X, y)
     assert ref.setup_info_["exchange"] == "none"
-    loop = SVC(exchange="peer", **kw).fit(X, y)
-    assert loop.setup_info_["exchange"] == "peer"
+    loop = SVC(exchange="peer", persist="off", **kw).fit(X, y)
+    assert loop.setup_info_["exchange"] == "loopback" and loop.setup_info_["iteration"] == "fused-dense"
     assert loop.n_iter_ == ref.n_iter_ and np.array_equal(loop.alpha_, ref.alpha_)
     g = C.ThreadCommGroup(2)
     comms = [g.comm(r) for r in range(2)]
