@@ -12,10 +12,11 @@
 //   1. wave 0 polls the keys tagged t (all ranks' workgroups), broadcasts the
 //      minima through LDS (barrier 1);
 //   2. pair (i_hi, i_lo), eta from the two sample rows, alpha update;
-//      alphas of older pairs come from memory, committed by workgroup 0 with
-//      write-through stores that it drains before publishing its keys — so a
-//      workgroup that has seen those keys sees the commit; the previous pair is
-//      still pending and is applied from registers;
+//      alphas of older pairs come from memory: workgroup 0 commits pair t with
+//      write-through stores right after publishing its keys t+1 and drains
+//      them (long complete by then) before publishing t+2 — a workgroup that
+//      has seen keys t+2 sees the commit; the last two pairs are applied from
+//      registers;
 //   3. f update of the own rows from the Gram rows K[i_hi][.], K[i_lo][.],
 //      classification, per-workgroup keys (barrier 2), published tagged t+1.
 // Alpha memory is written only by workgroup 0, thread 0, in program order
@@ -67,8 +68,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   if (s0.done != kRunning) return;
   int t = s0.iter, done = kRunning;
   float b_hi = s0.b_hi, b_lo = s0.b_lo;
-  int p_hi = -1, p_lo = -1;  // pending pair (applied by every workgroup, committed one iteration later)
-  float pa_hi = 0.f, pa_lo = 0.f;
+  // the last two pairs are applied from registers: workgroup 0 commits pair t
+  // right AFTER publishing its keys t+1 and drains that store before
+  // publishing t+2, so the commit is visible from iteration t+2 on
+  int p_hi = -1, p_lo = -1, q_hi = -1, q_lo = -1;  // pairs t-1 (p) and t-2 (q)
+  float pa_hi = 0.f, pa_lo = 0.f, qa_hi = 0.f, qa_lo = 0.f;
 
   for (int step = 0; step < steps; ++step) {
     // ---- 1. keys tagged t+1 (produced by iteration t) ----
@@ -112,8 +116,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
     const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
     const float dist2 = wave_dist2(xh, xl, a.dp, lane);  // identical tree in every wave
-    const float a_hi_old = i_hi == p_hi ? pa_hi : (i_hi == p_lo ? pa_lo : m_hi);
-    const float a_lo_old = i_lo == p_hi ? pa_hi : (i_lo == p_lo ? pa_lo : m_lo);
+    auto latest = [&](int i, float m) {
+      return i == p_hi ? pa_hi : i == p_lo ? pa_lo : i == q_hi ? qa_hi : i == q_lo ? qa_lo : m;
+    };
+    const float a_hi_old = latest(i_hi, m_hi);
+    const float a_lo_old = latest(i_lo, m_lo);
     float c_hi = 0.f, c_lo = 0.f, a_hi_new = a_hi_old, a_lo_new = a_lo_old;
     const int iter = t + 1;
     if (!isfinite(bh) || !isfinite(bl)) {
@@ -133,11 +140,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     b_lo = bl;
     if (done == kNonFinite) break;
 
-    // commit the pending pair (write-through; drained before this workgroup publishes)
-    if (lead && p_hi >= 0) {
-      store_alpha(a.alpha + p_lo, pa_lo);
-      store_alpha(a.alpha + p_hi, pa_hi);  // hi written last (svmTrainMain.cpp:298-299)
-    }
+    q_hi = p_hi;
+    q_lo = p_lo;
+    qa_hi = pa_hi;
+    qa_lo = pa_lo;
     p_hi = i_hi;
     p_lo = i_lo;
     pa_hi = a_hi_new;
@@ -178,10 +184,15 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
         nh = kscr[w] < nh ? kscr[w] : nh;
         nlk = kscr[4 + w] < nlk ? kscr[4 + w] : nlk;
       }
-      // the alpha commit above (thread 0 of this wave) lands before the keys
+      // the previous iteration's alpha commit (thread 0 of this wave) has
+      // landed before these keys: anyone who sees them sees that commit
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t otag = (uint32_t)t + 1u;
       xch_push(a, (int)(otag & 1u), blockIdx.x, nh, nlk, otag, lane);
+      if (lead) {  // commit this iteration's pair (write-through, drained next iteration)
+        store_alpha(a.alpha + p_lo, pa_lo);
+        store_alpha(a.alpha + p_hi, pa_hi);  // hi written last (svmTrainMain.cpp:298-299)
+      }
     }
   }
 
