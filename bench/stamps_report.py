@@ -44,6 +44,27 @@ def main_lru(path):
     print(json.dumps(out, indent=1))
 
 
+PERSIST_PHASES = ["poll", "alpha_update", "f_update", "key_reduce", "publish", "to_next_poll"]
+
+
+def main_persist(path):
+    """smo_persist slots: 0 poll start, 1 pair known, 2 alpha update, 3 f
+    update, 4 keys reduced, 5 published; ring index = iteration."""
+    a = np.fromfile(path, dtype=np.uint64).reshape(RING, 2, SLOTS).astype(np.int64)[:, :, :6]
+    out = {}
+    for b, name in ((0, "wg0"), (1, "wglast")):
+        t = a[:, b, :]
+        ok = (t > 0).all(1)
+        d = np.diff(t, axis=1) * 10.0
+        nxt = (np.roll(t[:, 0], -1) - t[:, 5]) * 10.0  # next iteration's poll start - this publish
+        okn = ok & np.roll(ok, -1)
+        out[name] = {ph + "_ns": float(np.median(d[ok, i])) for i, ph in enumerate(PERSIST_PHASES[:5])}
+        out[name]["to_next_poll_ns"] = float(np.median(nxt[okn]))
+        per = np.diff(t[:, 0]) * 10.0
+        out[name]["period_ns"] = float(np.median(per[(per > 0) & ok[1:] & ok[:-1]]))
+    print(json.dumps(out, indent=1))
+
+
 def main(path):
     a = np.fromfile(path, dtype=np.uint64).reshape(RING, 2, SLOTS).astype(np.int64)
     ok = (a[:, 0, 0] > 0) & (a[:, 0, 4] > 0) & (a[:, 1, 4] > 0)
@@ -73,5 +94,7 @@ def main(path):
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[2] == "--lru":
         main_lru(sys.argv[1])
+    elif len(sys.argv) > 2 and sys.argv[2] == "--persist":
+        main_persist(sys.argv[1])
     else:
         main(sys.argv[1])

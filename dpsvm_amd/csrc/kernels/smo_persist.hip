@@ -74,7 +74,16 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   int p_hi = -1, p_lo = -1, q_hi = -1, q_lo = -1;  // pairs t-1 (p) and t-2 (q)
   float pa_hi = 0.f, pa_lo = 0.f, qa_hi = 0.f, qa_lo = 0.f;
 
+  // diagnostics (DPSVM_STAMPS): thread 0 of workgroups 0 and G-1 keeps 6
+  // s_memrealtime stamps per iteration in registers and stores them after
+  // publishing (0 poll start, 1 pair known, 2 alpha update, 3 f update,
+  // 4 keys reduced, 5 published)
+  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+  uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
+#define PSTAMP(i) \
+  if (stamping) stv[i] = __builtin_amdgcn_s_memrealtime()
   for (int step = 0; step < steps; ++step) {
+    PSTAMP(0);
     // ---- 1. keys tagged t+1 (produced by iteration t) ----
     const uint32_t tag = (uint32_t)t + 1u;
     if (wave == 0) {
@@ -100,6 +109,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     }
     const int i_hi = (int)key_index(kh), i_lo = (int)key_index(kl);
     const float bh = key_value(kh), bl = -key_value(kl);
+    PSTAMP(1);
 
     // ---- 2. one round trip: Gram rows of the own rows, sample rows, pair state ----
     const float* line_hi = a.lines + (int64_t)i_hi * a.ldl;
@@ -138,6 +148,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     }
     b_hi = bh;
     b_lo = bl;
+    PSTAMP(2);
     if (done == kNonFinite) break;
 
     q_hi = p_hi;
@@ -169,6 +180,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       if (in_up(al[k], yv[k], a.C)) { const uint64_t key = make_key(f[k], (uint32_t)g); nh = key < nh ? key : nh; }
       if (in_low(al[k], yv[k], a.C)) { const uint64_t key = make_key(-f[k], (uint32_t)g); nlk = key < nlk ? key : nlk; }
     }
+    PSTAMP(3);
     if (done != kRunning) break;  // uniform: the last update is applied, no keys needed
 
     nh = wave_min_u64(nh);
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
         nh = kscr[w] < nh ? kscr[w] : nh;
         nlk = kscr[4 + w] < nlk ? kscr[4 + w] : nlk;
       }
+      PSTAMP(4);
       // the previous iteration's alpha commit (thread 0 of this wave) has
       // landed before these keys: anyone who sees them sees that commit
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -193,9 +206,16 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
         store_alpha(a.alpha + p_lo, pa_lo);
         store_alpha(a.alpha + p_hi, pa_hi);  // hi written last (svmTrainMain.cpp:298-299)
       }
+      PSTAMP(5);
+      if (stamping) {
+        uint64_t* dst = a.stamps + ((size_t)(t % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dst[i] = stv[i];
+      }
     }
   }
 
+#undef PSTAMP
   // ---- exit: own rows' f back to memory; workgroup 0 commits the last pair and the state ----
 #pragma unroll
   for (int k = 0; k < kPersistMaxRows; ++k) {
