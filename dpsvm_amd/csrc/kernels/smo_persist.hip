@@ -9,8 +9,9 @@
 //
 // Iteration t in workgroup b (identical arithmetic to smo_fused.hip, so the
 // two paths are bit-identical):
-//   1. wave 0 polls the keys tagged t (all ranks' workgroups), broadcasts the
-//      minima through LDS (barrier 1);
+//   1. every thread polls its share of the keys tagged t (all ranks'
+//      workgroups; two load rounds in flight), minima combined through LDS
+//      (barrier 1);
 //   2. pair (i_hi, i_lo), eta from the two sample rows, alpha update;
 //      alphas of older pairs come from memory: workgroup 0 commits pair t with
 //      write-through stores right after publishing its keys t+1 and drains
@@ -46,8 +47,8 @@ __device__ __forceinline__ void store_alpha(float* p, float v) {
 __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
-  __shared__ uint64_t pair_s[2];
-  __shared__ int fail_s;
+  __shared__ uint64_t pscr[8];
+  __shared__ int fail_s[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int rpt = a.fused_rows / kFusedThreads;  // rows per thread
@@ -86,20 +87,28 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     PSTAMP(0);
     // ---- 1. keys tagged t+1 (produced by iteration t) ----
     const uint32_t tag = (uint32_t)t + 1u;
-    if (wave == 0) {
-      uint64_t kh = kKeyNone, kl = kKeyNone;
-      const bool ok = xch_pull(a, (int)(tag & 1u), tag, kh, kl, lane);  // per-lane minima
-      kh = wave_min_u64(kh);
-      kl = wave_min_u64(kl);
+    uint64_t kh, kl;
+    {
+      // every thread watches its share of the entries (two load rounds in flight)
+      uint64_t h = kKeyNone, l = kKeyNone;
+      const bool ok = xch_poll(a, (int)(tag & 1u), tag, h, l, tid, kFusedThreads);
+      h = wave_min_u64(h);
+      l = wave_min_u64(l);
       if (lane == 0) {
-        pair_s[0] = kh;
-        pair_s[1] = kl;
-        fail_s = ok ? 0 : 1;
+        pscr[wave] = h;
+        pscr[4 + wave] = l;
+        fail_s[wave] = ok ? 0 : 1;
+      }
+      __syncthreads();
+      kh = pscr[0];
+      kl = pscr[4];
+#pragma unroll
+      for (int w = 1; w < kFusedThreads / 64; ++w) {
+        kh = pscr[w] < kh ? pscr[w] : kh;
+        kl = pscr[4 + w] < kl ? pscr[4 + w] : kl;
       }
     }
-    __syncthreads();
-    const uint64_t kh = pair_s[0], kl = pair_s[1];
-    if (fail_s) {
+    if (fail_s[0] | fail_s[1] | fail_s[2] | fail_s[3]) {
       done = kCommFail;
       break;
     }

@@ -28,17 +28,24 @@ __device__ __forceinline__ uint64_t* xch_entry(uint64_t* base, int par, const Sm
   return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * kXchGranules;
 }
 
+// global (address space 1) pointers: global_ instructions count only in
+// vmcnt, so two poll rounds can be in flight (flat ops also count in lgkmcnt
+// and make the compiler drain everything before each check)
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
 // system scope across GPUs (xGMI peer memory), agent scope within one GPU
 template <bool kSys>
 __device__ __forceinline__ void xch_store(uint64_t* g, uint64_t v) {
-  if constexpr (kSys) __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  gu64* p = (gu64*)g;
+  if constexpr (kSys) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool kSys>
 __device__ __forceinline__ uint64_t xch_load(const uint64_t* g) {
-  if constexpr (kSys) return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  gu64* p = (gu64*)g;
+  if constexpr (kSys) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool kSys>
@@ -81,6 +88,64 @@ __device__ __forceinline__ bool xch_pull_t(const SmoArgs& a, int par, uint32_t t
     if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
     __builtin_amdgcn_s_sleep(1);
   }
+}
+
+// Workgroup-parallel poll for the persistent engine: thread `tid` of the
+// workgroup watches entries tid, tid + 256, ... and keeps two load rounds in
+// flight (the next round is issued before the previous one is checked), so
+// an arrival is seen about half a round trip after it lands instead of up to
+// a full one.  Returns this thread's minima (the caller reduces); false on
+// give-up.
+template <bool kSys>
+__device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
+                                           int tid, int nthreads) {
+  const int E = a.xworld * a.fused_G;
+  const uint64_t* base = a.xpeer[a.xrank] + (int64_t)par * E * kXchGranules;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t h = kKeyNone, l = kKeyNone;
+  for (int c = 0; c < E; c += nthreads) {
+    const int e = c + tid;
+    const bool mine = e < E;
+    const uint64_t* g = base + (int64_t)(mine ? e : 0) * kXchGranules;
+    auto ready = [&](uint64_t x0, uint64_t x1, uint64_t x2, uint64_t x3) {
+      return !mine || ((uint32_t)(x0 >> 32) == tag && (uint32_t)(x1 >> 32) == tag && (uint32_t)(x2 >> 32) == tag &&
+                       (uint32_t)(x3 >> 32) == tag);
+    };
+    uint64_t a0 = xch_load<kSys>(g), a1 = xch_load<kSys>(g + 1), a2 = xch_load<kSys>(g + 2),
+             a3 = xch_load<kSys>(g + 3);
+    uint64_t r0, r1, r2, r3;
+    while (true) {
+      const uint64_t b0 = xch_load<kSys>(g), b1 = xch_load<kSys>(g + 1), b2 = xch_load<kSys>(g + 2),
+                     b3 = xch_load<kSys>(g + 3);
+      if (__all(ready(a0, a1, a2, a3))) {
+        r0 = a0; r1 = a1; r2 = a2; r3 = a3;
+        break;
+      }
+      a0 = xch_load<kSys>(g);
+      a1 = xch_load<kSys>(g + 1);
+      a2 = xch_load<kSys>(g + 2);
+      a3 = xch_load<kSys>(g + 3);
+      if (__all(ready(b0, b1, b2, b3))) {
+        r0 = b0; r1 = b1; r2 = b2; r3 = b3;
+        break;
+      }
+      if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
+    }
+    if (mine) {
+      const uint64_t vh = (r0 << 32) | (r1 & 0xffffffffull), vl = (r2 << 32) | (r3 & 0xffffffffull);
+      h = vh < h ? vh : h;
+      l = vl < l ? vl : l;
+    }
+  }
+  kh = h;
+  kl = l;
+  return true;
+}
+
+__device__ __forceinline__ bool xch_poll(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl, int tid,
+                                         int nthreads) {
+  return a.xworld > 1 ? xch_poll_t<true>(a, par, tag, kh, kl, tid, nthreads)
+                      : xch_poll_t<false>(a, par, tag, kh, kl, tid, nthreads);
 }
 
 // lane p < xworld pushes workgroup b's keys to rank p (parity par)
