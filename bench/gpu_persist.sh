@@ -4,8 +4,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp DPSVM_XCH_TIMEOUT_S=20
 timeout -k 10 300 python -m pytest tests/test_solver_gpu.py -q -x -k "persistent or peer_exchange" > gpurun_out/pytest_persist.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_persist.log
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_persist.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench/iter_latency.py --out gpurun_out/iter_latency.jsonl > gpurun_out/iter_latency.log 2>&1
-rc=$?; echo "iter_latency rc=$rc"; grep smo_loop gpurun_out/iter_latency.log
+DPSVM_STAMPS=/tmp/pst timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-accuracy > gpurun_out/pstamps_bench.log 2>&1 || exit $?
+python bench/stamps_report.py /tmp/pst.rank0 --persist > gpurun_out/persist_stamps.json 2>&1; cat gpurun_out/persist_stamps.json
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 > gpurun_out/bench1.log 2>&1
+rc=$?; echo "bench rc=$rc"; grep '^{' gpurun_out/bench1.log | tail -1
 exit $rc

@@ -49,30 +49,30 @@ __device__ __forceinline__ void commit_pending(const SmoArgs& a, const FusedRec&
   }
 }
 
-// per-workgroup min of two keys -> p_out[blockIdx], or pushed to every rank
-// (peer exchange, parity xpar, tag) (the kernel's one barrier)
-__device__ __forceinline__ void store_block_keys(const SmoArgs& a, uint64_t kh, uint64_t kl, uint64_t* p_out,
-                                                 uint64_t* scr, int xpar, uint32_t tag) {
+// per-workgroup min of two keys -> p_out[blockIdx], or (peer exchange)
+// pushed with the alphas of their rows to every rank, parity xpar / tag
+// (the kernel's one barrier)
+__device__ __forceinline__ void store_block_keys(const SmoArgs& a, XKeys k, uint64_t* p_out, uint64_t* scr,
+                                                 float* fscr, int xpar, uint32_t tag) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  kh = wave_min_u64(kh);
-  kl = wave_min_u64(kl);
+  k = wave_min_xk(k);
   if (lane == 0) {
-    scr[wave] = kh;
-    scr[4 + wave] = kl;
+    scr[wave] = k.kh;
+    scr[4 + wave] = k.kl;
+    fscr[wave] = k.ah;
+    fscr[4 + wave] = k.al;
   }
   __syncthreads();
   if (a.xworld > 0) {
     if (wave == 0) {
 #pragma unroll
-      for (int w = 1; w < kFusedThreads / 64; ++w) {
-        kh = scr[w] < kh ? scr[w] : kh;
-        kl = scr[4 + w] < kl ? scr[4 + w] : kl;
-      }
-      xch_push(a, xpar, blockIdx.x, kh, kl, tag, lane);
+      for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(k, XKeys{scr[w], scr[4 + w], fscr[w], fscr[4 + w]});
+      xch_push(a, xpar, blockIdx.x, k, tag, lane);
     }
     return;
   }
   if (threadIdx.x == 0) {
+    uint64_t kh = k.kh, kl = k.kl;
 #pragma unroll
     for (int w = 1; w < kFusedThreads / 64; ++w) {
       kh = scr[w] < kh ? scr[w] : kh;
@@ -92,6 +92,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
                                                                   FusedRec* __restrict__ r_out) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
+  __shared__ float fscr[8];
   const int tid = threadIdx.x, lane = tid & 63;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
@@ -116,18 +117,18 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   }
 
   if (mode == 0) {  // initial selection over the current f / alpha
-    uint64_t kh = kKeyNone, kl = kKeyNone;
+    XKeys k = xk_none();
     for (int64_t j = j0; j < row_end; j += kFusedThreads) {
       const int64_t g = a.off + j;
       const float fj = j == j0 ? f0 : a.f[j];
       const float av = j == j0 ? a0 : a.alpha[g];
       const float yv = j == j0 ? y0 : a.y[g];
-      if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); kh = k < kh ? k : kh; }
-      if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); kl = k < kl ? k : kl; }
+      if (in_up(av, yv, a.C)) xk_min(k, XKeys{make_key(fj, (uint32_t)g), kKeyNone, av, 0.f});
+      if (in_low(av, yv, a.C)) xk_min(k, XKeys{kKeyNone, make_key(-fj, (uint32_t)g), 0.f, av});
     }
     // peer exchange: the seed's keys carry tag iter0 + 1 (r_in = the seed record)
     const uint32_t tag = a.xworld > 0 ? (uint32_t)r_in->iter + 1u : 0u;
-    store_block_keys(a, kh, kl, p_out, kscr, (int)(tag & 1u), tag);
+    store_block_keys(a, k, p_out, kscr, fscr, (int)(tag & 1u), tag);
     return;
   }
 
@@ -142,8 +143,9 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       kl = v.y < kl ? v.y : kl;
     }
   }
+  XKeys xk = xk_none();
   if (rin.done == kRunning && a.xworld > 0 &&
-      !xch_pull(a, (int)(((uint32_t)rin.iter + 1u) & 1u), (uint32_t)rin.iter + 1u, kh, kl, lane)) {
+      !xch_poll(a, (int)(((uint32_t)rin.iter + 1u) & 1u), (uint32_t)rin.iter + 1u, xk, lane, 64)) {
     // a peer stopped publishing: give up (every rank that times out stops the same way)
     if (lead) {
       commit_pending(a, rin);
@@ -154,6 +156,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       publish_status(a.status, rin.iter, kCommFail, rin.b_hi, rin.b_lo);
     }
     return;
+  }
+  if (a.xworld > 0) {  // per-lane minima of the polled entries (alphas unused: memory + record)
+    kh = xk.kh;
+    kl = xk.kl;
   }
   if (rin.done != kRunning) {
     if (lead) {
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
 
   // ---- 3. f update + classification of this workgroup's rows ----
   const bool upd_f = c_hi != 0.f || c_lo != 0.f;
-  uint64_t nh = kKeyNone, nlk = kKeyNone;
+  XKeys nk = xk_none();
   for (int64_t j = j0; j < row_end; j += kFusedThreads) {
     const bool first = j == j0;
     const int64_t g = a.off + j;
@@ -260,13 +266,13 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       else if (g == rin.i_lo) av = rin.a_lo;
       else av = first ? a0 : a.alpha[g];
       const float yv = first ? y0 : a.y[g];
-      if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
-      if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
+      if (in_up(av, yv, a.C)) xk_min(nk, XKeys{make_key(fj, (uint32_t)g), kKeyNone, av, 0.f});
+      if (in_low(av, yv, a.C)) xk_min(nk, XKeys{kKeyNone, make_key(-fj, (uint32_t)g), 0.f, av});
     }
   }
   stamp(rin.iter, 3, 0);
   if (done != kRunning) return;  // uniform
-  store_block_keys(a, nh, nlk, p_out, kscr, (int)(((uint32_t)iter + 1u) & 1u), (uint32_t)iter + 1u);
+  store_block_keys(a, nk, p_out, kscr, fscr, (int)(((uint32_t)iter + 1u) & 1u), (uint32_t)iter + 1u);
   stamp(rin.iter, 4, 0);
 }
 

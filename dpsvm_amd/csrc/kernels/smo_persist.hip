@@ -9,19 +9,19 @@
 //
 // Iteration t in workgroup b (identical arithmetic to smo_fused.hip, so the
 // two paths are bit-identical):
-//   1. every thread polls its share of the keys tagged t (all ranks'
-//      workgroups; two load rounds in flight), minima combined through LDS
-//      (barrier 1);
-//   2. pair (i_hi, i_lo), eta from the two sample rows, alpha update;
-//      alphas of older pairs come from memory: workgroup 0 commits pair t with
-//      write-through stores right after publishing its keys t+1 and drains
-//      them (long complete by then) before publishing t+2 — a workgroup that
-//      has seen keys t+2 sees the commit; the last two pairs are applied from
-//      registers;
-//   3. f update of the own rows from the Gram rows K[i_hi][.], K[i_lo][.],
-//      classification, per-workgroup keys (barrier 2), published tagged t+1.
-// Alpha memory is written only by workgroup 0, thread 0, in program order
-// (commits during the run, the last pair at exit): no write-write race.
+//   1. every thread polls its share of the publications tagged t (all ranks'
+//      workgroups; two load rounds in flight): the minima, with the alphas of
+//      the rows behind them, combined through LDS (barrier 1);
+//   2. pair (i_hi, i_lo), eta from the two sample rows, alpha update — the
+//      pair's current alphas arrive with the keys from their owners'
+//      registers, so alpha memory is never read during the run (a plain or
+//      sc1 load could hit a stale line in this XCD's L2);
+//   3. f / alpha update of the own rows in registers from the Gram rows
+//      K[i_hi][.], K[i_lo][.], classification, per-workgroup keys with their
+//      alphas (barrier 2), published tagged t+1.
+// Workgroup 0 stores every pair's new alphas as it goes (every rank computes
+// every pair: the full alpha vector on every rank; nobody reads it before the
+// launch ends); at exit every workgroup writes its own rows' f.
 // Reference per-iteration path: svmTrainMain.cpp:235-310.
 #include <hip/hip_runtime.h>
 
@@ -37,17 +37,11 @@ namespace dev {
 
 constexpr int kPersistMaxRows = 4;  // rows per thread (fused_rows <= 1024)
 
-__device__ __forceinline__ float load_alpha(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_alpha(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
   __shared__ uint64_t pscr[8];
+  __shared__ float pfs[8], kfs[8];
   __shared__ int fail_s[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
@@ -69,12 +63,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   if (s0.done != kRunning) return;
   int t = s0.iter, done = kRunning;
   float b_hi = s0.b_hi, b_lo = s0.b_lo;
-  // the last two pairs are applied from registers: workgroup 0 commits pair t
-  // right AFTER publishing its keys t+1 and drains that store before
-  // publishing t+2, so the commit is visible from iteration t+2 on
-  int p_hi = -1, p_lo = -1, q_hi = -1, q_lo = -1;  // pairs t-1 (p) and t-2 (q)
-  float pa_hi = 0.f, pa_lo = 0.f, qa_hi = 0.f, qa_lo = 0.f;
-
   // diagnostics (DPSVM_STAMPS): thread 0 of workgroups 0 and G-1 keeps 6
   // s_memrealtime stamps per iteration in registers and stores them after
   // publishing (0 poll start, 1 pair known, 2 alpha update, 3 f update,
@@ -87,27 +75,27 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     PSTAMP(0);
     // ---- 1. keys tagged t+1 (produced by iteration t) ----
     const uint32_t tag = (uint32_t)t + 1u;
-    uint64_t kh, kl;
+    XKeys pk;
     {
       // every thread watches its share of the entries (two load rounds in flight)
-      uint64_t h = kKeyNone, l = kKeyNone;
-      const bool ok = xch_poll(a, (int)(tag & 1u), tag, h, l, tid, kFusedThreads);
-      h = wave_min_u64(h);
-      l = wave_min_u64(l);
+      XKeys m = xk_none();
+      bool ok = true;
+      if (a.xpoll == 0) ok = xch_poll(a, (int)(tag & 1u), tag, m, tid, kFusedThreads);
+      else if (wave == 0) ok = xch_poll(a, (int)(tag & 1u), tag, m, lane, 64);
+      m = wave_min_xk(m);
       if (lane == 0) {
-        pscr[wave] = h;
-        pscr[4 + wave] = l;
+        pscr[wave] = m.kh;
+        pscr[4 + wave] = m.kl;
+        pfs[wave] = m.ah;
+        pfs[4 + wave] = m.al;
         fail_s[wave] = ok ? 0 : 1;
       }
       __syncthreads();
-      kh = pscr[0];
-      kl = pscr[4];
+      pk = XKeys{pscr[0], pscr[4], pfs[0], pfs[4]};
 #pragma unroll
-      for (int w = 1; w < kFusedThreads / 64; ++w) {
-        kh = pscr[w] < kh ? pscr[w] : kh;
-        kl = pscr[4 + w] < kl ? pscr[4 + w] : kl;
-      }
+      for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(pk, XKeys{pscr[w], pscr[4 + w], pfs[w], pfs[4 + w]});
     }
+    const uint64_t kh = pk.kh, kl = pk.kl;
     if (fail_s[0] | fail_s[1] | fail_s[2] | fail_s[3]) {
       done = kCommFail;
       break;
@@ -130,16 +118,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       khv[k] = has[k] ? line_hi[j] : 0.f;
       klv[k] = has[k] ? line_lo[j] : 0.f;
     }
-    const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];
-    const float m_hi = load_alpha(a.alpha + i_hi), m_lo = load_alpha(a.alpha + i_lo);
+    const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];  // read-only during the run
     const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
     const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
     const float dist2 = wave_dist2(xh, xl, a.dp, lane);  // identical tree in every wave
-    auto latest = [&](int i, float m) {
-      return i == p_hi ? pa_hi : i == p_lo ? pa_lo : i == q_hi ? qa_hi : i == q_lo ? qa_lo : m;
-    };
-    const float a_hi_old = latest(i_hi, m_hi);
-    const float a_lo_old = latest(i_lo, m_lo);
+    const float a_hi_old = pk.ah, a_lo_old = pk.al;     // the owners' current values
     float c_hi = 0.f, c_lo = 0.f, a_hi_new = a_hi_old, a_lo_new = a_lo_old;
     const int iter = t + 1;
     if (!isfinite(bh) || !isfinite(bl)) {
@@ -159,20 +142,16 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     b_lo = bl;
     PSTAMP(2);
     if (done == kNonFinite) break;
+    if (lead) {  // alpha memory is write-only during the run (read after the launch)
+      a.alpha[i_lo] = a_lo_new;
+      a.alpha[i_hi] = a_hi_new;  // hi written last (svmTrainMain.cpp:298-299)
+    }
 
-    q_hi = p_hi;
-    q_lo = p_lo;
-    qa_hi = pa_hi;
-    qa_lo = pa_lo;
-    p_hi = i_hi;
-    p_lo = i_lo;
-    pa_hi = a_hi_new;
-    pa_lo = a_lo_new;
     t = iter;
 
     // ---- 3. f update + classification of the own rows ----
     const bool upd_f = c_hi != 0.f || c_lo != 0.f;
-    uint64_t nh = kKeyNone, nlk = kKeyNone;
+    XKeys nk = xk_none();
 #pragma unroll
     for (int k = 0; k < kPersistMaxRows; ++k) {
       if (!has[k]) continue;
@@ -186,35 +165,26 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       }
       if (g == i_lo) al[k] = a_lo_new;
       if (g == i_hi) al[k] = a_hi_new;  // hi wins when i_hi == i_lo
-      if (in_up(al[k], yv[k], a.C)) { const uint64_t key = make_key(f[k], (uint32_t)g); nh = key < nh ? key : nh; }
-      if (in_low(al[k], yv[k], a.C)) { const uint64_t key = make_key(-f[k], (uint32_t)g); nlk = key < nlk ? key : nlk; }
+      if (in_up(al[k], yv[k], a.C)) xk_min(nk, XKeys{make_key(f[k], (uint32_t)g), kKeyNone, al[k], 0.f});
+      if (in_low(al[k], yv[k], a.C)) xk_min(nk, XKeys{kKeyNone, make_key(-f[k], (uint32_t)g), 0.f, al[k]});
     }
     PSTAMP(3);
     if (done != kRunning) break;  // uniform: the last update is applied, no keys needed
 
-    nh = wave_min_u64(nh);
-    nlk = wave_min_u64(nlk);
+    nk = wave_min_xk(nk);
     if (lane == 0) {
-      kscr[wave] = nh;
-      kscr[4 + wave] = nlk;
+      kscr[wave] = nk.kh;
+      kscr[4 + wave] = nk.kl;
+      kfs[wave] = nk.ah;
+      kfs[4 + wave] = nk.al;
     }
     __syncthreads();
     if (wave == 0) {
 #pragma unroll
-      for (int w = 1; w < kFusedThreads / 64; ++w) {
-        nh = kscr[w] < nh ? kscr[w] : nh;
-        nlk = kscr[4 + w] < nlk ? kscr[4 + w] : nlk;
-      }
+      for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(nk, XKeys{kscr[w], kscr[4 + w], kfs[w], kfs[4 + w]});
       PSTAMP(4);
-      // the previous iteration's alpha commit (thread 0 of this wave) has
-      // landed before these keys: anyone who sees them sees that commit
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t otag = (uint32_t)t + 1u;
-      xch_push(a, (int)(otag & 1u), blockIdx.x, nh, nlk, otag, lane);
-      if (lead) {  // commit this iteration's pair (write-through, drained next iteration)
-        store_alpha(a.alpha + p_lo, pa_lo);
-        store_alpha(a.alpha + p_hi, pa_hi);  // hi written last (svmTrainMain.cpp:298-299)
-      }
+      xch_push(a, (int)(otag & 1u), blockIdx.x, nk, otag, lane);
       PSTAMP(5);
       if (stamping) {
         uint64_t* dst = a.stamps + ((size_t)(t % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots;
@@ -225,17 +195,13 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   }
 
 #undef PSTAMP
-  // ---- exit: own rows' f back to memory; workgroup 0 commits the last pair and the state ----
+  // ---- exit: own rows' f back to memory; workgroup 0 writes the state ----
 #pragma unroll
   for (int k = 0; k < kPersistMaxRows; ++k) {
     const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
     if (has[k]) a.f[j] = f[k];
   }
   if (lead) {
-    if (p_hi >= 0) {
-      store_alpha(a.alpha + p_lo, pa_lo);
-      store_alpha(a.alpha + p_hi, pa_hi);
-    }
     FusedRec o;
     o.i_hi = o.i_lo = -1;
     o.a_hi = o.a_lo = 0.f;

@@ -1,16 +1,19 @@
-// Peer exchange of per-workgroup selection keys (dense fused mode, world > 1):
-// the in-kernel replacement of the per-iteration all-reduce.
+// Peer exchange of per-workgroup selection keys (dense engines, and the
+// in-kernel replacement of the per-iteration all-reduce when world > 1).
 //
-// Each workgroup of launch t pushes its (up, low) keys to every rank as four
-// 8-byte granules {tag, 32-bit half} with system-scope relaxed stores (one
-// aligned store per granule: never torn; the data IS the flag, no fence).
-// Launch t+1 on every rank polls its own receive buffer with system-scope
-// loads until every granule of the parity carries the expected tag, then
-// reduces exactly as from an all-reduced buffer — so every rank derives the
-// same pair.  Tags are the iteration count + 1 (never 0; buffers are zeroed
-// before each solve); keys tagged T live in parity T & 1, and a rank cannot lap a peer: its
-// launch t+2 needs that peer's launch-t+1 keys, which the peer publishes only
-// after it has read the parity t+2 overwrites.
+// Each workgroup pushes its (up, low) keys — and the current alphas of the
+// two rows behind them — to every rank as six 8-byte granules {tag, 32-bit
+// value} with relaxed atomic stores (one aligned store per granule: never
+// torn; the data IS the flag, no fence).  Consumers poll their own receive
+// buffer until every granule of the parity carries the expected tag, then
+// reduce exactly as from an all-reduced buffer — every rank derives the same
+// pair, and the pair's alphas come from their owners' registers, so no
+// consumer ever reads a cross-workgroup-written alpha through a possibly
+// stale cache line (L2s are per XCD).  Tags are the iteration count + 1
+// (never 0; buffers are zeroed before each solve); keys tagged T live in
+// parity T & 1, and no workgroup can lap another: its publication T+2 needs
+// every T+1 publication, each made after its author had read parity T.
+// Scope: system across GPUs (xGMI peer memory), agent within one GPU.
 // Reference: one 16-byte MPI Allgather per iteration (svmTrainMain.cpp:244).
 #pragma once
 
@@ -20,20 +23,26 @@
 
 #include "dpsvm/common.hpp"
 #include "dpsvm/device_state.hpp"
+#include "device_util.hpp"
 
 namespace dpsvm {
 namespace dev {
-
-__device__ __forceinline__ uint64_t* xch_entry(uint64_t* base, int par, const SmoArgs& a, int rank, int b) {
-  return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * kXchGranules;
-}
 
 // global (address space 1) pointers: global_ instructions count only in
 // vmcnt, so two poll rounds can be in flight (flat ops also count in lgkmcnt
 // and make the compiler drain everything before each check)
 typedef __attribute__((address_space(1))) uint64_t gu64;
 
-// system scope across GPUs (xGMI peer memory), agent scope within one GPU
+// one workgroup's publication
+struct XKeys {
+  uint64_t kh, kl;  // up / low selection keys
+  float ah, al;     // alphas of the rows behind kh / kl
+};
+
+__device__ __forceinline__ uint64_t* xch_entry(uint64_t* base, int par, const SmoArgs& a, int rank, int b) {
+  return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * kXchGranules;
+}
+
 template <bool kSys>
 __device__ __forceinline__ void xch_store(uint64_t* g, uint64_t v) {
   gu64* p = (gu64*)g;
@@ -48,119 +57,115 @@ __device__ __forceinline__ uint64_t xch_load(const uint64_t* g) {
   else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ uint32_t fbits(float v) { return __float_as_uint(v); }
+
+// keep the smaller key (keys are unique; kKeyNone never wins) with its alpha
+__device__ __forceinline__ void xk_min(XKeys& m, const XKeys& o) {
+  if (o.kh < m.kh) {
+    m.kh = o.kh;
+    m.ah = o.ah;
+  }
+  if (o.kl < m.kl) {
+    m.kl = o.kl;
+    m.al = o.al;
+  }
+}
+
+__device__ __forceinline__ XKeys xk_none() { return XKeys{kKeyNone, kKeyNone, 0.f, 0.f}; }
+
+__device__ __forceinline__ XKeys xk_shfl_xor(const XKeys& v, int m) {
+  XKeys o;
+  o.kh = shfl_xor_u64(v.kh, m);
+  o.kl = shfl_xor_u64(v.kl, m);
+  o.ah = __shfl_xor(v.ah, m, 64);
+  o.al = __shfl_xor(v.al, m, 64);
+  return o;
+}
+
+__device__ __forceinline__ XKeys wave_min_xk(XKeys v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) xk_min(v, xk_shfl_xor(v, m));
+  return v;
+}
+
 template <bool kSys>
-__device__ __forceinline__ void xch_push_t(const SmoArgs& a, int par, int b, uint64_t kh, uint64_t kl, uint32_t tag,
-                                           int lane) {
+__device__ __forceinline__ void xch_push_t(const SmoArgs& a, int par, int b, const XKeys& k, uint32_t tag, int lane) {
   if (lane < a.xworld) {
     uint64_t* g = xch_entry(a.xpeer[lane], par, a, a.xrank, b);
     const uint64_t t = (uint64_t)tag << 32;
-    xch_store<kSys>(g + 0, t | (kh >> 32));
-    xch_store<kSys>(g + 1, t | (kh & 0xffffffffull));
-    xch_store<kSys>(g + 2, t | (kl >> 32));
-    xch_store<kSys>(g + 3, t | (kl & 0xffffffffull));
+    xch_store<kSys>(g + 0, t | (k.kh >> 32));
+    xch_store<kSys>(g + 1, t | (k.kh & 0xffffffffull));
+    xch_store<kSys>(g + 2, t | (k.kl >> 32));
+    xch_store<kSys>(g + 3, t | (k.kl & 0xffffffffull));
+    xch_store<kSys>(g + 4, t | fbits(k.ah));
+    xch_store<kSys>(g + 5, t | fbits(k.al));
   }
 }
 
-template <bool kSys>
-__device__ __forceinline__ bool xch_pull_t(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
-                                           int lane) {
-  const int E = a.xworld * a.fused_G;
-  const uint64_t* base = a.xpeer[a.xrank] + (int64_t)par * E * kXchGranules;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (true) {
-    uint64_t h = kKeyNone, l = kKeyNone;
-    bool ok = true;
-    for (int e = lane; e < E; e += 64) {
-      const uint64_t* g = base + (int64_t)e * kXchGranules;
-      const uint64_t g0 = xch_load<kSys>(g), g1 = xch_load<kSys>(g + 1), g2 = xch_load<kSys>(g + 2),
-                     g3 = xch_load<kSys>(g + 3);
-      ok &= (uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 32) == tag && (uint32_t)(g2 >> 32) == tag &&
-            (uint32_t)(g3 >> 32) == tag;
-      const uint64_t vh = (g0 << 32) | (g1 & 0xffffffffull), vl = (g2 << 32) | (g3 & 0xffffffffull);
-      h = vh < h ? vh : h;
-      l = vl < l ? vl : l;
-    }
-    if (__all(ok)) {
-      kh = h;
-      kl = l;
-      return true;
-    }
-    if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
+// lane p < xworld pushes workgroup b's publication to rank p (parity par)
+__device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, const XKeys& k, uint32_t tag, int lane) {
+  if (a.xworld > 1) xch_push_t<true>(a, par, b, k, tag, lane);
+  else xch_push_t<false>(a, par, b, k, tag, lane);
 }
 
-// Workgroup-parallel poll for the persistent engine: thread `tid` of the
-// workgroup watches entries tid, tid + 256, ... and keeps two load rounds in
-// flight (the next round is issued before the previous one is checked), so
-// an arrival is seen about half a round trip after it lands instead of up to
-// a full one.  Returns this thread's minima (the caller reduces); false on
-// give-up.
+__device__ __forceinline__ bool xg_ready(const uint64_t (&x)[kXchGranules], uint32_t tag) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < kXchGranules; ++i) ok &= (uint32_t)(x[i] >> 32) == tag;
+  return ok;
+}
+
+__device__ __forceinline__ XKeys xg_decode(const uint64_t (&x)[kXchGranules]) {
+  XKeys k;
+  k.kh = (x[0] << 32) | (x[1] & 0xffffffffull);
+  k.kl = (x[2] << 32) | (x[3] & 0xffffffffull);
+  k.ah = __uint_as_float((uint32_t)x[4]);
+  k.al = __uint_as_float((uint32_t)x[5]);
+  return k;
+}
+
+// Poll: thread `tid` of `nthreads` watches entries tid, tid + nthreads, ...
+// with two load rounds in flight (the next round is issued before the
+// previous one is checked), so an arrival is seen about half a round trip
+// after it lands.  Returns this thread's minimum (the caller reduces); false
+// on give-up.  The fused engine calls it per wave (tid = lane, 64), the
+// persistent engine per workgroup.
 template <bool kSys>
-__device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
-                                           int tid, int nthreads) {
+__device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, int par, uint32_t tag, XKeys& out, int tid,
+                                           int nthreads) {
   const int E = a.xworld * a.fused_G;
   const uint64_t* base = a.xpeer[a.xrank] + (int64_t)par * E * kXchGranules;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t h = kKeyNone, l = kKeyNone;
+  XKeys m = xk_none();
   for (int c = 0; c < E; c += nthreads) {
     const int e = c + tid;
     const bool mine = e < E;
     const uint64_t* g = base + (int64_t)(mine ? e : 0) * kXchGranules;
-    auto ready = [&](uint64_t x0, uint64_t x1, uint64_t x2, uint64_t x3) {
-      return !mine || ((uint32_t)(x0 >> 32) == tag && (uint32_t)(x1 >> 32) == tag && (uint32_t)(x2 >> 32) == tag &&
-                       (uint32_t)(x3 >> 32) == tag);
-    };
-    uint64_t a0 = xch_load<kSys>(g), a1 = xch_load<kSys>(g + 1), a2 = xch_load<kSys>(g + 2),
-             a3 = xch_load<kSys>(g + 3);
-    uint64_t r0, r1, r2, r3;
+    uint64_t ra[kXchGranules], rb[kXchGranules];
+#pragma unroll
+    for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
+    bool got_a = false;
     while (true) {
-      const uint64_t b0 = xch_load<kSys>(g), b1 = xch_load<kSys>(g + 1), b2 = xch_load<kSys>(g + 2),
-                     b3 = xch_load<kSys>(g + 3);
-      if (__all(ready(a0, a1, a2, a3))) {
-        r0 = a0; r1 = a1; r2 = a2; r3 = a3;
+#pragma unroll
+      for (int i = 0; i < kXchGranules; ++i) rb[i] = xch_load<kSys>(g + i);
+      if (__all(!mine || xg_ready(ra, tag))) {
+        got_a = true;
         break;
       }
-      a0 = xch_load<kSys>(g);
-      a1 = xch_load<kSys>(g + 1);
-      a2 = xch_load<kSys>(g + 2);
-      a3 = xch_load<kSys>(g + 3);
-      if (__all(ready(b0, b1, b2, b3))) {
-        r0 = b0; r1 = b1; r2 = b2; r3 = b3;
-        break;
-      }
+#pragma unroll
+      for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
+      if (__all(!mine || xg_ready(rb, tag))) break;
       if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
     }
-    if (mine) {
-      const uint64_t vh = (r0 << 32) | (r1 & 0xffffffffull), vl = (r2 << 32) | (r3 & 0xffffffffull);
-      h = vh < h ? vh : h;
-      l = vl < l ? vl : l;
-    }
+    if (mine) xk_min(m, got_a ? xg_decode(ra) : xg_decode(rb));
   }
-  kh = h;
-  kl = l;
+  out = m;
   return true;
 }
 
-__device__ __forceinline__ bool xch_poll(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl, int tid,
-                                         int nthreads) {
-  return a.xworld > 1 ? xch_poll_t<true>(a, par, tag, kh, kl, tid, nthreads)
-                      : xch_poll_t<false>(a, par, tag, kh, kl, tid, nthreads);
-}
-
-// lane p < xworld pushes workgroup b's keys to rank p (parity par)
-__device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, uint64_t kh, uint64_t kl, uint32_t tag,
-                                         int lane) {
-  if (a.xworld > 1) xch_push_t<true>(a, par, b, kh, kl, tag, lane);
-  else xch_push_t<false>(a, par, b, kh, kl, tag, lane);
-}
-
-// every lane of the calling wave: min keys over ITS entries (lane, lane + 64,
-// ...) of all ranks' workgroups of parity par, polling until every granule
-// carries `tag` (the caller reduces across the wave); false on give-up
-__device__ __forceinline__ bool xch_pull(const SmoArgs& a, int par, uint32_t tag, uint64_t& kh, uint64_t& kl,
-                                         int lane) {
-  return a.xworld > 1 ? xch_pull_t<true>(a, par, tag, kh, kl, lane) : xch_pull_t<false>(a, par, tag, kh, kl, lane);
+__device__ __forceinline__ bool xch_poll(const SmoArgs& a, int par, uint32_t tag, XKeys& out, int tid, int nthreads) {
+  return a.xworld > 1 ? xch_poll_t<true>(a, par, tag, out, tid, nthreads)
+                      : xch_poll_t<false>(a, par, tag, out, tid, nthreads);
 }
 
 }  // namespace dev
