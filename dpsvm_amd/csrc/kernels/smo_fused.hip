@@ -67,7 +67,7 @@ __device__ __forceinline__ void store_block_keys(const SmoArgs& a, XKeys k, uint
     if (wave == 0) {
 #pragma unroll
       for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(k, XKeys{scr[w], scr[4 + w], fscr[w], fscr[4 + w]});
-      xch_push(a, xpar, blockIdx.x, k, tag, lane);
+      xch_push(a, xch_peer(a, lane), xpar, blockIdx.x, k, tag, lane);
     }
     return;
   }
@@ -145,7 +145,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   }
   XKeys xk = xk_none();
   if (rin.done == kRunning && a.xworld > 0 &&
-      !xch_poll(a, (int)(((uint32_t)rin.iter + 1u) & 1u), (uint32_t)rin.iter + 1u, xk, lane, 64)) {
+      !xch_poll(a, a.xpeer[a.xrank], (int)(((uint32_t)rin.iter + 1u) & 1u), (uint32_t)rin.iter + 1u, xk, lane,
+                64)) {
     // a peer stopped publishing: give up (every rank that times out stops the same way)
     if (lead) {
       commit_pending(a, rin);

@@ -61,13 +61,19 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   }
   const FusedRec s0 = *st;
   if (s0.done != kRunning) return;
+  // exchange endpoints, loaded once; wave 3 publishes (its stores never delay
+  // the pollers' loads: vmcnt is per wave and counts stores too)
+  constexpr int kPub = kFusedThreads / 64 - 1;
+  const uint64_t* my_buf = a.xpeer[a.xrank];
+  uint64_t* peer_buf = wave == kPub ? xch_peer(a, lane) : nullptr;
+  const bool committer = blockIdx.x == 0 && tid == kPub * 64;
   int t = s0.iter, done = kRunning;
   float b_hi = s0.b_hi, b_lo = s0.b_lo;
-  // diagnostics (DPSVM_STAMPS): thread 0 of workgroups 0 and G-1 keeps 6
+  // diagnostics (DPSVM_STAMPS): the publishing wave's lane 0 of workgroups 0 and G-1 keeps 6
   // s_memrealtime stamps per iteration in registers and stores them after
   // publishing (0 poll start, 1 pair known, 2 alpha update, 3 f update,
   // 4 keys reduced, 5 published)
-  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+  const bool stamping = a.stamps != nullptr && tid == kPub * 64 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
   uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
 #define PSTAMP(i) \
   if (stamping) stv[i] = __builtin_amdgcn_s_memrealtime()
@@ -80,8 +86,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       // every thread watches its share of the entries (two load rounds in flight)
       XKeys m = xk_none();
       bool ok = true;
-      if (a.xpoll == 0) ok = xch_poll(a, (int)(tag & 1u), tag, m, tid, kFusedThreads);
-      else if (wave == 0) ok = xch_poll(a, (int)(tag & 1u), tag, m, lane, 64);
+      if (a.xpoll == 0) {
+        if (wave < kPub) ok = xch_poll(a, my_buf, (int)(tag & 1u), tag, m, tid, kPub * 64);
+      } else if (wave == 0) {
+        ok = xch_poll(a, my_buf, (int)(tag & 1u), tag, m, lane, 64);
+      }
       m = wave_min_xk(m);
       if (lane == 0) {
         pscr[wave] = m.kh;
@@ -142,7 +151,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     b_lo = bl;
     PSTAMP(2);
     if (done == kNonFinite) break;
-    if (lead) {  // alpha memory is write-only during the run (read after the launch)
+    if (committer) {  // alpha memory is write-only during the run (read after the launch)
       a.alpha[i_lo] = a_lo_new;
       a.alpha[i_hi] = a_hi_new;  // hi written last (svmTrainMain.cpp:298-299)
     }
@@ -179,12 +188,13 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       kfs[4 + wave] = nk.al;
     }
     __syncthreads();
-    if (wave == 0) {
+    if (wave == kPub) {
 #pragma unroll
-      for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(nk, XKeys{kscr[w], kscr[4 + w], kfs[w], kfs[4 + w]});
+      for (int w = 0; w < kFusedThreads / 64; ++w)
+        if (w != kPub) xk_min(nk, XKeys{kscr[w], kscr[4 + w], kfs[w], kfs[4 + w]});
       PSTAMP(4);
       const uint32_t otag = (uint32_t)t + 1u;
-      xch_push(a, (int)(otag & 1u), blockIdx.x, nk, otag, lane);
+      xch_push(a, peer_buf, (int)(otag & 1u), blockIdx.x, nk, otag, lane);
       PSTAMP(5);
       if (stamping) {
         uint64_t* dst = a.stamps + ((size_t)(t % kStampRing) * 2 + (blockIdx.x == 0 ? 0 : 1)) * kStampSlots;

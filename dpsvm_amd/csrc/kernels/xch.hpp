@@ -88,10 +88,14 @@ __device__ __forceinline__ XKeys wave_min_xk(XKeys v) {
   return v;
 }
 
+// lane p < xworld pushes to rank p; peer = that rank's receive buffer
+// (loaded once per launch: a pointer load here would make the compiler wait
+// for every earlier store of the wave first)
 template <bool kSys>
-__device__ __forceinline__ void xch_push_t(const SmoArgs& a, int par, int b, const XKeys& k, uint32_t tag, int lane) {
+__device__ __forceinline__ void xch_push_t(const SmoArgs& a, uint64_t* peer, int par, int b, const XKeys& k,
+                                           uint32_t tag, int lane) {
   if (lane < a.xworld) {
-    uint64_t* g = xch_entry(a.xpeer[lane], par, a, a.xrank, b);
+    uint64_t* g = xch_entry(peer, par, a, a.xrank, b);
     const uint64_t t = (uint64_t)tag << 32;
     xch_store<kSys>(g + 0, t | (k.kh >> 32));
     xch_store<kSys>(g + 1, t | (k.kh & 0xffffffffull));
@@ -103,9 +107,14 @@ __device__ __forceinline__ void xch_push_t(const SmoArgs& a, int par, int b, con
 }
 
 // lane p < xworld pushes workgroup b's publication to rank p (parity par)
-__device__ __forceinline__ void xch_push(const SmoArgs& a, int par, int b, const XKeys& k, uint32_t tag, int lane) {
-  if (a.xworld > 1) xch_push_t<true>(a, par, b, k, tag, lane);
-  else xch_push_t<false>(a, par, b, k, tag, lane);
+__device__ __forceinline__ void xch_push(const SmoArgs& a, uint64_t* peer, int par, int b, const XKeys& k,
+                                         uint32_t tag, int lane) {
+  if (a.xworld > 1) xch_push_t<true>(a, peer, par, b, k, tag, lane);
+  else xch_push_t<false>(a, peer, par, b, k, tag, lane);
+}
+
+__device__ __forceinline__ uint64_t* xch_peer(const SmoArgs& a, int lane) {
+  return lane < a.xworld ? a.xpeer[lane] : nullptr;
 }
 
 __device__ __forceinline__ bool xg_ready(const uint64_t (&x)[kXchGranules], uint32_t tag) {
@@ -131,10 +140,10 @@ __device__ __forceinline__ XKeys xg_decode(const uint64_t (&x)[kXchGranules]) {
 // on give-up.  The fused engine calls it per wave (tid = lane, 64), the
 // persistent engine per workgroup.
 template <bool kSys>
-__device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, int par, uint32_t tag, XKeys& out, int tid,
-                                           int nthreads) {
+__device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
+                                           XKeys& out, int tid, int nthreads) {
   const int E = a.xworld * a.fused_G;
-  const uint64_t* base = a.xpeer[a.xrank] + (int64_t)par * E * kXchGranules;
+  const uint64_t* base = mine_buf + (int64_t)par * E * kXchGranules;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   XKeys m = xk_none();
   for (int c = 0; c < E; c += nthreads) {
@@ -163,9 +172,11 @@ __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, int par, uint32_t t
   return true;
 }
 
-__device__ __forceinline__ bool xch_poll(const SmoArgs& a, int par, uint32_t tag, XKeys& out, int tid, int nthreads) {
-  return a.xworld > 1 ? xch_poll_t<true>(a, par, tag, out, tid, nthreads)
-                      : xch_poll_t<false>(a, par, tag, out, tid, nthreads);
+// mine_buf: this rank's receive buffer (a.xpeer[a.xrank], loaded once)
+__device__ __forceinline__ bool xch_poll(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
+                                         XKeys& out, int tid, int nthreads) {
+  return a.xworld > 1 ? xch_poll_t<true>(a, mine_buf, par, tag, out, tid, nthreads)
+                      : xch_poll_t<false>(a, mine_buf, par, tag, out, tid, nthreads);
 }
 
 }  // namespace dev
