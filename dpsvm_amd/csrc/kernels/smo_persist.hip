@@ -86,11 +86,9 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       // every thread watches its share of the entries (two load rounds in flight)
       XKeys m = xk_none();
       bool ok = true;
-      if (a.xpoll == 0) {
-        if (wave < kPub) ok = xch_poll(a, my_buf, (int)(tag & 1u), tag, m, tid, kPub * 64);
-      } else if (wave == 0) {
-        ok = xch_poll(a, my_buf, (int)(tag & 1u), tag, m, lane, 64);
-      }
+      // every thread watches <= 1 entry per chunk of 256 (xpoll 1: two rounds in flight)
+      if (a.xpoll == 0) ok = xch_poll<false>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
+      else ok = xch_poll<true>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
       m = wave_min_xk(m);
       if (lane == 0) {
         pscr[wave] = m.kh;

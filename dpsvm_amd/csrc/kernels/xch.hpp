@@ -134,12 +134,12 @@ __device__ __forceinline__ XKeys xg_decode(const uint64_t (&x)[kXchGranules]) {
 }
 
 // Poll: thread `tid` of `nthreads` watches entries tid, tid + nthreads, ...
-// with two load rounds in flight (the next round is issued before the
-// previous one is checked), so an arrival is seen about half a round trip
-// after it lands.  Returns this thread's minimum (the caller reduces); false
-// on give-up.  The fused engine calls it per wave (tid = lane, 64), the
-// persistent engine per workgroup.
-template <bool kSys>
+// One round = one load of each watched granule; kPipe keeps two rounds in
+// flight (the next one issued before the previous is checked: arrivals seen
+// half a round trip earlier, at twice the polling traffic — every round of
+// every workgroup reads all E entries past the L2).  Returns this thread's
+// minimum (the caller reduces); false on give-up.
+template <bool kSys, bool kPipe>
 __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
                                            XKeys& out, int tid, int nthreads) {
   const int E = a.xworld * a.fused_G;
@@ -154,17 +154,27 @@ __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* min
 #pragma unroll
     for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
     bool got_a = false;
-    while (true) {
+    if constexpr (kPipe) {
+      while (true) {
 #pragma unroll
-      for (int i = 0; i < kXchGranules; ++i) rb[i] = xch_load<kSys>(g + i);
-      if (__all(!mine || xg_ready(ra, tag))) {
-        got_a = true;
-        break;
+        for (int i = 0; i < kXchGranules; ++i) rb[i] = xch_load<kSys>(g + i);
+        if (__all(!mine || xg_ready(ra, tag))) {
+          got_a = true;
+          break;
+        }
+#pragma unroll
+        for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
+        if (__all(!mine || xg_ready(rb, tag))) break;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
       }
+    } else {
+      got_a = true;
+      while (!__all(!mine || xg_ready(ra, tag))) {
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
+        __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-      for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
-      if (__all(!mine || xg_ready(rb, tag))) break;
-      if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
+        for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
+      }
     }
     if (mine) xk_min(m, got_a ? xg_decode(ra) : xg_decode(rb));
   }
@@ -173,10 +183,11 @@ __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* min
 }
 
 // mine_buf: this rank's receive buffer (a.xpeer[a.xrank], loaded once)
+template <bool kPipe = false>
 __device__ __forceinline__ bool xch_poll(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
                                          XKeys& out, int tid, int nthreads) {
-  return a.xworld > 1 ? xch_poll_t<true>(a, mine_buf, par, tag, out, tid, nthreads)
-                      : xch_poll_t<false>(a, mine_buf, par, tag, out, tid, nthreads);
+  return a.xworld > 1 ? xch_poll_t<true, kPipe>(a, mine_buf, par, tag, out, tid, nthreads)
+                      : xch_poll_t<false, kPipe>(a, mine_buf, par, tag, out, tid, nthreads);
 }
 
 }  // namespace dev
