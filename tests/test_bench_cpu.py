@@ -17,7 +17,8 @@ def test_bench_json_contract():
         assert k in out
     assert out["higher_is_better"] is False and out["scaling"] == "strong" and out["n_gpus"] == 1
     assert out["converged"] and out["config"]["parallelism"] == "dp1"
-    assert abs(out["vs_baseline"] - out["value"] / 137.0) < 1e-6
+    # a reduced problem is not the reference's published config: no baseline ratio
+    assert out["vs_baseline"] is None and "1500x" in out["metric"]
 
 
 def test_graft_entry_build():
