@@ -86,9 +86,15 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       // every thread watches its share of the entries (two load rounds in flight)
       XKeys m = xk_none();
       bool ok = true;
-      // every thread watches <= 1 entry per chunk of 256 (xpoll 1: two rounds in flight)
-      if (a.xpoll == 0) ok = xch_poll<false>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
-      else ok = xch_poll<true>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
+      // wave 0 watches every entry (xpoll 1: every thread one entry, one round
+      // at a time; 2: the same with two rounds in flight — A/B diagnostics)
+      if (a.xpoll == 0) {
+        if (wave == 0) ok = xch_poll_wave(a, my_buf, (int)(tag & 1u), tag, m, lane);
+      } else if (a.xpoll == 1) {
+        ok = xch_poll<false>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
+      } else {
+        ok = xch_poll<true>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
+      }
       m = wave_min_xk(m);
       if (lane == 0) {
         pscr[wave] = m.kh;

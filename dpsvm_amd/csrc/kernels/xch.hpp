@@ -182,6 +182,51 @@ __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* min
   return true;
 }
 
+// One wave watches ALL entries (lane l: entries l + 64 i, up to 4 per lane
+// per batch, every load of a batch in flight together), sleeping between
+// rounds: the fewest poll requests on the hot buffer lines (every workgroup
+// polls the same few KB, so polling traffic itself delays the publications).
+template <bool kSys>
+__device__ __forceinline__ bool xch_poll_wave_t(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
+                                                XKeys& out, int lane) {
+  constexpr int kB = 4;
+  const int E = a.xworld * a.fused_G;
+  const uint64_t* base = mine_buf + (int64_t)par * E * kXchGranules;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  XKeys m = xk_none();
+  for (int c = 0; c < E; c += 64 * kB) {
+    uint64_t r[kB][kXchGranules];
+    bool mine[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) mine[j] = c + lane + 64 * j < E;
+    while (true) {
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        const uint64_t* g = base + (int64_t)(mine[j] ? c + lane + 64 * j : 0) * kXchGranules;
+#pragma unroll
+        for (int i = 0; i < kXchGranules; ++i) r[j][i] = xch_load<kSys>(g + i);
+      }
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < kB; ++j) ok &= !mine[j] || xg_ready(r[j], tag);
+      if (__all(ok)) break;
+      if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
+      __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      if (mine[j]) xk_min(m, xg_decode(r[j]));
+  }
+  out = m;
+  return true;
+}
+
+__device__ __forceinline__ bool xch_poll_wave(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
+                                              XKeys& out, int lane) {
+  return a.xworld > 1 ? xch_poll_wave_t<true>(a, mine_buf, par, tag, out, lane)
+                      : xch_poll_wave_t<false>(a, mine_buf, par, tag, out, lane);
+}
+
 // mine_buf: this rank's receive buffer (a.xpeer[a.xrank], loaded once)
 template <bool kPipe = false>
 __device__ __forceinline__ bool xch_poll(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
