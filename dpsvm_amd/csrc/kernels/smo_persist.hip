@@ -37,6 +37,11 @@ namespace dev {
 
 constexpr int kPersistMaxRows = 4;  // rows per thread (fused_rows <= 1024)
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for
+// the wave's outstanding global stores (its workgroup-scope fence), which
+// would hold the publishing wave for the write-through ack of its granules.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
@@ -103,7 +108,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
         pfs[4 + wave] = m.al;
         fail_s[wave] = ok ? 0 : 1;
       }
-      __syncthreads();
+      lds_barrier();
       pk = XKeys{pscr[0], pscr[4], pfs[0], pfs[4]};
 #pragma unroll
       for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(pk, XKeys{pscr[w], pscr[4 + w], pfs[w], pfs[4 + w]});
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       kfs[wave] = nk.ah;
       kfs[4 + wave] = nk.al;
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == kPub) {
 #pragma unroll
       for (int w = 0; w < kFusedThreads / 64; ++w)
