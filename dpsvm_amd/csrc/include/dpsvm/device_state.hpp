@@ -158,7 +158,6 @@ struct SmoArgs {
   uint64_t* const* xpeer;  // [xworld] receive buffers (device-accessible)
   int32_t xrank, xworld;
   int64_t xtimeout_ticks;  // give-up bound of one poll loop (s_memrealtime, 100 MHz)
-  int32_t xpoll;           // persistent engine poll: 0 wave 0 (default), 1 every thread, 2 pipelined (A/B)
 };
 constexpr int kXchGranules = 6;  // per workgroup entry: hi key (2 halves), lo key (2 halves), their alphas
 constexpr int kStampRing = 4096;

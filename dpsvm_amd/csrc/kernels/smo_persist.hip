@@ -74,11 +74,11 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   const bool committer = blockIdx.x == 0 && tid == kPub * 64;
   int t = s0.iter, done = kRunning;
   float b_hi = s0.b_hi, b_lo = s0.b_lo;
-  // diagnostics (DPSVM_STAMPS): the publishing wave's lane 0 of workgroups 0 and G-1 keeps 6
-  // s_memrealtime stamps per iteration in registers and stores them after
-  // publishing (0 poll start, 1 pair known, 2 alpha update, 3 f update,
-  // 4 keys reduced, 5 published)
-  const bool stamping = a.stamps != nullptr && tid == kPub * 64 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+  // diagnostics (DPSVM_STAMPS): lane 0 of wave 1 (neither polls nor publishes)
+  // of workgroups 0 and G-1 keeps s_memrealtime stamps per iteration in
+  // registers (0 loop top, 1 pair known, 2 alpha update, 3 f update, 4 keys
+  // reduced = after barrier 2, 5 = 4) and stores them after barrier 2
+  const bool stamping = a.stamps != nullptr && tid == 64 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
   uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
 #define PSTAMP(i) \
   if (stamping) stv[i] = __builtin_amdgcn_s_memrealtime()
@@ -91,15 +91,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       // every thread watches its share of the entries (two load rounds in flight)
       XKeys m = xk_none();
       bool ok = true;
-      // wave 0 watches every entry (xpoll 1: every thread one entry, one round
-      // at a time; 2: the same with two rounds in flight — A/B diagnostics)
-      if (a.xpoll == 0) {
-        if (wave == 0) ok = xch_poll_wave(a, my_buf, (int)(tag & 1u), tag, m, lane);
-      } else if (a.xpoll == 1) {
-        ok = xch_poll<false>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
-      } else {
-        ok = xch_poll<true>(a, my_buf, (int)(tag & 1u), tag, m, tid, kFusedThreads);
-      }
+      // wave 0 watches every entry
+      if (wave == 0) ok = xch_poll_wave(a, my_buf, (int)(tag & 1u), tag, m, lane);
       m = wave_min_xk(m);
       if (lane == 0) {
         pscr[wave] = m.kh;

@@ -688,8 +688,6 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       a.xrank = m.rank;
       a.xworld = m.world;
       a.xtimeout_ticks = (int64_t)(tmo * 1e8);
-      const char* xp = std::getenv("DPSVM_XCH_POLL");
-      a.xpoll = xp ? std::max(0, std::min(2, atoi(xp))) : 0;
     }
   }
   m.info.exchange = m.xch ? (m.world > 1 ? "peer" : "loopback")
