@@ -55,7 +55,12 @@ __device__ __forceinline__ void commit_pending(const SmoArgs& a, const FusedRec&
 __device__ __forceinline__ void store_block_keys(const SmoArgs& a, XKeys k, uint64_t* p_out, uint64_t* scr,
                                                  float* fscr, int xpar, uint32_t tag) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  k = wave_min_xk(k);
+  if (a.xworld > 0) {
+    k = wave_min_xk(k);  // keys with the alphas of their rows
+  } else {
+    k.kh = wave_min_u64(k.kh);  // keys only
+    k.kl = wave_min_u64(k.kl);
+  }
   if (lane == 0) {
     scr[wave] = k.kh;
     scr[4 + wave] = k.kl;

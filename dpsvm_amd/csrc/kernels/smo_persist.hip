@@ -37,17 +37,12 @@ namespace dev {
 
 constexpr int kPersistMaxRows = 4;  // rows per thread (fused_rows <= 1024)
 
-// Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for
-// the wave's outstanding global stores (its workgroup-scope fence), which
-// would hold the publishing wave for the write-through ack of its granules.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
 __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
-  __shared__ uint64_t pscr[8];
-  __shared__ float pfs[8], kfs[8];
-  __shared__ int fail_s[4];
+  __shared__ float kfs[8];
+  __shared__ XKeys pair_s;
+  __shared__ int fail_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int rpt = a.fused_rows / kFusedThreads;  // rows per thread
@@ -66,60 +61,48 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   }
   const FusedRec s0 = *st;
   if (s0.done != kRunning) return;
-  // exchange endpoints, loaded once; wave 3 publishes (its stores never delay
-  // the pollers' loads: vmcnt is per wave and counts stores too)
-  constexpr int kPub = kFusedThreads / 64 - 1;
+  // exchange endpoints, loaded once (wave 0 polls and publishes)
   const uint64_t* my_buf = a.xpeer[a.xrank];
-  uint64_t* peer_buf = wave == kPub ? xch_peer(a, lane) : nullptr;
-  const bool committer = blockIdx.x == 0 && tid == kPub * 64;
+  uint64_t* peer_buf = wave == 0 ? xch_peer(a, lane) : nullptr;
   int t = s0.iter, done = kRunning;
   float b_hi = s0.b_hi, b_lo = s0.b_lo;
-  // diagnostics (DPSVM_STAMPS): lane 0 of wave 1 (neither polls nor publishes)
-  // of workgroups 0 and G-1 keeps s_memrealtime stamps per iteration in
-  // registers (0 loop top, 1 pair known, 2 alpha update, 3 f update, 4 keys
-  // reduced = after barrier 2, 5 = 4) and stores them after barrier 2
-  const bool stamping = a.stamps != nullptr && tid == 64 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
+
+  // diagnostics (DPSVM_STAMPS): thread 0 of workgroups 0 and G-1 keeps 6
+  // s_memrealtime stamps per iteration in registers and stores them after
+  // publishing (0 poll start, 1 pair known, 2 alpha update, 3 f update,
+  // 4 keys reduced, 5 published)
+  const bool stamping = a.stamps != nullptr && tid == 0 && (blockIdx.x == 0 || blockIdx.x == a.fused_G - 1);
   uint64_t stv[6] = {0, 0, 0, 0, 0, 0};
 #define PSTAMP(i) \
   if (stamping) stv[i] = __builtin_amdgcn_s_memrealtime()
   for (int step = 0; step < steps; ++step) {
     PSTAMP(0);
-    // ---- 1. keys tagged t+1 (produced by iteration t) ----
+    // ---- 1. publications tagged t+1 (produced by iteration t) ----
     const uint32_t tag = (uint32_t)t + 1u;
-    XKeys pk;
-    {
-      // every thread watches its share of the entries (two load rounds in flight)
+    if (wave == 0) {
       XKeys m = xk_none();
-      bool ok = true;
-      // wave 0 watches every entry
-      if (wave == 0) ok = xch_poll_wave(a, my_buf, (int)(tag & 1u), tag, m, lane);
+      const bool ok = xch_poll_wave(a, my_buf, (int)(tag & 1u), tag, m, lane);
       m = wave_min_xk(m);
       if (lane == 0) {
-        pscr[wave] = m.kh;
-        pscr[4 + wave] = m.kl;
-        pfs[wave] = m.ah;
-        pfs[4 + wave] = m.al;
-        fail_s[wave] = ok ? 0 : 1;
+        pair_s = m;
+        fail_s = ok ? 0 : 1;
       }
-      lds_barrier();
-      pk = XKeys{pscr[0], pscr[4], pfs[0], pfs[4]};
-#pragma unroll
-      for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(pk, XKeys{pscr[w], pscr[4 + w], pfs[w], pfs[4 + w]});
     }
-    const uint64_t kh = pk.kh, kl = pk.kl;
-    if (fail_s[0] | fail_s[1] | fail_s[2] | fail_s[3]) {
+    __syncthreads();
+    const XKeys pk = pair_s;
+    if (fail_s) {
       done = kCommFail;
       break;
     }
-    if (kh == kKeyNone || kl == kKeyNone) {
+    if (pk.kh == kKeyNone || pk.kl == kKeyNone) {
       done = kNoPair;
       break;
     }
-    const int i_hi = (int)key_index(kh), i_lo = (int)key_index(kl);
-    const float bh = key_value(kh), bl = -key_value(kl);
+    const int i_hi = (int)key_index(pk.kh), i_lo = (int)key_index(pk.kl);
+    const float bh = key_value(pk.kh), bl = -key_value(pk.kl);
     PSTAMP(1);
 
-    // ---- 2. one round trip: Gram rows of the own rows, sample rows, pair state ----
+    // ---- 2. one round trip: Gram rows of the own rows, sample rows ----
     const float* line_hi = a.lines + (int64_t)i_hi * a.ldl;
     const float* line_lo = a.lines + (int64_t)i_lo * a.ldl;
     float khv[kPersistMaxRows], klv[kPersistMaxRows];
@@ -153,11 +136,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     b_lo = bl;
     PSTAMP(2);
     if (done == kNonFinite) break;
-    if (committer) {  // alpha memory is write-only during the run (read after the launch)
+    if (lead) {  // alpha memory is write-only during the run (read after the launch)
       a.alpha[i_lo] = a_lo_new;
       a.alpha[i_hi] = a_hi_new;  // hi written last (svmTrainMain.cpp:298-299)
     }
-
     t = iter;
 
     // ---- 3. f update + classification of the own rows ----
@@ -189,11 +171,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       kfs[wave] = nk.ah;
       kfs[4 + wave] = nk.al;
     }
-    lds_barrier();
-    if (wave == kPub) {
+    __syncthreads();
+    if (wave == 0) {
 #pragma unroll
-      for (int w = 0; w < kFusedThreads / 64; ++w)
-        if (w != kPub) xk_min(nk, XKeys{kscr[w], kscr[4 + w], kfs[w], kfs[4 + w]});
+      for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(nk, XKeys{kscr[w], kscr[4 + w], kfs[w], kfs[4 + w]});
       PSTAMP(4);
       const uint32_t otag = (uint32_t)t + 1u;
       xch_push(a, peer_buf, (int)(otag & 1u), blockIdx.x, nk, otag, lane);
@@ -205,8 +186,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       }
     }
   }
-
 #undef PSTAMP
+
   // ---- exit: own rows' f back to memory; workgroup 0 writes the state ----
 #pragma unroll
   for (int k = 0; k < kPersistMaxRows; ++k) {

@@ -211,7 +211,7 @@ __device__ __forceinline__ bool xch_poll_wave_t(const SmoArgs& a, const uint64_t
       for (int j = 0; j < kB; ++j) ok &= !mine[j] || xg_ready(r[j], tag);
       if (__all(ok)) break;
       if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j)
