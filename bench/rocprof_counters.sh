@@ -1,15 +1,18 @@
 #!/bin/bash
-# PMC counters for the hot kernels on the headline config (run on the GPU box).
-# Counters need their own run (no --sys-trace / runtime tracing with --pmc).
+# PMC counters for the hot kernels (run on the GPU box).  Counters need their
+# own run (no --sys-trace / runtime tracing together with --pmc).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
-# dense headline: fused SMO kernel + Gram GEMM
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --pmc FETCH_SIZE SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F32 \
-  -d "$OUT/dense" -o pmc --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-accuracy || exit $?
-# LRU mode: row kernel (X pass, MFMA 16x16x4) + finalize
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --pmc FETCH_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_MFMA_MOPS_F32 \
-  -d "$OUT/lru" -o pmc --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-accuracy \
-  --cache-lines 20000 || exit $?
+timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || true
+# dense headline: Gram GEMM (MFMA 32x32x2 f32) + persistent SMO kernel
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+  -d "$OUT/dense_mfma" -o pmc --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-accuracy || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE WRITE_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS \
+  -d "$OUT/dense_mem" -o pmc --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-accuracy || exit $?
+# cache mode: fused cache kernel (X pass on MFMA 16x16x4), bounded run
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+  -d "$OUT/lru" -o pmc --output-format csv -- python3 bench/lru_profile_run.py 14 3000 || exit $?
+python3 bench/pmc_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"
