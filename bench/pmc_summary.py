@@ -1,5 +1,9 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc counter CSVs per kernel (sums over dispatches)."""
+"""Summarise rocprofv3 --pmc counter CSVs per kernel (sums over dispatches).
+
+MFMA work: SQ_INSTS_VALU_MFMA_MOPS_F32 x 512 = f32 MFMA FLOPs (rocprofv3's
+MfmaFlopsF32); achieved TFLOP/s uses the dispatch durations of the same run
+(counter collection serialises dispatches)."""
 import csv
 import glob
 import os
@@ -10,20 +14,20 @@ from collections import defaultdict
 def main(root):
     for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         agg = defaultdict(lambda: defaultdict(float))
-        calls = defaultdict(set)
+        dur = defaultdict(dict)
         for r in csv.DictReader(open(f)):
-            k = r.get("Kernel_Name", "?")
-            short = k.split("(")[0].replace("dpsvm::dev::", "").replace("void ", "")
+            short = r.get("Kernel_Name", "?").split("(")[0].replace("dpsvm::dev::", "").replace("void ", "")
             agg[short][r["Counter_Name"]] += float(r["Counter_Value"])
-            calls[short].add(r.get("Dispatch_Id", ""))
+            dur[short][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         print(f"== {os.path.relpath(f, root)}")
         for k, cs in agg.items():
+            ns = sum(dur[k].values())
             line = ", ".join(f"{c}={v:.4g}" for c, v in sorted(cs.items()))
-            extra = ""
-            if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs and cs["GRBM_GUI_ACTIVE"] > 0:
-                # MFMA busy per CU-cycle: busy cycles are summed over the chip's CUs (256)
-                extra = f"  [MFMA busy ~{100.0 * cs['SQ_VALU_MFMA_BUSY_CYCLES'] / (cs['GRBM_GUI_ACTIVE'] * 256):.1f}% of CU-cycles]"
-            print(f"  {k} (dispatches {len(calls[k])}): {line}{extra}")
+            extra = f"  [{len(dur[k])} dispatches, {ns / 1e6:.3f} ms"
+            if cs.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0) > 0 and ns > 0:
+                fl = cs["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
+                extra += f", f32 MFMA {fl / 1e12:.3f} TFLOP = {fl / ns / 1e3:.1f} TFLOP/s ({100 * fl / ns / 1e3 / 157.3:.0f}% of 157.3)"
+            print(f"  {k}: {line}{extra}]")
 
 
 if __name__ == "__main__":

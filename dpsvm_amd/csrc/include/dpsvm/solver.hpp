@@ -115,6 +115,9 @@ void predict(const float* x, const float* xsq, int64_t n, int ld, const float* s
              const float* svsq, const float* coef, int64_t nsv, int sv_ld, float gamma, float b,
              float* dec, void* stream);
 int64_t compact_nonzero(const float* alpha, int64_t n, int* idx_out, void* stream);
+// Gram block K[i][j] = K(a_i, b_j) (dense-mode GEMM; symmetric: b == a)
+void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
+              float gamma, float* out, int64_t out_ld, bool symmetric, void* stream);
 }  // namespace kernels
 
 int device_count();

@@ -46,9 +46,11 @@ void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uin
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)
+//   symmetric: B == A (one rank): tiles above the diagonal only, each also
+//   stores its transpose (half the MFMA work, bit-identical values)
 void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                     const float* Bsq, int64_t N, int ldb, int dp, float gamma, float* out,
-                    int64_t ldo, hipStream_t s);
+                    int64_t ldo, hipStream_t s, bool symmetric = false);
 // Decision values: dec[i] = sum_j coef[j] K(A_i, B_j) - b   (B = SVs, coef = alpha*y)
 //   partial: scratch [splits][M_pad] (returned by predict_scratch_floats)
 int64_t predict_scratch_floats(int64_t M, int64_t N);

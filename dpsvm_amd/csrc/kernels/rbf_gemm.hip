@@ -34,7 +34,11 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     const float* __restrict__ A, const float* __restrict__ Asq, int64_t M, int lda,
     const float* __restrict__ B, const float* __restrict__ Bsq, int64_t N, int ldb, int dp,
     float gamma, float* __restrict__ out, int64_t ldo, const float* __restrict__ coef,
-    int n_tiles_per_split) {
+    int n_tiles_per_split, int sym) {
+  // sym (STORE, B == A, N == M): only tiles on/above the diagonal are computed;
+  // each off-diagonal tile also writes its transpose.  K(i,j) and K(j,i) are
+  // bit-identical (same products in the same k order, commutative norm sum).
+  if (EPI == EPI_STORE && sym && blockIdx.y < blockIdx.x) return;
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
   __shared__ float red[2][BM];
@@ -133,8 +137,38 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
           const float kv = rbf_from_dot(Asq[row], bsq, acc[i][j][r], gamma);
           if (EPI == EPI_STORE) {
             if (row < M && col < N) out[row * ldo + col] = kv;
+            if (sym) acc[i][j][r] = kv;  // kept for the transposed store
           } else {
             rowacc[i][r] += cf * kv;
+          }
+        }
+      }
+    }
+    if (EPI == EPI_STORE && sym && blockIdx.y != blockIdx.x) {
+      // transposed tile: lane holds 4 consecutive rows per group -> 16-B stores
+      // out[col][row .. row+3] (each store instruction: 32 rows x 32 B)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int64_t row = m0 + wm * 64 + i * 32 + 8 * q + 4 * (lane >> 5);
+            if (col >= M) continue;
+            float* dst = out + col * ldo + row;
+            if (row + 3 < N) {
+              f4 v;
+              v.x = acc[i][j][4 * q + 0];
+              v.y = acc[i][j][4 * q + 1];
+              v.z = acc[i][j][4 * q + 2];
+              v.w = acc[i][j][4 * q + 3];
+              *(f4*)dst = v;
+            } else {
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                if (row + c < N) dst[c] = acc[i][j][4 * q + c];
+            }
           }
         }
       }
@@ -198,13 +232,15 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
 void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                     const float* Bsq, int64_t N, int ldb, int dp, float gamma, float* out,
-                    int64_t ldo, hipStream_t s) {
+                    int64_t ldo, hipStream_t s, bool symmetric) {
   if (M <= 0 || N <= 0) return;
   DPSVM_CHECK(dp % 16 == 0, "rbf_gemm: dp must be a multiple of 16");
+  DPSVM_CHECK(!symmetric || (A == B && Asq == Bsq && M == N && lda == ldb && ldo % 4 == 0),
+              "rbf_gemm_store: symmetric mode needs B == A, N == M");
   const int64_t tm = (M + dev::BM - 1) / dev::BM, tn = (N + dev::BN - 1) / dev::BN;
   DPSVM_CHECK(tn < 65536, "rbf_gemm_store: N too large for grid.y");
   dev::rbf_gemm_kernel<dev::EPI_STORE><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
-      A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, out, ldo, nullptr, 1);
+      A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, out, ldo, nullptr, 1, symmetric ? 1 : 0);
   post_launch("rbf_gemm_store", s);
 }
 
@@ -235,7 +271,7 @@ void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const flo
     const int per = (int)((tn + splits - 1) / splits);
     splits = (int)((tn + per - 1) / per);
     dev::rbf_gemm_kernel<dev::EPI_PREDICT><<<dim3((unsigned)tm, (unsigned)splits), dev::GEMM_THREADS, 0, s>>>(
-        A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, partial, ldp, coef, per);
+        A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, partial, ldp, coef, per, 0);
     post_launch("rbf_predict", s);
   } else {
     HIP_CHECK(hipMemsetAsync(partial, 0, sizeof(float) * ldp, s));

@@ -399,6 +399,11 @@ PYBIND11_MODULE(_C, m) {
     kernels::predict((const float*)x, (const float*)xsq, n, ld, (const float*)sv, (const float*)svsq,
                      (const float*)coef, nsv, ld, gamma, b, (float*)dec, (void*)stream);
   });
+  m.def("k_rbf_gram", [](uintptr_t a, uintptr_t asq, int64_t m_, uintptr_t b, uintptr_t bsq, int64_t n, int ld,
+                         float gamma, uintptr_t out, int64_t out_ld, bool symmetric, uintptr_t stream) {
+    kernels::rbf_gram((const float*)a, (const float*)asq, m_, (const float*)b, (const float*)bsq, n, ld, gamma,
+                      (float*)out, out_ld, symmetric, (void*)stream);
+  });
   m.def("k_compact", [](uintptr_t alpha, int64_t n, uintptr_t idx, uintptr_t stream) {
     return kernels::compact_nonzero((const float*)alpha, n, (int*)idx, (void*)stream);
   });

@@ -794,8 +794,10 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     trace::Range gram_range("dpsvm/gram_gemm");
     // whole Gram shard K[i][j], i over all n rows, j over local rows: one MFMA GEMM
     gram_timer.start(m.stream);
+    // one rank holds the whole (symmetric) Gram: compute half, mirror the rest
+    const bool sym = m.off == 0 && m.nl == m.n && m.replicated;
     launch::rbf_gemm_store(m.x, m.xsq, m.n, m.dp, m.x + (size_t)m.off * m.dp, m.xsq + m.off, m.nl, m.dp,
-                           m.dp, m.gamma, m.lines, m.ldl, m.stream);
+                           m.dp, m.gamma, m.lines, m.ldl, m.stream, sym);
     gram_timer.stop(m.stream);
     res.rows_computed = m.n;
     res.x_passes = 1;
@@ -1264,6 +1266,11 @@ void predict(const float* x, const float* xsq, int64_t n, int ld, const float* s
   launch::rbf_predict(x, xsq, n, ld, sv, svsq, coef, nsv, sv_ld, ld, gamma, b, part, dec, nullptr, nullptr, s);
   HIP_CHECK(hipStreamSynchronize(s));
   (void)hipFree(part);
+}
+
+void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
+              float gamma, float* out, int64_t out_ld, bool symmetric, void* stream) {
+  launch::rbf_gemm_store(a, asq, m, ld, b, bsq, n, ld, ld, gamma, out, out_ld, (hipStream_t)stream, symmetric);
 }
 
 int64_t compact_nonzero(const float* alpha, int64_t n, int* idx_out, void* stream) {

@@ -37,6 +37,30 @@ def row_sqnorm(x: torch.Tensor) -> torch.Tensor:
     return out[: x.shape[0]]
 
 
+def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0) -> torch.Tensor:
+    """Gram block K[i, j] = exp(-gamma |a_i - b_j|^2) with the dense-mode MFMA
+    GEMM (32x32x2 f32, fused exp).  b=None: the symmetric Gram of a, computed
+    as upper-triangle tiles plus their mirrored transposes."""
+    C = load()
+    sym = b is None
+    ap, dp = _pad_rows_cols(a)
+    bp = ap if sym else _pad_rows_cols(b)[0]
+    asq = torch.zeros(ap.shape[0], device=a.device)
+    C.k_row_sqnorm(ap.data_ptr(), ap.shape[0], dp, dp, asq.data_ptr(), _stream(a))
+    if sym:
+        bsq = asq
+    else:
+        bsq = torch.zeros(bp.shape[0], device=a.device)
+        C.k_row_sqnorm(bp.data_ptr(), bp.shape[0], dp, dp, bsq.data_ptr(), _stream(a))
+    m = a.shape[0]
+    n = m if sym else b.shape[0]
+    ld = (n + 127) // 128 * 128
+    out = torch.full((m, ld), float("nan"), device=a.device)
+    C.k_rbf_gram(ap.data_ptr(), asq.data_ptr(), m, bp.data_ptr(), bsq.data_ptr(), n, dp, float(gamma),
+                 out.data_ptr(), ld, sym, _stream(a))
+    return out[:, :n]
+
+
 def rbf_rows(x: torch.Tensor, w: torch.Tensor, gamma: float) -> torch.Tensor:
     """K[q, j] = exp(-gamma |x_j - w_q|^2) for up to 16 query rows w (the
     smo_rows MFMA 16x16x4 kernel)."""

@@ -106,3 +106,20 @@ def test_compact(K):
     got = K.compact_positive(a).long()
     ref = torch.nonzero(a > 0).flatten()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("n,d", [(1000, 40), (777, 784), (256, 16)])
+def test_rbf_gram_symmetric_mirror(K, n, d):
+    """Dense-mode Gram GEMM: symmetric launch (upper tiles + mirrored
+    transposes) == full launch bit for bit, and == fp32 reference."""
+    g = torch.Generator().manual_seed(n + d)
+    x = torch.rand(n, d, generator=g).cuda()
+    gamma = 1.0 / d
+    full = K.rbf_gram(x, x.clone(), gamma)
+    sym = K.rbf_gram(x, None, gamma)
+    torch.cuda.synchronize()
+    assert torch.isfinite(sym).all()
+    assert torch.equal(full, sym)
+    assert torch.equal(sym, sym.T)
+    ref = torch.exp(-gamma * torch.cdist(x.double(), x.double()) ** 2).float()
+    assert torch.allclose(sym, ref, atol=2e-5, rtol=1e-4)
