@@ -91,6 +91,11 @@ def main(argv=None) -> int:
     from dpsvm_amd.parallel import init_distributed, make_comm, shutdown
     from dpsvm_amd.utils.datasets import synthetic
 
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # cross-rank alpha digest after every run (one 16-byte all-reduce): a
+        # diverged run fails loudly instead of reporting a time
+        os.environ.setdefault("DPSVM_VERIFY", "1")
+        os.environ.setdefault("DPSVM_XCH_TIMEOUT_S", "30")
     C = load()
     ctx = init_distributed(device=a.device)
     on_gpu = ctx.device.startswith("cuda")
@@ -119,6 +124,21 @@ def main(argv=None) -> int:
         solver = C.GpuSolver(params, comm, ctx.local_rank)
         info = solver.setup(X, X.shape[0], y)
         run = lambda: solver.solve()  # noqa: E731
+        if n_ranks > 1 and info.get("exchange") == "peer" and a.exchange == "auto":
+            # the in-kernel peer exchange is self-tested at setup; if a warmup run still
+            # fails on it (every rank fails the same way), fall back to the collective path
+            try:
+                run()
+            except C.NativeError as e:
+                if ctx.rank == 0:
+                    print(f"[bench] peer exchange run failed ({e}); falling back to the all-reduce",
+                          file=sys.stderr)
+                del solver
+                cfg.exchange, cfg.persist = "allreduce", "off"
+                params = cfg.to_native(X.shape[1])
+                solver = C.GpuSolver(params, comm, ctx.local_rank)
+                info = solver.setup(X, X.shape[0], y)
+                run = lambda: solver.solve()  # noqa: E731
     else:
         info = {"device_name": "cpu", "x_replicated": True, "cache_lines": 0}
         run = lambda: C.solve_cpu(X, y, params, comm if n_ranks > 1 else None)  # noqa: E731

@@ -52,10 +52,24 @@ __device__ __forceinline__ void commit_pending(const SmoArgs& a, const FusedRec&
 // per-workgroup min of two keys -> p_out[blockIdx], or (peer exchange)
 // pushed with the alphas of their rows to every rank, parity xpar / tag
 // (the kernel's one barrier)
+// key minimum; XCH: carry the alphas of the rows (peer exchange payload)
+template <bool XCH>
+__device__ __forceinline__ void key_min(XKeys& m, uint64_t kh, uint64_t kl, float ah, float al) {
+  if (kh < m.kh) {
+    m.kh = kh;
+    if (XCH) m.ah = ah;
+  }
+  if (kl < m.kl) {
+    m.kl = kl;
+    if (XCH) m.al = al;
+  }
+}
+
+template <bool XCH>
 __device__ __forceinline__ void store_block_keys(const SmoArgs& a, XKeys k, uint64_t* p_out, uint64_t* scr,
                                                  float* fscr, int xpar, uint32_t tag) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (a.xworld > 0) {
+  if (XCH) {
     k = wave_min_xk(k);  // keys with the alphas of their rows
   } else {
     k.kh = wave_min_u64(k.kh);  // keys only
@@ -68,7 +82,7 @@ __device__ __forceinline__ void store_block_keys(const SmoArgs& a, XKeys k, uint
     fscr[4 + wave] = k.al;
   }
   __syncthreads();
-  if (a.xworld > 0) {
+  if (XCH) {
     if (wave == 0) {
 #pragma unroll
       for (int w = 1; w < kFusedThreads / 64; ++w) xk_min(k, XKeys{scr[w], scr[4 + w], fscr[w], fscr[4 + w]});
@@ -90,6 +104,7 @@ __device__ __forceinline__ void store_block_keys(const SmoArgs& a, XKeys k, uint
   }
 }
 
+template <bool XCH>
 __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int mode,
                                                                   const uint64_t* __restrict__ p_in,
                                                                   uint64_t* __restrict__ p_out,
@@ -128,12 +143,12 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       const float fj = j == j0 ? f0 : a.f[j];
       const float av = j == j0 ? a0 : a.alpha[g];
       const float yv = j == j0 ? y0 : a.y[g];
-      if (in_up(av, yv, a.C)) xk_min(k, XKeys{make_key(fj, (uint32_t)g), kKeyNone, av, 0.f});
-      if (in_low(av, yv, a.C)) xk_min(k, XKeys{kKeyNone, make_key(-fj, (uint32_t)g), 0.f, av});
+      if (in_up(av, yv, a.C)) key_min<XCH>(k, make_key(fj, (uint32_t)g), kKeyNone, av, 0.f);
+      if (in_low(av, yv, a.C)) key_min<XCH>(k, kKeyNone, make_key(-fj, (uint32_t)g), 0.f, av);
     }
     // peer exchange: the seed's keys carry tag iter0 + 1 (r_in = the seed record)
-    const uint32_t tag = a.xworld > 0 ? (uint32_t)r_in->iter + 1u : 0u;
-    store_block_keys(a, k, p_out, kscr, fscr, (int)(tag & 1u), tag);
+    const uint32_t tag = XCH ? (uint32_t)r_in->iter + 1u : 0u;
+    store_block_keys<XCH>(a, k, p_out, kscr, fscr, (int)(tag & 1u), tag);
     return;
   }
 
@@ -141,7 +156,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
   // ---- 1. global pair: every wave reduces all workgroup keys (16-B loads) ----
   uint64_t kh = kKeyNone, kl = kKeyNone;
   const u64x2* pk = (const u64x2*)p_in;
-  if (a.xworld == 0) {
+  if (!XCH) {
     for (int b = lane; b < a.fused_G; b += 64) {
       const u64x2 v = pk[b];
       kh = v.x < kh ? v.x : kh;
@@ -149,7 +164,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
     }
   }
   XKeys xk = xk_none();
-  if (rin.done == kRunning && a.xworld > 0 &&
+  if (XCH && rin.done == kRunning &&
       !xch_poll(a, a.xpeer[a.xrank], (int)(((uint32_t)rin.iter + 1u) & 1u), (uint32_t)rin.iter + 1u, xk, lane,
                 64)) {
     // a peer stopped publishing: give up (every rank that times out stops the same way)
@@ -163,7 +178,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
     }
     return;
   }
-  if (a.xworld > 0) {  // per-lane minima of the polled entries (alphas unused: memory + record)
+  if (XCH) {  // per-lane minima of the polled entries (alphas unused: memory + record)
     kh = xk.kh;
     kl = xk.kl;
   }
@@ -272,13 +287,13 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
       else if (g == rin.i_lo) av = rin.a_lo;
       else av = first ? a0 : a.alpha[g];
       const float yv = first ? y0 : a.y[g];
-      if (in_up(av, yv, a.C)) xk_min(nk, XKeys{make_key(fj, (uint32_t)g), kKeyNone, av, 0.f});
-      if (in_low(av, yv, a.C)) xk_min(nk, XKeys{kKeyNone, make_key(-fj, (uint32_t)g), 0.f, av});
+      if (in_up(av, yv, a.C)) key_min<XCH>(nk, make_key(fj, (uint32_t)g), kKeyNone, av, 0.f);
+      if (in_low(av, yv, a.C)) key_min<XCH>(nk, kKeyNone, make_key(-fj, (uint32_t)g), 0.f, av);
     }
   }
   stamp(rin.iter, 3, 0);
   if (done != kRunning) return;  // uniform
-  store_block_keys(a, nk, p_out, kscr, fscr, (int)(((uint32_t)iter + 1u) & 1u), (uint32_t)iter + 1u);
+  store_block_keys<XCH>(a, nk, p_out, kscr, fscr, (int)(((uint32_t)iter + 1u) & 1u), (uint32_t)iter + 1u);
   stamp(rin.iter, 4, 0);
 }
 
@@ -318,7 +333,7 @@ void preload_fused_kernels(hipStream_t s) {
   SmoArgs z{};
   z.fused_G = 1;
   z.fused_rows = kFusedThreads;
-  dev::smo_fused_kernel<<<1, kFusedThreads, 0, s>>>(z, 0, nullptr, (uint64_t*)scratch, nullptr, nullptr);
+  dev::smo_fused_kernel<false><<<1, kFusedThreads, 0, s>>>(z, 0, nullptr, (uint64_t*)scratch, nullptr, nullptr);
   dev::xch_ping_kernel<<<1, 64, 0, s>>>(nullptr, 0, 0, 0, 1u, 0, (int32_t*)scratch + 32);
   HIP_CHECK(hipStreamSynchronize(s));
   HIP_CHECK(hipGetLastError());
@@ -333,7 +348,10 @@ void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uin
 
 void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out, const FusedRec* r_in,
                FusedRec* r_out, hipStream_t s) {
-  dev::smo_fused_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out);
+  if (a.xworld > 0)
+    dev::smo_fused_kernel<true><<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out);
+  else
+    dev::smo_fused_kernel<false><<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, mode, p_in, p_out, r_in, r_out);
   post_launch("smo_fused", s);
 }
 
