@@ -284,3 +284,21 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
         assert res[k]["exchange"] == "peer"
         assert res[k]["iters"] == ref.n_iter_
         assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
+
+
+def test_bench_two_processes_exchange_fallback(tmp_path):
+    """bench.py with 2 ranks: a peer exchange that gives up (1 us poll bound)
+    makes every rank fail the warmup run the same way; the bench falls back
+    to the all-reduce path and still reports a verified time."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="0.000001")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29611", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--samples", "4000", "--steps", "1", "--warmup", "1", "--comm", "gloo"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
+    assert out["exchange"] == "allreduce" and out["converged"] and out["n_gpus"] == 2
+    assert "falling back" in r.stderr
