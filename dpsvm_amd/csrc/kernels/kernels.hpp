@@ -22,7 +22,7 @@ void smo_finalize(const SmoArgs& a, hipStream_t s);
 size_t smo_rows_lds_bytes(int dp);
 // cache mode, replicated X: one fused SMO iteration with in-launch line fills
 bool smo_fused_lru_supported(int dp);
-size_t smo_fused_lru_lds_bytes(int dp);
+size_t smo_fused_lru_lds_bytes(int dp, int fused_rows);
 void smo_fused_lru(const SmoArgs& a, const uint64_t* p_in, uint64_t* p_out, const FusedCacheRec* r_in,
                    FusedCacheRec* r_out, hipStream_t s);
 // dense mode: init (selection only, mode 0; r_in = the seed record when

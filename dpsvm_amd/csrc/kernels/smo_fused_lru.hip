@@ -563,18 +563,111 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
       const bool qv = q < n_new && pl.op[q] == kOpCompute;
       const float wsq = qv ? a.xsq[pl.key[q]] : 0.f;
       const int64_t xbase = a.off - a.x_row0;
-      // 256 rows per pass: 4 waves x 4 tiles of 16 rows; query vectors staged in
-      // LDS in k-chunks of kRowsKC (same k order as smo_rows: bit-identical rows)
-      for (int64_t r0 = row0; r0 < row_end; r0 += 256) {
-        f4 acc[4];
+      const int npass = (int)((row_end - row0 + 255) / 256);
+      float* xsq_s = wsm + kNQ * ((dp < kRowsKC ? dp : kRowsKC) + 4);  // [fused_rows] |x_j|^2 of own rows
+      // X loads in batches of 4 k-steps x 4 tiles (16 KiB per wave in flight,
+      // one workgroup per CU: the pass is HBM-latency bound without deep
+      // prefetch); sched_barrier keeps the scheduler from sinking the loads
+      // back next to their MFMAs.  Same k order as smo_rows: bit-identical rows.
+      f4 acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
+      auto xrow = [&](int pass) {
+        return a.x + (xbase + row0 + (int64_t)pass * 256 + wave * 64 + (lane & 15)) * dp + 4 * (lane >> 4);
+      };
+      auto load = [&](f4 (&v)[4][4], const float* xk, int k) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[s][t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k + 16 * s);
+      };
+      auto comp = [&](const f4 (&v)[4][4], const float* wr, int k) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const f4 wv = *(const f4*)(wr + k + 16 * s);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            acc[t] = mfma16(v[s][t].x, wv.x, acc[t]);
+            acc[t] = mfma16(v[s][t].y, wv.y, acc[t]);
+            acc[t] = mfma16(v[s][t].z, wv.z, acc[t]);
+            acc[t] = mfma16(v[s][t].w, wv.w, acc[t]);
+          }
+        }
+      };
+      auto comp16 = [&](const float* xk, const float* wr, int k0, int k1) {  // 16-wide k-steps [k0, k1)
+        for (int k = k0; k < k1; k += 16) {
+          const f4 wv = *(const f4*)(wr + k);
+          f4 xv[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) xv[t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            acc[t] = mfma16(xv[t].x, wv.x, acc[t]);
+            acc[t] = mfma16(xv[t].y, wv.y, acc[t]);
+            acc[t] = mfma16(xv[t].z, wv.z, acc[t]);
+            acc[t] = mfma16(xv[t].w, wv.w, acc[t]);
+          }
+        }
+      };
+      auto epilogue = [&](int pass) {  // K values of this pass's 256 rows -> the new lines
+        if (qv) {
+          float* out = a.lines + (int64_t)pl.line[q] * a.ldl + row0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int rel = pass * 256 + wave * 64 + t * 16 + (lane >> 4) * 4;
+            f4 kv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) kv[r] = rbf_from_dot(xsq_s[rel + r], wsq, acc[t][r], a.gamma);
+            *(f4*)(out + rel) = kv;
+          }
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
-        const float* xr = a.x + (xbase + r0 + wave * 64 + (lane & 15)) * dp + 4 * (lane >> 4);
-        for (int kc = 0; kc < dp; kc += kRowsKC) {
-          const int kcl = min(kRowsKC, dp - kc), ldw = kcl + 4, k4n = kcl >> 2;
-          const bool restage = dp > kRowsKC;  // else the single chunk stays resident
-          if (restage || r0 == row0) {
-            if (restage) __syncthreads();  // previous readers of the staged chunk are done
+      };
+      // own rows' |x|^2 staged once (one round trip instead of one per pass)
+      for (int i = tid; i < npass * 256; i += kFusedThreads) xsq_s[i] = a.xsq[a.off + row0 + i];
+      if (dp <= kRowsKC) {
+        // single staged chunk: the batch sequence runs across passes, so the
+        // next pass's first X batch is in flight during this pass's epilogue
+        const int ldw = dp + 4, k4n = dp >> 2;
+        for (int i = tid; i < kNQ * k4n; i += kFusedThreads) {
+          const int qq = i / k4n, k4 = i - qq * k4n;
+          f4 v = {0.f, 0.f, 0.f, 0.f};
+          if (qq < n_new && pl.op[qq] == kOpCompute) v = *(const f4*)(a.x + ((int64_t)pl.key[qq] - a.x_row0) * dp + 4 * k4);
+          *(f4*)(wsm + qq * ldw + 4 * k4) = v;
+        }
+        __syncthreads();
+        const float* wr = wsm + q * ldw + 4 * (lane >> 4);
+        const int nb = dp >> 6, S = npass * nb;
+        auto finish = [&](int pass) {
+          comp16(xrow(pass), wr, nb * 64, dp);  // remainder k-steps (dp % 64)
+          epilogue(pass);
+        };
+        if (nb == 0) {
+          for (int pass = 0; pass < npass; ++pass) finish(pass);
+        } else {
+          f4 xa[4][4], xb[4][4];
+          load(xa, xrow(0), 0);
+          for (int st = 0; st < S; st += 2) {
+            if (st + 1 < S) load(xb, xrow((st + 1) / nb), ((st + 1) % nb) * 64);
+            __builtin_amdgcn_sched_barrier(0);
+            comp(xa, wr, (st % nb) * 64);
+            if ((st + 1) % nb == 0) finish(st / nb);
+            if (st + 1 < S) {
+              if (st + 2 < S) load(xa, xrow((st + 2) / nb), ((st + 2) % nb) * 64);
+              __builtin_amdgcn_sched_barrier(0);
+              comp(xb, wr, ((st + 1) % nb) * 64);
+              if ((st + 2) % nb == 0) finish((st + 1) / nb);
+            }
+          }
+        }
+      } else {
+        // wide rows: query vectors restaged per k-chunk of kRowsKC
+        for (int pass = 0; pass < npass; ++pass) {
+          const float* xr = xrow(pass);
+          for (int kc = 0; kc < dp; kc += kRowsKC) {
+            const int kcl = min(kRowsKC, dp - kc), ldw = kcl + 4, k4n = kcl >> 2;
+            __syncthreads();  // previous readers of the staged chunk are done
             for (int i = tid; i < kNQ * k4n; i += kFusedThreads) {
               const int qq = i / k4n, k4 = i - qq * k4n;
               f4 v = {0.f, 0.f, 0.f, 0.f};
@@ -583,70 +676,23 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
               *(f4*)(wsm + qq * ldw + 4 * k4) = v;
             }
             __syncthreads();
-          }
-          const float* wr = wsm + q * ldw + 4 * (lane >> 4);
-          const float* xk = xr + kc;
-          // X loads double-buffered in batches of 4 k-steps x 4 tiles (16 KiB
-          // per wave in flight; one workgroup per CU, so the pass is
-          // HBM-latency bound without deep prefetch).  sched_barrier keeps the
-          // scheduler from sinking the loads back next to their MFMAs.
-          const int nb = kcl >> 6;
-          f4 xa[4][4], xb[4][4];
-          auto load = [&](f4 (&v)[4][4], int k) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-              for (int t = 0; t < 4; ++t) v[s][t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k + 16 * s);
-          };
-          auto comp = [&](const f4 (&v)[4][4], int k) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const f4 wv = *(const f4*)(wr + k + 16 * s);
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                acc[t] = mfma16(v[s][t].x, wv.x, acc[t]);
-                acc[t] = mfma16(v[s][t].y, wv.y, acc[t]);
-                acc[t] = mfma16(v[s][t].z, wv.z, acc[t]);
-                acc[t] = mfma16(v[s][t].w, wv.w, acc[t]);
+            const float* wr = wsm + q * ldw + 4 * (lane >> 4) - kc;  // indexed with absolute k
+            const int nb = kcl >> 6;
+            f4 xa[4][4], xb[4][4];
+            if (nb > 0) load(xa, xr, kc);
+            for (int bb = 0; bb < nb; bb += 2) {
+              if (bb + 1 < nb) load(xb, xr, kc + (bb + 1) * 64);
+              __builtin_amdgcn_sched_barrier(0);
+              comp(xa, wr, kc + bb * 64);
+              if (bb + 1 < nb) {
+                if (bb + 2 < nb) load(xa, xr, kc + (bb + 2) * 64);
+                __builtin_amdgcn_sched_barrier(0);
+                comp(xb, wr, kc + (bb + 1) * 64);
               }
             }
-          };
-          if (nb > 0) load(xa, 0);
-          for (int b = 0; b < nb; b += 2) {
-            if (b + 1 < nb) load(xb, (b + 1) * 64);
-            __builtin_amdgcn_sched_barrier(0);
-            comp(xa, b * 64);
-            if (b + 1 < nb) {
-              if (b + 2 < nb) load(xa, (b + 2) * 64);
-              __builtin_amdgcn_sched_barrier(0);
-              comp(xb, (b + 1) * 64);
-            }
+            comp16(xr, wr, kc + nb * 64, kc + kcl);
           }
-          int k0 = nb * 64;
-          for (; k0 < kcl; k0 += 16) {
-            const f4 wv = *(const f4*)(wr + k0);
-            f4 xv[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) xv[t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k0);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              acc[t] = mfma16(xv[t].x, wv.x, acc[t]);
-              acc[t] = mfma16(xv[t].y, wv.y, acc[t]);
-              acc[t] = mfma16(xv[t].z, wv.z, acc[t]);
-              acc[t] = mfma16(xv[t].w, wv.w, acc[t]);
-            }
-          }
-        }
-        if (qv) {
-          float* out = a.lines + (int64_t)pl.line[q] * a.ldl;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int64_t base = r0 + wave * 64 + t * 16 + (lane >> 4) * 4;
-            f4 kv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) kv[r] = rbf_from_dot(a.xsq[a.off + base + r], wsq, acc[t][r], a.gamma);
-            *(f4*)(out + base) = kv;
-          }
+          epilogue(pass);
         }
       }
     }
@@ -704,32 +750,50 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   if (done == kNonFinite || done == kNoPair) return;
 
   // ---- 4. f update + classification of this workgroup's rows ----
+  // rows in chunks of kRowChunk per thread, every load of a chunk in flight
+  // together (one round trip per chunk instead of one per row)
   const bool upd_f = c_hi != 0.f || c_lo != 0.f;
   const float* line_hi = pl.line_hi >= 0 ? a.lines + (int64_t)pl.line_hi * a.ldl : nullptr;
   const float* line_lo = pl.line_lo >= 0 ? a.lines + (int64_t)pl.line_lo * a.ldl : nullptr;
   uint64_t nh = kKeyNone, nlk = kKeyNone;
-  for (int64_t j = j0; j < row_end; j += kFusedThreads) {
-    const bool first = j == j0;
-    const int64_t g = a.off + j;
-    float fj = first ? f0 : a.f[j];
-    if (upd_f) {
-      float delta;
-      if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * line_hi[j]) + (c_lo * line_lo[j]);
-      else if (c_hi != 0.f) delta = c_hi * line_hi[j];
-      else delta = c_lo * line_lo[j];
-      fj += delta;
-      a.f[j] = fj;
+  constexpr int kRowChunk = 8;
+  for (int64_t jb = j0; jb < row_end; jb += (int64_t)kRowChunk * kFusedThreads) {
+    float fv[kRowChunk], hv[kRowChunk], lv[kRowChunk], av[kRowChunk], yy[kRowChunk];
+#pragma unroll
+    for (int c = 0; c < kRowChunk; ++c) {
+      const int64_t j = jb + (int64_t)c * kFusedThreads;
+      const bool first = j == j0;
+      const int64_t jj = j < row_end ? j : j0;  // in-bounds address for idle slots
+      fv[c] = first ? f0 : a.f[jj];
+      hv[c] = c_hi != 0.f ? line_hi[jj] : 0.f;
+      lv[c] = c_lo != 0.f ? line_lo[jj] : 0.f;
+      av[c] = first ? a0 : a.alpha[a.off + jj];
+      yy[c] = first ? y0 : a.y[a.off + jj];
     }
-    if (done == kRunning) {
-      float av;
-      if (g == i_hi) av = a_hi_new;
-      else if (g == i_lo) av = a_lo_new;
-      else if (g == rin.i_hi) av = rin.a_hi;
-      else if (g == rin.i_lo) av = rin.a_lo;
-      else av = first ? a0 : a.alpha[g];
-      const float yv = first ? y0 : a.y[g];
-      if (in_up(av, yv, a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
-      if (in_low(av, yv, a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
+#pragma unroll
+    for (int c = 0; c < kRowChunk; ++c) {
+      const int64_t j = jb + (int64_t)c * kFusedThreads;
+      if (j >= row_end) continue;
+      const int64_t g = a.off + j;
+      float fj = fv[c];
+      if (upd_f) {
+        float delta;
+        if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * hv[c]) + (c_lo * lv[c]);
+        else if (c_hi != 0.f) delta = c_hi * hv[c];
+        else delta = c_lo * lv[c];
+        fj += delta;
+        a.f[j] = fj;
+      }
+      if (done == kRunning) {
+        float al;
+        if (g == i_hi) al = a_hi_new;
+        else if (g == i_lo) al = a_lo_new;
+        else if (g == rin.i_hi) al = rin.a_hi;
+        else if (g == rin.i_lo) al = rin.a_lo;
+        else al = av[c];
+        if (in_up(al, yy[c], a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
+        if (in_low(al, yy[c], a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
+      }
     }
   }
   if (done != kRunning) return;  // uniform
@@ -758,13 +822,23 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
 
 namespace launch {
 
-size_t smo_fused_lru_lds_bytes(int dp) { return (size_t)kNQ * ((dp < kRowsKC ? dp : kRowsKC) + 4) * sizeof(float); }
+size_t smo_fused_lru_lds_bytes(int dp, int fused_rows) {
+  return ((size_t)kNQ * ((dp < kRowsKC ? dp : kRowsKC) + 4) + (size_t)fused_rows) * sizeof(float);
+}
 
 bool smo_fused_lru_supported(int dp) { return dp >= 16 && dp % 16 == 0; }
 
 void smo_fused_lru(const SmoArgs& a, const uint64_t* p_in, uint64_t* p_out, const FusedCacheRec* r_in,
                    FusedCacheRec* r_out, hipStream_t s) {
-  dev::smo_fused_lru_kernel<<<dim3(a.fused_G), kFusedThreads, smo_fused_lru_lds_bytes(a.dp), s>>>(a, p_in, p_out,
+  const size_t lds = smo_fused_lru_lds_bytes(a.dp, a.fused_rows);
+  static bool attr_set = false;  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  if (!attr_set) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)dev::smo_fused_lru_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    attr_set = true;
+  }
+  DPSVM_CHECK(lds <= 160 * 1024, "smo_fused_lru: LDS budget exceeded");
+  dev::smo_fused_lru_kernel<<<dim3(a.fused_G), kFusedThreads, lds, s>>>(a, p_in, p_out,
                                                                                                   r_in, r_out);
   post_launch("smo_fused_lru", s);
 }
