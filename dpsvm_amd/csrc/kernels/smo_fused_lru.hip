@@ -831,13 +831,12 @@ bool smo_fused_lru_supported(int dp) { return dp >= 16 && dp % 16 == 0; }
 void smo_fused_lru(const SmoArgs& a, const uint64_t* p_in, uint64_t* p_out, const FusedCacheRec* r_in,
                    FusedCacheRec* r_out, hipStream_t s) {
   const size_t lds = smo_fused_lru_lds_bytes(a.dp, a.fused_rows);
-  static bool attr_set = false;  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
-  if (!attr_set) {
+  static size_t attr_bytes = 64 * 1024;  // dynamic LDS above 64 KiB needs the attribute (160 KiB LDS on gfx950)
+  if (lds > attr_bytes) {
     HIP_CHECK(hipFuncSetAttribute((const void*)dev::smo_fused_lru_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024));
-    attr_set = true;
+                                  (int)lds));
+    attr_bytes = lds;
   }
-  DPSVM_CHECK(lds <= 160 * 1024, "smo_fused_lru: LDS budget exceeded");
   dev::smo_fused_lru_kernel<<<dim3(a.fused_G), kFusedThreads, lds, s>>>(a, p_in, p_out,
                                                                                                   r_in, r_out);
   post_launch("smo_fused_lru", s);
