@@ -98,6 +98,7 @@ struct SolveResult {
   int64_t host_hits = 0, spec_rows = 0;
   int64_t cache_lines = 0, host_cache_lines = 0;
   int world = 1;
+  double verify_f_err = -1.0;  // DPSVM_VERIFY: max |f - f(alpha)| / (1 + |f(alpha)|), -1 = not run
   bool converged() const { return status == 1; }
 };
 

@@ -21,6 +21,8 @@
 // launch: they apply the previous record as a correction instead.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dpsvm/common.hpp"
 #include "dpsvm/device_state.hpp"
 #include "device_util.hpp"
@@ -243,13 +245,6 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
   const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
   const int64_t j0 = row0 + tid;
-  const bool has0 = j0 < row_end;
-  float f0 = 0.f, a0 = 0.f, y0 = 0.f;
-  if (has0) {
-    f0 = a.f[j0];
-    a0 = a.alpha[a.off + j0];
-    y0 = a.y[a.off + j0];
-  }
   const FusedCacheRec& rin = *r_in;  // read through the scalar cache (never written this launch)
   if (tid < 5 * kNQ) {
     const int arr = tid / kNQ, q = tid - arr * kNQ;
@@ -750,52 +745,62 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
   if (done == kNonFinite || done == kNoPair) return;
 
   // ---- 4. f update + classification of this workgroup's rows ----
-  // rows in chunks of kRowChunk per thread, every load of a chunk in flight
-  // together (one round trip per chunk instead of one per row)
+  // All of a thread's rows in one chunk when they fit (<= 12): every load of the
+  // chunk is issued unconditionally (idle slots and absent lines read a safe
+  // in-bounds address) so the whole chunk is one round trip with no branches.
   const bool upd_f = c_hi != 0.f || c_lo != 0.f;
-  const float* line_hi = pl.line_hi >= 0 ? a.lines + (int64_t)pl.line_hi * a.ldl : nullptr;
-  const float* line_lo = pl.line_lo >= 0 ? a.lines + (int64_t)pl.line_lo * a.ldl : nullptr;
+  const float* lh = pl.line_hi >= 0 ? a.lines + (int64_t)pl.line_hi * a.ldl : a.f;
+  const float* ll = pl.line_lo >= 0 ? a.lines + (int64_t)pl.line_lo * a.ldl : a.f;
+  const float chv = c_hi, clv = c_lo;
+  const float* fa = a.f;
+  const float* aa = a.alpha + a.off;
+  const float* ya = a.y + a.off;
   uint64_t nh = kKeyNone, nlk = kKeyNone;
-  constexpr int kRowChunk = 8;
-  for (int64_t jb = j0; jb < row_end; jb += (int64_t)kRowChunk * kFusedThreads) {
-    float fv[kRowChunk], hv[kRowChunk], lv[kRowChunk], av[kRowChunk], yy[kRowChunk];
+  auto rows_chunked = [&](auto chunk) {
+    constexpr int CH = decltype(chunk)::value;
+    for (int64_t jb = j0; jb < row_end; jb += (int64_t)CH * kFusedThreads) {
+      float fv[CH], hv[CH], lv[CH], av[CH], yy[CH];
 #pragma unroll
-    for (int c = 0; c < kRowChunk; ++c) {
-      const int64_t j = jb + (int64_t)c * kFusedThreads;
-      const bool first = j == j0;
-      const int64_t jj = j < row_end ? j : j0;  // in-bounds address for idle slots
-      fv[c] = first ? f0 : a.f[jj];
-      hv[c] = c_hi != 0.f ? line_hi[jj] : 0.f;
-      lv[c] = c_lo != 0.f ? line_lo[jj] : 0.f;
-      av[c] = first ? a0 : a.alpha[a.off + jj];
-      yy[c] = first ? y0 : a.y[a.off + jj];
-    }
+      for (int c = 0; c < CH; ++c) {
+        const int64_t j = jb + (int64_t)c * kFusedThreads;
+        const int64_t jj = j < row_end ? j : j0;  // in-bounds address for idle slots
+        fv[c] = fa[jj];
+        hv[c] = lh[jj];
+        lv[c] = ll[jj];
+        av[c] = aa[jj];
+        yy[c] = ya[jj];
+      }
 #pragma unroll
-    for (int c = 0; c < kRowChunk; ++c) {
-      const int64_t j = jb + (int64_t)c * kFusedThreads;
-      if (j >= row_end) continue;
-      const int64_t g = a.off + j;
-      float fj = fv[c];
-      if (upd_f) {
-        float delta;
-        if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * hv[c]) + (c_lo * lv[c]);
-        else if (c_hi != 0.f) delta = c_hi * hv[c];
-        else delta = c_lo * lv[c];
-        fj += delta;
-        a.f[j] = fj;
-      }
-      if (done == kRunning) {
-        float al;
-        if (g == i_hi) al = a_hi_new;
-        else if (g == i_lo) al = a_lo_new;
-        else if (g == rin.i_hi) al = rin.a_hi;
-        else if (g == rin.i_lo) al = rin.a_lo;
-        else al = av[c];
-        if (in_up(al, yy[c], a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
-        if (in_low(al, yy[c], a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
+      for (int c = 0; c < CH; ++c) {
+        const int64_t j = jb + (int64_t)c * kFusedThreads;
+        if (j >= row_end) break;  // slots are in increasing j
+        const int64_t g = a.off + j;
+        float fj = fv[c];
+        if (upd_f) {
+          float delta;
+          if (chv != 0.f && clv != 0.f) delta = (chv * hv[c]) + (clv * lv[c]);
+          else if (chv != 0.f) delta = chv * hv[c];
+          else delta = clv * lv[c];
+          fj += delta;
+          a.f[j] = fj;
+        }
+        if (done == kRunning) {
+          float al;
+          if (g == i_hi) al = a_hi_new;
+          else if (g == i_lo) al = a_lo_new;
+          else if (g == rin.i_hi) al = rin.a_hi;
+          else if (g == rin.i_lo) al = rin.a_lo;
+          else al = av[c];
+          if (in_up(al, yy[c], a.C)) { const uint64_t k = make_key(fj, (uint32_t)g); nh = k < nh ? k : nh; }
+          if (in_low(al, yy[c], a.C)) { const uint64_t k = make_key(-fj, (uint32_t)g); nlk = k < nlk ? k : nlk; }
+        }
       }
     }
-  }
+  };
+  const int64_t rpt = (row_end - row0 + kFusedThreads - 1) / kFusedThreads;  // uniform
+  if (rpt <= 2) rows_chunked(std::integral_constant<int, 2>{});
+  else if (rpt <= 4) rows_chunked(std::integral_constant<int, 4>{});
+  else rows_chunked(std::integral_constant<int, 12>{});
   if (done != kRunning) return;  // uniform
   nh = wave_min_u64(nh);
   nlk = wave_min_u64(nlk);

@@ -108,6 +108,7 @@ py::dict result_dict(const SolveResult& r) {
   d["t_setup"] = r.t_setup;
   d["t_solve"] = r.t_solve;
   d["t_gram"] = r.t_gram;
+  d["verify_f_err"] = r.verify_f_err;
   d["cache_hits"] = r.cache_hits;
   d["cache_misses"] = r.cache_misses;
   d["rows_computed"] = r.rows_computed;

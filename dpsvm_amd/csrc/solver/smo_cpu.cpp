@@ -108,6 +108,21 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
   std::vector<float> alpha((size_t)n, 0.f);
   std::vector<float> f((size_t)nl);
   for (int64_t j = 0; j < nl; ++j) f[j] = -Y[off + j];  // f = -y (svmTrain.cu:380)
+  // f_j = sum_i alpha_i y_i K(i, j) - y_j from scratch (resume without f, DPSVM_VERIFY)
+  auto recompute_f = [&](std::vector<float>& out) {
+    pool.run(nl, [&](int, int64_t b, int64_t e) {
+      for (int64_t j = b; j < e; ++j) {
+        const float* xj = X + (size_t)(off + j) * d;
+        float s = 0.f;
+        for (int64_t i = 0; i < n; ++i) {
+          if (alpha[i] == 0.f) continue;
+          float d2 = xsq[i] + xsq[off + j] - 2.f * dot_f32(X + (size_t)i * d, xj, d);
+          s += alpha[i] * Y[i] * std::exp(-gamma * std::max(d2, 0.f));
+        }
+        out[j] = s - Y[off + j];
+      }
+    }, 64);
+  };
   int64_t iter0 = 0;
   float b_hi = 0.f, b_lo = 0.f;
   if (resume) {
@@ -119,19 +134,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
     if ((int64_t)resume->f.size() == n) {
       for (int64_t j = 0; j < nl; ++j) f[j] = resume->f[off + j];
     } else {
-      // recompute f_j = sum_i alpha_i y_i K(i,j) - y_j
-      pool.run(nl, [&](int, int64_t b, int64_t e) {
-        for (int64_t j = b; j < e; ++j) {
-          const float* xj = X + (size_t)(off + j) * d;
-          float s = 0.f;
-          for (int64_t i = 0; i < n; ++i) {
-            if (alpha[i] == 0.f) continue;
-            float d2 = xsq[i] + xsq[off + j] - 2.f * dot_f32(X + (size_t)i * d, xj, d);
-            s += alpha[i] * Y[i] * std::exp(-gamma * std::max(d2, 0.f));
-          }
-          f[j] = s - Y[off + j];
-        }
-      }, 64);
+      recompute_f(f);
     }
   }
 
@@ -261,6 +264,23 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
     if (iter >= p.max_iter) { status = 2; break; }
   }
   res.t_solve = secs_since(t0);
+  if (trace::verify_enabled()) {
+    // invariants: alpha in [0, C]; incremental f == f recomputed from alpha
+    for (int64_t i = 0; i < n; ++i)
+      if (!(alpha[i] >= 0.f && alpha[i] <= C))
+        fail("DPSVM_VERIFY: alpha[" + std::to_string(i) + "] outside [0, C]");
+    std::vector<float> fr((size_t)nl);
+    recompute_f(fr);
+    double err = 0.0;
+    for (int64_t j = 0; j < nl; ++j) {
+      const double e = std::fabs((double)f[j] - fr[j]) / (1.0 + std::fabs((double)fr[j]));
+      err = std::isfinite(e) ? std::max(err, e) : INFINITY;
+    }
+    res.verify_f_err = err;
+    const char* te = std::getenv("DPSVM_VERIFY_FTOL");
+    if (!(err <= (te ? atof(te) : 1e-3)))
+      fail("DPSVM_VERIFY: f inconsistent with alpha (max relative error " + std::to_string(err) + ")");
+  }
   if (world > 1 && trace::verify_enabled()) {
     // cross-rank consistency: every rank must hold bit-identical alphas
     const uint64_t h = trace::hash_floats(alpha.data(), alpha.size());

@@ -698,6 +698,122 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   return m.info;
 }
 
+// Support-vector set (rows, |x|^2, alpha*y) gathered from a host alpha; every rank
+// ends with all SVs (padded per-rank blocks in partitioned mode).
+namespace {
+struct SvSet {
+  int64_t nsv = 0;
+  float *sv = nullptr, *svsq = nullptr, *coef = nullptr;
+  size_t bytes = 0;
+  ~SvSet() {
+    for (void* p : {(void*)sv, (void*)svsq, (void*)coef}) if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+static void build_svs(GpuSolver::Impl& m, const SolveResult& r, SvSet& s) {
+  HIP_CHECK(hipMemcpyAsync(m.alpha, r.alpha.data(), m.n * 4, hipMemcpyHostToDevice, m.stream));
+  std::vector<int32_t> local_idx;
+  if (m.replicated) {
+    size_t tb = 0;
+    int32_t* idx = dmalloc<int32_t>((size_t)m.n, &tb);
+    int32_t* cnt = dmalloc<int32_t>(1, &tb);
+    int32_t* scratch = dmalloc<int32_t>((size_t)launch::compact_scratch_ints(m.n), &tb);
+    launch::compact_positive(m.alpha, m.n, idx, cnt, scratch, m.stream);
+    int32_t nsv = 0;
+    HIP_CHECK(hipMemcpyAsync(&nsv, cnt, 4, hipMemcpyDeviceToHost, m.stream));
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    s.nsv = nsv;
+    const int64_t pad = round_up(std::max<int64_t>(nsv, 1), 128) + 128;
+    s.sv = dmalloc<float>((size_t)pad * m.dp, &s.bytes);
+    s.svsq = dmalloc<float>((size_t)pad, &s.bytes);
+    s.coef = dmalloc<float>((size_t)pad, &s.bytes);
+    HIP_CHECK(hipMemsetAsync(s.sv, 0, (size_t)pad * m.dp * 4, m.stream));
+    HIP_CHECK(hipMemsetAsync(s.svsq, 0, pad * 4, m.stream));
+    HIP_CHECK(hipMemsetAsync(s.coef, 0, pad * 4, m.stream));
+    launch::gather_sv(m.x, 0, m.xsq, m.alpha, m.y, idx, nsv, m.dp, s.sv, s.svsq, s.coef, m.stream);
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    for (void* p : {(void*)idx, (void*)cnt, (void*)scratch}) (void)hipFree(p);
+  } else {
+    // partitioned: each rank gathers its local SVs; all-gather padded blocks
+    for (int64_t j = 0; j < m.nl; ++j)
+      if (r.alpha[m.off + j] > 0.f) local_idx.push_back((int32_t)(m.off + j));
+    std::vector<double> cnts((size_t)m.world, 0.0);
+    cnts[m.rank] = (double)local_idx.size();
+    if (m.world > 1) {
+      if (m.comm->device_memory()) {
+        size_t tb = 0;
+        double* dc = dmalloc<double>((size_t)m.world, &tb);
+        HIP_CHECK(hipMemcpy(dc, cnts.data(), m.world * 8, hipMemcpyHostToDevice));
+        m.comm->allreduce_sum_f64(dc, m.world, m.stream);
+        HIP_CHECK(hipMemcpyAsync(cnts.data(), dc, m.world * 8, hipMemcpyDeviceToHost, m.stream));
+        HIP_CHECK(hipStreamSynchronize(m.stream));
+        (void)hipFree(dc);
+      } else {
+        m.comm->allreduce_sum_f64(cnts.data(), m.world, nullptr);
+      }
+    }
+    int64_t maxc = 0, total = 0;
+    for (double c : cnts) { maxc = std::max<int64_t>(maxc, (int64_t)c); total += (int64_t)c; }
+    const int64_t per = std::max<int64_t>(1, maxc);
+    const int64_t pad = round_up(per * m.world, 128) + 128;
+    s.sv = dmalloc<float>((size_t)pad * m.dp, &s.bytes);
+    s.svsq = dmalloc<float>((size_t)pad, &s.bytes);
+    s.coef = dmalloc<float>((size_t)pad, &s.bytes);
+    HIP_CHECK(hipMemsetAsync(s.sv, 0, (size_t)pad * m.dp * 4, m.stream));
+    HIP_CHECK(hipMemsetAsync(s.svsq, 0, pad * 4, m.stream));
+    HIP_CHECK(hipMemsetAsync(s.coef, 0, pad * 4, m.stream));
+    size_t tb = 0;
+    int32_t* didx = dmalloc<int32_t>(std::max<size_t>(1, local_idx.size()), &tb);
+    if (!local_idx.empty()) {
+      HIP_CHECK(hipMemcpyAsync(didx, local_idx.data(), local_idx.size() * 4, hipMemcpyHostToDevice, m.stream));
+      launch::gather_sv(m.x, m.args.x_row0, m.xsq, m.alpha, m.y, didx, (int64_t)local_idx.size(), m.dp,
+                        s.sv + (size_t)m.rank * per * m.dp, s.svsq + m.rank * per, s.coef + m.rank * per,
+                        m.stream);
+    }
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    (void)hipFree(didx);
+    if (m.world > 1) {
+      // zero-padded blocks; coef = 0 on padding rows makes them inert
+      auto gather = [&](float* buf, int64_t elems) {
+        if (m.comm->device_memory()) {
+          m.comm->allgather(buf + (size_t)m.rank * elems, buf, elems * 4, m.stream);
+          HIP_CHECK(hipStreamSynchronize(m.stream));
+        } else {
+          std::vector<float> h((size_t)elems * m.world);
+          HIP_CHECK(hipMemcpy(h.data() + (size_t)m.rank * elems, buf + (size_t)m.rank * elems, elems * 4,
+                              hipMemcpyDeviceToHost));
+          m.comm->allgather(h.data() + (size_t)m.rank * elems, h.data(), elems * 4, nullptr);
+          HIP_CHECK(hipMemcpy(buf, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        }
+      };
+      gather(s.sv, per * m.dp);
+      gather(s.svsq, per);
+      gather(s.coef, per);
+    }
+    s.nsv = per * m.world;
+    (void)total;
+  }
+}
+
+
+// f-style decision values of this rank's rows without b: out_j = sum_i alpha_i y_i K(i, j)
+// for j in [off, off + nl), from a host alpha (length n).  Used to rebuild f on resume and
+// by the DPSVM_VERIFY consistency check; collective in partitioned mode (SV all-gather).
+static void local_decision(GpuSolver::Impl& m, const std::vector<float>& alpha, float* out_dev) {
+  SolveResult tmp;
+  tmp.alpha = alpha;
+  SvSet s;
+  build_svs(m, tmp, s);
+  size_t tb = 0;
+  float* part = dmalloc<float>((size_t)launch::predict_scratch_floats(m.nl, s.nsv), &tb);
+  const int64_t lrow = m.off - m.args.x_row0;
+  launch::rbf_predict(m.x + (size_t)lrow * m.dp, m.xsq + m.off, m.nl, m.dp, s.sv, s.svsq, s.coef, s.nsv,
+                      m.dp, m.dp, m.gamma, 0.f, part, out_dev, nullptr, nullptr, m.stream);
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  (void)hipFree(part);
+}
+
 SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progress) {
   auto& m = *impl_;
   HIP_CHECK(hipSetDevice(m.device));
@@ -721,35 +837,11 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     HIP_CHECK(hipMemcpyAsync(m.f, resume->f.data() + m.off, m.nl * 4, hipMemcpyHostToDevice, m.stream));
   } else if (resume) {
     // f_j = sum_i alpha_i y_i K(i, j) - y_j via the predict GEMM (b = 0)
-    std::vector<int32_t> idx;
-    std::vector<float> sv, coef, svsq;
-    for (int64_t i = 0; i < m.n; ++i)
-      if (resume->alpha[i] != 0.f) idx.push_back((int32_t)i);
-    DPSVM_CHECK(m.replicated || idx.empty(), "resume without f needs replicated X");
-    const int64_t nsv = (int64_t)idx.size(), nsv_pad = round_up(std::max<int64_t>(nsv, 1), 128) + 128;
-    size_t tmpb = 0;
-    int32_t* didx = dmalloc<int32_t>(std::max<size_t>(1, idx.size()), &tmpb);
-    float* dsv = dmalloc<float>((size_t)nsv_pad * m.dp, &tmpb);
-    float* dsq = dmalloc<float>((size_t)nsv_pad, &tmpb);
-    float* dcoef = dmalloc<float>((size_t)nsv_pad, &tmpb);
-    float* dpart = dmalloc<float>((size_t)launch::predict_scratch_floats(m.nl, nsv), &tmpb);
-    HIP_CHECK(hipMemsetAsync(dsv, 0, (size_t)nsv_pad * m.dp * 4, m.stream));
-    HIP_CHECK(hipMemsetAsync(dsq, 0, nsv_pad * 4, m.stream));
-    HIP_CHECK(hipMemsetAsync(dcoef, 0, nsv_pad * 4, m.stream));
-    if (nsv) {
-      HIP_CHECK(hipMemcpyAsync(didx, idx.data(), nsv * 4, hipMemcpyHostToDevice, m.stream));
-      launch::gather_sv(m.x, 0, m.xsq, m.alpha, m.y, didx, nsv, m.dp, dsv, dsq, dcoef, m.stream);
-    }
-    launch::rbf_predict(m.x + (size_t)m.off * m.dp, m.xsq + m.off, m.nl, m.dp, dsv, dsq, dcoef, nsv,
-                        m.dp, m.dp, m.gamma, 0.f, dpart, m.f, nullptr, nullptr, m.stream);
-    // f -= y
+    local_decision(m, resume->alpha, m.f);
     std::vector<float> fh((size_t)m.nl);
-    HIP_CHECK(hipMemcpyAsync(fh.data(), m.f, m.nl * 4, hipMemcpyDeviceToHost, m.stream));
-    HIP_CHECK(hipStreamSynchronize(m.stream));
+    HIP_CHECK(hipMemcpy(fh.data(), m.f, m.nl * 4, hipMemcpyDeviceToHost));
     for (int64_t j = 0; j < m.nl; ++j) fh[j] -= m.h_y[m.off + j];
-    HIP_CHECK(hipMemcpyAsync(m.f, fh.data(), m.nl * 4, hipMemcpyHostToDevice, m.stream));
-    HIP_CHECK(hipStreamSynchronize(m.stream));
-    for (void* ptr : {(void*)didx, (void*)dsv, (void*)dsq, (void*)dcoef, (void*)dpart}) (void)hipFree(ptr);
+    HIP_CHECK(hipMemcpy(m.f, fh.data(), m.nl * 4, hipMemcpyHostToDevice));
   } else {
     launch::init_f(m.y, m.off, m.nl, m.f, m.stream);
   }
@@ -876,6 +968,35 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   }
   // ================= end of timed region =================
 
+  if (trace::verify_enabled()) {
+    // invariants: alpha in [0, C]; f consistent with alpha, i.e. the
+    // incrementally updated f_j equals sum_i alpha_i y_i K(i, j) - y_j recomputed
+    // from scratch (MFMA predict GEMM); float drift over 10^5 updates stays ~1e-5.
+    std::vector<float> ah((size_t)m.n);
+    HIP_CHECK(hipMemcpy(ah.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < m.n; ++i)
+      if (!(ah[i] >= 0.f && ah[i] <= m.p.C))
+        fail("DPSVM_VERIFY: alpha[" + std::to_string(i) + "] = " + std::to_string(ah[i]) +
+             " outside [0, C]");
+    std::vector<float> fd((size_t)m.nl), fr((size_t)m.nl);
+    HIP_CHECK(hipMemcpy(fd.data(), m.f, m.nl * 4, hipMemcpyDeviceToHost));
+    size_t tb = 0;
+    float* dref = dmalloc<float>((size_t)m.nl, &tb);
+    local_decision(m, ah, dref);
+    HIP_CHECK(hipMemcpy(fr.data(), dref, m.nl * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(dref);
+    double err = 0.0;
+    for (int64_t j = 0; j < m.nl; ++j) {
+      const double ref = (double)fr[j] - m.h_y[m.off + j];
+      const double e = std::fabs((double)fd[j] - ref) / (1.0 + std::fabs(ref));
+      err = std::isfinite(e) ? std::max(err, e) : INFINITY;
+    }
+    res.verify_f_err = err;
+    const char* te = std::getenv("DPSVM_VERIFY_FTOL");
+    const double tol = te ? atof(te) : 1e-3;
+    if (!(err <= tol))
+      fail("DPSVM_VERIFY: f inconsistent with alpha (max relative error " + std::to_string(err) + ")");
+  }
   if (m.collectives() && trace::verify_enabled()) {
     // cross-rank consistency: every rank must hold bit-identical alphas
     std::vector<float> ah((size_t)m.n);
@@ -929,102 +1050,6 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
 // replicated alpha, predicts its own shard rows on MFMA, one sum all-reduce.
 // Reference: rank 0 alone, n x (Sgemv + transform_reduce) (svmTrain.cu:633-665).
 // ---------------------------------------------------------------------------
-namespace {
-struct SvSet {
-  int64_t nsv = 0;
-  float *sv = nullptr, *svsq = nullptr, *coef = nullptr;
-  size_t bytes = 0;
-  ~SvSet() {
-    for (void* p : {(void*)sv, (void*)svsq, (void*)coef}) if (p) (void)hipFree(p);
-  }
-};
-}  // namespace
-
-static void build_svs(GpuSolver::Impl& m, const SolveResult& r, SvSet& s) {
-  HIP_CHECK(hipMemcpyAsync(m.alpha, r.alpha.data(), m.n * 4, hipMemcpyHostToDevice, m.stream));
-  std::vector<int32_t> local_idx;
-  if (m.replicated) {
-    size_t tb = 0;
-    int32_t* idx = dmalloc<int32_t>((size_t)m.n, &tb);
-    int32_t* cnt = dmalloc<int32_t>(1, &tb);
-    int32_t* scratch = dmalloc<int32_t>((size_t)launch::compact_scratch_ints(m.n), &tb);
-    launch::compact_positive(m.alpha, m.n, idx, cnt, scratch, m.stream);
-    int32_t nsv = 0;
-    HIP_CHECK(hipMemcpyAsync(&nsv, cnt, 4, hipMemcpyDeviceToHost, m.stream));
-    HIP_CHECK(hipStreamSynchronize(m.stream));
-    s.nsv = nsv;
-    const int64_t pad = round_up(std::max<int64_t>(nsv, 1), 128) + 128;
-    s.sv = dmalloc<float>((size_t)pad * m.dp, &s.bytes);
-    s.svsq = dmalloc<float>((size_t)pad, &s.bytes);
-    s.coef = dmalloc<float>((size_t)pad, &s.bytes);
-    HIP_CHECK(hipMemsetAsync(s.sv, 0, (size_t)pad * m.dp * 4, m.stream));
-    HIP_CHECK(hipMemsetAsync(s.svsq, 0, pad * 4, m.stream));
-    HIP_CHECK(hipMemsetAsync(s.coef, 0, pad * 4, m.stream));
-    launch::gather_sv(m.x, 0, m.xsq, m.alpha, m.y, idx, nsv, m.dp, s.sv, s.svsq, s.coef, m.stream);
-    HIP_CHECK(hipStreamSynchronize(m.stream));
-    for (void* p : {(void*)idx, (void*)cnt, (void*)scratch}) (void)hipFree(p);
-  } else {
-    // partitioned: each rank gathers its local SVs; all-gather padded blocks
-    for (int64_t j = 0; j < m.nl; ++j)
-      if (r.alpha[m.off + j] > 0.f) local_idx.push_back((int32_t)(m.off + j));
-    std::vector<double> cnts((size_t)m.world, 0.0);
-    cnts[m.rank] = (double)local_idx.size();
-    if (m.world > 1) {
-      if (m.comm->device_memory()) {
-        size_t tb = 0;
-        double* dc = dmalloc<double>((size_t)m.world, &tb);
-        HIP_CHECK(hipMemcpy(dc, cnts.data(), m.world * 8, hipMemcpyHostToDevice));
-        m.comm->allreduce_sum_f64(dc, m.world, m.stream);
-        HIP_CHECK(hipMemcpyAsync(cnts.data(), dc, m.world * 8, hipMemcpyDeviceToHost, m.stream));
-        HIP_CHECK(hipStreamSynchronize(m.stream));
-        (void)hipFree(dc);
-      } else {
-        m.comm->allreduce_sum_f64(cnts.data(), m.world, nullptr);
-      }
-    }
-    int64_t maxc = 0, total = 0;
-    for (double c : cnts) { maxc = std::max<int64_t>(maxc, (int64_t)c); total += (int64_t)c; }
-    const int64_t per = std::max<int64_t>(1, maxc);
-    const int64_t pad = round_up(per * m.world, 128) + 128;
-    s.sv = dmalloc<float>((size_t)pad * m.dp, &s.bytes);
-    s.svsq = dmalloc<float>((size_t)pad, &s.bytes);
-    s.coef = dmalloc<float>((size_t)pad, &s.bytes);
-    HIP_CHECK(hipMemsetAsync(s.sv, 0, (size_t)pad * m.dp * 4, m.stream));
-    HIP_CHECK(hipMemsetAsync(s.svsq, 0, pad * 4, m.stream));
-    HIP_CHECK(hipMemsetAsync(s.coef, 0, pad * 4, m.stream));
-    size_t tb = 0;
-    int32_t* didx = dmalloc<int32_t>(std::max<size_t>(1, local_idx.size()), &tb);
-    if (!local_idx.empty()) {
-      HIP_CHECK(hipMemcpyAsync(didx, local_idx.data(), local_idx.size() * 4, hipMemcpyHostToDevice, m.stream));
-      launch::gather_sv(m.x, m.args.x_row0, m.xsq, m.alpha, m.y, didx, (int64_t)local_idx.size(), m.dp,
-                        s.sv + (size_t)m.rank * per * m.dp, s.svsq + m.rank * per, s.coef + m.rank * per,
-                        m.stream);
-    }
-    HIP_CHECK(hipStreamSynchronize(m.stream));
-    (void)hipFree(didx);
-    if (m.world > 1) {
-      // zero-padded blocks; coef = 0 on padding rows makes them inert
-      auto gather = [&](float* buf, int64_t elems) {
-        if (m.comm->device_memory()) {
-          m.comm->allgather(buf + (size_t)m.rank * elems, buf, elems * 4, m.stream);
-          HIP_CHECK(hipStreamSynchronize(m.stream));
-        } else {
-          std::vector<float> h((size_t)elems * m.world);
-          HIP_CHECK(hipMemcpy(h.data() + (size_t)m.rank * elems, buf + (size_t)m.rank * elems, elems * 4,
-                              hipMemcpyDeviceToHost));
-          m.comm->allgather(h.data() + (size_t)m.rank * elems, h.data(), elems * 4, nullptr);
-          HIP_CHECK(hipMemcpy(buf, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-        }
-      };
-      gather(s.sv, per * m.dp);
-      gather(s.svsq, per);
-      gather(s.coef, per);
-    }
-    s.nsv = per * m.world;
-    (void)total;
-  }
-}
-
 double GpuSolver::train_accuracy(const SolveResult& r) {
   auto& m = *impl_;
   HIP_CHECK(hipSetDevice(m.device));

@@ -120,3 +120,5 @@ def test_verify_ranks_consistent(monkeypatch, C):
     [t.start() for t in ts]
     [t.join() for t in ts]
     assert not errs and out[0].converged_
+    # invariant check ran on both ranks: f consistent with alpha
+    assert all(0.0 <= o.stats_["verify_f_err"] < 1e-4 for o in out)

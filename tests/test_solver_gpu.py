@@ -171,6 +171,29 @@ def test_gpu_fault_injection_and_verify(monkeypatch, C):
     assert ok.converged_
 
 
+@pytest.mark.parametrize("engine", ["persistent", "fused", "cache", "chain", "partitioned"])
+def test_verify_invariants_every_engine(monkeypatch, engine):
+    """DPSVM_VERIFY=1: alpha in [0, C] and the incrementally updated f equals f
+    recomputed from alpha (predict GEMM) at the end of the run, for every engine."""
+    monkeypatch.setenv("DPSVM_VERIFY", "1")
+    X, y = synthetic("mnist-parity", n=3000, seed=2)
+    kw = dict(C=10.0, gamma=0.25, device="cuda")
+    if engine == "fused":
+        kw["persist"] = "off"
+    elif engine in ("cache", "chain"):
+        kw["cache_lines"] = 64
+        if engine == "chain":
+            monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
+    elif engine == "partitioned":
+        kw["x_mode"] = "partitioned"
+    clf = SVC(**kw).fit(X, y)
+    assert clf.converged_
+    assert 0.0 <= clf.stats_["verify_f_err"] < 1e-4
+    # also mid-run (max_iter stop): f and alpha must agree after any iteration
+    part = SVC(max_iter=777, **kw).fit(X, y)
+    assert part.n_iter_ == 777 and 0.0 <= part.stats_["verify_f_err"] < 1e-4
+
+
 @pytest.mark.parametrize("extra", [{"cache_lines": 64}, {"cache_lines": 2, "spec_rows": 0},
                                    {"cache_lines": 24, "host_cache_lines": 8}])
 def test_fused_cache_iteration_matches_kernel_chain(monkeypatch, extra):
