@@ -164,6 +164,9 @@ struct PairUpdate {
 DPSVM_HD PairUpdate pair_update(float a_hi_old, float a_lo_old, float y_hi, float y_lo, float b_hi,
                                 float b_lo, float k_hl, float C, float tau, int clip_mode,
                                 bool same) {
+#if defined(__clang__)
+#pragma clang fp contract(off)  // identical rounding wherever it is inlined
+#endif
   float eta = (1.0f + 1.0f) - 2.0f * k_hl;  // K(hi,hi) + K(lo,lo) - 2 K(hi,lo); K(i,i) = 1
   if (!(eta >= tau)) eta = tau;
   float s = y_lo * y_hi;

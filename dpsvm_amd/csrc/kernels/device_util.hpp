@@ -39,6 +39,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 // one wave.  Every kernel that derives eta uses this exact lane mapping and
 // summation tree, so all iteration variants agree bit for bit.
 __device__ __forceinline__ float wave_dist2(const float* xh, const float* xl, int dp, int lane) {
+#pragma clang fp contract(off)
   float part = 0.f;
   for (int k = 4 * lane; k < dp; k += 256) {
     const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
@@ -94,7 +95,21 @@ __device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// f_j + c_hi K_hi,j + c_lo K_lo,j (svmTrain.cu:133-135) with every rounding
+// explicit: no FMA contraction, so the result does not depend on how the
+// surrounding code is if-converted or scheduled.  All engines (chain, fused,
+// fused cache, persistent) update f through this one function and therefore
+// follow bit-identical SMO trajectories.  A zero coefficient (with a finite K,
+// pass 0 for an absent row) contributes an exact zero: no branch on which
+// rows are live.
+__device__ __forceinline__ float f_apply(float fj, float c_hi, float k_hi, float c_lo, float k_lo) {
+#pragma clang fp contract(off)
+  const float delta = c_hi * k_hi + c_lo * k_lo;
+  return fj + delta;
+}
+
 __device__ __forceinline__ float rbf_from_dot(float sq_a, float sq_b, float dot, float gamma) {
+#pragma clang fp contract(off)  // same rounding in every row kernel (GEMM, rows, fused X pass)
   float d2 = sq_a + sq_b - 2.0f * dot;  // expansion as svmTrain.cu:128-130
   d2 = d2 > 0.f ? d2 : 0.f;             // clamp
   return expf(-gamma * d2);

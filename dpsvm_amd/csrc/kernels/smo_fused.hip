@@ -272,11 +272,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_kernel(SmoArgs a, int
     if (upd_f) {
       const float khv = first ? kh0 : line_hi[j];
       const float klv = first ? kl0 : line_lo[j];
-      float delta;
-      if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * khv) + (c_lo * klv);
-      else if (c_hi != 0.f) delta = c_hi * khv;
-      else delta = c_lo * klv;
-      fj += delta;
+      fj = f_apply(fj, c_hi, khv, c_lo, klv);
       a.f[j] = fj;
     }
     if (done == kRunning) {

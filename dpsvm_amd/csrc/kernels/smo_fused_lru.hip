@@ -777,11 +777,8 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
         const int64_t g = a.off + j;
         float fj = fv[c];
         if (upd_f) {
-          float delta;
-          if (chv != 0.f && clv != 0.f) delta = (chv * hv[c]) + (clv * lv[c]);
-          else if (chv != 0.f) delta = chv * hv[c];
-          else delta = clv * lv[c];
-          fj += delta;
+          // absent lines read f (finite) through the dummy pointer: zero it
+          fj = f_apply(fj, chv, chv != 0.f ? hv[c] : 0.f, clv, clv != 0.f ? lv[c] : 0.f);
           a.f[j] = fj;
         }
         if (done == kRunning) {

@@ -169,15 +169,9 @@ __global__ __launch_bounds__(kStepThreads) void smo_step_kernel(SmoArgs a) {
     if (j < a.nl) {
       float fj = a.f[j];
       if (ch != 0.f || cl != 0.f) {
-        float delta;
-        if (ch != 0.f && cl != 0.f)
-          delta = (ch * a.lines[(int64_t)c->line_hi * a.ldl + j]) +
-                  (cl * a.lines[(int64_t)c->line_lo * a.ldl + j]);
-        else if (ch != 0.f)
-          delta = ch * a.lines[(int64_t)c->line_hi * a.ldl + j];
-        else
-          delta = cl * a.lines[(int64_t)c->line_lo * a.ldl + j];
-        fj += delta;
+        const float khv = ch != 0.f ? a.lines[(int64_t)c->line_hi * a.ldl + j] : 0.f;
+        const float klv = cl != 0.f ? a.lines[(int64_t)c->line_lo * a.ldl + j] : 0.f;
+        fj = f_apply(fj, ch, khv, cl, klv);
         a.f[j] = fj;
       }
       if (done == kRunning) {

@@ -149,13 +149,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     for (int k = 0; k < kPersistMaxRows; ++k) {
       if (!has[k]) continue;
       const int64_t g = a.off + row0 + tid + (int64_t)k * kFusedThreads;
-      if (upd_f) {
-        float delta;
-        if (c_hi != 0.f && c_lo != 0.f) delta = (c_hi * khv[k]) + (c_lo * klv[k]);
-        else if (c_hi != 0.f) delta = c_hi * khv[k];
-        else delta = c_lo * klv[k];
-        f[k] += delta;
-      }
+      if (upd_f) f[k] = f_apply(f[k], c_hi, khv[k], c_lo, klv[k]);
       if (g == i_lo) al[k] = a_lo_new;
       if (g == i_hi) al[k] = a_hi_new;  // hi wins when i_hi == i_lo
       if (in_up(al[k], yv[k], a.C)) xk_min(nk, XKeys{make_key(f[k], (uint32_t)g), kKeyNone, al[k], 0.f});
