@@ -45,7 +45,7 @@ def main():
                        "t_solve_s": round(info["t_solve"], 4), "wall_s": round(wall, 4),
                        "us_per_iter": round(1e6 * info["t_solve"] / max(1, info["iters"]), 3),
                        "x_passes": info["x_passes"], "rows_computed": info["rows_computed"],
-                       "misses": info["cache_misses"], "spec_rows": info["spec_rows"]}
+                       "misses": info["cache_misses"], "hits": info.get("cache_hits"), "spec_rows": info["spec_rows"]}
                 print(json.dumps(rec), flush=True)
                 out.append(rec)
                 del s

@@ -20,31 +20,103 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    uint64_t o = shfl_xor_u64(v, m);
-    v = o < v ? o : v;
-  }
-  return v;
+// ---- full-wave reductions on DPP (no LDS round trips) ----
+// Within each 16-lane row: quad_perm xor 1, quad_perm xor 2, row_half_mirror
+// (i <-> 7-i) and row_mirror (i <-> 15-i) leave every lane of the row holding
+// the row's reduction (each step pairs lanes that already agree, so the
+// operands are identical on both sides); the four rows are then combined from
+// lanes 0/16/32/48 through v_readlane (uniform operands).  A ds_bpermute
+// butterfly costs an LDS round trip per step; these steps are plain VALU ops.
+// All 64 lanes must be active (every call site reduces full waves).
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;
+constexpr int kDppMirror = 0x140;
+
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, false));
+}
+template <int kCtrl>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint64_t lo = dpp_u32<kCtrl>((uint32_t)v), hi = dpp_u32<kCtrl>((uint32_t)(v >> 32));
+  return (hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (hi << 32) | lo;
+}
+__device__ __forceinline__ float readlane_f32(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
+template <int kCtrl>
+__device__ __forceinline__ uint64_t min_step_u64(uint64_t v) {
+  const uint64_t o = dpp_u64<kCtrl>(v);
+  return o < v ? o : v;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  v = min_step_u64<kDppXor1>(v);
+  v = min_step_u64<kDppXor2>(v);
+  v = min_step_u64<kDppHalfMirror>(v);
+  v = min_step_u64<kDppMirror>(v);
+  uint64_t r = readlane_u64(v, 0);
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+  for (int row = 1; row < 4; ++row) {
+    const uint64_t o = readlane_u64(v, 16 * row);
+    r = o < r ? o : r;
+  }
+  return r;
+}
+
+// Deterministic wave sum: the same tree (and the same bits) in every lane.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma clang fp contract(off)
+  v = v + dpp_f32<kDppXor1>(v);
+  v = v + dpp_f32<kDppXor2>(v);
+  v = v + dpp_f32<kDppHalfMirror>(v);
+  v = v + dpp_f32<kDppMirror>(v);
+  return (readlane_f32(v, 0) + readlane_f32(v, 16)) + (readlane_f32(v, 32) + readlane_f32(v, 48));
 }
 
 // |x_h - x_l|^2 over dp floats (multiple of 4, zero padded, 16-B aligned) by
 // one wave.  Every kernel that derives eta uses this exact lane mapping and
 // summation tree, so all iteration variants agree bit for bit.
+__device__ __forceinline__ float dist2_term(f4 h, f4 l) {
+#pragma clang fp contract(off)
+  const f4 t = h - l;
+  return (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
+}
+
 __device__ __forceinline__ float wave_dist2(const float* xh, const float* xl, int dp, int lane) {
 #pragma clang fp contract(off)
   float part = 0.f;
-  for (int k = 4 * lane; k < dp; k += 256) {
-    const f4 h = *(const f4*)(xh + k), l = *(const f4*)(xl + k);
-    const f4 t = h - l;
-    part += (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
+  if (dp <= 1024) {
+    // d <= 1024 (every BASELINE config): all eight 16-B loads of the lane are
+    // issued before the first use — one memory round trip instead of one per
+    // 256-column step (the loop below waits for each step's loads).  Same
+    // per-lane summation order as the loop, so both forms agree bit for bit.
+    f4 h[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 4 * lane + 256 * i;
+      const int kk = k < dp ? k : 0;  // in-bounds address for idle slots
+      h[i] = *(const f4*)(xh + kk);
+      l[i] = *(const f4*)(xl + kk);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float s = dist2_term(h[i], l[i]);
+      part = 4 * lane + 256 * i < dp ? part + s : part;
+    }
+  } else {
+    for (int k = 4 * lane; k < dp; k += 256) part += dist2_term(*(const f4*)(xh + k), *(const f4*)(xl + k));
   }
   return wave_sum(part);
 }

@@ -43,6 +43,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   __shared__ float kfs[8];
   __shared__ XKeys pair_s;
   __shared__ int fail_s;
+  __shared__ float d2_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int rpt = a.fused_rows / kFusedThreads;  // rows per thread
@@ -105,17 +106,28 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     // ---- 2. one round trip: Gram rows of the own rows, sample rows ----
     const float* line_hi = a.lines + (int64_t)i_hi * a.ldl;
     const float* line_lo = a.lines + (int64_t)i_lo * a.ldl;
+    // unconditional loads (absent rows read the first own row): no exec-mask
+    // branches between them, so every load of the round trip is in flight together
     float khv[kPersistMaxRows], klv[kPersistMaxRows];
 #pragma unroll
     for (int k = 0; k < kPersistMaxRows; ++k) {
-      const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
-      khv[k] = has[k] ? line_hi[j] : 0.f;
-      klv[k] = has[k] ? line_lo[j] : 0.f;
+      const int64_t j = has[k] ? row0 + tid + (int64_t)k * kFusedThreads : row0;
+      khv[k] = line_hi[j];
+      klv[k] = line_lo[j];
     }
     const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];  // read-only during the run
     const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
     const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
-    const float dist2 = wave_dist2(xh, xl, a.dp, lane);  // identical tree in every wave
+    // wave 0 alone reads the two sample rows (one copy of their traffic per
+    // workgroup instead of four: with every workgroup on the same two rows the
+    // replicated loads delayed the slowest publisher) and shares |x_hi - x_lo|^2
+    // through LDS; the other waves' Gram-row loads are in flight meanwhile
+    if (wave == 0) {
+      const float d2 = wave_dist2(xh, xl, a.dp, lane);  // same tree as every other engine
+      if (lane == 0) d2_s = d2;
+    }
+    __syncthreads();
+    const float dist2 = d2_s;
     const float a_hi_old = pk.ah, a_lo_old = pk.al;     // the owners' current values
     float c_hi = 0.f, c_lo = 0.f, a_hi_new = a_hi_old, a_lo_new = a_lo_old;
     const int iter = t + 1;

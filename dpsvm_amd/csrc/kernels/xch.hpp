@@ -73,19 +73,24 @@ __device__ __forceinline__ void xk_min(XKeys& m, const XKeys& o) {
 
 __device__ __forceinline__ XKeys xk_none() { return XKeys{kKeyNone, kKeyNone, 0.f, 0.f}; }
 
-__device__ __forceinline__ XKeys xk_shfl_xor(const XKeys& v, int m) {
-  XKeys o;
-  o.kh = shfl_xor_u64(v.kh, m);
-  o.kl = shfl_xor_u64(v.kl, m);
-  o.ah = __shfl_xor(v.ah, m, 64);
-  o.al = __shfl_xor(v.al, m, 64);
-  return o;
+template <int kCtrl>
+__device__ __forceinline__ void xk_min_step(XKeys& v) {
+  xk_min(v, XKeys{dpp_u64<kCtrl>(v.kh), dpp_u64<kCtrl>(v.kl), dpp_f32<kCtrl>(v.ah), dpp_f32<kCtrl>(v.al)});
 }
 
+// full-wave minimum with payloads (DPP row steps + readlane across rows, see
+// wave_min_u64); the result is uniform
 __device__ __forceinline__ XKeys wave_min_xk(XKeys v) {
+  xk_min_step<kDppXor1>(v);
+  xk_min_step<kDppXor2>(v);
+  xk_min_step<kDppHalfMirror>(v);
+  xk_min_step<kDppMirror>(v);
+  XKeys r{readlane_u64(v.kh, 0), readlane_u64(v.kl, 0), readlane_f32(v.ah, 0), readlane_f32(v.al, 0)};
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) xk_min(v, xk_shfl_xor(v, m));
-  return v;
+  for (int row = 1; row < 4; ++row)
+    xk_min(r, XKeys{readlane_u64(v.kh, 16 * row), readlane_u64(v.kl, 16 * row), readlane_f32(v.ah, 16 * row),
+                    readlane_f32(v.al, 16 * row)});
+  return r;
 }
 
 // lane p < xworld pushes to rank p; peer = that rank's receive buffer

@@ -464,14 +464,32 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.off = sh.offset;
   const int64_t nl_max = (n + m.world - 1) / m.world;
   m.G = std::max<int64_t>(1, (nl_max + kStepRows - 1) / kStepRows);
-  // fused-iteration geometry: <= ~256 workgroups, rows per workgroup a multiple of 256
-  {
+  // fused-iteration geometry, rows per workgroup a multiple of 256.  Cache mode:
+  // <= ~256 workgroups (the X pass wants every CU).  Dense mode: the period is
+  // set by the all-to-all key exchange, whose cost grows with the number of
+  // publishers (world x G): ~128 publishers in all, <= 1024 rows per workgroup
+  // (the persistent kernel's register budget).  Measured on 60k x 784, 1 GPU:
+  // 235 workgroups 5.8-6.2 us per iteration, 118 -> 5.2 us (profiles/README.md).
+  auto geometry = [&](int64_t rows_min) {
     const int64_t per = (nl_max + 255) / 256;
-    m.RBf = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
-    m.Gf = std::max<int64_t>(1, (nl_max + m.RBf - 1) / m.RBf);
-  }
-  // lines cover every row a kernel may write (the fused X pass writes whole 256-row tiles)
-  m.ldl = std::max<int64_t>(m.G * kStepRows, m.Gf * m.RBf);
+    int64_t rb = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
+    rb = std::max(rb, rows_min);
+    if (const char* e = std::getenv("DPSVM_FUSED_ROWS")) {  // override: rows per workgroup
+      const int64_t r = atoll(e) / kFusedThreads * kFusedThreads;
+      if (r > rb) rb = r;
+    }
+    return std::pair<int64_t, int64_t>(rb, std::max<int64_t>(1, (nl_max + rb - 1) / rb));
+  };
+  const auto geo_cache = geometry(0);
+  const int64_t dense_rows =
+      std::min<int64_t>(1024, round_up(std::max<int64_t>(1, nl_max * m.world / 128), kFusedThreads));
+  const auto geo_dense = geometry(dense_rows);
+  m.RBf = geo_cache.first;
+  m.Gf = geo_cache.second;
+  // lines cover every row a kernel may write (the fused X pass writes whole
+  // 256-row tiles) under either geometry
+  m.ldl = std::max<int64_t>({m.G * kStepRows, geo_cache.first * geo_cache.second,
+                             geo_dense.first * geo_dense.second});
 
   // ---- X placement ----
   if (n_x_rows == n) {
@@ -569,6 +587,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   if (m.p.cache_lines > 0) want_lines = std::min<int64_t>(want_lines, m.p.cache_lines);
   m.dense = m.replicated && want_lines >= n;
   if (const char* e = std::getenv("DPSVM_FORCE_LRU")) if (e[0] == '1') m.dense = false;
+  if (m.dense) {
+    m.RBf = geo_dense.first;
+    m.Gf = geo_dense.second;
+  }
   m.L = m.dense ? n : std::max<int64_t>(2, std::min<int64_t>(want_lines, n));
   DPSVM_CHECK(m.L * line_bytes <= (double)freeb, "not enough device memory for 2 kernel-row lines");
   m.lines = dmalloc<float>((size_t)m.L * m.ldl, &m.bytes);
@@ -675,6 +697,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // auto: persistent unless the exchange is pinned to the communicator all-reduce
     // (and unless a test forces the per-iteration collective path or eager launches)
     want_persist = mode == 2 || (mode == 0 && m.p.exchange != 1 && m.p.use_graph && !m.p.force_collectives);
+    // register-resident rows and one resident workgroup per CU (launch::smo_persist)
+    want_persist = want_persist && m.RBf <= 4 * kFusedThreads && m.Gf <= 256;
   }
   if (m.dense && ((m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || want_persist)) {
     const bool ok = m.setup_exchange();
