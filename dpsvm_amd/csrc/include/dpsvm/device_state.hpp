@@ -157,9 +157,12 @@ struct SmoArgs {
   // all-reduce (no collective launch, no host involvement).
   uint64_t* const* xpeer;  // [xworld] receive buffers (device-accessible)
   int32_t xrank, xworld;
+  int32_t xstride;  // u64 slots per entry (>= kXchGranules; a multiple pads entries apart)
+  int32_t xpoll_kb;  // 0: poll batch from the entry count; else fixed (2, 4, 8)
+  int32_t xpoll_sleep;  // s_sleep(1) count between poll rounds
   int64_t xtimeout_ticks;  // give-up bound of one poll loop (s_memrealtime, 100 MHz)
 };
-constexpr int kXchGranules = 6;  // per workgroup entry: hi key (2 halves), lo key (2 halves), their alphas
+constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..16}, {key bits 15..0, alpha}
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;
 

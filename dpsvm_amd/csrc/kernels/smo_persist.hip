@@ -37,6 +37,10 @@ namespace dev {
 
 constexpr int kPersistMaxRows = 4;  // rows per thread (fused_rows <= 1024)
 
+// kSys: system-scope exchange (ranks on other devices / processes); kB: poll
+// batch, publications watched per lane per round (xch.hpp).  One poll loop per
+// instantiation: no dispatch inside the iteration.
+template <bool kSys, int kB>
 __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     const uint32_t tag = (uint32_t)t + 1u;
     if (wave == 0) {
       XKeys m = xk_none();
-      const bool ok = xch_poll_wave(a, my_buf, (int)(tag & 1u), tag, m, lane);
+      const bool ok = xch_poll_wave_t<kSys, kB>(a, my_buf, (int)(tag & 1u), tag, m, lane);
       m = wave_min_xk(m);
       if (lane == 0) {
         pair_s = m;
@@ -234,7 +238,12 @@ void preload_persist_kernel(hipStream_t s) {
   SmoArgs z{};
   z.fused_G = 1;
   z.fused_rows = kFusedThreads;
-  dev::smo_persist_kernel<<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 1><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 2><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 1><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 2><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
   HIP_CHECK(hipStreamSynchronize(s));
   HIP_CHECK(hipGetLastError());
   (void)hipFree(st);
@@ -243,7 +252,18 @@ void preload_persist_kernel(hipStream_t s) {
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {
   DPSVM_CHECK(a.xworld >= 1 && a.fused_G <= 256 && a.fused_rows <= dev::kPersistMaxRows * kFusedThreads,
               "persistent SMO needs the key exchange and <= 256 resident workgroups");
-  dev::smo_persist_kernel<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, st, steps);
+  const int E = a.xworld * a.fused_G;
+  const int kb = a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
+  const dim3 g(a.fused_G);
+  if (a.xworld > 1) {
+    if (kb == 1) dev::smo_persist_kernel<true, 1><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else if (kb == 2) dev::smo_persist_kernel<true, 2><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else dev::smo_persist_kernel<true, 4><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+  } else {
+    if (kb == 1) dev::smo_persist_kernel<false, 1><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else if (kb == 2) dev::smo_persist_kernel<false, 2><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else dev::smo_persist_kernel<false, 4><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+  }
   post_launch("smo_persist", s);
 }
 

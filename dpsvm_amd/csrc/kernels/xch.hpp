@@ -2,17 +2,20 @@
 // in-kernel replacement of the per-iteration all-reduce when world > 1).
 //
 // Each workgroup pushes its (up, low) keys — and the current alphas of the
-// two rows behind them — to every rank as six 8-byte granules {tag, 32-bit
-// value} with relaxed atomic stores (one aligned store per granule: never
-// torn; the data IS the flag, no fence).  Consumers poll their own receive
-// buffer until every granule of the parity carries the expected tag, then
-// reduce exactly as from an all-reduced buffer — every rank derives the same
-// pair, and the pair's alphas come from their owners' registers, so no
-// consumer ever reads a cross-workgroup-written alpha through a possibly
-// stale cache line (L2s are per XCD).  Tags are the iteration count + 1
-// (never 0; buffers are zeroed before each solve); keys tagged T live in
-// parity T & 1, and no workgroup can lap another: its publication T+2 needs
-// every T+1 publication, each made after its author had read parity T.
+// two rows behind them — to every rank as four 8-byte granules {16-bit tag,
+// 48-bit payload} with relaxed atomic stores (one aligned store per granule:
+// never torn; the data IS the flag, no fence): per side, the key's upper 48
+// bits, then its lower 16 bits with the 32-bit alpha.  Consumers poll their
+// own receive buffer until every granule of the parity carries the expected
+// tag, then reduce exactly as from an all-reduced buffer — every rank derives
+// the same pair, and the pair's alphas come from their owners' registers, so
+// no consumer ever reads a cross-workgroup-written alpha through a possibly
+// stale cache line (L2s are per XCD).  Iteration tags T = iteration + 1 are
+// sent as (T mod 65535) + 1: never 0 (buffers are zeroed before each solve)
+// and never equal for T and T - 2, the only older publication a slot can
+// still hold; keys tagged T live in parity T & 1, and no workgroup can lap
+// another: its publication T+2 needs every T+1 publication, each made after
+// its author had read parity T.
 // Scope: system across GPUs (xGMI peer memory), agent within one GPU.
 // Reference: one 16-byte MPI Allgather per iteration (svmTrainMain.cpp:244).
 #pragma once
@@ -40,7 +43,7 @@ struct XKeys {
 };
 
 __device__ __forceinline__ uint64_t* xch_entry(uint64_t* base, int par, const SmoArgs& a, int rank, int b) {
-  return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * kXchGranules;
+  return base + (((int64_t)par * a.xworld + rank) * a.fused_G + b) * a.xstride;
 }
 
 template <bool kSys>
@@ -58,6 +61,9 @@ __device__ __forceinline__ uint64_t xch_load(const uint64_t* g) {
 }
 
 __device__ __forceinline__ uint32_t fbits(float v) { return __float_as_uint(v); }
+
+// granule tag of iteration tag T (>= 1): 16 bits, never 0, T and T - 2 differ
+__device__ __forceinline__ uint64_t xtag(uint32_t T) { return (uint64_t)(T % 65535u + 1u) << 48; }
 
 // keep the smaller key (keys are unique; kKeyNone never wins) with its alpha
 __device__ __forceinline__ void xk_min(XKeys& m, const XKeys& o) {
@@ -101,13 +107,11 @@ __device__ __forceinline__ void xch_push_t(const SmoArgs& a, uint64_t* peer, int
                                            uint32_t tag, int lane) {
   if (lane < a.xworld) {
     uint64_t* g = xch_entry(peer, par, a, a.xrank, b);
-    const uint64_t t = (uint64_t)tag << 32;
-    xch_store<kSys>(g + 0, t | (k.kh >> 32));
-    xch_store<kSys>(g + 1, t | (k.kh & 0xffffffffull));
-    xch_store<kSys>(g + 2, t | (k.kl >> 32));
-    xch_store<kSys>(g + 3, t | (k.kl & 0xffffffffull));
-    xch_store<kSys>(g + 4, t | fbits(k.ah));
-    xch_store<kSys>(g + 5, t | fbits(k.al));
+    const uint64_t t = xtag(tag);
+    xch_store<kSys>(g + 0, t | (k.kh >> 16));
+    xch_store<kSys>(g + 1, t | ((k.kh & 0xffffull) << 32) | fbits(k.ah));
+    xch_store<kSys>(g + 2, t | (k.kl >> 16));
+    xch_store<kSys>(g + 3, t | ((k.kl & 0xffffull) << 32) | fbits(k.al));
   }
 }
 
@@ -122,19 +126,20 @@ __device__ __forceinline__ uint64_t* xch_peer(const SmoArgs& a, int lane) {
   return lane < a.xworld ? a.xpeer[lane] : nullptr;
 }
 
-__device__ __forceinline__ bool xg_ready(const uint64_t (&x)[kXchGranules], uint32_t tag) {
+__device__ __forceinline__ bool xg_ready(const uint64_t (&x)[kXchGranules], uint64_t t) {
   bool ok = true;
 #pragma unroll
-  for (int i = 0; i < kXchGranules; ++i) ok &= (uint32_t)(x[i] >> 32) == tag;
+  for (int i = 0; i < kXchGranules; ++i) ok &= (x[i] >> 48) == (t >> 48);
   return ok;
 }
 
 __device__ __forceinline__ XKeys xg_decode(const uint64_t (&x)[kXchGranules]) {
+  constexpr uint64_t m48 = (1ull << 48) - 1;
   XKeys k;
-  k.kh = (x[0] << 32) | (x[1] & 0xffffffffull);
-  k.kl = (x[2] << 32) | (x[3] & 0xffffffffull);
-  k.ah = __uint_as_float((uint32_t)x[4]);
-  k.al = __uint_as_float((uint32_t)x[5]);
+  k.kh = ((x[0] & m48) << 16) | ((x[1] >> 32) & 0xffffull);
+  k.ah = __uint_as_float((uint32_t)x[1]);
+  k.kl = ((x[2] & m48) << 16) | ((x[3] >> 32) & 0xffffull);
+  k.al = __uint_as_float((uint32_t)x[3]);
   return k;
 }
 
@@ -148,13 +153,14 @@ template <bool kSys, bool kPipe>
 __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
                                            XKeys& out, int tid, int nthreads) {
   const int E = a.xworld * a.fused_G;
-  const uint64_t* base = mine_buf + (int64_t)par * E * kXchGranules;
+  const uint64_t* base = mine_buf + (int64_t)par * E * a.xstride;
+  const uint64_t xt = xtag(tag);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   XKeys m = xk_none();
   for (int c = 0; c < E; c += nthreads) {
     const int e = c + tid;
     const bool mine = e < E;
-    const uint64_t* g = base + (int64_t)(mine ? e : 0) * kXchGranules;
+    const uint64_t* g = base + (int64_t)(mine ? e : 0) * a.xstride;
     uint64_t ra[kXchGranules], rb[kXchGranules];
 #pragma unroll
     for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
@@ -163,18 +169,18 @@ __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* min
       while (true) {
 #pragma unroll
         for (int i = 0; i < kXchGranules; ++i) rb[i] = xch_load<kSys>(g + i);
-        if (__all(!mine || xg_ready(ra, tag))) {
+        if (__all(!mine || xg_ready(ra, xt))) {
           got_a = true;
           break;
         }
 #pragma unroll
         for (int i = 0; i < kXchGranules; ++i) ra[i] = xch_load<kSys>(g + i);
-        if (__all(!mine || xg_ready(rb, tag))) break;
+        if (__all(!mine || xg_ready(rb, xt))) break;
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
       }
     } else {
       got_a = true;
-      while (!__all(!mine || xg_ready(ra, tag))) {
+      while (!__all(!mine || xg_ready(ra, xt))) {
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
@@ -187,16 +193,17 @@ __device__ __forceinline__ bool xch_poll_t(const SmoArgs& a, const uint64_t* min
   return true;
 }
 
-// One wave watches ALL entries (lane l: entries l + 64 i, up to 4 per lane
+// One wave watches ALL entries (lane l: entries l + 64 i, up to kB per lane
 // per batch, every load of a batch in flight together), sleeping between
 // rounds: the fewest poll requests on the hot buffer lines (every workgroup
 // polls the same few KB, so polling traffic itself delays the publications).
-template <bool kSys>
+// kB = ceil(E / 64) up to 4, so no load is issued for an absent entry.
+template <bool kSys, int kB>
 __device__ __forceinline__ bool xch_poll_wave_t(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
                                                 XKeys& out, int lane) {
-  constexpr int kB = 4;
   const int E = a.xworld * a.fused_G;
-  const uint64_t* base = mine_buf + (int64_t)par * E * kXchGranules;
+  const uint64_t* base = mine_buf + (int64_t)par * E * a.xstride;
+  const uint64_t xt = xtag(tag);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   XKeys m = xk_none();
   for (int c = 0; c < E; c += 64 * kB) {
@@ -207,16 +214,16 @@ __device__ __forceinline__ bool xch_poll_wave_t(const SmoArgs& a, const uint64_t
     while (true) {
 #pragma unroll
       for (int j = 0; j < kB; ++j) {
-        const uint64_t* g = base + (int64_t)(mine[j] ? c + lane + 64 * j : 0) * kXchGranules;
+        const uint64_t* g = base + (int64_t)(mine[j] ? c + lane + 64 * j : 0) * a.xstride;
 #pragma unroll
         for (int i = 0; i < kXchGranules; ++i) r[j][i] = xch_load<kSys>(g + i);
       }
       bool ok = true;
 #pragma unroll
-      for (int j = 0; j < kB; ++j) ok &= !mine[j] || xg_ready(r[j], tag);
+      for (int j = 0; j < kB; ++j) ok &= !mine[j] || xg_ready(r[j], xt);
       if (__all(ok)) break;
       if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
-      __builtin_amdgcn_s_sleep(1);
+      for (int z = 0; z < a.xpoll_sleep; ++z) __builtin_amdgcn_s_sleep(1);
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j)
@@ -226,10 +233,19 @@ __device__ __forceinline__ bool xch_poll_wave_t(const SmoArgs& a, const uint64_t
   return true;
 }
 
+template <bool kSys>
+__device__ __forceinline__ bool xch_poll_wave_s(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
+                                                XKeys& out, int lane) {
+  const int E = a.xworld * a.fused_G;  // uniform
+  if (E <= 64) return xch_poll_wave_t<kSys, 1>(a, mine_buf, par, tag, out, lane);
+  if (E <= 128) return xch_poll_wave_t<kSys, 2>(a, mine_buf, par, tag, out, lane);
+  return xch_poll_wave_t<kSys, 4>(a, mine_buf, par, tag, out, lane);
+}
+
 __device__ __forceinline__ bool xch_poll_wave(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
                                               XKeys& out, int lane) {
-  return a.xworld > 1 ? xch_poll_wave_t<true>(a, mine_buf, par, tag, out, lane)
-                      : xch_poll_wave_t<false>(a, mine_buf, par, tag, out, lane);
+  return a.xworld > 1 ? xch_poll_wave_s<true>(a, mine_buf, par, tag, out, lane)
+                      : xch_poll_wave_s<false>(a, mine_buf, par, tag, out, lane);
 }
 
 // mine_buf: this rank's receive buffer (a.xpeer[a.xrank], loaded once)

@@ -86,6 +86,7 @@ struct GpuSolver::Impl {
   uint64_t* xbuf = nullptr;
   uint64_t** xpeer_d = nullptr;
   int64_t xregion = 0;  // u64 words of the two key parities (zeroed per solve)
+  int64_t xstride = kXchGranules;  // u64 slots per exchange entry
   std::vector<void*> xopened;
   std::string xch_diag;
   int64_t Gf = 0, RBf = 0;
@@ -208,7 +209,9 @@ struct GpuSolver::Impl {
     me.device = device;
     me.ok = 1;
     const int64_t ping_words = 64;
-    xregion = (int64_t)2 * world * Gf * kXchGranules;
+    xstride = kXchGranules;
+    if (const char* e = std::getenv("DPSVM_XCH_STRIDE")) xstride = std::max(kXchGranules, atoi(e));
+    xregion = (int64_t)2 * world * Gf * xstride;
     try {
       DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
       launch::preload_fused_kernels(stream);
@@ -687,6 +690,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.xpeer = nullptr;
   a.xrank = 0;
   a.xworld = 0;
+  a.xstride = kXchGranules;
+  a.xpoll_kb = 0;
+  a.xpoll_sleep = 1;
   a.xtimeout_ticks = 0;
   m.xch = false;
   bool want_persist = false;
@@ -711,6 +717,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       a.xpeer = m.xpeer_d;
       a.xrank = m.rank;
       a.xworld = m.world;
+      a.xstride = (int32_t)m.xstride;
+      const char* kb = std::getenv("DPSVM_XCH_KB");
+      a.xpoll_kb = kb ? atoi(kb) : 0;
+      const char* ps = std::getenv("DPSVM_XCH_SLEEP");
+      a.xpoll_sleep = ps ? atoi(ps) : 1;
       a.xtimeout_ticks = (int64_t)(tmo * 1e8);
     }
   }
