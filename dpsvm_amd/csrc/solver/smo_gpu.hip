@@ -484,9 +484,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     return std::pair<int64_t, int64_t>(rb, std::max<int64_t>(1, (nl_max + rb - 1) / rb));
   };
   const auto geo_cache = geometry(0);
-  const int64_t dense_rows =
+  int64_t dense_rows =
       std::min<int64_t>(1024, round_up(std::max<int64_t>(1, nl_max * m.world / 128), kFusedThreads));
-  const auto geo_dense = geometry(dense_rows);
+  if (const char* e = std::getenv("DPSVM_DENSE_ROWS"))  // tests: more publishers (multi-batch polls)
+    dense_rows = std::max<int64_t>(kFusedThreads, std::min<int64_t>(1024, atoll(e) / kFusedThreads * kFusedThreads));
+  auto geo_dense = geometry(dense_rows);
+  if (std::getenv("DPSVM_DENSE_ROWS"))
+    geo_dense = {dense_rows, std::max<int64_t>(1, (nl_max + dense_rows - 1) / dense_rows)};
   m.RBf = geo_cache.first;
   m.Gf = geo_cache.second;
   // lines cover every row a kernel may write (the fused X pass writes whole

@@ -9,7 +9,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(out: str, engine: str) -> int:
+def main(out: str, engine: str, n: int) -> int:
     import torch  # noqa: F401
     from dpsvm_amd import SVC
     from dpsvm_amd.parallel import init_distributed, make_comm, shutdown
@@ -17,9 +17,9 @@ def main(out: str, engine: str) -> int:
 
     ctx = init_distributed(device="cuda")
     comm = make_comm(ctx, "gloo")
-    X, y = synthetic("covtype", n=6000, seed=2)
+    X, y = synthetic("covtype", n=n, seed=2)
     clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer",
-              persist="on" if engine == "persistent" else "off", persist_block=257).fit(X, y, comm=comm)
+              persist="off" if engine == "fused" else "on", persist_block=257).fit(X, y, comm=comm)
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
            "iters": int(clf.n_iter_), "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
     with open(f"{out}.rank{ctx.rank}.json", "w") as f:
@@ -30,4 +30,4 @@ def main(out: str, engine: str) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1], sys.argv[2]))
+    sys.exit(main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 6000))

@@ -115,6 +115,11 @@ def test_mnist_shape_headline_converges():
     assert clf.converged_
     assert clf.fit_time_ < 30.0
     assert clf.train_accuracy() > 0.99
+    # > 65535 iterations: the persistent engine's 16-bit exchange tags wrap;
+    # one launch per iteration (no exchange) must give the same iterates
+    assert clf.setup_info_["iteration"] == "persistent-dense" and clf.n_iter_ > 70000
+    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", persist="off").fit(X, y)
+    assert ref.n_iter_ == clf.n_iter_ and np.array_equal(ref.alpha_, clf.alpha_) and ref.b_ == clf.b_
 
 
 def test_bench_gpu_small():
@@ -286,25 +291,32 @@ def test_persistent_engine_matches_fused(monkeypatch, block):
     assert m.n_iter_ == 1000 and m.status_ == 2 and np.array_equal(m.alpha_, m_ref.alpha_)
 
 
-@pytest.mark.parametrize("engine", ["fused", "persistent"])
+@pytest.mark.parametrize("engine", ["fused", "persistent", "persistent-batches"])
 def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     """Two ranks as two processes sharing the GPU (gloo bootstrap, IPC-mapped
-    receive buffers): in-kernel exchange, bit-identical to one rank."""
+    receive buffers): in-kernel exchange, bit-identical to one rank.
+    persistent-batches: 256-row workgroups and one publication per lane per
+    poll round, so each poll sweeps its 2 x 40 publications in two batches."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     import subprocess
 
+    n = 20000 if engine == "persistent-batches" else 6000
     env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="30", DPSVM_VERIFY="1")
+    if engine == "persistent-batches":
+        env.update(DPSVM_DENSE_ROWS="256", DPSVM_XCH_KB="1")
     out = tmp_path / "mp"
+    port = 29600 + ["fused", "persistent", "persistent-batches"].index(engine)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + (engine == "persistent")),
-           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine]
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = [json.load(open(f"{out}.rank{k}.json")) for k in range(2)]
-    X, y = synthetic("covtype", n=6000, seed=2)
+    X, y = synthetic("covtype", n=n, seed=2)
     ref = SVC(C=4.0, gamma=0.5, eps=1e-3, device="cuda").fit(X, y)
     for k in range(2):
         assert res[k]["exchange"] == "peer"
+        assert res[k]["iteration"] == ("fused-dense" if engine == "fused" else "persistent-dense")
         assert res[k]["iters"] == ref.n_iter_
         assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
 
