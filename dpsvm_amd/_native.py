@@ -8,6 +8,7 @@ raises instead of silently falling back to Python code.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import sys
 
@@ -28,6 +29,13 @@ def load(build_if_missing: bool = True):
     if _C is not None:
         return _C
     _try_import_torch()
+    alt = os.environ.get("DPSVM_NATIVE_SO")  # A/B runs: another in-tree build of the same module
+    if alt:
+        spec = importlib.util.spec_from_file_location("dpsvm_amd._C", alt)
+        _C = importlib.util.module_from_spec(spec)
+        sys.modules["dpsvm_amd._C"] = _C
+        spec.loader.exec_module(_C)
+        return _C
     try:
         _C = importlib.import_module("dpsvm_amd._C")
         return _C
