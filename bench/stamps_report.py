@@ -91,7 +91,35 @@ def main(path):
     print(json.dumps(out, indent=1))
 
 
+PLRU_PHASES = ["poll", "pair_to_plan", "fill", "f_update", "keys_publish"]
+
+
+def main_plru(path):
+    """smo_persist_lru slots: 0 poll start, 1 pair known, 2 plan broadcast,
+    3 lines filled, 4 f update, 5 published, 6 rows filled; split by fills."""
+    a = np.fromfile(path, dtype=np.uint64).reshape(RING, 2, SLOTS).astype(np.int64)
+    out = {}
+    for b, name in ((0, "wg0"), (1, "wglast")):
+        t = a[:, b, :6]
+        ok = (t > 0).all(1)
+        rows = a[:, b, 6]
+        d = np.diff(t, axis=1) * 10.0
+        per = np.diff(t[:, 0]) * 10.0
+        for tag, sel in (("fill", ok & (rows > 0)), ("hit", ok & (rows == 0))):
+            if sel.sum() == 0:
+                continue
+            out[f"{name}_{tag}"] = {"n": int(sel.sum()),
+                                    **{ph + "_ns": float(np.median(d[sel, i])) for i, ph in enumerate(PLRU_PHASES)}}
+            pp = per[sel[:-1] & ok[1:] & (per > 0)]
+            if len(pp):
+                out[f"{name}_{tag}"]["period_ns"] = float(np.median(pp))
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "--plru":
+        main_plru(sys.argv[1])
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[2] == "--lru":
         main_lru(sys.argv[1])
     elif len(sys.argv) > 2 and sys.argv[2] == "--persist":

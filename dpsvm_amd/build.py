@@ -47,6 +47,7 @@ LIB_SOURCES = [
     "kernels/compact.hip",
     "kernels/smo_fused_lru.hip",
     "kernels/smo_persist.hip",
+    "kernels/smo_persist_lru.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

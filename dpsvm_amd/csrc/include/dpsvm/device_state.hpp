@@ -149,12 +149,17 @@ struct SmoArgs {
   // diagnostics (DPSVM_STAMPS): s_memrealtime stamps of workgroups 0 and G-1,
   // ring of kStampRing iterations x 2 workgroups x kStampSlots
   uint64_t* stamps;
-  // peer exchange (dense fused mode, xworld > 0): every workgroup pushes its
-  // two selection keys as tagged granules straight into every rank's receive
-  // buffer (xGMI peer stores); the next launch polls its own buffer until all
-  // tags match.  Layout per rank: [2 parity][xworld * fused_G][4] u64,
-  // granule = tag << 32 | 32-bit half of a key.  Replaces the per-iteration
-  // all-reduce (no collective launch, no host involvement).
+  // persistent cache engine (smo_persist_lru): every workgroup's private copy
+  // of the cache metadata, plru_stride int32 words each:
+  //   [0] CLOCK hand, [1..3] unused, slot_of[n], key_of[L], ref bits (L bytes)
+  int32_t* plru_meta;
+  int64_t plru_stride;
+  // peer exchange (fused / persistent engines, xworld > 0): every workgroup
+  // pushes its two selection keys as tagged granules straight into every rank's
+  // receive buffer (xGMI peer stores); the next iteration polls its own buffer
+  // until all tags match.  Layout per rank: [2 parity][xworld * fused_G][4] u64,
+  // granule = 16-bit tag << 48 | 48-bit payload (xch.hpp).  Replaces the
+  // per-iteration all-reduce (no collective launch, no host involvement).
   uint64_t* const* xpeer;  // [xworld] receive buffers (device-accessible)
   int32_t xrank, xworld;
   int32_t xstride;  // u64 slots per entry (>= kXchGranules; a multiple pads entries apart)

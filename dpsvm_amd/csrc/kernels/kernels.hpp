@@ -33,6 +33,14 @@ void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out
 // workgroup co-resident; keys exchanged as tagged granules, a.xworld >= 1);
 // st: state record in/out (iteration, done, b_hi, b_lo; no pending pair)
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s);
+// cache mode, persistent (smo_persist_lru.hip): up to `steps` SMO iterations in
+// one launch, private per-workgroup cache metadata (a.plru_meta, plru_init);
+// stats: int64 [hits, misses, rows computed, X passes, speculative rows] in/out
+bool smo_persist_lru_supported(int dp, int fused_rows, int fused_G);
+int64_t plru_stride_words(int64_t n, int64_t L);
+void plru_init(int32_t* meta, int64_t stride, int64_t G, int64_t n, int64_t L, hipStream_t s);
+void smo_persist_lru(const SmoArgs& a, FusedRec* st, int steps, int64_t* stats, hipStream_t s);
+void preload_persist_lru_kernel(hipStream_t s);
 // load the code objects of the kernels that spin on other ranks/workgroups
 // BEFORE any of them runs: a first launch that loads its code object while a
 // peer's spinning kernel occupies the device can stall behind it

@@ -83,6 +83,9 @@ struct GpuSolver::Impl {
   // exported), device table of every rank's buffer, IPC mappings to close
   bool xch = false;
   bool persist = false;  // dense mode: persistent kernel, persist_block iterations per launch
+  bool persist_lru = false;  // cache mode: persistent kernel with private per-workgroup cache metadata
+  int32_t* plru_meta = nullptr;
+  int64_t* plru_stats = nullptr;
   uint64_t* xbuf = nullptr;
   uint64_t** xpeer_d = nullptr;
   int64_t xregion = 0;  // u64 words of the two key parities (zeroed per solve)
@@ -117,7 +120,8 @@ struct GpuSolver::Impl {
     if (graph) (void)hipGraphDestroy(graph);
     for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines,
                       (void*)slot_of, (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of,
-                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps})
+                      (void*)partials, (void*)ctrl, (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
+                      (void*)plru_meta, (void*)plru_stats})
       if (ptr) (void)hipFree(ptr);
     if (status_h) (void)hipHostFree(status_h);
     if (hlines_h) (void)hipHostFree(hlines_h);
@@ -216,6 +220,7 @@ struct GpuSolver::Impl {
       DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
       launch::preload_fused_kernels(stream);
       launch::preload_persist_kernel(stream);
+      launch::preload_persist_lru_kernel(stream);
       HIP_CHECK(hipMalloc((void**)&xbuf, (size_t)(xregion + ping_words) * 8));  // own allocation: IPC export
       HIP_CHECK(hipMemset(xbuf, 0, (size_t)(xregion + ping_words) * 8));
       HIP_CHECK(hipDeviceSynchronize());
@@ -366,7 +371,7 @@ struct GpuSolver::Impl {
       // (the record is exact; the host-mapped status refreshes every kStatusEvery)
       int32_t ih = -1, il = -1;
       float ah = 0.f, al = 0.f;
-      if (dense) {
+      if (dense || persist_lru) {
         FusedRec r;
         HIP_CHECK(hipMemcpy(&r, rf + 1, sizeof(r), hipMemcpyDeviceToHost));
         ih = r.i_hi; il = r.i_lo; ah = r.a_hi; al = r.a_lo;
@@ -474,7 +479,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // (the persistent kernel's register budget).  Measured on 60k x 784, 1 GPU:
   // 235 workgroups 5.8-6.2 us per iteration, 118 -> 5.2 us (profiles/README.md).
   auto geometry = [&](int64_t rows_min) {
-    const int64_t per = (nl_max + 255) / 256;
+    int64_t wgs = 256;  // cache mode: one workgroup per CU
+    if (const char* e = std::getenv("DPSVM_CACHE_WGS")) wgs = std::max<int64_t>(1, atoll(e));
+    const int64_t per = (nl_max + wgs - 1) / wgs;
     int64_t rb = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
     rb = std::max(rb, rows_min);
     if (const char* e = std::getenv("DPSVM_FUSED_ROWS")) {  // override: rows per workgroup
@@ -598,6 +605,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     m.RBf = geo_dense.first;
     m.Gf = geo_dense.second;
   }
+  // cache mode, persistent engine candidate: every workgroup's private metadata
+  // copy comes out of the line budget (upper bound: L = n)
+  const char* ple = std::getenv("DPSVM_PERSIST_LRU");
+  const bool plru_cand = !m.dense && m.replicated && m.p.host_cache_lines == 0 && m.p.persist != 1 &&
+                         !(ple && ple[0] == '0') && m.p.use_graph && !m.p.force_collectives &&
+                         launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
+  if (plru_cand) {
+    const double meta_bytes = (double)m.Gf * launch::plru_stride_words(n, n) * 4.0;
+    want_lines = std::min<int64_t>(want_lines, (int64_t)((budget - meta_bytes) / line_bytes));
+  }
   m.L = m.dense ? n : std::max<int64_t>(2, std::min<int64_t>(want_lines, n));
   DPSVM_CHECK(m.L * line_bytes <= (double)freeb, "not enough device memory for 2 kernel-row lines");
   m.lines = dmalloc<float>((size_t)m.L * m.ldl, &m.bytes);
@@ -607,8 +624,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.fused_lru = !m.dense && m.replicated && launch::smo_fused_lru_supported(m.dp) && !(lk && lk[0] == '3');
   if (m.fused()) {
     m.pf = dmalloc<uint64_t>((size_t)4 * m.Gf, &m.bytes);
-    if (m.dense) m.rf = dmalloc<FusedRec>(2, &m.bytes);
-    else m.rcf = dmalloc<FusedCacheRec>(2, &m.bytes);
+    if (m.dense || plru_cand) m.rf = dmalloc<FusedRec>(2, &m.bytes);
+    if (!m.dense) m.rcf = dmalloc<FusedCacheRec>(2, &m.bytes);
   }
   if (!m.dense) {
     m.slot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
@@ -710,7 +727,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // register-resident rows and one resident workgroup per CU (launch::smo_persist)
     want_persist = want_persist && m.RBf <= 4 * kFusedThreads && m.Gf <= 256;
   }
-  if (m.dense && ((m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || want_persist)) {
+  // cache mode: the persistent cache engine (same exchange) unless the exchange
+  // is pinned to the communicator all-reduce or the geometry does not fit it
+  const bool want_plru = plru_cand && m.fused_lru && m.p.exchange != 1;
+  if ((m.dense && ((m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || want_persist)) || want_plru) {
     const bool ok = m.setup_exchange();
     DPSVM_CHECK(ok || (m.p.exchange != 2 && m.p.persist != 2),
                 "peer exchange requested (exchange=2 / persist=2) but its self test failed (" + m.xch_diag + ")");
@@ -733,6 +753,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                           : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
   m.persist = want_persist && m.xch;
   if (m.persist) m.info.iteration = "persistent-dense";
+  m.persist_lru = want_plru && m.xch;
+  a.plru_meta = nullptr;
+  a.plru_stride = 0;
+  if (m.persist_lru) {
+    a.plru_stride = launch::plru_stride_words(n, m.L);
+    m.plru_meta = dmalloc<int32_t>((size_t)m.Gf * a.plru_stride, &m.bytes);
+    m.plru_stats = dmalloc<int64_t>(8, &m.bytes);
+    a.plru_meta = m.plru_meta;
+    m.info.iteration = "persistent-cache";
+  }
   m.info.bytes_device = m.bytes;
   return m.info;
 }
@@ -892,6 +922,10 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
       launch::fill_i32(m.hslot_of, m.n, -1, m.stream);
       launch::fill_i32(m.hkey_of, m.H, -1, m.stream);
     }
+    if (m.persist_lru) {  // every workgroup's private copy: empty cache, hand 0
+      launch::plru_init(m.plru_meta, m.args.plru_stride, m.Gf, m.n, m.L, m.stream);
+      HIP_CHECK(hipMemsetAsync(m.plru_stats, 0, 8 * sizeof(int64_t), m.stream));
+    }
   }
   m.init_ctrl(iter0, b_hi0, b_lo0);
   if (m.xch) HIP_CHECK(hipMemsetAsync(m.xbuf, 0, (size_t)m.xregion * 8, m.stream));  // tags restart at iter0 + 1
@@ -905,7 +939,18 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   bool fault_done = false;
   auto t0 = Clock::now();
   EventTimer gram_timer;
-  if (m.fused_lru) {
+  if (m.persist_lru) {
+    // seed: "no pending pair" record + initial keys published to the exchange
+    FusedRec r0;
+    r0.i_hi = r0.i_lo = -1;
+    r0.a_hi = r0.a_lo = 0.f;
+    r0.iter = (int32_t)iter0;
+    r0.done = kRunning;
+    r0.b_hi = b_hi0;
+    r0.b_lo = b_lo0;
+    HIP_CHECK(hipMemcpyAsync(m.rf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
+    launch::smo_fused(m.args, 0, nullptr, m.pf + 2 * m.Gf, m.rf + 1, nullptr, m.stream);
+  } else if (m.fused_lru) {
     // seed: record "no pending pair, empty cache" in buffer 1 + initial keys
     FusedCacheRec r0;
     memset(&r0, 0, sizeof(r0));
@@ -948,8 +993,8 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
   int B = std::max(1, m.p.graph_block);
   if (m.fused()) B = std::max(2, (B + 1) / 2 * 2);  // ping-pong parity must survive graph replays
-  if (m.persist) B = std::max(1, m.p.persist_block);
-  if (graphs && !m.persist) {
+  if (m.persist || m.persist_lru) B = std::max(1, m.p.persist_block);
+  if (graphs && !m.persist && !m.persist_lru) {
     try {
       m.build_graph(B);
     } catch (const std::exception& e) {
@@ -963,6 +1008,8 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   while (true) {
     if (m.persist) {
       launch::smo_persist(m.args, m.rf + 1, B, m.stream);
+    } else if (m.persist_lru) {
+      launch::smo_persist_lru(m.args, m.rf + 1, B, m.plru_stats, m.stream);
     } else if (m.gexec) {
       HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
     } else {

@@ -176,7 +176,7 @@ def test_gpu_fault_injection_and_verify(monkeypatch, C):
     assert ok.converged_
 
 
-@pytest.mark.parametrize("engine", ["persistent", "fused", "cache", "chain", "partitioned"])
+@pytest.mark.parametrize("engine", ["persistent", "fused", "cache", "fused-cache", "chain", "partitioned"])
 def test_verify_invariants_every_engine(monkeypatch, engine):
     """DPSVM_VERIFY=1: alpha in [0, C] and the incrementally updated f equals f
     recomputed from alpha (predict GEMM) at the end of the run, for every engine."""
@@ -185,8 +185,10 @@ def test_verify_invariants_every_engine(monkeypatch, engine):
     kw = dict(C=10.0, gamma=0.25, device="cuda")
     if engine == "fused":
         kw["persist"] = "off"
-    elif engine in ("cache", "chain"):
+    elif engine in ("cache", "fused-cache", "chain"):
         kw["cache_lines"] = 64
+        if engine == "fused-cache":
+            kw["persist"] = "off"
         if engine == "chain":
             monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
     elif engine == "partitioned":
@@ -206,7 +208,7 @@ def test_fused_cache_iteration_matches_kernel_chain(monkeypatch, extra):
     rows/step/finalize chain compute bit-identical kernel rows, so they must
     follow the same SMO trajectory (whatever their cache decisions)."""
     X, y = synthetic("covtype", n=5000, seed=6)
-    kw = dict(C=4.0, gamma=0.5, device="cuda", **extra)
+    kw = dict(C=4.0, gamma=0.5, device="cuda", persist="off", **extra)
     fused = SVC(**kw).fit(X, y)
     assert fused.setup_info_["iteration"] == "fused-cache"
     monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
@@ -222,7 +224,7 @@ def test_fused_cache_iteration_matches_kernel_chain(monkeypatch, extra):
 def test_fused_cache_wide_features_and_checkpoint(monkeypatch, tmp_path):
     """d > one LDS k-chunk (multi-chunk X pass) + checkpoint/resume in cache mode."""
     X, y = synthetic("blobs", n=2500, d=1100, seed=8, sep=1.0)
-    kw = dict(C=1.0, gamma=1.0 / 1100, device="cuda", cache_lines=48)
+    kw = dict(C=1.0, gamma=1.0 / 1100, device="cuda", cache_lines=48, persist="off")
     cpu = SVC(C=1.0, gamma=1.0 / 1100, device="cpu").fit(X, y)
     full = SVC(**kw).fit(X, y)
     assert full.setup_info_["iteration"] == "fused-cache"
@@ -237,6 +239,31 @@ def test_fused_cache_wide_features_and_checkpoint(monkeypatch, tmp_path):
     monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
     chain = SVC(**kw).fit(X, y)
     assert np.array_equal(chain.alpha_, full.alpha_)
+
+
+@pytest.mark.parametrize("case", ["covtype-spec", "covtype-nospec", "tiny-cache", "wide", "max-iter", "box"])
+def test_persistent_cache_engine_matches_fused(monkeypatch, case):
+    """Persistent cache engine (private per-workgroup CLOCK metadata, keys
+    exchanged in-kernel, X pass per workgroup) == the one-launch-per-iteration
+    cache engine, bit for bit: same kernel rows, same trajectory."""
+    monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
+    if case == "wide":
+        X, y = synthetic("blobs", n=2500, d=1100, seed=8, sep=1.0)
+        kw = dict(C=1.0, gamma=1.0 / 1100, cache_lines=48)
+    else:
+        X, y = synthetic("covtype", n=6000, seed=6)
+        kw = dict(C=4.0, gamma=0.5, cache_lines=256)
+    kw.update({"covtype-spec": {}, "covtype-nospec": {"spec_rows": 0}, "tiny-cache": {"cache_lines": 2, "spec_rows": 0},
+               "wide": {}, "max-iter": {"max_iter": 1500}, "box": {"clip": "box"}}[case])
+    got = SVC(device="cuda", persist_block=301, **kw).fit(X, y)
+    assert got.setup_info_["iteration"] == "persistent-cache"
+    ref = SVC(device="cuda", persist="off", **kw).fit(X, y)
+    assert ref.setup_info_["iteration"] == "fused-cache"
+    assert got.n_iter_ == ref.n_iter_ and got.status_ == ref.status_
+    assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
+    assert got.stats_["cache_misses"] > 0 and got.stats_["x_passes"] > 0
+    if case == "max-iter":
+        assert got.n_iter_ == 1500 and got.status_ == 2
 
 
 def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
