@@ -27,6 +27,8 @@
 #include "dpsvm/device_state.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
+#include "plan_util.hpp"
+#include "xpass.hpp"
 #include "../runtime/hip_check.hpp"
 
 namespace dpsvm {
@@ -141,28 +143,6 @@ __device__ __forceinline__ void publish_status_lru(SmoStatus* st, const FusedCac
   __atomic_store_n(&st->seq, o.iter, __ATOMIC_RELEASE);
 }
 
-// exclusive prefix sum of v over the workgroup (kFusedThreads); *total = sum
-__device__ __forceinline__ int block_excl_scan(int v, int* total, int* wsum) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int incl = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  if (lane == 63) wsum[wave] = incl;
-  __syncthreads();
-  int before = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kFusedThreads / 64; ++w) {
-    before += w < wave ? wsum[w] : 0;
-    tot += wsum[w];
-  }
-  __syncthreads();
-  *total = tot;
-  return before + incl - v;
-}
-
 // Apply the previous record to memory (alphas + cache metadata) with threads
 // ct = 0..nt-1 (nt >= 32) of one workgroup, in parallel and without a barrier:
 // scanned window bits are written once with their final value (1 for new /
@@ -209,25 +189,6 @@ __device__ void commit_record(const SmoArgs& a, const FusedCacheRec& r, const Re
       a.hslot_of[o] = hl;
     }
   }
-}
-
-// lanes holding the t smallest of the wave's values among `valid` lanes
-// (values unique): MSB-first radix select on ballots, uniform SALU control
-__device__ __forceinline__ uint64_t wave_smallest(uint64_t v, int t, uint64_t valid) {
-  uint64_t chosen = 0, active = valid;
-  int need = t;
-  for (int bit = 63; bit >= 0 && need > 0 && active; --bit) {
-    const uint64_t zero = __ballot(((v >> bit) & 1ull) == 0ull) & active;
-    const int nz = __popcll(zero);
-    if (nz <= need) {
-      chosen |= zero;
-      need -= nz;
-      active &= ~zero;
-    } else {
-      active = zero;
-    }
-  }
-  return chosen;
 }
 
 __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
@@ -552,145 +513,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
         for (int64_t j = row0 + tid; j < row_end; j += kFusedThreads) dst[j] = src[j];
       }
     }
-    if (pl.n_compute > 0) {
-      const int dp = a.dp;
-      const int q = lane & 15;
-      const bool qv = q < n_new && pl.op[q] == kOpCompute;
-      const float wsq = qv ? a.xsq[pl.key[q]] : 0.f;
-      const int64_t xbase = a.off - a.x_row0;
-      const int npass = (int)((row_end - row0 + 255) / 256);
-      float* xsq_s = wsm + kNQ * ((dp < kRowsKC ? dp : kRowsKC) + 4);  // [fused_rows] |x_j|^2 of own rows
-      // X loads in batches of 4 k-steps x 4 tiles (16 KiB per wave in flight,
-      // one workgroup per CU: the pass is HBM-latency bound without deep
-      // prefetch); sched_barrier keeps the scheduler from sinking the loads
-      // back next to their MFMAs.  Same k order as smo_rows: bit-identical rows.
-      f4 acc[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
-      auto xrow = [&](int pass) {
-        return a.x + (xbase + row0 + (int64_t)pass * 256 + wave * 64 + (lane & 15)) * dp + 4 * (lane >> 4);
-      };
-      auto load = [&](f4 (&v)[4][4], const float* xk, int k) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) v[s][t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k + 16 * s);
-      };
-      auto comp = [&](const f4 (&v)[4][4], const float* wr, int k) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const f4 wv = *(const f4*)(wr + k + 16 * s);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            acc[t] = mfma16(v[s][t].x, wv.x, acc[t]);
-            acc[t] = mfma16(v[s][t].y, wv.y, acc[t]);
-            acc[t] = mfma16(v[s][t].z, wv.z, acc[t]);
-            acc[t] = mfma16(v[s][t].w, wv.w, acc[t]);
-          }
-        }
-      };
-      auto comp16 = [&](const float* xk, const float* wr, int k0, int k1) {  // 16-wide k-steps [k0, k1)
-        for (int k = k0; k < k1; k += 16) {
-          const f4 wv = *(const f4*)(wr + k);
-          f4 xv[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) xv[t] = *(const f4*)(xk + (int64_t)t * 16 * dp + k);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            acc[t] = mfma16(xv[t].x, wv.x, acc[t]);
-            acc[t] = mfma16(xv[t].y, wv.y, acc[t]);
-            acc[t] = mfma16(xv[t].z, wv.z, acc[t]);
-            acc[t] = mfma16(xv[t].w, wv.w, acc[t]);
-          }
-        }
-      };
-      auto epilogue = [&](int pass) {  // K values of this pass's 256 rows -> the new lines
-        if (qv) {
-          float* out = a.lines + (int64_t)pl.line[q] * a.ldl + row0;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int rel = pass * 256 + wave * 64 + t * 16 + (lane >> 4) * 4;
-            f4 kv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) kv[r] = rbf_from_dot(xsq_s[rel + r], wsq, acc[t][r], a.gamma);
-            *(f4*)(out + rel) = kv;
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
-      };
-      // own rows' |x|^2 staged once (one round trip instead of one per pass)
-      for (int i = tid; i < npass * 256; i += kFusedThreads) xsq_s[i] = a.xsq[a.off + row0 + i];
-      if (dp <= kRowsKC) {
-        // single staged chunk: the batch sequence runs across passes, so the
-        // next pass's first X batch is in flight during this pass's epilogue
-        const int ldw = dp + 4, k4n = dp >> 2;
-        for (int i = tid; i < kNQ * k4n; i += kFusedThreads) {
-          const int qq = i / k4n, k4 = i - qq * k4n;
-          f4 v = {0.f, 0.f, 0.f, 0.f};
-          if (qq < n_new && pl.op[qq] == kOpCompute) v = *(const f4*)(a.x + ((int64_t)pl.key[qq] - a.x_row0) * dp + 4 * k4);
-          *(f4*)(wsm + qq * ldw + 4 * k4) = v;
-        }
-        __syncthreads();
-        const float* wr = wsm + q * ldw + 4 * (lane >> 4);
-        const int nb = dp >> 6, S = npass * nb;
-        auto finish = [&](int pass) {
-          comp16(xrow(pass), wr, nb * 64, dp);  // remainder k-steps (dp % 64)
-          epilogue(pass);
-        };
-        if (nb == 0) {
-          for (int pass = 0; pass < npass; ++pass) finish(pass);
-        } else {
-          f4 xa[4][4], xb[4][4];
-          load(xa, xrow(0), 0);
-          for (int st = 0; st < S; st += 2) {
-            if (st + 1 < S) load(xb, xrow((st + 1) / nb), ((st + 1) % nb) * 64);
-            __builtin_amdgcn_sched_barrier(0);
-            comp(xa, wr, (st % nb) * 64);
-            if ((st + 1) % nb == 0) finish(st / nb);
-            if (st + 1 < S) {
-              if (st + 2 < S) load(xa, xrow((st + 2) / nb), ((st + 2) % nb) * 64);
-              __builtin_amdgcn_sched_barrier(0);
-              comp(xb, wr, ((st + 1) % nb) * 64);
-              if ((st + 2) % nb == 0) finish((st + 1) / nb);
-            }
-          }
-        }
-      } else {
-        // wide rows: query vectors restaged per k-chunk of kRowsKC
-        for (int pass = 0; pass < npass; ++pass) {
-          const float* xr = xrow(pass);
-          for (int kc = 0; kc < dp; kc += kRowsKC) {
-            const int kcl = min(kRowsKC, dp - kc), ldw = kcl + 4, k4n = kcl >> 2;
-            __syncthreads();  // previous readers of the staged chunk are done
-            for (int i = tid; i < kNQ * k4n; i += kFusedThreads) {
-              const int qq = i / k4n, k4 = i - qq * k4n;
-              f4 v = {0.f, 0.f, 0.f, 0.f};
-              if (qq < n_new && pl.op[qq] == kOpCompute)
-                v = *(const f4*)(a.x + ((int64_t)pl.key[qq] - a.x_row0) * dp + kc + 4 * k4);
-              *(f4*)(wsm + qq * ldw + 4 * k4) = v;
-            }
-            __syncthreads();
-            const float* wr = wsm + q * ldw + 4 * (lane >> 4) - kc;  // indexed with absolute k
-            const int nb = kcl >> 6;
-            f4 xa[4][4], xb[4][4];
-            if (nb > 0) load(xa, xr, kc);
-            for (int bb = 0; bb < nb; bb += 2) {
-              if (bb + 1 < nb) load(xb, xr, kc + (bb + 1) * 64);
-              __builtin_amdgcn_sched_barrier(0);
-              comp(xa, wr, kc + bb * 64);
-              if (bb + 1 < nb) {
-                if (bb + 2 < nb) load(xa, xr, kc + (bb + 2) * 64);
-                __builtin_amdgcn_sched_barrier(0);
-                comp(xb, wr, kc + (bb + 1) * 64);
-              }
-            }
-            comp16(xr, wr, kc + nb * 64, kc + kcl);
-          }
-          epilogue(pass);
-        }
-      }
-    }
+    if (pl.n_compute > 0) xpass_fill(a, row0, row_end, n_new, pl.key, pl.line, pl.op, wsm, false);
     __syncthreads();  // this workgroup's new line segments are visible to all its waves
   }
 
@@ -824,9 +647,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_fused_lru_kernel(SmoArgs a,
 
 namespace launch {
 
-size_t smo_fused_lru_lds_bytes(int dp, int fused_rows) {
-  return ((size_t)kNQ * ((dp < kRowsKC ? dp : kRowsKC) + 4) + (size_t)fused_rows) * sizeof(float);
-}
+size_t smo_fused_lru_lds_bytes(int dp, int fused_rows) { return dev::xpass_lds_floats(dp, fused_rows) * sizeof(float); }
 
 bool smo_fused_lru_supported(int dp) { return dp >= 16 && dp % 16 == 0; }
 
