@@ -67,7 +67,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --spec N            :  speculative kernel rows per X pass (LRU mode, default 14)\n"
                "   --host-cache-lines N:  pinned host spill tier for evicted kernel rows (LRU mode)\n"
                "   --graph-block N     :  SMO iterations per hipGraph (default 64); --no-graph\n"
-               "   --persist MODE      :  dense engine: auto | off (one launch/iteration) | on (persistent)\n"
+               "   --persist MODE      :  engine: auto | off (one launch/iteration) | on (persistent; dense and cache mode)\n"
                "   --persist-block N   :  SMO iterations per persistent launch (default 2048)\n"
                "   --exchange MODE     :  per-iteration keys: auto | allreduce | peer (in-kernel, xGMI)\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"

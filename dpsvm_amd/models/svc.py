@@ -76,7 +76,7 @@ class SVCConfig:
     verbose: bool = False
     force_collectives: bool = False  # run the per-iteration collective even with one rank (tests)
     exchange: str = "auto"          # per-iteration key exchange (dense mode): auto | allreduce | peer
-    persist: str = "auto"           # dense-mode engine: auto | off (one launch per iteration) | on (persistent)
+    persist: str = "auto"           # engine: auto | off (one launch per iteration) | on (persistent, dense or cache mode)
     persist_block: int = 2048       # SMO iterations per persistent launch
 
     def resolved_gamma(self, d: int) -> float:
