@@ -209,6 +209,7 @@ def main(argv=None) -> int:
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
             "exchange": info.get("exchange", "none"),
+            "exchange_mem": info.get("exchange_mem", "none"),
             "preset": a.config,
         }
         line = json.dumps(out)

@@ -63,6 +63,7 @@ struct GpuSetupInfo {
   size_t bytes_device = 0;
   std::string iteration;  // "fused-dense" | "fused-cache" | "chain" (rows/step/finalize)
   std::string exchange;   // per-iteration key exchange: "none" | "allreduce" | "peer" | "loopback" (1 rank)
+  std::string exchange_mem = "none";  // peer exchange receive buffer: "uncached" (across devices) | "coarse"
 };
 
 class GpuSolver {

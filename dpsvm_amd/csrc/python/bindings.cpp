@@ -329,6 +329,7 @@ PYBIND11_MODULE(_C, m) {
         d["x_replicated"] = i.x_replicated;
         d["iteration"] = i.iteration;
         d["exchange"] = i.exchange;
+        d["exchange_mem"] = i.exchange_mem;
         d["cache_lines"] = i.cache_lines;
         d["blocks"] = i.blocks;
         d["bytes_device"] = i.bytes_device;

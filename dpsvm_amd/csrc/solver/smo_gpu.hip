@@ -92,6 +92,7 @@ struct GpuSolver::Impl {
   int64_t xstride = kXchGranules;  // u64 slots per exchange entry
   std::vector<void*> xopened;
   std::string xch_diag;
+  std::string xch_mem = "none";  // receive-buffer memory kind (uncached across devices)
   int64_t Gf = 0, RBf = 0;
   uint64_t* stamps = nullptr;  // DPSVM_STAMPS diagnostics
   std::string stamps_path;
@@ -221,7 +222,21 @@ struct GpuSolver::Impl {
       launch::preload_fused_kernels(stream);
       launch::preload_persist_kernel(stream);
       launch::preload_persist_lru_kernel(stream);
-      HIP_CHECK(hipMalloc((void**)&xbuf, (size_t)(xregion + ping_words) * 8));  // own allocation: IPC export
+      // own allocation (IPC export).  Ranks on other devices write it over xGMI:
+      // uncached device memory, so no L2 of this device can hold a stale line of
+      // a granule a peer rewrote (coarse-grained memory is only coherent within
+      // one device); DPSVM_XCH_MEM=coarse keeps plain hipMalloc memory
+      const size_t xbytes = (size_t)(xregion + ping_words) * 8;
+      const char* xm = std::getenv("DPSVM_XCH_MEM");
+      const std::string xms = xm ? xm : "";
+      const bool uncached = (world > 1 || xms == "uncached") && xms != "coarse";
+      const bool got_uc = uncached && hipExtMallocWithFlags((void**)&xbuf, xbytes, hipDeviceMallocUncached) == hipSuccess;
+      if (!got_uc) {
+        (void)hipGetLastError();
+        xbuf = nullptr;
+        HIP_CHECK(hipMalloc((void**)&xbuf, xbytes));
+      }
+      xch_mem = got_uc ? "uncached" : "coarse";
       HIP_CHECK(hipMemset(xbuf, 0, (size_t)(xregion + ping_words) * 8));
       HIP_CHECK(hipDeviceSynchronize());
       me.ptr = (uint64_t)xbuf;
@@ -749,6 +764,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       a.xtimeout_ticks = (int64_t)(tmo * 1e8);
     }
   }
+  m.info.exchange_mem = m.xch ? m.xch_mem : "none";
   m.info.exchange = m.xch ? (m.world > 1 ? "peer" : "loopback")
                           : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
   m.persist = want_persist && m.xch;

@@ -21,6 +21,7 @@ def main(out: str, engine: str, n: int) -> int:
     clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer",
               persist="off" if engine == "fused" else "on", persist_block=257).fit(X, y, comm=comm)
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
+           "exchange_mem": clf.setup_info_["exchange_mem"],
            "iters": int(clf.n_iter_), "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
     with open(f"{out}.rank{ctx.rank}.json", "w") as f:
         json.dump(rec, f)

@@ -342,7 +342,7 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     X, y = synthetic("covtype", n=n, seed=2)
     ref = SVC(C=4.0, gamma=0.5, eps=1e-3, device="cuda").fit(X, y)
     for k in range(2):
-        assert res[k]["exchange"] == "peer"
+        assert res[k]["exchange"] == "peer" and res[k]["exchange_mem"] == "uncached"
         assert res[k]["iteration"] == ("fused-dense" if engine == "fused" else "persistent-dense")
         assert res[k]["iters"] == ref.n_iter_
         assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
