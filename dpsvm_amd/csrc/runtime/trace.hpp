@@ -64,6 +64,13 @@ inline bool verify_enabled() {
   return e && e[0] == '1';
 }
 
+// DPSVM_VERIFY=ranks: only the cross-rank alpha digest (one 16-byte all-reduce
+// per solve; what bench.py enables for N > 1), no f recomputation
+inline bool verify_ranks_enabled() {
+  const char* e = std::getenv("DPSVM_VERIFY");
+  return e && (e[0] == '1' || std::string(e) == "ranks");
+}
+
 // order-sensitive 64-bit hash of float bit patterns (FNV-1a over words)
 inline uint64_t hash_floats(const float* p, size_t n) {
   uint64_t h = 1469598103934665603ull;

@@ -281,7 +281,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
     if (!(err <= (te ? atof(te) : 1e-3)))
       fail("DPSVM_VERIFY: f inconsistent with alpha (max relative error " + std::to_string(err) + ")");
   }
-  if (world > 1 && trace::verify_enabled()) {
+  if (world > 1 && trace::verify_ranks_enabled()) {
     // cross-rank consistency: every rank must hold bit-identical alphas
     const uint64_t h = trace::hash_floats(alpha.data(), alpha.size());
     uint64_t hk[2] = {h, ~h};

@@ -1099,7 +1099,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     if (!(err <= tol))
       fail("DPSVM_VERIFY: f inconsistent with alpha (max relative error " + std::to_string(err) + ")");
   }
-  if (m.collectives() && trace::verify_enabled()) {
+  if (m.collectives() && trace::verify_ranks_enabled()) {
     // cross-rank consistency: every rank must hold bit-identical alphas
     std::vector<float> ah((size_t)m.n);
     HIP_CHECK(hipMemcpy(ah.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
