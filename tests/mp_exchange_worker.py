@@ -18,8 +18,9 @@ def main(out: str, engine: str, n: int) -> int:
     ctx = init_distributed(device="cuda")
     comm = make_comm(ctx, "gloo")
     X, y = synthetic("covtype", n=n, seed=2)
+    extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
     clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer",
-              persist="off" if engine == "fused" else "on", persist_block=257).fit(X, y, comm=comm)
+              persist="off" if engine == "fused" else "on", persist_block=257, **extra).fit(X, y, comm=comm)
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
            "exchange_mem": clf.setup_info_["exchange_mem"],
            "iters": int(clf.n_iter_), "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}

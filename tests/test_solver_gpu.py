@@ -318,7 +318,7 @@ def test_persistent_engine_matches_fused(monkeypatch, block):
     assert m.n_iter_ == 1000 and m.status_ == 2 and np.array_equal(m.alpha_, m_ref.alpha_)
 
 
-@pytest.mark.parametrize("engine", ["fused", "persistent", "persistent-batches"])
+@pytest.mark.parametrize("engine", ["fused", "persistent", "persistent-batches", "persistent-cache"])
 def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     """Two ranks as two processes sharing the GPU (gloo bootstrap, IPC-mapped
     receive buffers): in-kernel exchange, bit-identical to one rank.
@@ -332,7 +332,7 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     if engine == "persistent-batches":
         env.update(DPSVM_DENSE_ROWS="256", DPSVM_XCH_KB="1")
     out = tmp_path / "mp"
-    port = 29600 + ["fused", "persistent", "persistent-batches"].index(engine)
+    port = 29600 + ["fused", "persistent", "persistent-batches", "persistent-cache"].index(engine)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n)]
@@ -340,10 +340,12 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = [json.load(open(f"{out}.rank{k}.json")) for k in range(2)]
     X, y = synthetic("covtype", n=n, seed=2)
-    ref = SVC(C=4.0, gamma=0.5, eps=1e-3, device="cuda").fit(X, y)
+    extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
+    ref = SVC(C=4.0, gamma=0.5, eps=1e-3, device="cuda", **extra).fit(X, y)
+    want = {"fused": "fused-dense", "persistent-cache": "persistent-cache"}.get(engine, "persistent-dense")
     for k in range(2):
         assert res[k]["exchange"] == "peer" and res[k]["exchange_mem"] == "uncached"
-        assert res[k]["iteration"] == ("fused-dense" if engine == "fused" else "persistent-dense")
+        assert res[k]["iteration"] == want
         assert res[k]["iters"] == ref.n_iter_
         assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
 
