@@ -35,12 +35,12 @@
 namespace dpsvm {
 namespace dev {
 
-constexpr int kPersistMaxRows = 4;  // rows per thread (fused_rows <= 1024)
+constexpr int kPersistMaxRows = 12;  // rows per thread (fused_rows <= 3072); kR = 4 up to 1024 rows
 
 // kSys: system-scope exchange (ranks on other devices / processes); kB: poll
 // batch, publications watched per lane per round (xch.hpp).  One poll loop per
 // instantiation: no dispatch inside the iteration.
-template <bool kSys, int kB>
+template <bool kSys, int kB, int kR>
 __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, FusedRec* __restrict__ st, int steps) {
   static_assert(kFusedThreads == 256, "4 waves assumed");
   __shared__ uint64_t kscr[8];
@@ -54,10 +54,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
   const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
 
-  float f[kPersistMaxRows], al[kPersistMaxRows], yv[kPersistMaxRows];
-  bool has[kPersistMaxRows];
+  float f[kR], al[kR], yv[kR];
+  bool has[kR];
 #pragma unroll
-  for (int k = 0; k < kPersistMaxRows; ++k) {
+  for (int k = 0; k < kR; ++k) {
     const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
     has[k] = k < rpt && j < row_end;
     f[k] = has[k] ? a.f[j] : 0.f;
@@ -112,9 +112,9 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     const float* line_lo = a.lines + (int64_t)i_lo * a.ldl;
     // unconditional loads (absent rows read the first own row): no exec-mask
     // branches between them, so every load of the round trip is in flight together
-    float khv[kPersistMaxRows], klv[kPersistMaxRows];
+    float khv[kR], klv[kR];
 #pragma unroll
-    for (int k = 0; k < kPersistMaxRows; ++k) {
+    for (int k = 0; k < kR; ++k) {
       const int64_t j = has[k] ? row0 + tid + (int64_t)k * kFusedThreads : row0;
       khv[k] = line_hi[j];
       klv[k] = line_lo[j];
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
     const bool upd_f = c_hi != 0.f || c_lo != 0.f;
     XKeys nk = xk_none();
 #pragma unroll
-    for (int k = 0; k < kPersistMaxRows; ++k) {
+    for (int k = 0; k < kR; ++k) {
       if (!has[k]) continue;
       const int64_t g = a.off + row0 + tid + (int64_t)k * kFusedThreads;
       if (upd_f) f[k] = f_apply(f[k], c_hi, khv[k], c_lo, klv[k]);
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
 
   // ---- exit: own rows' f back to memory; workgroup 0 writes the state ----
 #pragma unroll
-  for (int k = 0; k < kPersistMaxRows; ++k) {
+  for (int k = 0; k < kR; ++k) {
     const int64_t j = row0 + tid + (int64_t)k * kFusedThreads;
     if (has[k]) a.f[j] = f[k];
   }
@@ -238,15 +238,34 @@ void preload_persist_kernel(hipStream_t s) {
   SmoArgs z{};
   z.fused_G = 1;
   z.fused_rows = kFusedThreads;
-  dev::smo_persist_kernel<false, 1><<<1, kFusedThreads, 0, s>>>(z, st, 0);
-  dev::smo_persist_kernel<false, 2><<<1, kFusedThreads, 0, s>>>(z, st, 0);
-  dev::smo_persist_kernel<false, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
-  dev::smo_persist_kernel<true, 1><<<1, kFusedThreads, 0, s>>>(z, st, 0);
-  dev::smo_persist_kernel<true, 2><<<1, kFusedThreads, 0, s>>>(z, st, 0);
-  dev::smo_persist_kernel<true, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 1, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 2, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 4, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 1, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 2, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 4, 4><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 1, dev::kPersistMaxRows><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 2, dev::kPersistMaxRows><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<false, 4, dev::kPersistMaxRows><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 1, dev::kPersistMaxRows><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 2, dev::kPersistMaxRows><<<1, kFusedThreads, 0, s>>>(z, st, 0);
+  dev::smo_persist_kernel<true, 4, dev::kPersistMaxRows><<<1, kFusedThreads, 0, s>>>(z, st, 0);
   HIP_CHECK(hipStreamSynchronize(s));
   HIP_CHECK(hipGetLastError());
   (void)hipFree(st);
+}
+
+template <int kR>
+static void launch_persist(const SmoArgs& a, FusedRec* st, int steps, int kb, dim3 g, hipStream_t s) {
+  if (a.xworld > 1) {
+    if (kb == 1) dev::smo_persist_kernel<true, 1, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else if (kb == 2) dev::smo_persist_kernel<true, 2, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else dev::smo_persist_kernel<true, 4, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+  } else {
+    if (kb == 1) dev::smo_persist_kernel<false, 1, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else if (kb == 2) dev::smo_persist_kernel<false, 2, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+    else dev::smo_persist_kernel<false, 4, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
+  }
 }
 
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {
@@ -255,15 +274,9 @@ void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {
   const int E = a.xworld * a.fused_G;
   const int kb = a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
   const dim3 g(a.fused_G);
-  if (a.xworld > 1) {
-    if (kb == 1) dev::smo_persist_kernel<true, 1><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else if (kb == 2) dev::smo_persist_kernel<true, 2><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else dev::smo_persist_kernel<true, 4><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-  } else {
-    if (kb == 1) dev::smo_persist_kernel<false, 1><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else if (kb == 2) dev::smo_persist_kernel<false, 2><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else dev::smo_persist_kernel<false, 4><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-  }
+  // rows per thread: 4 (<= 1024 rows per workgroup, the headline geometry) or 12
+  if (a.fused_rows <= 4 * kFusedThreads) launch_persist<4>(a, st, steps, kb, g, s);
+  else launch_persist<dev::kPersistMaxRows>(a, st, steps, kb, g, s);
   post_launch("smo_persist", s);
 }
 

@@ -491,7 +491,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // <= ~256 workgroups (the X pass wants every CU).  Dense mode: the period is
   // set by the all-to-all key exchange, whose cost grows with the number of
   // publishers (world x G): ~128 publishers in all, <= 1024 rows per workgroup
-  // (the persistent kernel's register budget).  Measured on 60k x 784, 1 GPU:
+  // (up to 3072 — 12 register rows per thread — only when 256 resident
+  // workgroups would not cover the shard).  Measured on 60k x 784, 1 GPU:
   // 235 workgroups 5.8-6.2 us per iteration, 118 -> 5.2 us (profiles/README.md).
   auto geometry = [&](int64_t rows_min) {
     int64_t wgs = 256;  // cache mode: one workgroup per CU
@@ -508,8 +509,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const auto geo_cache = geometry(0);
   int64_t dense_rows =
       std::min<int64_t>(1024, round_up(std::max<int64_t>(1, nl_max * m.world / 128), kFusedThreads));
+  // more rows per thread only when <= 256 resident workgroups need them (n = 200k
+  // dense on one GPU: 1024 rows x 196 workgroups 0.66 s vs 1792 x 112 0.69 s)
+  if ((nl_max + dense_rows - 1) / dense_rows > 256) dense_rows = round_up((nl_max + 255) / 256, kFusedThreads);
   if (const char* e = std::getenv("DPSVM_DENSE_ROWS"))  // tests: more publishers (multi-batch polls)
-    dense_rows = std::max<int64_t>(kFusedThreads, std::min<int64_t>(1024, atoll(e) / kFusedThreads * kFusedThreads));
+    dense_rows = std::max<int64_t>(kFusedThreads, std::min<int64_t>(3072, atoll(e) / kFusedThreads * kFusedThreads));
   auto geo_dense = geometry(dense_rows);
   if (std::getenv("DPSVM_DENSE_ROWS"))
     geo_dense = {dense_rows, std::max<int64_t>(1, (nl_max + dense_rows - 1) / dense_rows)};
@@ -740,7 +744,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // (and unless a test forces the per-iteration collective path or eager launches)
     want_persist = mode == 2 || (mode == 0 && m.p.exchange != 1 && m.p.use_graph && !m.p.force_collectives);
     // register-resident rows and one resident workgroup per CU (launch::smo_persist)
-    want_persist = want_persist && m.RBf <= 4 * kFusedThreads && m.Gf <= 256;
+    want_persist = want_persist && m.RBf <= 12 * kFusedThreads && m.Gf <= 256;
   }
   // cache mode: the persistent cache engine (same exchange) unless the exchange
   // is pinned to the communicator all-reduce or the geometry does not fit it

@@ -299,12 +299,14 @@ def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
         assert out[r].n_iter_ == ref.n_iter_ and np.array_equal(out[r].alpha_, ref.alpha_)
 
 
-@pytest.mark.parametrize("block", [2048, 37])
-def test_persistent_engine_matches_fused(monkeypatch, block):
+@pytest.mark.parametrize("block,rows", [(2048, None), (37, None), (501, 3072)])
+def test_persistent_engine_matches_fused(monkeypatch, block, rows):
     """Persistent dense kernel (keys exchanged in-kernel, row state in
     registers) == one launch per iteration, bit for bit; also across launches
-    of an odd block length and at max_iter."""
+    of an odd block length, at max_iter, and with 12 rows per thread."""
     monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
+    if rows:
+        monkeypatch.setenv("DPSVM_DENSE_ROWS", str(rows))
     X, y = synthetic("covtype", n=6000, seed=2)
     kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
     ref = SVC(persist="off", **kw).fit(X, y)
