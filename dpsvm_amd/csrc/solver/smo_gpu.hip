@@ -509,8 +509,12 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const auto geo_cache = geometry(0);
   int64_t dense_rows =
       std::min<int64_t>(1024, round_up(std::max<int64_t>(1, nl_max * m.world / 128), kFusedThreads));
-  // more rows per thread only when <= 256 resident workgroups need them (n = 200k
-  // dense on one GPU: 1024 rows x 196 workgroups 0.66 s vs 1792 x 112 0.69 s)
+  // more rows per thread only to keep every poll one batch (<= 256 publishers in
+  // all) and <= 256 resident workgroups per rank.  n = 200k dense on one GPU:
+  // 1024 rows x 196 workgroups 0.66 s, 1792 x 112 0.69 s, 512 x 391 (two poll
+  // batches) 0.89 s (profiles/r1_dense_rows_ab.txt)
+  if (m.world * ((nl_max + dense_rows - 1) / dense_rows) > 256)
+    dense_rows = std::max(dense_rows, round_up((nl_max * m.world + 255) / 256, kFusedThreads));
   if ((nl_max + dense_rows - 1) / dense_rows > 256) dense_rows = round_up((nl_max + 255) / 256, kFusedThreads);
   if (const char* e = std::getenv("DPSVM_DENSE_ROWS"))  // tests: more publishers (multi-batch polls)
     dense_rows = std::max<int64_t>(kFusedThreads, std::min<int64_t>(3072, atoll(e) / kFusedThreads * kFusedThreads));
