@@ -56,6 +56,30 @@ static void test_shards() {
     }
 }
 
+static void test_geometry() {
+  // headline (60k rows): 512 rows x 118 workgroups on 1 GPU, 15 per rank on 8
+  {
+    const Geometry g1 = make_geometry(60000, dense_rows_min(60000, 1));
+    EXPECT(g1.rows == 512 && g1.groups == 118);
+    const int64_t nl8 = (60000 + 7) / 8;
+    const Geometry g8 = make_geometry(nl8, dense_rows_min(nl8, 8));
+    EXPECT(g8.rows == 512 && g8.groups == 15);
+  }
+  for (int64_t n : {2, 1000, 60000, 200000, 581012, 786432, 2000000})
+    for (int w : {1, 2, 4, 8}) {
+      const int64_t nl = (n + w - 1) / w;
+      const Geometry d = make_geometry(nl, dense_rows_min(nl, w));
+      EXPECT(d.rows % 256 == 0 && d.rows * d.groups >= nl);
+      if (nl <= 256 * 3072) {  // the persistent dense engine's range
+        EXPECT(d.groups <= 256);
+        EXPECT(d.rows <= 3072);
+        if (nl * w <= 256 * 3072) EXPECT(w * d.groups <= 256);  // one poll batch
+      }
+      const Geometry c = make_geometry(nl, 0);  // cache mode: ~one workgroup per CU
+      EXPECT(c.rows % 256 == 0 && c.rows * c.groups >= nl && c.groups <= 256);
+    }
+}
+
 static void test_io() {
   char tmpl[] = "/tmp/dpsvm_unitXXXXXX";
   char* dir = mkdtemp(tmpl);

@@ -9,6 +9,7 @@
 //   - defaults (eps 1e-3, C 1, 150000 iters): svmTrainMain.cpp:60-136
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -235,6 +236,32 @@ inline Shard shard_of(int64_t n, int rank, int world) {
   s.size = base + (rank < rem ? 1 : 0);
   s.offset = rank * base + (rank < rem ? rank : rem);
   return s;
+}
+
+// Workgroup geometry of the fused / persistent engines (rows per workgroup, a
+// multiple of 256 threads; workgroups per rank).  nl_max = largest shard.
+//   cache mode: about `wgs` workgroups (one per CU: the X pass wants every CU);
+//   dense mode: ~128 publishers over all ranks, <= 1024 rows per workgroup, more
+//   rows (12 register rows per thread, <= 3072) only to keep every poll of the
+//   key exchange one batch (world x workgroups <= 256) and <= 256 resident
+//   workgroups per rank (profiles/r1_dense_rows_ab.txt).
+struct Geometry {
+  int64_t rows = 256, groups = 1;
+};
+inline int64_t geo_round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+inline Geometry make_geometry(int64_t nl_max, int64_t rows_min, int64_t wgs = 256) {
+  Geometry g;
+  const int64_t per = (nl_max + wgs - 1) / wgs;
+  g.rows = std::max<int64_t>(256, geo_round_up(per, 256));
+  g.rows = std::max(g.rows, rows_min);
+  g.groups = std::max<int64_t>(1, (nl_max + g.rows - 1) / g.rows);
+  return g;
+}
+inline int64_t dense_rows_min(int64_t nl_max, int world) {
+  int64_t r = std::min<int64_t>(1024, geo_round_up(std::max<int64_t>(1, nl_max * world / 128), 256));
+  if (world * ((nl_max + r - 1) / r) > 256) r = std::max(r, geo_round_up((nl_max * world + 255) / 256, 256));
+  if ((nl_max + r - 1) / r > 256) r = geo_round_up((nl_max + 255) / 256, 256);
+  return r;
 }
 
 }  // namespace dpsvm

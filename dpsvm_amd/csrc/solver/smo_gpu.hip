@@ -491,31 +491,21 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // <= ~256 workgroups (the X pass wants every CU).  Dense mode: the period is
   // set by the all-to-all key exchange, whose cost grows with the number of
   // publishers (world x G): ~128 publishers in all, <= 1024 rows per workgroup
-  // (up to 3072 — 12 register rows per thread — only when 256 resident
-  // workgroups would not cover the shard).  Measured on 60k x 784, 1 GPU:
+  // (more only to keep one poll batch / <= 256 resident workgroups:
+  // dense_rows_min, common.hpp).  Measured on 60k x 784, 1 GPU:
   // 235 workgroups 5.8-6.2 us per iteration, 118 -> 5.2 us (profiles/README.md).
+  int64_t wgs = 256;  // cache mode: one workgroup per CU
+  if (const char* e = std::getenv("DPSVM_CACHE_WGS")) wgs = std::max<int64_t>(1, atoll(e));
   auto geometry = [&](int64_t rows_min) {
-    int64_t wgs = 256;  // cache mode: one workgroup per CU
-    if (const char* e = std::getenv("DPSVM_CACHE_WGS")) wgs = std::max<int64_t>(1, atoll(e));
-    const int64_t per = (nl_max + wgs - 1) / wgs;
-    int64_t rb = std::max<int64_t>(kFusedThreads, (per + kFusedThreads - 1) / kFusedThreads * kFusedThreads);
-    rb = std::max(rb, rows_min);
+    Geometry g = make_geometry(nl_max, rows_min, wgs);
     if (const char* e = std::getenv("DPSVM_FUSED_ROWS")) {  // override: rows per workgroup
       const int64_t r = atoll(e) / kFusedThreads * kFusedThreads;
-      if (r > rb) rb = r;
+      if (r > g.rows) g = make_geometry(nl_max, r, wgs);
     }
-    return std::pair<int64_t, int64_t>(rb, std::max<int64_t>(1, (nl_max + rb - 1) / rb));
+    return std::pair<int64_t, int64_t>(g.rows, g.groups);
   };
   const auto geo_cache = geometry(0);
-  int64_t dense_rows =
-      std::min<int64_t>(1024, round_up(std::max<int64_t>(1, nl_max * m.world / 128), kFusedThreads));
-  // more rows per thread only to keep every poll one batch (<= 256 publishers in
-  // all) and <= 256 resident workgroups per rank.  n = 200k dense on one GPU:
-  // 1024 rows x 196 workgroups 0.66 s, 1792 x 112 0.69 s, 512 x 391 (two poll
-  // batches) 0.89 s (profiles/r1_dense_rows_ab.txt)
-  if (m.world * ((nl_max + dense_rows - 1) / dense_rows) > 256)
-    dense_rows = std::max(dense_rows, round_up((nl_max * m.world + 255) / 256, kFusedThreads));
-  if ((nl_max + dense_rows - 1) / dense_rows > 256) dense_rows = round_up((nl_max + 255) / 256, kFusedThreads);
+  int64_t dense_rows = dense_rows_min(nl_max, m.world);
   if (const char* e = std::getenv("DPSVM_DENSE_ROWS"))  // tests: more publishers (multi-batch polls)
     dense_rows = std::max<int64_t>(kFusedThreads, std::min<int64_t>(3072, atoll(e) / kFusedThreads * kFusedThreads));
   auto geo_dense = geometry(dense_rows);
