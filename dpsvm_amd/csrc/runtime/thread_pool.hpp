@@ -10,12 +10,42 @@
 #include <thread>
 #include <vector>
 
+#if defined(__x86_64__) || defined(__i386__)
+#include <xmmintrin.h>
+#endif
+
 namespace dpsvm {
+
+// Flush-to-zero + denormals-are-zero on this thread's SSE unit; returns the
+// previous control word (restore with set_fp_control).  Late SMO iterations
+// multiply tiny alpha steps by kernel values: with denormal results every
+// such multiply takes a microcode assist (x86), ~10x the time of the update.
+inline unsigned flush_denormals() {
+#if defined(__x86_64__) || defined(__i386__)
+  const unsigned old = _mm_getcsr();
+  _mm_setcsr(old | 0x8040u);  // FTZ (bit 15) | DAZ (bit 6)
+  return old;
+#else
+  return 0u;
+#endif
+}
+inline void set_fp_control(unsigned v) {
+#if defined(__x86_64__) || defined(__i386__)
+  _mm_setcsr(v);
+#else
+  (void)v;
+#endif
+}
 
 class ThreadPool {
  public:
-  explicit ThreadPool(int threads) : nthreads_(threads < 1 ? 1 : threads) {
-    for (int t = 1; t < nthreads_; ++t) workers_.emplace_back([this, t] { loop(t); });
+  // ftz: workers run with flush-to-zero / denormals-are-zero
+  explicit ThreadPool(int threads, bool ftz = false) : nthreads_(threads < 1 ? 1 : threads) {
+    for (int t = 1; t < nthreads_; ++t)
+      workers_.emplace_back([this, t, ftz] {
+        if (ftz) flush_denormals();
+        loop(t);
+      });
   }
   ~ThreadPool() {
     {
