@@ -22,6 +22,8 @@
 #include "dpsvm/common.hpp"
 #include "dpsvm/solver.hpp"
 #include "../runtime/thread_pool.hpp"
+#include <unistd.h>
+
 #include "../runtime/timer.hpp"
 #include "../runtime/trace.hpp"
 
@@ -144,10 +146,16 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
     }
   }
 
-  // cache sizing: explicit lines / MiB, else up to 1 GiB per rank (CPU path)
+  // cache sizing: explicit lines / MiB, else up to a quarter of the machine's
+  // RAM per process (all n rows when they fit: each kernel row computed once;
+  // adult-shape needs 4.2 GB — with 1 GiB the LRU thrashed, ~2 misses/iteration)
   int64_t lines = p.cache_lines;
   if (lines <= 0) {
-    double mb = p.cache_mb > 0 ? p.cache_mb : 1024.0;
+    double mb = p.cache_mb;
+    if (mb <= 0) {
+      const double phys = (double)sysconf(_SC_PHYS_PAGES) * (double)sysconf(_SC_PAGESIZE);
+      mb = phys > 0 ? 0.25 * phys / (1024.0 * 1024.0) / std::max(1, world) : 1024.0;
+    }
     lines = (int64_t)(mb * 1024.0 * 1024.0 / (4.0 * std::max<int64_t>(nl, 1)));
   }
   lines = std::max<int64_t>(2, std::min<int64_t>(lines, n));
@@ -176,21 +184,29 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
   auto t0 = Clock::now();
   int64_t iter = iter0;
   int status = 0;
+  // per-thread selection keys of rows [b, e) (I-set classification + argmin /
+  // argmax, svmTrain.cu:41-95), optionally after the f update of the same rows:
+  // one pass and one pool dispatch per iteration
+  auto select_rows = [&](int t, int64_t b, int64_t e) {
+    uint64_t kh = kKeyNone, kl = kKeyNone;
+    for (int64_t j = b; j < e; ++j) {
+      const int64_t g = off + j;
+      const float a = alpha[g], yj = Y[g], fj = f[j];
+      if (in_up(a, yj, C)) kh = std::min(kh, make_key(fj, (uint32_t)g));
+      if (in_low(a, yj, C)) kl = std::min(kl, make_key(-fj, (uint32_t)g));
+    }
+    th_hi[t] = kh;
+    th_lo[t] = kl;
+  };
+  bool keys_ready = false;  // th_hi / th_lo hold this iteration's keys
   while (true) {
-    // ---- local selection (fused I-set classification + argmin/argmax) ----
-    std::fill(th_hi.begin(), th_hi.end(), kKeyNone);
-    std::fill(th_lo.begin(), th_lo.end(), kKeyNone);
-    pool.run(nl, [&](int t, int64_t b, int64_t e) {
-      uint64_t kh = kKeyNone, kl = kKeyNone;
-      for (int64_t j = b; j < e; ++j) {
-        const int64_t g = off + j;
-        const float a = alpha[g], yj = Y[g], fj = f[j];
-        if (in_up(a, yj, C)) kh = std::min(kh, make_key(fj, (uint32_t)g));
-        if (in_low(a, yj, C)) kl = std::min(kl, make_key(-fj, (uint32_t)g));
-      }
-      th_hi[t] = kh;
-      th_lo[t] = kl;
-    });
+    // ---- local selection (unless the previous f update pass produced it) ----
+    if (!keys_ready) {
+      std::fill(th_hi.begin(), th_hi.end(), kKeyNone);
+      std::fill(th_lo.begin(), th_lo.end(), kKeyNone);
+      pool.run(nl, select_rows);
+    }
+    keys_ready = false;
     uint64_t keys[2] = {*std::min_element(th_hi.begin(), th_hi.end()),
                         *std::min_element(th_lo.begin(), th_lo.end())};
     if (world > 1) comm->allreduce_min_u64(keys, 2, nullptr);
@@ -233,8 +249,11 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
       klo = ptr;  // capacity >= 2 and the hi line is MRU -> never the victim here
     }
     if (khi || klo) {
+      // f update fused with the next iteration's selection over the same rows
       const float ch = u.c_hi, cl = u.c_lo;
-      pool.run(nl, [&](int, int64_t b, int64_t e) {
+      std::fill(th_hi.begin(), th_hi.end(), kKeyNone);
+      std::fill(th_lo.begin(), th_lo.end(), kKeyNone);
+      pool.run(nl, [&](int t, int64_t b, int64_t e) {
         for (int64_t j = b; j < e; ++j) {
           float delta;
           if (khi && klo) delta = (ch * khi[j]) + (cl * klo[j]);
@@ -242,10 +261,15 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
           else delta = cl * klo[j];
           f[j] += delta;
         }
+        select_rows(t, b, e);
       });
+      keys_ready = true;
     }
     ++iter;
-    if (fault_iter >= 0 && iter == fault_iter && nl > 0) f[0] = std::nanf("");  // DPSVM_FAULT
+    if (fault_iter >= 0 && iter == fault_iter && nl > 0) {  // DPSVM_FAULT
+      f[0] = std::nanf("");
+      keys_ready = false;
+    }
     const bool open = gap_open(b_hi, b_lo, p.eps);
     if (progress && p.log_every > 0 && iter % p.log_every == 0)
       progress(Progress{iter, b_hi, b_lo, secs_since(t0), res.cache_hits, res.cache_misses});
