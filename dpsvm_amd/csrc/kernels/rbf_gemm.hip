@@ -38,21 +38,47 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   // sym (STORE, B == A, N == M): only tiles on/above the diagonal are computed;
   // each off-diagonal tile also writes its transpose.  K(i,j) and K(j,i) are
   // bit-identical (same products in the same k order, commutative norm sum).
-  if (EPI == EPI_STORE && sym && blockIdx.y < blockIdx.x) return;
+  // Tile of this workgroup.  STORE: XCD-aware order — workgroups are dealt
+  // round-robin over the 8 XCDs (linear id L runs on XCD L % 8), so the tile
+  // sequence is cut in chunks of 64 and XCD x takes chunks x, x + 8, ...; a
+  // chunk is an 8 x 8 block of tiles (groups of 8 tile-rows, column-major), so
+  // an XCD's consecutive tiles share B panels and re-read A panels from its
+  // L2, while every XCD still sees the whole matrix (balanced under the
+  // symmetric mode's skipped lower triangle).  A bijection on the grid; the
+  // tile math is unchanged: bit-identical output.
+  int64_t tx = blockIdx.x, ty = blockIdx.y;
+  if (EPI == EPI_STORE) {
+    const int64_t tm = gridDim.x, tn = gridDim.y, total = tm * tn;
+    const int64_t L = blockIdx.x + (int64_t)blockIdx.y * tm;
+    constexpr int64_t CH = 64;
+    const int64_t full = total / (8 * CH) * (8 * CH);
+    int64_t T = L;  // the tail past the last whole round keeps its order
+    if (L < full) {
+      const int64_t xcd = L % 8, local = L / 8;
+      T = ((local / CH) * 8 + xcd) * CH + local % CH;
+    }
+    constexpr int64_t GM = 8;
+    const int64_t first_m = (T / (GM * tn)) * GM;
+    const int64_t gm = min(GM, tm - first_m);
+    const int64_t in = T - first_m * tn;  // position inside the group (column-major)
+    tx = first_m + in % gm;
+    ty = in / gm;
+  }
+  if (EPI == EPI_STORE && sym && ty < tx) return;
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
   __shared__ float red[2][BM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t m0 = tx * BM;
   const int64_t ntiles_total = (N + BN - 1) / BN;
   int64_t nt_begin, nt_end;
   if (EPI == EPI_STORE) {
-    nt_begin = blockIdx.y;
+    nt_begin = ty;
     nt_end = nt_begin + 1;
   } else {
-    nt_begin = (int64_t)blockIdx.y * n_tiles_per_split;
+    nt_begin = ty * n_tiles_per_split;
     nt_end = nt_begin + n_tiles_per_split;
     if (nt_end > ntiles_total) nt_end = ntiles_total;
   }
@@ -144,7 +170,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
         }
       }
     }
-    if (EPI == EPI_STORE && sym && blockIdx.y != blockIdx.x) {
+    if (EPI == EPI_STORE && sym && ty != tx) {
       // transposed tile: lane holds 4 consecutive rows per group -> 16-B stores
       // out[col][row .. row+3] (each store instruction: 32 rows x 32 B)
 #pragma unroll
@@ -202,7 +228,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     if (tid < BM) {
       const int64_t row = m0 + tid;
       // out = partial [splits][ldo], ldo = M_pad
-      out[(int64_t)blockIdx.y * ldo + row] = red[0][tid] + red[1][tid];
+      out[ty * ldo + row] = red[0][tid] + red[1][tid];
     }
   }
 }
