@@ -2,6 +2,7 @@
 import os
 
 import numpy as np
+import pytest
 
 from conftest import run
 from dpsvm_amd.utils import datasets
@@ -89,3 +90,32 @@ def test_svmtrain_synthetic_and_checkpoint_resume(tmp_path, bin_dir):
     assert r.returncode == 0, r.stderr
     assert f"Converged at iteration number: {full_it}" in r.stdout
     assert open(m).read() == full_model
+
+
+@pytest.mark.gpu
+def test_svmtrain_gpu_matches_cpu_and_svmtest(tmp_path, bin_dir):
+    """svmTrain on the GPU (default device): reference stdout lines, the same
+    SMO trajectory as --cpu within fp32 tolerance, model read back by svmTest."""
+    p, X, y = _data(tmp_path, n=2000)
+    outs = {}
+    for dev in ("gpu", "cpu"):
+        m = str(tmp_path / f"model_{dev}.txt")
+        js = str(tmp_path / f"metrics_{dev}.json")
+        cmd = [os.path.join(bin_dir, "svmTrain"), "-a", "5", "-x", "2000", "-f", p, "-c", "2", "-g", "0.4",
+               "-e", "0.001", "-m", m, "--metrics-json", js] + (["--cpu"] if dev == "cpu" else [])
+        r = run(cmd)
+        assert r.returncode == 0, r.stderr
+        for line in ("SETUP DONE", "Converged at iteration number:", "Training accuracy:"):
+            assert line in r.stdout, (line, r.stdout)
+        import json
+
+        tr_acc = float([l for l in r.stdout.split("\n") if l.startswith("Training accuracy:")][-1].split()[-1])
+        outs[dev] = (json.load(open(js)), m, tr_acc)
+    g, c = outs["gpu"][0], outs["cpu"][0]
+    assert g["converged"] and c["converged"]
+    assert abs(g["iterations"] - c["iterations"]) <= max(10, c["iterations"] // 50)
+    assert abs(g["n_sv"] - c["n_sv"]) <= max(3, c["n_sv"] // 100)
+    r = run([os.path.join(bin_dir, "svmTest"), "-a", "5", "-x", "2000", "-f", p, "-m", outs["gpu"][1]])
+    assert r.returncode == 0, r.stderr
+    acc = float([l for l in r.stdout.split("\n") if "accuracy" in l.lower()][-1].split()[-1])
+    assert abs(acc - outs["gpu"][2]) < 2e-3  # the predictor reproduces the trainer's accuracy
