@@ -108,7 +108,16 @@ def main(argv=None) -> int:
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
                     exchange=a.exchange, persist=a.persist, persist_block=a.persist_block)
     params = cfg.to_native(X.shape[1])
-    comm = make_comm(ctx, a.comm)
+    try:
+        comm = make_comm(ctx, a.comm)
+    except Exception as e:  # noqa: BLE001
+        if a.comm != "auto" or n_ranks == 1:
+            raise
+        # RCCL bootstrap failed: the host (gloo) communicator still carries the
+        # setup collectives; the per-iteration exchange is in-kernel either way
+        if ctx.rank == 0:
+            print(f"[bench] RCCL communicator unavailable ({e}); using gloo", file=sys.stderr)
+        comm = make_comm(ctx, "gloo")
     if a.comm == "rccl" and n_ranks == 1:
         params.force_collectives = True  # one-rank RCCL: exercise the collective + graph path
 
