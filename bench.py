@@ -68,7 +68,7 @@ def parse(argv=None):
                          "when its self test passes, else the communicator all-reduce)")
     ap.add_argument("--device", default="auto", help="auto | cuda | cpu")
     ap.add_argument("--persist", default="auto", choices=["auto", "off", "on"],
-                    help="dense-mode engine: persistent kernel (auto/on) or one launch per iteration (off)")
+                    help="iteration engine: persistent kernel (auto/on; dense and cache mode) or one launch per iteration (off)")
     ap.add_argument("--persist-block", type=int, default=2048)
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--json-out", default=None)
