@@ -203,9 +203,15 @@ inline std::string json_escape(const std::string& s) {
   return r;
 }
 
+// per-phase wall times and the engine actually used
+struct RunExtras {
+  double t_load = 0.0, t_accuracy = 0.0, t_model_write = 0.0;
+  std::string engine = "cpu", exchange = "none";
+};
+
 inline void write_metrics(const std::string& path, const Options& o, const SolveResult& r, int64_t n, int d,
                           int64_t nsv, double acc, const std::string& backend, const std::string& device,
-                          double t_load) {
+                          const RunExtras& x) {
   FILE* fp = fopen(path.c_str(), "w");
   if (!fp) {
     std::cerr << "cannot write metrics " << path << "\n";
@@ -216,12 +222,15 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           "\"gamma\": %g, \"eps\": %g, \"clip\": \"%s\", \"iterations\": %lld, \"status\": %d, "
           "\"converged\": %s, \"b\": %.9g, \"b_hi\": %.9g, \"b_lo\": %.9g, \"n_sv\": %lld, "
           "\"train_accuracy\": %.9g, \"t_load_s\": %.6f, \"t_setup_s\": %.6f, \"t_solve_s\": %.6f, "
+          "\"t_gram_s\": %.6f, \"t_accuracy_s\": %.6f, \"t_model_write_s\": %.6f, \"engine\": \"%s\", "
+          "\"exchange\": \"%s\", "
           "\"iters_per_s\": %.3f, \"cache_lines\": %lld, \"cache_hits\": %lld, \"cache_misses\": %lld, "
           "\"rows_computed\": %lld, \"x_passes\": %lld, \"spec_rows\": %lld, \"data\": \"%s\"}\n",
           backend.c_str(), json_escape(device).c_str(), r.world, (long long)n, d, o.p.C, o.p.gamma, o.p.eps,
           o.p.clip == ClipMode::Box ? "box" : "independent", (long long)r.iters, r.status,
-          r.converged() ? "true" : "false", r.b, r.b_hi, r.b_lo, (long long)nsv, acc, t_load, r.t_setup,
-          r.t_solve, r.t_solve > 0 ? r.iters / r.t_solve : 0.0, (long long)r.cache_lines,
+          r.converged() ? "true" : "false", r.b, r.b_hi, r.b_lo, (long long)nsv, acc, x.t_load, r.t_setup,
+          r.t_solve, r.t_gram, x.t_accuracy, x.t_model_write, x.engine.c_str(), x.exchange.c_str(),
+          r.t_solve > 0 ? r.iters / r.t_solve : 0.0, (long long)r.cache_lines,
           (long long)r.cache_hits, (long long)r.cache_misses, (long long)r.rows_computed,
           (long long)r.x_passes, (long long)r.spec_rows,
           json_escape(o.synthetic.empty() ? o.file : "synthetic:" + o.synthetic).c_str());

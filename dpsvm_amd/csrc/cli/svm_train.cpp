@@ -19,6 +19,8 @@ int main(int argc, char** argv) {
     const double tl0 = cli::now_s();
     Dataset ds = cli::load_data(o);
     const double t_load = cli::now_s() - tl0;
+    cli::RunExtras extras;
+    extras.t_load = t_load;
     const int64_t n = ds.n;
     const int d = ds.d;
     int world = o.ranks > 0 ? o.ranks : (o.cpu ? 1 : o.gpus);
@@ -87,8 +89,14 @@ int main(int argc, char** argv) {
                     << (info.cache_lines >= n ? " = whole Gram shard resident" : " LRU") << ")\n";
           std::cout << "SETUP DONE\n";
         }
+        if (r == 0) {
+          extras.engine = info.iteration;
+          extras.exchange = info.exchange;
+        }
         results[r] = solver.solve(resume.get(), prog);
+        const double ta0 = cli::now_s();
         if (!o.skip_accuracy) accs[r] = solver.train_accuracy(results[r]);
+        if (r == 0) extras.t_accuracy = cli::now_s() - ta0;
       } catch (...) {
         errs[r] = std::current_exception();
         if (world > 1) comms[r]->abort();
@@ -112,17 +120,21 @@ int main(int argc, char** argv) {
     double acc = accs[0];
     if (!o.skip_accuracy) {
       if (acc < 0) {
+        const double ta0 = cli::now_s();
         Model mdl = make_model(ds, r0.alpha, r0.b, o.p.gamma);
         auto dec = decision_cpu(mdl, ds.x.data(), n, d);
         acc = accuracy_from_decision(dec, ds.y.data(), n);
+        extras.t_accuracy = cli::now_s() - ta0;
       }
       std::cout << "Training accuracy: " << acc << "\n";
     }
+    const double tw0 = cli::now_s();
     Model mdl = make_model(ds, r0.alpha, r0.b, o.p.gamma);
     write_model(o.model, mdl, o.precision, o.legacy_model);
+    extras.t_model_write = cli::now_s() - tw0;
     std::cout << "Training model has been saved to the file " << o.model << "\n";
     if (!o.metrics_json.empty())
-      cli::write_metrics(o.metrics_json, o, r0, n, d, nsv, acc, backend, devname, t_load);
+      cli::write_metrics(o.metrics_json, o, r0, n, d, nsv, acc, backend, devname, extras);
     return 0;
   } catch (const std::exception& e) {
     std::cerr << "svmTrain: " << e.what() << "\n";
