@@ -300,11 +300,18 @@ __global__ __launch_bounds__(64) void xch_ping_kernel(uint64_t* const* peers, in
     if (lane == 0) *ok = 1;
     return;
   }
-  if (lane < world) xch_store<true>(peers[lane] + ping_off + rank, ((uint64_t)tag << 32) | (uint32_t)rank);
+  // the scope the exchange itself uses: system across ranks, agent for one rank
+  const bool sys = world > 1;
+  const uint64_t v = ((uint64_t)tag << 32) | (uint32_t)rank;
+  if (lane < world) {
+    if (sys) xch_store<true>(peers[lane] + ping_off + rank, v);
+    else xch_store<false>(peers[lane] + ping_off + rank, v);
+  }
   const uint64_t* mine = peers[rank] + ping_off;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
-    const bool good = lane >= world || (uint32_t)(xch_load<true>(mine + lane) >> 32) == tag;
+    const uint64_t got = lane >= world ? 0 : (sys ? xch_load<true>(mine + lane) : xch_load<false>(mine + lane));
+    const bool good = lane >= world || (uint32_t)(got >> 32) == tag;
     if (__all(good)) {
       if (lane == 0) *ok = 1;
       return;
