@@ -9,9 +9,10 @@
 //
 // Iteration t in workgroup b (identical arithmetic to smo_fused.hip, so the
 // two paths are bit-identical):
-//   1. every thread polls its share of the publications tagged t (all ranks'
-//      workgroups; two load rounds in flight): the minima, with the alphas of
-//      the rows behind them, combined through LDS (barrier 1);
+//   1. wave 0 polls the publications tagged t of every workgroup of every rank
+//      (each lane watches kB of them, all loads of a round in flight together,
+//      a short sleep between rounds): the minima, with the alphas of the rows
+//      behind them, broadcast through LDS (barrier 1);
 //   2. pair (i_hi, i_lo), eta from the two sample rows, alpha update — the
 //      pair's current alphas arrive with the keys from their owners'
 //      registers, so alpha memory is never read during the run (a plain or
