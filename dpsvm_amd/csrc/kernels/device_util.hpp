@@ -13,13 +13,6 @@ namespace dev {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  lo = __shfl_xor(lo, m, 64);
-  hi = __shfl_xor(hi, m, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // ---- full-wave reductions on DPP (no LDS round trips) ----
 // Within each 16-lane row: quad_perm xor 1, quad_perm xor 2, row_half_mirror
 // (i <-> 7-i) and row_mirror (i <-> 15-i) leave every lane of the row holding
@@ -143,21 +136,6 @@ __device__ __forceinline__ void block_min2_u64(uint64_t& a, uint64_t& b, uint64_
   a = ra;
   b = rb;
   __syncthreads();
-}
-
-// Deterministic block sum (fixed tree: wave shuffles then waves in order).
-template <int THREADS>
-__device__ __forceinline__ float block_sum(float v, float* scratch) {
-  constexpr int W = THREADS / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  v = wave_sum(v);
-  if (lane == 0) scratch[wave] = v;
-  __syncthreads();
-  float r = 0.f;
-#pragma unroll
-  for (int w = 0; w < W; ++w) r += scratch[w];
-  __syncthreads();
-  return r;
 }
 
 __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {

@@ -233,21 +233,6 @@ __device__ __forceinline__ bool xch_poll_wave_t(const SmoArgs& a, const uint64_t
   return true;
 }
 
-template <bool kSys>
-__device__ __forceinline__ bool xch_poll_wave_s(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
-                                                XKeys& out, int lane) {
-  const int E = a.xworld * a.fused_G;  // uniform
-  if (E <= 64) return xch_poll_wave_t<kSys, 1>(a, mine_buf, par, tag, out, lane);
-  if (E <= 128) return xch_poll_wave_t<kSys, 2>(a, mine_buf, par, tag, out, lane);
-  return xch_poll_wave_t<kSys, 4>(a, mine_buf, par, tag, out, lane);
-}
-
-__device__ __forceinline__ bool xch_poll_wave(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
-                                              XKeys& out, int lane) {
-  return a.xworld > 1 ? xch_poll_wave_s<true>(a, mine_buf, par, tag, out, lane)
-                      : xch_poll_wave_s<false>(a, mine_buf, par, tag, out, lane);
-}
-
 // mine_buf: this rank's receive buffer (a.xpeer[a.xrank], loaded once)
 template <bool kPipe = false>
 __device__ __forceinline__ bool xch_poll(const SmoArgs& a, const uint64_t* mine_buf, int par, uint32_t tag,
