@@ -1,5 +1,5 @@
-"""Worker for test_peer_exchange_two_processes_one_gpu (launched by
-torch.distributed.run): train with the in-kernel peer exchange, write the
+"""Worker for the peer-exchange multi-process GPU tests (two or four ranks,
+launched by torch.distributed.run): train with the in-kernel peer exchange, write the
 result digest to <out>.rank<r>.json."""
 import hashlib
 import json

@@ -352,6 +352,34 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
         assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
 
 
+@pytest.mark.parametrize("engine", ["persistent", "persistent-cache"])
+def test_peer_exchange_four_processes_one_gpu(tmp_path, engine):
+    """Four ranks as four processes sharing the GPU: every workgroup pushes
+    its publication to four receive buffers and polls 4 x G of them; the
+    result is bit-identical to one rank (rehearsal of the 4-GPU run)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+
+    n, world = 8000, 4
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="30", DPSVM_VERIFY="1")
+    out = tmp_path / "mp4"
+    port = 29620 + ["persistent", "persistent-cache"].index(engine)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(f"{out}.rank{k}.json")) for k in range(world)]
+    X, y = synthetic("covtype", n=n, seed=2)
+    extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
+    ref = SVC(C=4.0, gamma=0.5, eps=1e-3, device="cuda", **extra).fit(X, y)
+    sha = __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
+    for k in range(world):
+        assert res[k]["exchange"] == "peer" and res[k]["exchange_mem"] == "uncached"
+        assert res[k]["iteration"] == ("persistent-cache" if engine == "persistent-cache" else "persistent-dense")
+        assert res[k]["iters"] == ref.n_iter_ and res[k]["alpha_sha"] == sha
+
+
 def test_bench_two_processes_exchange_fallback(tmp_path):
     """bench.py with 2 ranks: a peer exchange that gives up (1 us poll bound)
     makes every rank fail the warmup run the same way; the bench falls back
