@@ -64,7 +64,7 @@ def _gloo_worker(rank, world, port, q):
     shutdown(ctx)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the rank count of one MI355X node
 def test_gloo_multiprocess_identical(world):
     X, y = synthetic("adult", n=900, seed=4)
     ref = _fit_single(X, y, C=1.0, gamma=0.1, eps=1e-3)
