@@ -26,3 +26,24 @@ def test_graft_entry_build():
     import __graft_entry__ as ge
 
     ge.build()
+
+
+def test_bench_multirank_launch_contract():
+    """The driver's N > 1 launch (torch.distributed.run, one process per rank,
+    127.0.0.1 rendezvous), rehearsed on the CPU path with 4 gloo ranks: exactly
+    one JSON line (rank 0), n_gpus / parallelism follow the rank count."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+             "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+             "--gpus", "4", "--device", "cpu", "--samples", "1500", "--steps", "1", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.strip().split("\n") if l.startswith("{")]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4" and out["converged"]
+    assert out["steps"] == 1 and out["warmup"] == 1 and out["value"] > 0
