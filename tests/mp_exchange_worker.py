@@ -1,4 +1,4 @@
-"""Worker for the peer-exchange multi-process GPU tests (two or four ranks,
+"""Worker for the peer-exchange multi-process GPU tests (two, four or eight ranks,
 launched by torch.distributed.run): train with the in-kernel peer exchange, write the
 result digest to <out>.rank<r>.json."""
 import hashlib

@@ -352,18 +352,20 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
         assert res[k]["alpha_sha"] == __import__("hashlib").sha256(ref.alpha_.tobytes()).hexdigest()
 
 
+@pytest.mark.parametrize("world", [4, 8])
 @pytest.mark.parametrize("engine", ["persistent", "persistent-cache"])
-def test_peer_exchange_four_processes_one_gpu(tmp_path, engine):
-    """Four ranks as four processes sharing the GPU: every workgroup pushes
-    its publication to four receive buffers and polls 4 x G of them; the
-    result is bit-identical to one rank (rehearsal of the 4-GPU run)."""
+def test_peer_exchange_four_processes_one_gpu(tmp_path, engine, world):
+    """Four (eight) ranks as four (eight) processes sharing the GPU: every
+    workgroup pushes its publication to `world` receive buffers and polls
+    world x G of them; the result is bit-identical to one rank (rehearsal of
+    the 4- and 8-GPU runs: same rank count and shard geometry)."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     import subprocess
 
-    n, world = 8000, 4
+    n = 8000
     env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="30", DPSVM_VERIFY="1")
-    out = tmp_path / "mp4"
-    port = 29620 + ["persistent", "persistent-cache"].index(engine)
+    out = tmp_path / f"mp{world}"
+    port = 29620 + ["persistent", "persistent-cache"].index(engine) + (4 if world == 8 else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n)]
