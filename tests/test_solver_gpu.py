@@ -398,3 +398,37 @@ def test_bench_two_processes_exchange_fallback(tmp_path):
     out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
     assert out["exchange"] == "allreduce" and out["converged"] and out["n_gpus"] == 2
     assert "falling back" in r.stderr
+
+
+_SHARED = os.environ.get("DPSVM_TEST_SHARED_GPU") == "1"
+
+
+@pytest.mark.skipif(not _SHARED and torch.cuda.device_count() < 2,
+                    reason="needs >= 2 GPUs (DPSVM_TEST_SHARED_GPU=1 rehearses it on one)")
+def test_bench_multi_gpu_rccl_matches_one_gpu(tmp_path):
+    """bench.py as one process per GPU (RCCL communicator over xGMI, in-kernel
+    peer exchange between devices) on up to 8 GPUs: same iteration count, b and
+    SV count as the one-GPU solve.  DPSVM_TEST_SHARED_GPU=1 runs the same ranks
+    on one GPU over gloo (RCCL refuses two ranks on one device)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+
+    world = 2 if _SHARED else min(torch.cuda.device_count(), 8)
+    env = dict(os.environ, DPSVM_XCH_TIMEOUT_S="30")
+    extra = ["--comm", "gloo"] if _SHARED else ["--comm", "rccl"]
+    if _SHARED:
+        env["DPSVM_FORCE_DEVICE"] = "0"
+    n = 8000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", "29641", os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--samples", str(n), "--steps", "1", "--warmup", "1", "--no-accuracy"] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
+    assert out["n_gpus"] == world and out["converged"] and out["exchange"] == "peer"
+    assert out["comm"] != "local" and out["config"]["parallelism"] == f"dp{world}"
+    X, y = synthetic("mnist", n=n, d=784, seed=0)
+    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
+    assert out["iterations"] == ref.n_iter_
+    assert out["b"] == ref.b_
+    assert out["n_sv"] == int((ref.alpha_ > 0).sum())
