@@ -110,7 +110,10 @@ def _link(out: Path, objs: list[Path], shared: bool, flags: list[str]) -> None:
     if shared:
         cmd += ["-shared"]
     cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lpthread", f"-Wl,-rpath,{ROCM / 'lib'}"]
-    cmd += [x for x in flags if x.startswith("-Xarch_host") or x.startswith("-fsanitize")]
+    # sanitizer runtimes: each -fsanitize= stays paired with the -Xarch_host before it
+    for i, x in enumerate(flags[:-1]):
+        if x == "-Xarch_host" and flags[i + 1].startswith("-fsanitize"):
+            cmd += [x, flags[i + 1]]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {out}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
