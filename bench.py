@@ -14,7 +14,12 @@ reference's untimed setup, svmTrainMain.cpp:194-202) happen once, before.
 W untimed warmup runs, then K timed runs bracketed by barrier + device sync;
 the per-run time is the MAX over ranks.  Data: synthetic MNIST-shape (no
 dataset or network on the box), identical on every rank (seeded).
-Strong scaling: the problem is fixed, ranks split the rows.
+Strong scaling: the problem is fixed.  Ranks split the rows (dp_policy
+"shard"), or — the auto policy when the whole Gram fits one GPU — every rank
+solves the whole problem (dp_policy "replicate": the SMO iteration is a latency
+chain and sharding adds a cross-device hop to each of its ~10^5 iterations);
+then one untimed sharded solve runs first and its time, iterations and b are
+reported as "shard_check" (docs/DESIGN.md, Multi-GPU).
 """
 from __future__ import annotations
 
@@ -70,6 +75,19 @@ def parse(argv=None):
     ap.add_argument("--persist", default="auto", choices=["auto", "off", "on"],
                     help="iteration engine: persistent kernel (auto/on; dense and cache mode) or one launch per iteration (off)")
     ap.add_argument("--persist-block", type=int, default=2048)
+    ap.add_argument("--dp", default="auto", choices=["auto", "shard", "replicate"],
+                    help="data parallelism at N > 1: shard the rows, or every rank solves the whole problem "
+                         "(auto: replicate when the whole Gram fits one GPU, docs/DESIGN.md)")
+    ap.add_argument("--shard-check", default="auto", choices=["auto", "off"],
+                    help="N > 1 with a replicated timed solve: one untimed sharded solve first (cross-device "
+                         "exchange evidence: its time, iterations and b go into the JSON line)")
+    ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
+    ap.add_argument("--cache-groups", type=int, default=256)
+    ap.add_argument("--force-cache", action="store_true")
+    ap.add_argument("--xch-poll-batch", type=int, default=0)
+    ap.add_argument("--xch-mem", default="auto", choices=["auto", "uncached", "coarse"])
+    ap.add_argument("--xch-timeout", type=float, default=None,
+                    help="give-up bound of one in-kernel exchange poll (default 30 s at N > 1, else 120 s)")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
@@ -91,14 +109,21 @@ def main(argv=None) -> int:
     from dpsvm_amd.parallel import init_distributed, make_comm, shutdown
     from dpsvm_amd.utils.datasets import synthetic
 
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        # cross-rank alpha digest after every run (one 16-byte all-reduce): a
-        # diverged run fails loudly instead of reporting a time
-        os.environ.setdefault("DPSVM_VERIFY", "ranks")
-        os.environ.setdefault("DPSVM_XCH_TIMEOUT_S", "30")
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    # (N > 1: the solver checks a cross-rank alpha digest after every run, so a
+    # diverged run fails loudly instead of reporting a time)
     C = load()
     ctx = init_distributed(device=a.device)
     on_gpu = ctx.device.startswith("cuda")
+
+    def barrier():
+        if ctx.world > 1:
+            dist.barrier()
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     if ctx.world != a.gpus and ctx.rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
     n_ranks = ctx.world
@@ -106,28 +131,17 @@ def main(argv=None) -> int:
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
     cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines,
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
-                    exchange=a.exchange, persist=a.persist, persist_block=a.persist_block)
+                    exchange=a.exchange, persist=a.persist, persist_block=a.persist_block, dp=a.dp,
+                    rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
+                    xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem,
+                    xch_timeout_s=a.xch_timeout if a.xch_timeout is not None else (30.0 if multi else 120.0))
     params = cfg.to_native(X.shape[1])
-    try:
-        comm = make_comm(ctx, a.comm)
-    except Exception as e:  # noqa: BLE001
-        if a.comm != "auto" or n_ranks == 1:
-            raise
-        # RCCL bootstrap failed: the host (gloo) communicator still carries the
-        # setup collectives; the per-iteration exchange is in-kernel either way
-        if ctx.rank == 0:
-            print(f"[bench] RCCL communicator unavailable ({e}); using gloo", file=sys.stderr)
-        comm = make_comm(ctx, "gloo")
+    # auto: RCCL, or gloo on EVERY rank when the RCCL bootstrap fails on any
+    # rank (agreed over the host group, dpsvm_amd.parallel.make_comm); the
+    # per-iteration exchange is in-kernel either way
+    comm = make_comm(ctx, a.comm)
     if a.comm == "rccl" and n_ranks == 1:
         params.force_collectives = True  # one-rank RCCL: exercise the collective + graph path
-
-    def barrier():
-        if n_ranks > 1:
-            dist.barrier()
-
-    def sync():
-        if on_gpu:
-            torch.cuda.synchronize()
 
     if on_gpu:
         solver = C.GpuSolver(params, comm, ctx.local_rank)
@@ -151,6 +165,36 @@ def main(argv=None) -> int:
     else:
         info = {"device_name": "cpu", "x_replicated": True, "cache_lines": 0}
         run = lambda: C.solve_cpu(X, y, params, comm if n_ranks > 1 else None)  # noqa: E731
+
+    shard_check = None
+    if on_gpu and n_ranks > 1 and info.get("dp_policy") == "replicate" and a.shard_check == "auto":
+        # the timed solve replicates (every rank solves it all); prove the
+        # sharded, cross-device path on this node too: one untimed solve
+        sp = cfg.to_native(X.shape[1])
+        sp.dp_policy = 1
+        try:
+            s_solver = C.GpuSolver(sp, comm, ctx.local_rank)
+            s_info = s_solver.setup(X, X.shape[0], y)
+            sync()
+            barrier()
+            t_s = time.perf_counter()
+            s_alpha, s_res = s_solver.solve()
+            sync()
+            barrier()
+            shard_check = {"s": round(time.perf_counter() - t_s, 6), "iterations": int(s_res["iters"]),
+                           "b": s_res["b"], "smo_loop_s": round(float(s_res["t_solve"]), 6),
+                           "gram_gemm_s": round(float(s_res.get("t_gram", 0.0)), 6),
+                           "engine": s_info.get("iteration"), "exchange": s_info.get("exchange"),
+                           "exchange_mem": s_info.get("exchange_mem"),
+                           "geometry": f"{s_info.get('rows_per_group')}x{s_info.get('groups')}",
+                           "us_per_iter": round(1e6 * float(s_res["t_solve"]) / max(1, int(s_res["iters"])), 3),
+                           "verified": True}
+            del s_solver, s_alpha
+        except Exception as e:  # noqa: BLE001  (the digest inside solve() fails on every rank alike)
+            shard_check = {"error": str(e)[:300]}
+            if ctx.rank == 0:
+                print(f"[bench] sharded check failed: {e}", file=sys.stderr)
+
 
     for _ in range(a.warmup):
         run()
@@ -212,6 +256,8 @@ def main(argv=None) -> int:
             "smo_loop_s_min": round(solve_min, 6),
             "smo_loop_s_max": round(solve_max, 6),
             "iters_per_s": round(res["iters"] / max(solve_max, 1e-9), 1),
+            "cache": {k: int(res.get(k, 0)) for k in ("cache_hits", "cache_misses", "x_passes", "rows_computed",
+                                                       "spec_rows", "host_hits")},
             "device": info.get("device_name", ""),
             "x_replicated": bool(info.get("x_replicated", True)),
             "iteration": info.get("iteration", "cpu"),
@@ -219,6 +265,13 @@ def main(argv=None) -> int:
             "comm": getattr(comm, "name", "local"),
             "exchange": info.get("exchange", "none"),
             "exchange_mem": info.get("exchange_mem", "none"),
+            "dp_policy": info.get("dp_policy", "shard"),
+            "geometry": f"{info.get('rows_per_group', 0)}x{info.get('groups', 0)}",
+            "poll_batch": info.get("poll_batch", 0),
+            "census": info.get("census", "n/a"),
+            "engine_note": info.get("engine_note", ""),
+            "shard_check": shard_check,
+            "params": json.loads(params.to_json()),
             "preset": a.config,
         }
         line = json.dumps(out)

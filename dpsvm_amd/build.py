@@ -39,7 +39,11 @@ LIB_SOURCES = [
     "comm/comm_rccl.cpp",
     "solver/smo_cpu.cpp",
     "solver/checkpoint.cpp",
-    "solver/smo_gpu.hip",
+    "solver/gpu_setup.hip",
+    "solver/gpu_exchange.hip",
+    "solver/gpu_engines.hip",
+    "solver/gpu_solve.hip",
+    "solver/gpu_predict.hip",
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/smo_fused.hip",

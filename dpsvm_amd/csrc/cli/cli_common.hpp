@@ -15,6 +15,7 @@
 
 #include "dpsvm/common.hpp"
 #include "dpsvm/io.hpp"
+#include "dpsvm/params_io.hpp"
 #include "dpsvm/solver.hpp"
 
 namespace dpsvm {
@@ -70,6 +71,17 @@ inline void usage_train(const char* prog, bool seq) {
                "   --persist MODE      :  engine: auto | off (one launch/iteration) | on (persistent; dense and cache mode)\n"
                "   --persist-block N   :  SMO iterations per persistent launch (default 2048)\n"
                "   --exchange MODE     :  per-iteration keys: auto | allreduce | peer (in-kernel, xGMI)\n"
+               "   --dp MODE           :  data parallelism at world > 1: auto | shard | replicate\n"
+               "   --force-cache       :  kernel-row cache mode even when the Gram fits\n"
+               "   --cache-engine E    :  cache mode, one launch per iteration: fused | chain\n"
+               "   --cache-groups N    :  cache mode workgroups per rank (default 256)\n"
+               "   --rows-per-group N  :  rows per workgroup of the fused/persistent engines (multiple of 256)\n"
+               "   --xch-poll-batch N --xch-sleep N --xch-stride N --xch-mem auto|uncached|coarse\n"
+               "   --xch-timeout S     :  give-up bound of one in-kernel exchange poll (default 120)\n"
+               "   --watchdog S        :  host bound on one block of iterations (default 1800)\n"
+               "   --census-groups N   :  residency census grid of the persistent engines (tests)\n"
+               "   --no-verify-ranks   :  skip the cross-rank alpha digest (world > 1)\n"
+               "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
                "   --log-every N       :  progress line every N iterations\n"
@@ -84,7 +96,9 @@ inline Options parse_train(int argc, char** argv, bool seq) {
   enum {
     OPT_RANKS = 1000, OPT_CPU, OPT_DEVICE, OPT_SYN, OPT_SEED, OPT_CLIP, OPT_CMB, OPT_XMODE, OPT_SPEC,
     OPT_GB, OPT_NOGRAPH, OPT_CK, OPT_CKE, OPT_RESUME, OPT_METRICS, OPT_LOG, OPT_PREC, OPT_LEGM,
-    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH
+    OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
+    OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
+    OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -106,6 +120,13 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"skip-accuracy", no_argument, 0, OPT_SKIPACC}, {"verbose", no_argument, 0, OPT_VERBOSE},
       {"persist", required_argument, 0, OPT_PERSIST}, {"persist-block", required_argument, 0, OPT_PBLOCK},
       {"exchange", required_argument, 0, OPT_XCH},
+      {"dp", required_argument, 0, OPT_DP},       {"force-cache", no_argument, 0, OPT_FCACHE},
+      {"cache-engine", required_argument, 0, OPT_CENG}, {"cache-groups", required_argument, 0, OPT_CGROUPS},
+      {"rows-per-group", required_argument, 0, OPT_ROWS}, {"xch-poll-batch", required_argument, 0, OPT_XKB},
+      {"xch-sleep", required_argument, 0, OPT_XSLEEP}, {"xch-stride", required_argument, 0, OPT_XSTRIDE},
+      {"xch-mem", required_argument, 0, OPT_XMEM}, {"xch-timeout", required_argument, 0, OPT_XTMO},
+      {"watchdog", required_argument, 0, OPT_WDOG}, {"census-groups", required_argument, 0, OPT_CENSUS},
+      {"no-verify-ranks", no_argument, 0, OPT_NOVR}, {"params-json", required_argument, 0, OPT_PJSON},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -166,6 +187,49 @@ inline Options parse_train(int argc, char** argv, bool seq) {
         o.p.exchange = v == "peer" ? 2 : v == "allreduce" ? 1 : 0;
         break;
       }
+      case OPT_DP: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "shard" && v != "replicate") usage_train(argv[0], seq);
+        o.p.dp_policy = v == "shard" ? 1 : v == "replicate" ? 2 : 0;
+        break;
+      }
+      case OPT_FCACHE: o.p.force_cache = true; break;
+      case OPT_CENG: {
+        const std::string v = optarg;
+        if (v != "fused" && v != "chain") usage_train(argv[0], seq);
+        o.p.cache_engine = v == "chain" ? 1 : 0;
+        break;
+      }
+      case OPT_CGROUPS: o.p.cache_groups = atoi(optarg); break;
+      case OPT_ROWS: o.p.rows_per_group = atoi(optarg); break;
+      case OPT_XKB: o.p.xch_poll_batch = atoi(optarg); break;
+      case OPT_XSLEEP: o.p.xch_sleep = atoi(optarg); break;
+      case OPT_XSTRIDE: o.p.xch_stride = atoi(optarg); break;
+      case OPT_XMEM: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "uncached" && v != "coarse") usage_train(argv[0], seq);
+        o.p.xch_mem = v == "uncached" ? 1 : v == "coarse" ? 2 : 0;
+        break;
+      }
+      case OPT_XTMO: o.p.xch_timeout_s = atof(optarg); break;
+      case OPT_WDOG: o.p.watchdog_s = atof(optarg); break;
+      case OPT_CENSUS: o.p.census_groups = atoi(optarg); break;
+      case OPT_NOVR: o.p.verify_ranks = false; break;
+      case OPT_PJSON: {
+        FILE* fp = fopen(optarg, "r");
+        if (!fp) {
+          std::cerr << "cannot read " << optarg << "\n";
+          usage_train(argv[0], seq);
+        }
+        std::string text;
+        char buf[4096];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof(buf), fp)) > 0) text.append(buf, k);
+        fclose(fp);
+        apply_params_json(text, o.p);
+        o.gamma_set = o.p.gamma >= 0;
+        break;
+      }
       default:
         std::cerr << "\nERROR: Unknown option: -" << (char)c << "\n";
         usage_train(argv[0], seq);
@@ -207,6 +271,7 @@ inline std::string json_escape(const std::string& s) {
 struct RunExtras {
   double t_load = 0.0, t_accuracy = 0.0, t_model_write = 0.0;
   std::string engine = "cpu", exchange = "none";
+  GpuSetupInfo setup;  // engine, geometry, exchange, residency (GPU runs)
 };
 
 inline void write_metrics(const std::string& path, const Options& o, const SolveResult& r, int64_t n, int d,
@@ -225,7 +290,10 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           "\"t_gram_s\": %.6f, \"t_accuracy_s\": %.6f, \"t_model_write_s\": %.6f, \"engine\": \"%s\", "
           "\"exchange\": \"%s\", "
           "\"iters_per_s\": %.3f, \"cache_lines\": %lld, \"cache_hits\": %lld, \"cache_misses\": %lld, "
-          "\"rows_computed\": %lld, \"x_passes\": %lld, \"spec_rows\": %lld, \"data\": \"%s\"}\n",
+          "\"rows_computed\": %lld, \"x_passes\": %lld, \"spec_rows\": %lld, \"data\": \"%s\", "
+          "\"exchange_mem\": \"%s\", \"dp_policy\": \"%s\", \"rows_per_group\": %lld, \"groups\": %lld, "
+          "\"poll_batch\": %d, \"cus\": %d, \"blocks_per_cu\": %d, \"census\": \"%s\", \"engine_note\": \"%s\", "
+          "\"params\": %s}\n",
           backend.c_str(), json_escape(device).c_str(), r.world, (long long)n, d, o.p.C, o.p.gamma, o.p.eps,
           o.p.clip == ClipMode::Box ? "box" : "independent", (long long)r.iters, r.status,
           r.converged() ? "true" : "false", r.b, r.b_hi, r.b_lo, (long long)nsv, acc, x.t_load, r.t_setup,
@@ -233,7 +301,10 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           r.t_solve > 0 ? r.iters / r.t_solve : 0.0, (long long)r.cache_lines,
           (long long)r.cache_hits, (long long)r.cache_misses, (long long)r.rows_computed,
           (long long)r.x_passes, (long long)r.spec_rows,
-          json_escape(o.synthetic.empty() ? o.file : "synthetic:" + o.synthetic).c_str());
+          json_escape(o.synthetic.empty() ? o.file : "synthetic:" + o.synthetic).c_str(),
+          x.setup.exchange_mem.c_str(), x.setup.dp_policy.c_str(), (long long)x.setup.rows_per_group,
+          (long long)x.setup.groups, x.setup.poll_batch, x.setup.cus, x.setup.blocks_per_cu,
+          x.setup.census.c_str(), json_escape(x.setup.engine_note).c_str(), params_json(o.p).c_str());
   fclose(fp);
 }
 

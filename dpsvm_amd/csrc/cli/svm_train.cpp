@@ -92,6 +92,7 @@ int main(int argc, char** argv) {
         if (r == 0) {
           extras.engine = info.iteration;
           extras.exchange = info.exchange;
+          extras.setup = info;
         }
         results[r] = solver.solve(resume.get(), prog);
         const double ta0 = cli::now_s();

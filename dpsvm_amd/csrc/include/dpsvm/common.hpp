@@ -81,11 +81,38 @@ struct SolverParams {
   // all-reduce), 1 communicator all-reduce, 2 peer exchange (required; also
   // at world 1 as a loopback, for tests)
   int exchange = 0;
-  // dense mode iteration engine: 0 auto, 1 one launch per iteration (graphs),
-  // 2 persistent kernel (persist_block iterations per launch)
+  // iteration engine: 0 auto, 1 one launch per iteration (graphs), 2 persistent
+  // kernel (persist_block iterations per launch; dense and cache mode)
   int persist = 0;
   int persist_block = 2048;
+  // ---- engine / geometry selection (recorded in GpuSetupInfo and --metrics-json;
+  //      every choice is a parameter, none comes from the environment) ----
+  bool force_cache = false;   // kernel-row cache mode even when the Gram shard fits
+  int cache_engine = 0;       // cache mode, one launch per iteration: 0 fused kernel, 1 rows/step/finalize chain
+  int cache_groups = 256;     // cache mode: workgroups per rank (one per CU: the X pass wants every CU)
+  int rows_per_group = 0;     // rows per workgroup of the fused / persistent engines (0 auto; multiple of 256)
+  // peer exchange (in-kernel key exchange of the fused / persistent engines)
+  int xch_poll_batch = 0;     // publications watched per lane per poll round: 0 auto, 1, 2, 4
+  int xch_sleep = 1;          // s_sleep(1) count between poll rounds
+  int xch_stride = 4;         // u64 slots per exchange entry (>= 4; larger pads entries apart)
+  int xch_mem = 0;            // receive buffer: 0 auto (uncached when world > 1), 1 uncached, 2 coarse
+  double xch_timeout_s = 120.0;  // give-up bound of one in-kernel poll loop (then status 5)
+  double watchdog_s = 1800.0;    // host bound on one block of iterations
+  // residency census of the persistent engines (tests: a grid of this many
+  // workgroups instead of the engine's, > the device's capacity forces the
+  // fallback to the one-launch-per-iteration engine)
+  int census_groups = 0;
+  bool verify_ranks = true;   // world > 1: cross-rank alpha digest after every solve
+  // data-parallel policy when world > 1: 0 auto, 1 shard the rows, 2 every rank
+  // solves the whole problem.  auto replicates only when the ranks sit on
+  // distinct devices, the whole Gram fits one device and the one-device
+  // persistent engine runs its fast geometry (<= 256 workgroups of <= 1024
+  // rows): the SMO iteration is a latency chain, and sharding such a problem
+  // adds a cross-device hop to every iteration while saving only the Gram
+  // GEMM (docs/DESIGN.md "Multi-GPU").
+  int dp_policy = 0;
 };
+
 
 // Per-run result, gathered on every rank.
 struct SolveResult {

@@ -38,6 +38,24 @@ enum DoneCode : int32_t {
   kCommFail = 5,   // peer exchange gave up waiting (a rank stopped or diverged)
 };
 
+// Iteration engines of the device solver (GpuSetupInfo::iteration names them).
+enum class EngineKind : int32_t {
+  PersistDense = 0,  // Gram resident, persistent kernel, in-kernel key exchange
+  FusedDense = 1,    // Gram resident, one launch per iteration (hipGraph blocks)
+  PersistCache = 2,  // kernel-row cache, persistent kernel, private cache metadata
+  FusedCache = 3,    // kernel-row cache, one launch per iteration (+ host spill tier)
+  Chain = 4,         // rows / step / finalize kernels + collective (partitioned X fallback)
+};
+inline const char* engine_name(EngineKind k) {
+  switch (k) {
+    case EngineKind::PersistDense: return "persistent-dense";
+    case EngineKind::FusedDense: return "fused-dense";
+    case EngineKind::PersistCache: return "persistent-cache";
+    case EngineKind::FusedCache: return "fused-cache";
+    default: return "chain";
+  }
+}
+
 // Written by smo_finalize, read by the next iteration's kernels.
 struct alignas(16) SmoCtrl {
   int32_t iter;        // SMO updates applied so far
@@ -166,6 +184,11 @@ struct SmoArgs {
   int32_t xpoll_kb;  // 0: poll batch from the entry count; else fixed (2, 4, 8)
   int32_t xpoll_sleep;  // s_sleep(1) count between poll rounds
   int64_t xtimeout_ticks;  // give-up bound of one poll loop (s_memrealtime, 100 MHz)
+  // residency census of the persistent engines (steps < 0: every workgroup
+  // counts itself in and waits for the whole grid, bounded by census_ticks;
+  // words [arrivals, abort])
+  int32_t* census;
+  int64_t census_ticks;
 };
 constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..16}, {key bits 15..0, alpha}
 constexpr int kStampRing = 4096;

@@ -36,6 +36,10 @@ struct Checkpoint {
 };
 void write_checkpoint(const std::string& path, const Checkpoint& ck);
 Checkpoint read_checkpoint(const std::string& path);
+// Rejects a checkpoint written for another problem: a different n, d, C, gamma
+// or clip mode (its f would be inconsistent with this kernel, its alphas may
+// violate this box).  eps and max_iter may differ.
+void check_resume(const Checkpoint& ck, int64_t n, int d, const SolverParams& p, float gamma);
 
 // ---------------------------------------------------------------------------
 // CPU solver (C10 seq / the no-GPU path and the test oracle).  X is replicated,
@@ -61,9 +65,15 @@ struct GpuSetupInfo {
   int64_t cache_lines = 0, host_cache_lines = 0;
   int blocks = 0;
   size_t bytes_device = 0;
-  std::string iteration;  // "fused-dense" | "fused-cache" | "chain" (rows/step/finalize)
+  std::string iteration;  // engine: "persistent-dense" | "fused-dense" | "persistent-cache" | "fused-cache" | "chain"
   std::string exchange;   // per-iteration key exchange: "none" | "allreduce" | "peer" | "loopback" (1 rank)
   std::string exchange_mem = "none";  // peer exchange receive buffer: "uncached" (across devices) | "coarse"
+  std::string dp_policy = "shard";    // "shard" (rows split over ranks) | "replicate" (every rank solves it all)
+  int64_t rows_per_group = 0, groups = 0;  // fused / persistent geometry
+  int poll_batch = 0;                 // publications per lane per poll round (peer exchange)
+  int cus = 0, blocks_per_cu = 0;     // residency of the persistent kernel (occupancy API)
+  std::string census = "n/a";         // residency census of the persistent grid: "ok" | "failed" | "n/a"
+  std::string engine_note;            // why the engine was chosen / refused (fallbacks)
 };
 
 class GpuSolver {
@@ -119,6 +129,14 @@ int64_t compact_nonzero(const float* alpha, int64_t n, int* idx_out, void* strea
 // Gram block K[i][j] = K(a_i, b_j) (dense-mode GEMM; symmetric: b == a)
 void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
               float gamma, float* out, int64_t out_ld, bool symmetric, void* stream);
+// the cache engines' X pass: out[q][j] = K(x_keys[q], x_j), q < nq <= 16, j < n
+// (x: [rows >= G*rows_per_group][ld], xsq likewise; out rows >= G*rows_per_group)
+void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* keys, int nq, float gamma,
+                float* out, int64_t out_ld, int rows_per_group, void* stream);
+// the fused / persistent engines' selection: per workgroup of rows_per_group rows
+// the (up, low) keys of its rows -> keys_out[2 * groups]
+void fused_select(const float* f, const float* alpha, const float* y, int64_t n, float C, int rows_per_group,
+                  uint64_t* keys_out, void* stream);
 }  // namespace kernels
 
 int device_count();

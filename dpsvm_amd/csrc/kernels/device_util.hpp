@@ -165,5 +165,29 @@ __device__ __forceinline__ float rbf_from_dot(float sq_a, float sq_b, float dot,
   return expf(-gamma * d2);
 }
 
+// Residency census of a persistent grid (run once at setup with the engine's
+// own kernel, grid and resources, before that engine is chosen).  Thread 0 of
+// every workgroup counts itself in and waits until the whole grid has arrived.
+// A grid that cannot be co-resident (a partitioned device, CUs held by another
+// job, an oversized grid) times out instead of hanging: the first workgroup to
+// give up raises the abort word, and workgroups that only get a CU after
+// others left see it and leave at once without counting themselves.  All
+// accesses are memory-side atomics (never a stale line of a per-XCD L2).
+// words: [arrivals, abort], zeroed by the host; success = {gridDim.x, 0}.
+__device__ inline void census_arrive(int32_t* words, int64_t ticks) {
+  if (threadIdx.x != 0) return;
+  auto rd = [&](int i) { return __hip_atomic_fetch_add(words + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  if (rd(1) != 0) return;
+  __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (rd(0) < (int)gridDim.x && rd(1) == 0) {
+    if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > ticks) {
+      __hip_atomic_fetch_add(words + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 }  // namespace dev
 }  // namespace dpsvm

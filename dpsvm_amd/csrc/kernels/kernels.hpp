@@ -33,6 +33,18 @@ void smo_fused(const SmoArgs& a, int mode, const uint64_t* p_in, uint64_t* p_out
 // workgroup co-resident; keys exchanged as tagged granules, a.xworld >= 1);
 // st: state record in/out (iteration, done, b_hi, b_lo; no pending pair)
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s);
+// publications watched per lane per poll round for a's exchange geometry
+int poll_batch(const SmoArgs& a);
+// residency of the persistent engines' kernels (the instantiation `a` runs):
+// occupancy API answer per CU, and the census launch (steps < 0) with `groups`
+// workgroups; a.census = two zeroed words, a.census_ticks = give-up bound
+int smo_persist_blocks_per_cu(const SmoArgs& a);
+void smo_persist_census(const SmoArgs& a, int groups, hipStream_t s);
+// test entry: the cache engines' X pass (xpass_fill) over a.nl rows, queries
+// keys_dev[0..n_new) into lines 0..n_new-1 (a.lines / a.ldl / a.fused_rows)
+void xpass_rows(const SmoArgs& a, const int* keys_dev, int n_new, hipStream_t s);
+int smo_persist_lru_blocks_per_cu(const SmoArgs& a);
+void smo_persist_lru_census(const SmoArgs& a, int groups, hipStream_t s);
 // cache mode, persistent (smo_persist_lru.hip): up to `steps` SMO iterations in
 // one launch, private per-workgroup cache metadata (a.plru_meta, plru_init);
 // stats: int64 [hits, misses, rows computed, X passes, speculative rows] in/out

@@ -49,6 +49,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
   __shared__ XKeys pair_s;
   __shared__ int fail_s;
   __shared__ float d2_s;
+  if (steps < 0) {  // residency census (setup): this kernel, this grid
+    census_arrive(a.census, a.census_ticks);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int rpt = a.fused_rows / kFusedThreads;  // rows per thread
@@ -256,28 +260,45 @@ void preload_persist_kernel(hipStream_t s) {
   (void)hipFree(st);
 }
 
+// The instantiation a launch of `a` runs: (scope, poll batch, register rows).
+using PersistFn = void (*)(SmoArgs, FusedRec*, int);
 template <int kR>
-static void launch_persist(const SmoArgs& a, FusedRec* st, int steps, int kb, dim3 g, hipStream_t s) {
-  if (a.xworld > 1) {
-    if (kb == 1) dev::smo_persist_kernel<true, 1, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else if (kb == 2) dev::smo_persist_kernel<true, 2, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else dev::smo_persist_kernel<true, 4, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-  } else {
-    if (kb == 1) dev::smo_persist_kernel<false, 1, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else if (kb == 2) dev::smo_persist_kernel<false, 2, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-    else dev::smo_persist_kernel<false, 4, kR><<<g, kFusedThreads, 0, s>>>(a, st, steps);
-  }
+static PersistFn persist_fn_r(bool sys, int kb) {
+  if (sys) return kb == 1 ? dev::smo_persist_kernel<true, 1, kR> : kb == 2 ? dev::smo_persist_kernel<true, 2, kR>
+                                                                           : dev::smo_persist_kernel<true, 4, kR>;
+  return kb == 1 ? dev::smo_persist_kernel<false, 1, kR> : kb == 2 ? dev::smo_persist_kernel<false, 2, kR>
+                                                                   : dev::smo_persist_kernel<false, 4, kR>;
+}
+static PersistFn persist_fn(const SmoArgs& a) {
+  const int E = a.xworld * a.fused_G;
+  const int kb = a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
+  // rows per thread: 4 (<= 1024 rows per workgroup, the headline geometry) or 12
+  return a.fused_rows <= 4 * kFusedThreads ? persist_fn_r<4>(a.xworld > 1, kb)
+                                           : persist_fn_r<dev::kPersistMaxRows>(a.xworld > 1, kb);
+}
+
+int poll_batch(const SmoArgs& a) {
+  const int E = a.xworld * a.fused_G;
+  return a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
+}
+
+int smo_persist_blocks_per_cu(const SmoArgs& a) {
+  int nb = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)persist_fn(a), kFusedThreads, 0));
+  return nb;
+}
+
+void smo_persist_census(const SmoArgs& a, int groups, hipStream_t s) {
+  PersistFn fn = persist_fn(a);
+  fn<<<dim3(groups), kFusedThreads, 0, s>>>(a, nullptr, -1);
+  post_launch("smo_persist census", s);
 }
 
 void smo_persist(const SmoArgs& a, FusedRec* st, int steps, hipStream_t s) {
   DPSVM_CHECK(a.xworld >= 1 && a.fused_G <= 256 && a.fused_rows <= dev::kPersistMaxRows * kFusedThreads,
               "persistent SMO needs the key exchange and <= 256 resident workgroups");
-  const int E = a.xworld * a.fused_G;
-  const int kb = a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
-  const dim3 g(a.fused_G);
-  // rows per thread: 4 (<= 1024 rows per workgroup, the headline geometry) or 12
-  if (a.fused_rows <= 4 * kFusedThreads) launch_persist<4>(a, st, steps, kb, g, s);
-  else launch_persist<dev::kPersistMaxRows>(a, st, steps, kb, g, s);
+  PersistFn fn = persist_fn(a);
+  fn<<<dim3(a.fused_G), kFusedThreads, 0, s>>>(a, st, steps);
   post_launch("smo_persist", s);
 }
 

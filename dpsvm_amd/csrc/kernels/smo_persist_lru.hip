@@ -61,6 +61,10 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_lru_kernel(SmoArgs 
   __shared__ float d2_s;
   __shared__ PLPlan pl;
   __shared__ int kscan[kFusedThreads / 64];
+  if (steps < 0) {  // residency census (setup): this kernel, this grid, this LDS
+    census_arrive(a.census, a.census_ticks);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool lead = blockIdx.x == 0 && tid == 0;
   const int rpt = (a.fused_rows + kFusedThreads - 1) / kFusedThreads;
@@ -439,29 +443,40 @@ void plru_init(int32_t* meta, int64_t stride, int64_t G, int64_t n, int64_t L, h
   post_launch("plru_init", s);
 }
 
-template <bool kSys, int kB>
-static void launch_plru(const SmoArgs& a, FusedRec* st, int steps, int64_t* stats, size_t lds, hipStream_t s) {
+using PlruFn = void (*)(SmoArgs, FusedRec*, int, int64_t*);
+static PlruFn plru_fn(const SmoArgs& a, size_t lds) {
+  const int E = a.xworld * a.fused_G;
+  const int kb = a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
+  PlruFn fn;
+  if (a.xworld > 1)
+    fn = kb == 1 ? dev::smo_persist_lru_kernel<true, 1> : kb == 2 ? dev::smo_persist_lru_kernel<true, 2>
+                                                                  : dev::smo_persist_lru_kernel<true, 4>;
+  else
+    fn = kb == 1 ? dev::smo_persist_lru_kernel<false, 1> : kb == 2 ? dev::smo_persist_lru_kernel<false, 2>
+                                                                   : dev::smo_persist_lru_kernel<false, 4>;
   if (lds > 64 * 1024)
-    HIP_CHECK(hipFuncSetAttribute((const void*)dev::smo_persist_lru_kernel<kSys, kB>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dev::smo_persist_lru_kernel<kSys, kB><<<dim3(a.fused_G), kFusedThreads, lds, s>>>(a, st, steps, stats);
+    HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return fn;
+}
+
+int smo_persist_lru_blocks_per_cu(const SmoArgs& a) {
+  const size_t lds = dev::xpass_lds_floats(a.dp, a.fused_rows) * sizeof(float);
+  int nb = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)plru_fn(a, lds), kFusedThreads, lds));
+  return nb;
+}
+
+void smo_persist_lru_census(const SmoArgs& a, int groups, hipStream_t s) {
+  const size_t lds = dev::xpass_lds_floats(a.dp, a.fused_rows) * sizeof(float);
+  plru_fn(a, lds)<<<dim3(groups), kFusedThreads, lds, s>>>(a, nullptr, -1, nullptr);
+  post_launch("smo_persist_lru census", s);
 }
 
 void smo_persist_lru(const SmoArgs& a, FusedRec* st, int steps, int64_t* stats, hipStream_t s) {
   DPSVM_CHECK(a.xworld >= 1 && smo_persist_lru_supported(a.dp, a.fused_rows, a.fused_G) && a.plru_meta,
               "persistent cache SMO: needs the key exchange, <= 256 resident workgroups, <= 3072 rows each");
   const size_t lds = dev::xpass_lds_floats(a.dp, a.fused_rows) * sizeof(float);
-  const int E = a.xworld * a.fused_G;
-  const int kb = a.xpoll_kb > 0 ? a.xpoll_kb : (E <= 64 ? 1 : E <= 128 ? 2 : 4);
-  if (a.xworld > 1) {
-    if (kb == 1) launch_plru<true, 1>(a, st, steps, stats, lds, s);
-    else if (kb == 2) launch_plru<true, 2>(a, st, steps, stats, lds, s);
-    else launch_plru<true, 4>(a, st, steps, stats, lds, s);
-  } else {
-    if (kb == 1) launch_plru<false, 1>(a, st, steps, stats, lds, s);
-    else if (kb == 2) launch_plru<false, 2>(a, st, steps, stats, lds, s);
-    else launch_plru<false, 4>(a, st, steps, stats, lds, s);
-  }
+  plru_fn(a, lds)<<<dim3(a.fused_G), kFusedThreads, lds, s>>>(a, st, steps, stats);
   post_launch("smo_persist_lru", s);
 }
 
@@ -488,5 +503,45 @@ void preload_persist_lru_kernel(hipStream_t s) {
   (void)hipFree(st);
 }
 
+}  // namespace launch
+}  // namespace dpsvm
+
+// ---------------------------------------------------------------------------
+// Kernel-level test entry of the X pass exactly as both cache engines run it
+// (xpass_fill): workgroup b fills rows [b * fused_rows, ...) of lines 0..n_new-1
+// with K(x_keys[q], x_j).
+// ---------------------------------------------------------------------------
+namespace dpsvm {
+namespace dev {
+__global__ __launch_bounds__(kFusedThreads) void xpass_test_kernel(SmoArgs a, const int* __restrict__ keys,
+                                                                   int n_new) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  __shared__ int key_s[kNQ], line_s[kNQ], op_s[kNQ];
+  const int tid = threadIdx.x;
+  if (tid < kNQ) {
+    key_s[tid] = tid < n_new ? keys[tid] : 0;
+    line_s[tid] = tid;
+    op_s[tid] = kOpCompute;
+  }
+  __syncthreads();
+  const int64_t row0 = (int64_t)blockIdx.x * a.fused_rows;
+  const int64_t row_end = min((int64_t)a.nl, row0 + (int64_t)a.fused_rows);
+  xpass_fill(a, row0, row_end, n_new, key_s, line_s, op_s, wsm, false);
+}
+}  // namespace dev
+
+namespace launch {
+void xpass_rows(const SmoArgs& a, const int* keys_dev, int n_new, hipStream_t s) {
+  DPSVM_CHECK(n_new >= 1 && n_new <= kNQ && a.fused_rows % kFusedThreads == 0 && a.dp % 16 == 0,
+              "xpass_rows: 1 <= n_new <= 16, rows a multiple of 256, dp a multiple of 16");
+  const size_t lds = dev::xpass_lds_floats(a.dp, a.fused_rows) * sizeof(float);
+  DPSVM_CHECK(lds <= 160 * 1024, "xpass_rows: LDS");
+  if (lds > 64 * 1024)
+    HIP_CHECK(hipFuncSetAttribute((const void*)dev::xpass_test_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+  const int G = (int)((a.nl + a.fused_rows - 1) / a.fused_rows);
+  dev::xpass_test_kernel<<<dim3(G), kFusedThreads, lds, s>>>(a, keys_dev, n_new);
+  post_launch("xpass_rows", s);
+}
 }  // namespace launch
 }  // namespace dpsvm

@@ -13,6 +13,7 @@
 #include "dpsvm/common.hpp"
 #include "dpsvm/io.hpp"
 #include "dpsvm/solver.hpp"
+#include "dpsvm/params_io.hpp"
 #include "../kernels/kernels.hpp"
 
 namespace py = pybind11;
@@ -165,7 +166,22 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("force_collectives", &SolverParams::force_collectives)
       .def_readwrite("exchange", &SolverParams::exchange)
       .def_readwrite("persist", &SolverParams::persist)
-      .def_readwrite("persist_block", &SolverParams::persist_block);
+      .def_readwrite("persist_block", &SolverParams::persist_block)
+      .def_readwrite("force_cache", &SolverParams::force_cache)
+      .def_readwrite("cache_engine", &SolverParams::cache_engine)
+      .def_readwrite("cache_groups", &SolverParams::cache_groups)
+      .def_readwrite("rows_per_group", &SolverParams::rows_per_group)
+      .def_readwrite("xch_poll_batch", &SolverParams::xch_poll_batch)
+      .def_readwrite("xch_sleep", &SolverParams::xch_sleep)
+      .def_readwrite("xch_stride", &SolverParams::xch_stride)
+      .def_readwrite("xch_mem", &SolverParams::xch_mem)
+      .def_readwrite("xch_timeout_s", &SolverParams::xch_timeout_s)
+      .def_readwrite("watchdog_s", &SolverParams::watchdog_s)
+      .def_readwrite("census_groups", &SolverParams::census_groups)
+      .def_readwrite("verify_ranks", &SolverParams::verify_ranks)
+      .def_readwrite("dp_policy", &SolverParams::dp_policy)
+      .def("to_json", [](const SolverParams& p) { return params_json(p); })
+      .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });
 
   py::class_<Checkpoint>(m, "Checkpoint")
       .def(py::init<>())
@@ -333,6 +349,14 @@ PYBIND11_MODULE(_C, m) {
         d["cache_lines"] = i.cache_lines;
         d["blocks"] = i.blocks;
         d["bytes_device"] = i.bytes_device;
+        d["dp_policy"] = i.dp_policy;
+        d["rows_per_group"] = i.rows_per_group;
+        d["groups"] = i.groups;
+        d["poll_batch"] = i.poll_batch;
+        d["cus"] = i.cus;
+        d["blocks_per_cu"] = i.blocks_per_cu;
+        d["census"] = i.census;
+        d["engine_note"] = i.engine_note;
         return d;
       })
       .def("solve", [](GpuSolver& s, const Checkpoint* resume, py::object progress) {
@@ -408,6 +432,16 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("k_compact", [](uintptr_t alpha, int64_t n, uintptr_t idx, uintptr_t stream) {
     return kernels::compact_nonzero((const float*)alpha, n, (int*)idx, (void*)stream);
+  });
+  m.def("k_xpass_rows", [](uintptr_t x, uintptr_t xsq, int64_t n, int ld, uintptr_t keys, int nq, float gamma,
+                           uintptr_t out, int64_t out_ld, int rows, uintptr_t stream) {
+    kernels::xpass_rows((const float*)x, (const float*)xsq, n, ld, (const int*)keys, nq, gamma, (float*)out, out_ld,
+                        rows, (void*)stream);
+  });
+  m.def("k_fused_select", [](uintptr_t f, uintptr_t alpha, uintptr_t y, int64_t n, float C, int rows, uintptr_t out,
+                             uintptr_t stream) {
+    kernels::fused_select((const float*)f, (const float*)alpha, (const float*)y, n, C, rows, (uint64_t*)out,
+                          (void*)stream);
   });
   m.def("make_key", [](float f, uint32_t idx) { return make_key(f, idx); });
   m.def("key_value", [](uint64_t k) { return key_value(k); });

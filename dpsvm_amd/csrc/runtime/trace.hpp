@@ -5,8 +5,14 @@
 //                        dlopen'ed so no link dependency exists when unused.
 //   DPSVM_FAULT=nan@K    poison f at the first block boundary at/after SMO
 //                        iteration K (exercises the non-finite abort path).
-//   DPSVM_VERIFY=1       after solve, all-reduce MIN and MAX of an alpha hash;
-//                        ranks that diverged raise an error.
+//   DPSVM_FAULT=exit@K:R rank R's process dies (_exit(3)) at the first block
+//                        boundary at/after iteration K: the surviving ranks
+//                        must fail (bounded exchange polls, collective errors,
+//                        watchdog) instead of hanging, and the last checkpoint
+//                        resumes the run (any rank count).
+//   DPSVM_VERIFY=1       after solve: alpha in [0, C], f recomputed from alpha,
+//                        and the cross-rank alpha digest (the digest alone runs
+//                        by default at world > 1: SolverParams::verify_ranks).
 #pragma once
 
 #include <dlfcn.h>
@@ -59,16 +65,18 @@ inline int64_t fault_nan_iter() {
   return atoll(e + 4);
 }
 
+// DPSVM_FAULT=exit@K:R -> K when this is rank R, else -1
+inline int64_t fault_exit_iter(int rank) {
+  const char* e = std::getenv("DPSVM_FAULT");
+  if (!e || strncmp(e, "exit@", 5) != 0) return -1;
+  const char* c = strchr(e + 5, ':');
+  if (!c || atoi(c + 1) != rank) return -1;
+  return atoll(e + 5);
+}
+
 inline bool verify_enabled() {
   const char* e = std::getenv("DPSVM_VERIFY");
   return e && e[0] == '1';
-}
-
-// DPSVM_VERIFY=ranks: only the cross-rank alpha digest (one 16-byte all-reduce
-// per solve; what bench.py enables for N > 1), no f recomputation
-inline bool verify_ranks_enabled() {
-  const char* e = std::getenv("DPSVM_VERIFY");
-  return e && (e[0] == '1' || std::string(e) == "ranks");
 }
 
 // order-sensitive 64-bit hash of float bit patterns (FNV-1a over words)

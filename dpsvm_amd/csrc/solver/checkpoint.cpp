@@ -82,4 +82,17 @@ Checkpoint read_checkpoint(const std::string& path) {
   return ck;
 }
 
+void check_resume(const Checkpoint& ck, int64_t n, int d, const SolverParams& p, float gamma) {
+  auto bad = [&](const std::string& what, const std::string& ckv, const std::string& now) {
+    fail("checkpoint does not match this problem: " + what + " = " + ckv + " in the checkpoint, " + now +
+         " now (resume needs the same n, d, C, gamma and clip mode)");
+  };
+  if (ck.n != n || (int64_t)ck.alpha.size() != n) bad("n", std::to_string(ck.n), std::to_string(n));
+  if (ck.d != d) bad("d", std::to_string(ck.d), std::to_string(d));
+  if (ck.C != p.C) bad("C", std::to_string(ck.C), std::to_string(p.C));
+  if (ck.gamma != gamma) bad("gamma", std::to_string(ck.gamma), std::to_string(gamma));
+  if (ck.clip != (int)p.clip) bad("clip", std::to_string(ck.clip), std::to_string((int)p.clip));
+  if (!ck.f.empty() && (int64_t)ck.f.size() != n) bad("f length", std::to_string(ck.f.size()), std::to_string(n));
+}
+
 }  // namespace dpsvm

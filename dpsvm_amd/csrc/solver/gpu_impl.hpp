@@ -1,0 +1,163 @@
+// Internal state of the device-resident SMO solver (one rank = one MI355X).
+//
+// Reference driver: svmTrainMain.cpp:142-365 + SvmTrain (svmTrain.cu:305-395).
+// The solver is split by concern:
+//   gpu_setup.hip     X placement, data-parallel policy, cache sizing, geometry,
+//                     engine choice (incl. the residency census)
+//   gpu_exchange.hip  in-kernel peer exchange buffers (IPC / peer mappings, ping),
+//                     small collectives that work on device and host communicators
+//   gpu_engines.hip   the five iteration engines (seed + block of iterations)
+//   gpu_solve.hip     the timed SMO loop, checkpoints, invariant checks
+//   gpu_predict.hip   SV compaction, accuracy, decision values, GpuPredictor,
+//                     kernel-level test entry points
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dpsvm/device_state.hpp"
+#include "dpsvm/solver.hpp"
+#include "../kernels/kernels.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace gpu {
+
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+template <class T>
+T* dmalloc(size_t count, size_t* total) {
+  void* p = nullptr;
+  if (count == 0) count = 1;
+  HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+  *total += count * sizeof(T);
+  return (T*)p;
+}
+
+// The pair a fused engine's last launch updated but has not committed to the
+// alpha array yet (its record carries the new alphas): checkpoints apply it.
+struct Pending {
+  bool valid = false;
+  int32_t i_hi = -1, i_lo = -1;
+  float a_hi = 0.f, a_lo = 0.f;
+  int64_t iter = 0;
+  float b_hi = 0.f, b_lo = 0.f;
+};
+
+struct Engine;
+
+}  // namespace gpu
+
+struct GpuSolver::Impl {
+  SolverParams p;
+  Communicator* comm = nullptr;        // the solve's communicator (local when replicated)
+  Communicator* outer = nullptr;       // the caller's communicator (== comm unless replicated)
+  std::unique_ptr<Communicator> own_comm;
+  int device = 0, rank = 0, world = 1;
+  int outer_rank = 0, outer_world = 1;
+  GpuSetupInfo info;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  size_t bytes = 0;
+
+  // device buffers
+  float *x = nullptr, *xsq = nullptr, *y = nullptr, *alpha = nullptr, *f = nullptr;
+  float* lines = nullptr;
+  int32_t *slot_of = nullptr, *key_of = nullptr;
+  uint8_t* ref = nullptr;  // CLOCK reference bits
+  float *hlines_h = nullptr, *hlines_d = nullptr;  // pinned host tier (host / device view)
+  int32_t *hslot_of = nullptr, *hkey_of = nullptr;
+  int64_t H = 0;
+  uint64_t* partials = nullptr;
+  SmoCtrl* ctrl = nullptr;
+  SmoStatus* status_h = nullptr;  // host view
+  SmoStatus* status_d = nullptr;  // device view
+  uint8_t *records = nullptr, *my_record = nullptr;
+  uint64_t* pf = nullptr;          // fused engines: two partial buffers [2][2*Gf]
+  FusedRec* rf = nullptr;          // dense / persistent engines: two records
+  FusedCacheRec* rcf = nullptr;    // fused cache engine: two records
+  int32_t* plru_meta = nullptr;    // persistent cache engine: private metadata per workgroup
+  int64_t* plru_stats = nullptr;
+  // peer exchange: own receive buffer (own allocation, IPC exported), device
+  // table of every rank's buffer, IPC mappings to close
+  bool xch = false;
+  uint64_t* xbuf = nullptr;
+  uint64_t** xpeer_d = nullptr;
+  int64_t xregion = 0;             // u64 words of the two key parities (zeroed per solve)
+  int64_t xstride = kXchGranules;  // u64 slots per exchange entry
+  std::vector<void*> xopened;
+  std::string xch_diag;
+  std::string xch_mem = "none";    // receive-buffer memory kind
+  int64_t Gf = 0, RBf = 0;         // fused / persistent geometry: workgroups, rows per workgroup
+  uint64_t* stamps = nullptr;      // DPSVM_STAMPS diagnostics
+  std::string stamps_path;
+  std::vector<uint64_t> h_partials;  // host staging for host-memory communicators
+  std::vector<uint8_t> h_records;
+
+  SmoArgs args{};
+  float gamma = 0.f;
+  int64_t n = 0, nl = 0, off = 0, x_rows = 0, G = 0, ldl = 0, L = 0;
+  int d = 0, dp = 0;
+  bool replicated = true, dense = false;
+  EngineKind kind = EngineKind::Chain;
+  std::unique_ptr<gpu::Engine> engine;
+  std::vector<float> h_y;
+
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+
+  ~Impl();
+
+  bool collectives() const { return world > 1 || p.force_collectives; }
+  bool device_comm() const { return world == 1 || comm->device_memory(); }
+  bool fused() const { return kind != EngineKind::Chain; }
+  bool persistent() const { return kind == EngineKind::PersistDense || kind == EngineKind::PersistCache; }
+
+  SmoStatus read_status() const;
+  void init_ctrl(int64_t iter0, float b_hi, float b_lo);
+  void wait_event(hipEvent_t e);
+
+  // ---- gpu_exchange.hip ----
+  // element-wise MIN over ranks of u64 device buffer (device or host communicator)
+  void allreduce_keys(uint64_t* buf, int64_t count);
+  void allgather_bytes(const void* send, void* recv, size_t bytes);  // host buffers
+  // every rank of `c` agrees: true only if `mine` is true everywhere
+  bool all_agree(bool mine, Communicator* c, int w);
+  bool setup_exchange();
+  // residency census of the chosen persistent engine (collective: agreed)
+  bool census(EngineKind k);
+
+  // ---- gpu_engines.hip ----
+  void enqueue_iteration(int k);  // one iteration of a launch-per-iteration engine
+  void build_graph(int iters);
+
+  // ---- gpu_solve.hip ----
+  void snapshot(const SmoStatus& st);
+};
+
+namespace gpu {
+
+// One iteration engine.  prepare() resets engine state before the timed
+// region; seed() runs at the start of the timed region (the
+// dense engines compute the resident Gram there) and leaves the device state
+// one block away from iteration iter0 + 1; run_block() enqueues B iterations
+// (early-exit once the status record says done); pending() reports a pair
+// whose alphas still sit in a record.
+struct Engine {
+  virtual ~Engine() = default;
+  virtual EngineKind kind() const = 0;
+  virtual int block(const SolverParams& p) const = 0;
+  virtual void prepare(GpuSolver::Impl&) {}  // per-solve state reset, before the timed region
+  virtual void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) = 0;
+  virtual void run_block(GpuSolver::Impl& m, int B) = 0;
+  virtual Pending pending(GpuSolver::Impl&) { return {}; }
+  virtual double gram_seconds() { return 0.0; }
+};
+
+std::unique_ptr<Engine> make_engine(EngineKind k);
+
+}  // namespace gpu
+}  // namespace dpsvm

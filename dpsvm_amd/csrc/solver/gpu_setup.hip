@@ -1,0 +1,456 @@
+// Device solver setup: data-parallel policy, X placement, global vectors,
+// kernel-row cache sizing (288 GB of HBM: the Gram shard is usually resident),
+// workgroup geometry and the choice of iteration engine.
+//
+// Reference: SvmTrain::setup (svmTrain.cu:319-395: full X H2D per rank, n
+// separate norm launches, 10 eager cache lines) and the shard tables of
+// svmTrainMain.cpp:367-384.  Every decision that must match across ranks
+// (dense vs cache mode, X placement, engine) is agreed by a collective, since
+// free memory and residency can differ per device.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <thread>
+
+#include <unistd.h>
+
+#include "gpu_impl.hpp"
+#include "../runtime/timer.hpp"
+
+namespace dpsvm {
+
+using gpu::dmalloc;
+using gpu::round_up;
+
+GpuSolver::Impl::~Impl() {
+  if (device >= 0) (void)hipSetDevice(device);
+  engine.reset();
+  for (void* q : xopened) (void)hipIpcCloseMemHandle(q);
+  if (xbuf) (void)hipFree(xbuf);
+  if (xpeer_d) (void)hipFree(xpeer_d);
+  if (gexec) (void)hipGraphExecDestroy(gexec);
+  if (graph) (void)hipGraphDestroy(graph);
+  for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
+                    (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
+                    (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
+                    (void*)plru_meta, (void*)plru_stats})
+    if (ptr) (void)hipFree(ptr);
+  if (status_h) (void)hipHostFree(status_h);
+  if (hlines_h) (void)hipHostFree(hlines_h);
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+SmoStatus GpuSolver::Impl::read_status() const {
+  SmoStatus s;
+  std::atomic_thread_fence(std::memory_order_acquire);
+  memcpy(&s, (const void*)status_h, sizeof(s));
+  return s;
+}
+
+void GpuSolver::Impl::init_ctrl(int64_t iter0, float b_hi, float b_lo) {
+  SmoCtrl c;
+  memset(&c, 0, sizeof(c));
+  c.iter = (int32_t)iter0;
+  c.line_hi = c.line_lo = -1;
+  c.b_hi = b_hi;
+  c.b_lo = b_lo;
+  HIP_CHECK(hipMemcpyAsync(ctrl, &c, sizeof(c), hipMemcpyHostToDevice, stream));
+  memset(status_h, 0, sizeof(SmoStatus));
+}
+
+void GpuSolver::Impl::wait_event(hipEvent_t e) {
+  // bounded wait with async-error polling (SURVEY §5.3 watchdog)
+  auto t0 = Clock::now();
+  const double limit = p.watchdog_s;
+  int spins = 0;
+  while (true) {
+    hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIP_CHECK(q);
+    if (world > 1) {
+      std::string err = comm->async_error();
+      if (!err.empty()) {
+        comm->abort();
+        fail("collective failed on rank " + std::to_string(rank) + ": " + err);
+      }
+    }
+    if (secs_since(t0) > limit) {
+      if (world > 1) comm->abort();
+      fail("watchdog: SMO block did not finish within " + std::to_string(limit) + " s");
+    }
+    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+GpuSolver::GpuSolver(const SolverParams& p, Communicator* comm, int device) : impl_(new Impl) {
+  auto& m = *impl_;
+  m.p = p;
+  if (!comm) {
+    m.own_comm = make_local_comm();
+    comm = m.own_comm.get();
+  }
+  m.comm = m.outer = comm;
+  m.rank = m.outer_rank = comm->rank();
+  m.world = m.outer_world = comm->size();
+  m.device = device;
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
+  HIP_CHECK(hipEventCreateWithFlags(&m.ev[0], hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&m.ev[1], hipEventDisableTiming));
+}
+
+GpuSolver::~GpuSolver() = default;
+const GpuSetupInfo& GpuSolver::info() const { return impl_->info; }
+
+namespace {
+
+// Fast geometry of the one-device persistent dense engine: <= 256 workgroups
+// of <= 1024 rows (4 register rows per thread, one poll batch per 64 lanes).
+constexpr int64_t kReplicateMaxRows = 256 * 1024;
+
+// every rank on its own physical device (PCI bus id; one node)?
+bool distinct_devices(GpuSolver::Impl& m) {
+  struct Id {
+    char bus[32];
+  } me{};
+  if (hipDeviceGetPCIBusId(me.bus, sizeof(me.bus), m.device) != hipSuccess) {
+    (void)hipGetLastError();
+    snprintf(me.bus, sizeof(me.bus), "pid%d-dev%d", (int)getpid(), m.device);
+  }
+  std::vector<Id> all((size_t)m.world);
+  m.allgather_bytes(&me, all.data(), sizeof(Id));
+  for (int a = 0; a < m.world; ++a)
+    for (int b = a + 1; b < m.world; ++b)
+      if (strncmp(all[a].bus, all[b].bus, sizeof(Id::bus)) == 0) return false;
+  return true;
+}
+
+}  // namespace
+
+GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int d, const float* yh) {
+  auto& m = *impl_;
+  HIP_CHECK(hipSetDevice(m.device));
+  DPSVM_CHECK(n >= 2 && d >= 1, "need at least 2 samples and 1 feature");
+  DPSVM_CHECK(n < (int64_t)1 << 31, "n must fit in 31 bits (packed selection keys)");
+  DPSVM_CHECK(m.p.C > 0.f, "C must be > 0");
+  DPSVM_CHECK(m.p.rows_per_group % kFusedThreads == 0 && m.p.rows_per_group >= 0,
+              "rows_per_group must be a multiple of 256");
+  m.n = n;
+  m.d = d;
+  m.dp = pad_features(d);
+  m.gamma = resolve_gamma(m.p.gamma, d);
+  size_t freeb = 0, totalb = 0;
+  HIP_CHECK(hipMemGetInfo(&freeb, &totalb));
+
+  // ---- data-parallel policy (world > 1): shard the rows or solve it all ----
+  if (m.world > 1 && m.p.dp_policy != 1 && n_x_rows == n && m.p.x_mode != 2) {
+    bool rep = m.p.dp_policy == 2;
+    if (!rep) {
+      const bool distinct = distinct_devices(m);  // collective: every rank calls it
+      const double gram_bytes = (double)n * (double)round_up(n, 256) * 4.0;
+      const bool fits = gram_bytes + (double)n * m.dp * 4.0 < m.p.cache_frac * (double)freeb - 512.0 * (1 << 20);
+      rep = distinct && fits && n <= kReplicateMaxRows && !m.p.force_cache && m.p.persist != 1 &&
+            m.p.exchange != 1 && !m.p.force_collectives && m.p.use_graph;
+      rep = m.all_agree(rep, m.comm, m.world);
+    }
+    if (rep) {
+      // every rank solves the whole problem on its own device: no per-iteration
+      // communication; the caller's communicator still verifies the result
+      m.own_comm = make_local_comm();
+      m.comm = m.own_comm.get();
+      m.rank = 0;
+      m.world = 1;
+      m.info.dp_policy = "replicate";
+    }
+  }
+
+  const Shard sh = shard_of(n, m.rank, m.world);
+  m.nl = sh.size;
+  m.off = sh.offset;
+  const int64_t nl_max = (n + m.world - 1) / m.world;
+  m.G = std::max<int64_t>(1, (nl_max + kStepRows - 1) / kStepRows);
+  // fused / persistent geometry, rows per workgroup a multiple of 256.  Cache
+  // mode: ~cache_groups workgroups (the X pass wants every CU).  Dense mode:
+  // ~128 publishers over all ranks, <= 1024 rows per workgroup (dense_rows_min,
+  // common.hpp; profiles/r1_dense_rows_ab.txt).  rows_per_group overrides both.
+  const int64_t wgs = std::max(1, m.p.cache_groups);
+  auto geometry = [&](int64_t rows_min) {
+    if (m.p.rows_per_group > 0) {
+      const int64_t r = m.p.rows_per_group;
+      return std::pair<int64_t, int64_t>(r, std::max<int64_t>(1, (nl_max + r - 1) / r));
+    }
+    const Geometry g = make_geometry(nl_max, rows_min, wgs);
+    return std::pair<int64_t, int64_t>(g.rows, g.groups);
+  };
+  const auto geo_cache = geometry(0);
+  const auto geo_dense = geometry(dense_rows_min(nl_max, m.world));
+  m.RBf = geo_cache.first;
+  m.Gf = geo_cache.second;
+  // lines cover every row a kernel may write (the fused X pass writes whole
+  // 256-row tiles) under either geometry
+  m.ldl = std::max<int64_t>({m.G * kStepRows, geo_cache.first * geo_cache.second, geo_dense.first * geo_dense.second});
+
+  // ---- X placement ----
+  if (n_x_rows == n) {
+    m.replicated = m.p.x_mode != 2;
+  } else {
+    DPSVM_CHECK(n_x_rows == m.nl, "x must hold all n rows (replicated) or this rank's shard rows");
+    m.replicated = false;
+  }
+  if (m.world == 1 && m.p.x_mode == 2) m.replicated = false;
+  if (m.replicated && m.p.x_mode == 0 && m.world > 1) {
+    // auto: replicate unless X would take more than 40% of free HBM (agreed)
+    const double xbytes = (double)n * m.dp * 4.0;
+    m.replicated = m.all_agree(xbytes <= 0.4 * (double)freeb, m.comm, m.world);
+    DPSVM_CHECK(m.replicated || n_x_rows == n, "internal: partition fallback needs full x");
+  }
+  const int64_t x_row0 = m.replicated ? 0 : m.off;
+  m.x_rows = m.replicated ? round_up(std::max<int64_t>(n, m.off + m.ldl), 128) + 128 : m.ldl + 128;
+  m.x = dmalloc<float>((size_t)m.x_rows * m.dp, &m.bytes);
+  HIP_CHECK(hipMemsetAsync(m.x, 0, (size_t)m.x_rows * m.dp * 4, m.stream));
+  {
+    const float* src = xh;
+    int64_t rows = n_x_rows;
+    if (!m.replicated && n_x_rows == n) {
+      src = xh + (size_t)m.off * d;
+      rows = m.nl;
+    }
+    if (rows > 0)
+      HIP_CHECK(hipMemcpy2DAsync(m.x, (size_t)m.dp * 4, src, (size_t)d * 4, (size_t)d * 4, (size_t)rows,
+                                 hipMemcpyHostToDevice, m.stream));
+  }
+  // ---- global vectors (n padded so padded local rows index in-bounds) ----
+  const int64_t n_pad = round_up(std::max<int64_t>(n, m.off + m.ldl), 128) + 128;
+  m.xsq = dmalloc<float>((size_t)n_pad, &m.bytes);
+  m.y = dmalloc<float>((size_t)n_pad, &m.bytes);
+  m.alpha = dmalloc<float>((size_t)n_pad, &m.bytes);
+  HIP_CHECK(hipMemsetAsync(m.xsq, 0, n_pad * 4, m.stream));
+  HIP_CHECK(hipMemsetAsync(m.y, 0, n_pad * 4, m.stream));
+  HIP_CHECK(hipMemsetAsync(m.alpha, 0, n_pad * 4, m.stream));
+  m.h_y.assign(yh, yh + n);
+  for (auto& v : m.h_y) v = v > 0 ? 1.f : -1.f;
+  HIP_CHECK(hipMemcpyAsync(m.y, m.h_y.data(), n * 4, hipMemcpyHostToDevice, m.stream));
+  if (m.replicated) {
+    launch::row_sqnorm(m.x, n, m.dp, m.dp, m.xsq, m.stream);  // one launch (was n)
+  } else {
+    // local norms, then all-gather the shards into the global vector
+    float* loc = dmalloc<float>((size_t)m.ldl, &m.bytes);
+    HIP_CHECK(hipMemsetAsync(loc, 0, m.ldl * 4, m.stream));
+    launch::row_sqnorm(m.x, m.nl, m.dp, m.dp, loc, m.stream);
+    std::vector<float> all((size_t)m.ldl * m.world), mine((size_t)m.ldl);
+    if (m.world > 1 && m.comm->device_memory()) {
+      float* gbuf = dmalloc<float>((size_t)m.ldl * m.world, &m.bytes);
+      m.comm->allgather(loc, gbuf, m.ldl * 4, m.stream);
+      HIP_CHECK(hipMemcpyAsync(all.data(), gbuf, all.size() * 4, hipMemcpyDeviceToHost, m.stream));
+      HIP_CHECK(hipStreamSynchronize(m.stream));
+      (void)hipFree(gbuf);
+    } else {
+      HIP_CHECK(hipMemcpyAsync(mine.data(), loc, m.ldl * 4, hipMemcpyDeviceToHost, m.stream));
+      HIP_CHECK(hipStreamSynchronize(m.stream));
+      m.comm->allgather(mine.data(), all.data(), m.ldl * 4, nullptr);
+    }
+    std::vector<float> g((size_t)n, 0.f);
+    for (int r = 0; r < m.world; ++r) {
+      Shard s = shard_of(n, r, m.world);
+      std::copy(all.begin() + (size_t)r * m.ldl, all.begin() + (size_t)r * m.ldl + s.size, g.begin() + s.offset);
+    }
+    HIP_CHECK(hipMemcpyAsync(m.xsq, g.data(), n * 4, hipMemcpyHostToDevice, m.stream));
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    (void)hipFree(loc);
+  }
+  m.f = dmalloc<float>((size_t)m.ldl, &m.bytes);
+  HIP_CHECK(hipMemsetAsync(m.f, 0, m.ldl * 4, m.stream));
+  m.partials = dmalloc<uint64_t>((size_t)2 * m.G, &m.bytes);
+  m.ctrl = dmalloc<SmoCtrl>(1, &m.bytes);
+  HIP_CHECK(hipHostMalloc((void**)&m.status_h, sizeof(SmoStatus), hipHostMallocMapped));
+  HIP_CHECK(hipHostGetDevicePointer((void**)&m.status_d, m.status_h, 0));
+  if (!m.replicated) {
+    const int64_t rb = round_up((int64_t)sizeof(CandRecord) + 2LL * m.dp * 4, 64);
+    m.my_record = dmalloc<uint8_t>((size_t)rb, &m.bytes);
+    m.records = dmalloc<uint8_t>((size_t)rb * m.world, &m.bytes);
+    HIP_CHECK(hipMemsetAsync(m.records, 0, rb * m.world, m.stream));
+    m.args.rec_bytes = rb;
+    m.h_records.assign((size_t)rb * m.world, 0);
+  }
+  m.h_partials.assign((size_t)2 * m.G, kKeyNone);
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+
+  // ---- kernel-row cache sizing (288 GB HBM: the Gram shard is usually resident) ----
+  HIP_CHECK(hipMemGetInfo(&freeb, &totalb));
+  const double line_bytes = (double)m.ldl * 4.0;
+  double budget = m.p.cache_frac * (double)freeb - 256.0 * 1024 * 1024;
+  if (m.p.cache_mb > 0) budget = std::min(budget, m.p.cache_mb * 1024.0 * 1024.0);
+  int64_t want_lines = (int64_t)(budget / line_bytes);
+  if (m.p.cache_lines > 0) want_lines = std::min<int64_t>(want_lines, m.p.cache_lines);
+  m.dense = m.replicated && want_lines >= n && !m.p.force_cache;
+  m.dense = m.all_agree(m.dense, m.comm, m.world);  // free memory can differ per device
+  if (m.dense) {
+    m.RBf = geo_dense.first;
+    m.Gf = geo_dense.second;
+  }
+  // engine candidates.  Persistent engines need the in-kernel exchange (set up
+  // below) and a co-resident grid (census); the one-launch-per-iteration
+  // engines are the fallbacks.
+  const bool fused_lru_ok = !m.dense && m.replicated && launch::smo_fused_lru_supported(m.dp) && m.p.cache_engine == 0;
+  const bool plru_cand = fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
+                         m.p.use_graph && !m.p.force_collectives &&
+                         launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
+  if (plru_cand) {
+    // every workgroup's private metadata copy comes out of the line budget (upper bound: L = n)
+    const double meta_bytes = (double)m.Gf * launch::plru_stride_words(n, n) * 4.0;
+    want_lines = std::min<int64_t>(want_lines, (int64_t)((budget - meta_bytes) / line_bytes));
+  }
+  const bool pdense_cand = m.dense && (m.p.persist == 2 || (m.p.persist == 0 && m.p.exchange != 1 && m.p.use_graph &&
+                                                            !m.p.force_collectives)) &&
+                           m.RBf <= 12 * kFusedThreads && m.Gf <= 256;
+  m.L = m.dense ? n : std::max<int64_t>(2, std::min<int64_t>(want_lines, n));
+  DPSVM_CHECK(m.L * line_bytes <= (double)freeb, "not enough device memory for 2 kernel-row lines");
+  m.lines = dmalloc<float>((size_t)m.L * m.ldl, &m.bytes);
+  if (m.dense || fused_lru_ok) {
+    m.pf = dmalloc<uint64_t>((size_t)4 * m.Gf, &m.bytes);
+    m.rf = dmalloc<FusedRec>(2, &m.bytes);
+    if (!m.dense) m.rcf = dmalloc<FusedCacheRec>(2, &m.bytes);
+  }
+  if (!m.dense) {
+    m.slot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
+    m.key_of = dmalloc<int32_t>((size_t)m.L, &m.bytes);
+    m.ref = dmalloc<uint8_t>((size_t)m.L, &m.bytes);
+    if (m.p.host_cache_lines > 0) {
+      // pinned host tier: a FIFO victim cache the row kernel spills to and
+      // fetches from with zero-copy PCIe accesses (no host round trip)
+      m.H = m.p.host_cache_lines;
+      HIP_CHECK(hipHostMalloc((void**)&m.hlines_h, (size_t)m.H * m.ldl * 4, hipHostMallocMapped));
+      HIP_CHECK(hipHostGetDevicePointer((void**)&m.hlines_d, m.hlines_h, 0));
+      m.hslot_of = dmalloc<int32_t>((size_t)n, &m.bytes);
+      m.hkey_of = dmalloc<int32_t>((size_t)m.H, &m.bytes);
+    }
+  }
+
+  SmoArgs& a = m.args;
+  a.x = m.x;
+  a.xsq = m.xsq;
+  a.y = m.y;
+  a.alpha = m.alpha;
+  a.f = m.f;
+  a.lines = m.lines;
+  a.ldl = m.ldl;
+  a.slot_of = m.slot_of;
+  a.key_of = m.key_of;
+  a.ref = m.ref;
+  a.hlines = m.hlines_d;
+  a.hslot_of = m.hslot_of;
+  a.hkey_of = m.hkey_of;
+  a.H = (int32_t)m.H;
+  a.partials = m.partials;
+  a.ctrl = m.ctrl;
+  a.status = m.status_d;
+  a.records = m.records;
+  a.my_record = m.my_record;
+  a.n = n;
+  a.nl = m.nl;
+  a.off = m.off;
+  a.x_row0 = x_row0;
+  a.d = d;
+  a.dp = m.dp;
+  a.G = (int32_t)m.G;
+  a.L = (int32_t)m.L;
+  a.world = m.world;
+  a.cache_mode = m.dense ? kCacheDense : kCacheLRU;
+  a.partitioned = m.replicated ? 0 : 1;
+  a.spec = (m.replicated && !m.dense) ? std::max(0, std::min(m.p.spec_rows, kNQ - 2)) : 0;
+  a.clip = (int)m.p.clip;
+  a.C = m.p.C;
+  a.gamma = m.gamma;
+  a.eps = m.p.eps;
+  a.tau = m.p.tau;
+  a.max_iter = m.p.max_iter;
+  a.fused_rows = (int32_t)m.RBf;
+  a.fused_G = (int32_t)m.Gf;
+  a.stamps = nullptr;
+  a.census = nullptr;
+  a.census_ticks = 0;
+  if (const char* sp = std::getenv("DPSVM_STAMPS")) {  // diagnostics only (bench/stamps_report.py)
+    m.stamps_path = std::string(sp) + ".rank" + std::to_string(m.rank);
+    const size_t cnt = (size_t)kStampRing * 2 * kStampSlots;
+    m.stamps = dmalloc<uint64_t>(cnt, &m.bytes);
+    HIP_CHECK(hipMemsetAsync(m.stamps, 0, cnt * 8, m.stream));
+    a.stamps = m.stamps;
+  }
+
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  hipDeviceProp_t prop;
+  HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+  m.info.device = dev;
+  m.info.device_name = prop.name[0] ? std::string(prop.name) : std::string(prop.gcnArchName);
+  if (m.info.device_name.empty() || m.info.device_name == " ") m.info.device_name = prop.gcnArchName;
+  m.info.n = n;
+  m.info.n_local = m.nl;
+  m.info.offset = m.off;
+  m.info.d = d;
+  m.info.dp = m.dp;
+  m.info.x_replicated = m.replicated;
+  m.info.cache_lines = m.L;
+  m.info.blocks = (int)m.G;
+
+  // ---- per-iteration key exchange and engine ----
+  a.xpeer = nullptr;
+  a.xrank = 0;
+  a.xworld = 0;
+  a.xstride = kXchGranules;
+  a.xpoll_kb = 0;
+  a.xpoll_sleep = 1;
+  a.xtimeout_ticks = 0;
+  m.xch = false;
+  const bool want_xch = (m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || pdense_cand ||
+                        plru_cand;
+  if (want_xch) {
+    const bool ok = m.setup_exchange();
+    DPSVM_CHECK(ok || (m.p.exchange != 2 && m.p.persist != 2),
+                "peer exchange requested (exchange=peer / persist=on) but its self test failed (" + m.xch_diag + ")");
+    if (ok) {
+      m.xch = true;
+      a.xpeer = m.xpeer_d;
+      a.xrank = m.rank;
+      a.xworld = m.world;
+      a.xstride = (int32_t)m.xstride;
+      a.xpoll_kb = m.p.xch_poll_batch;
+      a.xpoll_sleep = std::max(0, m.p.xch_sleep);
+      a.xtimeout_ticks = (int64_t)(std::max(1e-6, m.p.xch_timeout_s) * 1e8);
+    } else if (m.info.engine_note.empty()) {
+      m.info.engine_note = "peer exchange refused: " + m.xch_diag;
+    }
+  }
+  if (m.dense) m.kind = pdense_cand && m.xch ? EngineKind::PersistDense : EngineKind::FusedDense;
+  else if (fused_lru_ok) m.kind = plru_cand && m.xch ? EngineKind::PersistCache : EngineKind::FusedCache;
+  else m.kind = EngineKind::Chain;
+  if (m.persistent() && !m.census(m.kind)) {
+    DPSVM_CHECK(m.p.persist != 2, "persistent engine requested (persist=on) but its grid is not co-resident (" +
+                                      m.info.engine_note + ")");
+    m.kind = m.dense ? EngineKind::FusedDense : EngineKind::FusedCache;
+  }
+  if (m.kind == EngineKind::PersistCache) {
+    a.plru_stride = launch::plru_stride_words(n, m.L);
+    m.plru_meta = dmalloc<int32_t>((size_t)m.Gf * a.plru_stride, &m.bytes);
+    m.plru_stats = dmalloc<int64_t>(8, &m.bytes);
+    a.plru_meta = m.plru_meta;
+  } else {
+    a.plru_meta = nullptr;
+    a.plru_stride = 0;
+  }
+  m.engine = gpu::make_engine(m.kind);
+  m.info.iteration = engine_name(m.kind);
+  m.info.exchange_mem = m.xch ? m.xch_mem : "none";
+  m.info.exchange = m.xch ? (m.world > 1 ? "peer" : "loopback")
+                          : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
+  m.info.rows_per_group = m.fused() ? m.RBf : kStepRows;
+  m.info.groups = m.fused() ? m.Gf : m.G;
+  m.info.poll_batch = m.xch ? launch::poll_batch(a) : 0;
+  m.info.bytes_device = m.bytes;
+  return m.info;
+}
+
+}  // namespace dpsvm

@@ -1,0 +1,256 @@
+// The timed SMO loop of the device solver (reference: svmTrainMain.cpp:206-314),
+// checkpoints, fault injection and invariant checks (§5.2-5.3).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include <unistd.h>
+
+#include "gpu_impl.hpp"
+#include "../runtime/timer.hpp"
+#include "../runtime/trace.hpp"
+
+namespace dpsvm {
+
+using gpu::dmalloc;
+
+void gpu_local_decision(GpuSolver::Impl& m, const std::vector<float>& alpha, float* out_dev);  // gpu_predict.hip
+
+// Checkpoint snapshot (stream drained by the caller): alpha is replicated,
+// the f shards are all-gathered; rank 0 writes.
+void GpuSolver::Impl::snapshot(const SmoStatus& st) {
+  Checkpoint ck;
+  ck.n = n;
+  ck.d = d;
+  ck.C = p.C;
+  ck.gamma = gamma;
+  ck.eps = p.eps;
+  ck.clip = (int)p.clip;
+  ck.iter = st.iter;
+  ck.b_hi = st.b_hi;
+  ck.b_lo = st.b_lo;
+  ck.alpha.resize((size_t)n);
+  HIP_CHECK(hipMemcpy(ck.alpha.data(), alpha, n * 4, hipMemcpyDeviceToHost));
+  // the latest pair's alphas may still be pending in the last kernel's record
+  // (exact; the host-mapped status refreshes only every kStatusEvery)
+  const gpu::Pending q = engine->pending(*this);
+  if (q.valid) {
+    ck.iter = q.iter;
+    ck.b_hi = q.b_hi;
+    ck.b_lo = q.b_lo;
+    if (q.i_hi >= 0) {
+      ck.alpha[q.i_lo] = q.a_lo;
+      ck.alpha[q.i_hi] = q.a_hi;
+    }
+  }
+  std::vector<float> floc((size_t)ldl, 0.f), fall((size_t)ldl * world);
+  HIP_CHECK(hipMemcpy(floc.data(), f, nl * 4, hipMemcpyDeviceToHost));
+  if (world > 1) {
+    if (comm->device_memory()) {
+      size_t tb = 0;
+      float* gb = dmalloc<float>((size_t)ldl * world, &tb);
+      HIP_CHECK(hipMemcpy(gb + (size_t)rank * ldl, f, ldl * 4, hipMemcpyDeviceToDevice));
+      comm->allgather(gb + (size_t)rank * ldl, gb, ldl * 4, stream);
+      HIP_CHECK(hipMemcpyAsync(fall.data(), gb, fall.size() * 4, hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      (void)hipFree(gb);
+    } else {
+      comm->allgather(floc.data(), fall.data(), ldl * 4, nullptr);
+    }
+  } else {
+    fall = floc;
+  }
+  ck.f.assign((size_t)n, 0.f);
+  for (int r = 0; r < world; ++r) {
+    Shard s = shard_of(n, r, world);
+    std::copy(fall.begin() + (size_t)r * ldl, fall.begin() + (size_t)r * ldl + s.size, ck.f.begin() + s.offset);
+  }
+  // replicated solve: every rank holds everything, the caller's rank 0 writes
+  if (rank == 0 && outer_rank == 0) write_checkpoint(p.checkpoint_path, ck);
+}
+
+SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progress) {
+  auto& m = *impl_;
+  HIP_CHECK(hipSetDevice(m.device));
+  SolveResult res;
+  res.world = m.world;
+  res.cache_lines = m.L;
+  auto ts0 = Clock::now();
+
+  // ---- state init (alpha = 0, f = -y, empty cache) or resume ----
+  int64_t iter0 = 0;
+  float b_hi0 = 0.f, b_lo0 = 0.f;
+  HIP_CHECK(hipMemsetAsync(m.alpha, 0, m.n * 4, m.stream));
+  if (resume) {
+    check_resume(*resume, m.n, m.d, m.p, m.gamma);
+    HIP_CHECK(hipMemcpyAsync(m.alpha, resume->alpha.data(), m.n * 4, hipMemcpyHostToDevice, m.stream));
+    iter0 = resume->iter;
+    b_hi0 = resume->b_hi;
+    b_lo0 = resume->b_lo;
+  }
+  if (resume && (int64_t)resume->f.size() == m.n) {
+    HIP_CHECK(hipMemcpyAsync(m.f, resume->f.data() + m.off, m.nl * 4, hipMemcpyHostToDevice, m.stream));
+  } else if (resume) {
+    // f_j = sum_i alpha_i y_i K(i, j) - y_j via the predict GEMM (b = 0)
+    gpu_local_decision(m, resume->alpha, m.f);
+    std::vector<float> fh((size_t)m.nl);
+    HIP_CHECK(hipMemcpy(fh.data(), m.f, m.nl * 4, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < m.nl; ++j) fh[j] -= m.h_y[m.off + j];
+    HIP_CHECK(hipMemcpy(m.f, fh.data(), m.nl * 4, hipMemcpyHostToDevice));
+  } else {
+    launch::init_f(m.y, m.off, m.nl, m.f, m.stream);
+  }
+  if (!m.dense) {
+    launch::fill_i32(m.slot_of, m.n, -1, m.stream);
+    launch::fill_i32(m.key_of, m.L, -1, m.stream);
+    HIP_CHECK(hipMemsetAsync(m.ref, 0, m.L, m.stream));
+    if (m.H > 0) {
+      launch::fill_i32(m.hslot_of, m.n, -1, m.stream);
+      launch::fill_i32(m.hkey_of, m.H, -1, m.stream);
+    }
+  }
+  m.engine->prepare(m);
+  m.init_ctrl(iter0, b_hi0, b_lo0);
+  if (m.xch) HIP_CHECK(hipMemsetAsync(m.xbuf, 0, (size_t)m.xregion * 8, m.stream));  // tags restart at iter0 + 1
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  if (m.world > 1) m.comm->barrier();
+  res.t_setup = secs_since(ts0);
+
+  // ================= timed region: the SMO loop (svmTrainMain.cpp:206-314) =================
+  trace::Range loop_range("dpsvm/solve");
+  const int64_t fault_iter = trace::fault_nan_iter();
+  const int64_t exit_iter = trace::fault_exit_iter(m.outer_rank);
+  bool fault_done = false;
+  auto t0 = Clock::now();
+  m.engine->seed(m, iter0, b_hi0, b_lo0, res);
+  const int B = m.engine->block(m.p);
+  int64_t blocks = 0;
+  const int64_t max_blocks = (m.p.max_iter - iter0) / B + 3;
+  int64_t last_ck = iter0, last_log = iter0;
+  SmoStatus st{};
+  while (true) {
+    m.engine->run_block(m, B);
+    HIP_CHECK(hipEventRecord(m.ev[blocks & 1], m.stream));
+    if (blocks > 0) {
+      m.wait_event(m.ev[(blocks - 1) & 1]);
+      st = m.read_status();
+      if (progress && m.p.log_every > 0 && st.iter / m.p.log_every != last_log / m.p.log_every) {
+        last_log = st.iter;
+        progress(Progress{st.iter, st.b_hi, st.b_lo, secs_since(t0), st.hits, st.misses});
+      }
+      if (st.done != kRunning) break;
+      if (exit_iter >= 0 && st.iter >= exit_iter) {
+        // DPSVM_FAULT=exit@K:R: this rank's process dies mid-solve
+        fprintf(stderr, "[dpsvm] fault injection: rank %d exits at iteration %lld\n", m.outer_rank,
+                (long long)st.iter);
+        fflush(stderr);
+        _exit(3);
+      }
+      if (fault_iter >= 0 && !fault_done && st.iter >= fault_iter) {
+        // DPSVM_FAULT=nan@K: poison f[0]; lands between two enqueued blocks
+        static const float qnan = std::nanf("");
+        HIP_CHECK(hipMemcpyAsync(m.f, &qnan, 4, hipMemcpyHostToDevice, m.stream));
+        fault_done = true;
+      }
+      if (m.p.checkpoint_every > 0 && !m.p.checkpoint_path.empty() && st.iter - last_ck >= m.p.checkpoint_every) {
+        // drain the in-flight block, then snapshot (alpha replicated, f gathered)
+        m.wait_event(m.ev[blocks & 1]);
+        st = m.read_status();
+        if (st.done == kRunning) {
+          m.snapshot(st);
+          last_ck = st.iter;
+        }
+      }
+    }
+    ++blocks;
+    DPSVM_CHECK(blocks <= max_blocks + 2, "SMO loop did not terminate (internal error)");
+  }
+  m.wait_event(m.ev[blocks & 1]);  // the overshoot block (early-exit kernels)
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  res.t_solve = secs_since(t0);
+  res.t_gram = m.engine->gram_seconds();
+  if (m.p.checkpoint_every > 0 && !m.p.checkpoint_path.empty()) {
+    st = m.read_status();
+    if (st.done == kMaxIter) m.snapshot(st);  // resumable continuation point
+  }
+  // ================= end of timed region =================
+
+  if (trace::verify_enabled()) {
+    // invariants: alpha in [0, C]; f consistent with alpha, i.e. the
+    // incrementally updated f_j equals sum_i alpha_i y_i K(i, j) - y_j recomputed
+    // from scratch (MFMA predict GEMM); float drift over 10^5 updates stays ~1e-5.
+    std::vector<float> ah((size_t)m.n);
+    HIP_CHECK(hipMemcpy(ah.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < m.n; ++i)
+      if (!(ah[i] >= 0.f && ah[i] <= m.p.C))
+        fail("DPSVM_VERIFY: alpha[" + std::to_string(i) + "] = " + std::to_string(ah[i]) + " outside [0, C]");
+    std::vector<float> fd((size_t)m.nl), fr((size_t)m.nl);
+    HIP_CHECK(hipMemcpy(fd.data(), m.f, m.nl * 4, hipMemcpyDeviceToHost));
+    size_t tb = 0;
+    float* dref = dmalloc<float>((size_t)m.nl, &tb);
+    gpu_local_decision(m, ah, dref);
+    HIP_CHECK(hipMemcpy(fr.data(), dref, m.nl * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(dref);
+    double err = 0.0;
+    for (int64_t j = 0; j < m.nl; ++j) {
+      const double ref = (double)fr[j] - m.h_y[m.off + j];
+      const double e = std::fabs((double)fd[j] - ref) / (1.0 + std::fabs(ref));
+      err = std::isfinite(e) ? std::max(err, e) : INFINITY;
+    }
+    res.verify_f_err = err;
+    const char* te = std::getenv("DPSVM_VERIFY_FTOL");
+    const double tol = te ? atof(te) : 1e-3;
+    if (!(err <= tol)) fail("DPSVM_VERIFY: f inconsistent with alpha (max relative error " + std::to_string(err) + ")");
+  }
+  if ((m.outer_world > 1 || m.p.force_collectives) && (m.p.verify_ranks || trace::verify_enabled())) {
+    // cross-rank consistency (on by default at world > 1): every rank must hold
+    // bit-identical alphas; one 16-byte all-reduce per solve
+    std::vector<float> ah((size_t)m.n);
+    HIP_CHECK(hipMemcpy(ah.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
+    const uint64_t h = trace::hash_floats(ah.data(), ah.size());
+    uint64_t hk[2] = {h, ~h};
+    Communicator* c = m.outer;
+    if (c->device_memory()) {
+      size_t tb = 0;
+      uint64_t* dk = dmalloc<uint64_t>(2, &tb);
+      HIP_CHECK(hipMemcpy(dk, hk, 16, hipMemcpyHostToDevice));
+      c->allreduce_min_u64(dk, 2, m.stream);
+      HIP_CHECK(hipMemcpyAsync(hk, dk, 16, hipMemcpyDeviceToHost, m.stream));
+      HIP_CHECK(hipStreamSynchronize(m.stream));
+      (void)hipFree(dk);
+    } else {
+      c->allreduce_min_u64(hk, 2, nullptr);
+    }
+    if (hk[0] != h || ~hk[1] != h) fail("DPSVM_VERIFY: ranks hold different alphas (diverged)");
+  }
+  st = m.read_status();
+  res.iters = st.iter;
+  res.status = st.done;
+  if (st.done == kCommFail)
+    fail("peer exchange: a rank stopped publishing its selection keys (timeout after iteration " +
+         std::to_string(st.iter) + ")");
+  res.b_hi = st.b_hi;
+  res.b_lo = st.b_lo;
+  res.b = (st.b_lo + st.b_hi) / 2.0f;
+  res.cache_hits = st.hits;
+  res.cache_misses = st.misses;
+  res.rows_computed += st.rows_computed;
+  res.x_passes += st.x_passes;
+  res.spec_rows = st.spec_rows;
+  res.host_hits = st.host_hits;
+  res.host_cache_lines = m.H;
+  res.world = m.outer_world;
+  if (m.stamps) {
+    std::vector<uint64_t> h((size_t)kStampRing * 2 * kStampSlots);
+    HIP_CHECK(hipMemcpy(h.data(), m.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* fp = fopen(m.stamps_path.c_str(), "wb")) {
+      fwrite(h.data(), 8, h.size(), fp);
+      fclose(fp);
+    }
+  }
+  res.alpha.resize((size_t)m.n);
+  HIP_CHECK(hipMemcpy(res.alpha.data(), m.alpha, m.n * 4, hipMemcpyDeviceToHost));
+  return res;
+}
+
+}  // namespace dpsvm

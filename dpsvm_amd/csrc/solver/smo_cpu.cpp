@@ -134,7 +134,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
   int64_t iter0 = 0;
   float b_hi = 0.f, b_lo = 0.f;
   if (resume) {
-    DPSVM_CHECK(resume->n == n && (int64_t)resume->alpha.size() == n, "checkpoint n mismatch");
+    check_resume(*resume, n, d, p, gamma);
     alpha = resume->alpha;
     iter0 = resume->iter;
     b_hi = resume->b_hi;
@@ -180,6 +180,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
   const int T = pool.size();
   std::vector<uint64_t> th_hi(T), th_lo(T);
   const int64_t fault_iter = trace::fault_nan_iter();
+  const int64_t exit_iter = trace::fault_exit_iter(rank);
   trace::Range loop_range("dpsvm/smo_loop_cpu");
   auto t0 = Clock::now();
   int64_t iter = iter0;
@@ -266,6 +267,11 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
       keys_ready = true;
     }
     ++iter;
+    if (exit_iter >= 0 && iter >= exit_iter) {  // DPSVM_FAULT=exit@K:R: this rank's process dies
+      fprintf(stderr, "[dpsvm] fault injection: rank %d exits at iteration %lld\n", rank, (long long)iter);
+      fflush(stderr);
+      _exit(3);
+    }
     if (fault_iter >= 0 && iter == fault_iter && nl > 0) {  // DPSVM_FAULT
       f[0] = std::nanf("");
       keys_ready = false;
@@ -311,7 +317,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
     if (!(err <= (te ? atof(te) : 1e-3)))
       fail("DPSVM_VERIFY: f inconsistent with alpha (max relative error " + std::to_string(err) + ")");
   }
-  if (world > 1 && trace::verify_ranks_enabled()) {
+  if (world > 1 && (p.verify_ranks || trace::verify_enabled())) {
     // cross-rank consistency: every rank must hold bit-identical alphas
     const uint64_t h = trace::hash_floats(alpha.data(), alpha.size());
     uint64_t hk[2] = {h, ~h};

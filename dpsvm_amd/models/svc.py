@@ -49,6 +49,15 @@ _CLIP = {"independent": 0, "box": 1}
 _XMODE = {"auto": 0, "replicated": 1, "partitioned": 2}
 _EXCHANGE = {"auto": 0, "allreduce": 1, "peer": 2}
 _PERSIST = {"auto": 0, "off": 1, "on": 2}
+_CACHE_ENGINE = {"fused": 0, "chain": 1}
+_XCH_MEM = {"auto": 0, "uncached": 1, "coarse": 2}
+_DP = {"auto": 0, "shard": 1, "replicate": 2}
+
+
+def _pick(table: dict, value: str, name: str) -> int:
+    if value not in table:
+        raise ValueError(f"{name} must be one of {list(table)}, got {value!r}")
+    return table[value]
 
 
 @dataclass
@@ -78,6 +87,20 @@ class SVCConfig:
     exchange: str = "auto"          # per-iteration key exchange (dense mode): auto | allreduce | peer
     persist: str = "auto"           # engine: auto | off (one launch per iteration) | on (persistent, dense or cache mode)
     persist_block: int = 2048       # SMO iterations per persistent launch
+    # engine / geometry selection (all recorded in setup_info_ and the run summaries)
+    dp: str = "auto"                # world > 1: auto | shard (rows split) | replicate (every rank solves it all)
+    force_cache: bool = False       # kernel-row cache mode even when the Gram fits
+    cache_engine: str = "fused"     # cache mode, one launch per iteration: fused | chain
+    cache_groups: int = 256         # cache mode workgroups per rank
+    rows_per_group: int = 0         # rows per workgroup of the fused/persistent engines (0 auto; multiple of 256)
+    xch_poll_batch: int = 0         # peer exchange: publications per lane per poll round (0 auto)
+    xch_sleep: int = 1
+    xch_stride: int = 4
+    xch_mem: str = "auto"           # auto | uncached | coarse
+    xch_timeout_s: float = 120.0    # give-up bound of one in-kernel poll (then the solve fails)
+    watchdog_s: float = 1800.0
+    census_groups: int = 0          # residency census grid (tests)
+    verify_ranks: bool = True       # cross-rank alpha digest after each solve (world > 1)
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -117,6 +140,21 @@ class SVCConfig:
             raise ValueError(f"persist must be one of {list(_PERSIST)}")
         p.persist = _PERSIST[self.persist]
         p.persist_block = int(self.persist_block)
+        p.dp_policy = _pick(_DP, self.dp, "dp")
+        p.force_cache = bool(self.force_cache)
+        p.cache_engine = _pick(_CACHE_ENGINE, self.cache_engine, "cache_engine")
+        p.cache_groups = int(self.cache_groups)
+        if self.rows_per_group % 256:
+            raise ValueError("rows_per_group must be a multiple of 256")
+        p.rows_per_group = int(self.rows_per_group)
+        p.xch_poll_batch = int(self.xch_poll_batch)
+        p.xch_sleep = int(self.xch_sleep)
+        p.xch_stride = int(self.xch_stride)
+        p.xch_mem = _pick(_XCH_MEM, self.xch_mem, "xch_mem")
+        p.xch_timeout_s = float(self.xch_timeout_s)
+        p.watchdog_s = float(self.watchdog_s)
+        p.census_groups = int(self.census_groups)
+        p.verify_ranks = bool(self.verify_ranks)
         return p
 
     def device_kind(self) -> tuple[str, int]:

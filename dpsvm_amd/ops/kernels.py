@@ -127,3 +127,45 @@ def compact_positive(alpha: torch.Tensor) -> torch.Tensor:
     idx = torch.empty(a.shape[0] + 1, device=a.device, dtype=torch.int32)
     cnt = C.k_compact(a.data_ptr(), a.shape[0], idx.data_ptr(), _stream(a))
     return idx[:cnt]
+
+
+def xpass_rows(x: torch.Tensor, keys, gamma: float, rows_per_group: int = 256) -> torch.Tensor:
+    """The cache engines' X pass (xpass.hpp, v_mfma_f32_16x16x4_f32): rows
+    K(x_keys[q], x_j) for up to 16 query rows, every workgroup filling its own
+    rows_per_group-row segment of each line."""
+    C = load()
+    keys = [int(k) for k in keys]
+    if not 1 <= len(keys) <= 16:
+        raise ValueError("1..16 query rows per X pass")
+    n = x.shape[0]
+    groups = (n + rows_per_group - 1) // rows_per_group
+    span = groups * rows_per_group
+    xp, dp = _pad_rows_cols(x, row_mult=rows_per_group)
+    xsq = torch.zeros(xp.shape[0], device=x.device)
+    C.k_row_sqnorm(xp.data_ptr(), xp.shape[0], dp, dp, xsq.data_ptr(), _stream(x))
+    kd = torch.tensor(keys, dtype=torch.int32, device=x.device)
+    out = torch.full((len(keys), span), float("nan"), device=x.device)
+    C.k_xpass_rows(xp.data_ptr(), xsq.data_ptr(), n, dp, kd.data_ptr(), len(keys), float(gamma), out.data_ptr(),
+                   span, rows_per_group, _stream(x))
+    return out[:, :n]
+
+
+def fused_select(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: float, rows_per_group: int = 256):
+    """Per-workgroup (up, low) selection keys of the fused / persistent engines
+    (classification + wave-64 DPP minimum + LDS across waves): [groups, 2] u64
+    (as int64 tensor; decode with decode_key)."""
+    C = load()
+    n = f.shape[0]
+    groups = (n + rows_per_group - 1) // rows_per_group
+    pad = groups * rows_per_group + 256
+
+    def padded(t, fill):
+        o = torch.full((pad,), fill, device=f.device, dtype=torch.float32)
+        o[:n] = t.to(torch.float32)
+        return o
+
+    fp, ap, yp = padded(f, 0.0), padded(alpha, 0.0), padded(y, 1.0)
+    out = torch.zeros(2 * groups + 2, dtype=torch.int64, device=f.device)
+    C.k_fused_select(fp.data_ptr(), ap.data_ptr(), yp.data_ptr(), n, float(C_), rows_per_group, out.data_ptr(),
+                     _stream(f))
+    return out[: 2 * groups].view(groups, 2)

@@ -143,9 +143,30 @@ def gloo_comm(ctx: DistContext):
                            barrier)
 
 
+def agree(ok: bool) -> bool:
+    """True on every rank iff ``ok`` is true on every rank (host group MIN)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=_host_group())
+    return bool(t.item())
+
+
+class CommUnavailable(RuntimeError):
+    """Raised on EVERY rank when a communicator could not be built on some rank."""
+
+
 def rccl_comm(ctx: DistContext):
     """Native RCCL communicator on this rank's GPU (xGMI), bootstrapped by
-    broadcasting ncclGetUniqueId's 128 bytes through torch.distributed."""
+    broadcasting ncclGetUniqueId's 128 bytes through torch.distributed.
+
+    Every step that can fail on one rank only is followed by an agreement over
+    the host (gloo) group, so either all ranks hold an RCCL communicator or all
+    raise CommUnavailable together (no rank is left blocked in the RCCL
+    bootstrap while the others move on)."""
     import torch.distributed as dist
 
     C = load()
@@ -153,17 +174,39 @@ def rccl_comm(ctx: DistContext):
         # a real one-rank RCCL communicator (exercises the collective + graph
         # capture path on a single GPU; the solver needs force_collectives)
         return C.rccl_comm(C.rccl_unique_id(), 0, 1, ctx.local_rank)
-    obj = [C.rccl_unique_id() if ctx.rank == 0 else None]
+    uid, err = None, ""
+    if ctx.rank == 0:
+        try:
+            uid = C.rccl_unique_id()
+        except Exception as e:  # noqa: BLE001
+            err = str(e)
+    obj = [uid]
     dist.broadcast_object_list(obj, src=0, group=_host_group())
-    return C.rccl_comm(obj[0], ctx.rank, ctx.world, ctx.local_rank)
+    if not agree(obj[0] is not None):
+        raise CommUnavailable(f"ncclGetUniqueId failed on rank 0 {err}".strip())
+    comm, err = None, ""
+    try:
+        comm = C.rccl_comm(obj[0], ctx.rank, ctx.world, ctx.local_rank)
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    if not agree(comm is not None):
+        del comm
+        raise CommUnavailable(f"ncclCommInitRank failed on some rank {err}".strip())
+    return comm
 
 
 def make_comm(ctx: DistContext, kind: str = "auto"):
-    """kind: auto (rccl on GPU, gloo on CPU) | rccl | gloo | local."""
+    """kind: auto (rccl on GPU, gloo on CPU; RCCL failing on any rank falls back
+    to gloo on every rank) | rccl | gloo | local."""
     if kind == "local" or (ctx.world == 1 and kind in ("auto", "gloo")):
         return load().local_comm()
     if kind == "auto":
-        kind = "rccl" if ctx.device.startswith("cuda") else "gloo"
+        if not ctx.device.startswith("cuda"):
+            return gloo_comm(ctx)
+        try:
+            return rccl_comm(ctx)
+        except CommUnavailable:
+            return gloo_comm(ctx)
     return rccl_comm(ctx) if kind == "rccl" else gloo_comm(ctx)
 
 

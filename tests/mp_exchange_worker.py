@@ -9,7 +9,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(out: str, engine: str, n: int) -> int:
+def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
     import torch  # noqa: F401
     from dpsvm_amd import SVC
     from dpsvm_amd.parallel import init_distributed, make_comm, shutdown
@@ -19,8 +19,9 @@ def main(out: str, engine: str, n: int) -> int:
     comm = make_comm(ctx, "gloo")
     X, y = synthetic("covtype", n=n, seed=2)
     extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
+    extra.update(json.loads(extra_json))  # SVCConfig knobs (geometry, poll batch, ...)
     clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer",
-              persist="off" if engine == "fused" else "on", persist_block=257, **extra).fit(X, y, comm=comm)
+              persist="off" if engine == "fused" else "on", persist_block=257, xch_timeout_s=30.0, **extra).fit(X, y, comm=comm)
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
            "exchange_mem": clf.setup_info_["exchange_mem"],
            "iters": int(clf.n_iter_), "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
@@ -32,4 +33,12 @@ def main(out: str, engine: str, n: int) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 6000))
+    try:
+        sys.exit(main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 6000,
+                      sys.argv[4] if len(sys.argv) > 4 else "{}"))
+    except Exception as e:  # the test reads this instead of torchrun's summary
+        import traceback
+
+        with open(f"{sys.argv[1]}.rank{os.environ.get('RANK', '0')}.err", "w") as f:
+            f.write(f"{type(e).__name__}: {e}\n{traceback.format_exc()}")
+        raise

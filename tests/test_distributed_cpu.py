@@ -80,3 +80,49 @@ def test_gloo_multiprocess_identical(world):
         assert it == ref.n_iter_
         assert np.array_equal(np.frombuffer(ab, dtype=np.float32), ref.alpha_)
         assert b == ref.b_
+
+
+def _dying_worker(rank, world, port, ck, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DPSVM_FAULT="exit@300:1")
+    from dpsvm_amd.parallel import init_distributed, make_comm
+
+    ctx = init_distributed(device="cpu", timeout_s=30)
+    comm = make_comm(ctx)
+    X, y = synthetic("blobs", n=800, d=6, seed=31, sep=1.0)
+    try:
+        SVC(device="cpu", C=1.0, gamma=0.3, checkpoint_path=ck, checkpoint_every=100).fit(X, y, comm=comm)
+        q.put((rank, "finished"))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, "error: " + str(e)[:200]))
+
+
+def test_dead_rank_fails_survivors_and_checkpoint_resumes(tmp_path):
+    """rank 1's process dies mid-solve (DPSVM_FAULT=exit@300:1).
+    The surviving rank must fail (collective error), not hang, and the last
+    checkpoint resumes the job at another rank count on the same trajectory."""
+    import time
+
+    world, port, ck = 2, _free_port(), str(tmp_path / "ck.bin")
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    ps = [ctxm.Process(target=_dying_worker, args=(r, world, port, ck, q)) for r in range(world)]
+    t0 = time.time()
+    [p.start() for p in ps]
+    [p.join(timeout=120) for p in ps]
+    alive = [p for p in ps if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "a surviving rank hung after its peer died"
+    assert time.time() - t0 < 120
+    assert ps[1].exitcode == 3  # the injected death
+    msgs = dict(q.get(timeout=5) for _ in range(1))
+    assert msgs.get(0, "").startswith("error"), msgs
+    from dpsvm_amd._native import load
+
+    c = load().read_checkpoint(ck)
+    assert 0 < c.iter <= 300
+    X, y = synthetic("blobs", n=800, d=6, seed=31, sep=1.0)
+    full = SVC(device="cpu", C=1.0, gamma=0.3).fit(X, y)
+    res = SVC(device="cpu", C=1.0, gamma=0.3).fit(X, y, resume=ck)
+    assert res.n_iter_ == full.n_iter_ and np.array_equal(res.alpha_, full.alpha_)

@@ -123,3 +123,57 @@ def test_rbf_gram_symmetric_mirror(K, n, d):
     assert torch.equal(sym, sym.T)
     ref = torch.exp(-gamma * torch.cdist(x.double(), x.double()) ** 2).float()
     assert torch.allclose(sym, ref, atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("n,d,rows,nq", [(1000, 54, 256, 16), (5000, 784, 512, 7), (2600, 1100, 1024, 3),
+                                         (9000, 1024, 3072, 16)])
+def test_xpass_rows_vs_torch_and_row_kernel(K, n, d, rows, nq):
+    """The cache engines' X pass (xpass_fill: 16x16x4 f32 MFMA, double-buffered
+    X loads, multi-chunk query staging for d > 1008) vs a float64 torch
+    reference, and bit-identical to the chain's row kernel (the engines' shared
+    trajectory depends on it)."""
+    g = torch.Generator(device="cuda").manual_seed(n + d + nq)
+    x = torch.rand(n, d, device="cuda", generator=g)
+    keys = torch.randperm(n, generator=torch.Generator().manual_seed(n))[:nq].tolist()
+    keys[0] = n - 1  # last row: the padded tail of the last workgroup
+    gamma = 1.0 / d
+    got = K.xpass_rows(x, keys, gamma, rows_per_group=rows)
+    ref = _rbf_ref(x, x[keys], gamma)
+    assert got.shape == (nq, n) and torch.isfinite(got).all()
+    assert (got.double() - ref).abs().max().item() < 2e-5
+    assert float(got[0, n - 1]) == 1.0  # K(x, x) = exp(-0)
+    rows_k = K.rbf_rows(x, x[keys], gamma)
+    assert torch.equal(got, rows_k)
+
+
+def test_fused_select_vs_torch(K):
+    """Per-workgroup selection of the fused / persistent engines (I-set
+    classification, DPP wave-64 minimum with payload, LDS across waves): each
+    workgroup's keys equal a torch argmin / argmax over its rows, ties to the
+    lowest index."""
+    from dpsvm_amd.ops.kernels import decode_key
+
+    n, C_, rows = 9000, 2.0, 512
+    g = torch.Generator(device="cuda").manual_seed(5)
+    f = torch.randn(n, device="cuda", generator=g)
+    y = torch.where(torch.rand(n, device="cuda", generator=g) > 0.5, 1.0, -1.0)
+    a = torch.rand(n, device="cuda", generator=g) * C_
+    a[torch.rand(n, device="cuda", generator=g) < 0.3] = 0.0
+    a[torch.rand(n, device="cuda", generator=g) < 0.2] = C_
+    f[600:612] = -5.0  # ties inside one workgroup: lowest index wins
+    y[600:612] = 1.0
+    a[600:612] = 0.0
+    keys = K.fused_select(f, a, y, C_, rows_per_group=rows).cpu()
+    up = ((a == 0) & (y == 1)) | ((a == C_) & (y != 1)) | ((a > 0) & (a < C_))
+    lo = ((a == 0) & (y != 1)) | ((a == C_) & (y == 1)) | ((a > 0) & (a < C_))
+    fu = torch.where(up, f, torch.inf).cpu()
+    fl = torch.where(lo, -f, torch.inf).cpu()
+    for b in range((n + rows - 1) // rows):
+        s = slice(b * rows, min(n, (b + 1) * rows))
+        ih = b * rows + int(torch.argmin(fu[s]))  # torch.argmin: first occurrence
+        il = b * rows + int(torch.argmin(fl[s]))
+        vh, gh = decode_key(int(keys[b, 0]) & (2**64 - 1))
+        vl, gl = decode_key(int(keys[b, 1]) & (2**64 - 1))
+        assert (gh, vh) == (ih, float(f[ih])), b
+        assert (gl, -vl) == (il, float(f[il])), b
+    assert decode_key(int(keys[1, 0]) & (2**64 - 1))[1] == 600

@@ -21,6 +21,15 @@ def _gpu():
         pytest.skip("no GPU")
 
 
+def _worker_errors(out, world):
+    msgs = []
+    for k in range(world):
+        p = f"{out}.rank{k}.err"
+        if os.path.exists(p):
+            msgs.append(f"rank {k}: " + open(p).read()[-1500:])
+    return "\n".join(msgs) + "\n"
+
+
 def _close(g, c, n):
     assert g.converged_ and c.converged_
     assert abs(g.n_iter_ - c.n_iter_) <= max(10, c.n_iter_ // 50)
@@ -190,7 +199,7 @@ def test_verify_invariants_every_engine(monkeypatch, engine):
         if engine == "fused-cache":
             kw["persist"] = "off"
         if engine == "chain":
-            monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
+            kw["cache_engine"] = "chain"
     elif engine == "partitioned":
         kw["x_mode"] = "partitioned"
     clf = SVC(**kw).fit(X, y)
@@ -211,8 +220,7 @@ def test_fused_cache_iteration_matches_kernel_chain(monkeypatch, extra):
     kw = dict(C=4.0, gamma=0.5, device="cuda", persist="off", **extra)
     fused = SVC(**kw).fit(X, y)
     assert fused.setup_info_["iteration"] == "fused-cache"
-    monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
-    chain = SVC(**kw).fit(X, y)
+    chain = SVC(cache_engine="chain", **kw).fit(X, y)
     assert chain.setup_info_["iteration"] == "chain"
     assert fused.n_iter_ == chain.n_iter_
     assert np.array_equal(fused.alpha_, chain.alpha_)
@@ -236,8 +244,7 @@ def test_fused_cache_wide_features_and_checkpoint(monkeypatch, tmp_path):
     res = SVC(**kw).fit(X, y, resume=ck)
     assert res.n_iter_ == full.n_iter_
     assert np.array_equal(res.alpha_, full.alpha_)
-    monkeypatch.setenv("DPSVM_LRU_KERNELS", "3")
-    chain = SVC(**kw).fit(X, y)
+    chain = SVC(cache_engine="chain", **kw).fit(X, y)
     assert np.array_equal(chain.alpha_, full.alpha_)
 
 
@@ -246,7 +253,6 @@ def test_persistent_cache_engine_matches_fused(monkeypatch, case):
     """Persistent cache engine (private per-workgroup CLOCK metadata, keys
     exchanged in-kernel, X pass per workgroup) == the one-launch-per-iteration
     cache engine, bit for bit: same kernel rows, same trajectory."""
-    monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
     if case == "wide":
         X, y = synthetic("blobs", n=2500, d=1100, seed=8, sep=1.0)
         kw = dict(C=1.0, gamma=1.0 / 1100, cache_lines=48)
@@ -255,7 +261,7 @@ def test_persistent_cache_engine_matches_fused(monkeypatch, case):
         kw = dict(C=4.0, gamma=0.5, cache_lines=256)
     kw.update({"covtype-spec": {}, "covtype-nospec": {"spec_rows": 0}, "tiny-cache": {"cache_lines": 2, "spec_rows": 0},
                "wide": {}, "max-iter": {"max_iter": 1500}, "box": {"clip": "box"}}[case])
-    got = SVC(device="cuda", persist_block=301, **kw).fit(X, y)
+    got = SVC(device="cuda", persist_block=301, xch_timeout_s=30.0, **kw).fit(X, y)
     assert got.setup_info_["iteration"] == "persistent-cache"
     ref = SVC(device="cuda", persist="off", **kw).fit(X, y)
     assert ref.setup_info_["iteration"] == "fused-cache"
@@ -271,9 +277,8 @@ def test_peer_exchange_loopback_and_thread_ranks(monkeypatch, C):
     loopback reproduces the local run bit for bit; rank threads sharing one
     device in one process fall back to the all-reduce (their streams may share
     a hardware queue) with identical results."""
-    monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
     X, y = synthetic("covtype", n=6000, seed=2)
-    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", xch_timeout_s=30.0)
     ref = SVC(persist="off", **kw).fit(X, y)
     assert ref.setup_info_["exchange"] == "none"
     loop = SVC(exchange="peer", persist="off", **kw).fit(X, y)
@@ -304,11 +309,8 @@ def test_persistent_engine_matches_fused(monkeypatch, block, rows):
     """Persistent dense kernel (keys exchanged in-kernel, row state in
     registers) == one launch per iteration, bit for bit; also across launches
     of an odd block length, at max_iter, and with 12 rows per thread."""
-    monkeypatch.setenv("DPSVM_XCH_TIMEOUT_S", "30")
-    if rows:
-        monkeypatch.setenv("DPSVM_DENSE_ROWS", str(rows))
     X, y = synthetic("covtype", n=6000, seed=2)
-    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", xch_timeout_s=30.0, rows_per_group=rows or 0)
     ref = SVC(persist="off", **kw).fit(X, y)
     got = SVC(persist="on", persist_block=block, **kw).fit(X, y)
     assert got.setup_info_["iteration"] == "persistent-dense"
@@ -330,16 +332,15 @@ def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     import subprocess
 
     n = 20000 if engine == "persistent-batches" else 6000
-    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="30", DPSVM_VERIFY="1")
-    if engine == "persistent-batches":
-        env.update(DPSVM_DENSE_ROWS="256", DPSVM_XCH_KB="1")
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_VERIFY="1")
+    extra_json = json.dumps({"rows_per_group": 256, "xch_poll_batch": 1} if engine == "persistent-batches" else {})
     out = tmp_path / "mp"
     port = 29600 + ["fused", "persistent", "persistent-batches", "persistent-cache"].index(engine)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n)]
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n), extra_json]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _worker_errors(out, 2) + r.stderr[-2000:]
     res = [json.load(open(f"{out}.rank{k}.json")) for k in range(2)]
     X, y = synthetic("covtype", n=n, seed=2)
     extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
@@ -363,14 +364,14 @@ def test_peer_exchange_four_processes_one_gpu(tmp_path, engine, world):
     import subprocess
 
     n = 8000
-    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="30", DPSVM_VERIFY="1")
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_VERIFY="1")
     out = tmp_path / f"mp{world}"
     port = 29620 + ["persistent", "persistent-cache"].index(engine) + (4 if world == 8 else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _worker_errors(out, world) + r.stderr[-2000:]
     res = [json.load(open(f"{out}.rank{k}.json")) for k in range(world)]
     X, y = synthetic("covtype", n=n, seed=2)
     extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
@@ -389,10 +390,10 @@ def test_bench_two_processes_exchange_fallback(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     import subprocess
 
-    env = dict(os.environ, DPSVM_FORCE_DEVICE="0", DPSVM_XCH_TIMEOUT_S="0.000001")
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29611", os.path.join(root, "bench.py"), "--gpus", "2",
-           "--samples", "4000", "--steps", "1", "--warmup", "1", "--comm", "gloo"]
+           "--samples", "4000", "--steps", "1", "--warmup", "1", "--comm", "gloo", "--xch-timeout", "0.000001"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
@@ -401,34 +402,216 @@ def test_bench_two_processes_exchange_fallback(tmp_path):
 
 
 _SHARED = os.environ.get("DPSVM_TEST_SHARED_GPU") == "1"
+_NDEV = torch.cuda.device_count() if torch.cuda.is_available() else 0
+_MULTI = pytest.mark.skipif(not _SHARED and _NDEV < 2,
+                            reason="needs >= 2 GPUs (DPSVM_TEST_SHARED_GPU=1 rehearses it on one)")
 
 
-@pytest.mark.skipif(not _SHARED and torch.cuda.device_count() < 2,
-                    reason="needs >= 2 GPUs (DPSVM_TEST_SHARED_GPU=1 rehearses it on one)")
-def test_bench_multi_gpu_rccl_matches_one_gpu(tmp_path):
-    """bench.py as one process per GPU (RCCL communicator over xGMI, in-kernel
-    peer exchange between devices) on up to 8 GPUs: same iteration count, b and
-    SV count as the one-GPU solve.  DPSVM_TEST_SHARED_GPU=1 runs the same ranks
-    on one GPU over gloo (RCCL refuses two ranks on one device)."""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+def _bench_multi(root, world, extra, port):
     import subprocess
 
-    world = 2 if _SHARED else min(torch.cuda.device_count(), 8)
-    env = dict(os.environ, DPSVM_XCH_TIMEOUT_S="30")
-    extra = ["--comm", "gloo"] if _SHARED else ["--comm", "rccl"]
+    env = dict(os.environ)
+    comm = ["--comm", "gloo"] if _SHARED else ["--comm", "rccl"]
     if _SHARED:
         env["DPSVM_FORCE_DEVICE"] = "0"
-    n = 8000
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", "29641", os.path.join(root, "bench.py"),
-           "--gpus", str(world), "--samples", str(n), "--steps", "1", "--warmup", "1", "--no-accuracy"] + extra
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--samples", "8000", "--steps", "1", "--warmup", "1", "--no-accuracy"] + comm + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
+    return json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
+
+
+def _ref_8000():
+    X, y = synthetic("mnist", n=8000, d=784, seed=0)
+    return SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
+
+
+@_MULTI
+def test_bench_multi_gpu_sharded_matches_one_gpu(tmp_path):
+    """bench.py as one process per GPU with the rows SHARDED (RCCL communicator
+    over xGMI, in-kernel peer exchange between devices) on up to 8 GPUs: same
+    iteration count, b and SV count as the one-GPU solve, cross-rank verified.
+    DPSVM_TEST_SHARED_GPU=1 runs the same ranks on one GPU over gloo."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    world = 2 if _SHARED else min(_NDEV, 8)
+    out = _bench_multi(root, world, ["--dp", "shard"], 29641)
     assert out["n_gpus"] == world and out["converged"] and out["exchange"] == "peer"
+    assert out["dp_policy"] == "shard" and out["exchange_mem"] == "uncached"
     assert out["comm"] != "local" and out["config"]["parallelism"] == f"dp{world}"
-    X, y = synthetic("mnist", n=n, d=784, seed=0)
-    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
-    assert out["iterations"] == ref.n_iter_
-    assert out["b"] == ref.b_
+    ref = _ref_8000()
+    assert out["iterations"] == ref.n_iter_ and out["b"] == ref.b_
     assert out["n_sv"] == int((ref.alpha_ > 0).sum())
+
+
+@pytest.mark.skipif(_NDEV < 2, reason="needs >= 2 GPUs (replication needs distinct devices)")
+def test_bench_multi_gpu_auto_policy_replicates_and_checks_shards(tmp_path):
+    """Default policy on distinct GPUs for a problem whose Gram fits one GPU:
+    every rank solves it all (no per-iteration hop), and the untimed sharded
+    check solve reports the same iterations and b."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    world = min(_NDEV, 8)
+    out = _bench_multi(root, world, [], 29651)
+    ref = _ref_8000()
+    assert out["dp_policy"] == "replicate" and out["iterations"] == ref.n_iter_ and out["b"] == ref.b_
+    sc = out["shard_check"]
+    assert sc and "error" not in sc, sc
+    assert sc["exchange"] == "peer" and sc["iterations"] == ref.n_iter_ and sc["b"] == ref.b_
+
+
+@pytest.mark.skipif(_NDEV < 2, reason="needs >= 2 GPUs (svmTrain -p N: one thread per device)")
+@pytest.mark.parametrize("ranks", [2, 8])
+@pytest.mark.parametrize("dp", ["shard", "auto"])
+def test_svmtrain_in_process_multi_gpu(tmp_path, bin_dir, ranks, dp):
+    """svmTrain -p N: one process, one thread per GPU, ncclCommInitAll, the
+    in-kernel exchange over same-process peer pointers (hipDeviceEnablePeerAccess).
+    Sharded: bit-identical iterations and b to one rank; auto: replicated solve.
+    The cross-rank alpha digest runs by default."""
+    if ranks > _NDEV:
+        pytest.skip(f"needs {ranks} GPUs")
+    import subprocess
+
+    outs = {}
+    for p_ in (1, ranks):
+        mj = str(tmp_path / f"m{p_}.json")
+        cmd = [os.path.join(bin_dir, "svmTrain"), "-a", "784", "-x", "8000", "--synthetic", "mnist", "-c", "10",
+               "-g", "0.25", "-m", str(tmp_path / f"model{p_}.txt"), "-p", str(p_), "--dp", dp,
+               "--metrics-json", mj, "--xch-timeout", "30"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs[p_] = json.load(open(mj))
+    one, many = outs[1], outs[ranks]
+    assert many["world"] == ranks and many["iterations"] == one["iterations"] and many["b"] == one["b"]
+    assert many["n_sv"] == one["n_sv"]
+    if dp == "shard":
+        assert many["dp_policy"] == "shard" and many["exchange"] == "peer"
+        assert many["engine"] == "persistent-dense"
+    else:
+        assert many["dp_policy"] == "replicate"
+
+
+def test_census_forced_oversubscription_falls_back():
+    """A persistent grid that cannot be co-resident (here: a census grid of
+    4096 workgroups, more than the device holds) is detected at setup within
+    the census bound and the solver falls back to the one-launch-per-iteration
+    engine, bit-identical, instead of spinning to the exchange timeout."""
+    import time
+
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", xch_timeout_s=30.0)
+    ref = SVC(**kw).fit(X, y)
+    assert ref.setup_info_["iteration"] == "persistent-dense" and ref.setup_info_["census"] == "ok"
+    assert ref.setup_info_["blocks_per_cu"] >= 1 and ref.setup_info_["cus"] >= 1
+    t0 = time.perf_counter()
+    got = SVC(census_groups=4096, **kw).fit(X, y)
+    assert time.perf_counter() - t0 < 20.0
+    assert got.setup_info_["census"] == "failed" and got.setup_info_["iteration"] == "fused-dense"
+    assert "census" in got.setup_info_["engine_note"]
+    assert got.n_iter_ == ref.n_iter_ and np.array_equal(got.alpha_, ref.alpha_)
+    # cache mode: persistent cache engine -> fused cache engine
+    cref = SVC(cache_lines=256, **kw).fit(X, y)
+    assert cref.setup_info_["iteration"] == "persistent-cache"
+    cgot = SVC(cache_lines=256, census_groups=4096, **kw).fit(X, y)
+    assert cgot.setup_info_["iteration"] == "fused-cache" and cgot.setup_info_["census"] == "failed"
+    assert cgot.n_iter_ == cref.n_iter_ and np.array_equal(cgot.alpha_, cref.alpha_)
+    # persist="on" (required) refuses loudly instead of falling back
+    with pytest.raises(Exception, match="co-resident"):
+        SVC(persist="on", census_groups=4096, **kw).fit(X, y)
+
+
+def test_gpu_resume_rejects_mismatched_problem(tmp_path):
+    X, y = synthetic("blobs", n=3000, d=16, seed=9, sep=1.0)
+    ck = str(tmp_path / "ck.bin")
+    SVC(C=1.0, gamma=0.05, device="cuda", max_iter=300, checkpoint_path=ck, checkpoint_every=100).fit(X, y)
+    with pytest.raises(Exception, match="gamma"):
+        SVC(C=1.0, gamma=0.5, device="cuda").fit(X, y, resume=ck)
+    with pytest.raises(Exception, match="C ="):
+        SVC(C=0.5, gamma=0.05, device="cuda").fit(X, y, resume=ck)
+    ok = SVC(C=1.0, gamma=0.05, eps=1e-2, device="cuda").fit(X, y, resume=ck)  # eps may differ
+    assert ok.converged_
+
+
+@pytest.mark.parametrize("p_from,p_to", [(2, 1), (2, 3)])
+def test_gpu_checkpoint_resume_other_rank_count(tmp_path, C, p_from, p_to):
+    """A checkpoint written by P simulated ranks (alpha + all-gathered f) resumes
+    at P' ranks and finishes on the uninterrupted trajectory."""
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    full = SVC(**kw).fit(X, y)
+    ck = str(tmp_path / "ck.bin")
+
+    def run(world, resume=None, **extra):
+        if world == 1:
+            return [SVC(**kw, **extra).fit(X, y, resume=resume)]
+        g = C.ThreadCommGroup(world)
+        comms = [g.comm(r) for r in range(world)]
+        out, errs = [None] * world, []
+
+        def work(r):
+            try:
+                out[r] = SVC(**kw, **extra).fit(X, y, comm=comms[r], resume=resume)
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        assert not errs, errs
+        return out
+
+    part = run(p_from, max_iter=full.n_iter_ // 2, checkpoint_path=ck, checkpoint_every=max(1, full.n_iter_ // 5))
+    assert not part[0].converged_ and os.path.exists(ck)
+    assert C.read_checkpoint(ck).iter == full.n_iter_ // 2
+    res = run(p_to, resume=ck)
+    for r in res:
+        assert r.n_iter_ == full.n_iter_ and np.array_equal(r.alpha_, full.alpha_)
+
+
+_ORACLE_ENGINES = {
+    "persistent-dense": {},
+    "fused-dense": {"persist": "off"},
+    "persistent-cache": {"cache_lines": 64},
+    "fused-cache": {"cache_lines": 64, "persist": "off"},
+    "chain": {"cache_lines": 64, "cache_engine": "chain"},
+    "partitioned": {"x_mode": "partitioned"},
+}
+
+
+@pytest.mark.parametrize("clip", ["independent", "box"])
+@pytest.mark.parametrize("engine", sorted(_ORACLE_ENGINES))
+def test_gpu_engines_vs_float64_numpy_oracle(engine, clip):
+    """Every device engine vs an independent float64 numpy model of the
+    reference algorithm (tests/ref_smo.py: svmTrainMain.cpp:235-310), not the
+    builder's own CPU solver: same iterations (fp32 vs fp64 arithmetic allow a
+    small drift), same alphas, b and support set."""
+    from ref_smo import smo_reference
+
+    X, y = synthetic("blobs", n=2500, d=12, seed=41, sep=1.2)
+    C_, g = 2.0, 0.15
+    a_ref, b_ref, it_ref = smo_reference(X, y, C=C_, gamma=g, eps=1e-3, clip=clip)
+    clf = SVC(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", **_ORACLE_ENGINES[engine]).fit(X, y)
+    want = "chain" if engine == "partitioned" else engine
+    assert clf.setup_info_["iteration"] == want
+    assert clf.converged_
+    assert abs(clf.n_iter_ - it_ref) <= max(10, it_ref // 20), (clf.n_iter_, it_ref)
+    assert np.abs(clf.alpha_ - a_ref).max() < 5e-2 * C_
+    assert abs(clf.b_ - b_ref) < 5e-3
+    sv_ours, sv_ref = set(np.nonzero(clf.alpha_ > 0)[0]), set(np.nonzero(a_ref > 0)[0])
+    assert len(sv_ours ^ sv_ref) <= max(3, len(sv_ref) // 50)
+
+
+def test_gpu_box_clip_vs_sklearn_libsvm():
+    """Box clipping reaches LIBSVM's optimum (scikit-learn's libsvm, second-order
+    working sets): SV count, intercept, and decision signs agree."""
+    sk = pytest.importorskip("sklearn.svm")
+    X, y = synthetic("adult", n=3000, seed=2)
+    C_, g = 1.0, 0.05
+    ref = sk.SVC(C=C_, gamma=g, kernel="rbf", tol=1e-3).fit(X, y)
+    for extra in ({}, {"cache_lines": 64}):
+        clf = SVC(C=C_, gamma=g, eps=1e-3, clip="box", device="cuda", **extra).fit(X, y)
+        n_ref = int(ref.n_support_.sum())
+        assert abs(clf.n_support_ - n_ref) <= max(5, n_ref // 50)
+        assert abs(-clf.b_ - ref.intercept_[0]) < 0.05
+        agree = np.mean(np.sign(clf.decision_function(X)) == np.sign(ref.decision_function(X)))
+        assert agree > 0.99
+        assert abs(float((clf.alpha_ * np.where(y > 0, 1, -1)).sum())) < 1e-2
