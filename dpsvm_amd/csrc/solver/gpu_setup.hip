@@ -431,6 +431,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     DPSVM_CHECK(m.p.persist != 2, "persistent engine requested (persist=on) but its grid is not co-resident (" +
                                       m.info.engine_note + ")");
     m.kind = m.dense ? EngineKind::FusedDense : EngineKind::FusedCache;
+    if (m.kind == EngineKind::FusedCache && m.xch) {
+      // the exchange was set up for the persistent cache engine only; the fused
+      // cache engine combines keys through its records (and the all-reduce)
+      m.xch = false;
+      a.xpeer = nullptr;
+      a.xrank = 0;
+      a.xworld = 0;
+    }
   }
   if (m.kind == EngineKind::PersistCache) {
     a.plru_stride = launch::plru_stride_words(n, m.L);

@@ -31,12 +31,25 @@ def smo_reference(X, y, C, gamma, eps=1e-3, max_iter=150000, clip="independent")
         s = y[il] * y[ih]
         aln = a[il] + y[il] * (bh - bl) / eta
         if clip == "box" and ih != il:
+            # joint box; when alpha_lo lands on a bound that comes from alpha_hi's
+            # own bound, alpha_hi takes that bound exactly (in exact arithmetic it
+            # would): otherwise round-off leaves it a hair inside [0, C] and the
+            # same pair is selected forever with a zero-length step (LIBSVM snaps
+            # the same way)
             if y[ih] != y[il]:
-                L, H = max(0.0, a[il] - a[ih]), min(C, C + a[il] - a[ih])
+                dl = a[il] - a[ih]
+                L, hL = (dl, 0.0) if dl > 0 else (0.0, None)
+                H, hH = (C + dl, C) if dl < 0 else (C, None)
             else:
-                L, H = max(0.0, a[il] + a[ih] - C), min(C, a[il] + a[ih])
-            aln = min(max(aln, L), H)
-            ahn = min(max(a[ih] + s * (a[il] - aln), 0.0), C)
+                sm = a[il] + a[ih]
+                L, hL = (sm - C, C) if sm > C else (0.0, None)
+                H, hH = (sm, 0.0) if sm < C else (C, None)
+            snap = None
+            if aln <= L:
+                aln, snap = L, hL
+            elif aln >= H:
+                aln, snap = H, hH
+            ahn = snap if snap is not None else min(max(a[ih] + s * (a[il] - aln), 0.0), C)
         else:
             ahn = a[ih] + s * (a[il] - aln)
             aln, ahn = min(max(aln, 0.0), C), min(max(ahn, 0.0), C)
