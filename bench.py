@@ -81,6 +81,13 @@ def parse(argv=None):
     ap.add_argument("--shard-check", default="auto", choices=["auto", "off"],
                     help="N > 1 with a replicated timed solve: one untimed sharded solve first (cross-device "
                          "exchange evidence: its time, iterations and b go into the JSON line)")
+    ap.add_argument("--solver", default="auto", choices=["auto", "smo", "ws"],
+                    help="smo: pair-at-a-time engines (the reference's trajectory); ws: working-set rounds "
+                         "(the reference's pair rule on a q-row sub-problem in LDS, same global stop test)")
+    ap.add_argument("--ws-size", type=int, default=192)
+    ap.add_argument("--ws-new", type=int, default=0)
+    ap.add_argument("--ws-rel", type=float, default=0.1)
+    ap.add_argument("--ws-block", type=int, default=32)
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
     ap.add_argument("--cache-groups", type=int, default=256)
     ap.add_argument("--force-cache", action="store_true")
@@ -133,7 +140,8 @@ def main(argv=None) -> int:
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
                     exchange=a.exchange, persist=a.persist, persist_block=a.persist_block, dp=a.dp,
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
-                    xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem,
+                    xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
+                    ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block,
                     xch_timeout_s=a.xch_timeout if a.xch_timeout is not None else (30.0 if multi else 120.0))
     params = cfg.to_native(X.shape[1])
     # auto: RCCL, or gloo on EVERY rank when the RCCL bootstrap fails on any
@@ -248,6 +256,7 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{n_ranks}",
             },
             "iterations": int(res["iters"]),
+            "rounds": int(res.get("outer", 0)),
             "converged": bool(res["converged"]),
             "n_sv": nsv,
             "b": res["b"],

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Phase anatomy of the working-set engine from in-kernel s_memrealtime stamps
+(DPSVM_STAMPS; 100 MHz).  Ring slot r holds, in time order: ws_select
+workgroup 0 entry/exit (6, 7: the f update + candidates before round r),
+ws_gather workgroup 0 entry (1), merged (2), exit (8), ws_solve entry (0),
+sub-Gram loaded (3), sub-problem solved (4), pair steps (5).
+
+  python bench/ws_stamps.py [--samples N] [--features D] [...]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data", default="mnist")
+    ap.add_argument("--samples", type=int, default=60000)
+    ap.add_argument("--features", type=int, default=784)
+    ap.add_argument("--C", type=float, default=10.0)
+    ap.add_argument("--gamma", type=float, default=0.25)
+    ap.add_argument("--ws-size", type=int, default=192)
+    ap.add_argument("--ws-new", type=int, default=0)
+    ap.add_argument("--ws-rel", type=float, default=0.1)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    path = os.path.join(tempfile.mkdtemp(), "ws_stamps")
+    os.environ["DPSVM_STAMPS"] = path
+    from dpsvm_amd import SVC
+    from dpsvm_amd.utils.datasets import synthetic
+
+    X, y = synthetic(a.data, n=a.samples, d=a.features)
+    clf = SVC(C=a.C, gamma=a.gamma, eps=1e-3, device="cuda", solver="ws", ws_size=a.ws_size, ws_new=a.ws_new,
+              ws_rel=a.ws_rel).fit(X, y)
+    raw = np.fromfile(path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
+    rounds = min(clf.n_rounds_, 4096)
+    s = raw[2:rounds]
+    ok = (s[:, [0, 1, 2, 3, 4, 6, 7, 8]] > 0).all(axis=1)
+    us = lambda v: np.round(np.median(v) * 0.01, 2)  # noqa: E731  (10 ns ticks -> us)
+    s = s[ok]
+    nxt = np.roll(raw[:, 6], -1)[2:rounds][ok]
+    res = {
+        "rounds": clf.n_rounds_, "pair_steps": clf.n_iter_, "fit_time_s": round(clf.fit_time_, 4),
+        "b": float(clf.b_), "n_sv": int(clf.n_support_),
+        "steps_per_round_median": float(np.median(s[:, 5])),
+        "select_wg0_us": us(s[:, 7] - s[:, 6]),
+        "select_end_to_gather_us": us(s[:, 1] - s[:, 7]),
+        "merge_us": us(s[:, 2] - s[:, 1]),
+        "gather_rows_us": us(s[:, 8] - s[:, 2]),
+        "gather_end_to_solve_us": us(s[:, 0] - s[:, 8]),
+        "load_subgram_us": us(s[:, 3] - s[:, 0]),
+        "solve_us": us(s[:, 4] - s[:, 3]),
+        "solve_per_step_us": float(np.round(np.median((s[:, 4] - s[:, 3]) / np.maximum(1, s[:, 5])) * 0.01, 3)),
+        "solve_end_to_next_select_us": us(nxt - s[:, 4]),
+        "round_period_us": us(np.diff(s[:, 6])),
+    }
+    line = json.dumps(res)
+    print(line)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

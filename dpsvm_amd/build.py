@@ -52,6 +52,7 @@ LIB_SOURCES = [
     "kernels/smo_fused_lru.hip",
     "kernels/smo_persist.hip",
     "kernels/smo_persist_lru.hip",
+    "kernels/smo_ws.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

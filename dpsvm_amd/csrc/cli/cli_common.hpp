@@ -81,6 +81,9 @@ inline void usage_train(const char* prog, bool seq) {
                "   --watchdog S        :  host bound on one block of iterations (default 1800)\n"
                "   --census-groups N   :  residency census grid of the persistent engines (tests)\n"
                "   --no-verify-ranks   :  skip the cross-rank alpha digest (world > 1)\n"
+               "   --solver S          :  auto | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
+               "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
+               "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
@@ -98,7 +101,8 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_GB, OPT_NOGRAPH, OPT_CK, OPT_CKE, OPT_RESUME, OPT_METRICS, OPT_LOG, OPT_PREC, OPT_LEGM,
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
-    OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON
+    OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL,
+    OPT_WSINNER, OPT_WSBLOCK
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -127,6 +131,9 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"xch-mem", required_argument, 0, OPT_XMEM}, {"xch-timeout", required_argument, 0, OPT_XTMO},
       {"watchdog", required_argument, 0, OPT_WDOG}, {"census-groups", required_argument, 0, OPT_CENSUS},
       {"no-verify-ranks", no_argument, 0, OPT_NOVR}, {"params-json", required_argument, 0, OPT_PJSON},
+      {"solver", required_argument, 0, OPT_SOLVER}, {"ws-size", required_argument, 0, OPT_WSSIZE},
+      {"ws-new", required_argument, 0, OPT_WSNEW}, {"ws-rel", required_argument, 0, OPT_WSREL},
+      {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -215,6 +222,17 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_WDOG: o.p.watchdog_s = atof(optarg); break;
       case OPT_CENSUS: o.p.census_groups = atoi(optarg); break;
       case OPT_NOVR: o.p.verify_ranks = false; break;
+      case OPT_SOLVER: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "smo" && v != "ws") usage_train(argv[0], seq);
+        o.p.solver = v == "ws" ? 2 : v == "smo" ? 1 : 0;
+        break;
+      }
+      case OPT_WSSIZE: o.p.ws_size = atoi(optarg); break;
+      case OPT_WSNEW: o.p.ws_new = atoi(optarg); break;
+      case OPT_WSREL: o.p.ws_rel = (float)atof(optarg); break;
+      case OPT_WSINNER: o.p.ws_inner = atoi(optarg); break;
+      case OPT_WSBLOCK: o.p.ws_block = atoi(optarg); break;
       case OPT_PJSON: {
         FILE* fp = fopen(optarg, "r");
         if (!fp) {

@@ -111,6 +111,15 @@ struct SolverParams {
   // adds a cross-device hop to every iteration while saving only the Gram
   // GEMM (docs/DESIGN.md "Multi-GPU").
   int dp_policy = 0;
+  // solver: 0 auto, 1 pair-at-a-time SMO engines (the reference's trajectory),
+  // 2 working-set rounds (ws engine, smo_ws.hip: the reference's pair rule on
+  // a q-row sub-problem in LDS, the same global stop test)
+  int solver = 0;
+  int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
+  int ws_new = 0;             // rows replaced per round (0: ws_size / 2)
+  float ws_rel = 0.1f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2)
+  int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
+  int ws_block = 32;          // rounds per hipGraph block
 };
 
 
@@ -127,6 +136,7 @@ struct SolveResult {
   int64_t cache_lines = 0, host_cache_lines = 0;
   int world = 1;
   double verify_f_err = -1.0;  // DPSVM_VERIFY: max |f - f(alpha)| / (1 + |f(alpha)|), -1 = not run
+  int64_t outer = 0;           // working-set engine: rounds
   bool converged() const { return status == 1; }
 };
 

@@ -45,9 +45,11 @@ enum class EngineKind : int32_t {
   PersistCache = 2,  // kernel-row cache, persistent kernel, private cache metadata
   FusedCache = 3,    // kernel-row cache, one launch per iteration (+ host spill tier)
   Chain = 4,         // rows / step / finalize kernels + collective (partitioned X fallback)
+  WsDense = 5,       // Gram resident, working-set rounds (sub-problem in LDS, smo_ws.hip)
 };
 inline const char* engine_name(EngineKind k) {
   switch (k) {
+    case EngineKind::WsDense: return "ws-dense";
     case EngineKind::PersistDense: return "persistent-dense";
     case EngineKind::FusedDense: return "fused-dense";
     case EngineKind::PersistCache: return "persistent-cache";
@@ -88,6 +90,7 @@ struct alignas(16) SmoStatus {
   int32_t seq;
   float b_hi, b_lo;
   int64_t hits, misses, rows_computed, x_passes, spec_rows, host_hits, spills;
+  int64_t outer;  // working-set engine: rounds (selection + sub-problem solve) so far
 };
 
 // Partitioned-X candidate record: one per rank, all-gathered each iteration.
@@ -191,6 +194,56 @@ struct SmoArgs {
   int64_t census_ticks;
 };
 constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..16}, {key bits 15..0, alpha}
+
+// ---- working-set engine (smo_ws.hip) ----
+// Decomposition around the reference's pair update: each round selects a
+// working set of q rows (the most violating of I_up / I_low plus the newest
+// part of the previous set), one workgroup solves the q-row sub-problem with
+// the reference's pair rule from a q x q sub-Gram held in LDS, and one grid
+// pass applies the round's alpha changes to every f_j and selects the next
+// candidates.  ~10^5 dependent pair steps then cost an LDS round trip each
+// instead of a grid-wide exchange.
+constexpr int kWsMax = 192;          // working-set capacity: q x q fp32 sub-Gram in LDS (147 KiB)
+constexpr int kWsCand = 4;           // candidates per side per selection workgroup
+constexpr int kWsSelThreads = 256;   // selection / f-update workgroup
+constexpr int kWsMaxGroups = 256;    // selection workgroups (<= 2048 candidates per side)
+constexpr int kWsMaxRPT = 16;        // rows per selection thread
+constexpr int kWsSolveThreads = 1024;
+
+struct alignas(16) WsCtrl {
+  int64_t iter;      // pair updates applied so far
+  int64_t outer;     // rounds completed (round r builds its set into parity r & 1)
+  int32_t done;      // DoneCode
+  int32_t n_apply;   // alpha changes the next f update applies (0: none)
+  int32_t q[2];      // working-set size per round parity (q[1] = 0 before round 0)
+  float b_hi, b_lo;  // global selection of the current round
+  int32_t nonfinite; // set by ws_select when an f value is not finite
+  int32_t pad;
+  int32_t idx[2][kWsMax];     // working set per round parity (global rows), newest first
+  int32_t apply_idx[kWsMax];  // rows whose alpha changed in the last round
+  float apply_coef[kWsMax];   // their (alpha_new - alpha_old) * y
+};
+
+struct WsArgs {
+  const float* gram;   // resident Gram shard: K(i, off + j) at gram[i * ldg + j]
+  int64_t ldg;
+  const float* y;      // [n] global labels
+  float* alpha;        // [n] global
+  float* f;            // [nl] local gradient
+  int64_t n, nl, off;
+  int32_t G, rpt;      // selection geometry: G workgroups x 256 threads x rpt rows
+  int32_t q_max, n_new, inner_max;
+  float rel_local;     // sub-problem tolerance: max(eps, rel_local * global gap / 2)
+  float C, eps, tau;
+  int32_t clip;
+  int64_t max_iter;
+  uint64_t* cand;      // [G][2][kWsCand] per-workgroup candidate keys (up, low), ascending
+  float* subg;         // [q][q] sub-Gram of the current working set (ws_gather -> ws_solve)
+  float* aux;          // [3][kWsMax] alpha, y, f of the working set
+  WsCtrl* ctrl;
+  SmoStatus* status;   // host-mapped
+  uint64_t* stamps;    // DPSVM_STAMPS diagnostics: s_memrealtime per phase, ring of kStampRing rounds
+};
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;
 

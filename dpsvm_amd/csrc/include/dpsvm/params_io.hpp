@@ -50,6 +50,12 @@ void for_each_param(SolverParams& p, F&& f) {
   f("verify_ranks", p.verify_ranks);
   f("dp_policy", p.dp_policy);
   f("force_collectives", p.force_collectives);
+  f("solver", p.solver);
+  f("ws_size", p.ws_size);
+  f("ws_new", p.ws_new);
+  f("ws_rel", p.ws_rel);
+  f("ws_inner", p.ws_inner);
+  f("ws_block", p.ws_block);
 }
 
 inline std::string num(double v) {

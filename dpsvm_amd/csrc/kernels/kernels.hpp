@@ -64,6 +64,16 @@ void preload_persist_kernel(hipStream_t s);
 void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uint32_t tag, int64_t timeout_ticks,
               int32_t* ok, hipStream_t s);
 
+// working-set engine (smo_ws.hip): selection geometry for nl local rows
+// (<= 256 workgroups x 256 threads x rpt rows); one round = ws_gather (merge,
+// stop test, working set, sub-Gram rows), ws_solve (the sub-problem), then
+// ws_select (f update, next candidates)
+bool ws_supported(int64_t nl, int q_max);
+void ws_geometry(int64_t nl, int32_t* G, int32_t* rpt);
+void ws_select(const WsArgs& a, hipStream_t s);
+void ws_gather(const WsArgs& a, hipStream_t s);
+void ws_solve(const WsArgs& a, hipStream_t s);
+
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)
 //   symmetric: B == A (one rank): tiles above the diagonal only, each also

@@ -1,0 +1,845 @@
+// Working-set engine (Gram resident).  One round = three launches:
+//
+//   ws_gather  (q_max workgroups of 256 threads)
+//       every workgroup merges the candidate lists redundantly (identical
+//       inputs, identical arithmetic: no grid synchronisation needed): the
+//       global stop test — the reference's !(b_lo > b_hi + 2 eps)
+//       (svmTrainMain.cpp:310) on the exact f — then per side a 16-bit key
+//       prefix threshold from two radix-histogram passes (no sort), and the
+//       new working set: the most violating rows alternately from I_up /
+//       I_low (the global extremes first), duplicates removed through LDS
+//       hash tables, then the newest rows of the previous set.  Workgroup a then
+//       gathers row a of the q x q sub-Gram from the resident Gram (q random
+//       columns of one row: one load per thread — the whole grid does the
+//       scattered reads a single CU could not issue fast enough);
+//   ws_solve   (ONE workgroup; the sub-problem runs on wave 0 alone)
+//       sub-Gram -> LDS, then the reference's pair rule (selection
+//       svmTrainMain.cpp:255-277, update :282-299 through the same
+//       pair_update as every engine) on the q rows: per step two DPP wave
+//       minima (row_bcast reductions), ballots for the lowest position, seven
+//       LDS reads and a register update of f / alpha — no barrier, no global
+//       memory, ~150 instructions of one wave;
+//   ws_select  (grid over the local rows, 256-thread workgroups)
+//       f_j += sum_k coef_k K(idx_k, j) for the round's alpha changes (a
+//       stream over the changed Gram rows), I_up / I_low classification and
+//       each workgroup's kWsCand smallest keys per side.
+//
+// The reference spends one MPI Allgather and >= 7 host round trips per pair
+// (svmTrainMain.cpp:235-310); the persistent SMO engine one grid-wide key
+// exchange (~4.3 us).  Here a pair step costs ~0.3 us of one wave and the
+// grid-wide work happens once per round of ~50 pair steps.
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+constexpr int kWsGatherThreads = 256;
+constexpr int kWsMaxCand = kWsMaxGroups * kWsCand;  // per side
+constexpr int kWsHash = 1024;                        // LDS hash slots per side (load factor <= 0.19)
+
+// Phase stamps (DPSVM_STAMPS), ring slot = round: ws_gather workgroup 0
+// [1] entry [2] merged [8] exit; ws_solve [0] entry [3] sub-Gram loaded
+// [4] solved [5] pair steps; ws_select workgroup 0 [6] entry [7] exit.
+#define WS_STAMP(k)                                                                            \
+  do {                                                                                         \
+    if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + (k)] =          \
+        __builtin_amdgcn_s_memrealtime();                                                      \
+  } while (0)
+
+__device__ __forceinline__ float f_add1(float fj, float c, float k) {
+#pragma clang fp contract(off)
+  return fj + c * k;
+}
+
+// full-wave minima of two floats: v_min_f32 with DPP operands (in-row
+// butterflies, then row_bcast15 / row_bcast31 fold the rows into lane 63,
+// GFX9 DPP), the two chains interleaved so each fills the other's DPP read-
+// after-write wait states; one readlane each.  (The intrinsic path emits a
+// separate dpp move plus an IEEE canonicalize per step: 2.5x the issue slots.)
+__device__ __forceinline__ void wave_min2_f32(float& a, float& b) {
+  asm volatile(
+      "s_nop 1\n"
+      "v_min_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_min_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_min_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_min_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_min_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "v_min_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+      "v_min_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+      "s_nop 1\n"
+      : "+v"(a), "+v"(b));
+  a = readlane_f32(a, 63);
+  b = readlane_f32(b, 63);
+}
+
+// exclusive prefix of small counts (0..15) over a 256-thread block in thread
+// order, via bit-plane ballots; *total = block sum.  wsum: 4 ints.
+__device__ __forceinline__ int block_scan_small256(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  int pre = 0, wtot = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint64_t m = __ballot((v >> b) & 1);
+    pre += __popcll(m & below) << b;
+    wtot += __popcll(m) << b;
+  }
+  if (lane == 0) wsum[wave] = wtot;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWsGatherThreads / 64; ++w) {
+    off += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off + pre;
+}
+
+// first bin b of a 256-bin histogram (one wave: 4 bins per lane) whose
+// inclusive prefix reaches `target`; *below = count in bins < b.  -1 when the
+// histogram holds fewer than target.  Uniform result.
+__device__ __forceinline__ int wave_find_bin(const int* hist, int target, int* below) {
+  const int lane = threadIdx.x & 63;
+  const int h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+  const int s4 = h0 + h1 + h2 + h3;
+  int incl = s4;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o);
+    incl += lane >= o ? t : 0;
+  }
+  const uint64_t hit = __ballot(incl >= target);
+  if (!hit) {
+    *below = __shfl(incl, 63);
+    return -1;
+  }
+  const int L = (int)__builtin_ctzll(hit);
+  int acc = __shfl(incl - s4, L);
+  const int g0 = __shfl(h0, L), g1 = __shfl(h1, L), g2 = __shfl(h2, L);
+  int bin = 4 * L;
+  if (acc + g0 < target) {
+    acc += g0;
+    ++bin;
+    if (acc + g1 < target) {
+      acc += g1;
+      ++bin;
+      if (acc + g2 < target) {
+        acc += g2;
+        ++bin;
+      }
+    }
+  }
+  *below = acc;
+  return bin;
+}
+
+// exclusive prefix over a 256-thread block (thread order) of four packed
+// 12-bit fields (each per-thread value <= 7): bit-plane ballots of the three
+// low bits of every field; *total = block sums.  wsum: 4 u64.
+__device__ __forceinline__ uint64_t block_scan_fields(uint64_t v, uint64_t* wsum, uint64_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint64_t pre = 0, wtot = 0;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int bit = 12 * f + b;
+      const uint64_t mk = __ballot((v >> bit) & 1);
+      pre += (uint64_t)__popcll(mk & below) << bit;
+      wtot += (uint64_t)__popcll(mk) << bit;
+    }
+  }
+  if (lane == 0) wsum[wave] = wtot;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWsGatherThreads / 64; ++w) {
+    off += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off + pre;
+}
+
+__device__ __forceinline__ uint32_t ws_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 22; }
+
+__device__ __forceinline__ void ws_hash_insert(int32_t* keys, int32_t* vals, int32_t idx, int32_t v) {
+  uint32_t h = ws_hash(idx);
+  while (true) {
+    const int32_t old = atomicCAS(keys + h, -1, idx);
+    if (old == -1) {
+      vals[h] = v;
+      return;
+    }
+    h = (h + 1) & (kWsHash - 1);
+  }
+}
+
+__device__ __forceinline__ int32_t ws_hash_find(const int32_t* keys, const int32_t* vals, int32_t idx) {
+  uint32_t h = ws_hash(idx);
+  for (int probe = 0; probe < kWsHash; ++probe) {
+    const int32_t k = keys[h];
+    if (k == idx) return vals[h];
+    if (k == -1) return -1;
+    h = (h + 1) & (kWsHash - 1);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
+  if (!s) return;
+  s->iter = c->iter;
+  s->done = c->done;
+  s->b_hi = c->b_hi;
+  s->b_lo = c->b_lo;
+  s->outer = c->outer;
+  __atomic_store_n(&s->seq, (int32_t)c->outer, __ATOMIC_RELEASE);
+}
+
+// ---------------------------------------------------------------------------
+// ws_select: f update of the last round + per-workgroup candidates
+// ---------------------------------------------------------------------------
+// Threads of a workgroup: 256 rows (x RPT) times PARTS partitions of the
+// changed-row list.  Each partition sums its contiguous slice of the list in
+// list order; the slices combine in partition order — the rounding depends on
+// the list only (never on the grid or the rank count), and every thread has at
+// most ~48 Gram loads of one batch in flight instead of a chain of batches.
+template <int RPT>
+constexpr int ws_parts() {
+  return RPT <= 2 ? 4 : (RPT <= 4 ? 2 : 1);
+}
+
+template <int RPT>
+__global__ __launch_bounds__(kWsSelThreads * 4) void ws_select_kernel(WsArgs a) {
+  constexpr int PARTS = ws_parts<RPT>();
+  constexpr int CH = RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
+  __shared__ int32_t s_idx[kWsMax];
+  __shared__ float s_coef[kWsMax];
+  __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][kWsSelThreads * RPT];
+  __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x & (kWsSelThreads - 1), part = threadIdx.x / kWsSelThreads;
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(6);
+  const int na = c->n_apply;
+  const int done = c->done;
+  if (na == 0 && done != kRunning) return;
+  for (int k = threadIdx.x; k < na; k += kWsSelThreads * PARTS) {
+    s_idx[k] = c->apply_idx[k];
+    s_coef[k] = c->apply_coef[k];
+  }
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * RPT * kWsSelThreads + tid;
+  float f[RPT];
+  bool has[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int64_t j = base + (int64_t)r * kWsSelThreads;
+    has[r] = r < a.rpt && j < a.nl;
+    f[r] = has[r] && part == 0 ? a.f[j] : 0.f;
+  }
+  if (na > 0) {
+    const int per = (na + PARTS - 1) / PARTS;
+    const int k_lo = part * per, k_hi = min(na, k_lo + per);
+    float acc[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+    for (int k0 = k_lo; k0 < k_hi; k0 += CH) {
+      float kv[CH][RPT];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int kk = min(k0 + u, k_hi - 1);
+        const float* row = a.gram + (int64_t)s_idx[kk] * a.ldg;
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) kv[u][r] = has[r] ? row[base + r * kWsSelThreads] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        if (k0 + u < k_hi) {
+          const float cc = s_coef[k0 + u];
+#pragma unroll
+          for (int r = 0; r < RPT; ++r) acc[r] = f_add1(acc[r], cc, kv[u][r]);
+        }
+      }
+    }
+    if (PARTS > 1) {
+      if (part > 0) {
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) s_part[part - 1][r * kWsSelThreads + tid] = acc[r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 1; p < PARTS; ++p) {
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+#pragma clang fp contract(off)
+          acc[r] = acc[r] + s_part[p - 1][r * kWsSelThreads + tid];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+#pragma clang fp contract(off)
+      f[r] = f[r] + acc[r];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (has[r] && part == 0) a.f[base + r * kWsSelThreads] = f[r];
+      bad |= has[r] && part == 0 && !isfinite(f[r]);
+    }
+    if (bad) atomicOr(&c->nonfinite, 1);
+  }
+  if (done != kRunning) return;  // uniform
+
+  // partition 0 (waves 0..3) classifies and extracts; the other waves idle to
+  // the one barrier below (no wave leaves before it)
+  uint64_t ku[RPT], kl[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    ku[r] = kl[r] = kKeyNone;
+    if (has[r] && part == 0) {
+      const int64_t gj = a.off + base + r * kWsSelThreads;
+      const float av = a.alpha[gj], yv = a.y[gj];
+      if (in_up(av, yv, a.C)) ku[r] = make_key(f[r], (uint32_t)gj);
+      if (in_low(av, yv, a.C)) kl[r] = make_key(-f[r], (uint32_t)gj);
+    }
+  }
+  // each wave's kWsCand smallest keys per side (DPP minima, no barrier), then
+  // wave 0 merges the four lists; the owner of a winner drops it (keys are
+  // unique: the global index is in the low bits)
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int round = 0; round < kWsCand && part == 0; ++round) {
+    uint64_t mu = kKeyNone, ml = kKeyNone;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      mu = ku[r] < mu ? ku[r] : mu;
+      ml = kl[r] < ml ? kl[r] : ml;
+    }
+    mu = wave_min_u64(mu);
+    ml = wave_min_u64(ml);
+    if (lane == 0) {
+      s_wc[wave][0][round] = mu;
+      s_wc[wave][1][round] = ml;
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (ku[r] == mu) ku[r] = kKeyNone;
+      if (kl[r] == ml) kl[r] = kKeyNone;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    constexpr int W = kWsSelThreads / 64;
+    uint64_t eu = lane < W * kWsCand ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
+    uint64_t el = lane < W * kWsCand ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
+    uint64_t* out = a.cand + (size_t)blockIdx.x * 2 * kWsCand;
+    for (int round = 0; round < kWsCand; ++round) {
+      const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
+      if (lane == 0) {
+        out[round] = mu;
+        out[kWsCand + round] = ml;
+      }
+      if (eu == mu) eu = kKeyNone;
+      if (el == ml) el = kKeyNone;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(7);
+}
+
+// ---------------------------------------------------------------------------
+// ws_gather: merge (every workgroup) + one sub-Gram row per workgroup
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
+  __shared__ int s_hist[2][256];
+  __shared__ int s_sel[2][2];
+  __shared__ int s_thr[2];
+  __shared__ uint64_t s_wsum64[4];
+  __shared__ uint64_t s_sv[2][kWsMaxCand];
+  __shared__ int32_t s_hash[4][kWsHash];  // up keys, up ranks, low keys, low ranks
+  __shared__ int32_t s_idx[kWsMax];
+  __shared__ int32_t s_keep[2 * kWsMax];  // per interleaved position: final slot or -1
+  __shared__ uint64_t s_scr[8];
+  __shared__ int s_wsum[4];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  if (lead) WS_STAMP(1);
+  if (c->done != kRunning) {
+    // a round ended the run (max_iter / no pair): its changes were applied by
+    // the ws_select that followed it; nothing may be applied twice
+    if (lead) c->n_apply = 0;
+    return;
+  }
+  const int G = a.G;
+  const int64_t r_now = c->outer;
+  const int par = (int)(r_now & 1);
+  const int q_prev = c->q[par ^ 1];
+  const int want = q_prev == 0 ? a.q_max : min(a.n_new, a.q_max);
+
+  // ---- every candidate list in registers (one load batch) ----
+  uint64_t lu[kWsCand], ll[kWsCand];
+#pragma unroll
+  for (int r = 0; r < kWsCand; ++r) {
+    lu[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + r] : kKeyNone;
+    ll[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + kWsCand + r] : kKeyNone;
+  }
+  // ---- global minima (stop test) ----
+  uint64_t gu = lu[0], gl = ll[0];
+  block_min2_u64<kWsGatherThreads>(gu, gl, s_scr);
+  const float b_hi = key_value(gu), b_lo = -key_value(gl);
+  const int64_t it0 = c->iter;
+  int stop = kRunning;
+  if (c->nonfinite) stop = kNonFinite;
+  else if (gu == kKeyNone || gl == kKeyNone) stop = kNoPair;
+  else if (!isfinite(b_hi) || !isfinite(b_lo)) stop = kNonFinite;
+  else if (!(b_lo > b_hi + 2.0f * a.eps)) stop = kConverged;
+  else if (it0 >= a.max_iter) stop = kMaxIter;
+  if (stop != kRunning) {
+    if (lead) {
+      c->done = stop;
+      c->n_apply = 0;  // applied by the last ws_select already
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+      ws_status(a.status, c);
+    }
+    return;
+  }
+
+  // ---- per side, a 16-bit key prefix T: the rows whose prefix is <= T hold
+  // >= m depth-d list entries, hence >= m (d + 1) >= ceil(want / 2)
+  // candidates.  Two 8-bit radix passes over the depth-d entries (LDS
+  // histograms): no sort.  The new rows are then taken by class — the global
+  // extreme first, prefix < T, prefix == T — each class in list (row) order,
+  // so a cut only ever drops rows of the boundary class. ----
+  const int half = (want + 1) / 2;
+  const int d = min(kWsCand - 1, (half + G - 1) / G - 1);
+  const int m = (half + d) / (d + 1);
+  uint64_t hd[2] = {lu[0], ll[0]};
+#pragma unroll
+  for (int r = 1; r < kWsCand; ++r) {
+    hd[0] = r == d ? lu[r] : hd[0];
+    hd[1] = r == d ? ll[r] : hd[1];
+  }
+  for (int t = tid; t < 4 * kWsHash; t += kWsGatherThreads) (&s_hash[0][0])[t] = -1;
+  s_hist[0][tid] = 0;
+  s_hist[1][tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd)
+    if (hd[sd] != kKeyNone) atomicAdd(&s_hist[sd][(int)(hd[sd] >> 56)], 1);
+  __syncthreads();
+  if (tid < 128) {  // wave 0: up side, wave 1: low side
+    const int sd = tid >> 6;
+    int below = 0;
+    const int b1 = wave_find_bin(s_hist[sd], m, &below);
+    if ((tid & 63) == 0) {
+      s_sel[sd][0] = b1;
+      s_sel[sd][1] = below;
+    }
+  }
+  __syncthreads();
+  s_hist[0][tid] = 0;
+  s_hist[1][tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd)
+    if (hd[sd] != kKeyNone && s_sel[sd][0] >= 0 && (int)(hd[sd] >> 56) == s_sel[sd][0])
+      atomicAdd(&s_hist[sd][(int)(hd[sd] >> 48) & 255], 1);
+  __syncthreads();
+  if (tid < 128) {
+    const int sd = tid >> 6;
+    int below = 0;
+    const int b1 = s_sel[sd][0];
+    const int b2 = b1 >= 0 ? wave_find_bin(s_hist[sd], m - s_sel[sd][1], &below) : -1;
+    if ((tid & 63) == 0) s_thr[sd] = b1 >= 0 && b2 >= 0 ? (b1 << 8) | b2 : 0xFFFF;  // too few: every row
+  }
+  __syncthreads();
+  const uint32_t T[2] = {(uint32_t)s_thr[0], (uint32_t)s_thr[1]};
+  const uint64_t gmin[2] = {gu, gl};
+  // class counts per thread (the global extreme is placed first, separately)
+  uint64_t packed = 0;  // 12-bit fields: [up A, up B, low A, low B]
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+#pragma unroll
+    for (int r = 0; r < kWsCand; ++r) {
+      const uint64_t k = sd ? ll[r] : lu[r];
+      if (k == kKeyNone || k == gmin[sd]) continue;
+      const uint32_t pre = (uint32_t)(k >> 48);
+      if (pre < T[sd]) packed += 1ull << (24 * sd);
+      else if (pre == T[sd]) packed += 1ull << (24 * sd + 12);
+    }
+  }
+  uint64_t ptot = 0;
+  const uint64_t pofs = block_scan_fields(packed, s_wsum64, &ptot);
+  int S[2];
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+    const int totA = (int)((ptot >> (24 * sd)) & 4095), totB = (int)((ptot >> (24 * sd + 12)) & 4095);
+    int oA = 1 + (int)((pofs >> (24 * sd)) & 4095), oB = 1 + totA + (int)((pofs >> (24 * sd + 12)) & 4095);
+    S[sd] = 1 + totA + totB;
+#pragma unroll
+    for (int r = 0; r < kWsCand; ++r) {
+      const uint64_t k = sd ? ll[r] : lu[r];
+      if (k == kKeyNone) continue;
+      if (k == gmin[sd]) {
+        s_sv[sd][0] = k;
+        continue;
+      }
+      const uint32_t pre = (uint32_t)(k >> 48);
+      if (pre < T[sd]) s_sv[sd][oA++] = k;
+      else if (pre == T[sd]) s_sv[sd][oB++] = k;
+    }
+  }
+  __syncthreads();
+  if (lead) WS_STAMP(2);
+
+  // ---- the new working set ----
+  int32_t* hk_u = s_hash[0];
+  int32_t* hv_u = s_hash[1];
+  int32_t* hk_l = s_hash[2];
+  int32_t* hv_l = s_hash[3];
+  if (tid < want) {
+    if (tid < S[0]) ws_hash_insert(hk_u, hv_u, (int32_t)key_index(s_sv[0][tid]), tid);
+    if (tid < S[1]) ws_hash_insert(hk_l, hv_l, (int32_t)key_index(s_sv[1][tid]), tid);
+  }
+  __syncthreads();
+  // interleaved positions 2r (up rank r), 2r + 1 (low rank r); a row's first
+  // position wins; thread t owns positions 2t and 2t + 1
+  bool kp[2] = {false, false};
+  int32_t ki[2] = {-1, -1};
+  if (tid < want) {
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      const uint64_t kk = tid < S[sd] ? s_sv[sd][tid] : kKeyNone;
+      if (kk != kKeyNone) {
+        ki[sd] = (int32_t)key_index(kk);
+        if (sd == 0) {
+          const int rl = ws_hash_find(hk_l, hv_l, ki[sd]);
+          kp[sd] = !(rl >= 0 && rl < tid);
+        } else {
+          const int ru = ws_hash_find(hk_u, hv_u, ki[sd]);
+          kp[sd] = !(ru >= 0 && ru <= tid);
+        }
+      }
+    }
+  }
+  int kept = 0;
+  const int slot0 = block_scan_small256((int)kp[0] + (int)kp[1], s_wsum, &kept);
+  const int n_chosen = min(kept, want);
+  if (tid < want) {
+    const int s0 = slot0, s1 = slot0 + (int)kp[0];
+    const bool c0 = kp[0] && s0 < want, c1 = kp[1] && s1 < want;
+    s_keep[2 * tid] = c0 ? s0 : -1;
+    s_keep[2 * tid + 1] = c1 ? s1 : -1;
+    if (c0) s_idx[s0] = ki[0];
+    if (c1) s_idx[s1] = ki[1];
+  }
+  __syncthreads();
+  // the previous set (newest first): rows not chosen again, up to q_max
+  bool pk = false;
+  int32_t pidx = -1;
+  if (tid < q_prev) {
+    pidx = c->idx[par ^ 1][tid];
+    const int ru = ws_hash_find(hk_u, hv_u, pidx);
+    const int rl = ws_hash_find(hk_l, hv_l, pidx);
+    pk = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+  }
+  int ptotal = 0;
+  const int pslot = block_scan_small256((int)pk, s_wsum, &ptotal);
+  if (pk && n_chosen + pslot < a.q_max) s_idx[n_chosen + pslot] = pidx;
+  const int q = min(a.q_max, n_chosen + ptotal);
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (int t = tid; t < q; t += kWsGatherThreads) c->idx[par][t] = s_idx[t];
+    if (tid == 0) {
+      c->q[par] = q;
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+    }
+  }
+  // ---- row a of the sub-Gram, the row's alpha / y / f ----
+  const int ra = blockIdx.x;
+  if (ra < q) {
+    const int32_t gi = s_idx[ra];
+    const float* grow = a.gram + (int64_t)gi * a.ldg - a.off;
+    for (int b = tid; b < q; b += kWsGatherThreads) a.subg[ra * q + b] = grow[s_idx[b]];
+    if (tid == 0) {
+      a.aux[ra] = a.alpha[gi];
+      a.aux[kWsMax + ra] = a.y[gi];
+      a.aux[2 * kWsMax + ra] = a.f[gi - a.off];
+    }
+  }
+  if (lead) WS_STAMP(8);
+}
+
+// ---------------------------------------------------------------------------
+// ws_solve: the sub-problem on wave 0
+// ---------------------------------------------------------------------------
+// alpha of working-set position `pos` (uniform) becomes `an` (uniform):
+// reclassify that row in its owner lane (f is fu when the row is in I_up,
+// else -fl).  The slot is an SGPR: one scalar branch, selects on the lane.
+__device__ __forceinline__ void ws_set_slot(bool me, float an, float C, float& fu, float& fl, float yv) {
+  const float INF = __builtin_inff();
+  const float fv = fu != INF ? fu : -fl;
+  const float nu = in_up(an, yv, C) ? fv : INF;
+  const float nl = in_low(an, yv, C) ? -fv : INF;
+  fu = me ? nu : fu;
+  fl = me ? nl : fl;
+}
+__device__ __forceinline__ void ws_set_alpha(int pos, float an, int lane, float C, float (&fu)[3], float (&fl)[3],
+                                             const float (&yr)[3]) {
+  const int s = pos >> 6;
+  const bool me = lane == (pos & 63);
+  if (s == 0) ws_set_slot(me, an, C, fu[0], fl[0], yr[0]);
+  else if (s == 1) ws_set_slot(me, an, C, fu[1], fl[1], yr[1]);
+  else ws_set_slot(me, an, C, fu[2], fl[2], yr[2]);
+}
+
+// The reference's pair update (svmTrainMain.cpp:282-295; pair_update in
+// common.hpp, same clipping modes) on uniform operands, with the quotient
+// y_lo (b_hi - b_lo) / eta from a refined hardware reciprocal: the sub-problem
+// step needs no bit parity with the pair-at-a-time engines (f is updated from
+// the alphas actually taken, so it stays consistent), and the IEEE division
+// sequence is the longest dependent chain of a step.
+__device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float y_hi, float y_lo, float bh, float bl,
+                                                   float khl, float C, float tau, int clip, bool same) {
+#pragma clang fp contract(off)
+  float eta = (1.0f + 1.0f) - 2.0f * khl;
+  eta = eta >= tau ? eta : tau;
+  float r = __builtin_amdgcn_rcpf(eta);
+  r = r + r * __builtin_fmaf(-eta, r, 1.0f);  // one Newton step: ~0.5 ulp
+  const float s = y_lo * y_hi;
+  float a_lo_new = a_lo + (y_lo * (bh - bl)) * r;
+  float a_hi_new;
+  if (clip == (int)ClipMode::Box && !same) {
+    float L, H, hL, hH;
+    if (y_hi != y_lo) {
+      const float dl = a_lo - a_hi;
+      L = dl > 0.f ? dl : 0.f;
+      hL = dl > 0.f ? 0.f : -1.f;
+      H = C + dl < C ? C + dl : C;
+      hH = C + dl < C ? C : -1.f;
+    } else {
+      const float sm = a_lo + a_hi;
+      L = sm - C > 0.f ? sm - C : 0.f;
+      hL = sm - C > 0.f ? C : -1.f;
+      H = sm < C ? sm : C;
+      hH = sm < C ? 0.f : -1.f;
+    }
+    const bool atL = a_lo_new <= L, atH = !atL && a_lo_new >= H;
+    a_lo_new = atL ? L : (atH ? H : a_lo_new);
+    const float snap = atL ? hL : (atH ? hH : -1.f);
+    a_hi_new = snap >= 0.f ? snap : a_hi + (s * (a_lo - a_lo_new));
+    a_hi_new = clip01(a_hi_new, 0.0f, C);
+  } else {
+    a_hi_new = a_hi + (s * (a_lo - a_lo_new));
+    a_lo_new = clip01(a_lo_new, 0.0f, C);
+    a_hi_new = clip01(a_hi_new, 0.0f, C);
+  }
+  PairUpdate u;
+  u.a_hi_new = a_hi_new;
+  u.a_lo_new = a_lo_new;
+  u.c_hi = (a_hi_new - a_hi) * y_hi;
+  u.c_lo = (a_lo_new - a_lo) * y_lo;
+  return u;
+}
+
+// lowest working-set position whose value equals the (uniform) minimum v
+__device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
+  const uint64_t m0 = __ballot(x[0] == v), m1 = __ballot(x[1] == v), m2 = __ballot(x[2] == v);
+  if (m0) return __builtin_ctzll(m0);
+  if (m1) return 64 + __builtin_ctzll(m1);
+  if (m2) return 128 + __builtin_ctzll(m2);
+  return -1;
+}
+
+__global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float K[];  // q x q sub-Gram
+  __shared__ float s_a[kWsMax], s_y[kWsMax], s_f[kWsMax];
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) WS_STAMP(0);
+  if (c->done != kRunning) return;
+  const int par = (int)(c->outer & 1);
+  const int q = c->q[par];
+  const float b_hi = c->b_hi, b_lo = c->b_lo;
+  const int64_t it0 = c->iter;
+  {
+    const int qq = q * q;
+    const int n4 = qq >> 2;
+    const float4* src = (const float4*)a.subg;
+    float4* dst = (float4*)K;
+    for (int i = tid; i < n4; i += kWsSolveThreads) dst[i] = src[i];
+    for (int i = 4 * n4 + tid; i < qq; i += kWsSolveThreads) K[i] = a.subg[i];
+    if (tid < q) {
+      s_a[tid] = a.aux[tid];
+      s_y[tid] = a.aux[kWsMax + tid];
+      s_f[tid] = a.aux[2 * kWsMax + tid];
+      s_idx[tid] = c->idx[par][tid];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) WS_STAMP(3);
+  if (wave != 0) return;
+
+  const float INF = __builtin_inff();
+  const float C = a.C;
+  const float eps_in = fmaxf(a.eps, a.rel_local * 0.5f * (b_lo - b_hi));
+  float fu[3], fl[3], yr[3], a0[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int p = lane + 64 * s;
+    const bool v = p < q;
+    const float fv = v ? s_f[p] : 0.f;
+    a0[s] = v ? s_a[p] : 0.f;
+    yr[s] = v ? s_y[p] : 1.f;
+    fu[s] = v && in_up(a0[s], yr[s], C) ? fv : INF;
+    fl[s] = v && in_low(a0[s], yr[s], C) ? -fv : INF;
+  }
+  const int64_t room = a.max_iter - it0;
+  const int cap = (int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max);
+  int inner = 0;
+  bool bad = false;
+  while (inner < cap) {
+    float mu = fminf(fminf(fu[0], fu[1]), fu[2]);
+    float ml = fminf(fminf(fl[0], fl[1]), fl[2]);
+    wave_min2_f32(mu, ml);
+    if (!(mu < INF) || !(ml < INF)) break;
+    const float bh = mu, bl = -ml;
+    if (!(bl > bh + 2.0f * eps_in)) break;
+    const int ph = ws_argpos(fu, mu), pl = ws_argpos(fl, ml);
+    if (ph < 0 || pl < 0) {  // NaN
+      bad = true;
+      break;
+    }
+    // every LDS read of the step in one batch: the pair's alphas / labels,
+    // K(hi, lo) and the two sub-Gram rows
+    const float a_hi = s_a[ph], y_hi = s_y[ph], a_lo = s_a[pl], y_lo = s_y[pl];
+    const float khl = K[ph * q + pl];
+    float kh[3], kl[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int p = min(lane + 64 * s, q - 1);
+      kh[s] = K[ph * q + p];
+      kl[s] = K[pl * q + p];
+    }
+    const PairUpdate up = ws_pair_step(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, a.clip, ph == pl);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      float dl;
+      {
+#pragma clang fp contract(off)
+        dl = up.c_hi * kh[s] + up.c_lo * kl[s];  // f_apply's delta (device_util.hpp)
+        fu[s] = fu[s] + dl;
+        fl[s] = fl[s] - dl;  // -(f + delta): exact negation of the same rounding
+      }
+    }
+    ws_set_alpha(pl, up.a_lo_new, lane, C, fu, fl, yr);
+    ws_set_alpha(ph, up.a_hi_new, lane, C, fu, fl, yr);  // hi written last (svmTrainMain.cpp:298-299)
+    if (lane == 0) {
+      s_a[pl] = up.a_lo_new;
+      s_a[ph] = up.a_hi_new;
+    }
+    ++inner;
+  }
+  // ---- commit: alphas, the changed rows for the f update, control, status ----
+  int n_apply = 0;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int p = lane + 64 * s;
+    const float an = p < q ? s_a[p] : 0.f;
+    const bool nz = p < q && an != a0[s];
+    const uint64_t mk = __ballot(nz);
+    const int at = n_apply + __popcll(mk & ((1ull << lane) - 1ull));
+    if (nz) {
+      const int32_t gi = s_idx[p];
+      a.alpha[gi] = an;
+      float dc;
+      {
+#pragma clang fp contract(off)
+        dc = (an - a0[s]) * yr[s];
+      }
+      c->apply_idx[at] = gi;
+      c->apply_coef[at] = dc;
+    }
+    n_apply += __popcll(mk);
+  }
+  if (lane == 0) {
+    WS_STAMP(4);
+    if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + 5] = (uint64_t)inner;
+    c->n_apply = n_apply;
+    c->iter = it0 + inner;
+    c->outer = c->outer + 1;
+    c->done = bad ? kNonFinite : inner == 0 ? kNoPair : (it0 + inner >= a.max_iter ? kMaxIter : kRunning);
+    ws_status(a.status, c);
+  }
+}
+
+}  // namespace dev
+
+namespace launch {
+
+void ws_geometry(int64_t nl, int32_t* G, int32_t* rpt) {
+  const int64_t g = std::max<int64_t>(1, std::min<int64_t>(kWsMaxGroups, (nl + kWsSelThreads - 1) / kWsSelThreads));
+  const int64_t r = (nl + g * kWsSelThreads - 1) / (g * kWsSelThreads);
+  *G = (int32_t)g;
+  *rpt = (int32_t)std::max<int64_t>(1, r);
+}
+
+bool ws_supported(int64_t nl, int q_max) {
+  int32_t G = 0, rpt = 0;
+  ws_geometry(nl, &G, &rpt);
+  return q_max >= 2 && q_max <= kWsMax && rpt <= kWsMaxRPT && nl < (int64_t)1 << 31;
+}
+
+void ws_select(const WsArgs& a, hipStream_t s) {
+  const dim3 grid(a.G);
+  auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 2 ? 4 : rpt <= 4 ? 2 : 1)); };
+  if (a.rpt <= 1) dev::ws_select_kernel<1><<<grid, threads(1), 0, s>>>(a);
+  else if (a.rpt <= 2) dev::ws_select_kernel<2><<<grid, threads(2), 0, s>>>(a);
+  else if (a.rpt <= 4) dev::ws_select_kernel<4><<<grid, threads(4), 0, s>>>(a);
+  else if (a.rpt <= 8) dev::ws_select_kernel<8><<<grid, threads(8), 0, s>>>(a);
+  else dev::ws_select_kernel<16><<<grid, threads(16), 0, s>>>(a);
+  post_launch("ws_select", s);
+}
+
+void ws_gather(const WsArgs& a, hipStream_t s) {
+  dev::ws_gather_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+  post_launch("ws_gather", s);
+}
+
+void ws_solve(const WsArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)a.q_max * a.q_max * sizeof(float);
+  static size_t attr = 64 * 1024;  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  if (lds > attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)dev::ws_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    attr = lds;
+  }
+  dev::ws_solve_kernel<<<1, kWsSolveThreads, lds, s>>>(a);
+  post_launch("ws_solve", s);
+}
+
+}  // namespace launch
+}  // namespace dpsvm

@@ -116,6 +116,7 @@ py::dict result_dict(const SolveResult& r) {
   d["x_passes"] = r.x_passes;
   d["spec_rows"] = r.spec_rows;
   d["host_hits"] = r.host_hits;
+  d["outer"] = r.outer;
   d["host_cache_lines"] = r.host_cache_lines;
   d["cache_lines"] = r.cache_lines;
   d["world"] = r.world;
@@ -180,6 +181,12 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("census_groups", &SolverParams::census_groups)
       .def_readwrite("verify_ranks", &SolverParams::verify_ranks)
       .def_readwrite("dp_policy", &SolverParams::dp_policy)
+      .def_readwrite("solver", &SolverParams::solver)
+      .def_readwrite("ws_size", &SolverParams::ws_size)
+      .def_readwrite("ws_new", &SolverParams::ws_new)
+      .def_readwrite("ws_rel", &SolverParams::ws_rel)
+      .def_readwrite("ws_inner", &SolverParams::ws_inner)
+      .def_readwrite("ws_block", &SolverParams::ws_block)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
       .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });
 

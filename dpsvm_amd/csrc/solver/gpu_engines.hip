@@ -1,4 +1,4 @@
-// The five iteration engines of the device solver.  Each one seeds the device
+// The iteration engines of the device solver.  Each one seeds the device
 // state at the start of the timed region and then advances the SMO in blocks
 // of iterations that never return to the host (the host polls a pinned status
 // record one block behind).
@@ -13,6 +13,9 @@
 //                     iteration (smo_fused_lru.hip)
 //   chain             rows / step / [collective] / finalize per iteration
 //                     (smo_kernels.hip): the partitioned-X fallback
+//   ws-dense          Gram resident; working-set rounds: one workgroup solves a
+//                     q-row sub-problem from an LDS sub-Gram, one grid pass
+//                     updates f and selects the next candidates (smo_ws.hip)
 //
 // Reference per-iteration path: svmTrainMain.cpp:235-310 (host loop, >= 7
 // blocking host<->device round trips, one MPI Allgather).
@@ -244,6 +247,56 @@ struct FusedCache final : Engine {
   }
 };
 
+// Working-set rounds on the resident Gram (smo_ws.hip).  Seed: the Gram GEMM,
+// the control record (no working set yet) and the first candidate selection;
+// a block is B rounds of [ws_gather, ws_solve, ws_select] (one hipGraph), so f is
+// consistent with alpha at every block boundary (checkpoints need no pending
+// pair) and the host polls the status one block behind like the SMO engines.
+struct WsDense final : DenseBase {
+  EngineKind kind() const override { return EngineKind::WsDense; }
+  int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
+  static void round(GpuSolver::Impl& m) {
+    launch::ws_gather(m.wsa, m.stream);
+    launch::ws_solve(m.wsa, m.stream);
+    launch::ws_select(m.wsa, m.stream);
+  }
+  void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {
+    gram(m, res);
+    WsCtrl c;
+    memset(&c, 0, sizeof(c));
+    c.iter = iter0;
+    c.done = kRunning;
+    c.b_hi = b_hi;
+    c.b_lo = b_lo;
+    HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
+    launch::ws_select(m.wsa, m.stream);
+    const bool graphs = m.p.use_graph && !m.p.sync_debug && !sync_debug_env();
+    if (graphs && !m.gexec) {
+      const int B = block(m.p);
+      HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
+      try {
+        for (int i = 0; i < B; ++i) round(m);
+      } catch (...) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(m.stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        throw;
+      }
+      HIP_CHECK(hipStreamEndCapture(m.stream, &m.graph));
+      HIP_CHECK(hipGraphInstantiate(&m.gexec, m.graph, nullptr, nullptr, 0));
+    }
+  }
+  void run_block(GpuSolver::Impl& m, int B) override {
+    if (m.gexec) {
+      HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
+    } else {
+      for (int i = 0; i < B; ++i) round(m);
+    }
+  }
+  Pending pending(GpuSolver::Impl&) override { return {}; }  // alphas committed every round
+};
+
 struct Chain final : Engine {
   EngineKind kind() const override { return EngineKind::Chain; }
   int block(const SolverParams& p) const override { return std::max(1, p.graph_block); }
@@ -259,6 +312,7 @@ std::unique_ptr<Engine> make_engine(EngineKind k) {
     case EngineKind::FusedDense: return std::make_unique<FusedDense>();
     case EngineKind::PersistCache: return std::make_unique<PersistCache>();
     case EngineKind::FusedCache: return std::make_unique<FusedCache>();
+    case EngineKind::WsDense: return std::make_unique<WsDense>();
     default: return std::make_unique<Chain>();
   }
 }

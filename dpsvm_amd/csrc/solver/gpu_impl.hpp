@@ -6,7 +6,7 @@
 //                     engine choice (incl. the residency census)
 //   gpu_exchange.hip  in-kernel peer exchange buffers (IPC / peer mappings, ping),
 //                     small collectives that work on device and host communicators
-//   gpu_engines.hip   the five iteration engines (seed + block of iterations)
+//   gpu_engines.hip   the iteration engines (seed + block of iterations / rounds)
 //   gpu_solve.hip     the timed SMO loop, checkpoints, invariant checks
 //   gpu_predict.hip   SV compaction, accuracy, decision values, GpuPredictor,
 //                     kernel-level test entry points
@@ -92,6 +92,11 @@ struct GpuSolver::Impl {
   std::string xch_diag;
   std::string xch_mem = "none";    // receive-buffer memory kind
   int64_t Gf = 0, RBf = 0;         // fused / persistent geometry: workgroups, rows per workgroup
+  // working-set engine (smo_ws.hip): round control record, candidate keys
+  WsArgs wsa{};
+  WsCtrl* wsctrl = nullptr;
+  uint64_t* wscand = nullptr;
+  float* wssub = nullptr;          // q x q sub-Gram + [3][kWsMax] alpha / y / f of the working set
   uint64_t* stamps = nullptr;      // DPSVM_STAMPS diagnostics
   std::string stamps_path;
   std::vector<uint64_t> h_partials;  // host staging for host-memory communicators
@@ -115,6 +120,7 @@ struct GpuSolver::Impl {
   bool device_comm() const { return world == 1 || comm->device_memory(); }
   bool fused() const { return kind != EngineKind::Chain; }
   bool persistent() const { return kind == EngineKind::PersistDense || kind == EngineKind::PersistCache; }
+  bool working_set() const { return kind == EngineKind::WsDense; }
 
   SmoStatus read_status() const;
   void init_ctrl(int64_t iter0, float b_hi, float b_lo);

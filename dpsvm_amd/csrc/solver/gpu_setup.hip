@@ -34,7 +34,7 @@ GpuSolver::Impl::~Impl() {
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
-                    (void*)plru_meta, (void*)plru_stats})
+                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
   if (hlines_h) (void)hipHostFree(hlines_h);
@@ -303,8 +303,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     const double meta_bytes = (double)m.Gf * launch::plru_stride_words(n, n) * 4.0;
     want_lines = std::min<int64_t>(want_lines, (int64_t)((budget - meta_bytes) / line_bytes));
   }
-  const bool pdense_cand = m.dense && (m.p.persist == 2 || (m.p.persist == 0 && m.p.exchange != 1 && m.p.use_graph &&
-                                                            !m.p.force_collectives)) &&
+  // working-set engine (solver=ws): the resident Gram on one rank (the
+  // replicate dp policy gives every rank a one-rank problem)
+  const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
+  const bool ws_cand = m.p.solver == 2 && m.dense && m.world == 1 && m.replicated && !m.p.force_collectives &&
+                       launch::ws_supported(m.nl, ws_q);
+  if (m.p.solver == 2 && !ws_cand)
+    m.info.engine_note = "ws engine needs the resident Gram on one rank (dense mode, world 1): SMO engine used";
+  const bool pdense_cand = !ws_cand && m.dense &&
+                           (m.p.persist == 2 || (m.p.persist == 0 && m.p.exchange != 1 && m.p.use_graph &&
+                                                 !m.p.force_collectives)) &&
                            m.RBf <= 12 * kFusedThreads && m.Gf <= 256;
   m.L = m.dense ? n : std::max<int64_t>(2, std::min<int64_t>(want_lines, n));
   DPSVM_CHECK(m.L * line_bytes <= (double)freeb, "not enough device memory for 2 kernel-row lines");
@@ -424,7 +432,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       m.info.engine_note = "peer exchange refused: " + m.xch_diag;
     }
   }
-  if (m.dense) m.kind = pdense_cand && m.xch ? EngineKind::PersistDense : EngineKind::FusedDense;
+  if (ws_cand) m.kind = EngineKind::WsDense;
+  else if (m.dense) m.kind = pdense_cand && m.xch ? EngineKind::PersistDense : EngineKind::FusedDense;
   else if (fused_lru_ok) m.kind = plru_cand && m.xch ? EngineKind::PersistCache : EngineKind::FusedCache;
   else m.kind = EngineKind::Chain;
   if (m.persistent() && !m.census(m.kind)) {
@@ -449,13 +458,46 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     a.plru_meta = nullptr;
     a.plru_stride = 0;
   }
+  if (m.kind == EngineKind::WsDense) {
+    WsArgs& w = m.wsa;
+    w = WsArgs{};
+    w.gram = m.lines;
+    w.ldg = m.ldl;
+    w.y = m.y;
+    w.alpha = m.alpha;
+    w.f = m.f;
+    w.n = n;
+    w.nl = m.nl;
+    w.off = m.off;
+    launch::ws_geometry(m.nl, &w.G, &w.rpt);
+    w.q_max = ws_q;
+    // >= 2 new rows: the global maximal violating pair (up rank 0, low rank 0)
+    // is always in the set, so every round makes progress
+    w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, ws_q) : ws_q / 2);
+    w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * ws_q;
+    w.rel_local = m.p.ws_rel;
+    w.C = m.p.C;
+    w.eps = m.p.eps;
+    w.tau = m.p.tau;
+    w.clip = (int)m.p.clip;
+    w.max_iter = m.p.max_iter;
+    m.wscand = dmalloc<uint64_t>((size_t)w.G * 2 * kWsCand, &m.bytes);
+    m.wsctrl = dmalloc<WsCtrl>(1, &m.bytes);
+    m.wssub = dmalloc<float>((size_t)ws_q * ws_q + 3 * kWsMax, &m.bytes);
+    w.cand = m.wscand;
+    w.subg = m.wssub;
+    w.aux = m.wssub + (size_t)ws_q * ws_q;
+    w.ctrl = m.wsctrl;
+    w.status = m.status_d;
+    w.stamps = m.stamps;
+  }
   m.engine = gpu::make_engine(m.kind);
   m.info.iteration = engine_name(m.kind);
   m.info.exchange_mem = m.xch ? m.xch_mem : "none";
   m.info.exchange = m.xch ? (m.world > 1 ? "peer" : "loopback")
                           : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
-  m.info.rows_per_group = m.fused() ? m.RBf : kStepRows;
-  m.info.groups = m.fused() ? m.Gf : m.G;
+  m.info.rows_per_group = m.working_set() ? (int64_t)m.wsa.rpt * kWsSelThreads : m.fused() ? m.RBf : kStepRows;
+  m.info.groups = m.working_set() ? m.wsa.G : m.fused() ? m.Gf : m.G;
   m.info.poll_batch = m.xch ? launch::poll_batch(a) : 0;
   m.info.bytes_device = m.bytes;
   return m.info;

@@ -239,6 +239,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   res.spec_rows = st.spec_rows;
   res.host_hits = st.host_hits;
   res.host_cache_lines = m.H;
+  res.outer = st.outer;
   res.world = m.outer_world;
   if (m.stamps) {
     std::vector<uint64_t> h((size_t)kStampRing * 2 * kStampSlots);

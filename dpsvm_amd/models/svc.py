@@ -52,6 +52,7 @@ _PERSIST = {"auto": 0, "off": 1, "on": 2}
 _CACHE_ENGINE = {"fused": 0, "chain": 1}
 _XCH_MEM = {"auto": 0, "uncached": 1, "coarse": 2}
 _DP = {"auto": 0, "shard": 1, "replicate": 2}
+_SOLVER = {"auto": 0, "smo": 1, "ws": 2}
 
 
 def _pick(table: dict, value: str, name: str) -> int:
@@ -101,6 +102,15 @@ class SVCConfig:
     watchdog_s: float = 1800.0
     census_groups: int = 0          # residency census grid (tests)
     verify_ranks: bool = True       # cross-rank alpha digest after each solve (world > 1)
+    # solver: auto | smo (pair-at-a-time engines, the reference's trajectory) |
+    # ws (working-set rounds: the reference's pair rule on a q-row sub-problem
+    # in LDS, the same global stop test; smo_ws.hip)
+    solver: str = "auto"
+    ws_size: int = 192              # working-set rows (<= 192)
+    ws_new: int = 0                 # rows replaced per round (0: ws_size / 2)
+    ws_rel: float = 0.1             # sub-problem tolerance relative to the global gap
+    ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
+    ws_block: int = 32              # rounds per hipGraph block
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -155,6 +165,12 @@ class SVCConfig:
         p.watchdog_s = float(self.watchdog_s)
         p.census_groups = int(self.census_groups)
         p.verify_ranks = bool(self.verify_ranks)
+        p.solver = _pick(_SOLVER, self.solver, "solver")
+        p.ws_size = int(self.ws_size)
+        p.ws_new = int(self.ws_new)
+        p.ws_rel = float(self.ws_rel)
+        p.ws_inner = int(self.ws_inner)
+        p.ws_block = int(self.ws_block)
         return p
 
     def device_kind(self) -> tuple[str, int]:
@@ -244,6 +260,7 @@ class SVC:
         self.b_ = float(info["b"])
         self.intercept_ = -self.b_
         self.n_iter_ = int(info["iters"])
+        self.n_rounds_ = int(info.get("outer", 0))
         self.status_ = int(info["status"])
         self.converged_ = bool(info["converged"])
         self.fit_time_ = float(info["t_solve"])

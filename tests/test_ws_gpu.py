@@ -1,0 +1,108 @@
+"""Working-set engine (solver="ws", smo_ws.hip) on MI355X.
+
+The ws engine applies the reference's pair rule (svmTrainMain.cpp:255-299) to a
+q-row sub-problem per round, so its trajectory differs from the pair-at-a-time
+engines; what must agree is the optimum it stops at: the reference's stop test
+!(b_lo > b_hi + 2 eps) (svmTrainMain.cpp:310) on the exact gradient, the
+intercept, the support set and the decision function — checked here against
+the float64 numpy model of the reference (tests/ref_smo.py) and against the
+persistent SMO engine."""
+import numpy as np
+import pytest
+import torch
+
+from dpsvm_amd import SVC
+from dpsvm_amd.utils.datasets import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _kkt_gap(X, y, alpha, C, gamma):
+    """b_lo - b_hi of the exact float64 gradient f = K (alpha y) - y."""
+    from ref_smo import rbf_gram
+
+    yy = np.where(y > 0, 1.0, -1.0)
+    a = alpha.astype(np.float64)
+    f = rbf_gram(X, gamma) @ (a * yy) - yy
+    up = ((a == 0) & (yy == 1)) | ((a == C) & (yy != 1)) | ((a > 0) & (a < C))
+    lo = ((a == 0) & (yy != 1)) | ((a == C) & (yy == 1)) | ((a > 0) & (a < C))
+    return f[lo].max() - f[up].min()
+
+
+@pytest.mark.parametrize("clip", ["independent", "box"])
+@pytest.mark.parametrize("case", ["blobs", "mnist", "adult"])
+def test_ws_engine_reaches_the_reference_optimum(case, clip):
+    """box: the dual optimum is unique, so alphas, b, support set and decisions
+    match the float64 model.  independent (the reference's default clipping,
+    svmTrainMain.cpp:294-295) does not keep sum(alpha y) = 0, so the point it
+    stops at depends on the trajectory: there the ws engine must satisfy the
+    same stop test on the exact gradient and classify as well."""
+    from ref_smo import smo_reference, decision
+
+    X, y, C_, g = {
+        "blobs": synthetic("blobs", n=2500, d=12, seed=41, sep=1.2) + (2.0, 0.15),
+        "mnist": synthetic("mnist", n=3000, seed=4) + (10.0, 0.25),
+        "adult": synthetic("adult", n=3000, seed=2) + (1.0, 0.05),
+    }[case]
+    a_ref, b_ref, it_ref = smo_reference(X, y, C=C_, gamma=g, eps=1e-3, clip=clip)
+    ws = SVC(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", solver="ws").fit(X, y)
+    assert ws.setup_info_["iteration"] == "ws-dense"
+    assert ws.converged_ and ws.n_rounds_ > 0
+    gap = _kkt_gap(X, y, ws.alpha_, C_, g)
+    yy = np.where(y > 0, 1.0, -1.0)
+    d_ref = decision(X, y, a_ref, b_ref, g, X)
+    d_ws = ws.decision_function(X)
+    acc_ref, acc_ws = np.mean(np.sign(d_ref) == yy), np.mean(np.sign(d_ws) == yy)
+    agree = np.mean(np.sign(d_ref) == np.sign(d_ws))
+    print(f"{case}/{clip}: gap {gap:.2e} b {ws.b_:.5f} vs {b_ref:.5f} iters {ws.n_iter_} vs {it_ref} "
+          f"acc {acc_ws:.4f} vs {acc_ref:.4f} agree {agree:.4f} max|da| {np.abs(ws.alpha_ - a_ref).max():.3g}")
+    # the stop test holds on the exact gradient (fp32 drift allowance)
+    assert gap < 2e-3 + 2e-4
+    assert abs(acc_ws - acc_ref) < 0.02
+    assert ws.n_iter_ < 3 * it_ref
+    if clip == "box":
+        assert abs(ws.b_ - b_ref) < 1e-2
+        assert np.abs(ws.alpha_ - a_ref).max() < 0.1 * C_
+        sv_ws, sv_ref = set(np.nonzero(ws.alpha_ > 0)[0]), set(np.nonzero(a_ref > 0)[0])
+        assert len(sv_ws ^ sv_ref) <= max(3, len(sv_ref) // 50)
+        assert agree > 0.99
+
+
+def test_ws_engine_deterministic_and_matches_persistent_engine():
+    X, y = synthetic("mnist", n=6000, seed=7)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda")
+    a = SVC(solver="ws", **kw).fit(X, y)
+    b = SVC(solver="ws", **kw).fit(X, y)
+    assert a.n_iter_ == b.n_iter_ and np.array_equal(a.alpha_, b.alpha_)
+    p = SVC(solver="smo", **kw).fit(X, y)
+    assert p.setup_info_["iteration"] == "persistent-dense"
+    assert abs(a.b_ - p.b_) < 1e-2 and abs(a.n_support_ - p.n_support_) <= max(3, p.n_support_ // 100)
+    assert abs(a.train_accuracy() - p.train_accuracy()) < 0.01
+
+
+@pytest.mark.parametrize("q", [2, 16, 64, 130])
+def test_ws_engine_small_working_sets_and_max_iter(q):
+    X, y = synthetic("adult", n=2000, seed=9)
+    kw = dict(C=1.0, gamma=0.05, eps=1e-3, device="cuda", solver="ws", ws_size=q)
+    w = SVC(**kw).fit(X, y)
+    assert w.converged_ and _kkt_gap(X, y, w.alpha_, 1.0, 0.05) < 2.2e-3
+    capped = SVC(max_iter=500, **kw).fit(X, y)
+    assert not capped.converged_ and capped.n_iter_ == 500
+
+
+def test_ws_engine_checkpoint_resume(tmp_path):
+    X, y = synthetic("mnist", n=4000, seed=11)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws")
+    full = SVC(**kw).fit(X, y)
+    ck = str(tmp_path / "ws.ck")
+    part = SVC(max_iter=full.n_iter_ // 2, checkpoint_path=ck, checkpoint_every=10**9, **kw).fit(X, y)
+    assert not part.converged_
+    res = SVC(**kw).fit(X, y, resume=ck)
+    assert res.converged_ and abs(res.b_ - full.b_) < 1e-2
+    assert _kkt_gap(X, y, res.alpha_, 10.0, 0.25) < 2.2e-3
