@@ -81,9 +81,14 @@ def parse(argv=None):
     ap.add_argument("--shard-check", default="auto", choices=["auto", "off"],
                     help="N > 1 with a replicated timed solve: one untimed sharded solve first (cross-device "
                          "exchange evidence: its time, iterations and b go into the JSON line)")
-    ap.add_argument("--solver", default="auto", choices=["auto", "smo", "ws"],
-                    help="smo: pair-at-a-time engines (the reference's trajectory); ws: working-set rounds "
-                         "(the reference's pair rule on a q-row sub-problem in LDS, same global stop test)")
+    ap.add_argument("--solver", default="ws", choices=["auto", "smo", "ws"],
+                    help="ws (default): working-set rounds — the reference's pair rule on a q-row sub-problem "
+                         "in LDS, the reference's stop test on the exact gradient; smo: the pair-at-a-time "
+                         "engines (the reference's exact trajectory); auto: the library default (smo)")
+    ap.add_argument("--reference-check", default="auto", choices=["auto", "off"],
+                    help="auto: with --solver ws, one untimed solve by the pair-at-a-time engine (the reference's "
+                         "trajectory) after the timed runs; its time, iterations, b, support vectors and the "
+                         "decision agreement with the timed model go into the JSON line")
     ap.add_argument("--ws-size", type=int, default=192)
     ap.add_argument("--ws-new", type=int, default=0)
     ap.add_argument("--ws-rel", type=float, default=0.1)
@@ -226,6 +231,27 @@ def main(argv=None) -> int:
     if not a.no_accuracy and on_gpu:
         acc = float(solver.train_accuracy(alpha, res["b"]))
     nsv = int((alpha > 0).sum())
+    ref_check = None
+    if on_gpu and a.solver == "ws" and a.reference_check == "auto" and info.get("iteration") == "ws-dense":
+        # the same problem by the pair-at-a-time engine (the reference's exact
+        # trajectory, svmTrainMain.cpp:235-310), untimed: the two models must agree
+        rp = cfg.to_native(X.shape[1])
+        rp.solver = 1
+        r_solver = C.GpuSolver(rp, comm, ctx.local_rank)
+        r_info = r_solver.setup(X, X.shape[0], y)
+        sync()
+        t_r = time.perf_counter()
+        r_alpha, r_res = r_solver.solve()
+        sync()
+        t_r = time.perf_counter() - t_r
+        rows = np.arange(0, X.shape[0], max(1, X.shape[0] // 4096))
+        d_ws = np.asarray(solver.decision(alpha, res["b"], X[rows]))
+        d_ref = np.asarray(r_solver.decision(r_alpha, r_res["b"], X[rows]))
+        ref_check = {"engine": r_info.get("iteration"), "s": round(t_r, 6), "iterations": int(r_res["iters"]),
+                     "converged": bool(r_res["converged"]), "b": r_res["b"], "abs_b_diff": abs(r_res["b"] - res["b"]),
+                     "n_sv": int((r_alpha > 0).sum()), "decision_sign_agreement": float(np.mean(
+                         np.sign(d_ws) == np.sign(d_ref))), "rows_compared": int(len(rows))}
+        del r_solver
 
     if ctx.rank == 0:
         # the reference publishes numbers for the MNIST config only (README.md:23)
@@ -280,6 +306,7 @@ def main(argv=None) -> int:
             "census": info.get("census", "n/a"),
             "engine_note": info.get("engine_note", ""),
             "shard_check": shard_check,
+            "reference_check": ref_check,
             "params": json.loads(params.to_json()),
             "preset": a.config,
         }

@@ -60,6 +60,11 @@ def main() -> int:
         "solve_end_to_next_select_us": us(nxt - s[:, 4]),
         "round_period_us": us(np.diff(s[:, 6])),
     }
+    if (s[:, 18] > 0).any():  # experimental per-phase core-clock cycle sums (s_memtime)
+        st = np.maximum(1, s[:, 5])
+        res["cycles_per_step"] = {k: float(np.median(s[:, 12 + i] / st)) for i, k in enumerate(
+            ["reduce", "argpos", "lds", "pair", "fupdate", "set_alpha"])}
+        res["cycles_per_step"]["loop_total"] = float(np.median(s[:, 18] / st))
     line = json.dumps(res)
     print(line)
     if a.out:

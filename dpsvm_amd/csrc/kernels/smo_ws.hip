@@ -595,24 +595,25 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
 // ---------------------------------------------------------------------------
 // ws_solve: the sub-problem on wave 0
 // ---------------------------------------------------------------------------
-// alpha of working-set position `pos` (uniform) becomes `an` (uniform):
-// reclassify that row in its owner lane (f is fu when the row is in I_up,
-// else -fl).  The slot is an SGPR: one scalar branch, selects on the lane.
-__device__ __forceinline__ void ws_set_slot(bool me, float an, float C, float& fu, float& fl, float yv) {
+// Row `pos` (uniform) took alpha `an` and now has gradient fp (both uniform,
+// computed from values every lane holds): its I_up / I_low test
+// (svmTrain.cu:56-91) as mask logic on uniform operands, then the owner lane's
+// slot registers take the new fu / fl by selects.  No branch (every branch of a
+// one-wave loop is a fetch bubble) and no per-lane recomputation.
+__device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, int lane, float C, float (&fu)[3],
+                                         float (&fl)[3]) {
   const float INF = __builtin_inff();
-  const float fv = fu != INF ? fu : -fl;
-  const float nu = in_up(an, yv, C) ? fv : INF;
-  const float nl = in_low(an, yv, C) ? -fv : INF;
-  fu = me ? nu : fu;
-  fl = me ? nl : fl;
-}
-__device__ __forceinline__ void ws_set_alpha(int pos, float an, int lane, float C, float (&fu)[3], float (&fl)[3],
-                                             const float (&yr)[3]) {
-  const int s = pos >> 6;
+  const bool fr = (an > 0.f) & (an < C), z = an == 0.f, cc = an == C, py = yv > 0.f;
+  const float nu = (fr | (z & py) | (cc & !py)) ? fp : INF;
+  const float nl = (fr | (z & !py) | (cc & py)) ? -fp : INF;
   const bool me = lane == (pos & 63);
-  if (s == 0) ws_set_slot(me, an, C, fu[0], fl[0], yr[0]);
-  else if (s == 1) ws_set_slot(me, an, C, fu[1], fl[1], yr[1]);
-  else ws_set_slot(me, an, C, fu[2], fl[2], yr[2]);
+  const int s = pos >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const bool w = me & (s == k);
+    fu[k] = w ? nu : fu[k];
+    fl[k] = w ? nl : fl[k];
+  }
 }
 
 // The reference's pair update (svmTrainMain.cpp:282-295; pair_update in
@@ -621,8 +622,9 @@ __device__ __forceinline__ void ws_set_alpha(int pos, float an, int lane, float 
 // step needs no bit parity with the pair-at-a-time engines (f is updated from
 // the alphas actually taken, so it stays consistent), and the IEEE division
 // sequence is the longest dependent chain of a step.
+template <bool kBox>
 __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float y_hi, float y_lo, float bh, float bl,
-                                                   float khl, float C, float tau, int clip, bool same) {
+                                                   float khl, float C, float tau, bool same) {
 #pragma clang fp contract(off)
   float eta = (1.0f + 1.0f) - 2.0f * khl;
   eta = eta >= tau ? eta : tau;
@@ -631,7 +633,7 @@ __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float
   const float s = y_lo * y_hi;
   float a_lo_new = a_lo + (y_lo * (bh - bl)) * r;
   float a_hi_new;
-  if (clip == (int)ClipMode::Box && !same) {
+  if (kBox && !same) {
     float L, H, hL, hH;
     if (y_hi != y_lo) {
       const float dl = a_lo - a_hi;
@@ -665,14 +667,16 @@ __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float
 }
 
 // lowest working-set position whose value equals the (uniform) minimum v
+// (-1: none, i.e. NaN); scalar selects, no branch
 __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
   const uint64_t m0 = __ballot(x[0] == v), m1 = __ballot(x[1] == v), m2 = __ballot(x[2] == v);
-  if (m0) return __builtin_ctzll(m0);
-  if (m1) return 64 + __builtin_ctzll(m1);
-  if (m2) return 128 + __builtin_ctzll(m2);
-  return -1;
+  int r = m2 ? 127 + __builtin_ffsll((long long)m2) : -1;
+  r = m1 ? 63 + __builtin_ffsll((long long)m1) : r;
+  r = m0 ? __builtin_ffsll((long long)m0) - 1 : r;
+  return r;
 }
 
+template <bool kBox>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float K[];  // q x q sub-Gram
   __shared__ float s_a[kWsMax], s_y[kWsMax], s_f[kWsMax];
@@ -725,18 +729,18 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     float mu = fminf(fminf(fu[0], fu[1]), fu[2]);
     float ml = fminf(fminf(fl[0], fl[1]), fl[2]);
     wave_min2_f32(mu, ml);
-    if (!(mu < INF) || !(ml < INF)) break;
     const float bh = mu, bl = -ml;
-    if (!(bl > bh + 2.0f * eps_in)) break;
     const int ph = ws_argpos(fu, mu), pl = ws_argpos(fl, ml);
-    if (ph < 0 || pl < 0) {  // NaN
-      bad = true;
+    // one exit test: an empty side, the sub-problem's stop test, or NaN
+    const bool open = (mu < INF) & (ml < INF) & (bl > bh + 2.0f * eps_in);
+    if (!open || (ph | pl) < 0) {
+      bad = open;  // a violating pair exists but no position matches it: NaN
       break;
     }
     // every LDS read of the step in one batch: the pair's alphas / labels,
-    // K(hi, lo) and the two sub-Gram rows
+    // the 2 x 2 block K(hi|lo, hi|lo) and the two sub-Gram rows
     const float a_hi = s_a[ph], y_hi = s_y[ph], a_lo = s_a[pl], y_lo = s_y[pl];
-    const float khl = K[ph * q + pl];
+    const float khl = K[ph * q + pl], klh = K[pl * q + ph], khh = K[ph * q + ph], kll = K[pl * q + pl];
     float kh[3], kl[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
@@ -744,7 +748,8 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       kh[s] = K[ph * q + p];
       kl[s] = K[pl * q + p];
     }
-    const PairUpdate up = ws_pair_step(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, a.clip, ph == pl);
+    const PairUpdate up = ws_pair_step<kBox>(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, ph == pl);
+    float f_lo_new, f_hi_new;
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       float dl;
@@ -755,8 +760,15 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
         fl[s] = fl[s] - dl;  // -(f + delta): exact negation of the same rounding
       }
     }
-    ws_set_alpha(pl, up.a_lo_new, lane, C, fu, fl, yr);
-    ws_set_alpha(ph, up.a_hi_new, lane, C, fu, fl, yr);  // hi written last (svmTrainMain.cpp:298-299)
+    {
+      // the pair's own new gradients, uniformly: the owners computed exactly
+      // these sums (row ph: kh = K(hi,hi), kl = K(lo,hi); row pl: K(hi,lo), K(lo,lo))
+#pragma clang fp contract(off)
+      f_lo_new = bl + (up.c_hi * khl + up.c_lo * kll);
+      f_hi_new = bh + (up.c_hi * khh + up.c_lo * klh);
+    }
+    ws_place(pl, up.a_lo_new, y_lo, f_lo_new, lane, C, fu, fl);
+    ws_place(ph, up.a_hi_new, y_hi, f_hi_new, lane, C, fu, fl);  // hi written last (svmTrainMain.cpp:298-299)
     if (lane == 0) {
       s_a[pl] = up.a_lo_new;
       s_a[ph] = up.a_hi_new;
@@ -831,13 +843,14 @@ void ws_gather(const WsArgs& a, hipStream_t s) {
 
 void ws_solve(const WsArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.q_max * a.q_max * sizeof(float);
-  static size_t attr = 64 * 1024;  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
-  if (lds > attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)dev::ws_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-    attr = lds;
+  auto fn = a.clip == (int)ClipMode::Box ? dev::ws_solve_kernel<true> : dev::ws_solve_kernel<false>;
+  static size_t attr[2] = {64 * 1024, 64 * 1024};  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  size_t& at = attr[a.clip == (int)ClipMode::Box ? 1 : 0];
+  if (lds > at) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    at = lds;
   }
-  dev::ws_solve_kernel<<<1, kWsSolveThreads, lds, s>>>(a);
+  fn<<<1, kWsSolveThreads, lds, s>>>(a);
   post_launch("ws_solve", s);
 }
 
