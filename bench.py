@@ -91,7 +91,7 @@ def parse(argv=None):
                          "decision agreement with the timed model go into the JSON line")
     ap.add_argument("--ws-size", type=int, default=192)
     ap.add_argument("--ws-new", type=int, default=0)
-    ap.add_argument("--ws-rel", type=float, default=0.1)
+    ap.add_argument("--ws-rel", type=float, default=0.3)
     ap.add_argument("--ws-block", type=int, default=32)
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
     ap.add_argument("--cache-groups", type=int, default=256)

@@ -116,8 +116,8 @@ struct SolverParams {
   // a q-row sub-problem in LDS, the same global stop test)
   int solver = 0;
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
-  int ws_new = 0;             // rows replaced per round (0: ws_size / 2)
-  float ws_rel = 0.1f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2)
+  int ws_new = 0;             // rows replaced per round (0: 3 ws_size / 4)
+  float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_block = 32;          // rounds per hipGraph block
 };

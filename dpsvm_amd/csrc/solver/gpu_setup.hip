@@ -473,8 +473,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.q_max = ws_q;
     // >= 2 new rows: the global maximal violating pair (up rank 0, low rank 0)
     // is always in the set, so every round makes progress
-    w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, ws_q) : ws_q / 2);
+    // defaults measured on the MNIST-shape headline (profiles/r2_ws_param_sweep.txt)
+    w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, ws_q) : 3 * ws_q / 4);
     w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * ws_q;
+    DPSVM_CHECK(m.p.ws_rel >= 0.f && m.p.ws_rel < 1.f, "ws_rel must be in [0, 1)");
     w.rel_local = m.p.ws_rel;
     w.C = m.p.C;
     w.eps = m.p.eps;

@@ -107,8 +107,8 @@ class SVCConfig:
     # in LDS, the same global stop test; smo_ws.hip)
     solver: str = "auto"
     ws_size: int = 192              # working-set rows (<= 192)
-    ws_new: int = 0                 # rows replaced per round (0: ws_size / 2)
-    ws_rel: float = 0.1             # sub-problem tolerance relative to the global gap
+    ws_new: int = 0                 # rows replaced per round (0: 3 ws_size / 4)
+    ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_block: int = 32              # rounds per hipGraph block
 
