@@ -46,10 +46,12 @@ enum class EngineKind : int32_t {
   FusedCache = 3,    // kernel-row cache, one launch per iteration (+ host spill tier)
   Chain = 4,         // rows / step / finalize kernels + collective (partitioned X fallback)
   WsDense = 5,       // Gram resident, working-set rounds (sub-problem in LDS, smo_ws.hip)
+  WsCache = 6,       // kernel-row cache, working-set rounds (the set's missing rows by one MFMA GEMM)
 };
 inline const char* engine_name(EngineKind k) {
   switch (k) {
     case EngineKind::WsDense: return "ws-dense";
+    case EngineKind::WsCache: return "ws-cache";
     case EngineKind::PersistDense: return "persistent-dense";
     case EngineKind::FusedDense: return "fused-dense";
     case EngineKind::PersistCache: return "persistent-cache";
@@ -218,14 +220,20 @@ struct alignas(16) WsCtrl {
   int32_t q[2];      // working-set size per round parity (q[1] = 0 before round 0)
   float b_hi, b_lo;  // global selection of the current round
   int32_t nonfinite; // set by ws_select when an f value is not finite
-  int32_t pad;
+  int32_t n_miss;    // cache mode: rows of the current set without a line (computed this round)
+  int32_t hand;      // cache mode: next line the victim window starts at
+  int32_t pad[3];
   int32_t idx[2][kWsMax];     // working set per round parity (global rows), newest first
+  int32_t line[2][kWsMax];    // the line holding each member's kernel row (dense mode: the row itself)
   int32_t apply_idx[kWsMax];  // rows whose alpha changed in the last round
+  int32_t apply_line[kWsMax]; // their lines
   float apply_coef[kWsMax];   // their (alpha_new - alpha_old) * y
+  int32_t miss_row[kWsMax], miss_line[kWsMax];  // cache mode: rows to compute this round, their lines
+  int64_t rows_computed, row_hits;              // cache mode statistics
 };
 
 struct WsArgs {
-  const float* gram;   // resident Gram shard: K(i, off + j) at gram[i * ldg + j]
+  const float* gram;   // kernel-row lines: K(i, off + j) at gram[line(i) * ldg + j]
   int64_t ldg;
   const float* y;      // [n] global labels
   float* alpha;        // [n] global
@@ -237,6 +245,10 @@ struct WsArgs {
   float C, eps, tau;
   int32_t clip;
   int64_t max_iter;
+  int32_t cache;       // 0: gram = the resident Gram (line i = row i); 1: kernel-row cache
+  int32_t L;           // cache mode: lines
+  int32_t* slot_of;    // cache mode: [n] line of a global row or -1
+  int32_t* key_of;     // cache mode: [L] row held by a line or -1
   uint64_t* cand;      // [G][2][kWsCand] per-workgroup candidate keys (up, low), ascending
   float* subg;         // [q][q] sub-Gram of the current working set (ws_gather -> ws_solve)
   float* aux;          // [3][kWsMax] alpha, y, f of the working set

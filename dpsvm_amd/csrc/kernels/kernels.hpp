@@ -73,6 +73,10 @@ void ws_geometry(int64_t nl, int32_t* G, int32_t* rpt);
 void ws_select(const WsArgs& a, hipStream_t s);
 void ws_gather(const WsArgs& a, hipStream_t s);
 void ws_solve(const WsArgs& a, hipStream_t s);
+// cache mode: the merge + line assignment (one workgroup) runs before the
+// row GEMM; ws_gather then reads the sub-Gram from the members' lines
+void ws_merge(const WsArgs& a, hipStream_t s);
+bool ws_cache_supported(int64_t L, int q_max);
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)
@@ -81,6 +85,11 @@ void ws_solve(const WsArgs& a, hipStream_t s);
 void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                     const float* Bsq, int64_t N, int ldb, int dp, float gamma, float* out,
                     int64_t ldo, hipStream_t s, bool symmetric = false);
+// Kernel rows by index: lines[out_rows[i]][j] = K(X[a_rows[i]], B_j) for i < *m_dev
+// (<= M_max, read on the device), j < N — one MFMA GEMM for a set of cache misses
+void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, const int32_t* m_dev, int64_t M_max,
+                      const float* B, const float* Bsq, int64_t N, int dp, float gamma, float* lines,
+                      const int32_t* out_rows, int64_t ldl, hipStream_t s);
 // Decision values: dec[i] = sum_j coef[j] K(A_i, B_j) - b   (B = SVs, coef = alpha*y)
 //   partial: scratch [splits][M_pad] (returned by predict_scratch_floats)
 int64_t predict_scratch_floats(int64_t M, int64_t N);

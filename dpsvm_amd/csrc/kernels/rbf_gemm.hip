@@ -5,6 +5,10 @@
 //             -> the whole resident Gram shard in one launch (dense cache mode)
 //   PREDICT : partial[s][i] = sum_{j in split s} coef_j * exp(...)
 //             -> decision values / training accuracy in one launch.
+//   ROWS    : STORE with row indirection — A row i is X row a_rows[i], output
+//             row i goes to line out_rows[i], M read on the device (*m_dev):
+//             the kernel rows of a working set's cache misses in one launch
+//             (the working-set cache engine, smo_ws.hip).
 //             Replaces the reference's n x (cublasSgemv + thrust::transform_reduce)
 //             launches (svmTrain.cu:633-665, K12/K13).
 //
@@ -27,14 +31,15 @@ namespace dev {
 constexpr int BM = 128, BN = 128, BK = 16, LDP = BM + 4;
 constexpr int GEMM_THREADS = 256;
 
-enum Epi { EPI_STORE = 0, EPI_PREDICT = 1 };
+enum Epi { EPI_STORE = 0, EPI_PREDICT = 1, EPI_ROWS = 2 };
 
 template <int EPI>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     const float* __restrict__ A, const float* __restrict__ Asq, int64_t M, int lda,
     const float* __restrict__ B, const float* __restrict__ Bsq, int64_t N, int ldb, int dp,
     float gamma, float* __restrict__ out, int64_t ldo, const float* __restrict__ coef,
-    int n_tiles_per_split, int sym) {
+    int n_tiles_per_split, int sym, const int32_t* __restrict__ a_rows = nullptr,
+    const int32_t* __restrict__ out_rows = nullptr, const int32_t* __restrict__ m_dev = nullptr) {
   // sym (STORE, B == A, N == M): only tiles on/above the diagonal are computed;
   // each off-diagonal tile also writes its transpose.  K(i,j) and K(j,i) are
   // bit-identical (same products in the same k order, commutative norm sum).
@@ -47,7 +52,8 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   // symmetric mode's skipped lower triangle).  A bijection on the grid; the
   // tile math is unchanged: bit-identical output.
   int64_t tx = blockIdx.x, ty = blockIdx.y;
-  if (EPI == EPI_STORE) {
+  if (EPI == EPI_ROWS) M = *m_dev;
+  if (EPI == EPI_STORE || EPI == EPI_ROWS) {
     const int64_t tm = gridDim.x, tn = gridDim.y, total = tm * tn;
     const int64_t L = blockIdx.x + (int64_t)blockIdx.y * tm;
     constexpr int64_t CH = 64;
@@ -65,6 +71,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     ty = in / gm;
   }
   if (EPI == EPI_STORE && sym && ty < tx) return;
+  if (EPI == EPI_ROWS && tx * BM >= M) return;  // uniform: no barrier reached
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
   __shared__ float red[2][BM];
@@ -74,7 +81,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   const int64_t m0 = tx * BM;
   const int64_t ntiles_total = (N + BN - 1) / BN;
   int64_t nt_begin, nt_end;
-  if (EPI == EPI_STORE) {
+  if (EPI != EPI_PREDICT) {
     nt_begin = ty;
     nt_end = nt_begin + 1;
   } else {
@@ -104,6 +111,10 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
 
     const float* ga0 = A + (m0 + r_ld0) * (int64_t)lda + 4 * k4_ld;
     const float* ga1 = ga0 + 64 * (int64_t)lda;
+    if (EPI == EPI_ROWS) {  // rows past M repeat the last one (never stored)
+      ga0 = A + (int64_t)a_rows[min(m0 + r_ld0, M - 1)] * lda + 4 * k4_ld;
+      ga1 = A + (int64_t)a_rows[min(m0 + r_ld0 + 64, M - 1)] * lda + 4 * k4_ld;
+    }
     const float* gb0 = B + (n0 + r_ld0) * (int64_t)ldb + 4 * k4_ld;
     const float* gb1 = gb0 + 64 * (int64_t)ldb;
     f4 ra0 = *(const f4*)ga0, ra1 = *(const f4*)ga1;
@@ -160,6 +171,13 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
         for (int r = 0; r < 16; ++r) {
           const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int64_t row = m0 + wm * 64 + i * 32 + rl;
+          if (EPI == EPI_ROWS) {
+            if (row < M && col < N) {
+              const float kv = rbf_from_dot(Asq[a_rows[row]], bsq, acc[i][j][r], gamma);
+              out[(int64_t)out_rows[row] * ldo + col] = kv;
+            }
+            continue;
+          }
           const float kv = rbf_from_dot(Asq[row], bsq, acc[i][j][r], gamma);
           if (EPI == EPI_STORE) {
             if (row < M && col < N) out[row * ldo + col] = kv;
@@ -268,6 +286,18 @@ void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const 
   dev::rbf_gemm_kernel<dev::EPI_STORE><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
       A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, out, ldo, nullptr, 1, symmetric ? 1 : 0);
   post_launch("rbf_gemm_store", s);
+}
+
+void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, const int32_t* m_dev, int64_t M_max,
+                      const float* B, const float* Bsq, int64_t N, int dp, float gamma, float* lines,
+                      const int32_t* out_rows, int64_t ldl, hipStream_t s) {
+  if (M_max <= 0 || N <= 0) return;
+  DPSVM_CHECK(dp % 16 == 0, "rbf_rows_indexed: dp must be a multiple of 16");
+  const int64_t tm = (M_max + dev::BM - 1) / dev::BM, tn = (N + dev::BN - 1) / dev::BN;
+  DPSVM_CHECK(tn < 65536, "rbf_rows_indexed: N too large for grid.y");
+  dev::rbf_gemm_kernel<dev::EPI_ROWS><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
+      X, Xsq, M_max, dp, B, Bsq, N, dp, dp, gamma, lines, ldl, nullptr, 1, 0, a_rows, out_rows, m_dev);
+  post_launch("rbf_rows_indexed", s);
 }
 
 static int predict_splits(int64_t M, int64_t N) {

@@ -213,6 +213,9 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
   s->b_hi = c->b_hi;
   s->b_lo = c->b_lo;
   s->outer = c->outer;
+  s->rows_computed = c->rows_computed;  // cache mode: kernel rows computed, member rows found cached
+  s->misses = c->rows_computed;
+  s->hits = c->row_hits;
   __atomic_store_n(&s->seq, (int32_t)c->outer, __ATOMIC_RELEASE);
 }
 
@@ -233,7 +236,7 @@ template <int RPT>
 __global__ __launch_bounds__(kWsSelThreads * 4) void ws_select_kernel(WsArgs a) {
   constexpr int PARTS = ws_parts<RPT>();
   constexpr int CH = RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
-  __shared__ int32_t s_idx[kWsMax];
+  __shared__ int32_t s_idx[kWsMax];  // lines of the changed rows
   __shared__ float s_coef[kWsMax];
   __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][kWsSelThreads * RPT];
   __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(kWsSelThreads * 4) void ws_select_kernel(WsArgs a) 
   const int done = c->done;
   if (na == 0 && done != kRunning) return;
   for (int k = threadIdx.x; k < na; k += kWsSelThreads * PARTS) {
-    s_idx[k] = c->apply_idx[k];
+    s_idx[k] = c->apply_line[k];
     s_coef[k] = c->apply_coef[k];
   }
   __syncthreads();
@@ -367,28 +370,28 @@ __global__ __launch_bounds__(kWsSelThreads * 4) void ws_select_kernel(WsArgs a) 
 }
 
 // ---------------------------------------------------------------------------
-// ws_gather: merge (every workgroup) + one sub-Gram row per workgroup
+// the merge: stop test and the new working set (one 256-thread workgroup;
+// identical result in every workgroup that runs it).  Returns false when the
+// run stopped (done is then set by workgroup 0).  s_idx[0..*q) = the set,
+// newest first; *b_hi / *b_lo = the global selection.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
+__device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out, float* bh_out, float* bl_out) {
   __shared__ int s_hist[2][256];
   __shared__ int s_sel[2][2];
   __shared__ int s_thr[2];
   __shared__ uint64_t s_wsum64[4];
   __shared__ uint64_t s_sv[2][kWsMaxCand];
   __shared__ int32_t s_hash[4][kWsHash];  // up keys, up ranks, low keys, low ranks
-  __shared__ int32_t s_idx[kWsMax];
   __shared__ int32_t s_keep[2 * kWsMax];  // per interleaved position: final slot or -1
   __shared__ uint64_t s_scr[8];
   __shared__ int s_wsum[4];
-  WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x;
   const bool lead = blockIdx.x == 0 && tid == 0;
-  if (lead) WS_STAMP(1);
   if (c->done != kRunning) {
     // a round ended the run (max_iter / no pair): its changes were applied by
     // the ws_select that followed it; nothing may be applied twice
     if (lead) c->n_apply = 0;
-    return;
+    return false;
   }
   const int G = a.G;
   const int64_t r_now = c->outer;
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
       c->b_lo = b_lo;
       ws_status(a.status, c);
     }
-    return;
+    return false;
   }
 
   // ---- per side, a 16-bit key prefix T: the rows whose prefix is <= T hold
@@ -511,7 +514,6 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
     }
   }
   __syncthreads();
-  if (lead) WS_STAMP(2);
 
   // ---- the new working set ----
   int32_t* hk_u = s_hash[0];
@@ -569,15 +571,39 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
   if (pk && n_chosen + pslot < a.q_max) s_idx[n_chosen + pslot] = pidx;
   const int q = min(a.q_max, n_chosen + ptotal);
   __syncthreads();
+  *q_out = q;
+  *bh_out = b_hi;
+  *bl_out = b_lo;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// ws_gather (dense mode): the merge in every workgroup + one sub-Gram row per
+// workgroup (row a: q random columns of Gram row idx_a — one load per thread;
+// the whole grid issues the scattered reads a single CU could not)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  if (lead) WS_STAMP(1);
+  const int par = (int)(c->outer & 1);
+  int q = 0;
+  float b_hi = 0.f, b_lo = 0.f;
+  if (!ws_merge(a, c, s_idx, &q, &b_hi, &b_lo)) return;
+  if (lead) WS_STAMP(2);
   if (blockIdx.x == 0) {
-    for (int t = tid; t < q; t += kWsGatherThreads) c->idx[par][t] = s_idx[t];
+    for (int t = tid; t < q; t += kWsGatherThreads) {
+      c->idx[par][t] = s_idx[t];
+      c->line[par][t] = s_idx[t];  // the resident Gram: line i is row i
+    }
     if (tid == 0) {
       c->q[par] = q;
       c->b_hi = b_hi;
       c->b_lo = b_lo;
     }
   }
-  // ---- row a of the sub-Gram, the row's alpha / y / f ----
   const int ra = blockIdx.x;
   if (ra < q) {
     const int32_t gi = s_idx[ra];
@@ -590,6 +616,110 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
     }
   }
   if (lead) WS_STAMP(8);
+}
+
+// ---------------------------------------------------------------------------
+// cache mode, round part 1 — ws_merge (ONE workgroup): the merge, then lines
+// for the members: a member's row is cached (slot_of) or takes a victim line.
+// Victims come from a window of up to 512 lines after the CLOCK hand, skipping
+// lines that hold a member (pinned while the round uses them); all misses are
+// assigned at once (one prefix scan), their rows computed next by one GEMM.
+// ---------------------------------------------------------------------------
+constexpr int kWsWindow = 512;
+
+__global__ __launch_bounds__(kWsGatherThreads) void ws_merge_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  __shared__ int32_t s_line[kWsMax];
+  __shared__ int32_t s_pin[kWsWindow];
+  __shared__ int32_t s_victim[kWsMax];
+  __shared__ int s_wsum[4];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  if (tid == 0) WS_STAMP(1);
+  const int par = (int)(c->outer & 1);
+  int q = 0;
+  float b_hi = 0.f, b_lo = 0.f;
+  if (!ws_merge(a, c, s_idx, &q, &b_hi, &b_lo)) return;
+  if (tid == 0) WS_STAMP(2);
+  const int L = a.L, hand = c->hand;
+  const int W = min(L, kWsWindow);
+  for (int w = tid; w < kWsWindow; w += kWsGatherThreads) s_pin[w] = 0;
+  __syncthreads();
+  int32_t my_line = -1, my_row = -1;
+  if (tid < q) {
+    my_row = s_idx[tid];
+    my_line = a.slot_of[my_row];
+    if (my_line >= 0) {
+      const int o = (my_line - hand + L) % L;
+      if (o < W) s_pin[o] = 1;
+    }
+  }
+  __syncthreads();
+  int n_miss = 0;
+  const bool miss = tid < q && my_line < 0;
+  const int mrank = block_scan_small256((int)miss, s_wsum, &n_miss);
+  // free window slots 2t, 2t + 1 in window order
+  const bool f0 = 2 * tid < W && !s_pin[2 * tid], f1 = 2 * tid + 1 < W && !s_pin[2 * tid + 1];
+  int n_free = 0;
+  const int frank = block_scan_small256((int)f0 + (int)f1, s_wsum, &n_free);
+  int last_used = -1;
+  if (f0 && frank < n_miss) {
+    s_victim[frank] = (hand + 2 * tid) % L;
+    last_used = 2 * tid;
+  }
+  if (f1 && frank + (int)f0 < n_miss) {
+    s_victim[frank + (int)f0] = (hand + 2 * tid + 1) % L;
+    last_used = 2 * tid + 1;
+  }
+  __syncthreads();
+  if (miss) {  // n_free >= W - q >= n_miss whenever L >= q + 256 (setup guarantees L >= 2 q_max + 512)
+    const int32_t ln = s_victim[mrank];
+    const int32_t old = a.key_of[ln];
+    if (old >= 0) a.slot_of[old] = -1;  // evicted (never a member: members' lines are pinned)
+    a.key_of[ln] = my_row;
+    a.slot_of[my_row] = ln;
+    my_line = ln;
+    c->miss_row[mrank] = my_row;
+    c->miss_line[mrank] = ln;
+  }
+  if (tid < q) {
+    c->idx[par][tid] = my_row;
+    c->line[par][tid] = my_line;
+  }
+  if (n_miss > 0 && last_used >= 0 && (frank + (int)f0 + (int)f1 >= n_miss) && (frank < n_miss))
+    c->hand = (hand + last_used + 1) % L;  // the thread holding the last victim
+  if (tid == 0) {
+    c->q[par] = q;
+    c->b_hi = b_hi;
+    c->b_lo = b_lo;
+    c->n_miss = n_miss;
+    c->rows_computed += n_miss;
+    c->row_hits += q - n_miss;
+  }
+}
+
+// cache mode, round part 3 — ws_gather_lines (q_max workgroups): row a of the
+// sub-Gram from member a's line, its alpha / y / f
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  if (c->done != kRunning) return;
+  const int par = (int)(c->outer & 1);
+  const int q = c->q[par];
+  const int ra = blockIdx.x;
+  if (ra >= q) return;
+  for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][t];
+  __syncthreads();
+  const int32_t gi = s_idx[ra];
+  const float* grow = a.gram + (int64_t)c->line[par][ra] * a.ldg - a.off;
+  for (int b = tid; b < q; b += kWsGatherThreads) a.subg[ra * q + b] = grow[s_idx[b]];
+  if (tid == 0) {
+    a.aux[ra] = a.alpha[gi];
+    a.aux[kWsMax + ra] = a.y[gi];
+    a.aux[2 * kWsMax + ra] = a.f[gi - a.off];
+    if (ra == 0) WS_STAMP(8);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -680,7 +810,7 @@ template <bool kBox>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float K[];  // q x q sub-Gram
   __shared__ float s_a[kWsMax], s_y[kWsMax], s_f[kWsMax];
-  __shared__ int32_t s_idx[kWsMax];
+  __shared__ int32_t s_idx[kWsMax], s_line[kWsMax];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) WS_STAMP(0);
@@ -701,6 +831,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       s_y[tid] = a.aux[kWsMax + tid];
       s_f[tid] = a.aux[2 * kWsMax + tid];
       s_idx[tid] = c->idx[par][tid];
+      s_line[tid] = c->line[par][tid];
     }
   }
   __syncthreads();
@@ -793,6 +924,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
         dc = (an - a0[s]) * yr[s];
       }
       c->apply_idx[at] = gi;
+      c->apply_line[at] = s_line[p];
       c->apply_coef[at] = dc;
     }
     n_apply += __popcll(mk);
@@ -837,9 +969,21 @@ void ws_select(const WsArgs& a, hipStream_t s) {
 }
 
 void ws_gather(const WsArgs& a, hipStream_t s) {
-  dev::ws_gather_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
-  post_launch("ws_gather", s);
+  if (a.cache) {
+    dev::ws_gather_lines_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+    post_launch("ws_gather_lines", s);
+  } else {
+    dev::ws_gather_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+    post_launch("ws_gather", s);
+  }
 }
+
+void ws_merge(const WsArgs& a, hipStream_t s) {
+  dev::ws_merge_kernel<<<1, dev::kWsGatherThreads, 0, s>>>(a);
+  post_launch("ws_merge", s);
+}
+
+bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max + dev::kWsWindow; }
 
 void ws_solve(const WsArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.q_max * a.q_max * sizeof(float);

@@ -16,6 +16,8 @@
 //   ws-dense          Gram resident; working-set rounds: one workgroup solves a
 //                     q-row sub-problem from an LDS sub-Gram, one grid pass
 //                     updates f and selects the next candidates (smo_ws.hip)
+//   ws-cache          kernel-row cache; working-set rounds whose missing rows
+//                     come from one MFMA GEMM per round
 //
 // Reference per-iteration path: svmTrainMain.cpp:235-310 (host loop, >= 7
 // blocking host<->device round trips, one MPI Allgather).
@@ -297,6 +299,60 @@ struct WsDense final : DenseBase {
   Pending pending(GpuSolver::Impl&) override { return {}; }  // alphas committed every round
 };
 
+// Working-set rounds on a kernel-row cache (Gram too large for HBM).  A round
+// is [ws_merge (set + line assignment), one MFMA GEMM for the set's missing
+// rows (rbf_rows_indexed), ws_gather (sub-Gram from the lines), ws_solve,
+// ws_select (f update from the changed rows' lines + candidates)] — the X
+// pass of a round computes up to ~3/4 of q rows at once instead of 2 (+16
+// speculative) per SMO iteration.
+struct WsCache final : Engine {
+  EngineKind kind() const override { return EngineKind::WsCache; }
+  int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
+  static void round(GpuSolver::Impl& m) {
+    const WsArgs& w = m.wsa;
+    launch::ws_merge(w, m.stream);
+    launch::rbf_rows_indexed(m.x, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), w.q_max,
+                             m.x + (size_t)(m.off - m.args.x_row0) * m.dp, m.xsq + m.off, m.nl, m.dp, m.gamma,
+                             m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
+    launch::ws_gather(w, m.stream);
+    launch::ws_solve(w, m.stream);
+    launch::ws_select(w, m.stream);
+  }
+  void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult&) override {
+    WsCtrl c;
+    memset(&c, 0, sizeof(c));
+    c.iter = iter0;
+    c.done = kRunning;
+    c.b_hi = b_hi;
+    c.b_lo = b_lo;
+    HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
+    launch::ws_select(m.wsa, m.stream);
+    const bool graphs = m.p.use_graph && !m.p.sync_debug && !sync_debug_env();
+    if (graphs && !m.gexec) {
+      const int B = block(m.p);
+      HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
+      try {
+        for (int i = 0; i < B; ++i) round(m);
+      } catch (...) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(m.stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        throw;
+      }
+      HIP_CHECK(hipStreamEndCapture(m.stream, &m.graph));
+      HIP_CHECK(hipGraphInstantiate(&m.gexec, m.graph, nullptr, nullptr, 0));
+    }
+  }
+  void run_block(GpuSolver::Impl& m, int B) override {
+    if (m.gexec) {
+      HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
+    } else {
+      for (int i = 0; i < B; ++i) round(m);
+    }
+  }
+};
+
 struct Chain final : Engine {
   EngineKind kind() const override { return EngineKind::Chain; }
   int block(const SolverParams& p) const override { return std::max(1, p.graph_block); }
@@ -313,6 +369,7 @@ std::unique_ptr<Engine> make_engine(EngineKind k) {
     case EngineKind::PersistCache: return std::make_unique<PersistCache>();
     case EngineKind::FusedCache: return std::make_unique<FusedCache>();
     case EngineKind::WsDense: return std::make_unique<WsDense>();
+    case EngineKind::WsCache: return std::make_unique<WsCache>();
     default: return std::make_unique<Chain>();
   }
 }

@@ -120,7 +120,11 @@ struct GpuSolver::Impl {
   bool device_comm() const { return world == 1 || comm->device_memory(); }
   bool fused() const { return kind != EngineKind::Chain; }
   bool persistent() const { return kind == EngineKind::PersistDense || kind == EngineKind::PersistCache; }
-  bool working_set() const { return kind == EngineKind::WsDense; }
+  bool working_set() const { return kind == EngineKind::WsDense || kind == EngineKind::WsCache; }
+  // device addresses inside the working-set control record (cache mode GEMM operands)
+  int32_t* wsctrl_miss_row() const { return wsctrl ? wsctrl->miss_row : nullptr; }
+  int32_t* wsctrl_miss_line() const { return wsctrl ? wsctrl->miss_line : nullptr; }
+  int32_t* wsctrl_n_miss() const { return wsctrl ? &wsctrl->n_miss : nullptr; }
 
   SmoStatus read_status() const;
   void init_ctrl(int64_t iter0, float b_hi, float b_lo);

@@ -295,7 +295,17 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // below) and a co-resident grid (census); the one-launch-per-iteration
   // engines are the fallbacks.
   const bool fused_lru_ok = !m.dense && m.replicated && launch::smo_fused_lru_supported(m.dp) && m.p.cache_engine == 0;
-  const bool plru_cand = fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
+  // working-set engines (solver=ws), one rank (the replicate dp policy gives
+  // every rank a one-rank problem): the resident Gram (ws-dense), or a
+  // kernel-row cache whose missing rows come from one GEMM per round (ws-cache)
+  const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
+  const bool ws_ok = m.p.solver == 2 && m.world == 1 && m.replicated && !m.p.force_collectives &&
+                     launch::ws_supported(m.nl, ws_q);
+  const bool ws_cand = ws_ok && m.dense;
+  const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 && launch::smo_fused_lru_supported(m.dp);
+  if (m.p.solver == 2 && !ws_ok)
+    m.info.engine_note = "ws engines need one rank with replicated X (world 1 or dp replicate): SMO engine used";
+  const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
                          launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
   if (plru_cand) {
@@ -303,13 +313,6 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     const double meta_bytes = (double)m.Gf * launch::plru_stride_words(n, n) * 4.0;
     want_lines = std::min<int64_t>(want_lines, (int64_t)((budget - meta_bytes) / line_bytes));
   }
-  // working-set engine (solver=ws): the resident Gram on one rank (the
-  // replicate dp policy gives every rank a one-rank problem)
-  const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
-  const bool ws_cand = m.p.solver == 2 && m.dense && m.world == 1 && m.replicated && !m.p.force_collectives &&
-                       launch::ws_supported(m.nl, ws_q);
-  if (m.p.solver == 2 && !ws_cand)
-    m.info.engine_note = "ws engine needs the resident Gram on one rank (dense mode, world 1): SMO engine used";
   const bool pdense_cand = !ws_cand && m.dense &&
                            (m.p.persist == 2 || (m.p.persist == 0 && m.p.exchange != 1 && m.p.use_graph &&
                                                  !m.p.force_collectives)) &&
@@ -432,7 +435,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       m.info.engine_note = "peer exchange refused: " + m.xch_diag;
     }
   }
+  const bool wsc_fits = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
+  if (wsc_cand && !wsc_fits)
+    m.info.engine_note = "ws-cache needs >= " + std::to_string(2 * ws_q + 512) + " lines: SMO cache engine used";
   if (ws_cand) m.kind = EngineKind::WsDense;
+  else if (wsc_fits) m.kind = EngineKind::WsCache;
   else if (m.dense) m.kind = pdense_cand && m.xch ? EngineKind::PersistDense : EngineKind::FusedDense;
   else if (fused_lru_ok) m.kind = plru_cand && m.xch ? EngineKind::PersistCache : EngineKind::FusedCache;
   else m.kind = EngineKind::Chain;
@@ -458,11 +465,15 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     a.plru_meta = nullptr;
     a.plru_stride = 0;
   }
-  if (m.kind == EngineKind::WsDense) {
+  if (m.working_set()) {
     WsArgs& w = m.wsa;
     w = WsArgs{};
     w.gram = m.lines;
     w.ldg = m.ldl;
+    w.cache = m.kind == EngineKind::WsCache ? 1 : 0;
+    w.L = (int32_t)m.L;
+    w.slot_of = m.slot_of;
+    w.key_of = m.key_of;
     w.y = m.y;
     w.alpha = m.alpha;
     w.f = m.f;

@@ -106,3 +106,29 @@ def test_ws_engine_checkpoint_resume(tmp_path):
     res = SVC(**kw).fit(X, y, resume=ck)
     assert res.converged_ and abs(res.b_ - full.b_) < 1e-2
     assert _kkt_gap(X, y, res.alpha_, 10.0, 0.25) < 2.2e-3
+
+
+@pytest.mark.parametrize("case", [("mnist", 4000, 10.0, 0.25, 1500), ("adult", 5000, 1.0, 0.05, 900),
+                                  ("covtype", 6000, 4.0, 0.5, 2000)])
+def test_ws_cache_engine_bit_identical_to_resident_gram(case):
+    """ws-cache (kernel-row cache, the set's missing rows by one indexed MFMA
+    GEMM per round, CLOCK-window victims) follows the ws-dense trajectory bit
+    for bit: the same K values (same GEMM arithmetic), the same merge, the same
+    f-update order.  A cache of ~900-2000 lines forces evictions."""
+    name, n, C_, g, lines = case
+    X, y = synthetic(name, n=n, seed=5)
+    kw = dict(C=C_, gamma=g, eps=1e-3, device="cuda", solver="ws")
+    dense = SVC(**kw).fit(X, y)
+    cache = SVC(force_cache=True, cache_lines=lines, **kw).fit(X, y)
+    assert dense.setup_info_["iteration"] == "ws-dense"
+    assert cache.setup_info_["iteration"] == "ws-cache" and cache.setup_info_["cache_lines"] == lines
+    assert cache.converged_ and cache.n_iter_ == dense.n_iter_ and cache.n_rounds_ == dense.n_rounds_
+    assert np.array_equal(cache.alpha_, dense.alpha_) and cache.b_ == dense.b_
+    assert cache.stats_["rows_computed"] > lines  # more rows than lines: evictions happened
+
+
+def test_ws_cache_engine_small_cache_refused_cleanly():
+    X, y = synthetic("adult", n=3000, seed=1)
+    s = SVC(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300).fit(X, y)
+    assert s.setup_info_["iteration"] in ("persistent-cache", "fused-cache")
+    assert "ws-cache needs" in s.setup_info_["engine_note"]
