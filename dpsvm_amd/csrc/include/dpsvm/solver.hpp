@@ -131,6 +131,9 @@ void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const
               float gamma, float* out, int64_t out_ld, bool symmetric, void* stream);
 // the cache engines' X pass: out[q][j] = K(x_keys[q], x_j), q < nq <= 16, j < n
 // (x: [rows >= G*rows_per_group][ld], xsq likewise; out rows >= G*rows_per_group)
+// the working-set cache engine's row GEMM: out[out_rows[i]][j] = K(x[rows[i]], x_j), i < m, j < n
+void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const int* rows, int m, float gamma,
+                      float* out, int64_t out_ld, const int* out_rows, void* stream);
 void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* keys, int nq, float gamma,
                 float* out, int64_t out_ld, int rows_per_group, void* stream);
 // the fused / persistent engines' selection: per workgroup of rows_per_group rows

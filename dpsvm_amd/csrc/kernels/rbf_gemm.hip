@@ -75,6 +75,8 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
   __shared__ float red[2][BM];
+  __shared__ float s_asq[EPI == EPI_ROWS ? BM : 1];      // ROWS: |x|^2 of the tile's rows
+  __shared__ int32_t s_orow[EPI == EPI_ROWS ? BM : 1];   // ROWS: their output lines (-1: past M)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -92,6 +94,14 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   // staging map: 512 float4 per tile, 2 per thread: row r = idx>>2, k4 = idx&3
   const int r_ld0 = tid >> 2, k4_ld = tid & 3;
   const int nk = dp / BK;  // dp is a multiple of 16
+
+  if (EPI == EPI_ROWS && threadIdx.x < BM) {
+    // the tile's row metadata once (read from LDS in the epilogue instead of
+    // two dependent global loads per output element)
+    const int64_t row = m0 + threadIdx.x;
+    s_asq[threadIdx.x] = Asq[a_rows[min(row, M - 1)]];
+    s_orow[threadIdx.x] = row < M ? out_rows[row] : -1;
+  }
 
   float rowacc[2][16];
 #pragma unroll
@@ -141,8 +151,11 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
         rb0 = *(const f4*)(gb0 + koff);
         rb1 = *(const f4*)(gb1 + koff);
       }
+      // ROWS: a wave whose 64 rows all lie past M only stages (uniform skip)
+      const bool live = EPI != EPI_ROWS || m0 + wm * 64 < M;
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
+        if (!live) break;
         const int kr = 2 * kk + (lane >> 5);
         const float a0 = As[cur][kr][wm * 64 + (lane & 31)];
         const float a1 = As[cur][kr][wm * 64 + 32 + (lane & 31)];
@@ -161,6 +174,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     // ---- epilogue ----
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (EPI == EPI_ROWS && m0 + wm * 64 + i * 32 >= M) continue;  // uniform: no exp for rows past M
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
@@ -172,10 +186,9 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
           const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           const int64_t row = m0 + wm * 64 + i * 32 + rl;
           if (EPI == EPI_ROWS) {
-            if (row < M && col < N) {
-              const float kv = rbf_from_dot(Asq[a_rows[row]], bsq, acc[i][j][r], gamma);
-              out[(int64_t)out_rows[row] * ldo + col] = kv;
-            }
+            const int lr = wm * 64 + i * 32 + rl;
+            const int32_t orow = s_orow[lr];
+            if (orow >= 0 && col < N) out[(int64_t)orow * ldo + col] = rbf_from_dot(s_asq[lr], bsq, acc[i][j][r], gamma);
             continue;
           }
           const float kv = rbf_from_dot(Asq[row], bsq, acc[i][j][r], gamma);

@@ -229,11 +229,11 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
 // most ~48 Gram loads of one batch in flight instead of a chain of batches.
 template <int RPT>
 constexpr int ws_parts() {
-  return RPT <= 2 ? 4 : (RPT <= 4 ? 2 : 1);
+  return RPT <= 4 ? 4 : 2;  // register budget: <= 4 waves per SIMD at RPT <= 4, 2 above
 }
 
 template <int RPT>
-__global__ __launch_bounds__(kWsSelThreads * 4) void ws_select_kernel(WsArgs a) {
+__global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_kernel(WsArgs a) {
   constexpr int PARTS = ws_parts<RPT>();
   constexpr int CH = RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
   __shared__ int32_t s_idx[kWsMax];  // lines of the changed rows
@@ -959,7 +959,7 @@ bool ws_supported(int64_t nl, int q_max) {
 
 void ws_select(const WsArgs& a, hipStream_t s) {
   const dim3 grid(a.G);
-  auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 2 ? 4 : rpt <= 4 ? 2 : 1)); };
+  auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 4 ? 4 : 2)); };
   if (a.rpt <= 1) dev::ws_select_kernel<1><<<grid, threads(1), 0, s>>>(a);
   else if (a.rpt <= 2) dev::ws_select_kernel<2><<<grid, threads(2), 0, s>>>(a);
   else if (a.rpt <= 4) dev::ws_select_kernel<4><<<grid, threads(4), 0, s>>>(a);

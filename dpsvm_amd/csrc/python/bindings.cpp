@@ -445,6 +445,11 @@ PYBIND11_MODULE(_C, m) {
     kernels::xpass_rows((const float*)x, (const float*)xsq, n, ld, (const int*)keys, nq, gamma, (float*)out, out_ld,
                         rows, (void*)stream);
   });
+  m.def("k_rbf_rows_indexed", [](uintptr_t x, uintptr_t xsq, int64_t n, int ld, uintptr_t rows, int m_, float gamma,
+                                 uintptr_t out, int64_t out_ld, uintptr_t out_rows, uintptr_t stream) {
+    kernels::rbf_rows_indexed((const float*)x, (const float*)xsq, n, ld, (const int*)rows, m_, gamma, (float*)out,
+                              out_ld, (const int*)out_rows, (void*)stream);
+  });
   m.def("k_fused_select", [](uintptr_t f, uintptr_t alpha, uintptr_t y, int64_t n, float C, int rows, uintptr_t out,
                              uintptr_t stream) {
     kernels::fused_select((const float*)f, (const float*)alpha, (const float*)y, n, C, rows, (uint64_t*)out,

@@ -380,6 +380,18 @@ void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const
   launch::rbf_gemm_store(a, asq, m, ld, b, bsq, n, ld, ld, gamma, out, out_ld, (hipStream_t)stream, symmetric);
 }
 
+void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const int* rows, int m, float gamma,
+                      float* out, int64_t out_ld, const int* out_rows, void* stream) {
+  DPSVM_CHECK(ld % 16 == 0 && m >= 0 && m <= 4096, "rbf_rows_indexed: ld multiple of 16, m <= 4096");
+  hipStream_t s = (hipStream_t)stream;
+  size_t tb = 0;
+  int32_t* md = dmalloc<int32_t>(1, &tb);
+  HIP_CHECK(hipMemcpyAsync(md, &m, 4, hipMemcpyHostToDevice, s));
+  launch::rbf_rows_indexed(x, xsq, rows, md, m, x, xsq, n, ld, gamma, out, out_rows, out_ld, s);
+  HIP_CHECK(hipStreamSynchronize(s));
+  (void)hipFree(md);
+}
+
 void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* keys, int nq, float gamma,
                 float* out, int64_t out_ld, int rows_per_group, void* stream) {
   DPSVM_CHECK(ld % 16 == 0 && rows_per_group > 0 && rows_per_group % kFusedThreads == 0,

@@ -150,6 +150,28 @@ def xpass_rows(x: torch.Tensor, keys, gamma: float, rows_per_group: int = 256) -
     return out[:, :n]
 
 
+def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_lines: int = 0) -> torch.Tensor:
+    """The working-set cache engine's row GEMM (rbf_gemm EPI_ROWS: A rows by
+    index, output rows to their lines, M read on the device): lines
+    [n_lines][n] with line out_lines[i] = K(x_rows[i], x_j)."""
+    C = load()
+    rows = [int(r) for r in rows]
+    m = len(rows)
+    n = x.shape[0]
+    xp, dp = _pad_rows_cols(x, row_mult=128)  # the GEMM reads whole 128-row tiles
+    xsq = torch.zeros(xp.shape[0], device=x.device)
+    C.k_row_sqnorm(xp.data_ptr(), xp.shape[0], dp, dp, xsq.data_ptr(), _stream(x))
+    out_lines = list(range(m)) if out_lines is None else [int(v) for v in out_lines]
+    n_lines = max(n_lines, max(out_lines) + 1 if out_lines else 1)
+    rd = torch.tensor(rows or [0], dtype=torch.int32, device=x.device)
+    od = torch.tensor(out_lines or [0], dtype=torch.int32, device=x.device)
+    ld = (n + 127) // 128 * 128
+    out = torch.full((n_lines, ld), float("nan"), device=x.device)
+    C.k_rbf_rows_indexed(xp.data_ptr(), xsq.data_ptr(), n, dp, rd.data_ptr(), m, float(gamma), out.data_ptr(), ld,
+                         od.data_ptr(), _stream(x))
+    return out[:, :n]
+
+
 def fused_select(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: float, rows_per_group: int = 256):
     """Per-workgroup (up, low) selection keys of the fused / persistent engines
     (classification + wave-64 DPP minimum + LDS across waves): [groups, 2] u64

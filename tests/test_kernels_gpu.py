@@ -179,3 +179,25 @@ def test_fused_select_vs_torch(K):
         assert (gh, vh) == (ih, float(f[ih])), b
         assert (gl, -vl) == (il, float(f[il])), b
     assert decode_key(int(keys[1, 0]) & (2**64 - 1))[1] == 600
+
+
+@pytest.mark.parametrize("n,d,m", [(5000, 54, 35), (3000, 784, 130), (2000, 1024, 7), (777, 16, 1)])
+def test_rbf_rows_indexed_vs_torch_and_gram(K, n, d, m):
+    """The working-set cache engine's row GEMM (rbf_gemm EPI_ROWS: A rows by
+    index, output rows scattered to lines, M read on the device) vs a float64
+    torch reference, and bit-identical to the resident-Gram GEMM's rows (the
+    ws-cache / ws-dense engines share their trajectory through it)."""
+    g = torch.Generator(device="cuda").manual_seed(n + d + m)
+    x = torch.rand(n, d, device="cuda", generator=g)
+    rows = torch.randperm(n, generator=torch.Generator().manual_seed(m))[:m].tolist()
+    lines = torch.randperm(m + 5, generator=torch.Generator().manual_seed(n))[:m].tolist()
+    gamma = 1.0 / d
+    out = K.rbf_rows_indexed(x, rows, gamma, out_lines=lines, n_lines=m + 5)
+    got = out[lines]
+    ref = _rbf_ref(x, x[rows], gamma)
+    assert torch.isfinite(got).all()
+    assert (got.double() - ref).abs().max().item() < 2e-5
+    untouched = sorted(set(range(m + 5)) - set(lines))
+    assert torch.isnan(out[untouched]).all()  # only the assigned lines are written
+    gram = K.rbf_gram(x, x.clone(), gamma)
+    assert torch.equal(got, gram[rows])
