@@ -28,6 +28,9 @@ def main() -> int:
     ap.add_argument("--ws-size", type=int, default=192)
     ap.add_argument("--ws-new", type=int, default=0)
     ap.add_argument("--ws-rel", type=float, default=0.1)
+    ap.add_argument("--max-iter", type=int, default=10**7)
+    ap.add_argument("--cache-lines", type=int, default=0)
+    ap.add_argument("--force-cache", action="store_true")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "ws_stamps")
@@ -37,7 +40,7 @@ def main() -> int:
 
     X, y = synthetic(a.data, n=a.samples, d=a.features)
     clf = SVC(C=a.C, gamma=a.gamma, eps=1e-3, device="cuda", solver="ws", ws_size=a.ws_size, ws_new=a.ws_new,
-              ws_rel=a.ws_rel).fit(X, y)
+              ws_rel=a.ws_rel, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache).fit(X, y)
     raw = np.fromfile(path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
     rounds = min(clf.n_rounds_, 4096)
     s = raw[2:rounds]
@@ -47,7 +50,8 @@ def main() -> int:
     nxt = np.roll(raw[:, 6], -1)[2:rounds][ok]
     res = {
         "rounds": clf.n_rounds_, "pair_steps": clf.n_iter_, "fit_time_s": round(clf.fit_time_, 4),
-        "b": float(clf.b_), "n_sv": int(clf.n_support_),
+        "b": float(clf.b_), "n_sv": int(clf.n_support_), "engine": clf.setup_info_["iteration"],
+        "rows_computed": int(clf.stats_.get("rows_computed", 0)),
         "steps_per_round_median": float(np.median(s[:, 5])),
         "select_wg0_us": us(s[:, 7] - s[:, 6]),
         "select_end_to_gather_us": us(s[:, 1] - s[:, 7]),

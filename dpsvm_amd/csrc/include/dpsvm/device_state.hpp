@@ -239,7 +239,9 @@ struct WsArgs {
   float* alpha;        // [n] global
   float* f;            // [nl] local gradient
   int64_t n, nl, off;
-  int32_t G, rpt;      // selection geometry: G workgroups x 256 threads x rpt rows
+  int32_t G, rpt;      // selection geometry: G workgroups x 256 threads x rpt rows (same on every rank)
+  int32_t world;       // ranks (> 1: candidates all-gathered, the sub-Gram all-reduced)
+  int32_t G_all;       // candidate lists the merge reads: world * G
   int32_t q_max, n_new, inner_max;
   float rel_local;     // sub-problem tolerance: max(eps, rel_local * global gap / 2)
   float C, eps, tau;
@@ -249,9 +251,11 @@ struct WsArgs {
   int32_t L;           // cache mode: lines
   int32_t* slot_of;    // cache mode: [n] line of a global row or -1
   int32_t* key_of;     // cache mode: [L] row held by a line or -1
-  uint64_t* cand;      // [G][2][kWsCand] per-workgroup candidate keys (up, low), ascending
-  float* subg;         // [q][q] sub-Gram of the current working set (ws_gather -> ws_solve)
-  float* aux;          // [3][kWsMax] alpha, y, f of the working set
+  uint64_t* cand_out;  // [G][2][kWsCand] this rank's per-workgroup candidate keys (up, low), ascending
+  uint64_t* cand;      // [G_all][2][kWsCand] every rank's lists (== cand_out at world 1)
+  float* subg;         // [q_max][q_max] sub-Gram of the current working set (row stride q_max; at
+                       // world > 1 each rank fills the columns it owns, zeros elsewhere: summed)
+  float* aux;          // [3][kWsMax] f (owner-filled, summed with subg), alpha, y of the working set
   WsCtrl* ctrl;
   SmoStatus* status;   // host-mapped
   uint64_t* stamps;    // DPSVM_STAMPS diagnostics: s_memrealtime per phase, ring of kStampRing rounds

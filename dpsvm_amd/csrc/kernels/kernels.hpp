@@ -64,12 +64,12 @@ void preload_persist_kernel(hipStream_t s);
 void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uint32_t tag, int64_t timeout_ticks,
               int32_t* ok, hipStream_t s);
 
-// working-set engine (smo_ws.hip): selection geometry for nl local rows
-// (<= 256 workgroups x 256 threads x rpt rows); one round = ws_gather (merge,
+// working-set engine (smo_ws.hip): selection geometry for the largest shard
+// (<= 256 / world workgroups x 256 threads x rpt rows); one round = ws_gather (merge,
 // stop test, working set, sub-Gram rows), ws_solve (the sub-problem), then
 // ws_select (f update, next candidates)
-bool ws_supported(int64_t nl, int q_max);
-void ws_geometry(int64_t nl, int32_t* G, int32_t* rpt);
+bool ws_supported(int64_t nl_max, int world, int q_max);
+void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt);
 void ws_select(const WsArgs& a, hipStream_t s);
 void ws_gather(const WsArgs& a, hipStream_t s);
 void ws_solve(const WsArgs& a, hipStream_t s);

@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
     constexpr int W = kWsSelThreads / 64;
     uint64_t eu = lane < W * kWsCand ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
     uint64_t el = lane < W * kWsCand ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
-    uint64_t* out = a.cand + (size_t)blockIdx.x * 2 * kWsCand;
+    uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
     for (int round = 0; round < kWsCand; ++round) {
       const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
       if (lane == 0) {
@@ -393,7 +393,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
     if (lead) c->n_apply = 0;
     return false;
   }
-  const int G = a.G;
+  const int G = a.G_all;
   const int64_t r_now = c->outer;
   const int par = (int)(r_now & 1);
   const int q_prev = c->q[par ^ 1];
@@ -577,6 +577,32 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   return true;
 }
 
+// Row ra of the q_max-stride sub-Gram from line `line` (K(idx_ra, off + j) at
+// line[j]), plus the row's f / alpha / y.  A rank fills only the columns (and
+// the f) of rows it owns and zeros the rest, so at world > 1 one sum all-reduce
+// assembles the exact matrix (each entry has exactly one owner).  Rows ra >= q
+// are zeroed.
+__device__ __forceinline__ void ws_gather_row(const WsArgs& a, const int32_t* s_idx, int q, int ra, const float* line) {
+  const int tid = threadIdx.x;
+  float* dst = a.subg + (size_t)ra * a.q_max;
+  if (ra >= q) {
+    for (int b = tid; b < a.q_max; b += kWsGatherThreads) dst[b] = 0.f;
+    if (tid == 0) a.aux[ra] = 0.f;
+    return;
+  }
+  const int64_t lo = a.off, hi = a.off + a.nl;
+  for (int b = tid; b < a.q_max; b += kWsGatherThreads) {
+    const int64_t gj = b < q ? (int64_t)s_idx[b] : -1;
+    dst[b] = gj >= lo && gj < hi ? line[gj - lo] : 0.f;
+  }
+  if (tid == 0) {
+    const int64_t gi = s_idx[ra];
+    a.aux[ra] = gi >= lo && gi < hi ? a.f[gi - lo] : 0.f;
+    a.aux[kWsMax + ra] = a.alpha[gi];
+    a.aux[2 * kWsMax + ra] = a.y[gi];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // ws_gather (dense mode): the merge in every workgroup + one sub-Gram row per
 // workgroup (row a: q random columns of Gram row idx_a — one load per thread;
@@ -604,17 +630,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
       c->b_lo = b_lo;
     }
   }
-  const int ra = blockIdx.x;
-  if (ra < q) {
-    const int32_t gi = s_idx[ra];
-    const float* grow = a.gram + (int64_t)gi * a.ldg - a.off;
-    for (int b = tid; b < q; b += kWsGatherThreads) a.subg[ra * q + b] = grow[s_idx[b]];
-    if (tid == 0) {
-      a.aux[ra] = a.alpha[gi];
-      a.aux[kWsMax + ra] = a.y[gi];
-      a.aux[2 * kWsMax + ra] = a.f[gi - a.off];
-    }
-  }
+  ws_gather_row(a, s_idx, q, blockIdx.x, blockIdx.x < q ? a.gram + (int64_t)s_idx[blockIdx.x] * a.ldg : nullptr);
   if (lead) WS_STAMP(8);
 }
 
@@ -708,18 +724,14 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
   const int par = (int)(c->outer & 1);
   const int q = c->q[par];
   const int ra = blockIdx.x;
-  if (ra >= q) return;
+  if (ra >= q) {
+    ws_gather_row(a, s_idx, q, ra, nullptr);
+    return;
+  }
   for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][t];
   __syncthreads();
-  const int32_t gi = s_idx[ra];
-  const float* grow = a.gram + (int64_t)c->line[par][ra] * a.ldg - a.off;
-  for (int b = tid; b < q; b += kWsGatherThreads) a.subg[ra * q + b] = grow[s_idx[b]];
-  if (tid == 0) {
-    a.aux[ra] = a.alpha[gi];
-    a.aux[kWsMax + ra] = a.y[gi];
-    a.aux[2 * kWsMax + ra] = a.f[gi - a.off];
-    if (ra == 0) WS_STAMP(8);
-  }
+  ws_gather_row(a, s_idx, q, ra, a.gram + (int64_t)c->line[par][ra] * a.ldg);
+  if (tid == 0 && ra == 0) WS_STAMP(8);
 }
 
 // ---------------------------------------------------------------------------
@@ -820,16 +832,15 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const float b_hi = c->b_hi, b_lo = c->b_lo;
   const int64_t it0 = c->iter;
   {
-    const int qq = q * q;
-    const int n4 = qq >> 2;
-    const float4* src = (const float4*)a.subg;
-    float4* dst = (float4*)K;
-    for (int i = tid; i < n4; i += kWsSolveThreads) dst[i] = src[i];
-    for (int i = 4 * n4 + tid; i < qq; i += kWsSolveThreads) K[i] = a.subg[i];
+    // rows of the q_max-stride sub-Gram into the compact q x q LDS block
+    for (int r = wave; r < q; r += kWsSolveThreads / 64) {
+      const float* src = a.subg + (size_t)r * a.q_max;
+      for (int b = lane; b < q; b += 64) K[r * q + b] = src[b];
+    }
     if (tid < q) {
-      s_a[tid] = a.aux[tid];
-      s_y[tid] = a.aux[kWsMax + tid];
-      s_f[tid] = a.aux[2 * kWsMax + tid];
+      s_f[tid] = a.aux[tid];
+      s_a[tid] = a.aux[kWsMax + tid];
+      s_y[tid] = a.aux[2 * kWsMax + tid];
       s_idx[tid] = c->idx[par][tid];
       s_line[tid] = c->line[par][tid];
     }
@@ -944,17 +955,20 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
 
 namespace launch {
 
-void ws_geometry(int64_t nl, int32_t* G, int32_t* rpt) {
-  const int64_t g = std::max<int64_t>(1, std::min<int64_t>(kWsMaxGroups, (nl + kWsSelThreads - 1) / kWsSelThreads));
-  const int64_t r = (nl + g * kWsSelThreads - 1) / (g * kWsSelThreads);
+void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt) {
+  // every rank the same geometry (sized for the largest shard); the merge reads
+  // world * G <= 256 candidate lists
+  const int64_t gmax = std::max<int64_t>(1, kWsMaxGroups / std::max(1, world));
+  const int64_t g = std::max<int64_t>(1, std::min<int64_t>(gmax, (nl_max + kWsSelThreads - 1) / kWsSelThreads));
+  const int64_t r = (nl_max + g * kWsSelThreads - 1) / (g * kWsSelThreads);
   *G = (int32_t)g;
   *rpt = (int32_t)std::max<int64_t>(1, r);
 }
 
-bool ws_supported(int64_t nl, int q_max) {
+bool ws_supported(int64_t nl_max, int world, int q_max) {
   int32_t G = 0, rpt = 0;
-  ws_geometry(nl, &G, &rpt);
-  return q_max >= 2 && q_max <= kWsMax && rpt <= kWsMaxRPT && nl < (int64_t)1 << 31;
+  ws_geometry(nl_max, world, &G, &rpt);
+  return q_max >= 2 && q_max <= kWsMax && rpt <= kWsMaxRPT && nl_max < (int64_t)1 << 31 && world <= kWsMaxGroups;
 }
 
 void ws_select(const WsArgs& a, hipStream_t s) {

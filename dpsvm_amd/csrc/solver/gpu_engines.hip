@@ -249,6 +249,46 @@ struct FusedCache final : Engine {
   }
 };
 
+// Per-round collectives of the working-set engines at world > 1 (or forced at
+// world 1, which tests the RCCL + graph-capture path on one GPU; every rank
+// runs the merge and the sub-problem redundantly on identical inputs):
+// all-gather of the candidate lists, and one sum all-reduce that assembles the
+// sub-Gram (+ the members' f) from the columns each rank owns.  Device
+// communicators (RCCL) enqueue on the stream and are captured in the round
+// graph; host communicators stage through host memory.
+void ws_allgather_cand(GpuSolver::Impl& m) {
+  if (!m.collectives()) return;
+  const size_t bytes = (size_t)m.wsa.G * 2 * kWsCand * sizeof(uint64_t);
+  if (m.comm->device_memory()) {
+    m.comm->allgather(m.wsa.cand_out, m.wsa.cand, bytes, m.stream);  // in place: cand_out = cand + rank * bytes
+    return;
+  }
+  m.h_wscand.resize(bytes * m.world);
+  uint8_t* mine = m.h_wscand.data() + (size_t)m.rank * bytes;
+  HIP_CHECK(hipMemcpyAsync(mine, m.wsa.cand_out, bytes, hipMemcpyDeviceToHost, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  m.comm->allgather(mine, m.h_wscand.data(), bytes, nullptr);
+  HIP_CHECK(hipMemcpyAsync(m.wsa.cand, m.h_wscand.data(), bytes * m.world, hipMemcpyHostToDevice, m.stream));
+}
+
+void ws_allreduce_sub(GpuSolver::Impl& m) {
+  if (!m.collectives()) return;
+  const size_t count = (size_t)m.wsa.q_max * m.wsa.q_max + kWsMax;  // sub-Gram + the members' f
+  if (m.comm->device_memory()) {
+    m.comm->allreduce_sum_f32(m.wssub, count, m.stream);
+    return;
+  }
+  m.h_wssub.resize(count);
+  HIP_CHECK(hipMemcpyAsync(m.h_wssub.data(), m.wssub, count * 4, hipMemcpyDeviceToHost, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  m.comm->allreduce_sum_f32(m.h_wssub.data(), count, nullptr);
+  HIP_CHECK(hipMemcpyAsync(m.wssub, m.h_wssub.data(), count * 4, hipMemcpyHostToDevice, m.stream));
+}
+
+bool ws_graphs(GpuSolver::Impl& m) {
+  return m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
+}
+
 // Working-set rounds on the resident Gram (smo_ws.hip).  Seed: the Gram GEMM,
 // the control record (no working set yet) and the first candidate selection;
 // a block is B rounds of [ws_gather, ws_solve, ws_select] (one hipGraph), so f is
@@ -259,8 +299,10 @@ struct WsDense final : DenseBase {
   int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
   static void round(GpuSolver::Impl& m) {
     launch::ws_gather(m.wsa, m.stream);
+    ws_allreduce_sub(m);
     launch::ws_solve(m.wsa, m.stream);
     launch::ws_select(m.wsa, m.stream);
+    ws_allgather_cand(m);
   }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {
     gram(m, res);
@@ -272,8 +314,8 @@ struct WsDense final : DenseBase {
     c.b_lo = b_lo;
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
-    const bool graphs = m.p.use_graph && !m.p.sync_debug && !sync_debug_env();
-    if (graphs && !m.gexec) {
+    ws_allgather_cand(m);
+    if (ws_graphs(m) && !m.gexec) {
       const int B = block(m.p);
       HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
       try {
@@ -315,8 +357,10 @@ struct WsCache final : Engine {
                              m.x + (size_t)(m.off - m.args.x_row0) * m.dp, m.xsq + m.off, m.nl, m.dp, m.gamma,
                              m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
     launch::ws_gather(w, m.stream);
+    ws_allreduce_sub(m);
     launch::ws_solve(w, m.stream);
     launch::ws_select(w, m.stream);
+    ws_allgather_cand(m);
   }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult&) override {
     WsCtrl c;
@@ -327,8 +371,8 @@ struct WsCache final : Engine {
     c.b_lo = b_lo;
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
-    const bool graphs = m.p.use_graph && !m.p.sync_debug && !sync_debug_env();
-    if (graphs && !m.gexec) {
+    ws_allgather_cand(m);
+    if (ws_graphs(m) && !m.gexec) {
       const int B = block(m.p);
       HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
       try {

@@ -96,7 +96,9 @@ struct GpuSolver::Impl {
   WsArgs wsa{};
   WsCtrl* wsctrl = nullptr;
   uint64_t* wscand = nullptr;
-  float* wssub = nullptr;          // q x q sub-Gram + [3][kWsMax] alpha / y / f of the working set
+  float* wssub = nullptr;          // q_max x q_max sub-Gram + [3][kWsMax] f / alpha / y of the working set
+  std::vector<uint8_t> h_wscand;   // host staging of the per-round collectives (host communicators)
+  std::vector<float> h_wssub;
   uint64_t* stamps = nullptr;      // DPSVM_STAMPS diagnostics
   std::string stamps_path;
   std::vector<uint64_t> h_partials;  // host staging for host-memory communicators

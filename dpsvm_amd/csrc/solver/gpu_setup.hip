@@ -299,12 +299,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // every rank a one-rank problem): the resident Gram (ws-dense), or a
   // kernel-row cache whose missing rows come from one GEMM per round (ws-cache)
   const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
-  const bool ws_ok = m.p.solver == 2 && m.world == 1 && m.replicated && !m.p.force_collectives &&
-                     launch::ws_supported(m.nl, ws_q);
+  const bool ws_ok = m.p.solver == 2 && m.replicated && launch::ws_supported(nl_max, m.world, ws_q);
   const bool ws_cand = ws_ok && m.dense;
   const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 && launch::smo_fused_lru_supported(m.dp);
   if (m.p.solver == 2 && !ws_ok)
-    m.info.engine_note = "ws engines need one rank with replicated X (world 1 or dp replicate): SMO engine used";
+    m.info.engine_note = "ws engines need replicated X and <= 16 rows per selection thread: SMO engine used";
   const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
                          launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
@@ -416,8 +415,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.xpoll_sleep = 1;
   a.xtimeout_ticks = 0;
   m.xch = false;
-  const bool want_xch = (m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) || pdense_cand ||
-                        plru_cand;
+  const bool want_xch = (!ws_cand && !wsc_cand && m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) ||
+                        pdense_cand || plru_cand;
   if (want_xch) {
     const bool ok = m.setup_exchange();
     DPSVM_CHECK(ok || (m.p.exchange != 2 && m.p.persist != 2),
@@ -480,7 +479,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.n = n;
     w.nl = m.nl;
     w.off = m.off;
-    launch::ws_geometry(m.nl, &w.G, &w.rpt);
+    launch::ws_geometry(nl_max, m.world, &w.G, &w.rpt);
+    w.world = m.world;
+    w.G_all = w.G * m.world;
     w.q_max = ws_q;
     // >= 2 new rows: the global maximal violating pair (up rank 0, low rank 0)
     // is always in the set, so every round makes progress
@@ -494,10 +495,15 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.tau = m.p.tau;
     w.clip = (int)m.p.clip;
     w.max_iter = m.p.max_iter;
-    m.wscand = dmalloc<uint64_t>((size_t)w.G * 2 * kWsCand, &m.bytes);
+    // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)
+    m.wscand = dmalloc<uint64_t>((size_t)w.G_all * 2 * kWsCand, &m.bytes);
     m.wsctrl = dmalloc<WsCtrl>(1, &m.bytes);
+    // sub-Gram [q_max][q_max] then aux [f | alpha | y]: the first q_max^2 + kWsMax
+    // floats are the per-round sum all-reduce at world > 1
     m.wssub = dmalloc<float>((size_t)ws_q * ws_q + 3 * kWsMax, &m.bytes);
+    HIP_CHECK(hipMemsetAsync(m.wssub, 0, ((size_t)ws_q * ws_q + 3 * kWsMax) * 4, m.stream));
     w.cand = m.wscand;
+    w.cand_out = m.wscand + (size_t)m.rank * w.G * 2 * kWsCand;
     w.subg = m.wssub;
     w.aux = m.wssub + (size_t)ws_q * ws_q;
     w.ctrl = m.wsctrl;

@@ -132,3 +132,65 @@ def test_ws_cache_engine_small_cache_refused_cleanly():
     s = SVC(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300).fit(X, y)
     assert s.setup_info_["iteration"] in ("persistent-cache", "fused-cache")
     assert "ws-cache needs" in s.setup_info_["engine_note"]
+
+
+def _fit_threads(native, world, X, y, **kw):
+    import threading
+
+    g = native.ThreadCommGroup(world)
+    comms = [g.comm(r) for r in range(world)]
+    out, errs = [None] * world, []
+
+    def work(r):
+        try:
+            out[r] = SVC(**kw).fit(X, y, comm=comms[r])
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs, errs
+    return out
+
+
+@pytest.mark.parametrize("world,extra", [(2, {}), (3, {}), (4, {"force_cache": True, "cache_lines": 1200})])
+def test_ws_engine_sharded_ranks(world, extra):
+    """Rows sharded over ranks (threads sharing the GPU, host-staged
+    collectives): per round the candidate lists are all-gathered and the
+    sub-Gram is summed from the columns each rank owns; every rank runs the
+    merge and the sub-problem on identical inputs, so every rank ends with the
+    same alphas (cross-rank digest), and the run reaches the one-rank optimum
+    (box clipping: unique dual optimum)."""
+    from dpsvm_amd._native import load
+
+    X, y = synthetic("adult", n=4000, seed=13)
+    kw = dict(C=1.0, gamma=0.05, eps=1e-3, clip="box", device="cuda", solver="ws", dp="shard", **extra)
+    ref = SVC(**kw).fit(X, y)
+    out = _fit_threads(load(), world, X, y, **kw)
+    want = "ws-cache" if extra else "ws-dense"
+    for r in range(world):
+        assert out[r].setup_info_["iteration"] == want and out[r].setup_info_["n_local"] < 4000
+        assert out[r].converged_
+        assert np.array_equal(out[r].alpha_, out[0].alpha_)
+    assert _kkt_gap(X, y, out[0].alpha_, 1.0, 0.05) < 2.2e-3
+    assert abs(out[0].b_ - ref.b_) < 1e-2
+    assert abs(out[0].n_support_ - ref.n_support_) <= max(3, ref.n_support_ // 50)
+
+
+@pytest.mark.parametrize("extra", [{}, {"force_cache": True, "cache_lines": 1500}])
+def test_ws_engine_rccl_one_rank_collective_path(extra):
+    """The ws engines' RCCL collectives (in-place candidate all-gather, sub-Gram
+    sum all-reduce) captured in the round hipGraph, on one GPU with a one-rank
+    communicator (force_collectives): bit-identical to the local path."""
+    from dpsvm_amd._native import load
+
+    C = load()
+    X, y = synthetic("mnist", n=4000, seed=3)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws", **extra)
+    ref = SVC(**kw).fit(X, y)
+    comm = C.rccl_comm(C.rccl_unique_id(), 0, 1, 0)
+    got = SVC(force_collectives=True, **kw).fit(X, y, comm=comm)
+    assert got.setup_info_["iteration"] == ref.setup_info_["iteration"]
+    assert got.n_iter_ == ref.n_iter_ and got.n_rounds_ == ref.n_rounds_
+    assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
