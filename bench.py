@@ -101,6 +101,8 @@ def parse(argv=None):
     ap.add_argument("--xch-timeout", type=float, default=None,
                     help="give-up bound of one in-kernel exchange poll (default 30 s at N > 1, else 120 s)")
     ap.add_argument("--no-accuracy", action="store_true")
+    ap.add_argument("--log-every", type=int, default=0,
+                    help="rank 0 prints b_hi / b_lo / gap every N pair steps (long big-config runs)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     for k, v in PRESETS[a.config].items():
@@ -149,6 +151,8 @@ def main(argv=None) -> int:
                     ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block,
                     xch_timeout_s=a.xch_timeout if a.xch_timeout is not None else (30.0 if multi else 120.0))
     params = cfg.to_native(X.shape[1])
+    if ctx.rank == 0:
+        params.log_every = a.log_every
     # auto: RCCL, or gloo on EVERY rank when the RCCL bootstrap fails on any
     # rank (agreed over the host group, dpsvm_amd.parallel.make_comm); the
     # per-iteration exchange is in-kernel either way
@@ -159,7 +163,14 @@ def main(argv=None) -> int:
     if on_gpu:
         solver = C.GpuSolver(params, comm, ctx.local_rank)
         info = solver.setup(X, X.shape[0], y)
-        run = lambda: solver.solve()  # noqa: E731
+        def progress(it, bh, bl, el, hits, misses):
+            print(f"[bench] iter {it} b_hi {bh:.6g} b_lo {bl:.6g} gap {bl - bh:.3g} {el:.1f} s "
+                  f"hits {hits} misses {misses}", file=sys.stderr, flush=True)
+
+        if a.log_every and ctx.rank == 0:
+            run = lambda: solver.solve(None, progress)  # noqa: E731
+        else:
+            run = lambda: solver.solve()  # noqa: E731
         if n_ranks > 1 and info.get("exchange") == "peer" and a.exchange == "auto":
             # the in-kernel peer exchange is self-tested at setup; if a warmup run still
             # fails on it (every rank fails the same way), fall back to the collective path
@@ -185,8 +196,11 @@ def main(argv=None) -> int:
         # sharded, cross-device path on this node too: one untimed solve
         sp = cfg.to_native(X.shape[1])
         sp.dp_policy = 1
+        sp.watchdog_s = 120.0  # a stuck collective aborts ITS communicator and fails this check only
+        s_comm = None
         try:
-            s_solver = C.GpuSolver(sp, comm, ctx.local_rank)
+            s_comm = make_comm(ctx, comm.name if comm.name in ("rccl", "gloo") else "auto")
+            s_solver = C.GpuSolver(sp, s_comm, ctx.local_rank)
             s_info = s_solver.setup(X, X.shape[0], y)
             sync()
             barrier()
@@ -207,6 +221,7 @@ def main(argv=None) -> int:
             shard_check = {"error": str(e)[:300]}
             if ctx.rank == 0:
                 print(f"[bench] sharded check failed: {e}", file=sys.stderr)
+        del s_comm
 
 
     for _ in range(a.warmup):
@@ -286,6 +301,9 @@ def main(argv=None) -> int:
             "converged": bool(res["converged"]),
             "n_sv": nsv,
             "b": res["b"],
+            "b_hi": res.get("b_hi"),
+            "b_lo": res.get("b_lo"),
+            "final_gap": (res["b_lo"] - res["b_hi"]) if "b_lo" in res else None,  # stop: gap <= 2 eps
             "train_accuracy": acc,
             "gram_gemm_s": round(float(res.get("t_gram", 0.0)), 6),
             "smo_loop_s_min": round(solve_min, 6),

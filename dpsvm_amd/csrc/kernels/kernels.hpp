@@ -79,7 +79,8 @@ void ws_merge(const WsArgs& a, hipStream_t s);
 bool ws_cache_supported(int64_t L, int q_max);
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
-//   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled)
+//   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled; rbf_rows_indexed
+//   reads B rows to a multiple of 256)
 //   symmetric: B == A (one rank): tiles above the diagonal only, each also
 //   stores its transpose (half the MFMA work, bit-identical values)
 void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,

@@ -13,7 +13,10 @@
 //             launches (svmTrain.cu:633-665, K12/K13).
 //
 // Tiling: 128x128 block tile, BK = 16, 256 threads = 4 waves (2x2), each wave
-// 64x64 = 2x2 MFMA 32x32 tiles (64 accumulator registers).  A/B tiles are
+// 64x64 = 2x2 MFMA 32x32 tiles (64 accumulator registers).  ROWS with a short
+// row set (<= 64 rows per tile) uses a 64x256 tile (4 waves 1x4): with 128x128
+// the waves of the dead row half sit on SIMDs 2-3 (waves are dealt to SIMDs
+// in order), which then issue no MFMA at all — half the CU's matrix rate.  A/B tiles are
 // staged k-major in LDS (+4 float pad) through registers, double buffered so
 // the next tile's global loads overlap the current tile's 32 MFMAs per wave.
 // Operand maps (32x32x2 f32): A lane l -> (row l&31, k l>>5); B lane l ->
@@ -28,12 +31,13 @@
 namespace dpsvm {
 namespace dev {
 
-constexpr int BM = 128, BN = 128, BK = 16, LDP = BM + 4;
+constexpr int BM = 128, BN = 128, BK = 16;
 constexpr int GEMM_THREADS = 256;
 
 enum Epi { EPI_STORE = 0, EPI_PREDICT = 1, EPI_ROWS = 2 };
 
-template <int EPI>
+// WM: waves along M (2: 128x128 tile; 1: 64x256 tile, ROWS only)
+template <int EPI, int WM = 2>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     const float* __restrict__ A, const float* __restrict__ Asq, int64_t M, int lda,
     const float* __restrict__ B, const float* __restrict__ Bsq, int64_t N, int ldb, int dp,
@@ -51,6 +55,8 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   // L2, while every XCD still sees the whole matrix (balanced under the
   // symmetric mode's skipped lower triangle).  A bijection on the grid; the
   // tile math is unchanged: bit-identical output.
+  static_assert(WM == 2 || (WM == 1 && EPI == EPI_ROWS), "64x256 tiles: ROWS epilogue only");
+  constexpr int WN = 4 / WM, TM = 64 * WM, TN = 64 * WN, LDA = TM + 4, LDB = TN + 4;
   int64_t tx = blockIdx.x, ty = blockIdx.y;
   if (EPI == EPI_ROWS) M = *m_dev;
   if (EPI == EPI_STORE || EPI == EPI_ROWS) {
@@ -71,17 +77,17 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     ty = in / gm;
   }
   if (EPI == EPI_STORE && sym && ty < tx) return;
-  if (EPI == EPI_ROWS && tx * BM >= M) return;  // uniform: no barrier reached
-  __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
-  __shared__ float red[2][BM];
-  __shared__ float s_asq[EPI == EPI_ROWS ? BM : 1];      // ROWS: |x|^2 of the tile's rows
-  __shared__ int32_t s_orow[EPI == EPI_ROWS ? BM : 1];   // ROWS: their output lines (-1: past M)
+  if (EPI == EPI_ROWS && tx * TM >= M) return;  // uniform: no barrier reached
+  __shared__ __attribute__((aligned(16))) float As[2][BK][LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+  __shared__ float red[EPI == EPI_PREDICT ? 2 : 1][EPI == EPI_PREDICT ? BM : 1];
+  __shared__ float s_asq[EPI == EPI_ROWS ? TM : 1];      // ROWS: |x|^2 of the tile's rows
+  __shared__ int32_t s_orow[EPI == EPI_ROWS ? TM : 1];   // ROWS: their output lines (-1: past M)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = tx * BM;
-  const int64_t ntiles_total = (N + BN - 1) / BN;
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t m0 = tx * TM;
+  const int64_t ntiles_total = (N + TN - 1) / TN;
   int64_t nt_begin, nt_end;
   if (EPI != EPI_PREDICT) {
     nt_begin = ty;
@@ -91,11 +97,12 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     nt_end = nt_begin + n_tiles_per_split;
     if (nt_end > ntiles_total) nt_end = ntiles_total;
   }
-  // staging map: 512 float4 per tile, 2 per thread: row r = idx>>2, k4 = idx&3
+  // staging map: TM (TN) x 16 floats = WM (WN) float4 per thread: row r_ld0 +
+  // 64 i, k4 = tid & 3
   const int r_ld0 = tid >> 2, k4_ld = tid & 3;
   const int nk = dp / BK;  // dp is a multiple of 16
 
-  if (EPI == EPI_ROWS && threadIdx.x < BM) {
+  if (EPI == EPI_ROWS && threadIdx.x < TM) {
     // the tile's row metadata once (read from LDS in the epilogue instead of
     // two dependent global loads per output element)
     const int64_t row = m0 + threadIdx.x;
@@ -110,7 +117,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     for (int r = 0; r < 16; ++r) rowacc[i][r] = 0.f;
 
   for (int64_t nt = nt_begin; nt < nt_end; ++nt) {
-    const int64_t n0 = nt * BN;
+    const int64_t n0 = nt * TN;
     f16v acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -119,23 +126,28 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const float* ga0 = A + (m0 + r_ld0) * (int64_t)lda + 4 * k4_ld;
-    const float* ga1 = ga0 + 64 * (int64_t)lda;
-    if (EPI == EPI_ROWS) {  // rows past M repeat the last one (never stored)
-      ga0 = A + (int64_t)a_rows[min(m0 + r_ld0, M - 1)] * lda + 4 * k4_ld;
-      ga1 = A + (int64_t)a_rows[min(m0 + r_ld0 + 64, M - 1)] * lda + 4 * k4_ld;
+    const float* ga[WM];
+    const float* gb[WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      ga[i] = A + (m0 + r_ld0 + 64 * i) * (int64_t)lda + 4 * k4_ld;
+      if (EPI == EPI_ROWS)  // rows past M repeat the last one (never stored)
+        ga[i] = A + (int64_t)a_rows[min(m0 + r_ld0 + 64 * i, M - 1)] * lda + 4 * k4_ld;
     }
-    const float* gb0 = B + (n0 + r_ld0) * (int64_t)ldb + 4 * k4_ld;
-    const float* gb1 = gb0 + 64 * (int64_t)ldb;
-    f4 ra0 = *(const f4*)ga0, ra1 = *(const f4*)ga1;
-    f4 rb0 = *(const f4*)gb0, rb1 = *(const f4*)gb1;
+#pragma unroll
+    for (int i = 0; i < WN; ++i) gb[i] = B + (n0 + r_ld0 + 64 * i) * (int64_t)ldb + 4 * k4_ld;
+    f4 ra[WM], rb[WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) ra[i] = *(const f4*)ga[i];
+#pragma unroll
+    for (int i = 0; i < WN; ++i) rb[i] = *(const f4*)gb[i];
     auto stage = [&](int buf) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        As[buf][4 * k4_ld + c][r_ld0] = ra0[c];
-        As[buf][4 * k4_ld + c][r_ld0 + 64] = ra1[c];
-        Bs[buf][4 * k4_ld + c][r_ld0] = rb0[c];
-        Bs[buf][4 * k4_ld + c][r_ld0 + 64] = rb1[c];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) As[buf][4 * k4_ld + c][r_ld0 + 64 * i] = ra[i][c];
+#pragma unroll
+        for (int i = 0; i < WN; ++i) Bs[buf][4 * k4_ld + c][r_ld0 + 64 * i] = rb[i][c];
       }
     };
     __syncthreads();  // previous n-tile's readers are done with buffer 0
@@ -146,10 +158,10 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
       const bool more = kt + 1 < nk;
       if (more) {
         const int koff = (kt + 1) * BK;
-        ra0 = *(const f4*)(ga0 + koff);
-        ra1 = *(const f4*)(ga1 + koff);
-        rb0 = *(const f4*)(gb0 + koff);
-        rb1 = *(const f4*)(gb1 + koff);
+#pragma unroll
+        for (int i = 0; i < WM; ++i) ra[i] = *(const f4*)(ga[i] + koff);
+#pragma unroll
+        for (int i = 0; i < WN; ++i) rb[i] = *(const f4*)(gb[i] + koff);
       }
       // ROWS: a wave whose 64 rows all lie past M only stages (uniform skip)
       const bool live = EPI != EPI_ROWS || m0 + wm * 64 < M;
@@ -306,9 +318,10 @@ void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, c
                       const int32_t* out_rows, int64_t ldl, hipStream_t s) {
   if (M_max <= 0 || N <= 0) return;
   DPSVM_CHECK(dp % 16 == 0, "rbf_rows_indexed: dp must be a multiple of 16");
-  const int64_t tm = (M_max + dev::BM - 1) / dev::BM, tn = (N + dev::BN - 1) / dev::BN;
+  // 64x256 tiles: B (the columns) must be readable to a multiple of 256 rows
+  const int64_t tm = (M_max + 63) / 64, tn = (N + 255) / 256;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed: N too large for grid.y");
-  dev::rbf_gemm_kernel<dev::EPI_ROWS><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
+  dev::rbf_gemm_kernel<dev::EPI_ROWS, 1><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
       X, Xsq, M_max, dp, B, Bsq, N, dp, dp, gamma, lines, ldl, nullptr, 1, 0, a_rows, out_rows, m_dev);
   post_launch("rbf_rows_indexed", s);
 }
