@@ -209,7 +209,7 @@ constexpr int kWsMax = 192;          // working-set capacity: q x q fp32 sub-Gra
 constexpr int kWsCand = 4;           // candidates per side per selection workgroup
 constexpr int kWsSelThreads = 256;   // selection / f-update workgroup
 constexpr int kWsMaxGroups = 256;    // selection workgroups (<= 2048 candidates per side)
-constexpr int kWsMaxRPT = 16;        // rows per selection thread
+constexpr int kWsMaxRPT = 32;        // rows per selection thread (256 x 256 x 32 = 2.1M rows per rank)
 constexpr int kWsSolveThreads = 1024;
 
 struct alignas(16) WsCtrl {

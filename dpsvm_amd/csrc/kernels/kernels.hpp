@@ -77,6 +77,10 @@ void ws_solve(const WsArgs& a, hipStream_t s);
 // row GEMM; ws_gather then reads the sub-Gram from the members' lines
 void ws_merge(const WsArgs& a, hipStream_t s);
 bool ws_cache_supported(int64_t L, int q_max);
+// partitioned X, cache mode: out[i] = X row ctrl->miss_row[i] if this rank owns
+// it (rows off..off+nl-1 at x), else zeros; out_sq[i] = its global |x|^2
+void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* xsq, const WsCtrl* ctrl, int q_max,
+                  float* out, float* out_sq, hipStream_t s);
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled; rbf_rows_indexed

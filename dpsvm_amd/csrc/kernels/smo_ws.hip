@@ -229,16 +229,17 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
 // most ~48 Gram loads of one batch in flight instead of a chain of batches.
 template <int RPT>
 constexpr int ws_parts() {
-  return RPT <= 4 ? 4 : 2;  // register budget: <= 4 waves per SIMD at RPT <= 4, 2 above
+  // register budget: <= 4 waves per SIMD at RPT <= 4, 2 up to 16, 1 at 32 (2M rows on one GPU)
+  return RPT <= 4 ? 4 : RPT <= 16 ? 2 : 1;
 }
 
 template <int RPT>
 __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_kernel(WsArgs a) {
   constexpr int PARTS = ws_parts<RPT>();
-  constexpr int CH = RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
+  constexpr int CH = RPT >= 32 ? 1 : RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
   __shared__ int32_t s_idx[kWsMax];  // lines of the changed rows
   __shared__ float s_coef[kWsMax];
-  __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][kWsSelThreads * RPT];
+  __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][PARTS > 1 ? kWsSelThreads * RPT : 1];
   __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x & (kWsSelThreads - 1), part = threadIdx.x / kWsSelThreads;
@@ -251,7 +252,8 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
     s_coef[k] = c->apply_coef[k];
   }
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * RPT * kWsSelThreads + tid;
+  // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers
+  const int64_t base = (int64_t)blockIdx.x * a.rpt * kWsSelThreads + tid;
   float f[RPT];
   bool has[RPT];
 #pragma unroll
@@ -951,6 +953,27 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   }
 }
 
+// Partitioned X, cache mode: the X rows of this round's cache misses, packed
+// for the row GEMM.  Block i < q_max: row i of the pack = X row miss_row[i]
+// when this rank owns it, else zeros — the sum all-reduce over ranks then
+// leaves every rank holding the exact rows (x + 0 + ... = x); rows past n_miss
+// are zeroed too (never read by the GEMM, kept finite).  xsq is global on
+// every rank: the packed norms are local.
+__global__ __launch_bounds__(256) void ws_pack_rows_kernel(const float* __restrict__ x, int64_t off, int64_t nl,
+                                                           int dp, const float* __restrict__ xsq,
+                                                           const WsCtrl* __restrict__ c, float* __restrict__ out,
+                                                           float* __restrict__ out_sq) {
+  const int i = blockIdx.x;
+  const int m = c->n_miss;
+  const int64_t row = i < m ? (int64_t)c->miss_row[i] : -1;
+  const bool own = row >= off && row < off + nl;
+  f4* dst = (f4*)(out + (size_t)i * dp);
+  const f4* src = (const f4*)(x + (size_t)(own ? row - off : 0) * dp);
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int k = threadIdx.x; k < dp / 4; k += blockDim.x) dst[k] = own ? src[k] : z;
+  if (threadIdx.x == 0) out_sq[i] = row >= 0 ? xsq[row] : 0.f;
+}
+
 }  // namespace dev
 
 namespace launch {
@@ -973,12 +996,13 @@ bool ws_supported(int64_t nl_max, int world, int q_max) {
 
 void ws_select(const WsArgs& a, hipStream_t s) {
   const dim3 grid(a.G);
-  auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 4 ? 4 : 2)); };
+  auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 4 ? 4 : rpt <= 16 ? 2 : 1)); };
   if (a.rpt <= 1) dev::ws_select_kernel<1><<<grid, threads(1), 0, s>>>(a);
   else if (a.rpt <= 2) dev::ws_select_kernel<2><<<grid, threads(2), 0, s>>>(a);
   else if (a.rpt <= 4) dev::ws_select_kernel<4><<<grid, threads(4), 0, s>>>(a);
   else if (a.rpt <= 8) dev::ws_select_kernel<8><<<grid, threads(8), 0, s>>>(a);
-  else dev::ws_select_kernel<16><<<grid, threads(16), 0, s>>>(a);
+  else if (a.rpt <= 16) dev::ws_select_kernel<16><<<grid, threads(16), 0, s>>>(a);
+  else dev::ws_select_kernel<32><<<grid, threads(32), 0, s>>>(a);
   post_launch("ws_select", s);
 }
 
@@ -995,6 +1019,13 @@ void ws_gather(const WsArgs& a, hipStream_t s) {
 void ws_merge(const WsArgs& a, hipStream_t s) {
   dev::ws_merge_kernel<<<1, dev::kWsGatherThreads, 0, s>>>(a);
   post_launch("ws_merge", s);
+}
+
+void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* xsq, const WsCtrl* ctrl, int q_max,
+                  float* out, float* out_sq, hipStream_t s) {
+  DPSVM_CHECK(dp % 16 == 0, "ws_pack_rows: dp must be a multiple of 16");
+  dev::ws_pack_rows_kernel<<<dim3(q_max), 256, 0, s>>>(x, off, nl, dp, xsq, ctrl, out, out_sq);
+  post_launch("ws_pack_rows", s);
 }
 
 bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max + dev::kWsWindow; }

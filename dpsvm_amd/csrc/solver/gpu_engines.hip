@@ -143,13 +143,49 @@ struct DenseBase : Engine {
   void gram(GpuSolver::Impl& m, SolveResult& res) {
     trace::Range gram_range("dpsvm/gram_gemm");
     gram_timer.start(m.stream);
-    // one rank holds the whole (symmetric) Gram: compute half, mirror the rest
-    const bool sym = m.off == 0 && m.nl == m.n && m.replicated;
-    launch::rbf_gemm_store(m.x, m.xsq, m.n, m.dp, m.x + (size_t)(m.off - m.args.x_row0) * m.dp, m.xsq + m.off,
-                           m.nl, m.dp, m.dp, m.gamma, m.lines, m.ldl, m.stream, sym);
+    if (!m.replicated) {
+      gram_panels(m);
+    } else {
+      // one rank holds the whole (symmetric) Gram: compute half, mirror the rest
+      const bool sym = m.off == 0 && m.nl == m.n;
+      launch::rbf_gemm_store(m.x, m.xsq, m.n, m.dp, m.x + (size_t)m.off * m.dp, m.xsq + m.off, m.nl, m.dp, m.dp,
+                             m.gamma, m.lines, m.ldl, m.stream, sym);
+    }
     gram_timer.stop(m.stream);
     res.rows_computed = m.n;
     res.x_passes = 1;
+  }
+  // Partitioned X (ws-dense only: no later step reads a non-owned X row): the
+  // Gram block K(all rows, owned columns) panel by panel — rank r's shard is
+  // broadcast into a panel buffer and multiplied against the owned rows.  Every
+  // element is the same MFMA k-sequence as in the replicated launch
+  // (bit-identical Gram).  One panel of X lives at a time.
+  static void gram_panels(GpuSolver::Impl& m) {
+    const int64_t prow = round_up(m.ldl, 128) + 128;
+    size_t tb = 0;
+    float* panel = dmalloc<float>((size_t)prow * m.dp, &tb);
+    HIP_CHECK(hipMemsetAsync(panel, 0, (size_t)prow * m.dp * 4, m.stream));
+    std::vector<float> host;
+    for (int r = 0; r < m.world; ++r) {
+      const Shard s = shard_of(m.n, r, m.world);
+      const size_t bytes = (size_t)s.size * m.dp * 4;
+      if (r == m.rank) HIP_CHECK(hipMemcpyAsync(panel, m.x, bytes, hipMemcpyDeviceToDevice, m.stream));
+      if (m.world > 1 && bytes > 0) {
+        if (m.comm->device_memory()) {
+          m.comm->broadcast(panel, bytes, r, m.stream);
+        } else {
+          host.resize(bytes / 4);
+          HIP_CHECK(hipMemcpyAsync(host.data(), panel, bytes, hipMemcpyDeviceToHost, m.stream));
+          HIP_CHECK(hipStreamSynchronize(m.stream));
+          m.comm->broadcast(host.data(), bytes, r, nullptr);
+          HIP_CHECK(hipMemcpyAsync(panel, host.data(), bytes, hipMemcpyHostToDevice, m.stream));
+        }
+      }
+      launch::rbf_gemm_store(panel, m.xsq + s.offset, s.size, m.dp, m.x, m.xsq + m.off, m.nl, m.dp, m.dp, m.gamma,
+                             m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);
+    }
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    (void)hipFree(panel);
   }
   // record "no pending pair" in buffer 1 + the initial keys (published to the
   // exchange when there is one, else all-reduced when collectives run)
@@ -285,6 +321,21 @@ void ws_allreduce_sub(GpuSolver::Impl& m) {
   HIP_CHECK(hipMemcpyAsync(m.wssub, m.h_wssub.data(), count * 4, hipMemcpyHostToDevice, m.stream));
 }
 
+// partitioned X, cache mode: the packed miss rows (owner's row, zeros elsewhere)
+void ws_allreduce_rows(GpuSolver::Impl& m) {
+  if (!m.collectives()) return;
+  const size_t count = (size_t)m.wsa.q_max * m.dp;
+  if (m.comm->device_memory()) {
+    m.comm->allreduce_sum_f32(m.wsxq, count, m.stream);
+    return;
+  }
+  m.h_wsxq.resize(count);
+  HIP_CHECK(hipMemcpyAsync(m.h_wsxq.data(), m.wsxq, count * 4, hipMemcpyDeviceToHost, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  m.comm->allreduce_sum_f32(m.h_wsxq.data(), count, nullptr);
+  HIP_CHECK(hipMemcpyAsync(m.wsxq, m.h_wsxq.data(), count * 4, hipMemcpyHostToDevice, m.stream));
+}
+
 bool ws_graphs(GpuSolver::Impl& m) {
   return m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
 }
@@ -353,9 +404,16 @@ struct WsCache final : Engine {
   static void round(GpuSolver::Impl& m) {
     const WsArgs& w = m.wsa;
     launch::ws_merge(w, m.stream);
-    launch::rbf_rows_indexed(m.x, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), w.q_max,
-                             m.x + (size_t)(m.off - m.args.x_row0) * m.dp, m.xsq + m.off, m.nl, m.dp, m.gamma,
-                             m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
+    const float* B = m.x + (size_t)(m.off - m.args.x_row0) * m.dp;  // the owned rows
+    if (m.replicated) {
+      launch::rbf_rows_indexed(m.x, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), w.q_max, B, m.xsq + m.off, m.nl,
+                               m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
+    } else {
+      launch::ws_pack_rows(m.x, m.off, m.nl, m.dp, m.xsq, m.wsctrl, w.q_max, m.wsxq, m.wsxqsq, m.stream);
+      ws_allreduce_rows(m);
+      launch::rbf_rows_indexed(m.wsxq, m.wsxqsq, m.wsiota, m.wsctrl_n_miss(), w.q_max, B, m.xsq + m.off, m.nl,
+                               m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
+    }
     launch::ws_gather(w, m.stream);
     ws_allreduce_sub(m);
     launch::ws_solve(w, m.stream);

@@ -97,8 +97,10 @@ struct GpuSolver::Impl {
   WsCtrl* wsctrl = nullptr;
   uint64_t* wscand = nullptr;
   float* wssub = nullptr;          // q_max x q_max sub-Gram + [3][kWsMax] f / alpha / y of the working set
+  float *wsxq = nullptr, *wsxqsq = nullptr;  // partitioned X, cache mode: the misses' X rows / norms
+  int32_t* wsiota = nullptr;                  //   (their GEMM row indices: 0..q_max-1)
   std::vector<uint8_t> h_wscand;   // host staging of the per-round collectives (host communicators)
-  std::vector<float> h_wssub;
+  std::vector<float> h_wssub, h_wsxq;
   uint64_t* stamps = nullptr;      // DPSVM_STAMPS diagnostics
   std::string stamps_path;
   std::vector<uint64_t> h_partials;  // host staging for host-memory communicators

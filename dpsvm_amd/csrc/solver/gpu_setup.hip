@@ -34,7 +34,8 @@ GpuSolver::Impl::~Impl() {
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
-                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub})
+                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub,
+                    (void*)wsxq, (void*)wsxqsq, (void*)wsiota})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
   if (hlines_h) (void)hipHostFree(hlines_h);
@@ -285,7 +286,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   if (m.p.cache_mb > 0) budget = std::min(budget, m.p.cache_mb * 1024.0 * 1024.0);
   int64_t want_lines = (int64_t)(budget / line_bytes);
   if (m.p.cache_lines > 0) want_lines = std::min<int64_t>(want_lines, m.p.cache_lines);
-  m.dense = m.replicated && want_lines >= n && !m.p.force_cache;
+  // working-set engines (solver=ws): with replicated X, or with partitioned X
+  // (ws-dense builds its Gram block panel by panel from broadcast shards;
+  // ws-cache packs the misses' X rows and sums them over ranks each round —
+  // no engine step after the Gram reads a non-owned X row)
+  const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
+  const bool ws_ok = m.p.solver == 2 && launch::ws_supported(nl_max, m.world, ws_q);
+  m.dense = (m.replicated || ws_ok) && want_lines >= n && !m.p.force_cache;
   m.dense = m.all_agree(m.dense, m.comm, m.world);  // free memory can differ per device
   if (m.dense) {
     m.RBf = geo_dense.first;
@@ -295,15 +302,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // below) and a co-resident grid (census); the one-launch-per-iteration
   // engines are the fallbacks.
   const bool fused_lru_ok = !m.dense && m.replicated && launch::smo_fused_lru_supported(m.dp) && m.p.cache_engine == 0;
-  // working-set engines (solver=ws), one rank (the replicate dp policy gives
-  // every rank a one-rank problem): the resident Gram (ws-dense), or a
-  // kernel-row cache whose missing rows come from one GEMM per round (ws-cache)
-  const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
-  const bool ws_ok = m.p.solver == 2 && m.replicated && launch::ws_supported(nl_max, m.world, ws_q);
+  // working-set engines: the resident Gram (ws-dense), or a kernel-row cache
+  // whose missing rows come from one GEMM per round (ws-cache); rows sharded
+  // over ranks at world > 1 (per-round candidate all-gather + sub-Gram sum)
   const bool ws_cand = ws_ok && m.dense;
-  const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 && launch::smo_fused_lru_supported(m.dp);
+  const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 &&
+                        (!m.replicated || launch::smo_fused_lru_supported(m.dp));
   if (m.p.solver == 2 && !ws_ok)
-    m.info.engine_note = "ws engines need replicated X and <= 16 rows per selection thread: SMO engine used";
+    m.info.engine_note = "ws engines need <= 16 rows per selection thread: SMO engine used";
   const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
                          launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
@@ -509,6 +515,15 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.ctrl = m.wsctrl;
     w.status = m.status_d;
     w.stamps = m.stamps;
+    if (w.cache && !m.replicated) {
+      m.wsxq = dmalloc<float>((size_t)ws_q * m.dp, &m.bytes);
+      m.wsxqsq = dmalloc<float>((size_t)ws_q, &m.bytes);
+      m.wsiota = dmalloc<int32_t>((size_t)ws_q, &m.bytes);
+      std::vector<int32_t> io((size_t)ws_q);
+      for (int i = 0; i < ws_q; ++i) io[i] = i;
+      HIP_CHECK(hipMemcpyAsync(m.wsiota, io.data(), io.size() * 4, hipMemcpyHostToDevice, m.stream));
+      HIP_CHECK(hipStreamSynchronize(m.stream));
+    }
   }
   m.engine = gpu::make_engine(m.kind);
   m.info.iteration = engine_name(m.kind);

@@ -194,3 +194,65 @@ def test_ws_engine_rccl_one_rank_collective_path(extra):
     assert got.setup_info_["iteration"] == ref.setup_info_["iteration"]
     assert got.n_iter_ == ref.n_iter_ and got.n_rounds_ == ref.n_rounds_
     assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
+
+
+@pytest.mark.parametrize("world,extra", [(1, {}), (1, {"force_cache": True, "cache_lines": 1500}),
+                                         (2, {}), (4, {"force_cache": True, "cache_lines": 1500})])
+def test_ws_engine_partitioned_x_bit_identical(world, extra):
+    """x_mode=partitioned (each rank holds only its X shard): ws-dense builds
+    the Gram block from broadcast shard panels, ws-cache sums the misses' packed
+    X rows over ranks each round.  Same K values, same collectives: the
+    trajectory is bit-identical to replicated X at the same rank count."""
+    from dpsvm_amd._native import load
+
+    X, y = synthetic("mnist", n=4000, seed=21)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws", dp="shard", **extra)
+    if world == 1:
+        rep = [SVC(**kw).fit(X, y)]
+        part = [SVC(x_mode="partitioned", **kw).fit(X, y)]
+    else:
+        rep = _fit_threads(load(), world, X, y, **kw)
+        part = _fit_threads(load(), world, X, y, x_mode="partitioned", **kw)
+    want = "ws-cache" if extra else "ws-dense"
+    for r in range(world):
+        assert part[r].setup_info_["iteration"] == want and not part[r].setup_info_["x_replicated"]
+        assert rep[r].setup_info_["x_replicated"]
+        assert part[r].n_iter_ == rep[r].n_iter_ and part[r].n_rounds_ == rep[r].n_rounds_
+        assert np.array_equal(part[r].alpha_, rep[r].alpha_) and part[r].b_ == rep[r].b_
+    assert part[0].converged_
+
+
+@pytest.mark.parametrize("n", [150_000, 1_100_000])
+def test_ws_engine_large_n_rows_per_thread(n):
+    """Selection geometries whose rows per thread (a.rpt) is below the kernel's
+    register size RPT: 150k rows = 3 per thread on the RPT=4 kernel (ws-dense);
+    1.1M rows = 17 per thread on the RPT=32 kernel (ws-cache; 256 x 256 x 32 =
+    2.1M rows per rank, the synthetic-2m preset's geometry).  The stop test
+    must hold on the exact gradient (K(X, SVs) coef - y on the GPU in fp64) —
+    a workgroup indexing its rows by RPT instead of a.rpt once left rows
+    without f updates (a 'converged' run with an exact gap of 1.4)."""
+    d = 8
+    X, y = synthetic("blobs", n=n, d=d, seed=3, sep=10.0)  # well separated: few SVs
+    C_, g = 1.0, 0.125
+    s = SVC(C=C_, gamma=g, eps=1e-3, device="cuda", solver="ws", max_iter=200000).fit(X, y)
+    rpt = s.setup_info_["rows_per_group"] // 256
+    if n > 1_000_000:
+        assert s.setup_info_["iteration"] == "ws-cache" and rpt == 17  # RPT=32 kernel
+    else:
+        assert s.setup_info_["iteration"] == "ws-dense" and rpt == 3  # RPT=4 kernel
+    assert s.converged_
+    yy = torch.tensor(np.where(y > 0, 1.0, -1.0), device="cuda", dtype=torch.float64)
+    a = torch.tensor(s.alpha_, device="cuda", dtype=torch.float64)
+    Xd = torch.tensor(X, device="cuda", dtype=torch.float64)
+    sv = torch.nonzero(a > 0).flatten()
+    coef = a[sv] * yy[sv]
+    f = torch.empty(n, device="cuda", dtype=torch.float64)
+    for i in range(0, n, 1 << 16):
+        xb = Xd[i:i + (1 << 16)]
+        k = torch.exp(-g * torch.cdist(xb, Xd[sv]) ** 2)
+        f[i:i + (1 << 16)] = k @ coef - yy[i:i + (1 << 16)]
+    up = ((a == 0) & (yy == 1)) | ((a == C_) & (yy != 1)) | ((a > 0) & (a < C_))
+    lo = ((a == 0) & (yy != 1)) | ((a == C_) & (yy == 1)) | ((a > 0) & (a < C_))
+    gap = float(f[lo].max() - f[up].min())
+    print(f"{n} rows: {s.n_iter_} pair steps, {s.n_rounds_} rounds, {s.n_support_} SVs, gap {gap:.2e}")
+    assert gap < 2e-3 + 2e-4
