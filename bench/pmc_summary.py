@@ -27,6 +27,9 @@ def main(root):
             if cs.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0) > 0 and ns > 0:
                 fl = cs["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
                 extra += f", f32 MFMA {fl / 1e12:.3f} TFLOP = {fl / ns / 1e3:.1f} TFLOP/s ({100 * fl / ns / 1e3 / 157.3:.0f}% of 157.3)"
+            for c in ("FETCH_SIZE", "WRITE_SIZE"):  # KiB over the kernel's serialised dispatches
+                if cs.get(c, 0) > 0 and ns > 0:
+                    extra += f", {c} {cs[c] / 1024 ** 2:.2f} GiB = {cs[c] * 1024 / ns:.0f} GB/s"
             print(f"  {k}: {line}{extra}]")
 
 
