@@ -747,9 +747,13 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
 __device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, int lane, float C, float (&fu)[3],
                                          float (&fl)[3]) {
   const float INF = __builtin_inff();
-  const bool fr = (an > 0.f) & (an < C), z = an == 0.f, cc = an == C, py = yv > 0.f;
-  const float nu = (fr | (z & py) | (cc & !py)) ? fp : INF;
-  const float nl = (fr | (z & !py) | (cc & py)) ? -fp : INF;
+  // the operands are uniform: each test as a wave mask (all ones or zero; wave
+  // 0 runs with a full exec mask) keeps the set logic on the scalar unit
+  // instead of 0/1 VGPRs (~20 VALU per placement)
+  const uint64_t fr = __ballot(an > 0.f) & __ballot(an < C), z = __ballot(an == 0.f), cc = __ballot(an == C),
+                 py = __ballot(yv > 0.f);
+  const float nu = ((fr | (z & py) | (cc & ~py)) != 0) ? fp : INF;
+  const float nl = ((fr | (z & ~py) | (cc & py)) != 0) ? -fp : INF;
   const bool me = lane == (pos & 63);
   const int s = pos >> 6;
 #pragma unroll
@@ -822,8 +826,8 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
 
 template <bool kBox>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float K[];  // q x q sub-Gram
-  __shared__ float s_a[kWsMax], s_y[kWsMax], s_f[kWsMax];
+  extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
+  __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
   __shared__ int32_t s_idx[kWsMax], s_line[kWsMax];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -833,11 +837,28 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const int q = c->q[par];
   const float b_hi = c->b_hi, b_lo = c->b_lo;
   const int64_t it0 = c->iter;
+  const int ldk = a.q_max;  // LDS keeps the q_max stride: the load is one contiguous copy
   {
-    // rows of the q_max-stride sub-Gram into the compact q x q LDS block
-    for (int r = wave; r < q; r += kWsSolveThreads / 64) {
-      const float* src = a.subg + (size_t)r * a.q_max;
-      for (int b = lane; b < q; b += 64) K[r * q + b] = src[b];
+    // q rows of the q_max-stride sub-Gram into LDS (147 KiB at q = 192): 16-B
+    // loads, four in flight per thread before their stores
+    const int n = q * ldk;
+    if ((ldk & 3) == 0) {
+      const f4* src = (const f4*)a.subg;
+      f4* dst = (f4*)K;
+      const int n4 = n >> 2;
+      for (int e = tid; e < n4; e += 4 * kWsSolveThreads) {
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = e + u * kWsSolveThreads;
+          v[u] = src[k < n4 ? k : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (e + u * kWsSolveThreads < n4) dst[e + u * kWsSolveThreads] = v[u];
+      }
+    } else {
+      for (int e = tid; e < n; e += kWsSolveThreads) K[e] = a.subg[e];
     }
     if (tid < q) {
       s_f[tid] = a.aux[tid];
@@ -884,13 +905,13 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     // every LDS read of the step in one batch: the pair's alphas / labels,
     // the 2 x 2 block K(hi|lo, hi|lo) and the two sub-Gram rows
     const float a_hi = s_a[ph], y_hi = s_y[ph], a_lo = s_a[pl], y_lo = s_y[pl];
-    const float khl = K[ph * q + pl], klh = K[pl * q + ph], khh = K[ph * q + ph], kll = K[pl * q + pl];
+    const float khl = K[ph * ldk + pl], klh = K[pl * ldk + ph], khh = K[ph * ldk + ph], kll = K[pl * ldk + pl];
     float kh[3], kl[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       const int p = min(lane + 64 * s, q - 1);
-      kh[s] = K[ph * q + p];
-      kl[s] = K[pl * q + p];
+      kh[s] = K[ph * ldk + p];
+      kl[s] = K[pl * ldk + p];
     }
     const PairUpdate up = ws_pair_step<kBox>(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, ph == pl);
     float f_lo_new, f_hi_new;
@@ -913,10 +934,10 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     }
     ws_place(pl, up.a_lo_new, y_lo, f_lo_new, lane, C, fu, fl);
     ws_place(ph, up.a_hi_new, y_hi, f_hi_new, lane, C, fu, fl);  // hi written last (svmTrainMain.cpp:298-299)
-    if (lane == 0) {
-      s_a[pl] = up.a_lo_new;
-      s_a[ph] = up.a_hi_new;
-    }
+    // lane 0 writes the pair's alphas, the other lanes a private scratch word
+    // each (no exec-mask branch in the loop, no bank conflict)
+    s_a[lane == 0 ? pl : kWsMax + lane] = up.a_lo_new;
+    s_a[lane == 0 ? ph : kWsMax + 64 + lane] = up.a_hi_new;
     ++inner;
   }
   // ---- commit: alphas, the changed rows for the f update, control, status ----
