@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--host-cache-lines", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cache-lines", type=int, default=0)
+    ap.add_argument("--cache-mb", type=float, default=0,
+                    help="cap the kernel-row cache / resident Gram budget per rank (MiB; ranks sharing a device)")
     ap.add_argument("--x-mode", default="auto")
     ap.add_argument("--graph-block", type=int, default=64)
     ap.add_argument("--comm", default="auto", help="auto | rccl | gloo")
@@ -143,7 +145,7 @@ def main(argv=None) -> int:
     n_ranks = ctx.world
 
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
-    cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines,
+    cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines, cache_mb=a.cache_mb,
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
                     exchange=a.exchange, persist=a.persist, persist_block=a.persist_block, dp=a.dp,
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
@@ -247,7 +249,11 @@ def main(argv=None) -> int:
         acc = float(solver.train_accuracy(alpha, res["b"]))
     nsv = int((alpha > 0).sum())
     ref_check = None
-    if on_gpu and a.solver == "ws" and a.reference_check == "auto" and info.get("iteration") == "ws-dense":
+    if (on_gpu and a.solver == "ws" and a.reference_check == "auto" and info.get("iteration") == "ws-dense"
+            and (n_ranks == 1 or info.get("dp_policy") == "replicate")):
+        rows = np.arange(0, X.shape[0], max(1, X.shape[0] // 4096))
+        d_ws = np.asarray(solver.decision(alpha, res["b"], X[rows]))
+        del solver  # its resident Gram: the cross-check builds its own
         # the same problem by the pair-at-a-time engine (the reference's exact
         # trajectory, svmTrainMain.cpp:235-310), untimed: the two models must agree
         rp = cfg.to_native(X.shape[1])
@@ -259,8 +265,6 @@ def main(argv=None) -> int:
         r_alpha, r_res = r_solver.solve()
         sync()
         t_r = time.perf_counter() - t_r
-        rows = np.arange(0, X.shape[0], max(1, X.shape[0] // 4096))
-        d_ws = np.asarray(solver.decision(alpha, res["b"], X[rows]))
         d_ref = np.asarray(r_solver.decision(r_alpha, r_res["b"], X[rows]))
         ref_check = {"engine": r_info.get("iteration"), "s": round(t_r, 6), "iterations": int(r_res["iters"]),
                      "converged": bool(r_res["converged"]), "b": r_res["b"], "abs_b_diff": abs(r_res["b"] - res["b"]),
