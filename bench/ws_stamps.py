@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase anatomy of the working-set engine from in-kernel s_memrealtime stamps
 (DPSVM_STAMPS; 100 MHz).  Ring slot r holds, in time order: ws_select
-workgroup 0 entry/exit (6, 7: the f update + candidates before round r),
+workgroup 0 entry/f updated/exit (6, 10, 7: the f update + candidates before round r),
 ws_gather workgroup 0 entry (1), merged (2), exit (8), ws_solve entry (0),
 sub-Gram loaded (3), sub-problem solved (4), pair steps (5).
 
@@ -54,6 +54,8 @@ def main() -> int:
         "rows_computed": int(clf.stats_.get("rows_computed", 0)),
         "steps_per_round_median": float(np.median(s[:, 5])),
         "select_wg0_us": us(s[:, 7] - s[:, 6]),
+        "select_fupdate_us": us(s[:, 10] - s[:, 6]),
+        "select_candidates_us": us(s[:, 7] - s[:, 10]),
         "select_end_to_gather_us": us(s[:, 1] - s[:, 7]),
         "merge_us": us(s[:, 2] - s[:, 1]),
         "gather_rows_us": us(s[:, 8] - s[:, 2]),

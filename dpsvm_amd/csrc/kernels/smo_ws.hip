@@ -314,6 +314,7 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
     }
     if (bad) atomicOr(&c->nonfinite, 1);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(10);
   if (done != kRunning) return;  // uniform
 
   // partition 0 (waves 0..3) classifies and extracts; the other waves idle to
@@ -400,6 +401,9 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   const int par = (int)(r_now & 1);
   const int q_prev = c->q[par ^ 1];
   const int want = q_prev == 0 ? a.q_max : min(a.n_new, a.q_max);
+  // the previous set's row (read at the end) in the same load batch as the
+  // candidate lists: one global round trip fewer on the merge's serial path
+  const int32_t pidx_pre = tid < q_prev ? c->idx[par ^ 1][tid] : -1;
 
   // ---- every candidate list in registers (one load batch) ----
   uint64_t lu[kWsCand], ll[kWsCand];
@@ -563,7 +567,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   bool pk = false;
   int32_t pidx = -1;
   if (tid < q_prev) {
-    pidx = c->idx[par ^ 1][tid];
+    pidx = pidx_pre;
     const int ru = ws_hash_find(hk_u, hv_u, pidx);
     const int rl = ws_hash_find(hk_l, hv_l, pidx);
     pk = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
