@@ -393,7 +393,8 @@ def test_bench_two_processes_exchange_fallback(tmp_path):
     env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29611", os.path.join(root, "bench.py"), "--gpus", "2",
-           "--samples", "4000", "--steps", "1", "--warmup", "1", "--comm", "gloo", "--xch-timeout", "0.000001"]
+           "--samples", "4000", "--steps", "1", "--warmup", "1", "--comm", "gloo", "--xch-timeout", "0.000001",
+           "--solver", "smo"]  # the pair-at-a-time engines' peer exchange
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
@@ -435,7 +436,7 @@ def test_bench_multi_gpu_sharded_matches_one_gpu(tmp_path):
     DPSVM_TEST_SHARED_GPU=1 runs the same ranks on one GPU over gloo."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     world = 2 if _SHARED else min(_NDEV, 8)
-    out = _bench_multi(root, world, ["--dp", "shard"], 29641)
+    out = _bench_multi(root, world, ["--dp", "shard", "--solver", "smo"], 29641)
     assert out["n_gpus"] == world and out["converged"] and out["exchange"] == "peer"
     assert out["dp_policy"] == "shard" and out["exchange_mem"] == "uncached"
     assert out["comm"] != "local" and out["config"]["parallelism"] == f"dp{world}"
@@ -451,12 +452,32 @@ def test_bench_multi_gpu_auto_policy_replicates_and_checks_shards(tmp_path):
     check solve reports the same iterations and b."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     world = min(_NDEV, 8)
-    out = _bench_multi(root, world, [], 29651)
+    out = _bench_multi(root, world, ["--solver", "smo"], 29651)
     ref = _ref_8000()
     assert out["dp_policy"] == "replicate" and out["iterations"] == ref.n_iter_ and out["b"] == ref.b_
     sc = out["shard_check"]
     assert sc and "error" not in sc, sc
     assert sc["exchange"] == "peer" and sc["iterations"] == ref.n_iter_ and sc["b"] == ref.b_
+
+
+@_MULTI
+def test_bench_multi_gpu_ws_sharded_and_default(tmp_path):
+    """bench.py defaults (working-set engine) on up to 8 GPUs: sharded rows
+    (per-round candidate all-gather + sub-Gram sum over RCCL, graph-captured)
+    converge to the one-GPU optimum, cross-rank verified; the default policy
+    replicates on distinct GPUs and its untimed sharded check succeeds."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    world = 2 if _SHARED else min(_NDEV, 8)
+    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws").fit(*synthetic("mnist", n=8000, d=784, seed=0))
+    out = _bench_multi(root, world, ["--dp", "shard"], 29661)
+    assert out["iteration"] == "ws-dense" and out["dp_policy"] == "shard" and out["converged"]
+    assert abs(out["b"] - ref.b_) < 1e-3 and abs(out["n_sv"] - ref.n_support_) <= 8
+    if _NDEV >= 2:
+        dflt = _bench_multi(root, world, [], 29671)
+        assert dflt["dp_policy"] == "replicate" and dflt["iterations"] == ref.n_iter_ and dflt["b"] == ref.b_
+        sc = dflt["shard_check"]
+        assert sc and "error" not in sc and sc["engine"] == "ws-dense", sc
+        assert abs(sc["b"] - ref.b_) < 1e-3
 
 
 @pytest.mark.skipif(_NDEV < 2, reason="needs >= 2 GPUs (svmTrain -p N: one thread per device)")
