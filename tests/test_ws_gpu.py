@@ -256,3 +256,26 @@ def test_ws_engine_large_n_rows_per_thread(n):
     gap = float(f[lo].max() - f[up].min())
     print(f"{n} rows: {s.n_iter_} pair steps, {s.n_rounds_} rounds, {s.n_support_} SVs, gap {gap:.2e}")
     assert gap < 2e-3 + 2e-4
+
+
+def test_svmtrain_cli_ws_simulated_ranks_partitioned(tmp_path, bin_dir):
+    """svmTrain --solver ws with 3 simulated ranks on one device (in-process
+    communicator) and partitioned X: converges to the one-rank optimum (box
+    clipping), reports the ws engine in --metrics-json, and writes a model
+    whose b matches."""
+    import json
+    import os
+    import subprocess
+
+    outs = {}
+    for ranks, extra in ((1, []), (3, ["--ranks", "3", "--x-mode", "partitioned", "--dp", "shard"])):
+        mj = str(tmp_path / f"m{ranks}.json")
+        cmd = [os.path.join(bin_dir, "svmTrain"), "-a", "123", "-x", "4000", "--synthetic", "adult", "-c", "1",
+               "-g", "0.05", "-m", str(tmp_path / f"model{ranks}.txt"), "--solver", "ws", "--clip", "box",
+               "--metrics-json", mj] + extra
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs[ranks] = json.load(open(mj))
+    one, three = outs[1], outs[3]
+    assert one["engine"] == "ws-dense" and three["engine"] == "ws-dense" and three["world"] == 3
+    assert abs(one["b"] - three["b"]) < 1e-2 and abs(one["n_sv"] - three["n_sv"]) <= 40
