@@ -81,7 +81,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --watchdog S        :  host bound on one block of iterations (default 1800)\n"
                "   --census-groups N   :  residency census grid of the persistent engines (tests)\n"
                "   --no-verify-ranks   :  skip the cross-rank alpha digest (world > 1)\n"
-               "   --solver S          :  auto | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
+               "   --solver S          :  auto (ws from 100k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"

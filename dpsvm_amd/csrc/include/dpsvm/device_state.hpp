@@ -211,6 +211,7 @@ constexpr int kWsSelThreads = 256;   // selection / f-update workgroup
 constexpr int kWsMaxGroups = 256;    // selection workgroups (<= 2048 candidates per side)
 constexpr int kWsMaxRPT = 32;        // rows per selection thread (256 x 256 x 32 = 2.1M rows per rank)
 constexpr int kWsSolveThreads = 1024;
+constexpr int64_t kWsAutoRows = 100000;  // solver auto: working-set engines from this many rows on
 
 struct alignas(16) WsCtrl {
   int64_t iter;      // pair updates applied so far

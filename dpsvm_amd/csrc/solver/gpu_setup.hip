@@ -291,7 +291,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // ws-cache packs the misses' X rows and sums them over ranks each round —
   // no engine step after the Gram reads a non-owned X row)
   const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
-  const bool ws_ok = m.p.solver == 2 && launch::ws_supported(nl_max, m.world, ws_q);
+  // solver auto: the working-set engines from kWsAutoRows rows on (the pair-at-a-time
+  // engines follow the reference's trajectory exactly and win on small problems;
+  // on 500k-2M rows ws is 5-10x faster: profiles/r2_*_converged.json)
+  const bool want_ws = m.p.solver == 2 || (m.p.solver == 0 && n >= kWsAutoRows);
+  const bool ws_ok = want_ws && launch::ws_supported(nl_max, m.world, ws_q);
   m.dense = (m.replicated || ws_ok) && want_lines >= n && !m.p.force_cache;
   m.dense = m.all_agree(m.dense, m.comm, m.world);  // free memory can differ per device
   if (m.dense) {
@@ -308,7 +312,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool ws_cand = ws_ok && m.dense;
   const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 &&
                         (!m.replicated || launch::smo_fused_lru_supported(m.dp));
-  if (m.p.solver == 2 && !ws_ok)
+  if (want_ws && !ws_ok)
     m.info.engine_note = "ws engines need <= 16 rows per selection thread: SMO engine used";
   const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
