@@ -84,7 +84,7 @@ void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* 
 
 // RBF GEMM: out[i*ldo + j] = K(A_i, B_j) for i < M, j < N
 //   A: [M_pad][lda], B: [N_pad][ldb] (rows padded to 128, zero filled; rbf_rows_indexed
-//   reads B rows to a multiple of 256)
+//   reads B rows to a multiple of 512)
 //   symmetric: B == A (one rank): tiles above the diagonal only, each also
 //   stores its transpose (half the MFMA work, bit-identical values)
 void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const float* B,

@@ -36,8 +36,12 @@ constexpr int GEMM_THREADS = 256;
 
 enum Epi { EPI_STORE = 0, EPI_PREDICT = 1, EPI_ROWS = 2 };
 
-// WM: waves along M (2: 128x128 tile; 1: 64x256 tile, ROWS only)
-template <int EPI, int WM = 2>
+// Tile shapes (4 waves; each wave MI x NJ MFMA 32x32 tiles = 64 accumulators):
+//   <128, 2, 2>  128x128, waves 2x2     STORE (incl. symmetric) / PREDICT
+//   < 64, 2, 2>   64x256, waves 1x4     ROWS (row sets of 33-64 rows per tile)
+//   < 32, 1, 4>   32x512, waves 1x4     ROWS variant padding rows to 32 (measured
+//                                       slower than 64x256, not launched)
+template <int EPI, int TM = 128, int MI = 2, int NJ = 2>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     const float* __restrict__ A, const float* __restrict__ Asq, int64_t M, int lda,
     const float* __restrict__ B, const float* __restrict__ Bsq, int64_t N, int ldb, int dp,
@@ -54,9 +58,13 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   // an XCD's consecutive tiles share B panels and re-read A panels from its
   // L2, while every XCD still sees the whole matrix (balanced under the
   // symmetric mode's skipped lower triangle).  A bijection on the grid; the
-  // tile math is unchanged: bit-identical output.
-  static_assert(WM == 2 || (WM == 1 && EPI == EPI_ROWS), "64x256 tiles: ROWS epilogue only");
-  constexpr int WN = 4 / WM, TM = 64 * WM, TN = 64 * WN, LDA = TM + 4, LDB = TN + 4;
+  // tile math is unchanged: bit-identical output (every element is the same
+  // MFMA k-sequence in every tile shape).
+  constexpr int WM = TM / (32 * MI), WN = 4 / WM, TN = WN * 32 * NJ, LDA = TM + 4, LDB = TN + 4;
+  static_assert(WM * WN == 4 && MI * NJ == 4, "4 waves of 2x2 / 1x4 MFMA tiles");
+  static_assert((TM == 128 && MI == 2 && NJ == 2) || EPI == EPI_ROWS, "narrow tiles: ROWS epilogue only");
+  constexpr int NA = TM >= 64 ? TM / 64 : 1;  // A float4 loads per thread (TM = 32: threads < 128)
+  constexpr int NB = TN / 64;                 // B float4 loads per thread
   int64_t tx = blockIdx.x, ty = blockIdx.y;
   if (EPI == EPI_ROWS) M = *m_dev;
   if (EPI == EPI_STORE || EPI == EPI_ROWS) {
@@ -86,6 +94,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  const int rw = wm * 32 * MI, cw = wn * 32 * NJ;  // the wave's tile origin
   const int64_t m0 = tx * TM;
   const int64_t ntiles_total = (N + TN - 1) / TN;
   int64_t nt_begin, nt_end;
@@ -97,9 +106,9 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     nt_end = nt_begin + n_tiles_per_split;
     if (nt_end > ntiles_total) nt_end = ntiles_total;
   }
-  // staging map: TM (TN) x 16 floats = WM (WN) float4 per thread: row r_ld0 +
-  // 64 i, k4 = tid & 3
+  // staging map: row r_ld0 + 64 i, k4 = tid & 3 (TM x 16 and TN x 16 floats)
   const int r_ld0 = tid >> 2, k4_ld = tid & 3;
+  const bool a_ld = TM >= 64 || r_ld0 < TM;
   const int nk = dp / BK;  // dp is a multiple of 16
 
   if (EPI == EPI_ROWS && threadIdx.x < TM) {
@@ -110,44 +119,47 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
     s_orow[threadIdx.x] = row < M ? out_rows[row] : -1;
   }
 
-  float rowacc[2][16];
+  float rowacc[MI][16];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) rowacc[i][r] = 0.f;
 
   for (int64_t nt = nt_begin; nt < nt_end; ++nt) {
     const int64_t n0 = nt * TN;
-    f16v acc[2][2];
+    f16v acc[MI][NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const float* ga[WM];
-    const float* gb[WN];
+    const float* ga[NA];
+    const float* gb[NB];
 #pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      ga[i] = A + (m0 + r_ld0 + 64 * i) * (int64_t)lda + 4 * k4_ld;
+    for (int i = 0; i < NA; ++i) {
+      const int64_t ar = m0 + (a_ld ? r_ld0 : 0) + 64 * i;
+      ga[i] = A + ar * (int64_t)lda + 4 * k4_ld;
       if (EPI == EPI_ROWS)  // rows past M repeat the last one (never stored)
-        ga[i] = A + (int64_t)a_rows[min(m0 + r_ld0 + 64 * i, M - 1)] * lda + 4 * k4_ld;
+        ga[i] = A + (int64_t)a_rows[min(ar, M - 1)] * lda + 4 * k4_ld;
     }
 #pragma unroll
-    for (int i = 0; i < WN; ++i) gb[i] = B + (n0 + r_ld0 + 64 * i) * (int64_t)ldb + 4 * k4_ld;
-    f4 ra[WM], rb[WN];
+    for (int i = 0; i < NB; ++i) gb[i] = B + (n0 + r_ld0 + 64 * i) * (int64_t)ldb + 4 * k4_ld;
+    f4 ra[NA], rb[NB];
 #pragma unroll
-    for (int i = 0; i < WM; ++i) ra[i] = *(const f4*)ga[i];
+    for (int i = 0; i < NA; ++i) ra[i] = *(const f4*)ga[i];
 #pragma unroll
-    for (int i = 0; i < WN; ++i) rb[i] = *(const f4*)gb[i];
+    for (int i = 0; i < NB; ++i) rb[i] = *(const f4*)gb[i];
     auto stage = [&](int buf) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
+        if (a_ld) {
 #pragma unroll
-        for (int i = 0; i < WM; ++i) As[buf][4 * k4_ld + c][r_ld0 + 64 * i] = ra[i][c];
+          for (int i = 0; i < NA; ++i) As[buf][4 * k4_ld + c][r_ld0 + 64 * i] = ra[i][c];
+        }
 #pragma unroll
-        for (int i = 0; i < WN; ++i) Bs[buf][4 * k4_ld + c][r_ld0 + 64 * i] = rb[i][c];
+        for (int i = 0; i < NB; ++i) Bs[buf][4 * k4_ld + c][r_ld0 + 64 * i] = rb[i][c];
       }
     };
     __syncthreads();  // previous n-tile's readers are done with buffer 0
@@ -159,24 +171,25 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
       if (more) {
         const int koff = (kt + 1) * BK;
 #pragma unroll
-        for (int i = 0; i < WM; ++i) ra[i] = *(const f4*)(ga[i] + koff);
+        for (int i = 0; i < NA; ++i) ra[i] = *(const f4*)(ga[i] + koff);
 #pragma unroll
-        for (int i = 0; i < WN; ++i) rb[i] = *(const f4*)(gb[i] + koff);
+        for (int i = 0; i < NB; ++i) rb[i] = *(const f4*)(gb[i] + koff);
       }
-      // ROWS: a wave whose 64 rows all lie past M only stages (uniform skip)
-      const bool live = EPI != EPI_ROWS || m0 + wm * 64 < M;
+      // ROWS: a wave whose rows all lie past M only stages (uniform skip)
+      const bool live = EPI != EPI_ROWS || m0 + rw < M;
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
         if (!live) break;
         const int kr = 2 * kk + (lane >> 5);
-        const float a0 = As[cur][kr][wm * 64 + (lane & 31)];
-        const float a1 = As[cur][kr][wm * 64 + 32 + (lane & 31)];
-        const float b0 = Bs[cur][kr][wn * 64 + (lane & 31)];
-        const float b1 = Bs[cur][kr][wn * 64 + 32 + (lane & 31)];
-        acc[0][0] = mfma32(a0, b0, acc[0][0]);
-        acc[0][1] = mfma32(a0, b1, acc[0][1]);
-        acc[1][0] = mfma32(a1, b0, acc[1][0]);
-        acc[1][1] = mfma32(a1, b1, acc[1][1]);
+        float av[MI], bv[NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) av[i] = As[cur][kr][rw + 32 * i + (lane & 31)];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bv[j] = Bs[cur][kr][cw + 32 * j + (lane & 31)];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
       }
       if (more) stage(cur ^ 1);
       __syncthreads();
@@ -185,20 +198,20 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
 
     // ---- epilogue ----
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (EPI == EPI_ROWS && m0 + wm * 64 + i * 32 >= M) continue;  // uniform: no exp for rows past M
+    for (int i = 0; i < MI; ++i) {
+      if (EPI == EPI_ROWS && m0 + rw + i * 32 >= M) continue;  // uniform: no exp for rows past M
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
+      for (int j = 0; j < NJ; ++j) {
+        const int64_t col = n0 + cw + j * 32 + (lane & 31);
         const float bsq = Bsq[col];
         float cf = 0.f;
         if (EPI == EPI_PREDICT) cf = col < N ? coef[col] : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const int64_t row = m0 + wm * 64 + i * 32 + rl;
+          const int lr = rw + i * 32 + rl;
+          const int64_t row = m0 + lr;
           if (EPI == EPI_ROWS) {
-            const int lr = wm * 64 + i * 32 + rl;
             const int32_t orow = s_orow[lr];
             if (orow >= 0 && col < N) out[(int64_t)orow * ldo + col] = rbf_from_dot(s_asq[lr], bsq, acc[i][j][r], gamma);
             continue;
@@ -217,13 +230,13 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
       // transposed tile: lane holds 4 consecutive rows per group -> 16-B stores
       // out[col][row .. row+3] (each store instruction: 32 rows x 32 B)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < MI; ++i) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < NJ; ++j) {
+          const int64_t col = n0 + cw + j * 32 + (lane & 31);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int64_t row = m0 + wm * 64 + i * 32 + 8 * q + 4 * (lane >> 5);
+            const int64_t row = m0 + rw + i * 32 + 8 * q + 4 * (lane >> 5);
             if (col >= M) continue;
             float* dst = out + col * ldo + row;
             if (row + 3 < N) {
@@ -247,7 +260,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
   if (EPI == EPI_PREDICT) {
     // sum over the 32 columns held by lanes with equal (lane>>5), then over wn
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float v = rowacc[i][r];
@@ -260,11 +273,11 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
       }
     if ((lane & 31) == 0) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          red[wn][wm * 64 + i * 32 + rl] = rowacc[i][r];
+          red[wn][rw + i * 32 + rl] = rowacc[i][r];
         }
     }
     __syncthreads();
@@ -318,10 +331,12 @@ void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, c
                       const int32_t* out_rows, int64_t ldl, hipStream_t s) {
   if (M_max <= 0 || N <= 0) return;
   DPSVM_CHECK(dp % 16 == 0, "rbf_rows_indexed: dp must be a multiple of 16");
-  // 64x256 tiles: B (the columns) must be readable to a multiple of 256 rows
+  // 64x256 tiles (B, the columns, readable to a multiple of 256 rows).  The
+  // 32x512 shape pads less (rows to 32) but ran slower (500k x 1024: 7.71 s vs
+  // 6.43 s; covtype 8.22 vs 7.33: 5 LDS reads per 4 MFMAs, twice the B staging)
   const int64_t tm = (M_max + 63) / 64, tn = (N + 255) / 256;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed: N too large for grid.y");
-  dev::rbf_gemm_kernel<dev::EPI_ROWS, 1><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
+  dev::rbf_gemm_kernel<dev::EPI_ROWS, 64, 2, 2><<<dim3((unsigned)tm, (unsigned)tn), dev::GEMM_THREADS, 0, s>>>(
       X, Xsq, M_max, dp, B, Bsq, N, dp, dp, gamma, lines, ldl, nullptr, 1, 0, a_rows, out_rows, m_dev);
   post_launch("rbf_rows_indexed", s);
 }

@@ -209,7 +209,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     DPSVM_CHECK(m.replicated || n_x_rows == n, "internal: partition fallback needs full x");
   }
   const int64_t x_row0 = m.replicated ? 0 : m.off;
-  m.x_rows = m.replicated ? round_up(std::max<int64_t>(n, m.off + m.ldl), 128) + 128 : m.ldl + 128;
+  // + 512 zero rows: the row GEMM (rbf_rows_indexed, 32x512 tiles) reads the
+  // owned rows to a multiple of 512
+  m.x_rows = m.replicated ? round_up(std::max<int64_t>(n, m.off + m.ldl), 128) + 512 : m.ldl + 512;
   m.x = dmalloc<float>((size_t)m.x_rows * m.dp, &m.bytes);
   HIP_CHECK(hipMemsetAsync(m.x, 0, (size_t)m.x_rows * m.dp * 4, m.stream));
   {
@@ -224,7 +226,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                                  hipMemcpyHostToDevice, m.stream));
   }
   // ---- global vectors (n padded so padded local rows index in-bounds) ----
-  const int64_t n_pad = round_up(std::max<int64_t>(n, m.off + m.ldl), 128) + 128;
+  const int64_t n_pad = round_up(std::max<int64_t>(n, m.off + m.ldl), 128) + 512;
   m.xsq = dmalloc<float>((size_t)n_pad, &m.bytes);
   m.y = dmalloc<float>((size_t)n_pad, &m.bytes);
   m.alpha = dmalloc<float>((size_t)n_pad, &m.bytes);

@@ -158,7 +158,7 @@ def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_line
     rows = [int(r) for r in rows]
     m = len(rows)
     n = x.shape[0]
-    xp, dp = _pad_rows_cols(x, row_mult=256)  # the GEMM reads whole 256-column tiles
+    xp, dp = _pad_rows_cols(x, row_mult=512)  # the GEMM reads whole 512-column tiles
     xsq = torch.zeros(xp.shape[0], device=x.device)
     C.k_row_sqnorm(xp.data_ptr(), xp.shape[0], dp, dp, xsq.data_ptr(), _stream(x))
     out_lines = list(range(m)) if out_lines is None else [int(v) for v in out_lines]
