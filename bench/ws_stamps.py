@@ -58,6 +58,9 @@ def main() -> int:
         "select_candidates_us": us(s[:, 7] - s[:, 10]),
         "select_end_to_gather_us": us(s[:, 1] - s[:, 7]),
         "merge_us": us(s[:, 2] - s[:, 1]),
+        "merge_phases_us": {"lists_and_stop_test": us(s[:, 11] - s[:, 1]), "radix_thresholds": us(s[:, 12] - s[:, 11]),
+                            "class_compaction": us(s[:, 13] - s[:, 12]), "hash_dedup": us(s[:, 14] - s[:, 13]),
+                            "previous_set": us(s[:, 2] - s[:, 14])},
         "gather_rows_us": us(s[:, 8] - s[:, 2]),
         "gather_end_to_solve_us": us(s[:, 0] - s[:, 8]),
         "load_subgram_us": us(s[:, 3] - s[:, 0]),

@@ -416,6 +416,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   uint64_t gu = lu[0], gl = ll[0];
   block_min2_u64<kWsGatherThreads>(gu, gl, s_scr);
   const float b_hi = key_value(gu), b_lo = -key_value(gl);
+  if (lead) WS_STAMP(11);
   const int64_t it0 = c->iter;
   int stop = kRunning;
   if (c->nonfinite) stop = kNonFinite;
@@ -483,6 +484,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
     if ((tid & 63) == 0) s_thr[sd] = b1 >= 0 && b2 >= 0 ? (b1 << 8) | b2 : 0xFFFF;  // too few: every row
   }
   __syncthreads();
+  if (lead) WS_STAMP(12);
   const uint32_t T[2] = {(uint32_t)s_thr[0], (uint32_t)s_thr[1]};
   const uint64_t gmin[2] = {gu, gl};
   // class counts per thread (the global extreme is placed first, separately)
@@ -521,6 +523,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   }
   __syncthreads();
 
+  if (lead) WS_STAMP(13);
   // ---- the new working set ----
   int32_t* hk_u = s_hash[0];
   int32_t* hv_u = s_hash[1];
@@ -563,6 +566,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
     if (c1) s_idx[s1] = ki[1];
   }
   __syncthreads();
+  if (lead) WS_STAMP(14);
   // the previous set (newest first): rows not chosen again, up to q_max
   bool pk = false;
   int32_t pidx = -1;
