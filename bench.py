@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--host-cache-lines", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cache-lines", type=int, default=0)
+    ap.add_argument("--clip", default="independent", choices=["independent", "box"],
+                    help="alpha clipping: the reference's independent clip (default) or the joint box")
     ap.add_argument("--cache-mb", type=float, default=0,
                     help="cap the kernel-row cache / resident Gram budget per rank (MiB; ranks sharing a device)")
     ap.add_argument("--x-mode", default="auto")
@@ -146,6 +148,7 @@ def main(argv=None) -> int:
 
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)
     cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines, cache_mb=a.cache_mb,
+                    clip=a.clip,
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
                     exchange=a.exchange, persist=a.persist, persist_block=a.persist_block, dp=a.dp,
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,

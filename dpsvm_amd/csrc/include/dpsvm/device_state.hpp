@@ -244,7 +244,8 @@ struct WsArgs {
   int32_t world;       // ranks (> 1: candidates all-gathered, the sub-Gram all-reduced)
   int32_t G_all;       // candidate lists the merge reads: world * G
   int32_t q_max, n_new, inner_max;
-  float rel_local;     // sub-problem tolerance: max(eps, rel_local * global gap / 2)
+  float rel_local;     // sub-problem tolerance: max(eps_floor, rel_local * global gap / 2)
+  float eps_floor;     // its floor (rel_local * eps: rounds near the end keep taking steps)
   float C, eps, tau;
   int32_t clip;
   int64_t max_iter;

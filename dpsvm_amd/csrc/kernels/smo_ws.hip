@@ -882,7 +882,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
 
   const float INF = __builtin_inff();
   const float C = a.C;
-  const float eps_in = fmaxf(a.eps, a.rel_local * 0.5f * (b_lo - b_hi));
+  const float eps_in = fmaxf(a.eps_floor, a.rel_local * 0.5f * (b_lo - b_hi));
   float fu[3], fl[3], yr[3], a0[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
