@@ -84,6 +84,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --solver S          :  auto (ws from 100k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
+               "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
@@ -102,7 +103,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
     OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL,
-    OPT_WSINNER, OPT_WSBLOCK
+    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -132,7 +133,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"watchdog", required_argument, 0, OPT_WDOG}, {"census-groups", required_argument, 0, OPT_CENSUS},
       {"no-verify-ranks", no_argument, 0, OPT_NOVR}, {"params-json", required_argument, 0, OPT_PJSON},
       {"solver", required_argument, 0, OPT_SOLVER}, {"ws-size", required_argument, 0, OPT_WSSIZE},
-      {"ws-new", required_argument, 0, OPT_WSNEW}, {"ws-rel", required_argument, 0, OPT_WSREL},
+      {"ws-new", required_argument, 0, OPT_WSNEW}, {"eta", required_argument, 0, OPT_ETA}, {"ws-rel", required_argument, 0, OPT_WSREL},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {0, 0, 0, 0}};
   while (true) {
@@ -233,6 +234,12 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_WSREL: o.p.ws_rel = (float)atof(optarg); break;
       case OPT_WSINNER: o.p.ws_inner = atoi(optarg); break;
       case OPT_WSBLOCK: o.p.ws_block = atoi(optarg); break;
+      case OPT_ETA: {
+        const std::string v = optarg;
+        if (v != "x" && v != "gram") usage_train(argv[0], seq);
+        o.p.eta = v == "gram" ? 1 : 0;
+        break;
+      }
       case OPT_PJSON: {
         FILE* fp = fopen(optarg, "r");
         if (!fp) {

@@ -120,6 +120,11 @@ struct SolverParams {
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_block = 32;          // rounds per hipGraph block
+  // eta's K(i_hi, i_lo) in the pair-at-a-time dense engines: 0 from the two X
+  // rows (explicit difference, the same tree in every engine: bit parity), 1
+  // from the resident Gram (persistent dense engine with every column local;
+  // one load in the Gram-row round trip instead of the X-row reads and a barrier)
+  int eta = 0;
 };
 
 

@@ -194,6 +194,7 @@ struct SmoArgs {
   // words [arrivals, abort])
   int32_t* census;
   int64_t census_ticks;
+  int32_t eta_gram;  // 1: K(i_hi, i_lo) from the resident Gram (every column local)
 };
 constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..16}, {key bits 15..0, alpha}
 

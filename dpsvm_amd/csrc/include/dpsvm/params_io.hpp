@@ -56,6 +56,7 @@ void for_each_param(SolverParams& p, F&& f) {
   f("ws_rel", p.ws_rel);
   f("ws_inner", p.ws_inner);
   f("ws_block", p.ws_block);
+  f("eta", p.eta);
 }
 
 inline std::string num(double v) {

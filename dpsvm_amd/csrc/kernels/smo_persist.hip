@@ -125,25 +125,33 @@ __global__ __launch_bounds__(kFusedThreads) void smo_persist_kernel(SmoArgs a, F
       klv[k] = line_lo[j];
     }
     const float y_hi = a.y[i_hi], y_lo = a.y[i_lo];  // read-only during the run
-    const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
-    const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
-    // wave 0 alone reads the two sample rows (one copy of their traffic per
-    // workgroup instead of four: with every workgroup on the same two rows the
-    // replicated loads delayed the slowest publisher) and shares |x_hi - x_lo|^2
-    // through LDS; the other waves' Gram-row loads are in flight meanwhile
-    if (wave == 0) {
-      const float d2 = wave_dist2(xh, xl, a.dp, lane);  // same tree as every other engine
-      if (lane == 0) d2_s = d2;
+    float k_hl;
+    if (a.eta_gram) {
+      // K(hi, lo) straight from the resident Gram (every column local): one
+      // more load of the same round trip, no sample-row reads, no barrier.
+      // The GEMM's |x|^2 expansion rounds differently from the explicit
+      // difference below, so the trajectory matches to tolerance, not bits.
+      k_hl = line_hi[i_lo - a.off];
+    } else {
+      const float* xh = a.x + ((int64_t)i_hi - a.x_row0) * a.dp;
+      const float* xl = a.x + ((int64_t)i_lo - a.x_row0) * a.dp;
+      // wave 0 alone reads the two sample rows (one copy of their traffic per
+      // workgroup instead of four: with every workgroup on the same two rows the
+      // replicated loads delayed the slowest publisher) and shares |x_hi - x_lo|^2
+      // through LDS; the other waves' Gram-row loads are in flight meanwhile
+      if (wave == 0) {
+        const float d2 = wave_dist2(xh, xl, a.dp, lane);  // same tree as every other engine
+        if (lane == 0) d2_s = d2;
+      }
+      __syncthreads();
+      k_hl = expf(-a.gamma * d2_s);
     }
-    __syncthreads();
-    const float dist2 = d2_s;
     const float a_hi_old = pk.ah, a_lo_old = pk.al;     // the owners' current values
     float c_hi = 0.f, c_lo = 0.f, a_hi_new = a_hi_old, a_lo_new = a_lo_old;
     const int iter = t + 1;
     if (!isfinite(bh) || !isfinite(bl)) {
       done = kNonFinite;
     } else {
-      const float k_hl = expf(-a.gamma * dist2);
       const PairUpdate u =
           pair_update(a_hi_old, a_lo_old, y_hi, y_lo, bh, bl, k_hl, a.C, a.tau, a.clip, i_hi == i_lo);
       a_hi_new = u.a_hi_new;

@@ -179,6 +179,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("xch_timeout_s", &SolverParams::xch_timeout_s)
       .def_readwrite("watchdog_s", &SolverParams::watchdog_s)
       .def_readwrite("census_groups", &SolverParams::census_groups)
+      .def_readwrite("eta", &SolverParams::eta)
       .def_readwrite("verify_ranks", &SolverParams::verify_ranks)
       .def_readwrite("dp_policy", &SolverParams::dp_policy)
       .def_readwrite("solver", &SolverParams::solver)

@@ -394,6 +394,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   a.stamps = nullptr;
   a.census = nullptr;
   a.census_ticks = 0;
+  a.eta_gram = (m.p.eta == 1 && m.dense && m.nl == n) ? 1 : 0;
   if (const char* sp = std::getenv("DPSVM_STAMPS")) {  // diagnostics only (bench/stamps_report.py)
     m.stamps_path = std::string(sp) + ".rank" + std::to_string(m.rank);
     const size_t cnt = (size_t)kStampRing * 2 * kStampSlots;

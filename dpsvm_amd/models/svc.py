@@ -111,6 +111,7 @@ class SVCConfig:
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_block: int = 32              # rounds per hipGraph block
+    eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -171,6 +172,7 @@ class SVCConfig:
         p.ws_rel = float(self.ws_rel)
         p.ws_inner = int(self.ws_inner)
         p.ws_block = int(self.ws_block)
+        p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         return p
 
     def device_kind(self) -> tuple[str, int]:

@@ -322,6 +322,34 @@ def test_persistent_engine_matches_fused(monkeypatch, block, rows):
     assert m.n_iter_ == 1000 and m.status_ == 2 and np.array_equal(m.alpha_, m_ref.alpha_)
 
 
+@pytest.mark.parametrize("clip", ["independent", "box"])
+def test_persistent_eta_from_gram_matches_to_tolerance(clip):
+    """eta="gram": the persistent dense engine takes K(hi, lo) from the resident
+    Gram instead of the two X rows (no sample-row reads, one barrier fewer).
+    The GEMM rounds K differently from the explicit difference, so the run is
+    pinned to the float64 oracle of the reference algorithm and to the default
+    engine at tolerance level, not bit for bit; ignored (default path) in cache mode."""
+    from ref_smo import decision, smo_reference
+    X, y = synthetic("blobs", n=2500, d=12, seed=41, sep=1.2)
+    C_, g = 2.0, 0.15
+    kw = dict(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", persist="on", xch_timeout_s=30.0)
+    ref = SVC(**kw).fit(X, y)
+    got = SVC(eta="gram", **kw).fit(X, y)
+    assert got.setup_info_["iteration"] == "persistent-dense" and got.converged_
+    assert abs(got.n_iter_ - ref.n_iter_) <= max(20, ref.n_iter_ // 20)
+    assert abs(got.b_ - ref.b_) < 2e-3
+    assert abs(got.n_support_ - ref.n_support_) <= max(3, ref.n_support_ // 50)
+    a_o, b_o, it_o = smo_reference(X, y, C=C_, gamma=g, eps=1e-3, clip=clip)
+    assert abs(got.n_iter_ - it_o) <= max(10, it_o // 20) and abs(got.b_ - b_o) < 5e-3
+    assert np.abs(got.alpha_ - a_o).max() < 5e-2 * C_
+    d_o = decision(X, y, a_o, b_o, g, X)
+    assert np.mean(np.sign(got.decision_function(X)) == np.sign(d_o)) > 0.995
+    # cache mode has no resident Gram: the flag changes nothing there
+    c0 = SVC(cache_lines=256, **kw).fit(X, y)
+    c1 = SVC(cache_lines=256, eta="gram", **kw).fit(X, y)
+    assert c0.n_iter_ == c1.n_iter_ and np.array_equal(c0.alpha_, c1.alpha_)
+
+
 @pytest.mark.parametrize("engine", ["fused", "persistent", "persistent-batches", "persistent-cache"])
 def test_peer_exchange_two_processes_one_gpu(tmp_path, engine):
     """Two ranks as two processes sharing the GPU (gloo bootstrap, IPC-mapped
