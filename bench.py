@@ -79,9 +79,11 @@ def parse(argv=None):
     ap.add_argument("--persist", default="auto", choices=["auto", "off", "on"],
                     help="iteration engine: persistent kernel (auto/on; dense and cache mode) or one launch per iteration (off)")
     ap.add_argument("--persist-block", type=int, default=2048)
-    ap.add_argument("--dp", default="auto", choices=["auto", "shard", "replicate"],
+    ap.add_argument("--dp", default="auto", choices=["auto", "shard", "replicate", "measure"],
                     help="data parallelism at N > 1: shard the rows, or every rank solves the whole problem "
-                         "(auto: replicate when the whole Gram fits one GPU, docs/DESIGN.md)")
+                         "(auto: replicate when the whole Gram fits one GPU, docs/DESIGN.md — then both "
+                         "policies are timed once on this node and the timed runs use the faster; measure: "
+                         "that measured choice whatever the shape-based policy says)")
     ap.add_argument("--shard-check", default="auto", choices=["auto", "off"],
                     help="N > 1 with a replicated timed solve: one untimed sharded solve first (cross-device "
                          "exchange evidence: its time, iterations and b go into the JSON line)")
@@ -152,7 +154,8 @@ def main(argv=None) -> int:
     cfg = SVCConfig(C=a.C, gamma=a.gamma, eps=a.eps, max_iter=a.max_iter, cache_lines=a.cache_lines, cache_mb=a.cache_mb,
                     clip=a.clip,
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
-                    exchange=a.exchange, persist=a.persist, persist_block=a.persist_block, dp=a.dp,
+                    exchange=a.exchange, persist=a.persist, persist_block=a.persist_block,
+                    dp="replicate" if a.dp == "measure" else a.dp,
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
                     xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
                     ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, eta=a.eta,
@@ -197,25 +200,37 @@ def main(argv=None) -> int:
         info = {"device_name": "cpu", "x_replicated": True, "cache_lines": 0}
         run = lambda: C.solve_cpu(X, y, params, comm if n_ranks > 1 else None)  # noqa: E731
 
+    def timed_once(fn):
+        """one solve bracketed by barrier + device sync; the max over ranks"""
+        sync()
+        barrier()
+        t_s = time.perf_counter()
+        r = fn()
+        sync()
+        barrier()
+        tt = torch.tensor([time.perf_counter() - t_s], dtype=torch.float64)
+        if n_ranks > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)  # host (gloo) group: every rank sees the same value
+        return float(tt[0]), r
+
     shard_check = None
+    dp_choice = None
+    s_solver = s_comm = None
     if on_gpu and n_ranks > 1 and info.get("dp_policy") == "replicate" and a.shard_check == "auto":
-        # the timed solve replicates (every rank solves it all); prove the
-        # sharded, cross-device path on this node too: one untimed solve
+        # the replicated policy (every rank solves it all) was chosen from the
+        # problem's shape; prove the sharded, cross-device path on this node too
+        # (one untimed solve), and with --dp auto MEASURE both policies: the
+        # timed runs use the faster one on this node (the choice is made from
+        # max-over-ranks times, identical on every rank)
         sp = cfg.to_native(X.shape[1])
         sp.dp_policy = 1
         sp.watchdog_s = 120.0  # a stuck collective aborts ITS communicator and fails this check only
-        s_comm = None
         try:
             s_comm = make_comm(ctx, comm.name if comm.name in ("rccl", "gloo") else "auto")
             s_solver = C.GpuSolver(sp, s_comm, ctx.local_rank)
             s_info = s_solver.setup(X, X.shape[0], y)
-            sync()
-            barrier()
-            t_s = time.perf_counter()
-            s_alpha, s_res = s_solver.solve()
-            sync()
-            barrier()
-            shard_check = {"s": round(time.perf_counter() - t_s, 6), "iterations": int(s_res["iters"]),
+            t_first, (s_alpha, s_res) = timed_once(s_solver.solve)
+            shard_check = {"s": round(t_first, 6), "iterations": int(s_res["iters"]),
                            "b": s_res["b"], "smo_loop_s": round(float(s_res["t_solve"]), 6),
                            "gram_gemm_s": round(float(s_res.get("t_gram", 0.0)), 6),
                            "engine": s_info.get("iteration"), "exchange": s_info.get("exchange"),
@@ -223,12 +238,26 @@ def main(argv=None) -> int:
                            "geometry": f"{s_info.get('rows_per_group')}x{s_info.get('groups')}",
                            "us_per_iter": round(1e6 * float(s_res["t_solve"]) / max(1, int(s_res["iters"])), 3),
                            "verified": True}
-            del s_solver, s_alpha
+            del s_alpha
+            if a.dp in ("auto", "measure"):
+                t_shard, _ = timed_once(s_solver.solve)  # warm (graphs instantiated)
+                for _ in range(max(1, a.warmup)):
+                    run()
+                t_repl, _ = timed_once(run)
+                use_shard = t_shard < 0.97 * t_repl
+                dp_choice = {"replicate_s": round(t_repl, 6), "shard_s": round(t_shard, 6),
+                             "chosen": "shard" if use_shard else "replicate"}
+                if use_shard:
+                    solver, info = s_solver, s_info
+                    run = lambda: solver.solve()  # noqa: E731
+                    comm = s_comm
         except Exception as e:  # noqa: BLE001  (the digest inside solve() fails on every rank alike)
             shard_check = {"error": str(e)[:300]}
             if ctx.rank == 0:
                 print(f"[bench] sharded check failed: {e}", file=sys.stderr)
-        del s_comm
+        if dp_choice is None or dp_choice["chosen"] != "shard":
+            s_solver = None
+            s_comm = None
 
 
     for _ in range(a.warmup):
@@ -333,6 +362,7 @@ def main(argv=None) -> int:
             "census": info.get("census", "n/a"),
             "engine_note": info.get("engine_note", ""),
             "shard_check": shard_check,
+            "dp_autotune": dp_choice,
             "reference_check": ref_check,
             "params": json.loads(params.to_json()),
             "preset": a.config,

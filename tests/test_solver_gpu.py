@@ -482,7 +482,10 @@ def test_bench_multi_gpu_auto_policy_replicates_and_checks_shards(tmp_path):
     world = min(_NDEV, 8)
     out = _bench_multi(root, world, ["--solver", "smo"], 29651)
     ref = _ref_8000()
-    assert out["dp_policy"] == "replicate" and out["iterations"] == ref.n_iter_ and out["b"] == ref.b_
+    # the timed runs use whichever policy measured faster on this node; the
+    # pair-at-a-time engine is bit-identical to one GPU either way
+    assert out["dp_autotune"]["chosen"] == out["dp_policy"]
+    assert out["iterations"] == ref.n_iter_ and out["b"] == ref.b_
     sc = out["shard_check"]
     assert sc and "error" not in sc, sc
     assert sc["exchange"] == "peer" and sc["iterations"] == ref.n_iter_ and sc["b"] == ref.b_
@@ -502,10 +505,36 @@ def test_bench_multi_gpu_ws_sharded_and_default(tmp_path):
     assert abs(out["b"] - ref.b_) < 1e-3 and abs(out["n_sv"] - ref.n_support_) <= 8
     if _NDEV >= 2:
         dflt = _bench_multi(root, world, [], 29671)
-        assert dflt["dp_policy"] == "replicate" and dflt["iterations"] == ref.n_iter_ and dflt["b"] == ref.b_
+        assert dflt["dp_autotune"]["chosen"] == dflt["dp_policy"]
+        if dflt["dp_policy"] == "replicate":
+            assert dflt["iterations"] == ref.n_iter_ and dflt["b"] == ref.b_
+        assert abs(dflt["b"] - ref.b_) < 1e-3
         sc = dflt["shard_check"]
         assert sc and "error" not in sc and sc["engine"] == "ws-dense", sc
         assert abs(sc["b"] - ref.b_) < 1e-3
+
+
+def test_bench_two_processes_measured_dp_policy(tmp_path):
+    """--dp measure (the default's measured choice, forced on shared-GPU
+    rehearsal ranks): the replicated solve and one sharded solve are both timed
+    (max over ranks, identical on every rank), the timed runs use the faster,
+    and the JSON line records both times and the choice."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29615", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--samples", "6000", "--steps", "1", "--warmup", "1", "--comm", "gloo", "--dp", "measure",
+           "--no-accuracy", "--reference-check", "off"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.split("\n") if l.startswith("{")][-1])
+    at, sc = out["dp_autotune"], out["shard_check"]
+    assert sc and "error" not in sc, sc
+    assert at and at["chosen"] in ("shard", "replicate") and at["replicate_s"] > 0 and at["shard_s"] > 0
+    assert out["dp_policy"] == at["chosen"] and out["converged"] and out["n_gpus"] == 2
+    assert abs(sc["b"] - out["b"]) < 1e-3
 
 
 @pytest.mark.skipif(_NDEV < 2, reason="needs >= 2 GPUs (svmTrain -p N: one thread per device)")
