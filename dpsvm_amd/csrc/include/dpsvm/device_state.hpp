@@ -262,7 +262,20 @@ struct WsArgs {
   WsCtrl* ctrl;
   SmoStatus* status;   // host-mapped
   uint64_t* stamps;    // DPSVM_STAMPS diagnostics: s_memrealtime per phase, ring of kStampRing rounds
+  // in-kernel peer exchange of the rounds (world > 1; nullptr: the communicator's
+  // collectives).  Every rank's receive buffer (uncached, IPC-mapped by its
+  // peers; smo_ws.hip "peer exchange"): [2 parity][G_all][2 kWsCand][2] candidate
+  // granules, then from word xsub [2 parity][q_max][q_max + 1] sub-Gram rows with
+  // the row's f in the last column
+  uint64_t* const* xpeer;
+  int32_t xrank;
+  int64_t xsub;
+  int64_t xtimeout_ticks;  // give-up bound of one poll (s_memrealtime, 100 MHz)
 };
+// u64 words of the working-set exchange region (both parities)
+constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {
+  return 2 * G_all * 4 * kWsCand + 2 * q_max * (q_max + 1);
+}
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;
 

@@ -34,6 +34,7 @@
 #include "dpsvm/device_state.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
+#include "xch.hpp"
 #include "../runtime/hip_check.hpp"
 
 namespace dpsvm {
@@ -220,6 +221,44 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
 }
 
 // ---------------------------------------------------------------------------
+// Peer exchange of the rounds (world > 1 with a.xpeer: replaces the candidate
+// all-gather and the sub-Gram sum all-reduce, so a round has no collective
+// launch and no host step).  Round R = c->outer uses parity R & 1 and granule
+// tag xtag(R + 1) (xch.hpp: 16-bit tag << 48 | 48-bit payload, one aligned
+// 8-byte system-scope store — never torn, the data is the flag).  Producers:
+// each ws_select workgroup stores its 2 x kWsCand keys (two granules each: bits
+// 63..16, 15..0) into slot rank * G + b of EVERY rank's buffer; gather workgroup
+// a stores the sub-Gram entries (a, b) of the columns b its rank owns, and the
+// row's f when it owns row a, into row a of every rank's buffer.  Consumers
+// poll their own buffer: every merge workgroup the G_all candidate slots,
+// gather workgroup a its row a.  Every entry has exactly one producer, so the
+// assembled values are the owners' bits (== the sum all-reduce's x + 0 + ...).
+// A parity-(R & 1) slot is rewritten (round R + 2) only after every rank
+// finished round R + 1's merge, which on each rank follows its round-R reads in
+// stream order: no slot is lapped.  Buffers are zeroed before each solve (a tag
+// is never 0).  A poll gives up after a.xtimeout_ticks: the run then ends with
+// kCommFail on this rank, and its peers time out the same way.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t ws_xcand(const WsArgs& a, int par, int slot) {
+  return ((int64_t)par * a.G_all + slot) * (4 * kWsCand);
+}
+
+__device__ __forceinline__ int64_t ws_xrow(const WsArgs& a, int par, int row) {
+  return a.xsub + ((int64_t)par * a.q_max + row) * (a.q_max + 1);
+}
+
+__device__ __forceinline__ bool ws_tag_ok(uint64_t g, uint64_t t) { return (g >> 48) == (t >> 48); }
+
+// a poll gave up: the run stops here (any workgroup may call it; same values)
+__device__ __forceinline__ void ws_comm_fail(const WsArgs& a, WsCtrl* c) {
+  if (threadIdx.x == 0) {
+    c->done = kCommFail;
+    c->n_apply = 0;  // nothing of this round is applied
+    ws_status(a.status, c);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // ws_select: f update of the last round + per-workgroup candidates
 // ---------------------------------------------------------------------------
 // Threads of a workgroup: 256 rows (x RPT) times PARTS partitions of the
@@ -359,14 +398,28 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
     uint64_t eu = lane < W * kWsCand ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
     uint64_t el = lane < W * kWsCand ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
     uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
+    uint64_t pu[kWsCand], pl[kWsCand];  // uniform: every lane holds the lists
     for (int round = 0; round < kWsCand; ++round) {
       const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
       if (lane == 0) {
         out[round] = mu;
         out[kWsCand + round] = ml;
       }
+      pu[round] = mu;
+      pl[round] = ml;
       if (eu == mu) eu = kKeyNone;
       if (el == ml) el = kKeyNone;
+    }
+    if (a.xpeer != nullptr && lane < a.world) {  // lane p publishes to rank p
+      uint64_t* dst = a.xpeer[lane] + ws_xcand(a, (int)(c->outer & 1), a.xrank * a.G + blockIdx.x);
+      const uint64_t t = xtag((uint32_t)c->outer + 1u);
+#pragma unroll
+      for (int r = 0; r < kWsCand; ++r) {
+        xch_store<true>(dst + 2 * r, t | (pu[r] >> 16));
+        xch_store<true>(dst + 2 * r + 1, t | (pu[r] & 0xffffull));
+        xch_store<true>(dst + 2 * kWsCand + 2 * r, t | (pl[r] >> 16));
+        xch_store<true>(dst + 2 * kWsCand + 2 * r + 1, t | (pl[r] & 0xffffull));
+      }
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(7);
@@ -407,10 +460,46 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
 
   // ---- every candidate list in registers (one load batch) ----
   uint64_t lu[kWsCand], ll[kWsCand];
+  if (a.xpeer == nullptr) {
 #pragma unroll
-  for (int r = 0; r < kWsCand; ++r) {
-    lu[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + r] : kKeyNone;
-    ll[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + kWsCand + r] : kKeyNone;
+    for (int r = 0; r < kWsCand; ++r) {
+      lu[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + r] : kKeyNone;
+      ll[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + kWsCand + r] : kKeyNone;
+    }
+  } else {
+    // peer exchange: thread tid polls slot tid of this rank's buffer
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kWsCand; ++r) lu[r] = ll[r] = kKeyNone;
+    if (tid < G) {
+      const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, tid);
+      const uint64_t t = xtag((uint32_t)r_now + 1u);
+      uint64_t g[4 * kWsCand];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {
+#pragma unroll
+        for (int i = 0; i < 4 * kWsCand; ++i) g[i] = xch_load<true>(e + i);
+        bool all = true;
+#pragma unroll
+        for (int i = 0; i < 4 * kWsCand; ++i) all &= ws_tag_ok(g[i], t);
+        if (all) break;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      constexpr uint64_t m48 = (1ull << 48) - 1;
+#pragma unroll
+      for (int r = 0; r < kWsCand; ++r) {
+        lu[r] = ((g[2 * r] & m48) << 16) | (g[2 * r + 1] & 0xffffull);
+        ll[r] = ((g[2 * kWsCand + 2 * r] & m48) << 16) | (g[2 * kWsCand + 2 * r + 1] & 0xffffull);
+      }
+    }
+    if (!__syncthreads_and(ok)) {
+      ws_comm_fail(a, c);
+      return false;
+    }
   }
   // ---- global minima (stop test) ----
   uint64_t gu = lu[0], gl = ll[0];
@@ -592,7 +681,8 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
 // the f) of rows it owns and zeros the rest, so at world > 1 one sum all-reduce
 // assembles the exact matrix (each entry has exactly one owner).  Rows ra >= q
 // are zeroed.
-__device__ __forceinline__ void ws_gather_row(const WsArgs& a, const int32_t* s_idx, int q, int ra, const float* line) {
+__device__ __forceinline__ void ws_gather_row(const WsArgs& a, WsCtrl* c, const int32_t* s_idx, int q, int ra,
+                                              const float* line) {
   const int tid = threadIdx.x;
   float* dst = a.subg + (size_t)ra * a.q_max;
   if (ra >= q) {
@@ -601,6 +691,52 @@ __device__ __forceinline__ void ws_gather_row(const WsArgs& a, const int32_t* s_
     return;
   }
   const int64_t lo = a.off, hi = a.off + a.nl;
+  if (a.xpeer != nullptr) {
+    // peer exchange: push the owned entries of row ra (+ its f) to every rank,
+    // then poll this rank's copy of the row (q_max <= 192 < 256: one column per
+    // thread, the last thread takes f)
+    const int64_t R = c->outer;
+    const uint64_t t = xtag((uint32_t)R + 1u);
+    const int64_t row = ws_xrow(a, (int)(R & 1), ra);
+    constexpr int kF = kWsGatherThreads - 1;
+    const int64_t gi = s_idx[ra];
+    if (tid < q) {
+      const int64_t gj = s_idx[tid];
+      if (gj >= lo && gj < hi) {
+        const uint64_t v = t | __float_as_uint(line[gj - lo]);
+        for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + tid, v);
+      }
+    } else if (tid == kF && gi >= lo && gi < hi) {
+      const uint64_t v = t | __float_as_uint(a.f[gi - lo]);
+      for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + a.q_max, v);
+    }
+    bool ok = true;
+    const int col = tid < q ? tid : tid == kF ? a.q_max : -1;
+    if (col >= 0) {
+      const uint64_t* g = a.xpeer[a.xrank] + row + col;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t v = xch_load<true>(g);
+      while (!ws_tag_ok(v, t)) {
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = xch_load<true>(g);
+      }
+      const float fv = __uint_as_float((uint32_t)v);
+      if (tid == kF) a.aux[ra] = fv;
+      else dst[tid] = fv;
+    } else if (tid < a.q_max) {
+      dst[tid] = 0.f;
+    }
+    if (tid == 0) {
+      a.aux[kWsMax + ra] = a.alpha[gi];
+      a.aux[2 * kWsMax + ra] = a.y[gi];
+    }
+    if (!__syncthreads_and(ok)) ws_comm_fail(a, c);
+    return;
+  }
   for (int b = tid; b < a.q_max; b += kWsGatherThreads) {
     const int64_t gj = b < q ? (int64_t)s_idx[b] : -1;
     dst[b] = gj >= lo && gj < hi ? line[gj - lo] : 0.f;
@@ -640,7 +776,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
       c->b_lo = b_lo;
     }
   }
-  ws_gather_row(a, s_idx, q, blockIdx.x, blockIdx.x < q ? a.gram + (int64_t)s_idx[blockIdx.x] * a.ldg : nullptr);
+  ws_gather_row(a, c, s_idx, q, blockIdx.x, blockIdx.x < q ? a.gram + (int64_t)s_idx[blockIdx.x] * a.ldg : nullptr);
   if (lead) WS_STAMP(8);
 }
 
@@ -735,12 +871,12 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
   const int q = c->q[par];
   const int ra = blockIdx.x;
   if (ra >= q) {
-    ws_gather_row(a, s_idx, q, ra, nullptr);
+    ws_gather_row(a, c, s_idx, q, ra, nullptr);
     return;
   }
   for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][t];
   __syncthreads();
-  ws_gather_row(a, s_idx, q, ra, a.gram + (int64_t)c->line[par][ra] * a.ldg);
+  ws_gather_row(a, c, s_idx, q, ra, a.gram + (int64_t)c->line[par][ra] * a.ldg);
   if (tid == 0 && ra == 0) WS_STAMP(8);
 }
 

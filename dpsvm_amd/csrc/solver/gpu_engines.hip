@@ -293,7 +293,7 @@ struct FusedCache final : Engine {
 // communicators (RCCL) enqueue on the stream and are captured in the round
 // graph; host communicators stage through host memory.
 void ws_allgather_cand(GpuSolver::Impl& m) {
-  if (!m.collectives()) return;
+  if (!m.collectives() || m.wsa.xpeer) return;  // peer exchange: pushed by ws_select itself
   const size_t bytes = (size_t)m.wsa.G * 2 * kWsCand * sizeof(uint64_t);
   if (m.comm->device_memory()) {
     m.comm->allgather(m.wsa.cand_out, m.wsa.cand, bytes, m.stream);  // in place: cand_out = cand + rank * bytes
@@ -308,7 +308,7 @@ void ws_allgather_cand(GpuSolver::Impl& m) {
 }
 
 void ws_allreduce_sub(GpuSolver::Impl& m) {
-  if (!m.collectives()) return;
+  if (!m.collectives() || m.wsa.xpeer) return;  // peer exchange: assembled by the gather kernel
   const size_t count = (size_t)m.wsa.q_max * m.wsa.q_max + kWsMax;  // sub-Gram + the members' f
   if (m.comm->device_memory()) {
     m.comm->allreduce_sum_f32(m.wssub, count, m.stream);
@@ -337,7 +337,9 @@ void ws_allreduce_rows(GpuSolver::Impl& m) {
 }
 
 bool ws_graphs(GpuSolver::Impl& m) {
-  return m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
+  // host communicators stage through host memory: no graph, unless the rounds
+  // need no collective at all (peer exchange)
+  return m.p.use_graph && (m.device_comm() || !m.ws_round_collectives()) && !m.p.sync_debug && !sync_debug_env();
 }
 
 // Working-set rounds on the resident Gram (smo_ws.hip).  Seed: the Gram GEMM,

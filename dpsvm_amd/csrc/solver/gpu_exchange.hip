@@ -72,7 +72,7 @@ bool GpuSolver::Impl::all_agree(bool mine, Communicator* c, int w) {
 // allocation fails at world > 1 the exchange is refused (every rank falls back
 // to the communicator's all-reduce) unless coarse memory was asked for
 // explicitly (xch_mem = 2, A/B runs on one device).
-bool GpuSolver::Impl::setup_exchange() {
+bool GpuSolver::Impl::setup_exchange(int64_t region_words) {
   struct alignas(16) XInfo {
     int64_t pid, device, ok;
     uint64_t ptr;
@@ -84,7 +84,7 @@ bool GpuSolver::Impl::setup_exchange() {
   me.ok = 1;
   const int64_t ping_words = 64;
   xstride = std::max<int64_t>(kXchGranules, p.xch_stride);
-  xregion = (int64_t)2 * world * Gf * xstride;
+  xregion = region_words > 0 ? region_words : (int64_t)2 * world * Gf * xstride;
   try {
     DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
     launch::preload_fused_kernels(stream);

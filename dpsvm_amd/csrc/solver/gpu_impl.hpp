@@ -125,6 +125,12 @@ struct GpuSolver::Impl {
   bool fused() const { return kind != EngineKind::Chain; }
   bool persistent() const { return kind == EngineKind::PersistDense || kind == EngineKind::PersistCache; }
   bool working_set() const { return kind == EngineKind::WsDense || kind == EngineKind::WsCache; }
+  // a working-set round still runs communicator collectives (candidates and
+  // sub-Gram travel through the in-kernel peer exchange when it is set up;
+  // partitioned-X ws-cache always sums its packed miss rows)
+  bool ws_round_collectives() const {
+    return collectives() && (wsa.xpeer == nullptr || (kind == EngineKind::WsCache && !replicated));
+  }
   // device addresses inside the working-set control record (cache mode GEMM operands)
   int32_t* wsctrl_miss_row() const { return wsctrl ? wsctrl->miss_row : nullptr; }
   int32_t* wsctrl_miss_line() const { return wsctrl ? wsctrl->miss_line : nullptr; }
@@ -140,7 +146,8 @@ struct GpuSolver::Impl {
   void allgather_bytes(const void* send, void* recv, size_t bytes);  // host buffers
   // every rank of `c` agrees: true only if `mine` is true everywhere
   bool all_agree(bool mine, Communicator* c, int w);
-  bool setup_exchange();
+  // region_words: u64 words of the exchange region (0: the SMO engines' key parities)
+  bool setup_exchange(int64_t region_words = 0);
   // residency census of the chosen persistent engine (collective: agreed)
   bool census(EngineKind k);
 

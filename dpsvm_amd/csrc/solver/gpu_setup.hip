@@ -430,7 +430,20 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.xch = false;
   const bool want_xch = (!ws_cand && !wsc_cand && m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) ||
                         pdense_cand || plru_cand;
-  if (want_xch) {
+  // working-set engines at world > 1: the rounds' candidate lists and sub-Gram
+  // rows through the same kind of receive buffers (smo_ws.hip, "peer exchange")
+  const bool wsc_fits_pre = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
+  const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives &&
+                           (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
+  int32_t ws_G = 0, ws_rpt = 0;
+  if (ws_cand || wsc_cand) launch::ws_geometry(nl_max, m.world, &ws_G, &ws_rpt);
+  if (want_ws_xch) {
+    const bool ok = m.setup_exchange(ws_xch_words((int64_t)ws_G * m.world, ws_q));
+    DPSVM_CHECK(ok || m.p.exchange != 2,
+                "peer exchange requested (exchange=peer) but its self test failed (" + m.xch_diag + ")");
+    if (ok) m.xch = true;
+    else m.info.engine_note = "peer exchange refused: " + m.xch_diag + " (working-set rounds use the collectives)";
+  } else if (want_xch) {
     const bool ok = m.setup_exchange();
     DPSVM_CHECK(ok || (m.p.exchange != 2 && m.p.persist != 2),
                 "peer exchange requested (exchange=peer / persist=on) but its self test failed (" + m.xch_diag + ")");
@@ -492,7 +505,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.n = n;
     w.nl = m.nl;
     w.off = m.off;
-    launch::ws_geometry(nl_max, m.world, &w.G, &w.rpt);
+    w.G = ws_G;
+    w.rpt = ws_rpt;
     w.world = m.world;
     w.G_all = w.G * m.world;
     w.q_max = ws_q;
@@ -526,6 +540,12 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.ctrl = m.wsctrl;
     w.status = m.status_d;
     w.stamps = m.stamps;
+    if (m.xch) {
+      w.xpeer = m.xpeer_d;
+      w.xrank = m.rank;
+      w.xsub = 2 * (int64_t)w.G_all * 4 * kWsCand;
+      w.xtimeout_ticks = (int64_t)(std::max(1e-6, m.p.xch_timeout_s) * 1e8);
+    }
     if (w.cache && !m.replicated) {
       m.wsxq = dmalloc<float>((size_t)ws_q * m.dp, &m.bytes);
       m.wsxqsq = dmalloc<float>((size_t)ws_q, &m.bytes);
@@ -543,7 +563,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                           : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
   m.info.rows_per_group = m.working_set() ? (int64_t)m.wsa.rpt * kWsSelThreads : m.fused() ? m.RBf : kStepRows;
   m.info.groups = m.working_set() ? m.wsa.G : m.fused() ? m.Gf : m.G;
-  m.info.poll_batch = m.xch ? launch::poll_batch(a) : 0;
+  m.info.poll_batch = m.xch && !m.working_set() ? launch::poll_batch(a) : 0;
   m.info.bytes_device = m.bytes;
   return m.info;
 }

@@ -19,12 +19,19 @@ def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
     comm = make_comm(ctx, "gloo")
     X, y = synthetic("covtype", n=n, seed=2)
     extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
+    if engine.startswith("ws"):  # working-set rounds, rows sharded (candidates + sub-Gram rows in-kernel)
+        extra = {"solver": "ws", "dp": "shard"}
+        if engine == "ws-cache":
+            extra.update(force_cache=True, cache_lines=1500)
+    else:
+        extra.update(persist="off" if engine == "fused" else "on", persist_block=257)
     extra.update(json.loads(extra_json))  # SVCConfig knobs (geometry, poll batch, ...)
-    clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer",
-              persist="off" if engine == "fused" else "on", persist_block=257, xch_timeout_s=30.0, **extra).fit(X, y, comm=comm)
+    clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer", xch_timeout_s=30.0,
+              **extra).fit(X, y, comm=comm)
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
            "exchange_mem": clf.setup_info_["exchange_mem"],
-           "iters": int(clf.n_iter_), "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
+           "iters": int(clf.n_iter_), "rounds": int(getattr(clf, "n_rounds_", 0) or 0), "b": float(clf.b_),
+           "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
     with open(f"{out}.rank{ctx.rank}.json", "w") as f:
         json.dump(rec, f)
     del comm

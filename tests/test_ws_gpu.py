@@ -280,3 +280,67 @@ def test_svmtrain_cli_ws_simulated_ranks_partitioned(tmp_path, bin_dir):
     one, three = outs[1], outs[3]
     assert one["engine"] == "ws-dense" and three["engine"] == "ws-dense" and three["world"] == 3
     assert abs(one["b"] - three["b"]) < 1e-2 and abs(one["n_sv"] - three["n_sv"]) <= 40
+
+
+@pytest.mark.parametrize("extra", [{}, {"force_cache": True, "cache_lines": 1500}])
+def test_ws_peer_exchange_loopback_bit_identical(extra):
+    """exchange="peer" at world 1: the rounds' candidate lists and sub-Gram rows
+    go through the in-kernel exchange (pushed to the own receive buffer, polled
+    back) — the same values as the direct path, so the same trajectory bit for bit."""
+    X, y = synthetic("mnist", n=4000, seed=3)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws", xch_timeout_s=30.0, **extra)
+    ref = SVC(**kw).fit(X, y)
+    got = SVC(exchange="peer", **kw).fit(X, y)
+    assert got.setup_info_["exchange"] == "loopback" and ref.setup_info_["exchange"] == "none"
+    assert got.setup_info_["iteration"] == ref.setup_info_["iteration"]
+    assert got.n_iter_ == ref.n_iter_ and got.n_rounds_ == ref.n_rounds_
+    assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
+
+
+@pytest.mark.parametrize("world,engine", [(2, "ws"), (4, "ws"), (2, "ws-cache")])
+def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine):
+    """Sharded working-set rounds with ranks as processes sharing the GPU (gloo
+    bootstrap, IPC-mapped uncached receive buffers): no collective per round —
+    each selection workgroup pushes its candidate lists to every rank, each
+    gather workgroup the sub-Gram entries its rank owns.  Every rank ends with
+    the same alphas (cross-rank digest, on by default), bit-identical to the
+    same rank count over host-staged collectives (thread ranks).  Four ranks
+    sharing one GPU run q = 64: gather workgroups of three ranks spinning on one
+    device must leave CUs (LDS) free for the fourth rank's solve workgroup —
+    on distinct GPUs each device runs only its own rank's kernels."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from dpsvm_amd._native import load
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 6000
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
+    out = tmp_path / f"ws{world}"
+    port = 29680 + world + (10 if engine == "ws-cache" else 0)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n),
+           json.dumps({"ws_size": 64} if world > 2 else {})]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    errs = "".join(open(f"{out}.rank{k}.err").read()[-1500:] for k in range(world)
+                   if os.path.exists(f"{out}.rank{k}.err"))
+    assert r.returncode == 0, errs + r.stderr[-2000:]
+    res = [json.load(open(f"{out}.rank{k}.json")) for k in range(world)]
+    X, y = synthetic("covtype", n=n, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", solver="ws", dp="shard")
+    if engine == "ws-cache":
+        kw.update(force_cache=True, cache_lines=1500)
+    if world > 2:
+        kw.update(ws_size=64)
+    ref = _fit_threads(load(), world, X, y, **kw)
+    sha = hashlib.sha256(ref[0].alpha_.tobytes()).hexdigest()
+    for k in range(world):
+        assert res[k]["exchange"] == "peer" and res[k]["exchange_mem"] == "uncached"
+        assert res[k]["iteration"] == ("ws-cache" if engine == "ws-cache" else "ws-dense")
+        assert ref[k].setup_info_["exchange"] == "allreduce"
+        assert res[k]["iters"] == ref[0].n_iter_ and res[k]["rounds"] == ref[0].n_rounds_
+        assert res[k]["alpha_sha"] == sha
