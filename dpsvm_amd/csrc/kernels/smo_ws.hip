@@ -888,23 +888,34 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
 // (svmTrain.cu:56-91) as mask logic on uniform operands, then the owner lane's
 // slot registers take the new fu / fl by selects.  No branch (every branch of a
 // one-wave loop is a fetch bubble) and no per-lane recomputation.
+// per lane: the lanes set in the (uniform) mask m take b, the others keep a
+__device__ __forceinline__ float sel_lanes(float a, float b, uint64_t m) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+
 __device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, int lane, float C, float (&fu)[3],
                                          float (&fl)[3]) {
   const float INF = __builtin_inff();
   // the operands are uniform: each test as a wave mask (all ones or zero; wave
   // 0 runs with a full exec mask) keeps the set logic on the scalar unit
   // instead of 0/1 VGPRs (~20 VALU per placement)
-  const uint64_t fr = __ballot(an > 0.f) & __ballot(an < C), z = __ballot(an == 0.f), cc = __ballot(an == C),
-                 py = __ballot(yv > 0.f);
-  const float nu = ((fr | (z & py) | (cc & ~py)) != 0) ? fp : INF;
-  const float nl = ((fr | (z & ~py) | (cc & py)) != 0) ? -fp : INF;
-  const bool me = lane == (pos & 63);
+  // with alpha in [0, C] (clipped), in_up(a, y) == (y > 0 ? a < C : a > 0) and
+  // in_low(a, y) == (y > 0 ? a > 0 : a < C) (common.hpp): three compares
+  const uint64_t lt = __ballot(an < C), gt = __ballot(an > 0.f), py = __ballot(yv > 0.f);
+  const float nu = (((py & lt) | (~py & gt)) != 0) ? fp : INF;
+  const float nl = (((py & gt) | (~py & lt)) != 0) ? -fp : INF;
+  // the owner lane of slot pos >> 6 as a scalar lane mask per slot, applied by
+  // v_cndmask straight from the SGPR pair (no per-lane compare)
+  const uint64_t bit = 1ull << (pos & 63);
   const int s = pos >> 6;
+  (void)lane;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const bool w = me & (s == k);
-    fu[k] = w ? nu : fu[k];
-    fl[k] = w ? nl : fl[k];
+    const uint64_t w = s == k ? bit : 0ull;
+    fu[k] = sel_lanes(fu[k], nu, w);
+    fl[k] = sel_lanes(fl[k], nl, w);
   }
 }
 
@@ -960,12 +971,22 @@ __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float
 
 // lowest working-set position whose value equals the (uniform) minimum v
 // (-1: none, i.e. NaN); scalar selects, no branch
+// s_ff1 of an SGPR-pair mask: the lowest set bit, 0xFFFFFFFF when none (the
+// builtins add a zero test and a select per mask)
+__device__ __forceinline__ uint32_t sff1_u64(uint64_t m) {
+  uint32_t r;
+  asm volatile("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+  return r;
+}
+
 __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
   const uint64_t m0 = __ballot(x[0] == v), m1 = __ballot(x[1] == v), m2 = __ballot(x[2] == v);
-  int r = m2 ? 127 + __builtin_ffsll((long long)m2) : -1;
-  r = m1 ? 63 + __builtin_ffsll((long long)m1) : r;
-  r = m0 ? __builtin_ffsll((long long)m0) - 1 : r;
-  return r;
+  // slot s's first lane | 64 s (none stays all ones), the lowest valid one wins
+  // as an unsigned minimum: 3 compares, 3 s_ff1, 2 s_or, 2 s_min
+  const uint32_t r0 = sff1_u64(m0), r1 = sff1_u64(m1) | 64u, r2 = sff1_u64(m2) | 128u;
+  uint32_t r;
+  asm volatile("s_min_u32 %0, %1, %2\n\ts_min_u32 %0, %0, %3" : "=&s"(r) : "s"(r0), "s"(r1), "s"(r2));
+  return (int)r;
 }
 
 template <bool kBox>
@@ -1031,7 +1052,8 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     fl[s] = v && in_low(a0[s], yr[s], C) ? -fv : INF;
   }
   const int64_t room = a.max_iter - it0;
-  const int cap = (int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max);
+  // uniform: in an SGPR, so the loop test is one scalar compare
+  const int cap = __builtin_amdgcn_readfirstlane((int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max));
   int inner = 0;
   bool bad = false;
   while (inner < cap) {
