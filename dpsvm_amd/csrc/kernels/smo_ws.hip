@@ -989,7 +989,10 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
   return (int)r;
 }
 
-template <bool kBox>
+// kFull: q_max == kWsMax, the three 64-row slots fill a sub-Gram row (stride
+// 192): row reads need no clamp (columns q..191 hold zeros) and take immediate
+// LDS offsets
+template <bool kBox, bool kFull>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
   __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
@@ -1075,7 +1078,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     float kh[3], kl[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      const int p = min(lane + 64 * s, q - 1);
+      const int p = kFull ? lane + 64 * s : min(lane + 64 * s, q - 1);
       kh[s] = K[ph * ldk + p];
       kl[s] = K[pl * ldk + p];
     }
@@ -1219,9 +1222,11 @@ bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max +
 
 void ws_solve(const WsArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.q_max * a.q_max * sizeof(float);
-  auto fn = a.clip == (int)ClipMode::Box ? dev::ws_solve_kernel<true> : dev::ws_solve_kernel<false>;
-  static size_t attr[2] = {64 * 1024, 64 * 1024};  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
-  size_t& at = attr[a.clip == (int)ClipMode::Box ? 1 : 0];
+  const bool box = a.clip == (int)ClipMode::Box, full = a.q_max == kWsMax;
+  auto fn = box ? (full ? dev::ws_solve_kernel<true, true> : dev::ws_solve_kernel<true, false>)
+                : (full ? dev::ws_solve_kernel<false, true> : dev::ws_solve_kernel<false, false>);
+  static size_t attr[4] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  size_t& at = attr[(box ? 2 : 0) + (full ? 1 : 0)];
   if (lds > at) {
     HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     at = lds;
