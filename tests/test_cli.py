@@ -55,6 +55,27 @@ def test_svmtrain_usage_errors(tmp_path, bin_dir):
     assert r.returncode == 255 and "Missing a required parameter" in r.stderr
     r = run([os.path.join(bin_dir, "svmTrain"), "--bogus"])
     assert r.returncode == 255
+    r = run([os.path.join(bin_dir, "svmTrain"), "-f", "x.csv", "-m", "m.txt", "--eta", "bogus"])
+    assert r.returncode == 255 and "--eta x|gram" in r.stderr
+
+
+def test_svmtrain_params_roundtrip_new_knobs(tmp_path, bin_dir):
+    """--eta and the exchange choice are recorded in --metrics-json and read back
+    by --params-json (a run's engine is reproducible from its summary)."""
+    import json
+
+    p, X, y = _data(tmp_path)
+    js, js2 = str(tmp_path / "a.json"), str(tmp_path / "b.json")
+    base = [os.path.join(bin_dir, "svmTrain"), "-a", "5", "-x", "400", "-f", p, "-c", "2", "-g", "0.4",
+            "-m", str(tmp_path / "m.txt"), "--cpu"]
+    r = run(base + ["--eta", "gram", "--exchange", "peer", "--metrics-json", js])
+    assert r.returncode == 0, r.stderr
+    pa = json.load(open(js))["params"]
+    assert pa["eta"] == 1 and pa["exchange"] == 2
+    r = run(base + ["--params-json", js, "--metrics-json", js2])
+    assert r.returncode == 0, r.stderr
+    pb = json.load(open(js2))["params"]
+    assert pb["eta"] == 1 and pb["exchange"] == 2
 
 
 def test_svmseq_and_svmtest(tmp_path, bin_dir):
