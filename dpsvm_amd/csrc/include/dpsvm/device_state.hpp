@@ -209,7 +209,8 @@ constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..
 constexpr int kWsMax = 192;          // working-set capacity: q x q fp32 sub-Gram in LDS (147 KiB)
 constexpr int kWsCand = 4;           // candidates per side per selection workgroup
 constexpr int kWsSelThreads = 256;   // selection / f-update workgroup
-constexpr int kWsMaxGroups = 256;    // selection workgroups (<= 2048 candidates per side)
+constexpr int kWsMaxGroups = 256;    // selection workgroups per rank
+constexpr int kWsListsPerThread = 4; // candidate lists a merge thread folds into one (<= 1024 lists over ranks)
 constexpr int kWsMaxRPT = 32;        // rows per selection thread (256 x 256 x 32 = 2.1M rows per rank)
 constexpr int kWsSolveThreads = 1024;
 constexpr int64_t kWsAutoRows = 100000;  // solver auto: working-set engines from this many rows on

@@ -249,6 +249,25 @@ __device__ __forceinline__ int64_t ws_xrow(const WsArgs& a, int par, int row) {
 
 __device__ __forceinline__ bool ws_tag_ok(uint64_t g, uint64_t t) { return (g >> 48) == (t >> 48); }
 
+// a <- the kWsCand smallest of the two ascending lists a, b (unique keys):
+// min(a[i], b[3 - i]) is a bitonic sequence of the 4 smallest, two
+// compare-exchange stages sort it
+__device__ __forceinline__ void ws_cx(uint64_t& x, uint64_t& y) {
+  const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+  x = lo;
+  y = hi;
+}
+
+__device__ __forceinline__ void ws_top4_merge(uint64_t (&a)[kWsCand], const uint64_t (&b)[kWsCand]) {
+  static_assert(kWsCand == 4, "4-entry bitonic merge");
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = a[i] < b[3 - i] ? a[i] : b[3 - i];
+  ws_cx(a[0], a[2]);
+  ws_cx(a[1], a[3]);
+  ws_cx(a[0], a[1]);
+  ws_cx(a[2], a[3]);
+}
+
 // a poll gave up: the run stops here (any workgroup may call it; same values)
 __device__ __forceinline__ void ws_comm_fail(const WsArgs& a, WsCtrl* c) {
   if (threadIdx.x == 0) {
@@ -458,22 +477,27 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   // candidate lists: one global round trip fewer on the merge's serial path
   const int32_t pidx_pre = tid < q_prev ? c->idx[par ^ 1][tid] : -1;
 
-  // ---- every candidate list in registers (one load batch) ----
+  // ---- every candidate list in registers: thread t holds lists t, t + 256,
+  // ... (up to kWsListsPerThread, merged to one sorted top-kWsCand list per side:
+  // the same as one selection workgroup over their rows) ----
   uint64_t lu[kWsCand], ll[kWsCand];
-  if (a.xpeer == nullptr) {
 #pragma unroll
-    for (int r = 0; r < kWsCand; ++r) {
-      lu[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + r] : kKeyNone;
-      ll[r] = tid < G ? a.cand[(size_t)tid * 2 * kWsCand + kWsCand + r] : kKeyNone;
-    }
-  } else {
-    // peer exchange: thread tid polls slot tid of this rank's buffer
-    bool ok = true;
+  for (int r = 0; r < kWsCand; ++r) lu[r] = ll[r] = kKeyNone;
+  bool ok = true;
+  const uint64_t xt = xtag((uint32_t)r_now + 1u);
+  for (int j = 0; j < kWsListsPerThread; ++j) {
+    const int slot = tid + j * kWsGatherThreads;
+    if (slot >= G) break;
+    uint64_t cu[kWsCand], cl[kWsCand];
+    if (a.xpeer == nullptr) {
 #pragma unroll
-    for (int r = 0; r < kWsCand; ++r) lu[r] = ll[r] = kKeyNone;
-    if (tid < G) {
-      const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, tid);
-      const uint64_t t = xtag((uint32_t)r_now + 1u);
+      for (int r = 0; r < kWsCand; ++r) {
+        cu[r] = a.cand[(size_t)slot * 2 * kWsCand + r];
+        cl[r] = a.cand[(size_t)slot * 2 * kWsCand + kWsCand + r];
+      }
+    } else {
+      // peer exchange: poll slot `slot` of this rank's buffer
+      const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, slot);
       uint64_t g[4 * kWsCand];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (true) {
@@ -481,7 +505,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
         for (int i = 0; i < 4 * kWsCand; ++i) g[i] = xch_load<true>(e + i);
         bool all = true;
 #pragma unroll
-        for (int i = 0; i < 4 * kWsCand; ++i) all &= ws_tag_ok(g[i], t);
+        for (int i = 0; i < 4 * kWsCand; ++i) all &= ws_tag_ok(g[i], xt);
         if (all) break;
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
           ok = false;
@@ -492,14 +516,24 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
       constexpr uint64_t m48 = (1ull << 48) - 1;
 #pragma unroll
       for (int r = 0; r < kWsCand; ++r) {
-        lu[r] = ((g[2 * r] & m48) << 16) | (g[2 * r + 1] & 0xffffull);
-        ll[r] = ((g[2 * kWsCand + 2 * r] & m48) << 16) | (g[2 * kWsCand + 2 * r + 1] & 0xffffull);
+        cu[r] = ((g[2 * r] & m48) << 16) | (g[2 * r + 1] & 0xffffull);
+        cl[r] = ((g[2 * kWsCand + 2 * r] & m48) << 16) | (g[2 * kWsCand + 2 * r + 1] & 0xffffull);
       }
     }
-    if (!__syncthreads_and(ok)) {
-      ws_comm_fail(a, c);
-      return false;
+    if (j == 0) {
+#pragma unroll
+      for (int r = 0; r < kWsCand; ++r) {
+        lu[r] = cu[r];
+        ll[r] = cl[r];
+      }
+    } else {
+      ws_top4_merge(lu, cu);
+      ws_top4_merge(ll, cl);
     }
+  }
+  if (a.xpeer != nullptr && !__syncthreads_and(ok)) {
+    ws_comm_fail(a, c);
+    return false;
   }
   // ---- global minima (stop test) ----
   uint64_t gu = lu[0], gl = ll[0];
@@ -531,7 +565,8 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   // extreme first, prefix < T, prefix == T — each class in list (row) order,
   // so a cut only ever drops rows of the boundary class. ----
   const int half = (want + 1) / 2;
-  const int d = min(kWsCand - 1, (half + G - 1) / G - 1);
+  const int Gl = min(G, kWsGatherThreads);  // lists held (one merged list per thread)
+  const int d = min(kWsCand - 1, (half + Gl - 1) / Gl - 1);
   const int m = (half + d) / (d + 1);
   uint64_t hd[2] = {lu[0], ll[0]};
 #pragma unroll
@@ -1170,8 +1205,10 @@ namespace launch {
 
 void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt) {
   // every rank the same geometry (sized for the largest shard); the merge reads
-  // world * G <= 256 candidate lists
-  const int64_t gmax = std::max<int64_t>(1, kWsMaxGroups / std::max(1, world));
+  // world * G <= 1024 candidate lists (kWsListsPerThread per merge thread), so
+  // up to 8 ranks keep 128-256 selection workgroups each
+  const int64_t gmax = std::max<int64_t>(
+      1, std::min<int64_t>(kWsMaxGroups, (int64_t)kWsListsPerThread * 256 / std::max(1, world)));
   const int64_t g = std::max<int64_t>(1, std::min<int64_t>(gmax, (nl_max + kWsSelThreads - 1) / kWsSelThreads));
   const int64_t r = (nl_max + g * kWsSelThreads - 1) / (g * kWsSelThreads);
   *G = (int32_t)g;

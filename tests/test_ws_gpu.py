@@ -297,8 +297,9 @@ def test_ws_peer_exchange_loopback_bit_identical(extra):
     assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
 
 
-@pytest.mark.parametrize("world,engine", [(2, "ws"), (4, "ws"), (2, "ws-cache")])
-def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine):
+@pytest.mark.parametrize("world,engine,n", [(2, "ws", 6000), (4, "ws", 6000), (2, "ws-cache", 6000),
+                                           (2, "ws", 70000)])
+def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine, n):
     """Sharded working-set rounds with ranks as processes sharing the GPU (gloo
     bootstrap, IPC-mapped uncached receive buffers): no collective per round —
     each selection workgroup pushes its candidate lists to every rank, each
@@ -317,10 +318,9 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine):
     from dpsvm_amd._native import load
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    n = 6000
     env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
     out = tmp_path / f"ws{world}"
-    port = 29680 + world + (10 if engine == "ws-cache" else 0)
+    port = 29680 + world + (10 if engine == "ws-cache" else 0) + (20 if n > 6000 else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), engine, str(n),
@@ -344,3 +344,5 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine):
         assert ref[k].setup_info_["exchange"] == "allreduce"
         assert res[k]["iters"] == ref[0].n_iter_ and res[k]["rounds"] == ref[0].n_rounds_
         assert res[k]["alpha_sha"] == sha
+    if n > 6000:  # 2 x 137 selection workgroups: the merge folds two candidate lists per thread
+        assert ref[0].setup_info_["groups"] * world > 256
