@@ -84,6 +84,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --solver S          :  auto (ws from 100k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
+               "   --ws-blocks P :  ws-dense: P sub-problems per round on P workgroups (1..4)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
@@ -102,7 +103,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_GB, OPT_NOGRAPH, OPT_CK, OPT_CKE, OPT_RESUME, OPT_METRICS, OPT_LOG, OPT_PREC, OPT_LEGM,
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
-    OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL,
+    OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL, OPT_WSBLOCKS,
     OPT_WSINNER, OPT_WSBLOCK, OPT_ETA
   };
   static struct option longopts[] = {
@@ -134,6 +135,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"no-verify-ranks", no_argument, 0, OPT_NOVR}, {"params-json", required_argument, 0, OPT_PJSON},
       {"solver", required_argument, 0, OPT_SOLVER}, {"ws-size", required_argument, 0, OPT_WSSIZE},
       {"ws-new", required_argument, 0, OPT_WSNEW}, {"eta", required_argument, 0, OPT_ETA}, {"ws-rel", required_argument, 0, OPT_WSREL},
+      {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {0, 0, 0, 0}};
   while (true) {
@@ -232,6 +234,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_WSSIZE: o.p.ws_size = atoi(optarg); break;
       case OPT_WSNEW: o.p.ws_new = atoi(optarg); break;
       case OPT_WSREL: o.p.ws_rel = (float)atof(optarg); break;
+      case OPT_WSBLOCKS: o.p.ws_blocks = atoi(optarg); break;
       case OPT_WSINNER: o.p.ws_inner = atoi(optarg); break;
       case OPT_WSBLOCK: o.p.ws_block = atoi(optarg); break;
       case OPT_ETA: {

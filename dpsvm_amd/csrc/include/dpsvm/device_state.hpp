@@ -214,6 +214,13 @@ constexpr int kWsListsPerThread = 4; // candidate lists a merge thread folds int
 constexpr int kWsMaxRPT = 32;        // rows per selection thread (256 x 256 x 32 = 2.1M rows per rank)
 constexpr int kWsSolveThreads = 1024;
 constexpr int64_t kWsAutoRows = 100000;  // solver auto: working-set engines from this many rows on
+// multi-block rounds (ws_blocks = P > 1, ws-dense at world 1): a round selects
+// up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
+// workgroups; the combined step is scaled by the exact line-search factor
+// t = min(1, g'd / d'Qd) of the dual (smo_ws.hip "multi-block rounds")
+constexpr int kWsMaxBlocks = 4;
+constexpr int kWsMaxAll = kWsMaxBlocks * kWsMax;  // union capacity (768)
+constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 
 struct alignas(16) WsCtrl {
   int64_t iter;      // pair updates applied so far
@@ -225,14 +232,27 @@ struct alignas(16) WsCtrl {
   int32_t nonfinite; // set by ws_select when an f value is not finite
   int32_t n_miss;    // cache mode: rows of the current set without a line (computed this round)
   int32_t hand;      // cache mode: next line the victim window starts at
-  int32_t pad[3];
-  int32_t idx[2][kWsMax];     // working set per round parity (global rows), newest first
-  int32_t line[2][kWsMax];    // the line holding each member's kernel row (dense mode: the row itself)
-  int32_t apply_idx[kWsMax];  // rows whose alpha changed in the last round
-  int32_t apply_line[kWsMax]; // their lines
-  float apply_coef[kWsMax];   // their (alpha_new - alpha_old) * y
+  int32_t solve_cnt; // multi-block: solve workgroups finished this round (the last one commits)
+  int32_t pad[2];
+  // block p's rows at [p * q_max, p * q_max + qb[par][p]) (one block: idx[par][0..q))
+  int32_t idx[2][kWsMaxAll];     // working set per round parity (global rows), newest first
+  int32_t line[2][kWsMaxAll];    // the line holding each member's kernel row (dense mode: the row itself)
+  int32_t apply_idx[kWsMaxAll];  // rows whose alpha changed in the last round (multi-block: per-block segments)
+  int32_t apply_line[kWsMaxAll]; // their lines
+  float apply_coef[kWsMaxAll];   // their (alpha_new - alpha_old) * y
   int32_t miss_row[kWsMax], miss_line[kWsMax];  // cache mode: rows to compute this round, their lines
   int64_t rows_computed, row_hits;              // cache mode statistics
+  // multi-block rounds
+  int32_t uidx[2][kWsMaxAll];    // the union, newest first (previous-set retention)
+  int32_t uq[2];                 // its size
+  int32_t qb[2][kWsMaxBlocks];   // rows per block
+  int32_t nab[kWsMaxBlocks];     // alpha changes per block (apply segment p at p * q_max)
+  int32_t inb[kWsMaxBlocks];     // pair steps per block
+  int32_t badb[kWsMaxBlocks];    // non-finite per block
+  int32_t pad2[3];
+  float t_last;                  // line-search factor of the last applied round
+  int32_t n_damped;              // rounds applied with t < 1
+  int32_t pad3[2];
 };
 
 struct WsArgs {
@@ -272,6 +292,12 @@ struct WsArgs {
   int32_t xrank;
   int64_t xsub;
   int64_t xtimeout_ticks;  // give-up bound of one poll (s_memrealtime, 100 MHz)
+  // multi-block rounds (P = blocks > 1): subg / aux hold P blocks
+  // ([P][q_max][q_max], [P][3][kWsMax]); the f update runs in two passes
+  int32_t blocks;
+  float* dfs;          // [nl] the round's f change before the line search
+  float* dalpha;       // [n] alpha_new - alpha_old of the round's changed rows (0 elsewhere)
+  double* part;        // [G][2] per-workgroup partial sums: d'Qd, -g'd
 };
 // u64 words of the working-set exchange region (both parities)
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {

@@ -54,6 +54,7 @@ void for_each_param(SolverParams& p, F&& f) {
   f("ws_size", p.ws_size);
   f("ws_new", p.ws_new);
   f("ws_rel", p.ws_rel);
+  f("ws_blocks", p.ws_blocks);
   f("ws_inner", p.ws_inner);
   f("ws_block", p.ws_block);
   f("eta", p.eta);

@@ -76,6 +76,8 @@ void ws_solve(const WsArgs& a, hipStream_t s);
 // cache mode: the merge + line assignment (one workgroup) runs before the
 // row GEMM; ws_gather then reads the sub-Gram from the members' lines
 void ws_merge(const WsArgs& a, hipStream_t s);
+// multi-block rounds (a.blocks > 1, ws-dense at one rank): the union merge before ws_gather
+void ws_merge_multi(const WsArgs& a, hipStream_t s);
 bool ws_cache_supported(int64_t L, int q_max);
 // partitioned X, cache mode: out[i] = X row ctrl->miss_row[i] if this rank owns
 // it (rows off..off+nl-1 at x), else zeros; out_sq[i] = its global |x|^2

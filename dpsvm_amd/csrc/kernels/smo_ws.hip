@@ -277,6 +277,31 @@ __device__ __forceinline__ void ws_comm_fail(const WsArgs& a, WsCtrl* c) {
   }
 }
 
+// fixed-order wave sum (xor butterfly: every lane ends with the same bits)
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// multi-block rounds: the exact line search along the combined step d of the
+// P sub-problems.  W(alpha + t d) = W + t g'd - t^2 d'Qd / 2 peaks at
+// t = g'd / d'Qd; each block's step alone raises W, so g'd > 0 and the
+// capped t keeps every round an ascent step however the blocks couple (t = 1
+// when they do not: K ~ I).  Every wave reduces the workgroup partials in the
+// same order: identical t everywhere.
+__device__ __forceinline__ float ws_line_search(const WsArgs& a) {
+  const int lane = threadIdx.x & 63;
+  double q = 0.0, g = 0.0;
+  for (int k = lane; k < a.G; k += 64) {
+    q += a.part[2 * k];
+    g += a.part[2 * k + 1];
+  }
+  q = wave_sum_f64(q);
+  g = wave_sum_f64(g);
+  return (g > 0.0 && q > g) ? (float)(g / q) : 1.f;
+}
+
 // ---------------------------------------------------------------------------
 // ws_select: f update of the last round + per-workgroup candidates
 // ---------------------------------------------------------------------------
@@ -291,12 +316,21 @@ constexpr int ws_parts() {
   return RPT <= 4 ? 4 : RPT <= 16 ? 2 : 1;
 }
 
-template <int RPT>
+// MODE 0: one pass (f += the round's change, then candidates).  Multi-block
+// rounds split it: MODE 1 computes the change d_f into a.dfs and per-workgroup
+// partial sums of the line search (d'Qd = sum_j c_j d_f_j and g'd = -sum_j c_j
+// f_j over the changed rows j, c_j = d_alpha_j y_j), MODE 2 takes
+// t = min(1, g'd / d'Qd) from the partials (fixed order: every workgroup the
+// same t), applies f += t d_f and alpha = alpha_new - (1 - t) d_alpha, then
+// selects the candidates.
+template <int RPT, int MODE>
 __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_kernel(WsArgs a) {
   constexpr int PARTS = ws_parts<RPT>();
   constexpr int CH = RPT >= 32 ? 1 : RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
-  __shared__ int32_t s_idx[kWsMax];  // lines of the changed rows
-  __shared__ float s_coef[kWsMax];
+  constexpr int LMAX = MODE == 1 ? kWsMaxAll : MODE == 0 ? kWsMax : 1;
+  __shared__ int32_t s_idx[LMAX];  // lines of the changed rows
+  __shared__ float s_coef[LMAX];
+  __shared__ double s_red[2][kWsSelThreads * PARTS / 64];
   __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][PARTS > 1 ? kWsSelThreads * RPT : 1];
   __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
   WsCtrl* c = a.ctrl;
@@ -304,10 +338,23 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(6);
   const int na = c->n_apply;
   const int done = c->done;
-  if (na == 0 && done != kRunning) return;
-  for (int k = threadIdx.x; k < na; k += kWsSelThreads * PARTS) {
-    s_idx[k] = c->apply_line[k];
-    s_coef[k] = c->apply_coef[k];
+  if (na == 0 && (done != kRunning || MODE == 1)) return;
+  if constexpr (MODE == 0) {
+    for (int k = threadIdx.x; k < na; k += kWsSelThreads * PARTS) {
+      s_idx[k] = c->apply_line[k];
+      s_coef[k] = c->apply_coef[k];
+    }
+  } else if constexpr (MODE == 1) {
+    // the blocks' apply segments, concatenated in block order
+    int at = 0;
+    for (int p = 0; p < a.blocks; ++p) {
+      const int nb = c->nab[p];
+      for (int k = threadIdx.x; k < nb; k += kWsSelThreads * PARTS) {
+        s_idx[at + k] = c->apply_line[p * a.q_max + k];
+        s_coef[at + k] = c->apply_coef[p * a.q_max + k];
+      }
+      at += nb;
+    }
   }
   __syncthreads();
   // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers
@@ -321,11 +368,12 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
     f[r] = has[r] && part == 0 ? a.f[j] : 0.f;
   }
   if (na > 0) {
-    const int per = (na + PARTS - 1) / PARTS;
-    const int k_lo = part * per, k_hi = min(na, k_lo + per);
     float acc[RPT];
 #pragma unroll
     for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+    if constexpr (MODE != 2) {
+    const int per = (na + PARTS - 1) / PARTS;
+    const int k_lo = part * per, k_hi = min(na, k_lo + per);
     for (int k0 = k_lo; k0 < k_hi; k0 += CH) {
       float kv[CH][RPT];
 #pragma unroll
@@ -356,6 +404,62 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
         for (int r = 0; r < RPT; ++r) {
 #pragma clang fp contract(off)
           acc[r] = acc[r] + s_part[p - 1][r * kWsSelThreads + tid];
+        }
+      }
+    }
+    }  // MODE != 2
+    if constexpr (MODE == 1) {
+      double sq = 0.0, sg = 0.0;
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        if (has[r] && part == 0) {
+          const int64_t j = base + r * kWsSelThreads;
+          a.dfs[j] = acc[r];
+          const float dj = a.dalpha[a.off + j];
+          if (dj != 0.f) {
+            const double cj = (double)dj * (double)a.y[a.off + j];
+            sq += cj * (double)acc[r];
+            sg -= cj * (double)f[r];
+          }
+        }
+      }
+      // fixed-order block sums (butterfly per wave, waves in order)
+      sq = wave_sum_f64(sq);
+      sg = wave_sum_f64(sg);
+      const int w = threadIdx.x >> 6;
+      if ((threadIdx.x & 63) == 0) {
+        s_red[0][w] = sq;
+        s_red[1][w] = sg;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double tq = 0.0, tg = 0.0;
+        for (int k = 0; k < kWsSelThreads * PARTS / 64; ++k) {
+          tq += s_red[0][k];
+          tg += s_red[1][k];
+        }
+        a.part[2 * blockIdx.x] = tq;
+        a.part[2 * blockIdx.x + 1] = tg;
+      }
+      return;
+    }
+    if constexpr (MODE == 2) {
+      const float t = ws_line_search(a);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->t_last = t;
+        if (t < 1.f) c->n_damped = c->n_damped + 1;
+      }
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        if (has[r] && part == 0) {
+          const int64_t j = base + r * kWsSelThreads;
+          const float d = a.dfs[j];
+          acc[r] = t == 1.f ? d : t * d;
+          const float dj = a.dalpha[a.off + j];
+          if (dj != 0.f) {
+            if (t < 1.f) a.alpha[a.off + j] = clip01(a.alpha[a.off + j] - (1.f - t) * dj, 0.f, a.C);
+            a.dalpha[a.off + j] = 0.f;
+          }
         }
       }
     }
@@ -916,6 +1020,192 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
 }
 
 // ---------------------------------------------------------------------------
+// multi-block rounds (a.blocks = P > 1; ws-dense at world 1).  The grid-wide
+// work of a round (merge, f update, candidates) is shared by P sub-problems
+// solved at once on P workgroups (the one-wave solve leaves the other CUs
+// idle): ws_merge_multi picks up to P q_max rows, ws_gather_multi their P
+// diagonal q x q blocks, ws_solve<kMulti> one block per workgroup, and the
+// two-pass ws_select applies the combined step with the exact line search.
+// ---------------------------------------------------------------------------
+// exclusive prefix of counts 0..3 over kWsMergeThreads threads in thread order
+__device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  int pre = 0, wtot = 0;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const uint64_t m = __ballot((v >> b) & 1);
+    pre += __popcll(m & below) << b;
+    wtot += __popcll(m) << b;
+  }
+  if (lane == 0) wsum[wave] = wtot;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWsMergeThreads / 64; ++w) {
+    off += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off + pre;
+}
+
+// ONE workgroup: every candidate key of both sides sorted (bitonic, 1024 per
+// side), the stop test, then the union: up rank r / low rank r interleaved
+// (most violating first, a row's first position wins), then the newest rows
+// of the previous union.  Union position i goes to block ((i / 2) mod P): each
+// block gets up / low pairs, block 0 the global extremes (so a round always
+// holds the maximal violating pair and makes progress).
+__global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
+  constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
+  static_assert(2 * (NK / 2) == kWsMergeThreads, "one comparator per thread and side");
+  __shared__ uint64_t s_k[2][NK];
+  __shared__ int32_t s_hash[4][kWsHash];
+  __shared__ int32_t s_keep[kWsMaxAll + 2];
+  __shared__ int32_t s_idx[kWsMaxAll];
+  __shared__ int s_wsum[kWsMergeThreads / 64];
+  __shared__ int s_qb[kWsMaxBlocks];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  const bool lead = tid == 0;
+  if (c->done != kRunning) {
+    if (lead) c->n_apply = 0;  // applied by the last ws_select already
+    return;
+  }
+  if (lead) WS_STAMP(1);
+  const int G = a.G_all;
+  const int par = (int)(c->outer & 1);
+  const int P = a.blocks, Qmax = P * a.q_max;
+  const int q_prev = c->uq[par ^ 1];
+  const int want = q_prev == 0 ? Qmax : min(P * a.n_new, Qmax);
+  const int32_t pidx = tid < q_prev ? c->uidx[par ^ 1][tid] : -1;
+  {
+    const int l = tid / kWsCand, r = tid % kWsCand;
+    s_k[0][tid] = l < G ? a.cand[(size_t)l * 2 * kWsCand + r] : kKeyNone;
+    s_k[1][tid] = l < G ? a.cand[(size_t)l * 2 * kWsCand + kWsCand + r] : kKeyNone;
+  }
+  if (tid < kWsMaxBlocks) s_qb[tid] = 0;
+  for (int t = tid; t < 4 * kWsHash; t += kWsMergeThreads) (&s_hash[0][0])[t] = -1;
+  __syncthreads();
+  {
+    uint64_t* sk = s_k[tid / (NK / 2)];
+    const int i = tid % (NK / 2);
+    for (int k = 2; k <= NK; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+        const bool asc = (lo & k) == 0;
+        const uint64_t x = sk[lo], y = sk[hi];
+        if ((x > y) == asc) {
+          sk[lo] = y;
+          sk[hi] = x;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  const uint64_t gu = s_k[0][0], gl = s_k[1][0];
+  const float b_hi = key_value(gu), b_lo = -key_value(gl);
+  const int64_t it0 = c->iter;
+  int stop = kRunning;
+  if (c->nonfinite) stop = kNonFinite;
+  else if (gu == kKeyNone || gl == kKeyNone) stop = kNoPair;
+  else if (!isfinite(b_hi) || !isfinite(b_lo)) stop = kNonFinite;
+  else if (!(b_lo > b_hi + 2.0f * a.eps)) stop = kConverged;
+  else if (it0 >= a.max_iter) stop = kMaxIter;
+  if (stop != kRunning) {
+    if (lead) {
+      c->done = stop;
+      c->n_apply = 0;
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+      ws_status(a.status, c);
+    }
+    return;
+  }
+  int32_t* hk_u = s_hash[0];
+  int32_t* hv_u = s_hash[1];
+  int32_t* hk_l = s_hash[2];
+  int32_t* hv_l = s_hash[3];
+  const int half = (want + 1) / 2;
+  const uint64_t ku = tid < half ? s_k[0][tid] : kKeyNone, kl = tid < half ? s_k[1][tid] : kKeyNone;
+  if (ku != kKeyNone) ws_hash_insert(hk_u, hv_u, (int32_t)key_index(ku), tid);
+  if (kl != kKeyNone) ws_hash_insert(hk_l, hv_l, (int32_t)key_index(kl), tid);
+  __syncthreads();
+  bool kp0 = false, kp1 = false;
+  if (ku != kKeyNone) {
+    const int rl = ws_hash_find(hk_l, hv_l, (int32_t)key_index(ku));
+    kp0 = !(rl >= 0 && rl < tid);
+  }
+  if (kl != kKeyNone) {
+    const int ru = ws_hash_find(hk_u, hv_u, (int32_t)key_index(kl));
+    kp1 = !(ru >= 0 && ru <= tid);
+  }
+  int kept = 0;
+  const int slot0 = block_scan_merge((int)kp0 + (int)kp1, s_wsum, &kept);
+  const int n_chosen = min(kept, want);
+  if (tid < half) {
+    const int s0 = slot0, s1 = slot0 + (int)kp0;
+    const bool c0 = kp0 && s0 < want, c1 = kp1 && s1 < want;
+    s_keep[2 * tid] = c0 ? s0 : -1;
+    s_keep[2 * tid + 1] = c1 ? s1 : -1;
+    if (c0) s_idx[s0] = (int32_t)key_index(ku);
+    if (c1) s_idx[s1] = (int32_t)key_index(kl);
+  }
+  __syncthreads();
+  bool pk = false;
+  if (pidx >= 0) {
+    const int ru = ws_hash_find(hk_u, hv_u, pidx), rl = ws_hash_find(hk_l, hv_l, pidx);
+    pk = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+  }
+  int ptotal = 0;
+  const int pslot = block_scan_merge((int)pk, s_wsum, &ptotal);
+  if (pk && n_chosen + pslot < Qmax) s_idx[n_chosen + pslot] = pidx;
+  const int Q = min(Qmax, n_chosen + ptotal);
+  __syncthreads();
+  if (tid < Q) {
+    const int32_t row = s_idx[tid];
+    c->uidx[par][tid] = row;
+    const int pi = tid >> 1, b = pi % P, la = 2 * (pi / P) + (tid & 1);
+    c->idx[par][b * a.q_max + la] = row;
+    c->line[par][b * a.q_max + la] = row;  // the resident Gram: line i is row i
+    atomicMax(&s_qb[b], la + 1);
+  }
+  __syncthreads();
+  if (tid < P) c->qb[par][tid] = s_qb[tid];
+  if (lead) {
+    c->uq[par] = Q;
+    c->q[par] = Q;
+    c->b_hi = b_hi;
+    c->b_lo = b_lo;
+    WS_STAMP(2);
+  }
+}
+
+// P x q_max workgroups: workgroup p q_max + a gathers row a of block p's
+// sub-Gram (block p's columns) and the row's f / alpha / y
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  if (c->done != kRunning) return;
+  const int tid = threadIdx.x;
+  const int par = (int)(c->outer & 1);
+  const int p = (int)blockIdx.x / a.q_max, ra = (int)blockIdx.x % a.q_max;
+  const int q = c->qb[par][p];
+  WsArgs b = a;
+  b.subg = a.subg + (size_t)p * a.q_max * a.q_max;
+  b.aux = a.aux + (size_t)p * 3 * kWsMax;
+  if (ra >= q) {
+    ws_gather_row(b, c, s_idx, q, ra, nullptr);
+    return;
+  }
+  for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][p * a.q_max + t];
+  __syncthreads();
+  ws_gather_row(b, c, s_idx, q, ra, a.gram + (int64_t)s_idx[ra] * a.ldg);
+  if (tid == 0 && blockIdx.x == 0) WS_STAMP(8);
+}
+
+// ---------------------------------------------------------------------------
 // ws_solve: the sub-problem on wave 0
 // ---------------------------------------------------------------------------
 // Row `pos` (uniform) took alpha `an` and now has gradient fp (both uniform,
@@ -1027,7 +1317,7 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
 // kFull: q_max == kWsMax, the three 64-row slots fill a sub-Gram row (stride
 // 192): row reads need no clamp (columns q..191 hold zeros) and take immediate
 // LDS offsets
-template <bool kBox, bool kFull>
+template <bool kBox, bool kFull, bool kMulti>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
   __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
@@ -1037,16 +1327,21 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   if (tid == 0) WS_STAMP(0);
   if (c->done != kRunning) return;
   const int par = (int)(c->outer & 1);
-  const int q = c->q[par];
+  // multi-block rounds: workgroup p solves block p (rows idx[par][p q_max ..])
+  const int blk = kMulti ? (int)blockIdx.x : 0;
+  const int q = kMulti ? c->qb[par][blk] : c->q[par];
   const float b_hi = c->b_hi, b_lo = c->b_lo;
   const int64_t it0 = c->iter;
   const int ldk = a.q_max;  // LDS keeps the q_max stride: the load is one contiguous copy
+  const int ib = blk * a.q_max;
+  const float* subg = a.subg + (size_t)blk * ldk * ldk;
+  const float* aux = a.aux + (size_t)blk * 3 * kWsMax;
   {
     // q rows of the q_max-stride sub-Gram into LDS (147 KiB at q = 192): 16-B
     // loads, four in flight per thread before their stores
     const int n = q * ldk;
     if ((ldk & 3) == 0) {
-      const f4* src = (const f4*)a.subg;
+      const f4* src = (const f4*)subg;
       f4* dst = (f4*)K;
       const int n4 = n >> 2;
       for (int e = tid; e < n4; e += 4 * kWsSolveThreads) {
@@ -1061,14 +1356,14 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
           if (e + u * kWsSolveThreads < n4) dst[e + u * kWsSolveThreads] = v[u];
       }
     } else {
-      for (int e = tid; e < n; e += kWsSolveThreads) K[e] = a.subg[e];
+      for (int e = tid; e < n; e += kWsSolveThreads) K[e] = subg[e];
     }
     if (tid < q) {
-      s_f[tid] = a.aux[tid];
-      s_a[tid] = a.aux[kWsMax + tid];
-      s_y[tid] = a.aux[2 * kWsMax + tid];
-      s_idx[tid] = c->idx[par][tid];
-      s_line[tid] = c->line[par][tid];
+      s_f[tid] = aux[tid];
+      s_a[tid] = aux[kWsMax + tid];
+      s_y[tid] = aux[2 * kWsMax + tid];
+      s_idx[tid] = c->idx[par][ib + tid];
+      s_line[tid] = c->line[par][ib + tid];
     }
   }
   __syncthreads();
@@ -1089,7 +1384,8 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     fu[s] = v && in_up(a0[s], yr[s], C) ? fv : INF;
     fl[s] = v && in_low(a0[s], yr[s], C) ? -fv : INF;
   }
-  const int64_t room = a.max_iter - it0;
+  int64_t room = a.max_iter - it0;
+  if (kMulti) room = room / a.blocks + (blk < room % a.blocks ? 1 : 0);  // the blocks share max_iter
   // uniform: in an SGPR, so the loop test is one scalar compare
   const int cap = __builtin_amdgcn_readfirstlane((int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max));
   int inner = 0;
@@ -1161,13 +1457,14 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
 #pragma clang fp contract(off)
         dc = (an - a0[s]) * yr[s];
       }
-      c->apply_idx[at] = gi;
-      c->apply_line[at] = s_line[p];
-      c->apply_coef[at] = dc;
+      c->apply_idx[ib + at] = gi;
+      c->apply_line[ib + at] = s_line[p];
+      c->apply_coef[ib + at] = dc;
+      if (kMulti) a.dalpha[gi] = an - a0[s];
     }
     n_apply += __popcll(mk);
   }
-  if (lane == 0) {
+  if (lane == 0 && !kMulti) {
     WS_STAMP(4);
     if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + 5] = (uint64_t)inner;
     c->n_apply = n_apply;
@@ -1175,6 +1472,32 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     c->outer = c->outer + 1;
     c->done = bad ? kNonFinite : inner == 0 ? kNoPair : (it0 + inner >= a.max_iter ? kMaxIter : kRunning);
     ws_status(a.status, c);
+  }
+  if (lane == 0 && kMulti) {
+    // publish this block's counts; the last block to finish commits the round
+    // (threadfence + counter: no workgroup waits for another)
+    c->nab[blk] = n_apply;
+    c->inb[blk] = inner;
+    c->badb[blk] = bad ? 1 : 0;
+    __threadfence();
+    const int prev = atomicAdd(&c->solve_cnt, 1);
+    if (prev == a.blocks - 1) {
+      __threadfence();
+      int tot_a = 0, tot_i = 0, any_bad = 0;
+      for (int p = 0; p < a.blocks; ++p) {
+        tot_a += __hip_atomic_load(&c->nab[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tot_i += __hip_atomic_load(&c->inb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        any_bad |= __hip_atomic_load(&c->badb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      c->solve_cnt = 0;
+      WS_STAMP(4);
+      if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + 5] = (uint64_t)tot_i;
+      c->n_apply = tot_a;
+      c->iter = it0 + tot_i;
+      c->outer = c->outer + 1;
+      c->done = any_bad ? kNonFinite : tot_i == 0 ? kNoPair : (it0 + tot_i >= a.max_iter ? kMaxIter : kRunning);
+      ws_status(a.status, c);
+    }
   }
 }
 
@@ -1221,20 +1544,41 @@ bool ws_supported(int64_t nl_max, int world, int q_max) {
   return q_max >= 2 && q_max <= kWsMax && rpt <= kWsMaxRPT && nl_max < (int64_t)1 << 31 && world <= kWsMaxGroups;
 }
 
-void ws_select(const WsArgs& a, hipStream_t s) {
+template <int MODE>
+static void ws_select_mode(const WsArgs& a, hipStream_t s) {
   const dim3 grid(a.G);
   auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 4 ? 4 : rpt <= 16 ? 2 : 1)); };
-  if (a.rpt <= 1) dev::ws_select_kernel<1><<<grid, threads(1), 0, s>>>(a);
-  else if (a.rpt <= 2) dev::ws_select_kernel<2><<<grid, threads(2), 0, s>>>(a);
-  else if (a.rpt <= 4) dev::ws_select_kernel<4><<<grid, threads(4), 0, s>>>(a);
-  else if (a.rpt <= 8) dev::ws_select_kernel<8><<<grid, threads(8), 0, s>>>(a);
-  else if (a.rpt <= 16) dev::ws_select_kernel<16><<<grid, threads(16), 0, s>>>(a);
-  else dev::ws_select_kernel<32><<<grid, threads(32), 0, s>>>(a);
+  if (a.rpt <= 1) dev::ws_select_kernel<1, MODE><<<grid, threads(1), 0, s>>>(a);
+  else if (a.rpt <= 2) dev::ws_select_kernel<2, MODE><<<grid, threads(2), 0, s>>>(a);
+  else if (a.rpt <= 4) dev::ws_select_kernel<4, MODE><<<grid, threads(4), 0, s>>>(a);
+  else if (a.rpt <= 8) dev::ws_select_kernel<8, MODE><<<grid, threads(8), 0, s>>>(a);
+  else if (a.rpt <= 16) dev::ws_select_kernel<16, MODE><<<grid, threads(16), 0, s>>>(a);
+  else dev::ws_select_kernel<32, MODE><<<grid, threads(32), 0, s>>>(a);
   post_launch("ws_select", s);
 }
 
+void ws_select(const WsArgs& a, hipStream_t s) {
+  if (a.blocks > 1) {
+    ws_select_mode<1>(a, s);  // d_f + line-search partials
+    ws_select_mode<2>(a, s);  // f += t d_f, candidates
+  } else {
+    ws_select_mode<0>(a, s);
+  }
+}
+
+void ws_merge_multi(const WsArgs& a, hipStream_t s) {
+  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.world == 1 && !a.cache && a.G_all <= kWsMaxGroups &&
+                  a.q_max % 2 == 0,
+              "ws_merge_multi: multi-block rounds need ws-dense at one rank and an even q_max");
+  dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
+  post_launch("ws_merge_multi", s);
+}
+
 void ws_gather(const WsArgs& a, hipStream_t s) {
-  if (a.cache) {
+  if (a.blocks > 1) {
+    dev::ws_gather_multi_kernel<<<dim3(a.blocks * a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+    post_launch("ws_gather_multi", s);
+  } else if (a.cache) {
     dev::ws_gather_lines_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
     post_launch("ws_gather_lines", s);
   } else {
@@ -1259,16 +1603,22 @@ bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max +
 
 void ws_solve(const WsArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.q_max * a.q_max * sizeof(float);
-  const bool box = a.clip == (int)ClipMode::Box, full = a.q_max == kWsMax;
-  auto fn = box ? (full ? dev::ws_solve_kernel<true, true> : dev::ws_solve_kernel<true, false>)
-                : (full ? dev::ws_solve_kernel<false, true> : dev::ws_solve_kernel<false, false>);
-  static size_t attr[4] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
-  size_t& at = attr[(box ? 2 : 0) + (full ? 1 : 0)];
+  const bool box = a.clip == (int)ClipMode::Box, full = a.q_max == kWsMax, multi = a.blocks > 1;
+  using Fn = void (*)(WsArgs);
+  static const Fn fns[8] = {dev::ws_solve_kernel<false, false, false>, dev::ws_solve_kernel<false, true, false>,
+                            dev::ws_solve_kernel<true, false, false>,  dev::ws_solve_kernel<true, true, false>,
+                            dev::ws_solve_kernel<false, false, true>,  dev::ws_solve_kernel<false, true, true>,
+                            dev::ws_solve_kernel<true, false, true>,   dev::ws_solve_kernel<true, true, true>};
+  const int v = (multi ? 4 : 0) + (box ? 2 : 0) + (full ? 1 : 0);
+  const Fn fn = fns[v];
+  static size_t attr[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024,
+                           64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  size_t& at = attr[v];
   if (lds > at) {
     HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     at = lds;
   }
-  fn<<<1, kWsSolveThreads, lds, s>>>(a);
+  fn<<<multi ? a.blocks : 1, kWsSolveThreads, lds, s>>>(a);
   post_launch("ws_solve", s);
 }
 

@@ -186,6 +186,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_size", &SolverParams::ws_size)
       .def_readwrite("ws_new", &SolverParams::ws_new)
       .def_readwrite("ws_rel", &SolverParams::ws_rel)
+      .def_readwrite("ws_blocks", &SolverParams::ws_blocks)
       .def_readwrite("ws_inner", &SolverParams::ws_inner)
       .def_readwrite("ws_block", &SolverParams::ws_block)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })

@@ -351,6 +351,7 @@ struct WsDense final : DenseBase {
   EngineKind kind() const override { return EngineKind::WsDense; }
   int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
   static void round(GpuSolver::Impl& m) {
+    if (m.wsa.blocks > 1) launch::ws_merge_multi(m.wsa, m.stream);  // else merged inside ws_gather
     launch::ws_gather(m.wsa, m.stream);
     ws_allreduce_sub(m);
     launch::ws_solve(m.wsa, m.stream);
@@ -359,6 +360,7 @@ struct WsDense final : DenseBase {
   }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {
     gram(m, res);
+    if (m.wsa.blocks > 1) HIP_CHECK(hipMemsetAsync(m.wsa.dalpha, 0, (size_t)m.n * 4, m.stream));
     WsCtrl c;
     memset(&c, 0, sizeof(c));
     c.iter = iter0;

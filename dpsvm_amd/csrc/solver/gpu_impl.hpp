@@ -96,6 +96,9 @@ struct GpuSolver::Impl {
   WsArgs wsa{};
   WsCtrl* wsctrl = nullptr;
   uint64_t* wscand = nullptr;
+  float* wsdfs = nullptr;           // multi-block rounds: d_f [nl], d_alpha [n], line-search partials [G][2]
+  float* wsdalpha = nullptr;
+  double* wspart = nullptr;
   float* wssub = nullptr;          // q_max x q_max sub-Gram + [3][kWsMax] f / alpha / y of the working set
   float *wsxq = nullptr, *wsxqsq = nullptr;  // partitioned X, cache mode: the misses' X rows / norms
   int32_t* wsiota = nullptr;                  //   (their GEMM row indices: 0..q_max-1)

@@ -34,7 +34,7 @@ GpuSolver::Impl::~Impl() {
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
-                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub,
+                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wsdfs, (void*)wsdalpha, (void*)wspart,
                     (void*)wsxq, (void*)wsxqsq, (void*)wsiota})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
@@ -526,17 +526,38 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.tau = m.p.tau;
     w.clip = (int)m.p.clip;
     w.max_iter = m.p.max_iter;
+    // multi-block rounds: ws-dense with no per-round communication (world 1 or
+    // every rank solving the whole problem), an even q_max
+    w.blocks = 1;
+    if (m.p.ws_blocks > 1) {
+      DPSVM_CHECK(m.p.ws_blocks <= kWsMaxBlocks, "ws_blocks must be in 1.." + std::to_string(kWsMaxBlocks));
+      const bool ok = m.kind == EngineKind::WsDense && m.world == 1 && !m.xch && ws_q % 2 == 0 && !m.p.force_collectives;
+      if (ok) w.blocks = m.p.ws_blocks;
+      else m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
+                                 "ws_blocks > 1 needs ws-dense at one rank and an even ws_size: one block per round";
+    }
     // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)
     m.wscand = dmalloc<uint64_t>((size_t)w.G_all * 2 * kWsCand, &m.bytes);
     m.wsctrl = dmalloc<WsCtrl>(1, &m.bytes);
     // sub-Gram [q_max][q_max] then aux [f | alpha | y]: the first q_max^2 + kWsMax
     // floats are the per-round sum all-reduce at world > 1
-    m.wssub = dmalloc<float>((size_t)ws_q * ws_q + 3 * kWsMax, &m.bytes);
-    HIP_CHECK(hipMemsetAsync(m.wssub, 0, ((size_t)ws_q * ws_q + 3 * kWsMax) * 4, m.stream));
+    // (multi-block: P sub-Grams, then P aux blocks)
+    const size_t sub_floats = (size_t)w.blocks * ((size_t)ws_q * ws_q + 3 * kWsMax);
+    m.wssub = dmalloc<float>(sub_floats, &m.bytes);
+    HIP_CHECK(hipMemsetAsync(m.wssub, 0, sub_floats * 4, m.stream));
     w.cand = m.wscand;
     w.cand_out = m.wscand + (size_t)m.rank * w.G * 2 * kWsCand;
     w.subg = m.wssub;
-    w.aux = m.wssub + (size_t)ws_q * ws_q;
+    w.aux = m.wssub + (size_t)w.blocks * ws_q * ws_q;
+    if (w.blocks > 1) {
+      m.wsdfs = dmalloc<float>((size_t)m.nl, &m.bytes);
+      m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
+      m.wspart = dmalloc<double>((size_t)2 * w.G, &m.bytes);
+      HIP_CHECK(hipMemsetAsync(m.wsdalpha, 0, (size_t)n * 4, m.stream));
+      w.dfs = m.wsdfs;
+      w.dalpha = m.wsdalpha;
+      w.part = m.wspart;
+    }
     w.ctrl = m.wsctrl;
     w.status = m.status_d;
     w.stamps = m.stamps;

@@ -109,6 +109,7 @@ class SVCConfig:
     ws_size: int = 192              # working-set rows (<= 192)
     ws_new: int = 0                 # rows replaced per round (0: 3 ws_size / 4)
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
+    ws_blocks: int = 1              # ws-dense at one rank: sub-problems solved per round (1..4)
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_block: int = 32              # rounds per hipGraph block
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
@@ -170,6 +171,7 @@ class SVCConfig:
         p.ws_size = int(self.ws_size)
         p.ws_new = int(self.ws_new)
         p.ws_rel = float(self.ws_rel)
+        p.ws_blocks = int(self.ws_blocks)
         p.ws_inner = int(self.ws_inner)
         p.ws_block = int(self.ws_block)
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
