@@ -27,7 +27,8 @@ def main() -> int:
     ap.add_argument("--gamma", type=float, default=0.25)
     ap.add_argument("--ws-size", type=int, default=192)
     ap.add_argument("--ws-new", type=int, default=0)
-    ap.add_argument("--ws-rel", type=float, default=0.1)
+    ap.add_argument("--ws-rel", type=float, default=0.3)
+    ap.add_argument("--ws-blocks", type=int, default=1)
     ap.add_argument("--max-iter", type=int, default=10**7)
     ap.add_argument("--cache-lines", type=int, default=0)
     ap.add_argument("--force-cache", action="store_true")
@@ -40,7 +41,7 @@ def main() -> int:
 
     X, y = synthetic(a.data, n=a.samples, d=a.features)
     clf = SVC(C=a.C, gamma=a.gamma, eps=1e-3, device="cuda", solver="ws", ws_size=a.ws_size, ws_new=a.ws_new,
-              ws_rel=a.ws_rel, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache).fit(X, y)
+              ws_rel=a.ws_rel, ws_blocks=a.ws_blocks, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache).fit(X, y)
     raw = np.fromfile(path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
     rounds = min(clf.n_rounds_, 4096)
     s = raw[2:rounds]
@@ -58,9 +59,12 @@ def main() -> int:
         "select_candidates_us": us(s[:, 7] - s[:, 10]),
         "select_end_to_gather_us": us(s[:, 1] - s[:, 7]),
         "merge_us": us(s[:, 2] - s[:, 1]),
-        "merge_phases_us": {"lists_and_stop_test": us(s[:, 11] - s[:, 1]), "radix_thresholds": us(s[:, 12] - s[:, 11]),
-                            "class_compaction": us(s[:, 13] - s[:, 12]), "hash_dedup": us(s[:, 14] - s[:, 13]),
-                            "previous_set": us(s[:, 2] - s[:, 14])},
+        "merge_phases_us": ({"lists_and_stop_test": us(s[:, 11] - s[:, 1]), "radix_thresholds": us(s[:, 12] - s[:, 11]),
+                             "class_compaction": us(s[:, 13] - s[:, 12]), "hash_dedup": us(s[:, 14] - s[:, 13]),
+                             "previous_set": us(s[:, 2] - s[:, 14])} if a.ws_blocks <= 1 else
+                            {"lists_and_sort": us(s[:, 11] - s[:, 1]), "stop_test_hash_insert": us(s[:, 12] - s[:, 11]),
+                             "dedup_compaction": us(s[:, 13] - s[:, 12]), "previous_union": us(s[:, 14] - s[:, 13]),
+                             "block_assignment": us(s[:, 2] - s[:, 14])}),
         "gather_rows_us": us(s[:, 8] - s[:, 2]),
         "gather_end_to_solve_us": us(s[:, 0] - s[:, 8]),
         "load_subgram_us": us(s[:, 3] - s[:, 0]),

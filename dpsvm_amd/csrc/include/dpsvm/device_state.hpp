@@ -218,8 +218,8 @@ constexpr int64_t kWsAutoRows = 100000;  // solver auto: working-set engines fro
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor
 // t = min(1, g'd / d'Qd) of the dual (smo_ws.hip "multi-block rounds")
-constexpr int kWsMaxBlocks = 4;
-constexpr int kWsMaxAll = kWsMaxBlocks * kWsMax;  // union capacity (768)
+constexpr int kWsMaxBlocks = 8;
+constexpr int kWsMaxAll = kWsMaxBlocks * kWsMax;  // union capacity (1536)
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 
 struct alignas(16) WsCtrl {
@@ -252,7 +252,9 @@ struct alignas(16) WsCtrl {
   int32_t pad2[3];
   float t_last;                  // line-search factor of the last applied round
   int32_t n_damped;              // rounds applied with t < 1
-  int32_t pad3[2];
+  int32_t multi_off;             // independent clipping broke sum(alpha y) = 0: one block per round from now on
+  int32_t pad3;
+  int32_t clipb[kWsMaxBlocks];   // per block: a pair step was clipped (independent clipping)
 };
 
 struct WsArgs {

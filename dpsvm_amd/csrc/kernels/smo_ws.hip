@@ -1057,11 +1057,36 @@ __device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
 // of the previous union.  Union position i goes to block ((i / 2) mod P): each
 // block gets up / low pairs, block 0 the global extremes (so a round always
 // holds the maximal violating pair and makes progress).
+constexpr int kMH = 2048;  // merge hash slots per side (load <= 0.28)
+__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 21; }
+__device__ __forceinline__ void mh_insert(int32_t* keys, int32_t* vals, int32_t idx, int32_t v) {
+  uint32_t h = mh_hash(idx);
+  while (true) {
+    const int32_t old = atomicCAS(keys + h, -1, idx);
+    if (old == -1) {
+      vals[h] = v;
+      return;
+    }
+    h = (h + 1) & (kMH - 1);
+  }
+}
+__device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* vals, int32_t idx) {
+  uint32_t h = mh_hash(idx);
+  for (int probe = 0; probe < kMH; ++probe) {
+    const int32_t k = keys[h];
+    if (k == idx) return vals[h];
+    if (k == -1) return -1;
+    h = (h + 1) & (kMH - 1);
+  }
+  return -1;
+}
+
 __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
   constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
-  static_assert(2 * (NK / 2) == kWsMergeThreads, "one comparator per thread and side");
+  static_assert(NK == kWsMergeThreads, "one key per thread and side");
+  static_assert(kWsMaxAll <= 2 * kWsMergeThreads, "previous union: two rows per thread");
   __shared__ uint64_t s_k[2][NK];
-  __shared__ int32_t s_hash[4][kWsHash];
+  __shared__ int32_t s_hash[4][kMH];
   __shared__ int32_t s_keep[kWsMaxAll + 2];
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ int s_wsum[kWsMergeThreads / 64];
@@ -1076,34 +1101,47 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   if (lead) WS_STAMP(1);
   const int G = a.G_all;
   const int par = (int)(c->outer & 1);
-  const int P = a.blocks, Qmax = P * a.q_max;
+  const int P = c->multi_off ? 1 : a.blocks, Qmax = P * a.q_max;
   const int q_prev = c->uq[par ^ 1];
   const int want = q_prev == 0 ? Qmax : min(P * a.n_new, Qmax);
-  const int32_t pidx = tid < q_prev ? c->uidx[par ^ 1][tid] : -1;
+  // the previous union, newest first: thread t holds rows 2t, 2t + 1
+  const int32_t pidx0 = 2 * tid < q_prev ? c->uidx[par ^ 1][2 * tid] : -1;
+  const int32_t pidx1 = 2 * tid + 1 < q_prev ? c->uidx[par ^ 1][2 * tid + 1] : -1;
+  // key t of each side in thread t's registers (list t / 4, rank t % 4)
+  uint64_t v0, v1;
   {
     const int l = tid / kWsCand, r = tid % kWsCand;
-    s_k[0][tid] = l < G ? a.cand[(size_t)l * 2 * kWsCand + r] : kKeyNone;
-    s_k[1][tid] = l < G ? a.cand[(size_t)l * 2 * kWsCand + kWsCand + r] : kKeyNone;
+    v0 = l < G ? a.cand[(size_t)l * 2 * kWsCand + r] : kKeyNone;
+    v1 = l < G ? a.cand[(size_t)l * 2 * kWsCand + kWsCand + r] : kKeyNone;
   }
   if (tid < kWsMaxBlocks) s_qb[tid] = 0;
-  for (int t = tid; t < 4 * kWsHash; t += kWsMergeThreads) (&s_hash[0][0])[t] = -1;
-  __syncthreads();
-  {
-    uint64_t* sk = s_k[tid / (NK / 2)];
-    const int i = tid % (NK / 2);
-    for (int k = 2; k <= NK; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
-        const bool asc = (lo & k) == 0;
-        const uint64_t x = sk[lo], y = sk[hi];
-        if ((x > y) == asc) {
-          sk[lo] = y;
-          sk[hi] = x;
-        }
+  for (int t = tid; t < 4 * kMH; t += kWsMergeThreads) (&s_hash[0][0])[t] = -1;
+  // bitonic sort of both sides, element e in thread e: partner distances < 64
+  // exchange by wave shuffles (no barrier: 45 of the 55 stages), the others
+  // through LDS
+  for (int k = 2; k <= NK; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t p0, p1;
+      if (j >= 64) {
+        s_k[0][tid] = v0;
+        s_k[1][tid] = v1;
         __syncthreads();
+        p0 = s_k[0][tid ^ j];
+        p1 = s_k[1][tid ^ j];
+        __syncthreads();
+      } else {
+        p0 = __shfl_xor(v0, j);
+        p1 = __shfl_xor(v1, j);
       }
+      const bool keep_min = ((tid & k) == 0) == ((tid & j) == 0);
+      v0 = keep_min ? (p0 < v0 ? p0 : v0) : (p0 > v0 ? p0 : v0);
+      v1 = keep_min ? (p1 < v1 ? p1 : v1) : (p1 > v1 ? p1 : v1);
     }
   }
+  s_k[0][tid] = v0;
+  s_k[1][tid] = v1;
+  __syncthreads();
+  if (lead) WS_STAMP(11);
   const uint64_t gu = s_k[0][0], gl = s_k[1][0];
   const float b_hi = key_value(gu), b_lo = -key_value(gl);
   const int64_t it0 = c->iter;
@@ -1128,17 +1166,18 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   int32_t* hk_l = s_hash[2];
   int32_t* hv_l = s_hash[3];
   const int half = (want + 1) / 2;
-  const uint64_t ku = tid < half ? s_k[0][tid] : kKeyNone, kl = tid < half ? s_k[1][tid] : kKeyNone;
-  if (ku != kKeyNone) ws_hash_insert(hk_u, hv_u, (int32_t)key_index(ku), tid);
-  if (kl != kKeyNone) ws_hash_insert(hk_l, hv_l, (int32_t)key_index(kl), tid);
+  const uint64_t ku = tid < half ? v0 : kKeyNone, kl = tid < half ? v1 : kKeyNone;
+  if (ku != kKeyNone) mh_insert(hk_u, hv_u, (int32_t)key_index(ku), tid);
+  if (kl != kKeyNone) mh_insert(hk_l, hv_l, (int32_t)key_index(kl), tid);
   __syncthreads();
+  if (lead) WS_STAMP(12);
   bool kp0 = false, kp1 = false;
   if (ku != kKeyNone) {
-    const int rl = ws_hash_find(hk_l, hv_l, (int32_t)key_index(ku));
+    const int rl = mh_find(hk_l, hv_l, (int32_t)key_index(ku));
     kp0 = !(rl >= 0 && rl < tid);
   }
   if (kl != kKeyNone) {
-    const int ru = ws_hash_find(hk_u, hv_u, (int32_t)key_index(kl));
+    const int ru = mh_find(hk_u, hv_u, (int32_t)key_index(kl));
     kp1 = !(ru >= 0 && ru <= tid);
   }
   int kept = 0;
@@ -1153,26 +1192,34 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     if (c1) s_idx[s1] = (int32_t)key_index(kl);
   }
   __syncthreads();
-  bool pk = false;
-  if (pidx >= 0) {
-    const int ru = ws_hash_find(hk_u, hv_u, pidx), rl = ws_hash_find(hk_l, hv_l, pidx);
-    pk = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+  if (lead) WS_STAMP(13);
+  // previous-union rows not chosen again keep their order after the new rows
+  bool pk0 = false, pk1 = false;
+  if (pidx0 >= 0) {
+    const int ru = mh_find(hk_u, hv_u, pidx0), rl = mh_find(hk_l, hv_l, pidx0);
+    pk0 = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+  }
+  if (pidx1 >= 0) {
+    const int ru = mh_find(hk_u, hv_u, pidx1), rl = mh_find(hk_l, hv_l, pidx1);
+    pk1 = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
   }
   int ptotal = 0;
-  const int pslot = block_scan_merge((int)pk, s_wsum, &ptotal);
-  if (pk && n_chosen + pslot < Qmax) s_idx[n_chosen + pslot] = pidx;
+  const int pslot = block_scan_merge((int)pk0 + (int)pk1, s_wsum, &ptotal);
+  if (pk0 && n_chosen + pslot < Qmax) s_idx[n_chosen + pslot] = pidx0;
+  if (pk1 && n_chosen + pslot + (int)pk0 < Qmax) s_idx[n_chosen + pslot + (int)pk0] = pidx1;
   const int Q = min(Qmax, n_chosen + ptotal);
   __syncthreads();
-  if (tid < Q) {
-    const int32_t row = s_idx[tid];
-    c->uidx[par][tid] = row;
-    const int pi = tid >> 1, b = pi % P, la = 2 * (pi / P) + (tid & 1);
+  if (lead) WS_STAMP(14);
+  for (int u = tid; u < Q; u += kWsMergeThreads) {
+    const int32_t row = s_idx[u];
+    c->uidx[par][u] = row;
+    const int pi = u >> 1, b = pi % P, la = 2 * (pi / P) + (u & 1);
     c->idx[par][b * a.q_max + la] = row;
     c->line[par][b * a.q_max + la] = row;  // the resident Gram: line i is row i
     atomicMax(&s_qb[b], la + 1);
   }
   __syncthreads();
-  if (tid < P) c->qb[par][tid] = s_qb[tid];
+  if (tid < a.blocks) c->qb[par][tid] = s_qb[tid];  // inactive blocks: 0 rows
   if (lead) {
     c->uq[par] = Q;
     c->q[par] = Q;
@@ -1252,7 +1299,7 @@ __device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, 
 // sequence is the longest dependent chain of a step.
 template <bool kBox>
 __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float y_hi, float y_lo, float bh, float bl,
-                                                   float khl, float C, float tau, bool same) {
+                                                   float khl, float C, float tau, bool same, bool* clipped) {
 #pragma clang fp contract(off)
   float eta = (1.0f + 1.0f) - 2.0f * khl;
   eta = eta >= tau ? eta : tau;
@@ -1283,8 +1330,10 @@ __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float
     a_hi_new = clip01(a_hi_new, 0.0f, C);
   } else {
     a_hi_new = a_hi + (s * (a_lo - a_lo_new));
+    const float lo_raw = a_lo_new, hi_raw = a_hi_new;
     a_lo_new = clip01(a_lo_new, 0.0f, C);
     a_hi_new = clip01(a_hi_new, 0.0f, C);
+    *clipped = (lo_raw != a_lo_new) | (hi_raw != a_hi_new);  // sum(alpha y) no longer kept
   }
   PairUpdate u;
   u.a_hi_new = a_hi_new;
@@ -1385,11 +1434,14 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     fl[s] = v && in_low(a0[s], yr[s], C) ? -fv : INF;
   }
   int64_t room = a.max_iter - it0;
-  if (kMulti) room = room / a.blocks + (blk < room % a.blocks ? 1 : 0);  // the blocks share max_iter
+  if (kMulti) {  // the active blocks share max_iter
+    const int pa = c->multi_off ? 1 : a.blocks;
+    room = blk < pa ? room / pa + (blk < room % pa ? 1 : 0) : 0;
+  }
   // uniform: in an SGPR, so the loop test is one scalar compare
   const int cap = __builtin_amdgcn_readfirstlane((int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max));
   int inner = 0;
-  bool bad = false;
+  bool bad = false, clipped_any = false;
   while (inner < cap) {
     float mu = fminf(fminf(fu[0], fu[1]), fu[2]);
     float ml = fminf(fminf(fl[0], fl[1]), fl[2]);
@@ -1413,7 +1465,9 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       kh[s] = K[ph * ldk + p];
       kl[s] = K[pl * ldk + p];
     }
-    const PairUpdate up = ws_pair_step<kBox>(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, ph == pl);
+    bool clipped = false;
+    const PairUpdate up = ws_pair_step<kBox>(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, ph == pl, &clipped);
+    if (kMulti && !kBox) clipped_any |= clipped;
     float f_lo_new, f_hi_new;
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
@@ -1479,17 +1533,23 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     c->nab[blk] = n_apply;
     c->inb[blk] = inner;
     c->badb[blk] = bad ? 1 : 0;
+    c->clipb[blk] = clipped_any ? 1 : 0;
     __threadfence();
     const int prev = atomicAdd(&c->solve_cnt, 1);
     if (prev == a.blocks - 1) {
       __threadfence();
-      int tot_a = 0, tot_i = 0, any_bad = 0;
+      int tot_a = 0, tot_i = 0, any_bad = 0, any_clip = 0;
       for (int p = 0; p < a.blocks; ++p) {
         tot_a += __hip_atomic_load(&c->nab[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tot_i += __hip_atomic_load(&c->inb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         any_bad |= __hip_atomic_load(&c->badb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        any_clip |= __hip_atomic_load(&c->clipb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       c->solve_cnt = 0;
+      // the reference's independent clipping does not keep sum(alpha y) = 0: once
+      // a clip broke it, the blocks' combined steps drift it further (measured:
+      // adult-shape P = 8 never converges) — one block per round from here on
+      if (any_clip) c->multi_off = 1;
       WS_STAMP(4);
       if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + 5] = (uint64_t)tot_i;
       c->n_apply = tot_a;

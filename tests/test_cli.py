@@ -68,14 +68,14 @@ def test_svmtrain_params_roundtrip_new_knobs(tmp_path, bin_dir):
     js, js2 = str(tmp_path / "a.json"), str(tmp_path / "b.json")
     base = [os.path.join(bin_dir, "svmTrain"), "-a", "5", "-x", "400", "-f", p, "-c", "2", "-g", "0.4",
             "-m", str(tmp_path / "m.txt"), "--cpu"]
-    r = run(base + ["--eta", "gram", "--exchange", "peer", "--metrics-json", js])
+    r = run(base + ["--eta", "gram", "--exchange", "peer", "--ws-blocks", "4", "--metrics-json", js])
     assert r.returncode == 0, r.stderr
     pa = json.load(open(js))["params"]
-    assert pa["eta"] == 1 and pa["exchange"] == 2
+    assert pa["eta"] == 1 and pa["exchange"] == 2 and pa["ws_blocks"] == 4
     r = run(base + ["--params-json", js, "--metrics-json", js2])
     assert r.returncode == 0, r.stderr
     pb = json.load(open(js2))["params"]
-    assert pb["eta"] == 1 and pb["exchange"] == 2
+    assert pb["eta"] == 1 and pb["exchange"] == 2 and pb["ws_blocks"] == 4
 
 
 def test_svmseq_and_svmtest(tmp_path, bin_dir):

@@ -346,3 +346,61 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine, n):
         assert res[k]["alpha_sha"] == sha
     if n > 6000:  # 2 x 137 selection workgroups: the merge folds two candidate lists per thread
         assert ref[0].setup_info_["groups"] * world > 256
+
+
+@pytest.mark.parametrize("blocks", [2, 8])
+@pytest.mark.parametrize("clip", ["independent", "box"])
+@pytest.mark.parametrize("case", ["blobs", "mnist", "adult"])
+def test_ws_multi_block_rounds_reach_the_reference_optimum(case, clip, blocks):
+    """ws_blocks = P: P disjoint sub-problems per round, the combined step scaled
+    by the exact line search (smo_ws.hip, multi-block rounds).  Coupled problems
+    (blobs, adult: K far from I) exercise t < 1; the stop test must hold on the
+    exact float64 gradient and, with box clipping, the unique dual optimum must
+    be reached."""
+    from ref_smo import smo_reference, decision
+
+    X, y, C_, g = {
+        "blobs": synthetic("blobs", n=2500, d=12, seed=41, sep=1.2) + (2.0, 0.15),
+        "mnist": synthetic("mnist", n=3000, seed=4) + (10.0, 0.25),
+        "adult": synthetic("adult", n=3000, seed=2) + (1.0, 0.05),
+    }[case]
+    a_ref, b_ref, it_ref = smo_reference(X, y, C=C_, gamma=g, eps=1e-3, clip=clip)
+    ws = SVC(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", solver="ws", ws_blocks=blocks).fit(X, y)
+    assert ws.setup_info_["iteration"] == "ws-dense" and "ws_blocks" not in ws.setup_info_.get("engine_note", "")
+    assert ws.converged_
+    gap = _kkt_gap(X, y, ws.alpha_, C_, g)
+    yy = np.where(y > 0, 1.0, -1.0)
+    d_ref = decision(X, y, a_ref, b_ref, g, X)
+    d_ws = ws.decision_function(X)
+    acc_ref, acc_ws = np.mean(np.sign(d_ref) == yy), np.mean(np.sign(d_ws) == yy)
+    agree = np.mean(np.sign(d_ref) == np.sign(d_ws))
+    print(f"P={blocks} {case}/{clip}: gap {gap:.2e} b {ws.b_:.5f} vs {b_ref:.5f} steps {ws.n_iter_} vs {it_ref} "
+          f"rounds {ws.n_rounds_} acc {acc_ws:.4f} vs {acc_ref:.4f} agree {agree:.4f}")
+    assert gap < 2e-3 + 2e-4
+    assert np.all((ws.alpha_ >= 0) & (ws.alpha_ <= C_))
+    assert abs(acc_ws - acc_ref) < 0.02
+    if clip == "box":
+        assert abs(float(np.sum(ws.alpha_ * yy))) < 1e-2 * C_  # the line search keeps sum(alpha y)
+        assert abs(ws.b_ - b_ref) < 1e-2
+        assert np.abs(ws.alpha_ - a_ref).max() < 0.1 * C_
+        assert agree > 0.99
+
+
+def test_ws_multi_block_deterministic_max_iter_and_fallback():
+    X, y = synthetic("adult", n=4000, seed=9)
+    kw = dict(C=1.0, gamma=0.05, eps=1e-3, device="cuda", solver="ws", ws_blocks=4)
+    a = SVC(**kw).fit(X, y)
+    b = SVC(**kw).fit(X, y)
+    assert a.converged_ and a.n_iter_ == b.n_iter_ and np.array_equal(a.alpha_, b.alpha_)
+    # fewer rounds where the blocks decouple (K ~ I, no clipping: the headline's regime)
+    Xm, ym = synthetic("mnist", n=20000, seed=5)
+    km = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws")
+    m4, m1 = SVC(ws_blocks=4, **km).fit(Xm, ym), SVC(ws_blocks=1, **km).fit(Xm, ym)
+    assert m4.converged_ and m1.converged_ and m4.n_rounds_ < 0.5 * m1.n_rounds_
+    assert abs(m4.b_ - m1.b_) < 2e-3 and abs(m4.train_accuracy() - m1.train_accuracy()) < 0.005
+    capped = SVC(max_iter=700, **kw).fit(X, y)  # the blocks share the pair-step budget exactly
+    assert not capped.converged_ and capped.n_iter_ == 700
+    # ineligible engine (kernel-row cache): one block per round, said so
+    c = SVC(cache_lines=900, force_cache=True, **kw).fit(X, y)
+    assert c.setup_info_["iteration"] == "ws-cache" and "ws_blocks" in c.setup_info_["engine_note"]
+    assert c.converged_
