@@ -299,7 +299,9 @@ struct WsArgs {
   int32_t blocks;
   float* dfs;          // [nl] the round's f change before the line search
   float* dalpha;       // [n] alpha_new - alpha_old of the round's changed rows (0 elsewhere)
-  double* part;        // [G][2] per-workgroup partial sums: d'Qd, -g'd
+  double* part;        // [G_all][2] per-workgroup partial sums: d'Qd, g'd (this rank's at rank * G)
+  int32_t rank;        // this rank (its partials slot)
+  int32_t aux_stride;  // aux: [3][blocks][kWsMax] (f of every block first: one sum all-reduce with subg)
 };
 // u64 words of the working-set exchange region (both parities)
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {

@@ -71,6 +71,9 @@ void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uin
 bool ws_supported(int64_t nl_max, int world, int q_max);
 void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt);
 void ws_select(const WsArgs& a, hipStream_t s);
+// multi-block rounds: pass 1 (d_f + line-search partials), pass 2 (apply, candidates); at
+// world > 1 the partials are all-gathered between them
+void ws_select_pass(const WsArgs& a, int pass, hipStream_t s);
 void ws_gather(const WsArgs& a, hipStream_t s);
 void ws_solve(const WsArgs& a, hipStream_t s);
 // cache mode: the merge + line assignment (one workgroup) runs before the

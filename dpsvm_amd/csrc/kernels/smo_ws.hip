@@ -293,7 +293,7 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 __device__ __forceinline__ float ws_line_search(const WsArgs& a) {
   const int lane = threadIdx.x & 63;
   double q = 0.0, g = 0.0;
-  for (int k = lane; k < a.G; k += 64) {
+  for (int k = lane; k < a.G_all; k += 64) {  // every rank's partials (all-gathered)
     q += a.part[2 * k];
     g += a.part[2 * k + 1];
   }
@@ -438,8 +438,8 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
           tq += s_red[0][k];
           tg += s_red[1][k];
         }
-        a.part[2 * blockIdx.x] = tq;
-        a.part[2 * blockIdx.x + 1] = tg;
+        a.part[2 * ((int64_t)a.rank * a.G + blockIdx.x)] = tq;
+        a.part[2 * ((int64_t)a.rank * a.G + blockIdx.x) + 1] = tg;
       }
       return;
     }
@@ -448,6 +448,19 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         c->t_last = t;
         if (t < 1.f) c->n_damped = c->n_damped + 1;
+      }
+      if (a.world > 1 && blockIdx.x == 0) {
+        // alpha is global on every rank: the changed rows this rank does not own
+        // (its threads below fix the owned ones before classifying them)
+        for (int p = 0; p < a.blocks; ++p) {
+          const int nb = c->nab[p];
+          for (int k = threadIdx.x; k < nb; k += kWsSelThreads * PARTS) {
+            const int64_t gi = c->apply_idx[p * a.q_max + k];
+            if (gi >= a.off && gi < a.off + a.nl) continue;
+            if (t < 1.f) a.alpha[gi] = clip01(a.alpha[gi] - (1.f - t) * a.dalpha[gi], 0.f, a.C);
+            a.dalpha[gi] = 0.f;
+          }
+        }
       }
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
@@ -870,8 +883,8 @@ __device__ __forceinline__ void ws_gather_row(const WsArgs& a, WsCtrl* c, const 
       dst[tid] = 0.f;
     }
     if (tid == 0) {
-      a.aux[kWsMax + ra] = a.alpha[gi];
-      a.aux[2 * kWsMax + ra] = a.y[gi];
+      a.aux[a.aux_stride + ra] = a.alpha[gi];
+      a.aux[2 * a.aux_stride + ra] = a.y[gi];
     }
     if (!__syncthreads_and(ok)) ws_comm_fail(a, c);
     return;
@@ -883,8 +896,8 @@ __device__ __forceinline__ void ws_gather_row(const WsArgs& a, WsCtrl* c, const 
   if (tid == 0) {
     const int64_t gi = s_idx[ra];
     a.aux[ra] = gi >= lo && gi < hi ? a.f[gi - lo] : 0.f;
-    a.aux[kWsMax + ra] = a.alpha[gi];
-    a.aux[2 * kWsMax + ra] = a.y[gi];
+    a.aux[a.aux_stride + ra] = a.alpha[gi];
+    a.aux[2 * a.aux_stride + ra] = a.y[gi];
   }
 }
 
@@ -1241,7 +1254,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArg
   const int q = c->qb[par][p];
   WsArgs b = a;
   b.subg = a.subg + (size_t)p * a.q_max * a.q_max;
-  b.aux = a.aux + (size_t)p * 3 * kWsMax;
+  b.aux = a.aux + (size_t)p * kWsMax;  // f / alpha / y of block p at stride aux_stride
   if (ra >= q) {
     ws_gather_row(b, c, s_idx, q, ra, nullptr);
     return;
@@ -1384,7 +1397,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const int ldk = a.q_max;  // LDS keeps the q_max stride: the load is one contiguous copy
   const int ib = blk * a.q_max;
   const float* subg = a.subg + (size_t)blk * ldk * ldk;
-  const float* aux = a.aux + (size_t)blk * 3 * kWsMax;
+  const float* aux = a.aux + (size_t)blk * kWsMax;
   {
     // q rows of the q_max-stride sub-Gram into LDS (147 KiB at q = 192): 16-B
     // loads, four in flight per thread before their stores
@@ -1409,8 +1422,8 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     }
     if (tid < q) {
       s_f[tid] = aux[tid];
-      s_a[tid] = aux[kWsMax + tid];
-      s_y[tid] = aux[2 * kWsMax + tid];
+      s_a[tid] = aux[a.aux_stride + tid];
+      s_y[tid] = aux[2 * a.aux_stride + tid];
       s_idx[tid] = c->idx[par][ib + tid];
       s_line[tid] = c->line[par][ib + tid];
     }
@@ -1626,10 +1639,15 @@ void ws_select(const WsArgs& a, hipStream_t s) {
   }
 }
 
+void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
+  if (pass == 1) ws_select_mode<1>(a, s);
+  else ws_select_mode<2>(a, s);
+}
+
 void ws_merge_multi(const WsArgs& a, hipStream_t s) {
-  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.world == 1 && !a.cache && a.G_all <= kWsMaxGroups &&
+  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && !a.cache && !a.xpeer && a.G_all <= kWsMaxGroups &&
                   a.q_max % 2 == 0,
-              "ws_merge_multi: multi-block rounds need ws-dense at one rank and an even q_max");
+              "ws_merge_multi: multi-block rounds need ws-dense over collectives, <= 256 candidate lists, even q_max");
   dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
   post_launch("ws_merge_multi", s);
 }

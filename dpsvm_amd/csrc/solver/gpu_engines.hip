@@ -307,9 +307,27 @@ void ws_allgather_cand(GpuSolver::Impl& m) {
   HIP_CHECK(hipMemcpyAsync(m.wsa.cand, m.h_wscand.data(), bytes * m.world, hipMemcpyHostToDevice, m.stream));
 }
 
+// multi-block rounds at world > 1: every rank's line-search partials
+void ws_allgather_part(GpuSolver::Impl& m) {
+  if (!m.collectives()) return;
+  const size_t bytes = (size_t)m.wsa.G * 2 * sizeof(double);
+  uint8_t* all = (uint8_t*)m.wsa.part;
+  if (m.comm->device_memory()) {
+    m.comm->allgather(all + (size_t)m.rank * bytes, all, bytes, m.stream);
+    return;
+  }
+  m.h_wspart.resize(bytes * m.world);
+  uint8_t* mine = m.h_wspart.data() + (size_t)m.rank * bytes;
+  HIP_CHECK(hipMemcpyAsync(mine, all + (size_t)m.rank * bytes, bytes, hipMemcpyDeviceToHost, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  m.comm->allgather(mine, m.h_wspart.data(), bytes, nullptr);
+  HIP_CHECK(hipMemcpyAsync(all, m.h_wspart.data(), bytes * m.world, hipMemcpyHostToDevice, m.stream));
+}
+
 void ws_allreduce_sub(GpuSolver::Impl& m) {
   if (!m.collectives() || m.wsa.xpeer) return;  // peer exchange: assembled by the gather kernel
-  const size_t count = (size_t)m.wsa.q_max * m.wsa.q_max + kWsMax;  // sub-Gram + the members' f
+  // the P sub-Grams + the members' f of every block ([3][P][kWsMax] aux: f first)
+  const size_t count = (size_t)m.wsa.blocks * ((size_t)m.wsa.q_max * m.wsa.q_max + kWsMax);
   if (m.comm->device_memory()) {
     m.comm->allreduce_sum_f32(m.wssub, count, m.stream);
     return;
@@ -355,7 +373,13 @@ struct WsDense final : DenseBase {
     launch::ws_gather(m.wsa, m.stream);
     ws_allreduce_sub(m);
     launch::ws_solve(m.wsa, m.stream);
-    launch::ws_select(m.wsa, m.stream);
+    if (m.wsa.blocks > 1) {
+      launch::ws_select_pass(m.wsa, 1, m.stream);
+      ws_allgather_part(m);
+      launch::ws_select_pass(m.wsa, 2, m.stream);
+    } else {
+      launch::ws_select(m.wsa, m.stream);
+    }
     ws_allgather_cand(m);
   }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {

@@ -104,6 +104,7 @@ struct GpuSolver::Impl {
   int32_t* wsiota = nullptr;                  //   (their GEMM row indices: 0..q_max-1)
   std::vector<uint8_t> h_wscand;   // host staging of the per-round collectives (host communicators)
   std::vector<float> h_wssub, h_wsxq;
+  std::vector<uint8_t> h_wspart;
   uint64_t* stamps = nullptr;      // DPSVM_STAMPS diagnostics
   std::string stamps_path;
   std::vector<uint64_t> h_partials;  // host staging for host-memory communicators

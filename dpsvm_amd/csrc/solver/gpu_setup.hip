@@ -433,10 +433,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // working-set engines at world > 1: the rounds' candidate lists and sub-Gram
   // rows through the same kind of receive buffers (smo_ws.hip, "peer exchange")
   const bool wsc_fits_pre = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
-  const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives &&
-                           (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
   int32_t ws_G = 0, ws_rpt = 0;
   if (ws_cand || wsc_cand) launch::ws_geometry(nl_max, m.world, &ws_G, &ws_rpt);
+  // multi-block rounds (ws_blocks > 1): ws-dense, the union merge reads <= 256
+  // candidate lists, an even q_max; at world > 1 over the collectives (their
+  // extra per-round all-gather of line-search partials has no peer-exchange form)
+  DPSVM_CHECK(m.p.ws_blocks >= 0 && m.p.ws_blocks <= kWsMaxBlocks, "ws_blocks must be in 1.." + std::to_string(kWsMaxBlocks));
+  const bool multi_ok = m.p.ws_blocks > 1 && ws_cand && ws_q % 2 == 0 && (int64_t)ws_G * m.world <= kWsMaxGroups &&
+                        m.p.exchange != 2;
+  const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives && !multi_ok &&
+                           (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
   if (want_ws_xch) {
     const bool ok = m.setup_exchange(ws_xch_words((int64_t)ws_G * m.world, ws_q));
     DPSVM_CHECK(ok || m.p.exchange != 2,
@@ -530,12 +536,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // every rank solving the whole problem), an even q_max
     w.blocks = 1;
     if (m.p.ws_blocks > 1) {
-      DPSVM_CHECK(m.p.ws_blocks <= kWsMaxBlocks, "ws_blocks must be in 1.." + std::to_string(kWsMaxBlocks));
-      const bool ok = m.kind == EngineKind::WsDense && m.world == 1 && !m.xch && ws_q % 2 == 0 && !m.p.force_collectives;
-      if (ok) w.blocks = m.p.ws_blocks;
+      if (multi_ok && m.kind == EngineKind::WsDense && !m.xch) w.blocks = m.p.ws_blocks;
       else m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
-                                 "ws_blocks > 1 needs ws-dense at one rank and an even ws_size: one block per round";
+                                 "ws_blocks > 1 needs ws-dense, an even ws_size and <= 256 candidate lists over "
+                                 "the collectives: one block per round";
     }
+    w.rank = m.rank;
+    w.aux_stride = w.blocks * kWsMax;
     // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)
     m.wscand = dmalloc<uint64_t>((size_t)w.G_all * 2 * kWsCand, &m.bytes);
     m.wsctrl = dmalloc<WsCtrl>(1, &m.bytes);
@@ -552,7 +559,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     if (w.blocks > 1) {
       m.wsdfs = dmalloc<float>((size_t)m.nl, &m.bytes);
       m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
-      m.wspart = dmalloc<double>((size_t)2 * w.G, &m.bytes);
+      m.wspart = dmalloc<double>((size_t)2 * w.G_all, &m.bytes);
       HIP_CHECK(hipMemsetAsync(m.wsdalpha, 0, (size_t)n * 4, m.stream));
       w.dfs = m.wsdfs;
       w.dalpha = m.wsdalpha;

@@ -404,3 +404,43 @@ def test_ws_multi_block_deterministic_max_iter_and_fallback():
     c = SVC(cache_lines=900, force_cache=True, **kw).fit(X, y)
     assert c.setup_info_["iteration"] == "ws-cache" and "ws_blocks" in c.setup_info_["engine_note"]
     assert c.converged_
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ws_multi_block_sharded_ranks(world):
+    """Multi-block rounds with rows sharded over ranks (threads sharing the GPU,
+    host-staged collectives): candidate lists all-gathered, the P sub-Grams and
+    the members' f summed from the owners' columns, the line-search partials
+    all-gathered between the two f-update passes.  Every rank ends with the same
+    alphas and the run reaches the one-rank optimum (box clipping)."""
+    from dpsvm_amd._native import load
+
+    X, y = synthetic("adult", n=4000, seed=13)
+    kw = dict(C=1.0, gamma=0.05, eps=1e-3, clip="box", device="cuda", solver="ws", dp="shard", ws_blocks=4)
+    ref = SVC(**kw).fit(X, y)
+    out = _fit_threads(load(), world, X, y, **kw)
+    for r in range(world):
+        assert out[r].setup_info_["iteration"] == "ws-dense" and out[r].setup_info_["n_local"] < 4000
+        assert "ws_blocks" not in out[r].setup_info_.get("engine_note", "")
+        assert out[r].converged_
+        assert np.array_equal(out[r].alpha_, out[0].alpha_)
+    assert _kkt_gap(X, y, out[0].alpha_, 1.0, 0.05) < 2.2e-3
+    assert abs(out[0].b_ - ref.b_) < 1e-2
+    assert abs(out[0].n_support_ - ref.n_support_) <= max(3, ref.n_support_ // 50)
+
+
+def test_ws_multi_block_rccl_one_rank_collective_path():
+    """Multi-block rounds over a one-rank RCCL communicator (force_collectives:
+    sub-Gram sum, partials and candidate all-gathers captured in the round
+    graph): bit-identical to the local path."""
+    from dpsvm_amd._native import load
+
+    C = load()
+    X, y = synthetic("mnist", n=8000, seed=3)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws", ws_blocks=4)
+    ref = SVC(**kw).fit(X, y)
+    comm = C.rccl_comm(C.rccl_unique_id(), 0, 1, 0)
+    got = SVC(force_collectives=True, **kw).fit(X, y, comm=comm)
+    assert "ws_blocks" not in got.setup_info_.get("engine_note", "")
+    assert got.n_iter_ == ref.n_iter_ and got.n_rounds_ == ref.n_rounds_
+    assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
