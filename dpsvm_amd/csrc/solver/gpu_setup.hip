@@ -541,6 +541,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                                  "ws_blocks > 1 needs ws-dense, an even ws_size and <= 256 candidate lists over "
                                  "the collectives: one block per round";
     }
+    // multi-block rounds replace the whole union each round by default (measured on the
+    // headline at P = 8: 3/4 q new 0.0506 s, all new 0.0493 s; profiles/r2_ws_blocks_sweep.txt)
+    if (w.blocks > 1 && m.p.ws_new <= 0) w.n_new = ws_q;
     w.rank = m.rank;
     w.aux_stride = w.blocks * kWsMax;
     // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)
