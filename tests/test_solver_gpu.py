@@ -499,19 +499,23 @@ def test_bench_multi_gpu_ws_sharded_and_default(tmp_path):
     replicates on distinct GPUs and its untimed sharded check succeeds."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     world = 2 if _SHARED else min(_NDEV, 8)
-    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws").fit(*synthetic("mnist", n=8000, d=784, seed=0))
+    # bench.py's default: 8 sub-problems per round (multi-block rounds); sharded
+    # ranks read other candidate lists than one GPU, so b agrees to the stop gap
+    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws",
+              ws_blocks=8).fit(*synthetic("mnist", n=8000, d=784, seed=0))
     out = _bench_multi(root, world, ["--dp", "shard"], 29661)
     assert out["iteration"] == "ws-dense" and out["dp_policy"] == "shard" and out["converged"]
-    assert abs(out["b"] - ref.b_) < 1e-3 and abs(out["n_sv"] - ref.n_support_) <= 8
+    assert out["params"]["ws_blocks"] == 8 and "ws_blocks" not in out["engine_note"]
+    assert abs(out["b"] - ref.b_) < 2e-3 and abs(out["n_sv"] - ref.n_support_) <= 8
     if _NDEV >= 2:
         dflt = _bench_multi(root, world, [], 29671)
         assert dflt["dp_autotune"]["chosen"] == dflt["dp_policy"]
         if dflt["dp_policy"] == "replicate":
             assert dflt["iterations"] == ref.n_iter_ and dflt["b"] == ref.b_
-        assert abs(dflt["b"] - ref.b_) < 1e-3
+        assert abs(dflt["b"] - ref.b_) < 2e-3
         sc = dflt["shard_check"]
         assert sc and "error" not in sc and sc["engine"] == "ws-dense", sc
-        assert abs(sc["b"] - ref.b_) < 1e-3
+        assert abs(sc["b"] - ref.b_) < 2e-3
 
 
 def test_bench_two_processes_measured_dp_policy(tmp_path):
