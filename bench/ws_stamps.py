@@ -62,7 +62,8 @@ def main() -> int:
         "merge_phases_us": ({"lists_and_stop_test": us(s[:, 11] - s[:, 1]), "radix_thresholds": us(s[:, 12] - s[:, 11]),
                              "class_compaction": us(s[:, 13] - s[:, 12]), "hash_dedup": us(s[:, 14] - s[:, 13]),
                              "previous_set": us(s[:, 2] - s[:, 14])} if a.ws_blocks <= 1 else
-                            {"lists_and_sort": us(s[:, 11] - s[:, 1]), "stop_test_hash_insert": us(s[:, 12] - s[:, 11]),
+                            {"loads_and_hash_init": us(s[:, 20] - s[:, 1]), "sort_k_le_64": us(s[:, 21] - s[:, 20]),
+                             "sort_k_gt_64": us(s[:, 11] - s[:, 21]), "lists_and_sort": us(s[:, 11] - s[:, 1]), "stop_test_hash_insert": us(s[:, 12] - s[:, 11]),
                              "dedup_compaction": us(s[:, 13] - s[:, 12]), "previous_union": us(s[:, 14] - s[:, 13]),
                              "block_assignment": us(s[:, 2] - s[:, 14])}),
         "gather_rows_us": us(s[:, 8] - s[:, 2]),

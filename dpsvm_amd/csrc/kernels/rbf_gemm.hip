@@ -42,7 +42,7 @@ enum Epi { EPI_STORE = 0, EPI_PREDICT = 1, EPI_ROWS = 2 };
 //   < 32, 1, 4>   32x512, waves 1x4     ROWS variant padding rows to 32 (measured
 //                                       slower than 64x256, not launched)
 template <int EPI, int TM = 128, int MI = 2, int NJ = 2>
-__global__ __launch_bounds__(GEMM_THREADS, 2) void rbf_gemm_kernel(
+__global__ __launch_bounds__(GEMM_THREADS, EPI == EPI_STORE ? 3 : 2) void rbf_gemm_kernel(
     const float* __restrict__ A, const float* __restrict__ Asq, int64_t M, int lda,
     const float* __restrict__ B, const float* __restrict__ Bsq, int64_t N, int ldb, int dp,
     float gamma, float* __restrict__ out, int64_t ldo, const float* __restrict__ coef,

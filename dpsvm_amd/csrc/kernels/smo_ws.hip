@@ -1129,6 +1129,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   }
   if (tid < kWsMaxBlocks) s_qb[tid] = 0;
   for (int t = tid; t < 4 * kMH; t += kWsMergeThreads) (&s_hash[0][0])[t] = -1;
+  if (lead) WS_STAMP(20);
   // bitonic sort of both sides, element e in thread e: partner distances < 64
   // exchange by wave shuffles (no barrier: 45 of the 55 stages), the others
   // through LDS
@@ -1150,6 +1151,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
       v0 = keep_min ? (p0 < v0 ? p0 : v0) : (p0 > v0 ? p0 : v0);
       v1 = keep_min ? (p1 < v1 ? p1 : v1) : (p1 > v1 ? p1 : v1);
     }
+    if (k == 64 && lead) WS_STAMP(21);
   }
   s_k[0][tid] = v0;
   s_k[1][tid] = v1;
@@ -1207,19 +1209,22 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   __syncthreads();
   if (lead) WS_STAMP(13);
   // previous-union rows not chosen again keep their order after the new rows
+  // (uniform skip when the new rows already fill the union)
   bool pk0 = false, pk1 = false;
-  if (pidx0 >= 0) {
+  if (n_chosen < Qmax && pidx0 >= 0) {
     const int ru = mh_find(hk_u, hv_u, pidx0), rl = mh_find(hk_l, hv_l, pidx0);
     pk0 = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
   }
-  if (pidx1 >= 0) {
+  if (n_chosen < Qmax && pidx1 >= 0) {
     const int ru = mh_find(hk_u, hv_u, pidx1), rl = mh_find(hk_l, hv_l, pidx1);
     pk1 = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
   }
   int ptotal = 0;
-  const int pslot = block_scan_merge((int)pk0 + (int)pk1, s_wsum, &ptotal);
-  if (pk0 && n_chosen + pslot < Qmax) s_idx[n_chosen + pslot] = pidx0;
-  if (pk1 && n_chosen + pslot + (int)pk0 < Qmax) s_idx[n_chosen + pslot + (int)pk0] = pidx1;
+  if (n_chosen < Qmax) {  // uniform
+    const int pslot = block_scan_merge((int)pk0 + (int)pk1, s_wsum, &ptotal);
+    if (pk0 && n_chosen + pslot < Qmax) s_idx[n_chosen + pslot] = pidx0;
+    if (pk1 && n_chosen + pslot + (int)pk0 < Qmax) s_idx[n_chosen + pslot + (int)pk0] = pidx1;
+  }
   const int Q = min(Qmax, n_chosen + ptotal);
   __syncthreads();
   if (lead) WS_STAMP(14);
