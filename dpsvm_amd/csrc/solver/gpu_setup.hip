@@ -439,8 +439,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // candidate lists, an even q_max; at world > 1 over the collectives (their
   // extra per-round all-gather of line-search partials has no peer-exchange form)
   DPSVM_CHECK(m.p.ws_blocks >= 0 && m.p.ws_blocks <= kWsMaxBlocks, "ws_blocks must be in 1.." + std::to_string(kWsMaxBlocks));
+  // host communicators stage every collective through host memory (three per
+  // round): there the one-block rounds over the in-kernel peer exchange are
+  // faster (2 processes on one GPU: 0.163 vs 0.198 s), so multi-block rounds at
+  // world > 1 need a device communicator (RCCL) or exchange=allreduce
+  const bool multi_comm = m.world == 1 || m.comm->device_memory() || m.p.exchange == 1;
   const bool multi_ok = m.p.ws_blocks > 1 && ws_cand && ws_q % 2 == 0 && (int64_t)ws_G * m.world <= kWsMaxGroups &&
-                        m.p.exchange != 2;
+                        m.p.exchange != 2 && multi_comm;
   const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives && !multi_ok &&
                            (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
   if (want_ws_xch) {

@@ -418,7 +418,9 @@ def test_ws_multi_block_sharded_ranks(world):
     X, y = synthetic("adult", n=4000, seed=13)
     kw = dict(C=1.0, gamma=0.05, eps=1e-3, clip="box", device="cuda", solver="ws", dp="shard", ws_blocks=4)
     ref = SVC(**kw).fit(X, y)
-    out = _fit_threads(load(), world, X, y, **kw)
+    # host communicators take multi-block rounds only with exchange=allreduce
+    # (else the one-block rounds over the peer exchange)
+    out = _fit_threads(load(), world, X, y, exchange="allreduce", **kw)
     for r in range(world):
         assert out[r].setup_info_["iteration"] == "ws-dense" and out[r].setup_info_["n_local"] < 4000
         assert "ws_blocks" not in out[r].setup_info_.get("engine_note", "")
