@@ -221,6 +221,7 @@ constexpr int64_t kWsAutoRows = 100000;  // solver auto: working-set engines fro
 constexpr int kWsMaxBlocks = 8;
 constexpr int kWsMaxAll = kWsMaxBlocks * kWsMax;  // union capacity (1536)
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
+constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: kWsMaxBlocks from this many rows on
 
 struct alignas(16) WsCtrl {
   int64_t iter;      // pair updates applied so far

@@ -444,7 +444,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // faster (2 processes on one GPU: 0.163 vs 0.198 s), so multi-block rounds at
   // world > 1 need a device communicator (RCCL) or exchange=allreduce
   const bool multi_comm = m.world == 1 || m.comm->device_memory() || m.p.exchange == 1;
-  const bool multi_ok = m.p.ws_blocks > 1 && ws_cand && ws_q % 2 == 0 && (int64_t)ws_G * m.world <= kWsMaxGroups &&
+  // ws_blocks auto (0): every block from kWsAutoBlocksRows rows on (the round's
+  // fixed cost is amortised over P sub-problems; small problems need few rounds)
+  const int want_blocks = m.p.ws_blocks > 0 ? m.p.ws_blocks : (n >= kWsAutoBlocksRows ? kWsMaxBlocks : 1);
+  const bool multi_ok = want_blocks > 1 && ws_cand && ws_q % 2 == 0 && (int64_t)ws_G * m.world <= kWsMaxGroups &&
                         m.p.exchange != 2 && multi_comm;
   const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives && !multi_ok &&
                            (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
@@ -540,9 +543,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // multi-block rounds: ws-dense with no per-round communication (world 1 or
     // every rank solving the whole problem), an even q_max
     w.blocks = 1;
-    if (m.p.ws_blocks > 1) {
-      if (multi_ok && m.kind == EngineKind::WsDense && !m.xch) w.blocks = m.p.ws_blocks;
-      else m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
+    if (want_blocks > 1) {
+      if (multi_ok && m.kind == EngineKind::WsDense && !m.xch) w.blocks = want_blocks;
+      else if (m.p.ws_blocks > 1) m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
                                  "ws_blocks > 1 needs ws-dense, an even ws_size and <= 256 candidate lists over "
                                  "the collectives: one block per round";
     }

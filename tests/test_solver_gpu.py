@@ -506,7 +506,7 @@ def test_bench_multi_gpu_ws_sharded_and_default(tmp_path):
     out = _bench_multi(root, world, ["--dp", "shard"], 29661)
     assert out["iteration"] == "ws-dense" and out["dp_policy"] == "shard" and out["converged"]
     # RCCL: multi-block rounds; gloo rehearsal: one-block rounds over the peer exchange
-    assert out["params"]["ws_blocks"] == 8 and (_SHARED or "ws_blocks" not in out["engine_note"])
+    assert out["params"]["ws_blocks"] in (0, 8) and (_SHARED or "ws_blocks" not in out["engine_note"])
     assert abs(out["b"] - ref.b_) < 2e-3 and abs(out["n_sv"] - ref.n_support_) <= 8
     if _NDEV >= 2:
         dflt = _bench_multi(root, world, [], 29671)
