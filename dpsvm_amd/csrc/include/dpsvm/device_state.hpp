@@ -213,7 +213,7 @@ constexpr int kWsMaxGroups = 256;    // selection workgroups per rank
 constexpr int kWsListsPerThread = 4; // candidate lists a merge thread folds into one (<= 1024 lists over ranks)
 constexpr int kWsMaxRPT = 32;        // rows per selection thread (256 x 256 x 32 = 2.1M rows per rank)
 constexpr int kWsSolveThreads = 1024;
-constexpr int64_t kWsAutoRows = 100000;  // solver auto: working-set engines from this many rows on
+constexpr int64_t kWsAutoRows = 50000;   // solver auto: working-set engines from this many rows on (60k headline: ws 0.048 s vs smo 0.45 s)
 // multi-block rounds (ws_blocks = P > 1, ws-dense at world 1): a round selects
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor

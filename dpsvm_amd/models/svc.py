@@ -102,7 +102,7 @@ class SVCConfig:
     watchdog_s: float = 1800.0
     census_groups: int = 0          # residency census grid (tests)
     verify_ranks: bool = True       # cross-rank alpha digest after each solve (world > 1)
-    # solver: auto (ws from 100k rows, else smo) | smo (pair-at-a-time engines, the reference's trajectory) |
+    # solver: auto (ws from 50k rows, else smo) | smo (pair-at-a-time engines, the reference's trajectory) |
     # ws (working-set rounds: the reference's pair rule on a q-row sub-problem
     # in LDS, the same global stop test; smo_ws.hip)
     solver: str = "auto"

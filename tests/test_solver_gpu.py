@@ -120,14 +120,20 @@ def test_gpu_predictor_and_model_file(tmp_path):
 def test_mnist_shape_headline_converges():
     """The BASELINE config (60000 x 784, C=10, gamma=0.25, tol=1e-3) on one GPU."""
     X, y = synthetic("mnist", n=60000, seed=0)
-    clf = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
+    # the library default (solver auto from 50k rows: ws-dense, 8 blocks per round)
+    auto = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
+    assert auto.setup_info_["iteration"] == "ws-dense" and auto.converged_ and auto.n_rounds_ < 400
+    assert auto.train_accuracy() > 0.99
+    # the pair-at-a-time engine (the reference's trajectory)
+    clf = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="smo").fit(X, y)
     assert clf.converged_
     assert clf.fit_time_ < 30.0
     assert clf.train_accuracy() > 0.99
+    assert abs(auto.b_ - clf.b_) < 2e-3
     # > 65535 iterations: the persistent engine's 16-bit exchange tags wrap;
     # one launch per iteration (no exchange) must give the same iterates
     assert clf.setup_info_["iteration"] == "persistent-dense" and clf.n_iter_ > 70000
-    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", persist="off").fit(X, y)
+    ref = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", persist="off", solver="smo").fit(X, y)
     assert ref.n_iter_ == clf.n_iter_ and np.array_equal(ref.alpha_, clf.alpha_) and ref.b_ == clf.b_
 
 
