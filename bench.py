@@ -98,6 +98,7 @@ def parse(argv=None):
     ap.add_argument("--ws-size", type=int, default=192)
     ap.add_argument("--ws-new", type=int, default=0)
     ap.add_argument("--ws-rel", type=float, default=0.3)
+    ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
     ap.add_argument("--ws-block", type=int, default=32)
     ap.add_argument("--ws-blocks", type=int, default=0,
                     help="ws-dense at one rank (or replicated): sub-problems solved per round on separate "
@@ -162,7 +163,7 @@ def main(argv=None) -> int:
                     dp="replicate" if a.dp == "measure" else a.dp,
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
                     xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
-                    ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, ws_blocks=a.ws_blocks, eta=a.eta,
+                    ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, ws_blocks=a.ws_blocks, ws_inner=a.ws_inner, eta=a.eta,
                     xch_timeout_s=a.xch_timeout if a.xch_timeout is not None else (30.0 if multi else 120.0))
     params = cfg.to_native(X.shape[1])
     if ctx.rank == 0:
