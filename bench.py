@@ -100,10 +100,9 @@ def parse(argv=None):
     ap.add_argument("--ws-rel", type=float, default=0.3)
     ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
     ap.add_argument("--ws-block", type=int, default=32)
-    ap.add_argument("--ws-blocks", type=int, default=0,
-                    help="ws-dense at one rank (or replicated): sub-problems solved per round on separate "
-                         "workgroups, combined by an exact line search (1..8; 0 = the library default: 8 from "
-                         "50k rows)")
+    ap.add_argument("--ws-blocks", type=int, default=8,
+                    help="ws-dense: sub-problems solved per round on separate workgroups, combined by an exact "
+                         "line search (1..8; the headline's K ~ I decouples them; the library default is 1)")
     ap.add_argument("--eta", default="x", choices=["x", "gram"],
                     help="pair-at-a-time engines: K(hi, lo) of eta from the two X rows (default) or the resident Gram")
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")

@@ -84,7 +84,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --solver S          :  auto (ws from 100k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
-               "   --ws-blocks P :  ws-dense: P sub-problems per round on P workgroups (1..8; 0 = auto: 8 from 50k rows)\n"
+               "   --ws-blocks P :  ws-dense: P sub-problems per round on P workgroups (1..8, default 1)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"

@@ -118,7 +118,8 @@ struct SolverParams {
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
   int ws_new = 0;             // rows replaced per round (0: 3 ws_size / 4)
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
-  int ws_blocks = 0;          // ws-dense: P disjoint q-row sub-problems per round (1..8; 0 = auto: 8 from 50k rows)
+  int ws_blocks = 1;          // ws-dense: P disjoint q-row sub-problems per round (1..8; 0 = 8 from 50k rows). Default 1:
+                              // strongly coupled problems (covtype-shape) take more rounds with P > 1
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_block = 32;          // rounds per hipGraph block
   // eta's K(i_hi, i_lo) in the pair-at-a-time dense engines: 0 from the two X

@@ -120,8 +120,8 @@ def test_gpu_predictor_and_model_file(tmp_path):
 def test_mnist_shape_headline_converges():
     """The BASELINE config (60000 x 784, C=10, gamma=0.25, tol=1e-3) on one GPU."""
     X, y = synthetic("mnist", n=60000, seed=0)
-    # the library default (solver auto from 50k rows: ws-dense, 8 blocks per round)
-    auto = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda").fit(X, y)
+    # solver auto from 50k rows: ws-dense (here with 8 blocks per round, bench.py's setting)
+    auto = SVC(C=10.0, gamma=0.25, eps=1e-3, device="cuda", ws_blocks=8).fit(X, y)
     assert auto.setup_info_["iteration"] == "ws-dense" and auto.converged_ and auto.n_rounds_ < 400
     assert auto.train_accuracy() > 0.99
     # the pair-at-a-time engine (the reference's trajectory)
