@@ -87,12 +87,12 @@ def parse(argv=None):
     ap.add_argument("--shard-check", default="auto", choices=["auto", "off"],
                     help="N > 1 with a replicated timed solve: one untimed sharded solve first (cross-device "
                          "exchange evidence: its time, iterations and b go into the JSON line)")
-    ap.add_argument("--solver", default="ws", choices=["auto", "smo", "ws"],
-                    help="ws (default): working-set rounds — the reference's pair rule on a q-row sub-problem "
-                         "in LDS, the reference's stop test on the exact gradient; smo: the pair-at-a-time "
-                         "engines (the reference's exact trajectory); auto: the library default (smo)")
+    ap.add_argument("--solver", default="auto", choices=["auto", "smo", "ws"],
+                    help="auto (default, the library's and svmTrain's default): working-set rounds from 50k rows "
+                         "(the reference's pair rule on q-row sub-problems in LDS, the reference's stop test on "
+                         "the exact gradient), else the pair-at-a-time engines; ws / smo force one of them")
     ap.add_argument("--reference-check", default="auto", choices=["auto", "off"],
-                    help="auto: with --solver ws, one untimed solve by the pair-at-a-time engine (the reference's "
+                    help="auto: when the timed solve ran ws-dense, one untimed solve by the pair-at-a-time engine (the reference's "
                          "trajectory) after the timed runs; its time, iterations, b, support vectors and the "
                          "decision agreement with the timed model go into the JSON line")
     ap.add_argument("--ws-size", type=int, default=192)
@@ -100,9 +100,10 @@ def parse(argv=None):
     ap.add_argument("--ws-rel", type=float, default=0.3)
     ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
     ap.add_argument("--ws-block", type=int, default=32)
-    ap.add_argument("--ws-blocks", type=int, default=8,
-                    help="ws-dense: sub-problems solved per round on separate workgroups, combined by an exact "
-                         "line search (1..8; the headline's K ~ I decouples them; the library default is 1)")
+    ap.add_argument("--ws-blocks", type=int, default=0,
+                    help="ws-dense: up to P sub-problems solved per round on separate workgroups, combined by a "
+                         "line search (1..8; 0 = the library default: 8 from 50k rows, halved after every damped "
+                         "round)")
     ap.add_argument("--eta", default="x", choices=["x", "gram"],
                     help="pair-at-a-time engines: K(hi, lo) of eta from the two X rows (default) or the resident Gram")
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
@@ -287,7 +288,7 @@ def main(argv=None) -> int:
         acc = float(solver.train_accuracy(alpha, res["b"]))
     nsv = int((alpha > 0).sum())
     ref_check = None
-    if (on_gpu and a.solver == "ws" and a.reference_check == "auto" and info.get("iteration") == "ws-dense"
+    if (on_gpu and a.solver != "smo" and a.reference_check == "auto" and info.get("iteration") == "ws-dense"
             and (n_ranks == 1 or info.get("dp_policy") == "replicate")):
         rows = np.arange(0, X.shape[0], max(1, X.shape[0] // 4096))
         d_ws = np.asarray(solver.decision(alpha, res["b"], X[rows]))
@@ -340,6 +341,9 @@ def main(argv=None) -> int:
             },
             "iterations": int(res["iters"]),
             "rounds": int(res.get("outer", 0)),
+            "ws_blocks": {"start": int(res.get("ws_blocks", 1)), "end": int(res.get("ws_blocks_end", 1)),
+                          "one_block_from_round": int(res.get("ws_p1_round", 0)),
+                          "damped_rounds": int(res.get("ws_damped", 0))},
             "converged": bool(res["converged"]),
             "n_sv": nsv,
             "b": res["b"],

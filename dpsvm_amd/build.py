@@ -44,6 +44,7 @@ LIB_SOURCES = [
     "solver/gpu_engines.hip",
     "solver/gpu_solve.hip",
     "solver/gpu_predict.hip",
+    "solver/ws_kernel_entry.hip",
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/smo_fused.hip",

@@ -81,10 +81,11 @@ inline void usage_train(const char* prog, bool seq) {
                "   --watchdog S        :  host bound on one block of iterations (default 1800)\n"
                "   --census-groups N   :  residency census grid of the persistent engines (tests)\n"
                "   --no-verify-ranks   :  skip the cross-rank alpha digest (world > 1)\n"
-               "   --solver S          :  auto (ws from 100k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
+               "   --solver S          :  auto (ws from 50k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
-               "   --ws-blocks P :  ws-dense: P sub-problems per round on P workgroups (1..8, default 1)\n"
+               "   --ws-blocks P       :  ws-dense: up to P sub-problems per round on P workgroups (1..8; default 0 = auto:\n"
+               "                          8 from 50k rows, halved after every damped round)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"

@@ -4,6 +4,7 @@
 // over TCP (Makefile:74), ranks are the GPUs of this node driven by one thread
 // each over RCCL/xGMI (-p N), or simulated ranks sharing one device (--ranks N).
 // Each rank binds its own GPU (the reference never calls cudaSetDevice).
+#include <atomic>
 #include <iostream>
 #include <mutex>
 #include <thread>
@@ -68,6 +69,7 @@ int main(int argc, char** argv) {
     }
 
     std::vector<std::exception_ptr> errs((size_t)world);
+    std::atomic<int> first_fail{-1};  // the rank whose error is the root cause
     auto rank_main = [&](int r) {
       try {
         Communicator* comm = comms[r].get();
@@ -100,7 +102,13 @@ int main(int argc, char** argv) {
         if (r == 0) extras.t_accuracy = cli::now_s() - ta0;
       } catch (...) {
         errs[r] = std::current_exception();
-        if (world > 1) comms[r]->abort();
+        int none = -1;
+        first_fail.compare_exchange_strong(none, r);
+        // abort EVERY rank's communicator: peers blocked in a collective (or a
+        // captured round graph) on a dead rank return now instead of at their
+        // watchdog, and fail with "communicator aborted"
+        if (world > 1)
+          for (auto& c : comms) c->abort();
       }
     };
     if (world == 1) {
@@ -110,8 +118,7 @@ int main(int argc, char** argv) {
       for (int r = 0; r < world; ++r) ts.emplace_back(rank_main, r);
       for (auto& t : ts) t.join();
     }
-    for (auto& e : errs)
-      if (e) std::rethrow_exception(e);
+    if (first_fail.load() >= 0) std::rethrow_exception(errs[first_fail.load()]);
 
     SolveResult& r0 = results[0];
     cli::print_outcome(r0, o.p.eps);

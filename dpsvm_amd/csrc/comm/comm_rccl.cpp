@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "dpsvm/comm.hpp"
 #include "dpsvm/common.hpp"
 #include "../runtime/hip_check.hpp"
@@ -32,10 +35,8 @@ class RcclComm final : public Communicator {
     (void)hipSetDevice(device_);
     if (scratch_) (void)hipFree(scratch_);
     if (bstream_) (void)hipStreamDestroy(bstream_);
-    if (comm_) {
-      if (aborted_) ncclCommAbort(comm_);
-      else ncclCommDestroy(comm_);
-    }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (comm_) ncclCommDestroy(comm_);
   }
   int rank() const override { return rank_; }
   int size() const override { return world_; }
@@ -43,38 +44,59 @@ class RcclComm final : public Communicator {
   std::string name() const override { return "rccl"; }
 
   void allreduce_min_u64(uint64_t* buf, size_t count, hipStream_t s) override {
-    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclMin, comm_, s));
+    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclMin, live(), s));
   }
   void allreduce_sum_f64(double* buf, size_t count, hipStream_t s) override {
-    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm_, s));
+    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, live(), s));
   }
   void allreduce_sum_f32(float* buf, size_t count, hipStream_t s) override {
-    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, s));
+    RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, live(), s));
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-    RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
+    RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, live(), s));
   }
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
-    RCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, s));
+    RCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, live(), s));
   }
   void barrier() override {
     HIP_CHECK(hipSetDevice(device_));
-    RCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, bstream_));
+    RCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, live(), bstream_));
     HIP_CHECK(hipStreamSynchronize(bstream_));
   }
   std::string async_error() override {
+    if (aborted_.load()) return "communicator aborted";
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!comm_) return "communicator aborted";
     ncclResult_t e = ncclSuccess;
     if (ncclCommGetAsyncError(comm_, &e) != ncclSuccess) return "ncclCommGetAsyncError failed";
     return e == ncclSuccess ? std::string() : std::string(ncclGetErrorString(e));
   }
-  void abort() override { aborted_ = true; }
+  // Immediate: ncclCommAbort raises the communicator's abort flag, which its
+  // in-flight kernels poll, so a collective blocked on a dead peer ends now
+  // (the solver's wait loop then sees async_error() and fails) instead of when
+  // the watchdog fires.  Safe from any thread; the handle is gone afterwards
+  // and every later call fails with "communicator aborted".
+  void abort() override {
+    if (aborted_.exchange(true)) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (comm_) {
+      (void)hipSetDevice(device_);
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
 
  private:
+  ncclComm_t live() {
+    if (aborted_.load()) ::dpsvm::fail("RCCL communicator aborted (rank " + std::to_string(rank_) + ")");
+    return comm_;
+  }
   ncclComm_t comm_ = nullptr;
   int rank_, world_, device_;
   void* scratch_ = nullptr;
   hipStream_t bstream_ = nullptr;
-  bool aborted_ = false;
+  std::atomic<bool> aborted_{false};
+  std::mutex mu_;
 };
 
 }  // namespace

@@ -118,8 +118,9 @@ struct SolverParams {
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
   int ws_new = 0;             // rows replaced per round (0: 3 ws_size / 4)
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
-  int ws_blocks = 1;          // ws-dense: P disjoint q-row sub-problems per round (1..8; 0 = 8 from 50k rows). Default 1:
-                              // strongly coupled problems (covtype-shape) take more rounds with P > 1
+  int ws_blocks = 0;          // ws-dense: up to P disjoint q-row sub-problems per round (1..8; 0 auto = 8 from 50k
+                              // rows).  Adaptive: halved after every damped round (coupled blocks), 1 after an
+                              // independent-clip event, then the one-block round kernels (smo_ws.hip)
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_block = 32;          // rounds per hipGraph block
   // eta's K(i_hi, i_lo) in the pair-at-a-time dense engines: 0 from the two X
@@ -144,6 +145,10 @@ struct SolveResult {
   int world = 1;
   double verify_f_err = -1.0;  // DPSVM_VERIFY: max |f - f(alpha)| / (1 + |f(alpha)|), -1 = not run
   int64_t outer = 0;           // working-set engine: rounds
+  // multi-block working-set rounds: blocks at the start / at the end (adaptive),
+  // rounds completed when the count reached 1 (0: never), damped rounds
+  int ws_blocks = 1, ws_blocks_end = 1;
+  int64_t ws_p1_round = 0, ws_damped = 0;
   bool converged() const { return status == 1; }
 };
 

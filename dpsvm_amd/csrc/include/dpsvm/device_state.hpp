@@ -93,6 +93,11 @@ struct alignas(16) SmoStatus {
   float b_hi, b_lo;
   int64_t hits, misses, rows_computed, x_passes, spec_rows, host_hits, spills;
   int64_t outer;  // working-set engine: rounds (selection + sub-problem solve) so far
+  // multi-block working-set rounds: rounds completed when the adaptive block
+  // count reached 1 (0: not yet; identical on every rank), the current count,
+  // damped rounds so far
+  int64_t ws_p1_round;
+  int32_t ws_p, ws_damped;
 };
 
 // Partitioned-X candidate record: one per rank, all-gathered each iteration.
@@ -253,9 +258,16 @@ struct alignas(16) WsCtrl {
   int32_t pad2[3];
   float t_last;                  // line-search factor of the last applied round
   int32_t n_damped;              // rounds applied with t < 1
-  int32_t multi_off;             // independent clipping broke sum(alpha y) = 0: one block per round from now on
-  int32_t pad3;
+  // adaptive block count: the next round's merge takes p_act blocks (seeded with
+  // blocks; halved after every damped round — strongly coupled blocks; 1 after an
+  // independent-clip event, which breaks sum(alpha y) = 0 and would drift P times
+  // as fast with P blocks).  p_round: the blocks of the current round (its merge
+  // writes it; the solve and the line search read it).
+  int32_t p_act;
+  int32_t p_round;
   int32_t clipb[kWsMaxBlocks];   // per block: a pair step was clipped (independent clipping)
+  int64_t p1_round;              // rounds completed when p_act reached 1 (0: not yet) — the host
+                                 // then switches to the one-block round graph at a block boundary
 };
 
 struct WsArgs {

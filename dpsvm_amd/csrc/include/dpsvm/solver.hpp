@@ -140,6 +140,55 @@ void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* 
 // the (up, low) keys of its rows -> keys_out[2 * groups]
 void fused_select(const float* f, const float* alpha, const float* y, int64_t n, float C, int rows_per_group,
                   uint64_t* keys_out, void* stream);
+
+// ---- working-set kernels (smo_ws.hip), one launch each on crafted state
+// (host vectors in and out; ws_kernel_entry.hip).  Reference counterparts:
+// the selection / update functors svmTrain.cu:41-137, the pair rule
+// svmTrainMain.cpp:255-299. ----
+// ws_merge_multi: cand = [G][2][kWsCand] per-list keys (up, low), the previous
+// union (newest first), the adaptive block count p_act of `blocks`
+struct WsMergeProbe {
+  std::vector<int32_t> uidx;  // the union, newest first
+  std::vector<int32_t> idx;   // [blocks][q_max] block layout (-1: unused)
+  std::vector<int32_t> qb;    // rows per block
+  float b_hi = 0.f, b_lo = 0.f;
+  int done = 0, p_round = 0;
+};
+WsMergeProbe ws_merge_multi_probe(const std::vector<uint64_t>& cand, int G, int blocks, int p_act, int q_max,
+                                  int n_new, float eps, const std::vector<int32_t>& prev_union, int64_t iter,
+                                  int64_t max_iter);
+// ws_solve: P blocks; block p = qb[p] rows with sub-Gram K[p] ([q_max][q_max]),
+// f / alpha / y (row a of block p is global row p q_max + a)
+struct WsSolveProbe {
+  std::vector<float> alpha;       // [P * q_max] after the solve (untouched rows 0)
+  std::vector<int32_t> steps;     // pair steps per block
+  std::vector<int32_t> apply_idx; // changed rows per block segment (concatenated, block order)
+  std::vector<float> apply_coef;  // their (alpha_new - alpha_old) y
+  std::vector<int32_t> nab;       // changed rows per block
+  int64_t iter = 0, outer = 0, p1_round = 0;
+  int done = 0, p_act = 0;
+};
+WsSolveProbe ws_solve_probe(const std::vector<float>& K, const std::vector<float>& f, const std::vector<float>& alpha,
+                            const std::vector<float>& y, const std::vector<int32_t>& qb, int q_max, int blocks,
+                            int p_round, float C, int clip, float eps, float rel, float eps_floor, float tau,
+                            float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter);
+// ws_select: the f update of a round's alpha changes (apply rows: lines into
+// gram [L][ldg], coefficients) and the per-workgroup candidates.  blocks == 1:
+// the one-pass kernel; blocks > 1: pass 1 (d_f, line-search partials) and pass 2
+// (t, f += t d_f, alpha fix-up, candidates) with p_round blocks this round.
+struct WsSelectProbe {
+  std::vector<float> f, alpha, dalpha, dfs;
+  std::vector<double> part;      // [G][2] d'Qd, g'd partials (two-pass mode)
+  std::vector<uint64_t> cand;    // [G][2][kWsCand]
+  int G = 0, rpt = 0, p_act = 0, n_damped = 0, nonfinite = 0;
+  float t = 1.f;
+  int64_t p1_round = 0;
+};
+WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t ldg, const std::vector<float>& f,
+                              const std::vector<float>& alpha, const std::vector<float>& y,
+                              const std::vector<float>& dalpha, const std::vector<int32_t>& apply_line,
+                              const std::vector<float>& apply_coef, const std::vector<int32_t>& nab, int blocks,
+                              int p_round, int p_act, int q_max, float C, int64_t outer);
 }  // namespace kernels
 
 int device_count();

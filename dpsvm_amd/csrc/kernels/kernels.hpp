@@ -81,6 +81,9 @@ void ws_solve(const WsArgs& a, hipStream_t s);
 void ws_merge(const WsArgs& a, hipStream_t s);
 // multi-block rounds (a.blocks > 1, ws-dense at one rank): the union merge before ws_gather
 void ws_merge_multi(const WsArgs& a, hipStream_t s);
+// the adaptive block count reached 1: the last union becomes the one-block
+// kernels' previous set (run once, between two rounds)
+void ws_to_single(const WsArgs& a, hipStream_t s);
 bool ws_cache_supported(int64_t L, int q_max);
 // partitioned X, cache mode: out[i] = X row ctrl->miss_row[i] if this rank owns
 // it (rows off..off+nl-1 at x), else zeros; out_sq[i] = its global |x|^2

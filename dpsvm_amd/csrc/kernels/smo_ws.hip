@@ -217,6 +217,9 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
   s->rows_computed = c->rows_computed;  // cache mode: kernel rows computed, member rows found cached
   s->misses = c->rows_computed;
   s->hits = c->row_hits;
+  s->ws_p1_round = c->p1_round;
+  s->ws_p = c->p_act;
+  s->ws_damped = c->n_damped;
   __atomic_store_n(&s->seq, (int32_t)c->outer, __ATOMIC_RELEASE);
 }
 
@@ -284,13 +287,27 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-// multi-block rounds: the exact line search along the combined step d of the
+// multi-block rounds: the line search along the combined step d of the round's
 // P sub-problems.  W(alpha + t d) = W + t g'd - t^2 d'Qd / 2 peaks at
-// t = g'd / d'Qd; each block's step alone raises W, so g'd > 0 and the
-// capped t keeps every round an ascent step however the blocks couple (t = 1
-// when they do not: K ~ I).  Every wave reduces the workgroup partials in the
-// same order: identical t everywhere.
-__device__ __forceinline__ float ws_line_search(const WsArgs& a) {
+// t* = g'd / d'Qd, and W(alpha + d) - W(alpha) = d'Qd (t* - 1/2).  The step
+// taken is
+//   t = 1       P = 1 (one block: its own sub-problem step, exactly the
+//               one-block engine's round), or t* >= kWsTFull — the full step
+//               keeps >= 99% of the optimal gain, and keeps every alpha the
+//               blocks put on a bound exactly there (a factor a hair below 1
+//               would leave alpha_new - (1 - t) d_alpha a hair inside the box:
+//               a row every later round selects for a zero-length step — the
+//               diagnosed cause of the ~3.5-pair-step rounds of round 2);
+//   t = t*      kWsTFull > t* (strongly coupled blocks: damped, ascent);
+//   t = 0       g'd <= 0: no ascent along d (float cancellation, or an
+//               independent-clip round whose steps do not follow W) — the round
+//               is discarded and the next one runs with fewer blocks.
+// Every wave reduces the workgroup partials in the same order: identical t
+// everywhere (and on every rank).
+constexpr float kWsTFull = 0.9f;
+
+__device__ __forceinline__ float ws_line_search(const WsArgs& a, int P) {
+  if (P <= 1) return 1.f;
   const int lane = threadIdx.x & 63;
   double q = 0.0, g = 0.0;
   for (int k = lane; k < a.G_all; k += 64) {  // every rank's partials (all-gathered)
@@ -299,7 +316,10 @@ __device__ __forceinline__ float ws_line_search(const WsArgs& a) {
   }
   q = wave_sum_f64(q);
   g = wave_sum_f64(g);
-  return (g > 0.0 && q > g) ? (float)(g / q) : 1.f;
+  if (!(g > 0.0)) return 0.f;
+  if (!(q > g)) return 1.f;
+  const float t = (float)(g / q);
+  return t >= kWsTFull ? 1.f : t;
 }
 
 // ---------------------------------------------------------------------------
@@ -444,10 +464,19 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
       return;
     }
     if constexpr (MODE == 2) {
-      const float t = ws_line_search(a);
+      const int pr = c->p_round;  // written by this round's merge (p_act may change below)
+      const float t = ws_line_search(a, pr);
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         c->t_last = t;
-        if (t < 1.f) c->n_damped = c->n_damped + 1;
+        if (t < 1.f) {
+          // strongly coupled blocks: fewer from the next round on (the solve's
+          // commit may have set p_act = 1 already: an independent-clip event)
+          c->n_damped = c->n_damped + 1;
+          const int np = max(1, pr / 2);
+          if (np < c->p_act) c->p_act = np;
+          if (c->p_act == 1 && c->p1_round == 0) c->p1_round = c->outer;
+          ws_status(a.status, c);  // p1_round visible with the round that set it (gpu_engines.hip)
+        }
       }
       if (a.world > 1 && blockIdx.x == 0) {
         // alpha is global on every rank: the changed rows this rank does not own
@@ -1114,7 +1143,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   if (lead) WS_STAMP(1);
   const int G = a.G_all;
   const int par = (int)(c->outer & 1);
-  const int P = c->multi_off ? 1 : a.blocks, Qmax = P * a.q_max;
+  const int P = max(1, min(c->p_act, a.blocks)), Qmax = P * a.q_max;
   const int q_prev = c->uq[par ^ 1];
   const int want = q_prev == 0 ? Qmax : min(P * a.n_new, Qmax);
   // the previous union, newest first: thread t holds rows 2t, 2t + 1
@@ -1241,6 +1270,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   if (lead) {
     c->uq[par] = Q;
     c->q[par] = Q;
+    c->p_round = P;
     c->b_hi = b_hi;
     c->b_lo = b_lo;
     WS_STAMP(2);
@@ -1453,7 +1483,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   }
   int64_t room = a.max_iter - it0;
   if (kMulti) {  // the active blocks share max_iter
-    const int pa = c->multi_off ? 1 : a.blocks;
+    const int pa = c->p_round;
     room = blk < pa ? room / pa + (blk < room % pa ? 1 : 0) : 0;
   }
   // uniform: in an SGPR, so the loop test is one scalar compare
@@ -1567,16 +1597,32 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       // the reference's independent clipping does not keep sum(alpha y) = 0: once
       // a clip broke it, the blocks' combined steps drift it further (measured:
       // adult-shape P = 8 never converges) — one block per round from here on
-      if (any_clip) c->multi_off = 1;
       WS_STAMP(4);
       if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + 5] = (uint64_t)tot_i;
       c->n_apply = tot_a;
       c->iter = it0 + tot_i;
       c->outer = c->outer + 1;
+      if (any_clip && c->p_act > 1) {
+        c->p_act = 1;
+        if (c->p1_round == 0) c->p1_round = c->outer;
+      }
       c->done = any_bad ? kNonFinite : tot_i == 0 ? kNoPair : (it0 + tot_i >= a.max_iter ? kMaxIter : kRunning);
       ws_status(a.status, c);
     }
   }
+}
+
+// The adaptive block count reached 1: the host switches to the one-block round
+// kernels at a block boundary (gpu_engines.hip).  Their merge retains the
+// previous set from idx[par ^ 1][0 .. q[par ^ 1]) in newest-first order, which
+// the multi-block merge kept as the union (uidx, uq): copy it over (at most
+// q_max rows, the newest).  One workgroup, stream-ordered between two rounds.
+__global__ __launch_bounds__(256) void ws_to_single_kernel(WsArgs a) {
+  WsCtrl* c = a.ctrl;
+  const int pp = (int)((c->outer + 1) & 1);  // the last round's parity (outer - 1) & 1
+  const int q = min(c->uq[pp], a.q_max);
+  for (int i = threadIdx.x; i < q; i += blockDim.x) c->idx[pp][i] = c->uidx[pp][i];
+  if (threadIdx.x == 0) c->q[pp] = q;
 }
 
 // Partitioned X, cache mode: the X rows of this round's cache misses, packed
@@ -1673,6 +1719,11 @@ void ws_gather(const WsArgs& a, hipStream_t s) {
 void ws_merge(const WsArgs& a, hipStream_t s) {
   dev::ws_merge_kernel<<<1, dev::kWsGatherThreads, 0, s>>>(a);
   post_launch("ws_merge", s);
+}
+
+void ws_to_single(const WsArgs& a, hipStream_t s) {
+  dev::ws_to_single_kernel<<<1, 256, 0, s>>>(a);
+  post_launch("ws_to_single", s);
 }
 
 void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* xsq, const WsCtrl* ctrl, int q_max,

@@ -117,6 +117,10 @@ py::dict result_dict(const SolveResult& r) {
   d["spec_rows"] = r.spec_rows;
   d["host_hits"] = r.host_hits;
   d["outer"] = r.outer;
+  d["ws_blocks"] = r.ws_blocks;
+  d["ws_blocks_end"] = r.ws_blocks_end;
+  d["ws_p1_round"] = r.ws_p1_round;
+  d["ws_damped"] = r.ws_damped;
   d["host_cache_lines"] = r.host_cache_lines;
   d["cache_lines"] = r.cache_lines;
   d["world"] = r.world;
@@ -456,6 +460,65 @@ PYBIND11_MODULE(_C, m) {
                              uintptr_t stream) {
     kernels::fused_select((const float*)f, (const float*)alpha, (const float*)y, n, C, rows, (uint64_t*)out,
                           (void*)stream);
+  });
+  // working-set kernels on crafted state (ws_kernel_entry.hip)
+  using U64 = py::array_t<uint64_t, py::array::c_style | py::array::forcecast>;
+  using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+  auto vi = [](const I32& a) { return std::vector<int32_t>(a.data(), a.data() + a.size()); };
+  m.def("k_ws_merge_multi", [vi](const U64& cand, int G, int blocks, int p_act, int q_max, int n_new, float eps,
+                                 const I32& prev, int64_t iter, int64_t max_iter) {
+    const auto r = kernels::ws_merge_multi_probe(std::vector<uint64_t>(cand.data(), cand.data() + cand.size()), G,
+                                                 blocks, p_act, q_max, n_new, eps, vi(prev), iter, max_iter);
+    py::dict d;
+    d["uidx"] = r.uidx;
+    d["idx"] = r.idx;
+    d["qb"] = r.qb;
+    d["b_hi"] = r.b_hi;
+    d["b_lo"] = r.b_lo;
+    d["done"] = r.done;
+    d["p_round"] = r.p_round;
+    return d;
+  });
+  m.def("k_ws_solve", [vi](const F32& K, const F32& f, const F32& alpha, const F32& y, const I32& qb, int q_max,
+                           int blocks, int p_round, float C, int clip, float eps, float rel, float eps_floor, float tau,
+                           float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter) {
+    const auto r = kernels::ws_solve_probe(from_np(K), from_np(f), from_np(alpha), from_np(y), vi(qb), q_max, blocks,
+                                           p_round, C, clip, eps, rel, eps_floor, tau, b_hi, b_lo, inner_max, iter0,
+                                           max_iter);
+    py::dict d;
+    d["alpha"] = to_np(r.alpha);
+    d["steps"] = r.steps;
+    d["apply_idx"] = r.apply_idx;
+    d["apply_coef"] = to_np(r.apply_coef);
+    d["nab"] = r.nab;
+    d["iter"] = r.iter;
+    d["outer"] = r.outer;
+    d["done"] = r.done;
+    d["p_act"] = r.p_act;
+    d["p1_round"] = r.p1_round;
+    return d;
+  });
+  m.def("k_ws_select", [vi](const F32& gram, int64_t L, int64_t ldg, const F32& f, const F32& alpha, const F32& y,
+                            const F32& dalpha, const I32& lines, const F32& coef, const I32& nab, int blocks,
+                            int p_round, int p_act, int q_max, float C, int64_t outer) {
+    const auto r = kernels::ws_select_probe(from_np(gram), L, ldg, from_np(f), from_np(alpha), from_np(y),
+                                            from_np(dalpha), vi(lines), from_np(coef), vi(nab), blocks, p_round, p_act,
+                                            q_max, C, outer);
+    py::dict d;
+    d["f"] = to_np(r.f);
+    d["alpha"] = to_np(r.alpha);
+    d["dalpha"] = to_np(r.dalpha);
+    d["dfs"] = to_np(r.dfs);
+    d["part"] = r.part;
+    d["cand"] = r.cand;
+    d["G"] = r.G;
+    d["rpt"] = r.rpt;
+    d["t"] = r.t;
+    d["p_act"] = r.p_act;
+    d["n_damped"] = r.n_damped;
+    d["p1_round"] = r.p1_round;
+    d["nonfinite"] = r.nonfinite;
+    return d;
   });
   m.def("make_key", [](float f, uint32_t idx) { return make_key(f, idx); });
   m.def("key_value", [](uint64_t k) { return key_value(k); });

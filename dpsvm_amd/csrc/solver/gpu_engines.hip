@@ -324,10 +324,10 @@ void ws_allgather_part(GpuSolver::Impl& m) {
   HIP_CHECK(hipMemcpyAsync(all, m.h_wspart.data(), bytes * m.world, hipMemcpyHostToDevice, m.stream));
 }
 
-void ws_allreduce_sub(GpuSolver::Impl& m) {
-  if (!m.collectives() || m.wsa.xpeer) return;  // peer exchange: assembled by the gather kernel
+void ws_allreduce_sub(GpuSolver::Impl& m, const WsArgs& w) {
+  if (!m.collectives() || w.xpeer) return;  // peer exchange: assembled by the gather kernel
   // the P sub-Grams + the members' f of every block ([3][P][kWsMax] aux: f first)
-  const size_t count = (size_t)m.wsa.blocks * ((size_t)m.wsa.q_max * m.wsa.q_max + kWsMax);
+  const size_t count = (size_t)w.blocks * ((size_t)w.q_max * w.q_max + kWsMax);
   if (m.comm->device_memory()) {
     m.comm->allreduce_sum_f32(m.wssub, count, m.stream);
     return;
@@ -360,30 +360,65 @@ bool ws_graphs(GpuSolver::Impl& m) {
   return m.p.use_graph && (m.device_comm() || !m.ws_round_collectives()) && !m.p.sync_debug && !sync_debug_env();
 }
 
+// B rounds captured into one hipGraph (`round` enqueues one round on m.stream)
+template <class Fn>
+void capture_rounds(GpuSolver::Impl& m, int B, hipGraph_t* graph, hipGraphExec_t* exec, Fn round) {
+  HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
+  try {
+    for (int i = 0; i < B; ++i) round();
+  } catch (...) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(m.stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    throw;
+  }
+  HIP_CHECK(hipStreamEndCapture(m.stream, graph));
+  HIP_CHECK(hipGraphInstantiate(exec, *graph, nullptr, nullptr, 0));
+}
+
 // Working-set rounds on the resident Gram (smo_ws.hip).  Seed: the Gram GEMM,
 // the control record (no working set yet) and the first candidate selection;
 // a block is B rounds of [ws_gather, ws_solve, ws_select] (one hipGraph), so f is
 // consistent with alpha at every block boundary (checkpoints need no pending
 // pair) and the host polls the status one block behind like the SMO engines.
+//
+// Multi-block rounds (wsa.blocks = P > 1) are adaptive: the device halves the
+// block count after every damped round (strongly coupled blocks) and drops to
+// one after an independent-clip event; once it is 1, the host switches to the
+// one-block round kernels (cheaper merge, one f-update pass) at the first block
+// boundary whose completed rounds include the one that set it — a value every
+// rank reads identically, so every rank switches at the same round.
 struct WsDense final : DenseBase {
+  bool single = false;  // multi-block engine now running one-block rounds
   EngineKind kind() const override { return EngineKind::WsDense; }
   int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
-  static void round(GpuSolver::Impl& m) {
-    if (m.wsa.blocks > 1) launch::ws_merge_multi(m.wsa, m.stream);  // else merged inside ws_gather
-    launch::ws_gather(m.wsa, m.stream);
-    ws_allreduce_sub(m);
-    launch::ws_solve(m.wsa, m.stream);
-    if (m.wsa.blocks > 1) {
-      launch::ws_select_pass(m.wsa, 1, m.stream);
+  // the one-block view of a multi-block engine's buffers: sub-Gram at the start
+  // of wssub, its f / alpha / y right after it (one contiguous sum all-reduce)
+  static WsArgs one_block(const GpuSolver::Impl& m) {
+    WsArgs w = m.wsa;
+    w.blocks = 1;
+    w.aux = m.wssub + (size_t)w.q_max * w.q_max;
+    w.aux_stride = kWsMax;
+    return w;
+  }
+  static void round(GpuSolver::Impl& m, const WsArgs& w) {
+    if (w.blocks > 1) launch::ws_merge_multi(w, m.stream);  // else merged inside ws_gather
+    launch::ws_gather(w, m.stream);
+    ws_allreduce_sub(m, w);
+    launch::ws_solve(w, m.stream);
+    if (w.blocks > 1) {
+      launch::ws_select_pass(w, 1, m.stream);
       ws_allgather_part(m);
-      launch::ws_select_pass(m.wsa, 2, m.stream);
+      launch::ws_select_pass(w, 2, m.stream);
     } else {
-      launch::ws_select(m.wsa, m.stream);
+      launch::ws_select(w, m.stream);
     }
     ws_allgather_cand(m);
   }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {
     gram(m, res);
+    single = false;
     if (m.wsa.blocks > 1) HIP_CHECK(hipMemsetAsync(m.wsa.dalpha, 0, (size_t)m.n * 4, m.stream));
     WsCtrl c;
     memset(&c, 0, sizeof(c));
@@ -391,30 +426,27 @@ struct WsDense final : DenseBase {
     c.done = kRunning;
     c.b_hi = b_hi;
     c.b_lo = b_lo;
+    c.p_act = c.p_round = m.wsa.blocks;
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
     ws_allgather_cand(m);
-    if (ws_graphs(m) && !m.gexec) {
-      const int B = block(m.p);
-      HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
-      try {
-        for (int i = 0; i < B; ++i) round(m);
-      } catch (...) {
-        hipGraph_t g = nullptr;
-        (void)hipStreamEndCapture(m.stream, &g);
-        if (g) (void)hipGraphDestroy(g);
-        (void)hipGetLastError();
-        throw;
-      }
-      HIP_CHECK(hipStreamEndCapture(m.stream, &m.graph));
-      HIP_CHECK(hipGraphInstantiate(&m.gexec, m.graph, nullptr, nullptr, 0));
-    }
+    if (ws_graphs(m) && !m.gexec) capture_rounds(m, block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });
+  }
+  void observe(GpuSolver::Impl& m, const SmoStatus& st, int64_t blocks_done) override {
+    if (single || m.wsa.blocks <= 1 || st.ws_p1_round <= 0) return;
+    if (st.ws_p1_round > blocks_done * block(m.p)) return;  // set by the block in flight: next time
+    single = true;
+    const WsArgs w = one_block(m);
+    launch::ws_to_single(w, m.stream);
+    if (ws_graphs(m) && !m.gexec1) capture_rounds(m, block(m.p), &m.graph1, &m.gexec1, [&] { round(m, w); });
   }
   void run_block(GpuSolver::Impl& m, int B) override {
-    if (m.gexec) {
-      HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
+    hipGraphExec_t g = single ? m.gexec1 : m.gexec;
+    if (g) {
+      HIP_CHECK(hipGraphLaunch(g, m.stream));
     } else {
-      for (int i = 0; i < B; ++i) round(m);
+      const WsArgs w = single ? one_block(m) : m.wsa;
+      for (int i = 0; i < B; ++i) round(m, w);
     }
   }
   Pending pending(GpuSolver::Impl&) override { return {}; }  // alphas committed every round
@@ -443,7 +475,7 @@ struct WsCache final : Engine {
                                m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
     }
     launch::ws_gather(w, m.stream);
-    ws_allreduce_sub(m);
+    ws_allreduce_sub(m, w);
     launch::ws_solve(w, m.stream);
     launch::ws_select(w, m.stream);
     ws_allgather_cand(m);
@@ -458,21 +490,7 @@ struct WsCache final : Engine {
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
     ws_allgather_cand(m);
-    if (ws_graphs(m) && !m.gexec) {
-      const int B = block(m.p);
-      HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
-      try {
-        for (int i = 0; i < B; ++i) round(m);
-      } catch (...) {
-        hipGraph_t g = nullptr;
-        (void)hipStreamEndCapture(m.stream, &g);
-        if (g) (void)hipGraphDestroy(g);
-        (void)hipGetLastError();
-        throw;
-      }
-      HIP_CHECK(hipStreamEndCapture(m.stream, &m.graph));
-      HIP_CHECK(hipGraphInstantiate(&m.gexec, m.graph, nullptr, nullptr, 0));
-    }
+    if (ws_graphs(m) && !m.gexec) capture_rounds(m, block(m.p), &m.graph, &m.gexec, [&] { round(m); });
   }
   void run_block(GpuSolver::Impl& m, int B) override {
     if (m.gexec) {

@@ -121,6 +121,10 @@ struct GpuSolver::Impl {
 
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
+  // multi-block working-set rounds: the one-block round graph the engine
+  // switches to once the adaptive block count reached 1 (built on first use)
+  hipGraphExec_t gexec1 = nullptr;
+  hipGraph_t graph1 = nullptr;
 
   ~Impl();
 
@@ -141,6 +145,10 @@ struct GpuSolver::Impl {
   int32_t* wsctrl_n_miss() const { return wsctrl ? &wsctrl->n_miss : nullptr; }
 
   SmoStatus read_status() const;
+  // bound of the next wait_event (0: p.watchdog_s).  At world > 1 the solve
+  // loop derives it from the measured block times (a dead peer is detected in
+  // seconds, not at the 1800 s default)
+  double wd_limit = 0.0;
   void init_ctrl(int64_t iter0, float b_hi, float b_lo);
   void wait_event(hipEvent_t e);
 
@@ -178,6 +186,10 @@ struct Engine {
   virtual void prepare(GpuSolver::Impl&) {}  // per-solve state reset, before the timed region
   virtual void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) = 0;
   virtual void run_block(GpuSolver::Impl& m, int B) = 0;
+  // the status after `blocks_done` completed blocks (the next block not yet
+  // enqueued): engines may change what they enqueue next — identically on every
+  // rank, so only from values that completed blocks wrote
+  virtual void observe(GpuSolver::Impl&, const SmoStatus&, int64_t /*blocks_done*/) {}
   virtual Pending pending(GpuSolver::Impl&) { return {}; }
   virtual double gram_seconds() { return 0.0; }
 };

@@ -31,6 +31,8 @@ GpuSolver::Impl::~Impl() {
   if (xpeer_d) (void)hipFree(xpeer_d);
   if (gexec) (void)hipGraphExecDestroy(gexec);
   if (graph) (void)hipGraphDestroy(graph);
+  if (gexec1) (void)hipGraphExecDestroy(gexec1);
+  if (graph1) (void)hipGraphDestroy(graph1);
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
@@ -65,7 +67,7 @@ void GpuSolver::Impl::init_ctrl(int64_t iter0, float b_hi, float b_lo) {
 void GpuSolver::Impl::wait_event(hipEvent_t e) {
   // bounded wait with async-error polling (SURVEY §5.3 watchdog)
   auto t0 = Clock::now();
-  const double limit = p.watchdog_s;
+  const double limit = wd_limit > 0.0 ? wd_limit : p.watchdog_s;
   int spins = 0;
   while (true) {
     hipError_t q = hipEventQuery(e);
@@ -127,6 +129,26 @@ bool distinct_devices(GpuSolver::Impl& m) {
     for (int b = a + 1; b < m.world; ++b)
       if (strncmp(all[a].bus, all[b].bus, sizeof(Id::bus)) == 0) return false;
   return true;
+}
+
+// the most ranks any one device carries (collective: every rank calls it)
+int max_device_sharing(GpuSolver::Impl& m) {
+  struct Id {
+    char bus[32];
+  } me{};
+  if (hipDeviceGetPCIBusId(me.bus, sizeof(me.bus), m.device) != hipSuccess) {
+    (void)hipGetLastError();
+    snprintf(me.bus, sizeof(me.bus), "pid%d-dev%d", (int)getpid(), m.device);
+  }
+  std::vector<Id> all((size_t)m.world);
+  m.allgather_bytes(&me, all.data(), sizeof(Id));
+  int most = 1;
+  for (int a = 0; a < m.world; ++a) {
+    int k = 0;
+    for (int b = 0; b < m.world; ++b) k += strncmp(all[a].bus, all[b].bus, sizeof(Id::bus)) == 0;
+    most = std::max(most, k);
+  }
+  return most;
 }
 
 }  // namespace
@@ -315,7 +337,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 &&
                         (!m.replicated || launch::smo_fused_lru_supported(m.dp));
   if (want_ws && !ws_ok)
-    m.info.engine_note = "ws engines need <= 16 rows per selection thread: SMO engine used";
+    m.info.engine_note = "ws engines need <= " + std::to_string(kWsMaxRPT) + " rows per selection thread: SMO engine used";
   const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
                          launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
@@ -438,7 +460,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // multi-block rounds (ws_blocks > 1): ws-dense, the union merge reads <= 256
   // candidate lists, an even q_max; at world > 1 over the collectives (their
   // extra per-round all-gather of line-search partials has no peer-exchange form)
-  DPSVM_CHECK(m.p.ws_blocks >= 0 && m.p.ws_blocks <= kWsMaxBlocks, "ws_blocks must be in 1.." + std::to_string(kWsMaxBlocks));
+  DPSVM_CHECK(m.p.ws_blocks >= 0 && m.p.ws_blocks <= kWsMaxBlocks,
+              "ws_blocks must be 0 (auto) or 1.." + std::to_string(kWsMaxBlocks));
   // host communicators stage every collective through host memory (three per
   // round): there the one-block rounds over the in-kernel peer exchange are
   // faster (2 processes on one GPU: 0.163 vs 0.198 s), so multi-block rounds at
@@ -449,7 +472,26 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const int want_blocks = m.p.ws_blocks > 0 ? m.p.ws_blocks : (n >= kWsAutoBlocksRows ? kWsMaxBlocks : 1);
   const bool multi_ok = want_blocks > 1 && ws_cand && ws_q % 2 == 0 && (int64_t)ws_G * m.world <= kWsMaxGroups &&
                         m.p.exchange != 2 && multi_comm;
+  // Residency of the ws peer exchange: gather workgroup a of every rank spins
+  // until the same workgroup of every other rank has pushed its row, so with
+  // ranks sharing a device (rehearsals) the spinning gathers of the other
+  // ranks — (share - 1) x q_max workgroups, one per CU at worst — must leave a
+  // CU free for this rank's solve workgroup (q_max^2 floats of LDS), or the
+  // round deadlocks until the poll timeout.  On distinct devices share = 1.
+  // Refused (collectives instead) unless exchange=peer is explicit.
+  bool ws_xch_resident = true;
+  if (m.world > 1) {
+    const int share = max_device_sharing(m);  // collective
+    int cus = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m.device));
+    ws_xch_resident = m.all_agree((int64_t)(share - 1) * ws_q < (int64_t)cus, m.comm, m.world);
+    if (!ws_xch_resident && m.p.exchange != 2 && (ws_cand || wsc_fits_pre))
+      m.info.engine_note = "ws peer exchange refused: " + std::to_string(share) + " ranks share a device (" +
+                           std::to_string((share - 1) * ws_q) + " spinning gather workgroups >= " +
+                           std::to_string(cus) + " CUs): collectives";
+  }
   const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives && !multi_ok &&
+                           (ws_xch_resident || m.p.exchange == 2) &&
                            (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
   if (want_ws_xch) {
     const bool ok = m.setup_exchange(ws_xch_words((int64_t)ws_G * m.world, ws_q));

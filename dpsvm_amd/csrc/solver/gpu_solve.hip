@@ -128,17 +128,38 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   const int64_t max_blocks = (m.p.max_iter - iter0) / B + 3;
   int64_t last_ck = iter0, last_log = iter0;
   SmoStatus st{};
+  // watchdog at world > 1: the first blocks (the seed's Gram GEMM, graph
+  // instantiation) get min(watchdog_s, kWatchdogFirstS); later ones 50x the
+  // slowest block seen, at least kWatchdogFloorS — a peer that died mid-solve
+  // (a collective that never completes) fails this rank within seconds
+  constexpr double kWatchdogFirstS = 120.0, kWatchdogFloorS = 20.0;
+  auto t_prev = Clock::now();
+  double blk_max = 0.0;
+  int n_timed = 0;
   while (true) {
     m.engine->run_block(m, B);
     HIP_CHECK(hipEventRecord(m.ev[blocks & 1], m.stream));
     if (blocks > 0) {
+      if (m.world > 1)
+        m.wd_limit = n_timed >= 2 ? std::min(m.p.watchdog_s, std::max(kWatchdogFloorS, 50.0 * blk_max))
+                                  : std::min(m.p.watchdog_s, kWatchdogFirstS);
       m.wait_event(m.ev[(blocks - 1) & 1]);
+      {
+        const auto now = Clock::now();
+        const double dt = std::chrono::duration<double>(now - t_prev).count();
+        t_prev = now;
+        if (blocks >= 2) {  // block 0's completion includes the seed
+          blk_max = std::max(blk_max, dt);
+          ++n_timed;
+        }
+      }
       st = m.read_status();
       if (progress && m.p.log_every > 0 && st.iter / m.p.log_every != last_log / m.p.log_every) {
         last_log = st.iter;
         progress(Progress{st.iter, st.b_hi, st.b_lo, secs_since(t0), st.hits, st.misses});
       }
       if (st.done != kRunning) break;
+      m.engine->observe(m, st, blocks);  // blocks 0 .. blocks - 1 completed, block `blocks` in flight
       if (exit_iter >= 0 && st.iter >= exit_iter) {
         // DPSVM_FAULT=exit@K:R: this rank's process dies mid-solve
         fprintf(stderr, "[dpsvm] fault injection: rank %d exits at iteration %lld\n", m.outer_rank,
@@ -166,6 +187,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     DPSVM_CHECK(blocks <= max_blocks + 2, "SMO loop did not terminate (internal error)");
   }
   m.wait_event(m.ev[blocks & 1]);  // the overshoot block (early-exit kernels)
+  m.wd_limit = 0.0;
   HIP_CHECK(hipStreamSynchronize(m.stream));
   res.t_solve = secs_since(t0);
   res.t_gram = m.engine->gram_seconds();
@@ -240,6 +262,12 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   res.host_hits = st.host_hits;
   res.host_cache_lines = m.H;
   res.outer = st.outer;
+  if (m.working_set() && m.wsa.blocks > 1) {
+    res.ws_blocks = m.wsa.blocks;
+    res.ws_blocks_end = st.ws_p;
+    res.ws_p1_round = st.ws_p1_round;
+    res.ws_damped = st.ws_damped;
+  }
   res.world = m.outer_world;
   if (m.stamps) {
     std::vector<uint64_t> h((size_t)kStampRing * 2 * kStampSlots);

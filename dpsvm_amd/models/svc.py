@@ -109,7 +109,9 @@ class SVCConfig:
     ws_size: int = 192              # working-set rows (<= 192)
     ws_new: int = 0                 # rows replaced per round (0: 3 ws_size / 4)
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
-    ws_blocks: int = 1              # ws-dense: sub-problems per round (1..8; 0 = 8 from 50k rows); P > 1 for weakly coupled problems (K ~ I)
+    # ws-dense: up to P sub-problems per round (1..8; 0 auto = 8 from 50k rows, else 1); adaptive — halved
+    # after every damped round (coupled blocks), then the one-block round kernels (smo_ws.hip)
+    ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_block: int = 32              # rounds per hipGraph block
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)

@@ -172,6 +172,60 @@ def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_line
     return out[:, :n]
 
 
+KEY_NONE = (1 << 64) - 1
+WS_CAND = 4  # candidates per side per selection workgroup (kWsCand)
+
+
+def ws_merge_multi(cand, blocks: int, q_max: int, n_new: int, eps: float, prev_union=(), p_act: int | None = None,
+                   iteration: int = 0, max_iter: int = 1 << 40) -> dict:
+    """One launch of the multi-block merge (smo_ws.hip ws_merge_multi_kernel) on
+    crafted candidate lists ``cand`` [G][2][4] (u64 keys, up then low; KEY_NONE
+    for empty slots) and a previous union (newest first).  Returns the new
+    union, the [blocks][q_max] block layout (-1 unused), rows per block, the
+    global b_hi / b_lo and the stop code (0 running, 1 converged)."""
+    import numpy as np
+
+    c = np.ascontiguousarray(np.asarray(cand, dtype=np.uint64).reshape(-1, 2, WS_CAND))
+    prev = np.asarray(list(prev_union), dtype=np.int32)
+    return load().k_ws_merge_multi(c.reshape(-1), c.shape[0], blocks, blocks if p_act is None else p_act, q_max,
+                                   n_new, float(eps), prev, int(iteration), int(max_iter))
+
+
+def ws_solve(K, f, alpha, y, qb, q_max: int, C_: float, clip: str = "independent", eps: float = 1e-3,
+             rel: float = 0.3, eps_floor: float = 3e-4, tau: float = 1e-12, b_hi: float = 0.0, b_lo: float = 0.0,
+             inner_max: int = 768, p_round: int | None = None, iteration: int = 0, max_iter: int = 1 << 40) -> dict:
+    """One launch of the sub-problem solver (ws_solve_kernel): P = len(qb)
+    blocks, block p with qb[p] rows, sub-Gram K[p] ([q_max][q_max]) and f /
+    alpha / y [p][q_max]; b_hi / b_lo = the round's global selection (the local
+    tolerance is max(eps_floor, rel (b_lo - b_hi) / 2)).  P > 1 runs the
+    multi-block kernel (p_round active blocks share max_iter)."""
+    import numpy as np
+
+    P = len(qb)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float32)).reshape(-1)  # noqa: E731
+    return load().k_ws_solve(f32(K), f32(f), f32(alpha), f32(y), np.asarray(qb, dtype=np.int32), q_max, P,
+                             P if p_round is None else p_round, float(C_), 1 if clip == "box" else 0, float(eps),
+                             float(rel), float(eps_floor), float(tau), float(b_hi), float(b_lo), int(inner_max),
+                             int(iteration), int(max_iter))
+
+
+def ws_select(gram, f, alpha, y, dalpha, apply_lines, apply_coef, nab, C_: float, q_max: int = 192,
+              p_round: int | None = None, p_act: int | None = None, outer: int = 1) -> dict:
+    """The working-set f update + candidate selection (ws_select_kernel) on a
+    dense gram [L][ldg >= n] (rows = lines).  len(nab) == 1: the one-pass
+    kernel; more blocks: pass 1 (d_f, d'Qd / g'd partials) and pass 2 (line
+    search t, f += t d_f, alpha = alpha_new - (1 - t) d_alpha, candidates)."""
+    import numpy as np
+
+    g = np.ascontiguousarray(np.asarray(gram, dtype=np.float32))
+    P = len(nab)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float32)).reshape(-1)  # noqa: E731
+    return load().k_ws_select(g.reshape(-1), g.shape[0], g.shape[1], f32(f), f32(alpha), f32(y), f32(dalpha),
+                              np.asarray(apply_lines, dtype=np.int32), f32(apply_coef), np.asarray(nab, dtype=np.int32),
+                              P, P if p_round is None else p_round, P if p_act is None else p_act, q_max, float(C_),
+                              int(outer))
+
+
 def fused_select(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: float, rows_per_group: int = 256):
     """Per-workgroup (up, low) selection keys of the fused / persistent engines
     (classification + wave-64 DPP minimum + LDS across waves): [groups, 2] u64

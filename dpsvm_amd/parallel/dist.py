@@ -163,10 +163,14 @@ def rccl_comm(ctx: DistContext):
     """Native RCCL communicator on this rank's GPU (xGMI), bootstrapped by
     broadcasting ncclGetUniqueId's 128 bytes through torch.distributed.
 
-    Every step that can fail on one rank only is followed by an agreement over
-    the host (gloo) group, so either all ranks hold an RCCL communicator or all
-    raise CommUnavailable together (no rank is left blocked in the RCCL
-    bootstrap while the others move on)."""
+    Every step BEFORE the blocking ncclCommInitRank that can fail on one rank
+    only — the unique id on rank 0, this rank's device (present and bindable)
+    — is followed by an agreement over the host (gloo) group, so a rank that
+    cannot even start the bootstrap makes every rank raise CommUnavailable
+    together instead of leaving the others blocked inside ncclCommInitRank.
+    ncclCommInitRank itself is a collective: a rank that fails INSIDE it (after
+    its peers entered) is only bounded by RCCL's bootstrap timeout; its own
+    error is then agreed like the others."""
     import torch.distributed as dist
 
     C = load()
@@ -184,6 +188,18 @@ def rccl_comm(ctx: DistContext):
     dist.broadcast_object_list(obj, src=0, group=_host_group())
     if not agree(obj[0] is not None):
         raise CommUnavailable(f"ncclGetUniqueId failed on rank 0 {err}".strip())
+    dev_err = ""
+    try:
+        import torch
+
+        n_dev = C.device_count()
+        if ctx.local_rank >= n_dev:
+            raise RuntimeError(f"local rank {ctx.local_rank} but {n_dev} visible devices")
+        torch.cuda.set_device(ctx.local_rank)
+    except Exception as e:  # noqa: BLE001
+        dev_err = str(e) or type(e).__name__
+    if not agree(not dev_err):
+        raise CommUnavailable(f"device binding failed on some rank {dev_err}".strip())
     comm, err = None, ""
     try:
         comm = C.rccl_comm(obj[0], ctx.rank, ctx.world, ctx.local_rank)
