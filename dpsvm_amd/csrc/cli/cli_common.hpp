@@ -84,6 +84,7 @@ inline void usage_train(const char* prog, bool seq) {
                "   --solver S          :  auto (ws from 50k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
+               "   --ws-wss 1|2        :  sub-problem pair choice: 1 first order (reference), 2 second order\n"
                "   --ws-blocks P       :  ws-dense: up to P sub-problems per round on P workgroups (1..8; default 0 = auto:\n"
                "                          8 from 50k rows, halved after every damped round)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
@@ -105,7 +106,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
     OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL, OPT_WSBLOCKS,
-    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA
+    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -138,6 +139,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"ws-new", required_argument, 0, OPT_WSNEW}, {"eta", required_argument, 0, OPT_ETA}, {"ws-rel", required_argument, 0, OPT_WSREL},
       {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
+      {"ws-wss", required_argument, 0, OPT_WSWSS},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -237,6 +239,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_WSREL: o.p.ws_rel = (float)atof(optarg); break;
       case OPT_WSBLOCKS: o.p.ws_blocks = atoi(optarg); break;
       case OPT_WSINNER: o.p.ws_inner = atoi(optarg); break;
+      case OPT_WSWSS: o.p.ws_wss = atoi(optarg); break;
       case OPT_WSBLOCK: o.p.ws_block = atoi(optarg); break;
       case OPT_ETA: {
         const std::string v = optarg;
@@ -322,7 +325,8 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           "\"rows_computed\": %lld, \"x_passes\": %lld, \"spec_rows\": %lld, \"data\": \"%s\", "
           "\"exchange_mem\": \"%s\", \"dp_policy\": \"%s\", \"rows_per_group\": %lld, \"groups\": %lld, "
           "\"poll_batch\": %d, \"cus\": %d, \"blocks_per_cu\": %d, \"census\": \"%s\", \"engine_note\": \"%s\", "
-          "\"params\": %s}\n",
+          "\"rounds\": %lld, \"ws_blocks\": %d, \"ws_blocks_end\": %d, \"ws_one_block_from_round\": %lld, "
+          "\"ws_damped_rounds\": %lld, \"params\": %s}\n",
           backend.c_str(), json_escape(device).c_str(), r.world, (long long)n, d, o.p.C, o.p.gamma, o.p.eps,
           o.p.clip == ClipMode::Box ? "box" : "independent", (long long)r.iters, r.status,
           r.converged() ? "true" : "false", r.b, r.b_hi, r.b_lo, (long long)nsv, acc, x.t_load, r.t_setup,
@@ -333,7 +337,8 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           json_escape(o.synthetic.empty() ? o.file : "synthetic:" + o.synthetic).c_str(),
           x.setup.exchange_mem.c_str(), x.setup.dp_policy.c_str(), (long long)x.setup.rows_per_group,
           (long long)x.setup.groups, x.setup.poll_batch, x.setup.cus, x.setup.blocks_per_cu,
-          x.setup.census.c_str(), json_escape(x.setup.engine_note).c_str(), params_json(o.p).c_str());
+          x.setup.census.c_str(), json_escape(x.setup.engine_note).c_str(), (long long)r.outer, r.ws_blocks,
+          r.ws_blocks_end, (long long)r.ws_p1_round, (long long)r.ws_damped, params_json(o.p).c_str());
   fclose(fp);
 }
 
@@ -344,6 +349,10 @@ inline void print_outcome(const SolveResult& r, float eps) {
   } else {
     std::cout << "Converged at iteration number: " << r.iters << "\n";
   }
+  if (r.outer > 0)  // working-set engines: "iterations" are pair steps inside the rounds' sub-problems
+    std::cout << "Working-set rounds: " << r.outer << " (pair steps counted as iterations; blocks per round "
+              << r.ws_blocks << (r.ws_blocks_end != r.ws_blocks ? " -> " + std::to_string(r.ws_blocks_end) : "")
+              << ")\n";
   if (r.status == 4) std::cout << "WARNING: non-finite b_hi/b_lo encountered; training stopped\n";
   std::cout << "b: " << r.b << "\n";
 }

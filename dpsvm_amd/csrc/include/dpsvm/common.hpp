@@ -122,6 +122,9 @@ struct SolverParams {
                               // rows).  Adaptive: halved after every damped round (coupled blocks), 1 after an
                               // independent-clip event, then the one-block round kernels (smo_ws.hip)
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
+  int ws_wss = 0;             // sub-problem pair choice: 1 the reference's first-order rule (max f over I_low),
+                              // 2 second order (WSS2: max (f_lo - b_hi)^2 / eta); the stop test is unchanged;
+                              // 0 auto: second order when a row sample's mean off-diagonal K > 0.1
   int ws_block = 32;          // rounds per hipGraph block
   // eta's K(i_hi, i_lo) in the pair-at-a-time dense engines: 0 from the two X
   // rows (explicit difference, the same tree in every engine: bit parity), 1

@@ -246,7 +246,7 @@ struct alignas(16) WsCtrl {
   int32_t apply_idx[kWsMaxAll];  // rows whose alpha changed in the last round (multi-block: per-block segments)
   int32_t apply_line[kWsMaxAll]; // their lines
   float apply_coef[kWsMaxAll];   // their (alpha_new - alpha_old) * y
-  int32_t miss_row[kWsMax], miss_line[kWsMax];  // cache mode: rows to compute this round, their lines
+  int32_t miss_row[kWsMaxAll], miss_line[kWsMaxAll];  // cache mode: rows to compute this round, their lines
   int64_t rows_computed, row_hits;              // cache mode statistics
   // multi-block rounds
   int32_t uidx[2][kWsMaxAll];    // the union, newest first (previous-set retention)
@@ -315,6 +315,7 @@ struct WsArgs {
   double* part;        // [G_all][2] per-workgroup partial sums: d'Qd, g'd (this rank's at rank * G)
   int32_t rank;        // this rank (its partials slot)
   int32_t aux_stride;  // aux: [3][blocks][kWsMax] (f of every block first: one sum all-reduce with subg)
+  int32_t wss;         // sub-problem pair selection: 1 first order (the reference's), 2 second order (WSS2)
 };
 // u64 words of the working-set exchange region (both parities)
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {

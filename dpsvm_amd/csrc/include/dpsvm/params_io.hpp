@@ -56,6 +56,7 @@ void for_each_param(SolverParams& p, F&& f) {
   f("ws_rel", p.ws_rel);
   f("ws_blocks", p.ws_blocks);
   f("ws_inner", p.ws_inner);
+  f("ws_wss", p.ws_wss);
   f("ws_block", p.ws_block);
   f("eta", p.eta);
 }

@@ -74,6 +74,7 @@ struct GpuSetupInfo {
   int cus = 0, blocks_per_cu = 0;     // residency of the persistent kernel (occupancy API)
   std::string census = "n/a";         // residency census of the persistent grid: "ok" | "failed" | "n/a"
   std::string engine_note;            // why the engine was chosen / refused (fallbacks)
+  int ws_wss = 0;                     // working-set engines: sub-problem pair choice (1 first, 2 second order)
 };
 
 class GpuSolver {
@@ -171,7 +172,7 @@ struct WsSolveProbe {
 WsSolveProbe ws_solve_probe(const std::vector<float>& K, const std::vector<float>& f, const std::vector<float>& alpha,
                             const std::vector<float>& y, const std::vector<int32_t>& qb, int q_max, int blocks,
                             int p_round, float C, int clip, float eps, float rel, float eps_floor, float tau,
-                            float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter);
+                            float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter, int wss = 1);
 // ws_select: the f update of a round's alpha changes (apply rows: lines into
 // gram [L][ldg], coefficients) and the per-workgroup candidates.  blocks == 1:
 // the one-pass kernel; blocks > 1: pass 1 (d_f, line-search partials) and pass 2

@@ -85,6 +85,8 @@ void ws_merge_multi(const WsArgs& a, hipStream_t s);
 // kernels' previous set (run once, between two rounds)
 void ws_to_single(const WsArgs& a, hipStream_t s);
 bool ws_cache_supported(int64_t L, int q_max);
+// multi-block rounds in cache mode: the union's lines come from a 4096-line window
+bool ws_cache_multi_supported(int64_t L, int blocks, int q_max);
 // partitioned X, cache mode: out[i] = X row ctrl->miss_row[i] if this rank owns
 // it (rows off..off+nl-1 at x), else zeros; out_sq[i] = its global |x|^2
 void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* xsq, const WsCtrl* ctrl, int q_max,

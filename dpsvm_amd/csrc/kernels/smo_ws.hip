@@ -1069,13 +1069,15 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
 // diagonal q x q blocks, ws_solve<kMulti> one block per workgroup, and the
 // two-pass ws_select applies the combined step with the exact line search.
 // ---------------------------------------------------------------------------
-// exclusive prefix of counts 0..3 over kWsMergeThreads threads in thread order
+// exclusive prefix of counts 0 .. 2^BITS - 1 over kWsMergeThreads threads in
+// thread order (bit-plane ballots)
+template <int BITS = 2>
 __device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
   int pre = 0, wtot = 0;
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < BITS; ++b) {
     const uint64_t m = __ballot((v >> b) & 1);
     pre += __popcll(m & below) << b;
     wtot += __popcll(m) << b;
@@ -1100,6 +1102,7 @@ __device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
 // block gets up / low pairs, block 0 the global extremes (so a round always
 // holds the maximal violating pair and makes progress).
 constexpr int kMH = 2048;  // merge hash slots per side (load <= 0.28)
+constexpr int kWsWindowMulti = 4096;  // cache mode: CLOCK victim window of the multi-block merge
 __device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 21; }
 __device__ __forceinline__ void mh_insert(int32_t* keys, int32_t* vals, int32_t idx, int32_t v) {
   uint32_t h = mh_hash(idx);
@@ -1257,12 +1260,91 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   const int Q = min(Qmax, n_chosen + ptotal);
   __syncthreads();
   if (lead) WS_STAMP(14);
+  if (a.cache) {
+    // ---- kernel-row cache: a line for every union row.  A member's row is
+    // cached (slot_of) or takes a victim from the window of kWsWindowMulti
+    // lines after the CLOCK hand, skipping lines that hold a member (pinned
+    // while the round uses them); all misses at once (prefix scans), their
+    // rows computed next by one row GEMM.  Setup guarantees
+    // L >= 2 Qmax + kWsWindowMulti, so the window holds >= n_miss free lines. ----
+    int32_t* s_pin = (int32_t*)&s_k[0][0];  // the sort keys are dead: 4096 words
+    int32_t* s_victim = s_hash[0];         // the hash tables too: 2 x 2048 words
+    int32_t* s_line = s_hash[1];
+    const int L = a.L, hand = c->hand;
+    const int W = min(L, kWsWindowMulti);
+    for (int w = tid; w < kWsWindowMulti; w += kWsMergeThreads) s_pin[w] = 0;
+    __syncthreads();
+    int32_t ln[2] = {-1, -1};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + h * kWsMergeThreads;
+      if (u < Q) {
+        ln[h] = a.slot_of[s_idx[u]];
+        if (ln[h] >= 0) {
+          const int o = (ln[h] - hand + L) % L;
+          if (o < W) s_pin[o] = 1;
+        }
+      }
+    }
+    __syncthreads();
+    const bool m0 = tid < Q && ln[0] < 0, m1 = tid + kWsMergeThreads < Q && ln[1] < 0;
+    int n_miss = 0;
+    const int mrank = block_scan_merge<2>((int)m0 + (int)m1, s_wsum, &n_miss);
+    // free window slots 4t .. 4t + 3 in window order
+    constexpr int SPT = kWsWindowMulti / kWsMergeThreads;
+    static_assert(SPT == 4, "four window slots per merge thread");
+    bool fr[SPT];
+    int nf = 0;
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      fr[k] = SPT * tid + k < W && !s_pin[SPT * tid + k];
+      nf += (int)fr[k];
+    }
+    int n_free = 0;
+    const int frank = block_scan_merge<3>(nf, s_wsum, &n_free);
+    int at = frank, last_used = -1;
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      if (fr[k]) {
+        if (at < n_miss) {
+          s_victim[at] = (hand + SPT * tid + k) % L;
+          last_used = SPT * tid + k;
+        }
+        ++at;
+      }
+    }
+    __syncthreads();
+    if (last_used >= 0 && frank < n_miss && at >= n_miss) c->hand = (hand + last_used + 1) % L;  // the last victim
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + h * kWsMergeThreads;
+      if (u < Q && ln[h] < 0) {
+        const int r = mrank + (h == 1 ? (int)m0 : 0);
+        const int32_t row = s_idx[u];
+        const int32_t v = s_victim[r];
+        const int32_t old = a.key_of[v];
+        if (old >= 0) a.slot_of[old] = -1;  // evicted (never a member: members' lines are pinned)
+        a.key_of[v] = row;
+        a.slot_of[row] = v;
+        c->miss_row[r] = row;
+        c->miss_line[r] = v;
+        ln[h] = v;
+      }
+      if (u < Q) s_line[u] = ln[h];
+    }
+    if (lead) {
+      c->n_miss = n_miss;
+      c->rows_computed += n_miss;
+      c->row_hits += Q - n_miss;
+    }
+    __syncthreads();
+  }
   for (int u = tid; u < Q; u += kWsMergeThreads) {
     const int32_t row = s_idx[u];
     c->uidx[par][u] = row;
     const int pi = u >> 1, b = pi % P, la = 2 * (pi / P) + (u & 1);
     c->idx[par][b * a.q_max + la] = row;
-    c->line[par][b * a.q_max + la] = row;  // the resident Gram: line i is row i
+    c->line[par][b * a.q_max + la] = a.cache ? s_hash[1][u] : row;  // cache: s_line; dense: line i is row i
     atomicMax(&s_qb[b], la + 1);
   }
   __syncthreads();
@@ -1296,7 +1378,9 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArg
   }
   for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][p * a.q_max + t];
   __syncthreads();
-  ws_gather_row(b, c, s_idx, q, ra, a.gram + (int64_t)s_idx[ra] * a.ldg);
+  // the row's line (dense: the resident Gram's row itself)
+  const int64_t line = a.cache ? (int64_t)c->line[par][p * a.q_max + ra] : (int64_t)s_idx[ra];
+  ws_gather_row(b, c, s_idx, q, ra, a.gram + line * a.ldg);
   if (tid == 0 && blockIdx.x == 0) WS_STAMP(8);
 }
 
@@ -1414,7 +1498,12 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
 // kFull: q_max == kWsMax, the three 64-row slots fill a sub-Gram row (stride
 // 192): row reads need no clamp (columns q..191 hold zeros) and take immediate
 // LDS offsets
-template <bool kBox, bool kFull, bool kMulti>
+// kW2: second-order choice of the low row (Fan, Chen & Lin's WSS2, the rule
+// LIBSVM uses): hi = argmin f over I_up as in the reference, then lo = the
+// I_low row with f_lo > b_hi that maximises (f_lo - b_hi)^2 / eta(hi, lo) —
+// the pair whose step gains the most dual objective — instead of argmax f.
+// The stop test stays the reference's first-order one (b_lo = max f over I_low).
+template <bool kBox, bool kFull, bool kMulti, bool kW2>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
   __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
@@ -1494,23 +1583,49 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     float mu = fminf(fminf(fu[0], fu[1]), fu[2]);
     float ml = fminf(fminf(fl[0], fl[1]), fl[2]);
     wave_min2_f32(mu, ml);
-    const float bh = mu, bl = -ml;
-    const int ph = ws_argpos(fu, mu), pl = ws_argpos(fl, ml);
+    const float bh = mu;
+    float bl = -ml;  // first order: b_lo = max f over I_low (also the stop test's)
+    const int ph = ws_argpos(fu, mu);
+    int pl = -1;
+    float kh[3], kl[3];
+    if constexpr (!kW2) pl = ws_argpos(fl, ml);
     // one exit test: an empty side, the sub-problem's stop test, or NaN
     const bool open = (mu < INF) & (ml < INF) & (bl > bh + 2.0f * eps_in);
+    if constexpr (kW2) {
+      if (open && ph >= 0) {
+        // hi's sub-Gram row first, then the gain of every violating I_low row
+        // as a minimum of -gain (INF: not a candidate)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) kh[s] = K[ph * ldk + (kFull ? lane + 64 * s : min(lane + 64 * s, q - 1))];
+        float g[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const float dv = -fl[s] - bh;
+          float eta = (1.0f + 1.0f) - 2.0f * kh[s];
+          eta = eta >= a.tau ? eta : a.tau;
+          g[s] = ((fl[s] < INF) & (dv > 0.f)) ? -(dv * dv) * __builtin_amdgcn_rcpf(eta) : INF;
+        }
+        float gm = fminf(fminf(g[0], g[1]), g[2]), gm2 = gm;
+        wave_min2_f32(gm, gm2);
+        pl = gm < INF ? ws_argpos(g, gm) : -1;
+        if (pl >= 0) {
+          const int sl = pl >> 6;
+          bl = -readlane_f32(sl == 0 ? fl[0] : sl == 1 ? fl[1] : fl[2], pl & 63);  // f of the chosen lo
+        }
+      }
+    }
     if (!open || (ph | pl) < 0) {
       bad = open;  // a violating pair exists but no position matches it: NaN
       break;
     }
-    // every LDS read of the step in one batch: the pair's alphas / labels,
-    // the 2 x 2 block K(hi|lo, hi|lo) and the two sub-Gram rows
+    // every remaining LDS read of the step in one batch: the pair's alphas /
+    // labels, the 2 x 2 block K(hi|lo, hi|lo) and the sub-Gram rows
     const float a_hi = s_a[ph], y_hi = s_y[ph], a_lo = s_a[pl], y_lo = s_y[pl];
     const float khl = K[ph * ldk + pl], klh = K[pl * ldk + ph], khh = K[ph * ldk + ph], kll = K[pl * ldk + pl];
-    float kh[3], kl[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       const int p = kFull ? lane + 64 * s : min(lane + 64 * s, q - 1);
-      kh[s] = K[ph * ldk + p];
+      if constexpr (!kW2) kh[s] = K[ph * ldk + p];
       kl[s] = K[pl * ldk + p];
     }
     bool clipped = false;
@@ -1696,9 +1811,10 @@ void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
 }
 
 void ws_merge_multi(const WsArgs& a, hipStream_t s) {
-  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && !a.cache && !a.xpeer && a.G_all <= kWsMaxGroups &&
-                  a.q_max % 2 == 0,
-              "ws_merge_multi: multi-block rounds need ws-dense over collectives, <= 256 candidate lists, even q_max");
+  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && !a.xpeer && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
+                  (!a.cache || ws_cache_multi_supported(a.L, a.blocks, a.q_max)),
+              "ws_merge_multi: multi-block rounds need the collectives, <= 256 candidate lists, an even q_max and "
+              "(cache mode) L >= 2 P q_max + 4096 lines");
   dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
   post_launch("ws_merge_multi", s);
 }
@@ -1735,18 +1851,26 @@ void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* 
 
 bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max + dev::kWsWindow; }
 
+bool ws_cache_multi_supported(int64_t L, int blocks, int q_max) {
+  return L >= 2 * (int64_t)blocks * q_max + dev::kWsWindowMulti;
+}
+
 void ws_solve(const WsArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.q_max * a.q_max * sizeof(float);
-  const bool box = a.clip == (int)ClipMode::Box, full = a.q_max == kWsMax, multi = a.blocks > 1;
+  const bool box = a.clip == (int)ClipMode::Box, full = a.q_max == kWsMax, multi = a.blocks > 1, w2 = a.wss == 2;
   using Fn = void (*)(WsArgs);
-  static const Fn fns[8] = {dev::ws_solve_kernel<false, false, false>, dev::ws_solve_kernel<false, true, false>,
-                            dev::ws_solve_kernel<true, false, false>,  dev::ws_solve_kernel<true, true, false>,
-                            dev::ws_solve_kernel<false, false, true>,  dev::ws_solve_kernel<false, true, true>,
-                            dev::ws_solve_kernel<true, false, true>,   dev::ws_solve_kernel<true, true, true>};
-  const int v = (multi ? 4 : 0) + (box ? 2 : 0) + (full ? 1 : 0);
+#define WS_SOLVE_FNS(W2)                                                                                         \
+  dev::ws_solve_kernel<false, false, false, W2>, dev::ws_solve_kernel<false, true, false, W2>,                  \
+      dev::ws_solve_kernel<true, false, false, W2>, dev::ws_solve_kernel<true, true, false, W2>,                \
+      dev::ws_solve_kernel<false, false, true, W2>, dev::ws_solve_kernel<false, true, true, W2>,                \
+      dev::ws_solve_kernel<true, false, true, W2>, dev::ws_solve_kernel<true, true, true, W2>
+  static const Fn fns[16] = {WS_SOLVE_FNS(false), WS_SOLVE_FNS(true)};
+#undef WS_SOLVE_FNS
+  const int v = (w2 ? 8 : 0) + (multi ? 4 : 0) + (box ? 2 : 0) + (full ? 1 : 0);
   const Fn fn = fns[v];
-  static size_t attr[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024,
-                           64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
+  static size_t attr[16] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024,
+                            64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
   size_t& at = attr[v];
   if (lds > at) {
     HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -192,6 +192,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_rel", &SolverParams::ws_rel)
       .def_readwrite("ws_blocks", &SolverParams::ws_blocks)
       .def_readwrite("ws_inner", &SolverParams::ws_inner)
+      .def_readwrite("ws_wss", &SolverParams::ws_wss)
       .def_readwrite("ws_block", &SolverParams::ws_block)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
       .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });
@@ -370,6 +371,7 @@ PYBIND11_MODULE(_C, m) {
         d["blocks_per_cu"] = i.blocks_per_cu;
         d["census"] = i.census;
         d["engine_note"] = i.engine_note;
+        d["ws_wss"] = i.ws_wss;
         return d;
       })
       .def("solve", [](GpuSolver& s, const Checkpoint* resume, py::object progress) {
@@ -481,10 +483,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("k_ws_solve", [vi](const F32& K, const F32& f, const F32& alpha, const F32& y, const I32& qb, int q_max,
                            int blocks, int p_round, float C, int clip, float eps, float rel, float eps_floor, float tau,
-                           float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter) {
+                           float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter, int wss) {
     const auto r = kernels::ws_solve_probe(from_np(K), from_np(f), from_np(alpha), from_np(y), vi(qb), q_max, blocks,
                                            p_round, C, clip, eps, rel, eps_floor, tau, b_hi, b_lo, inner_max, iter0,
-                                           max_iter);
+                                           max_iter, wss);
     py::dict d;
     d["alpha"] = to_np(r.alpha);
     d["steps"] = r.steps;

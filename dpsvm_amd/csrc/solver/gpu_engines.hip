@@ -340,9 +340,9 @@ void ws_allreduce_sub(GpuSolver::Impl& m, const WsArgs& w) {
 }
 
 // partitioned X, cache mode: the packed miss rows (owner's row, zeros elsewhere)
-void ws_allreduce_rows(GpuSolver::Impl& m) {
+void ws_allreduce_rows(GpuSolver::Impl& m, int64_t rows) {
   if (!m.collectives()) return;
-  const size_t count = (size_t)m.wsa.q_max * m.dp;
+  const size_t count = (size_t)rows * m.dp;
   if (m.comm->device_memory()) {
     m.comm->allreduce_sum_f32(m.wsxq, count, m.stream);
     return;
@@ -377,11 +377,15 @@ void capture_rounds(GpuSolver::Impl& m, int B, hipGraph_t* graph, hipGraphExec_t
   HIP_CHECK(hipGraphInstantiate(exec, *graph, nullptr, nullptr, 0));
 }
 
-// Working-set rounds on the resident Gram (smo_ws.hip).  Seed: the Gram GEMM,
-// the control record (no working set yet) and the first candidate selection;
-// a block is B rounds of [ws_gather, ws_solve, ws_select] (one hipGraph), so f is
-// consistent with alpha at every block boundary (checkpoints need no pending
-// pair) and the host polls the status one block behind like the SMO engines.
+// Working-set rounds (smo_ws.hip) on the resident Gram (ws-dense) or on a
+// kernel-row cache (ws-cache: the Gram does not fit HBM).  A round is
+//   [merge (+ cache mode: line assignment, one MFMA GEMM for the set's missing
+//   rows)] -> gather (sub-Gram rows) -> solve (LDS sub-problem) -> select (f
+//   update + next candidates)
+// and a block is B rounds (one hipGraph), so f is consistent with alpha at
+// every block boundary (checkpoints need no pending pair) and the host polls
+// the status one block behind like the SMO engines.  Seed: (ws-dense) the Gram
+// GEMM, the control record (no working set yet) and the first candidates.
 //
 // Multi-block rounds (wsa.blocks = P > 1) are adaptive: the device halves the
 // block count after every damped round (strongly coupled blocks) and drops to
@@ -389,9 +393,9 @@ void capture_rounds(GpuSolver::Impl& m, int B, hipGraph_t* graph, hipGraphExec_t
 // one-block round kernels (cheaper merge, one f-update pass) at the first block
 // boundary whose completed rounds include the one that set it — a value every
 // rank reads identically, so every rank switches at the same round.
-struct WsDense final : DenseBase {
+template <class Base, bool kCache>
+struct WsRounds : Base {
   bool single = false;  // multi-block engine now running one-block rounds
-  EngineKind kind() const override { return EngineKind::WsDense; }
   int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
   // the one-block view of a multi-block engine's buffers: sub-Gram at the start
   // of wssub, its f / alpha / y right after it (one contiguous sum all-reduce)
@@ -400,10 +404,29 @@ struct WsDense final : DenseBase {
     w.blocks = 1;
     w.aux = m.wssub + (size_t)w.q_max * w.q_max;
     w.aux_stride = kWsMax;
+    // the one-block engine's set turnover (multi-block rounds replace the
+    // whole union): 3/4 new rows, the newest quarter of the previous set kept
+    w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, w.q_max) : 3 * w.q_max / 4);
     return w;
   }
+  // cache mode: the kernel rows of the round's misses (<= blocks x q_max rows), one GEMM
+  static void miss_rows(GpuSolver::Impl& m, const WsArgs& w) {
+    const int64_t mmax = (int64_t)w.blocks * w.q_max;
+    const float* B = m.x + (size_t)(m.off - m.args.x_row0) * m.dp;  // the owned rows
+    if (m.replicated) {
+      launch::rbf_rows_indexed(m.x, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), mmax, B, m.xsq + m.off, m.nl,
+                               m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
+    } else {
+      launch::ws_pack_rows(m.x, m.off, m.nl, m.dp, m.xsq, m.wsctrl, (int)mmax, m.wsxq, m.wsxqsq, m.stream);
+      ws_allreduce_rows(m, mmax);
+      launch::rbf_rows_indexed(m.wsxq, m.wsxqsq, m.wsiota, m.wsctrl_n_miss(), mmax, B, m.xsq + m.off, m.nl, m.dp,
+                               m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
+    }
+  }
   static void round(GpuSolver::Impl& m, const WsArgs& w) {
-    if (w.blocks > 1) launch::ws_merge_multi(w, m.stream);  // else merged inside ws_gather
+    if (w.blocks > 1) launch::ws_merge_multi(w, m.stream);
+    else if (kCache) launch::ws_merge(w, m.stream);  // ws-dense one-block rounds merge inside ws_gather
+    if (kCache) miss_rows(m, w);
     launch::ws_gather(w, m.stream);
     ws_allreduce_sub(m, w);
     launch::ws_solve(w, m.stream);
@@ -416,8 +439,7 @@ struct WsDense final : DenseBase {
     }
     ws_allgather_cand(m);
   }
-  void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {
-    gram(m, res);
+  void seed_rounds(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo) {
     single = false;
     if (m.wsa.blocks > 1) HIP_CHECK(hipMemsetAsync(m.wsa.dalpha, 0, (size_t)m.n * 4, m.stream));
     WsCtrl c;
@@ -430,15 +452,15 @@ struct WsDense final : DenseBase {
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
     ws_allgather_cand(m);
-    if (ws_graphs(m) && !m.gexec) capture_rounds(m, block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });
+    if (ws_graphs(m) && !m.gexec) capture_rounds(m, this->block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });
   }
   void observe(GpuSolver::Impl& m, const SmoStatus& st, int64_t blocks_done) override {
     if (single || m.wsa.blocks <= 1 || st.ws_p1_round <= 0) return;
-    if (st.ws_p1_round > blocks_done * block(m.p)) return;  // set by the block in flight: next time
+    if (st.ws_p1_round > blocks_done * this->block(m.p)) return;  // set by the block in flight: next time
     single = true;
     const WsArgs w = one_block(m);
     launch::ws_to_single(w, m.stream);
-    if (ws_graphs(m) && !m.gexec1) capture_rounds(m, block(m.p), &m.graph1, &m.gexec1, [&] { round(m, w); });
+    if (ws_graphs(m) && !m.gexec1) capture_rounds(m, this->block(m.p), &m.graph1, &m.gexec1, [&] { round(m, w); });
   }
   void run_block(GpuSolver::Impl& m, int B) override {
     hipGraphExec_t g = single ? m.gexec1 : m.gexec;
@@ -452,52 +474,21 @@ struct WsDense final : DenseBase {
   Pending pending(GpuSolver::Impl&) override { return {}; }  // alphas committed every round
 };
 
-// Working-set rounds on a kernel-row cache (Gram too large for HBM).  A round
-// is [ws_merge (set + line assignment), one MFMA GEMM for the set's missing
-// rows (rbf_rows_indexed), ws_gather (sub-Gram from the lines), ws_solve,
-// ws_select (f update from the changed rows' lines + candidates)] — the X
-// pass of a round computes up to ~3/4 of q rows at once instead of 2 (+16
-// speculative) per SMO iteration.
-struct WsCache final : Engine {
+struct WsDense final : WsRounds<DenseBase, false> {
+  EngineKind kind() const override { return EngineKind::WsDense; }
+  void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) override {
+    gram(m, res);
+    seed_rounds(m, iter0, b_hi, b_lo);
+  }
+};
+
+// ws-cache: the X pass of a round computes all of its set's missing rows in one
+// GEMM (up to blocks x q_max rows) instead of 2 (+16 speculative) rows per SMO
+// iteration in the pair-at-a-time cache engines.
+struct WsCache final : WsRounds<Engine, true> {
   EngineKind kind() const override { return EngineKind::WsCache; }
-  int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
-  static void round(GpuSolver::Impl& m) {
-    const WsArgs& w = m.wsa;
-    launch::ws_merge(w, m.stream);
-    const float* B = m.x + (size_t)(m.off - m.args.x_row0) * m.dp;  // the owned rows
-    if (m.replicated) {
-      launch::rbf_rows_indexed(m.x, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), w.q_max, B, m.xsq + m.off, m.nl,
-                               m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
-    } else {
-      launch::ws_pack_rows(m.x, m.off, m.nl, m.dp, m.xsq, m.wsctrl, w.q_max, m.wsxq, m.wsxqsq, m.stream);
-      ws_allreduce_rows(m);
-      launch::rbf_rows_indexed(m.wsxq, m.wsxqsq, m.wsiota, m.wsctrl_n_miss(), w.q_max, B, m.xsq + m.off, m.nl,
-                               m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
-    }
-    launch::ws_gather(w, m.stream);
-    ws_allreduce_sub(m, w);
-    launch::ws_solve(w, m.stream);
-    launch::ws_select(w, m.stream);
-    ws_allgather_cand(m);
-  }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult&) override {
-    WsCtrl c;
-    memset(&c, 0, sizeof(c));
-    c.iter = iter0;
-    c.done = kRunning;
-    c.b_hi = b_hi;
-    c.b_lo = b_lo;
-    HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
-    launch::ws_select(m.wsa, m.stream);
-    ws_allgather_cand(m);
-    if (ws_graphs(m) && !m.gexec) capture_rounds(m, block(m.p), &m.graph, &m.gexec, [&] { round(m); });
-  }
-  void run_block(GpuSolver::Impl& m, int B) override {
-    if (m.gexec) {
-      HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
-    } else {
-      for (int i = 0; i < B; ++i) round(m);
-    }
+    seed_rounds(m, iter0, b_hi, b_lo);
   }
 };
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cmath>
 #include <chrono>
 #include <thread>
 
@@ -129,6 +130,29 @@ bool distinct_devices(GpuSolver::Impl& m) {
     for (int b = a + 1; b < m.world; ++b)
       if (strncmp(all[a].bus, all[b].bus, sizeof(Id::bus)) == 0) return false;
   return true;
+}
+
+// mean off-diagonal kernel value K(x_a, x_b) over a deterministic sample of up
+// to 96 rows (fixed stride, float64): how strongly the rows of a working set
+// couple — ~0 when K ~ I (MNIST-shape at gamma 0.25), ~0.85 for covtype-shape
+constexpr double kWsW2Coupling = 0.1;
+double mean_offdiag_kernel(const float* xh, int64_t rows, int d, float gamma) {
+  const int64_t s = std::min<int64_t>(96, rows);
+  if (s < 2) return 0.0;
+  const int64_t stride = rows / s;
+  double acc = 0.0;
+  for (int64_t a = 0; a < s; ++a)
+    for (int64_t b = a + 1; b < s; ++b) {
+      const float* xa = xh + (size_t)(a * stride) * d;
+      const float* xb = xh + (size_t)(b * stride) * d;
+      double d2 = 0.0;
+      for (int k = 0; k < d; ++k) {
+        const double t = (double)xa[k] - (double)xb[k];
+        d2 += t * t;
+      }
+      acc += std::exp(-(double)gamma * d2);
+    }
+  return acc / (double)(s * (s - 1) / 2);
 }
 
 // the most ranks any one device carries (collective: every rank calls it)
@@ -457,9 +481,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool wsc_fits_pre = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
   int32_t ws_G = 0, ws_rpt = 0;
   if (ws_cand || wsc_cand) launch::ws_geometry(nl_max, m.world, &ws_G, &ws_rpt);
-  // multi-block rounds (ws_blocks > 1): ws-dense, the union merge reads <= 256
-  // candidate lists, an even q_max; at world > 1 over the collectives (their
-  // extra per-round all-gather of line-search partials has no peer-exchange form)
+  // multi-block rounds (ws_blocks > 1): the union merge reads <= 256 candidate
+  // lists, an even q_max; at world > 1 over the collectives (their extra
+  // per-round all-gather of line-search partials has no peer-exchange form)
   DPSVM_CHECK(m.p.ws_blocks >= 0 && m.p.ws_blocks <= kWsMaxBlocks,
               "ws_blocks must be 0 (auto) or 1.." + std::to_string(kWsMaxBlocks));
   // host communicators stage every collective through host memory (three per
@@ -470,8 +494,12 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // ws_blocks auto (0): every block from kWsAutoBlocksRows rows on (the round's
   // fixed cost is amortised over P sub-problems; small problems need few rounds)
   const int want_blocks = m.p.ws_blocks > 0 ? m.p.ws_blocks : (n >= kWsAutoBlocksRows ? kWsMaxBlocks : 1);
-  const bool multi_ok = want_blocks > 1 && ws_cand && ws_q % 2 == 0 && (int64_t)ws_G * m.world <= kWsMaxGroups &&
-                        m.p.exchange != 2 && multi_comm;
+  // ws-cache takes them too when its cache holds the union's lines plus the
+  // victim window (L >= 2 P q_max + 4096; agreed: L follows each device's free memory)
+  const bool wsc_multi = wsc_fits_pre && launch::ws_cache_multi_supported(m.L, want_blocks, ws_q);
+  bool multi_ok = want_blocks > 1 && (ws_cand || wsc_multi) && ws_q % 2 == 0 &&
+                  (int64_t)ws_G * m.world <= kWsMaxGroups && m.p.exchange != 2 && multi_comm;
+  if (m.world > 1) multi_ok = m.all_agree(multi_ok, m.comm, m.world);
   // Residency of the ws peer exchange: gather workgroup a of every rank spins
   // until the same workgroup of every other rank has pushed its row, so with
   // ranks sharing a device (rehearsals) the spinning gathers of the other
@@ -571,6 +599,18 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // defaults measured on the MNIST-shape headline (profiles/r2_ws_param_sweep.txt)
     w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, ws_q) : 3 * ws_q / 4);
     w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * ws_q;
+    DPSVM_CHECK(m.p.ws_wss >= 0 && m.p.ws_wss <= 2, "ws_wss must be 0 (auto), 1 (first order) or 2 (second order)");
+    if (m.p.ws_wss > 0) {
+      w.wss = m.p.ws_wss;
+    } else {
+      // auto: second order where the kernel couples rows (mean off-diagonal K of
+      // a row sample: covtype-shape 0.85, synthetic-2m 0.85 -> WSS2 converges
+      // covtype-200k in 21.2 s vs 27.7 s; MNIST-shape 0.0000, adult 0.0002 ->
+      // WSS2 only adds ~0.25 us per pair step; profiles/r3_wss2_*.txt)
+      const double k = mean_offdiag_kernel(xh, n_x_rows, d, m.gamma);
+      w.wss = m.all_agree(k > kWsW2Coupling, m.comm, m.world) ? 2 : 1;
+    }
+    m.info.ws_wss = w.wss;
     DPSVM_CHECK(m.p.ws_rel >= 0.f && m.p.ws_rel < 1.f, "ws_rel must be in [0, 1)");
     w.rel_local = m.p.ws_rel;
     // sub-problem tolerance ws_rel * max(eps, gap / 2): floored at ws_rel * eps
@@ -582,14 +622,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.tau = m.p.tau;
     w.clip = (int)m.p.clip;
     w.max_iter = m.p.max_iter;
-    // multi-block rounds: ws-dense with no per-round communication (world 1 or
-    // every rank solving the whole problem), an even q_max
+    // multi-block rounds (adaptive block count, smo_ws.hip)
     w.blocks = 1;
     if (want_blocks > 1) {
-      if (multi_ok && m.kind == EngineKind::WsDense && !m.xch) w.blocks = want_blocks;
+      if (multi_ok && !m.xch) w.blocks = want_blocks;
       else if (m.p.ws_blocks > 1) m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
-                                 "ws_blocks > 1 needs ws-dense, an even ws_size and <= 256 candidate lists over "
-                                 "the collectives: one block per round";
+                                 "ws_blocks > 1 needs an even ws_size, <= 256 candidate lists over the collectives "
+                                 "and (ws-cache) >= 2 P ws_size + 4096 lines: one block per round";
     }
     // multi-block rounds replace the whole union each round by default (measured on the
     // headline at P = 8: 3/4 q new 0.0506 s, all new 0.0493 s; profiles/r2_ws_blocks_sweep.txt)
@@ -628,11 +667,12 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       w.xtimeout_ticks = (int64_t)(std::max(1e-6, m.p.xch_timeout_s) * 1e8);
     }
     if (w.cache && !m.replicated) {
-      m.wsxq = dmalloc<float>((size_t)ws_q * m.dp, &m.bytes);
-      m.wsxqsq = dmalloc<float>((size_t)ws_q, &m.bytes);
-      m.wsiota = dmalloc<int32_t>((size_t)ws_q, &m.bytes);
-      std::vector<int32_t> io((size_t)ws_q);
-      for (int i = 0; i < ws_q; ++i) io[i] = i;
+      const int64_t rows = (int64_t)w.blocks * ws_q;  // the round's misses at most
+      m.wsxq = dmalloc<float>((size_t)rows * m.dp, &m.bytes);
+      m.wsxqsq = dmalloc<float>((size_t)rows, &m.bytes);
+      m.wsiota = dmalloc<int32_t>((size_t)rows, &m.bytes);
+      std::vector<int32_t> io((size_t)rows);
+      for (int64_t i = 0; i < rows; ++i) io[i] = (int32_t)i;
       HIP_CHECK(hipMemcpyAsync(m.wsiota, io.data(), io.size() * 4, hipMemcpyHostToDevice, m.stream));
       HIP_CHECK(hipStreamSynchronize(m.stream));
     }

@@ -111,7 +111,7 @@ WsMergeProbe ws_merge_multi_probe(const std::vector<uint64_t>& cand, int G, int 
 WsSolveProbe ws_solve_probe(const std::vector<float>& K, const std::vector<float>& f, const std::vector<float>& alpha,
                             const std::vector<float>& y, const std::vector<int32_t>& qb, int q_max, int blocks,
                             int p_round, float C, int clip, float eps, float rel, float eps_floor, float tau,
-                            float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter) {
+                            float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter, int wss) {
   DPSVM_CHECK(blocks >= 1 && blocks <= kWsMaxBlocks && (int)qb.size() == blocks && q_max >= 2 && q_max <= kWsMax,
               "ws_solve_probe: 1 <= blocks <= 8, qb per block, q_max <= 192");
   const size_t nq = (size_t)blocks * q_max;
@@ -162,6 +162,7 @@ WsSolveProbe ws_solve_probe(const std::vector<float>& K, const std::vector<float
   a.tau = tau;
   a.clip = clip;
   a.max_iter = max_iter;
+  a.wss = wss;
   a.world = 1;
   a.ctrl = dc;
   launch::ws_solve(a, st.s);

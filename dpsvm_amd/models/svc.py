@@ -113,6 +113,7 @@ class SVCConfig:
     # after every damped round (coupled blocks), then the one-block round kernels (smo_ws.hip)
     ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
+    ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
     ws_block: int = 32              # rounds per hipGraph block
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
 
@@ -175,6 +176,7 @@ class SVCConfig:
         p.ws_rel = float(self.ws_rel)
         p.ws_blocks = int(self.ws_blocks)
         p.ws_inner = int(self.ws_inner)
+        p.ws_wss = int(self.ws_wss)
         p.ws_block = int(self.ws_block)
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         return p

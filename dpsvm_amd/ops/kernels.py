@@ -193,12 +193,14 @@ def ws_merge_multi(cand, blocks: int, q_max: int, n_new: int, eps: float, prev_u
 
 def ws_solve(K, f, alpha, y, qb, q_max: int, C_: float, clip: str = "independent", eps: float = 1e-3,
              rel: float = 0.3, eps_floor: float = 3e-4, tau: float = 1e-12, b_hi: float = 0.0, b_lo: float = 0.0,
-             inner_max: int = 768, p_round: int | None = None, iteration: int = 0, max_iter: int = 1 << 40) -> dict:
+             inner_max: int = 768, p_round: int | None = None, iteration: int = 0, max_iter: int = 1 << 40,
+             wss: int = 1) -> dict:
     """One launch of the sub-problem solver (ws_solve_kernel): P = len(qb)
     blocks, block p with qb[p] rows, sub-Gram K[p] ([q_max][q_max]) and f /
     alpha / y [p][q_max]; b_hi / b_lo = the round's global selection (the local
     tolerance is max(eps_floor, rel (b_lo - b_hi) / 2)).  P > 1 runs the
-    multi-block kernel (p_round active blocks share max_iter)."""
+    multi-block kernel (p_round active blocks share max_iter).  wss: 1 the
+    reference's first-order pair choice, 2 second order (WSS2)."""
     import numpy as np
 
     P = len(qb)
@@ -206,7 +208,7 @@ def ws_solve(K, f, alpha, y, qb, q_max: int, C_: float, clip: str = "independent
     return load().k_ws_solve(f32(K), f32(f), f32(alpha), f32(y), np.asarray(qb, dtype=np.int32), q_max, P,
                              P if p_round is None else p_round, float(C_), 1 if clip == "box" else 0, float(eps),
                              float(rel), float(eps_floor), float(tau), float(b_hi), float(b_lo), int(inner_max),
-                             int(iteration), int(max_iter))
+                             int(iteration), int(max_iter), int(wss))
 
 
 def ws_select(gram, f, alpha, y, dalpha, apply_lines, apply_coef, nab, C_: float, q_max: int = 192,

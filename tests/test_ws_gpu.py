@@ -446,3 +446,66 @@ def test_ws_multi_block_rccl_one_rank_collective_path():
     assert "ws_blocks" not in got.setup_info_.get("engine_note", "")
     assert got.n_iter_ == ref.n_iter_ and got.n_rounds_ == ref.n_rounds_
     assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
+
+
+def test_ws_multi_block_checkpoint_resume(tmp_path):
+    """Multi-block rounds (4 blocks, box clipping) stopped at half the pair
+    steps with a checkpoint, resumed: the resumed run reaches the uninterrupted
+    run's optimum (unique with box clipping)."""
+    X, y = synthetic("mnist", n=6000, seed=11)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, clip="box", device="cuda", solver="ws", ws_blocks=4)
+    full = SVC(**kw).fit(X, y)
+    assert full.stats_["ws_blocks"] == 4
+    ck = str(tmp_path / "wsm.ck")
+    part = SVC(max_iter=full.n_iter_ // 2, checkpoint_path=ck, checkpoint_every=10**9, **kw).fit(X, y)
+    assert not part.converged_
+    res = SVC(**kw).fit(X, y, resume=ck)
+    assert res.converged_ and abs(res.b_ - full.b_) < 1e-2
+    assert _kkt_gap(X, y, res.alpha_, 10.0, 0.25) < 2.2e-3
+    assert np.abs(res.alpha_ - full.alpha_).max() < 0.05 * 10.0
+
+
+@pytest.mark.parametrize("clip", ["independent", "box"])
+def test_ws_adaptive_blocks_fall_back_to_one_block_rounds(clip):
+    """Coupled data (adult-shape, C = 100): the adaptive block count falls from
+    8 on damped rounds (or to 1 on a clip event with independent clipping), and
+    at 1 the engine runs the one-block round kernels; the run converges to the
+    reference stop test on the exact gradient in no more rounds than one block
+    per round, and never collapses into the ~3.5-pair-step rounds of round 2."""
+    X, y = synthetic("adult", n=6000, seed=4)
+    kw = dict(C=100.0, gamma=0.5, eps=1e-3, clip=clip, device="cuda", solver="ws")
+    m8 = SVC(ws_blocks=8, **kw).fit(X, y)
+    m1 = SVC(ws_blocks=1, **kw).fit(X, y)
+    assert m8.converged_ and m1.converged_
+    st = m8.stats_
+    print(f"{clip}: P=8 rounds {m8.n_rounds_} steps {m8.n_iter_} end {st['ws_blocks_end']} one-block from round "
+          f"{st['ws_p1_round']} damped {st['ws_damped']} | P=1 rounds {m1.n_rounds_} steps {m1.n_iter_}")
+    assert st["ws_blocks"] == 8
+    if st["ws_blocks_end"] == 1:  # fell back: from a round the status reported
+        assert st["ws_p1_round"] > 0
+    else:
+        assert st["ws_p1_round"] == 0
+    # no short-round collapse after a fallback (round 2: ~3.5 pair steps per round)
+    assert m8.n_rounds_ <= 1.5 * m1.n_rounds_ + 64
+    assert m8.n_iter_ / m8.n_rounds_ > 0.5 * m1.n_iter_ / m1.n_rounds_
+    assert _kkt_gap(X, y, m8.alpha_, 100.0, 0.5) < 2e-3 + 2e-4
+
+
+@pytest.mark.parametrize("clip", ["independent", "box"])
+def test_ws_cache_multi_block_bit_identical_to_resident_gram(clip):
+    """Multi-block rounds on the kernel-row cache: the union's lines come from
+    a 4096-line CLOCK window (misses computed by one row GEMM per round).  The
+    K values and the round arithmetic are the dense engine's, so the trajectory
+    — including the adaptive block count — is bit-identical to ws-dense with the
+    same blocks, with a cache small enough to evict."""
+    X, y = synthetic("mnist", n=9000, seed=12)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, clip=clip, device="cuda", solver="ws", ws_blocks=4, ws_size=64)
+    dense = SVC(**kw).fit(X, y)
+    cache = SVC(force_cache=True, cache_lines=4700, **kw).fit(X, y)
+    assert dense.setup_info_["iteration"] == "ws-dense" and cache.setup_info_["iteration"] == "ws-cache"
+    assert "ws_blocks" not in cache.setup_info_.get("engine_note", "")
+    assert cache.stats_["ws_blocks"] == 4
+    assert cache.converged_ and cache.n_iter_ == dense.n_iter_ and cache.n_rounds_ == dense.n_rounds_
+    assert np.array_equal(cache.alpha_, dense.alpha_) and cache.b_ == dense.b_
+    assert cache.stats_["ws_blocks_end"] == dense.stats_["ws_blocks_end"]
+    assert cache.stats_["rows_computed"] > 4700  # more rows than lines: evictions happened

@@ -183,9 +183,10 @@ def pair_step_model(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, tau, box, same):
     return a_hi_new, a_lo_new, f32(f32(a_hi_new - a_hi) * y_hi), f32(f32(a_lo_new - a_lo) * y_lo), clipped
 
 
-def solve_model(Kq, f, a, y, C, box, eps_in, tau, cap):
+def solve_model(Kq, f, a, y, C, box, eps_in, tau, cap, w2=False):
     """the ws_solve loop in float32 (IEEE division where the kernel uses a
-    refined v_rcp: results agree to ~1 ulp per step)"""
+    refined v_rcp: results agree to ~1 ulp per step).  w2: the low row by the
+    second-order gain (f_lo - b_hi)^2 / eta(hi, lo) (WSS2)."""
     f32 = np.float32
     Kq = Kq.astype(np.float32)
     a = a.astype(np.float32).copy()
@@ -199,6 +200,12 @@ def solve_model(Kq, f, a, y, C, box, eps_in, tau, cap):
         if not (mu < np.inf and ml < np.inf and bl > f32(bh + f32(f32(2.0) * f32(eps_in)))):
             break
         ph, pl = int(np.argmin(fu)), int(np.argmin(fl))
+        if w2:
+            dv = (-fl - bh).astype(np.float32)
+            eta = np.maximum(np.float32(2.0) - np.float32(2.0) * Kq[ph, :], np.float32(tau)).astype(np.float32)
+            g = np.where(np.isfinite(fl) & (dv > 0), -(dv * dv) / eta, np.inf)
+            pl = int(np.argmin(g))
+            bl = f32(-fl[pl])
         a_hi_new, a_lo_new, c_hi, c_lo, cl = pair_step_model(a[ph], a[pl], y[ph], y[pl], bh, bl, Kq[ph, pl], C, tau,
                                                              box, ph == pl)
         clipped_any |= cl
@@ -452,3 +459,34 @@ def test_ws_select_one_pass_matches_model(K):
     np.testing.assert_array_equal(got["alpha"], a)
     cand = np.asarray(got["cand"], dtype=np.uint64).reshape(G, 2, 4)
     np.testing.assert_array_equal(cand, candidates_model(got["f"], a, y, C, G, rpt))
+
+
+@pytest.mark.parametrize("clip", ["independent", "box"])
+def test_ws_solve_second_order_matches_model(K, clip):
+    """WSS2 (ws_wss = 2): hi by the reference's first-order rule, lo by the
+    largest (f_lo - b_hi)^2 / eta(hi, lo); the first steps match the numpy
+    model exactly, and the full solve ends on the same first-order stop test."""
+    rng = np.random.default_rng(91 + (clip == "box"))
+    C, q, q_max = 2.0, 120, 192
+    Kq, f, a, y = sub_problem(rng, q, C, gamma=0.05)  # coupled rows: the choice differs from first order
+    bh, bl = extremes(f, a, y, C)
+    eps_floor = np.float32(3e-4)
+    eps_in = max(eps_floor, np.float32(np.float32(0.3 * np.float32(0.5)) * np.float32(bl - bh)))
+    Kp, fp, ap, yp = padded_block(Kq, f, a, y, q_max)
+    box = clip == "box"
+    for cap in (1, 3, 8):
+        got = K.ws_solve(Kp, fp, ap, yp, [q], q_max, C, clip=clip, eps_floor=eps_floor, b_hi=bh, b_lo=bl,
+                         inner_max=cap, wss=2)
+        ref_a, ref_steps, _ = solve_model(Kq, f, a, y, C, box, eps_in, 1e-12, cap, w2=True)
+        assert got["steps"] == [ref_steps]
+        np.testing.assert_allclose(got["alpha"][:q], ref_a, rtol=2e-6, atol=2e-6 * C)
+    first = solve_model(Kq, f, a, y, C, box, eps_in, 1e-12, 1, w2=False)[0]
+    second = solve_model(Kq, f, a, y, C, box, eps_in, 1e-12, 1, w2=True)[0]
+    assert not np.array_equal(first, second)  # the case really exercises a different choice
+    got = K.ws_solve(Kp, fp, ap, yp, [q], q_max, C, clip=clip, eps_floor=eps_floor, b_hi=bh, b_lo=bl,
+                     inner_max=4 * q_max, wss=2)
+    an = got["alpha"][:q]
+    fn = f + Kq.astype(np.float64) @ ((an.astype(np.float64) - a) * y)
+    if got["steps"][0] < 4 * q_max:
+        bh2, bl2 = extremes(fn, an, y, C)
+        assert bl2 <= bh2 + 2 * eps_in + 1e-4
