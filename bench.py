@@ -100,6 +100,9 @@ def parse(argv=None):
     ap.add_argument("--ws-rel", type=float, default=0.3)
     ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
     ap.add_argument("--ws-block", type=int, default=32)
+    ap.add_argument("--ws-t-halve", type=float, default=None, help="multi-block: damped rounds below this t halve P")
+    ap.add_argument("--ws-no-clip-fallback", action="store_true",
+                    help="multi-block, independent clipping: keep the blocks after a clip event")
     ap.add_argument("--ws-wss", type=int, default=None, choices=[0, 1, 2],
                     help="sub-problem pair choice: 1 first order (the reference's rule), 2 second order (WSS2), "
                          "0 auto (second order when the kernel couples rows); default: the library's (auto)")
@@ -168,6 +171,8 @@ def main(argv=None) -> int:
                     xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
                     ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, ws_blocks=a.ws_blocks, ws_inner=a.ws_inner, eta=a.eta,
                     **({} if a.ws_wss is None else {"ws_wss": a.ws_wss}),
+                    **({} if a.ws_t_halve is None else {"ws_t_halve": a.ws_t_halve}),
+                    **({"ws_clip_fallback": False} if a.ws_no_clip_fallback else {}),
                     xch_timeout_s=a.xch_timeout if a.xch_timeout is not None else (30.0 if multi else 120.0))
     params = cfg.to_native(X.shape[1])
     if ctx.rank == 0:

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""PROJECTION (not a measurement) of the sharded headline solve at 1/2/4/8
+MI355X, from the one-GPU measurements of bench/shard_projection.py plus an
+explicitly ASSUMED cost of the per-round collectives over xGMI.
+
+Per round, a rank of P:
+  * runs the merge, the sub-Gram gather / load and the P-block solve
+    redundantly (identical on every rank: the measured one-GPU times);
+  * runs the two f-update passes over its n / P rows (measured time / P);
+  * pays the launch gaps of the round graph (measured);
+  * waits for three collectives: the candidate all-gather (tiny), the sum
+    all-reduce of the P sub-Grams + members' f (blocks x (q^2 + 192) floats),
+    the line-search partials all-gather (tiny) — ASSUMED latency L each plus
+    the all-reduce's ring traffic 2 (P - 1) / P x bytes at an ASSUMED bus
+    bandwidth B.
+plus the rank's Gram slab K(all rows, n / P columns) (measured at P = 1..8).
+The rounds are the one-GPU count (the trajectory is bit-identical at any
+rank count: tests/test_ws_gpu.py sharded-vs-replicated tests).
+
+  python bench/project_shard.py [profiles/r3_shard_projection_inputs_1gpu.json]
+"""
+import json
+import sys
+
+PASS1_US = 50.0   # f-update pass 1 at P = 1 (profiles/r2_ws_blocks8_phase_stamps.json: ~50 us)
+
+
+def main() -> int:
+    path = sys.argv[1] if len(sys.argv) > 1 else "profiles/r3_shard_projection_inputs_1gpu.json"
+    m = json.load(open(path))
+    r = m["round_us"]
+    rounds = m["local"]["rounds"]
+    blocks = m["local"]["blocks"][0]
+    q = 192
+    ar_bytes = blocks * (q * q + 192) * 4
+    fixed = r["merge"] + r["gather"] + r["load_subgram"] + r["solve"]
+    rows_part = PASS1_US + r["select_pass2"]
+    gaps = max(0.0, r["period"] - fixed - rows_part)
+    print(f"inputs: {path}")
+    print(f"  measured: rounds {rounds}, round period {r['period']} us = redundant {fixed:.1f} (merge, gather, "
+          f"load, solve) + row passes {rows_part:.1f} + launch gaps {gaps:.1f}; one-rank RCCL launch cost "
+          f"{m['rccl_one_rank']['extra_us_per_round']} us/round")
+    print(f"  measured Gram slab (s): {m['gram_slab_s']};  local solve {m['local']['s']} s")
+    print(f"  sub-Gram all-reduce: {ar_bytes / 1e6:.2f} MB per round")
+    print("PROJECTION (assumed xGMI collective cost: latency L per collective, all-reduce bus bandwidth B)")
+    print(f"{'L us':>6} {'B GB/s':>7} | " + " | ".join(f"P={p:<2d} s" for p in (1, 2, 4, 8)))
+    for L, B in ((5, 100), (10, 64), (20, 40)):
+        row = []
+        for P in (1, 2, 4, 8):
+            gram = m["gram_slab_s"][str(P)]
+            if P == 1:
+                row.append(m["local"]["s"])
+                continue
+            coll = 3 * L + 2 * (P - 1) / P * ar_bytes / (B * 1e3)  # bytes / (GB/s) -> us
+            per_round = fixed + rows_part / P + gaps + coll
+            row.append(gram + rounds * per_round * 1e-6)
+        print(f"{L:>6} {B:>7} | " + " | ".join(f"{v:.4f}  " for v in row))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -126,6 +126,8 @@ struct SolverParams {
                               // 2 second order (WSS2: max (f_lo - b_hi)^2 / eta); the stop test is unchanged;
                               // 0 auto: second order when a row sample's mean off-diagonal K > 0.1
   int ws_block = 32;          // rounds per hipGraph block
+  float ws_t_halve = 0.9f;    // multi-block: a round damped below this line-search factor halves the block count
+  int ws_clip_fallback = 1;   // multi-block, independent clipping: 1 = one block per round after a clip event
   // eta's K(i_hi, i_lo) in the pair-at-a-time dense engines: 0 from the two X
   // rows (explicit difference, the same tree in every engine: bit parity), 1
   // from the resident Gram (persistent dense engine with every column local;

@@ -316,6 +316,8 @@ struct WsArgs {
   int32_t rank;        // this rank (its partials slot)
   int32_t aux_stride;  // aux: [3][blocks][kWsMax] (f of every block first: one sum all-reduce with subg)
   int32_t wss;         // sub-problem pair selection: 1 first order (the reference's), 2 second order (WSS2)
+  float t_halve;       // multi-block: a round damped to t < t_halve halves the block count
+  int32_t clip_fallback;  // multi-block, independent clipping: a clip event drops to one block (1) or not (0)
 };
 // u64 words of the working-set exchange region (both parities)
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {

@@ -57,6 +57,8 @@ void for_each_param(SolverParams& p, F&& f) {
   f("ws_blocks", p.ws_blocks);
   f("ws_inner", p.ws_inner);
   f("ws_wss", p.ws_wss);
+  f("ws_t_halve", p.ws_t_halve);
+  f("ws_clip_fallback", p.ws_clip_fallback);
   f("ws_block", p.ws_block);
   f("eta", p.eta);
 }

@@ -472,7 +472,7 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
           // strongly coupled blocks: fewer from the next round on (the solve's
           // commit may have set p_act = 1 already: an independent-clip event)
           c->n_damped = c->n_damped + 1;
-          const int np = max(1, pr / 2);
+          const int np = t < a.t_halve ? max(1, pr / 2) : pr;
           if (np < c->p_act) c->p_act = np;
           if (c->p_act == 1 && c->p1_round == 0) c->p1_round = c->outer;
           ws_status(a.status, c);  // p1_round visible with the round that set it (gpu_engines.hip)
@@ -1717,7 +1717,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       c->n_apply = tot_a;
       c->iter = it0 + tot_i;
       c->outer = c->outer + 1;
-      if (any_clip && c->p_act > 1) {
+      if (any_clip && a.clip_fallback && c->p_act > 1) {
         c->p_act = 1;
         if (c->p1_round == 0) c->p1_round = c->outer;
       }

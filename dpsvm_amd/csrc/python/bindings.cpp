@@ -193,6 +193,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_blocks", &SolverParams::ws_blocks)
       .def_readwrite("ws_inner", &SolverParams::ws_inner)
       .def_readwrite("ws_wss", &SolverParams::ws_wss)
+      .def_readwrite("ws_t_halve", &SolverParams::ws_t_halve)
+      .def_readwrite("ws_clip_fallback", &SolverParams::ws_clip_fallback)
       .def_readwrite("ws_block", &SolverParams::ws_block)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
       .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });

@@ -611,6 +611,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       w.wss = m.all_agree(k > kWsW2Coupling, m.comm, m.world) ? 2 : 1;
     }
     m.info.ws_wss = w.wss;
+    DPSVM_CHECK(m.p.ws_t_halve >= 0.f && m.p.ws_t_halve <= 1.f, "ws_t_halve must be in [0, 1]");
+    w.t_halve = m.p.ws_t_halve;
+    w.clip_fallback = m.p.ws_clip_fallback ? 1 : 0;
     DPSVM_CHECK(m.p.ws_rel >= 0.f && m.p.ws_rel < 1.f, "ws_rel must be in [0, 1)");
     w.rel_local = m.p.ws_rel;
     // sub-problem tolerance ws_rel * max(eps, gap / 2): floored at ws_rel * eps

@@ -163,6 +163,8 @@ WsSolveProbe ws_solve_probe(const std::vector<float>& K, const std::vector<float
   a.clip = clip;
   a.max_iter = max_iter;
   a.wss = wss;
+  a.clip_fallback = 1;
+  a.t_halve = 0.9f;
   a.world = 1;
   a.ctrl = dc;
   launch::ws_solve(a, st.s);
@@ -250,6 +252,8 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
   a.q_max = q_max;
   a.C = C;
   a.blocks = blocks;
+  a.t_halve = 0.9f;
+  a.clip_fallback = 1;
   launch::ws_select(a, st.s);  // blocks > 1: pass 1 then pass 2
   const WsCtrl o = download(a.ctrl, 1, st.s)[0];
   WsSelectProbe r;

@@ -115,6 +115,8 @@ class SVCConfig:
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
     ws_block: int = 32              # rounds per hipGraph block
+    ws_t_halve: float = 0.9         # multi-block: a round damped below this t halves the block count
+    ws_clip_fallback: bool = True   # multi-block, independent clipping: one block per round after a clip
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
 
     def resolved_gamma(self, d: int) -> float:
@@ -177,6 +179,8 @@ class SVCConfig:
         p.ws_blocks = int(self.ws_blocks)
         p.ws_inner = int(self.ws_inner)
         p.ws_wss = int(self.ws_wss)
+        p.ws_t_halve = float(self.ws_t_halve)
+        p.ws_clip_fallback = int(bool(self.ws_clip_fallback))
         p.ws_block = int(self.ws_block)
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         return p
