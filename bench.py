@@ -101,6 +101,8 @@ def parse(argv=None):
     ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
     ap.add_argument("--ws-block", type=int, default=32)
     ap.add_argument("--ws-t-halve", type=float, default=None, help="multi-block: damped rounds below this t halve P")
+    ap.add_argument("--shrink", action="store_true",
+                    help="one GPU: LIBSVM-style shrinking as problem reduction (phases on the active rows)")
     ap.add_argument("--ws-no-clip-fallback", action="store_true",
                     help="multi-block, independent clipping: keep the blocks after a clip event")
     ap.add_argument("--ws-wss", type=int, default=None, choices=[0, 1, 2],
@@ -184,12 +186,21 @@ def main(argv=None) -> int:
     if a.comm == "rccl" and n_ranks == 1:
         params.force_collectives = True  # one-rank RCCL: exercise the collective + graph path
 
-    if on_gpu:
+    def progress(it, bh, bl, el, hits, misses):
+        print(f"[bench] iter {it} b_hi {bh:.6g} b_lo {bl:.6g} gap {bl - bh:.3g} {el:.1f} s "
+              f"hits {hits} misses {misses}", file=sys.stderr, flush=True)
+
+    if on_gpu and a.shrink:
+        # shrinking phases (one GPU): every phase sets its solver up inside the timed run
+        if n_ranks > 1:
+            raise SystemExit("--shrink runs on one GPU")
+        solver = None
+        info = {"device_name": C.device_name(ctx.local_rank), "x_replicated": True, "iteration": "ws+shrinking"}
+        run = lambda: C.solve_shrinking(X, y, params, ctx.local_rank, None,  # noqa: E731
+                                        progress if a.log_every else None)
+    elif on_gpu:
         solver = C.GpuSolver(params, comm, ctx.local_rank)
         info = solver.setup(X, X.shape[0], y)
-        def progress(it, bh, bl, el, hits, misses):
-            print(f"[bench] iter {it} b_hi {bh:.6g} b_lo {bl:.6g} gap {bl - bh:.3g} {el:.1f} s "
-                  f"hits {hits} misses {misses}", file=sys.stderr, flush=True)
 
         if a.log_every and ctx.rank == 0:
             run = lambda: solver.solve(None, progress)  # noqa: E731
@@ -293,7 +304,7 @@ def main(argv=None) -> int:
     per_run, solve_max, solve_min = t.tolist()
     alpha, res = results[-1]
     acc = None
-    if not a.no_accuracy and on_gpu:
+    if not a.no_accuracy and on_gpu and solver is not None:
         acc = float(solver.train_accuracy(alpha, res["b"]))
     nsv = int((alpha > 0).sum())
     ref_check = None

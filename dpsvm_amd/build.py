@@ -45,6 +45,7 @@ LIB_SOURCES = [
     "solver/gpu_solve.hip",
     "solver/gpu_predict.hip",
     "solver/ws_kernel_entry.hip",
+    "solver/gpu_shrink.cpp",
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/smo_fused.hip",

@@ -154,6 +154,7 @@ struct SolveResult {
   // rounds completed when the count reached 1 (0: never), damped rounds
   int ws_blocks = 1, ws_blocks_end = 1;
   int64_t ws_p1_round = 0, ws_damped = 0;
+  int shrink_phases = 0;       // solve_shrinking: device solves on the (active) rows
   bool converged() const { return status == 1; }
 };
 

@@ -92,12 +92,24 @@ class GpuSolver {
   double train_accuracy(const SolveResult& r);
   // decision values for rows of a host matrix using the trained SVs (any rank)
   std::vector<float> decision(const SolveResult& r, const float* x, int64_t n, int d);
+  // after solve(): this rank's gradient f_j = sum_i alpha_i y_i K(i, j) - y_j
+  // as the solver maintained it (its local rows)
+  std::vector<float> gradient() const;
   const GpuSetupInfo& info() const;
   struct Impl;
 
  private:
   std::unique_ptr<Impl> impl_;
 };
+
+// Shrinking (LIBSVM's heuristic, as problem reduction; one device): phases of
+// the device solver on the active rows only — free alphas and bounded ones that
+// can still violate (f below b_lo on the up side, above b_hi on the low side) —
+// each to its own stop test, then the inactive rows' gradient is brought up to
+// date by one predict GEMM over the phase's alpha changes and the reference's
+// stop test is evaluated on the whole problem.  x, y: host, all n rows.
+SolveResult solve_shrinking(const SolverParams& p, int device, const float* x, int64_t n, int d, const float* y,
+                            const Checkpoint* resume = nullptr, const ProgressFn& progress = {});
 
 // Stand-alone GPU predictor (svmTest GPU path): model SVs resident on device,
 // decision values of a host or device matrix via the MFMA predict kernel.

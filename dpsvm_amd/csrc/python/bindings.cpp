@@ -121,6 +121,7 @@ py::dict result_dict(const SolveResult& r) {
   d["ws_blocks_end"] = r.ws_blocks_end;
   d["ws_p1_round"] = r.ws_p1_round;
   d["ws_damped"] = r.ws_damped;
+  d["shrink_phases"] = r.shrink_phases;
   d["host_cache_lines"] = r.host_cache_lines;
   d["cache_lines"] = r.cache_lines;
   d["world"] = r.world;
@@ -333,6 +334,21 @@ PYBIND11_MODULE(_C, m) {
     }
     return py::make_tuple(to_np(r.alpha), result_dict(r));
   }, py::arg("x"), py::arg("y"), py::arg("params"), py::arg("comm") = nullptr, py::arg("resume") = nullptr,
+     py::arg("progress") = py::none());
+
+  m.def("solve_shrinking", [](F32 x, F32 y, const SolverParams& p, int device, const Checkpoint* resume,
+                              py::object progress) {
+    int64_t n = 0;
+    int d = 0;
+    check_xy(x, y, n, d);
+    auto prog = wrap_progress(progress);
+    SolveResult r;
+    {
+      py::gil_scoped_release rel;
+      r = solve_shrinking(p, device, x.data(), n, d, y.data(), resume, prog);
+    }
+    return py::make_tuple(to_np(r.alpha), result_dict(r));
+  }, py::arg("x"), py::arg("y"), py::arg("params"), py::arg("device") = 0, py::arg("resume") = nullptr,
      py::arg("progress") = py::none());
 
   py::class_<GpuSolver, std::shared_ptr<GpuSolver>>(m, "GpuSolver")

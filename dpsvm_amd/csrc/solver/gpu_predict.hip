@@ -165,6 +165,14 @@ double GpuSolver::train_accuracy(const SolveResult& r) {
   return tot / (double)m.n;
 }
 
+std::vector<float> GpuSolver::gradient() const {
+  const auto& m = *impl_;
+  HIP_CHECK(hipSetDevice(m.device));
+  std::vector<float> f((size_t)m.nl);
+  if (m.nl > 0) HIP_CHECK(hipMemcpy(f.data(), m.f, (size_t)m.nl * 4, hipMemcpyDeviceToHost));
+  return f;
+}
+
 std::vector<float> GpuSolver::decision(const SolveResult& r, const float* xh, int64_t nt, int d) {
   auto& m = *impl_;
   DPSVM_CHECK(d == m.d, "feature count mismatch");

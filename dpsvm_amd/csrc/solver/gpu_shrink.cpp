@@ -1,0 +1,240 @@
+// Shrinking for the device solver (one GPU), as problem reduction.
+//
+// LIBSVM's shrinking heuristic in the reference's f-notation (f_j = sum_i
+// alpha_i y_i K(i, j) - y_j, b_hi = min f over I_up, b_lo = max f over I_low;
+// svmTrain.cu:41-95): a row whose alpha sits on a bound can only take part in
+// a violating pair from one side — an up-only row (alpha = 0, y = +1 or
+// alpha = C, y = -1) when f_j < b_lo, a low-only row (alpha = 0, y = -1 or
+// alpha = C, y = +1) when f_j > b_hi.  Rows failing that test are shrunk: the
+// reduced problem keeps the free rows and the rows that can still violate,
+// with the shrunk alphas fixed (their contribution is already in every f).
+//
+// On the device the win is a smaller problem, not a masked one: every round of
+// the working-set engines streams its changed rows' kernel lines over all rows
+// (the f update), and the reduced problem's lines are |A| long (often short
+// enough to make its Gram resident: ws-dense instead of ws-cache).  So a phase
+// is a fresh GpuSolver on the active rows, resumed from the current alphas and
+// gradient; afterwards the inactive rows' gradient is brought up to date by
+// one predict GEMM over the phase's alpha changes
+//     f_j += sum_{i changed} (alpha'_i - alpha_i) y_i K(i, j)     (j inactive)
+// — the same incremental form the solver maintains, so no from-scratch
+// recomputation (whose fp32 cancellation error with C = 2048 would exceed eps)
+// — and the reference's stop test !(b_lo > b_hi + 2 eps) (svmTrainMain.cpp:310)
+// is evaluated on the whole problem.  Phase 0 solves the whole problem to a
+// loose tolerance; the last phase, if the shrunk ones keep failing the global
+// test, solves the whole problem to eps.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+
+#include "dpsvm/device_state.hpp"
+#include "dpsvm/solver.hpp"
+
+namespace dpsvm {
+
+namespace {
+
+struct Extremes {
+  float b_hi = 0.f, b_lo = 0.f;
+  bool ok = false;
+};
+
+Extremes extremes(const std::vector<float>& f, const std::vector<float>& a, const float* y, float C) {
+  Extremes e;
+  float hi = INFINITY, lo = -INFINITY;
+  for (size_t j = 0; j < f.size(); ++j) {
+    if (in_up(a[j], y[j], C) && f[j] < hi) hi = f[j];
+    if (in_low(a[j], y[j], C) && f[j] > lo) lo = f[j];
+  }
+  e.b_hi = hi;
+  e.b_lo = lo;
+  e.ok = std::isfinite(hi) && std::isfinite(lo);
+  return e;
+}
+
+// rows that can still take part in a violating pair (LIBSVM's shrinking test)
+std::vector<int64_t> active_rows(const std::vector<float>& f, const std::vector<float>& a, const float* y, float C,
+                                 const Extremes& e) {
+  std::vector<int64_t> act;
+  for (int64_t j = 0; j < (int64_t)f.size(); ++j) {
+    const bool up = in_up(a[j], y[j], C), low = in_low(a[j], y[j], C);
+    const bool keep = (up && low) || (up && f[j] < e.b_lo) || (low && f[j] > e.b_hi);
+    if (keep) act.push_back(j);
+  }
+  return act;
+}
+
+std::vector<float> gather_rows(const float* x, int d, const std::vector<int64_t>& rows) {
+  std::vector<float> out(rows.size() * (size_t)d);
+  for (size_t k = 0; k < rows.size(); ++k) std::copy(x + rows[k] * d, x + rows[k] * d + d, out.begin() + k * d);
+  return out;
+}
+
+double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+constexpr float kPhase0EpsScale = 50.f;   // phase 0: the whole problem to 50 eps
+constexpr double kShrinkMaxFrac = 0.6;    // shrink only if the active set is at most 60% of the rows
+constexpr int kMaxPhases = 8;             // then the whole problem to eps
+
+}  // namespace
+
+SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, int64_t n, int d, const float* y_in,
+                            const Checkpoint* resume, const ProgressFn& progress) {
+  DPSVM_CHECK(n >= 2 && d >= 1, "solve_shrinking: need at least 2 samples and 1 feature");
+  const double t_start = now();
+  SolverParams p = p0;
+  p.checkpoint_every = 0;  // phases are not checkpointed (the final state is)
+  if (p.solver == 0) p.solver = 2;  // the phases are parts of a large problem: working-set rounds at any size
+  const float gamma = resolve_gamma(p.gamma, d);
+  p.gamma = gamma;
+  const float C = p.C;
+  std::vector<float> y((size_t)n);
+  for (int64_t j = 0; j < n; ++j) y[j] = y_in[j] > 0 ? 1.f : -1.f;
+  std::vector<float> alpha((size_t)n, 0.f), f((size_t)n);
+  int64_t iters = 0;
+  bool have_f = false;
+  if (resume) {
+    check_resume(*resume, n, d, p, gamma);
+    alpha = resume->alpha;
+    iters = resume->iter;
+    if ((int64_t)resume->f.size() == n) {
+      f = resume->f;
+      have_f = true;
+    }
+  }
+  if (!have_f && !resume)
+    for (int64_t j = 0; j < n; ++j) f[j] = -y[j];
+
+  SolveResult res;
+  res.world = 1;
+  int phases = 0;
+  int64_t rounds = 0, rows_computed = 0;
+  double t_gram = 0.0;
+  std::vector<int64_t> act;  // empty: every row
+  bool full_to_eps = false;
+  while (true) {
+    const bool all = act.empty() || (int64_t)act.size() == n;
+    const int64_t na = all ? n : (int64_t)act.size();
+    SolverParams sp = p;
+    // phase 0 (every row, the first time): a loose tolerance; later phases to eps
+    if (phases == 0 && !full_to_eps && (have_f || !resume)) sp.eps = p.eps * kPhase0EpsScale;
+    std::vector<float> xa, ya, aa, fa;
+    const float* xp = x;
+    if (!all) {
+      xa = gather_rows(x, d, act);
+      ya.resize((size_t)na);
+      aa.resize((size_t)na);
+      fa.resize((size_t)na);
+      for (int64_t k = 0; k < na; ++k) {
+        ya[k] = y[act[k]];
+        aa[k] = alpha[act[k]];
+        fa[k] = f[act[k]];
+      }
+      xp = xa.data();
+    }
+    const Extremes e0 = extremes(all ? f : fa, all ? alpha : aa, all ? y.data() : ya.data(), C);
+    Checkpoint ck;
+    ck.n = na;
+    ck.d = d;
+    ck.C = p.C;
+    ck.gamma = gamma;
+    ck.eps = sp.eps;
+    ck.clip = (int)p.clip;
+    ck.iter = iters;
+    ck.b_hi = e0.b_hi;
+    ck.b_lo = e0.b_lo;
+    ck.alpha = all ? alpha : aa;
+    if (have_f || phases > 0) ck.f = all ? f : fa;  // else recomputed from alpha by the solver
+    std::vector<float> a_new, f_new;
+    SolveResult r;
+    {
+      GpuSolver s(sp, nullptr, device);
+      s.setup(xp, na, na, d, all ? y.data() : ya.data());
+      r = s.solve((phases == 0 && !resume) ? nullptr : &ck, progress);
+      f_new = s.gradient();
+    }  // the phase's device memory is released before the next phase
+    ++phases;
+    iters = r.iters;
+    rounds += r.outer;
+    rows_computed += r.rows_computed;
+    t_gram += r.t_gram;
+    if (all) {
+      alpha = r.alpha;
+      f = f_new;
+    } else {
+      // the inactive rows' gradient: one predict GEMM over the phase's changes
+      Model dm;
+      dm.gamma = gamma;
+      dm.b = 0.f;
+      dm.d = d;
+      std::vector<int64_t> changed;
+      for (int64_t k = 0; k < na; ++k)
+        if (r.alpha[k] != aa[k]) {
+          dm.alpha.push_back(r.alpha[k] - aa[k]);
+          dm.y.push_back(ya[k]);
+          changed.push_back(act[k]);
+        }
+      std::vector<char> is_act((size_t)n, 0);
+      for (int64_t j : act) is_act[j] = 1;
+      std::vector<int64_t> inact;
+      inact.reserve((size_t)(n - na));
+      for (int64_t j = 0; j < n; ++j)
+        if (!is_act[j]) inact.push_back(j);
+      if (!changed.empty() && !inact.empty()) {
+        dm.x = gather_rows(x, d, changed);
+        const std::vector<float> xi = gather_rows(x, d, inact);
+        GpuPredictor pr(dm, device);
+        const std::vector<float> df = pr.decision(xi.data(), (int64_t)inact.size(), d);
+        for (size_t k = 0; k < inact.size(); ++k) f[inact[k]] += df[k];
+      }
+      for (int64_t k = 0; k < na; ++k) {
+        alpha[act[k]] = r.alpha[k];
+        f[act[k]] = f_new[k];
+      }
+    }
+    const Extremes e = extremes(f, alpha, y.data(), C);
+    res.b_hi = e.b_hi;
+    res.b_lo = e.b_lo;
+    const bool open = e.ok && gap_open(e.b_hi, e.b_lo, p.eps);
+    if (p.verbose)
+      fprintf(stderr, "[dpsvm] shrink phase %d: %lld active rows, %lld pair steps, global gap %g (status %d)\n",
+              phases, (long long)na, (long long)iters, (double)(e.b_lo - e.b_hi), r.status);
+    if (!e.ok) {
+      res.status = kNoPair;
+      break;
+    }
+    if (!open) {
+      res.status = kConverged;
+      break;
+    }
+    if (r.status == kMaxIter || iters >= p.max_iter) {
+      res.status = kMaxIter;
+      break;
+    }
+    if (r.status == kNonFinite || r.status == kCommFail) {
+      res.status = r.status;
+      break;
+    }
+    if (full_to_eps && all) {  // the whole problem solved to eps and still open: fp32 limit
+      res.status = r.status;
+      break;
+    }
+    act = active_rows(f, alpha, y.data(), C, e);
+    if (phases >= kMaxPhases || (double)act.size() > kShrinkMaxFrac * (double)n) {
+      act.clear();  // the whole problem to eps
+      full_to_eps = true;
+    }
+  }
+  res.alpha = alpha;
+  res.iters = iters;
+  res.outer = rounds;
+  res.rows_computed = rows_computed;
+  res.t_gram = t_gram;
+  res.b = (res.b_hi + res.b_lo) / 2.f;
+  res.t_solve = now() - t_start;
+  res.shrink_phases = phases;
+  return res;
+}
+
+}  // namespace dpsvm

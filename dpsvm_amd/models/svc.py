@@ -115,6 +115,9 @@ class SVCConfig:
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
     ws_block: int = 32              # rounds per hipGraph block
+    # one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking: phases on the rows that can
+    # still violate, the rest of the gradient updated by one predict GEMM per phase)
+    shrink: bool = False
     ws_t_halve: float = 0.9         # multi-block: a round damped below this t halves the block count
     ws_clip_fallback: bool = True   # multi-block, independent clipping: one block per round after a clip
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
@@ -257,7 +260,12 @@ class SVC:
         kind, dev = cfg.device_kind()
         self.device_ = f"{kind}:{dev}" if kind == "cuda" else "cpu"
         t0 = time.perf_counter()
-        if kind == "cuda":
+        if kind == "cuda" and cfg.shrink and comm is None and rank_rows is None:
+            alpha, info = C.solve_shrinking(X, ys, p, dev, ck, progress)
+            self.setup_info_ = {"iteration": "ws+shrinking", "device_name": C.device_name(dev), "n_local": n,
+                                "x_replicated": True, "engine_note": f"{info['shrink_phases']} shrinking phases"}
+            self._solver = None
+        elif kind == "cuda":
             solver = C.GpuSolver(p, comm, dev)
             self.setup_info_ = solver.setup(X, ys.shape[0], ys)
             alpha, info = solver.solve(ck, progress)

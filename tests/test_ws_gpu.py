@@ -509,3 +509,27 @@ def test_ws_cache_multi_block_bit_identical_to_resident_gram(clip):
     assert np.array_equal(cache.alpha_, dense.alpha_) and cache.b_ == dense.b_
     assert cache.stats_["ws_blocks_end"] == dense.stats_["ws_blocks_end"]
     assert cache.stats_["rows_computed"] > 4700  # more rows than lines: evictions happened
+
+
+@pytest.mark.parametrize("clip", ["box", "independent"])
+def test_shrinking_reaches_the_stop_test_on_the_whole_problem(clip):
+    """solve_shrinking: phases on the active rows (free alphas and bounded ones
+    that can still violate), the inactive rows' gradient updated by a predict
+    GEMM over each phase's changes; the result satisfies the reference's stop
+    test on the exact float64 gradient of the WHOLE problem, and (box clipping:
+    unique optimum) matches the unshrunk solve."""
+    X, y = synthetic("covtype", n=30000, seed=8)
+    C_, g = 64.0, 0.25
+    kw = dict(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", solver="ws")
+    full = SVC(**kw).fit(X, y)
+    shr = SVC(shrink=True, **kw).fit(X, y)
+    assert shr.setup_info_["iteration"] == "ws+shrinking" and shr.stats_["shrink_phases"] >= 2
+    assert shr.converged_ and full.converged_
+    gap = _kkt_gap(X, y, shr.alpha_, C_, g)
+    print(f"{clip}: phases {shr.stats_['shrink_phases']} gap {gap:.2e} b {shr.b_:.5f} vs {full.b_:.5f} "
+          f"nsv {shr.n_support_} vs {full.n_support_} steps {shr.n_iter_} vs {full.n_iter_}")
+    assert gap < 2e-3 + 5e-4
+    assert np.all((shr.alpha_ >= 0) & (shr.alpha_ <= C_))
+    if clip == "box":
+        assert abs(shr.b_ - full.b_) < 2e-2
+        assert abs(shr.n_support_ - full.n_support_) <= max(5, full.n_support_ // 50)
