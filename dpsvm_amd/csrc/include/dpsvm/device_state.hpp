@@ -60,6 +60,46 @@ inline const char* engine_name(EngineKind k) {
   }
 }
 
+// What gpu_setup established before choosing an engine (every flag already
+// agreed across ranks).
+struct EngineFacts {
+  bool ws_dense = false;          // working-set rounds wanted and supported, Gram resident
+  bool ws_cache = false;          // ... Gram not resident, cache holds >= 2 q + 512 lines, no host tier
+  bool dense = false;             // Gram resident
+  bool cache_replicated = false;  // Gram not resident, X replicated (the pair cache engines' X pass)
+  bool persistent = false;        // in-kernel exchange set up and its candidate's geometry fits
+};
+
+// The engine choice: first matching row wins.  `use` is the path that reaches
+// the row (docs/DESIGN.md §2 lists the same table).  A persistent row whose
+// grid then fails the co-residency census drops to the fused row below it.
+struct EngineRule {
+  EngineKind kind;
+  bool (*when)(const EngineFacts&);
+  const char* use;
+};
+inline constexpr EngineRule kEngineTable[] = {
+    {EngineKind::WsDense, [](const EngineFacts& f) { return f.ws_dense; },
+     "default from 50k rows (solver auto) or solver=ws, Gram resident"},
+    {EngineKind::WsCache, [](const EngineFacts& f) { return f.ws_cache; },
+     "default from 50k rows (solver auto) or solver=ws, Gram not resident"},
+    {EngineKind::PersistDense, [](const EngineFacts& f) { return f.dense && f.persistent; },
+     "default below 50k rows (solver auto) or solver=smo: the reference's trajectory"},
+    {EngineKind::FusedDense, [](const EngineFacts& f) { return f.dense; },
+     "fallback of persistent-dense (census or exchange self-test failed, persist=off, forced collectives)"},
+    {EngineKind::PersistCache, [](const EngineFacts& f) { return f.cache_replicated && f.persistent; },
+     "pair-at-a-time in cache mode: solver=smo, or a cache too small for ws-cache"},
+    {EngineKind::FusedCache, [](const EngineFacts& f) { return f.cache_replicated; },
+     "fallback of persistent-cache; host spill tier (host_cache_lines); persist=off"},
+    {EngineKind::Chain, [](const EngineFacts&) { return true; },
+     "pair-at-a-time with X partitioned (x_mode=partitioned, solver=smo or below 50k rows); cache_engine=chain"},
+};
+inline EngineKind choose_engine(const EngineFacts& f) {
+  for (const EngineRule& r : kEngineTable)
+    if (r.when(f)) return r.kind;
+  return EngineKind::Chain;
+}
+
 // Written by smo_finalize, read by the next iteration's kernels.
 struct alignas(16) SmoCtrl {
   int32_t iter;        // SMO updates applied so far

@@ -11,6 +11,7 @@
 
 #include "dpsvm/comm.hpp"
 #include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
 #include "dpsvm/io.hpp"
 #include "dpsvm/solver.hpp"
 #include "dpsvm/params_io.hpp"
@@ -215,6 +216,22 @@ PYBIND11_MODULE(_C, m) {
                     [](Checkpoint& c, F32 a) { c.alpha = from_np(a); })
       .def_property("f", [](const Checkpoint& c) { return to_np(c.f); },
                     [](Checkpoint& c, F32 a) { c.f = from_np(a); });
+  // the device solver's engine choice (device_state.hpp kEngineTable), for docs and tests
+  m.def("engine_table", []() {
+    std::vector<std::pair<std::string, std::string>> out;
+    for (const EngineRule& r : kEngineTable) out.emplace_back(engine_name(r.kind), r.use);
+    return out;
+  });
+  m.def("choose_engine", [](bool ws_dense, bool ws_cache, bool dense, bool cache_replicated, bool persistent) {
+    EngineFacts f;
+    f.ws_dense = ws_dense;
+    f.ws_cache = ws_cache;
+    f.dense = dense;
+    f.cache_replicated = cache_replicated;
+    f.persistent = persistent;
+    return std::string(engine_name(choose_engine(f)));
+  }, py::arg("ws_dense") = false, py::arg("ws_cache") = false, py::arg("dense") = false,
+        py::arg("cache_replicated") = false, py::arg("persistent") = false);
   m.def("write_checkpoint", &write_checkpoint, py::arg("path"), py::arg("ck"));
   m.def("read_checkpoint", &read_checkpoint, py::arg("path"));
 

@@ -547,11 +547,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool wsc_fits = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
   if (wsc_cand && !wsc_fits)
     m.info.engine_note = "ws-cache needs >= " + std::to_string(2 * ws_q + 512) + " lines: SMO cache engine used";
-  if (ws_cand) m.kind = EngineKind::WsDense;
-  else if (wsc_fits) m.kind = EngineKind::WsCache;
-  else if (m.dense) m.kind = pdense_cand && m.xch ? EngineKind::PersistDense : EngineKind::FusedDense;
-  else if (fused_lru_ok) m.kind = plru_cand && m.xch ? EngineKind::PersistCache : EngineKind::FusedCache;
-  else m.kind = EngineKind::Chain;
+  EngineFacts facts;
+  facts.ws_dense = ws_cand;
+  facts.ws_cache = wsc_fits;
+  facts.dense = m.dense;
+  facts.cache_replicated = fused_lru_ok;
+  facts.persistent = (m.dense ? pdense_cand : plru_cand) && m.xch;
+  m.kind = choose_engine(facts);
   if (m.persistent() && !m.census(m.kind)) {
     DPSVM_CHECK(m.p.persist != 2, "persistent engine requested (persist=on) but its grid is not co-resident (" +
                                       m.info.engine_note + ")");
