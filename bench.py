@@ -114,6 +114,9 @@ def parse(argv=None):
                          "round)")
     ap.add_argument("--eta", default="x", choices=["x", "gram"],
                     help="pair-at-a-time engines: K(hi, lo) of eta from the two X rows (default) or the resident Gram")
+    ap.add_argument("--gram", default="auto", choices=["auto", "f32", "split"],
+                    help="Gram / kernel-row GEMMs: f32-input MFMA or fp16 MFMA over hi/lo split operands (fp32 "
+                         "accuracy); auto = split for the working-set engines")
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
     ap.add_argument("--cache-groups", type=int, default=256)
     ap.add_argument("--force-cache", action="store_true")
@@ -172,6 +175,7 @@ def main(argv=None) -> int:
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
                     xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
                     ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, ws_blocks=a.ws_blocks, ws_inner=a.ws_inner, eta=a.eta,
+                    gram=a.gram,
                     **({} if a.ws_wss is None else {"ws_wss": a.ws_wss}),
                     **({} if a.ws_t_halve is None else {"ws_t_halve": a.ws_t_halve}),
                     **({"ws_clip_fallback": False} if a.ws_no_clip_fallback else {}),
@@ -380,6 +384,7 @@ def main(argv=None) -> int:
             "device": info.get("device_name", ""),
             "x_replicated": bool(info.get("x_replicated", True)),
             "iteration": info.get("iteration", "cpu"),
+            "gram": info.get("gram", "f32"),
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
             "exchange": info.get("exchange", "none"),

@@ -48,6 +48,7 @@ LIB_SOURCES = [
     "solver/gpu_shrink.cpp",
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
+    "kernels/rbf_gemm_split.hip",
     "kernels/smo_fused.hip",
     "kernels/microbench.hip",
     "kernels/compact.hip",

@@ -88,6 +88,8 @@ inline void usage_train(const char* prog, bool seq) {
                "   --ws-blocks P       :  ws-dense: up to P sub-problems per round on P workgroups (1..8; default 0 = auto:\n"
                "                          8 from 50k rows, halved after every damped round)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
+               "   --gram auto|f32|split :  Gram / kernel-row GEMMs: f32-input MFMA, or fp16 MFMA over hi/lo split\n"
+               "                          operands (fp32 accuracy); auto = split for the ws engines\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
@@ -106,7 +108,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
     OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL, OPT_WSBLOCKS,
-    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS
+    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -139,7 +141,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"ws-new", required_argument, 0, OPT_WSNEW}, {"eta", required_argument, 0, OPT_ETA}, {"ws-rel", required_argument, 0, OPT_WSREL},
       {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
-      {"ws-wss", required_argument, 0, OPT_WSWSS},
+      {"ws-wss", required_argument, 0, OPT_WSWSS}, {"gram", required_argument, 0, OPT_GRAM},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -247,6 +249,12 @@ inline Options parse_train(int argc, char** argv, bool seq) {
         o.p.eta = v == "gram" ? 1 : 0;
         break;
       }
+      case OPT_GRAM: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "f32" && v != "split") usage_train(argv[0], seq);
+        o.p.gram_precision = v == "split" ? 2 : v == "f32" ? 1 : 0;
+        break;
+      }
       case OPT_PJSON: {
         FILE* fp = fopen(optarg, "r");
         if (!fp) {
@@ -326,7 +334,7 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           "\"exchange_mem\": \"%s\", \"dp_policy\": \"%s\", \"rows_per_group\": %lld, \"groups\": %lld, "
           "\"poll_batch\": %d, \"cus\": %d, \"blocks_per_cu\": %d, \"census\": \"%s\", \"engine_note\": \"%s\", "
           "\"rounds\": %lld, \"ws_blocks\": %d, \"ws_blocks_end\": %d, \"ws_one_block_from_round\": %lld, "
-          "\"ws_damped_rounds\": %lld, \"params\": %s}\n",
+          "\"ws_damped_rounds\": %lld, \"gram\": \"%s\", \"params\": %s}\n",
           backend.c_str(), json_escape(device).c_str(), r.world, (long long)n, d, o.p.C, o.p.gamma, o.p.eps,
           o.p.clip == ClipMode::Box ? "box" : "independent", (long long)r.iters, r.status,
           r.converged() ? "true" : "false", r.b, r.b_hi, r.b_lo, (long long)nsv, acc, x.t_load, r.t_setup,
@@ -338,7 +346,8 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           x.setup.exchange_mem.c_str(), x.setup.dp_policy.c_str(), (long long)x.setup.rows_per_group,
           (long long)x.setup.groups, x.setup.poll_batch, x.setup.cus, x.setup.blocks_per_cu,
           x.setup.census.c_str(), json_escape(x.setup.engine_note).c_str(), (long long)r.outer, r.ws_blocks,
-          r.ws_blocks_end, (long long)r.ws_p1_round, (long long)r.ws_damped, params_json(o.p).c_str());
+          r.ws_blocks_end, (long long)r.ws_p1_round, (long long)r.ws_damped, x.setup.gram.c_str(),
+          params_json(o.p).c_str());
   fclose(fp);
 }
 

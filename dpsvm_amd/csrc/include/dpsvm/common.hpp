@@ -133,6 +133,11 @@ struct SolverParams {
   // from the resident Gram (persistent dense engine with every column local;
   // one load in the Gram-row round trip instead of the X-row reads and a barrier)
   int eta = 0;
+  // Gram / kernel-row GEMM arithmetic: 1 f32-input MFMA (rbf_gemm.hip), 2 fp16
+  // MFMA over hi / lo split operands (rbf_gemm_split.hip: fp32 accuracy, 3/16 of
+  // the MFMA time), 0 auto = split for the working-set engines, f32 for the
+  // pair-at-a-time engines (the reference's trajectory)
+  int gram_precision = 0;
 };
 
 

@@ -75,6 +75,7 @@ struct GpuSetupInfo {
   std::string census = "n/a";         // residency census of the persistent grid: "ok" | "failed" | "n/a"
   std::string engine_note;            // why the engine was chosen / refused (fallbacks)
   int ws_wss = 0;                     // working-set engines: sub-problem pair choice (1 first, 2 second order)
+  std::string gram = "f32";           // Gram / kernel-row GEMM arithmetic: "f32" or "split-f16" (rbf_gemm_split.hip)
 };
 
 class GpuSolver {
@@ -146,7 +147,10 @@ void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const
 // (x: [rows >= G*rows_per_group][ld], xsq likewise; out rows >= G*rows_per_group)
 // the working-set cache engine's row GEMM: out[out_rows[i]][j] = K(x[rows[i]], x_j), i < m, j < n
 void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const int* rows, int m, float gamma,
-                      float* out, int64_t out_ld, const int* out_rows, void* stream);
+                      float* out, int64_t out_ld, const int* out_rows, void* stream, bool split = false);
+// the same two GEMMs on fp16 MFMA over split operands (rbf_gemm_split.hip)
+void rbf_gram_split(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
+                    float gamma, float* out, int64_t out_ld, bool symmetric, void* stream);
 void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* keys, int nq, float gamma,
                 float* out, int64_t out_ld, int rows_per_group, void* stream);
 // the fused / persistent engines' selection: per workgroup of rows_per_group rows

@@ -105,6 +105,20 @@ void rbf_gemm_store(const float* A, const float* Asq, int64_t M, int lda, const 
 void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, const int32_t* m_dev, int64_t M_max,
                       const float* B, const float* Bsq, int64_t N, int dp, float gamma, float* lines,
                       const int32_t* out_rows, int64_t ldl, hipStream_t s);
+// The same two GEMMs on fp16 MFMA over split operands (rbf_gemm_split.hip):
+// every X row scaled by 2^shift and stored as fp16 hi / lo planes ("split
+// rows", split_row_u4(dp) 16-B units per row; buffers hold split_pad_rows(rows)
+// rows, pad zeroed); fp32 accuracy, bit-identical under operand swap
+int64_t split_row_u4(int dp);
+int64_t split_pad_rows(int64_t rows);
+void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, int32_t* shift, hipStream_t s);
+void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
+                          const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
+                          int64_t ldo, hipStream_t s, bool symmetric = false);
+void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq, const int32_t* a_rows,
+                            const int32_t* m_dev, int64_t M_max, const void* B, const int32_t* Bsh, const float* Bsq,
+                            int64_t N, int dp, float gamma, float* lines, const int32_t* out_rows, int64_t ldl,
+                            hipStream_t s);
 // Decision values: dec[i] = sum_j coef[j] K(A_i, B_j) - b   (B = SVs, coef = alpha*y)
 //   partial: scratch [splits][M_pad] (returned by predict_scratch_floats)
 int64_t predict_scratch_floats(int64_t M, int64_t N);

@@ -1,0 +1,309 @@
+// RBF GEMM on fp16 MFMA with split operands (v_mfma_f32_32x32x16_f16): the
+// fp32 dot products of the Gram at fp32 accuracy for 3/16 of the f32-MFMA time.
+//
+// Why: the f32-input MFMA (rbf_gemm.hip) runs at 1/16 of the f16 rate, and the
+// Gram GEMM is half of the headline solve.  Every X row is scaled by a power of
+// two (its largest |x| to [2^14, 2^15)) and split into two fp16 planes,
+//     x * 2^s = h + l,   h = fp16(x 2^s),  l = fp16(x 2^s - h)      (22 bits)
+// and a . b = 2^-(s_a + s_b) (h_a.h_b + (h_a.l_b + l_a.h_b)), the l_a.l_b term
+// (2^-22 relative) dropped.  Each fp16 product is exact in fp32 and the MFMA
+// accumulates in fp32, so the error vs fp64 is that of an f32 GEMM
+// (tests/test_split_gemm_gpu.py and profiles/r3_split_gemm_*: max relative
+// error per sum |a_k b_k| within 1.5x of the f32 MFMA kernel's on MNIST-shape,
+// Gaussian and covtype-shape data).
+//
+// Symmetry: the three products go to three accumulators H = sum h_a h_b,
+// P = sum h_a l_b, Q = sum l_a h_b and the result is H + (P + Q).  Swapping the
+// operands swaps P and Q bit for bit (the same products in the same k order)
+// and leaves H unchanged, so K(i, j) computed with i as the A row equals K(j, i)
+// computed with j as the A row, bit for bit.  The symmetric Gram (upper tiles
+// mirrored), the sharded Gram (every rank's columns, A = all rows) and the
+// working-set cache's indexed rows therefore hold identical values, as the
+// f32 kernels do.
+//
+// Operand layout ("split rows", split_rows_f16 below): row i is dp32/32 blocks
+// of 128 B, each 32 h values then the 32 l values of k = 32 b .. 32 b + 31, so
+// one 128-B line per row per k-stage (a whole line per load group of 8 lanes).
+//
+// Tiling: 8 waves, each 32 rows x 64 columns (2 MFMA 32x32 tiles, three
+// accumulators each: 96 accumulator registers).  STORE: waves 4 x 2 = 128 x 128
+// block tiles; ROWS (a working set's cache misses): 2 x 4 = 64 x 256 (short row
+// sets).  BK = 32 per stage (two k16 MFMA steps), LDS double buffered through
+// registers; LDS rows are the 128-B row blocks with the 16-B chunk index XORed
+// by (row >> 1) & 7, which makes every ds_read_b128 lane group of the operand
+// reads (16 rows, one chunk) hit 16 distinct bank quads.
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+constexpr int kSplitThreads = 512;
+constexpr int kSplitShiftTarget = 15;  // largest |x| scaled into [2^14, 2^15)
+
+__device__ __forceinline__ f16v mfma32_f16(h8 a, h8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// One wave per row: shift[r] and the h / l planes of row r (columns past dp
+// are zero).
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ x, int64_t rows, int dp, int ldx,
+                                                         u4* __restrict__ out, int32_t* __restrict__ shift,
+                                                         int nkb) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * (int64_t)ldx;
+  // largest |x| of the row (the wave's max; order-free, exact)
+  float m = 0.f;
+  for (int k = lane; k < dp; k += 64) m = fmaxf(m, fabsf(xr[k]));
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  int e = 0;
+  if (m > 0.f && isfinite(m)) (void)frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
+  const int s = m > 0.f && isfinite(m) ? kSplitShiftTarget - e : 0;
+  if (lane == 0) shift[r] = s;
+  // chunk c of block b: lanes write 8 fp16 (16 B); chunks 0-3 h, 4-7 l
+  u4* orow = out + r * (int64_t)nkb * 8;
+  for (int q = lane; q < nkb * 4; q += 64) {
+    const int b = q >> 2, c = q & 3, k0 = 32 * b + 8 * c;
+    h8 hv, lv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      const float v = k < dp ? ldexpf(xr[k], s) : 0.f;
+      const _Float16 h = (_Float16)v;
+      hv[j] = h;
+      lv[j] = (_Float16)(v - (float)h);
+    }
+    orow[8 * b + c] = __builtin_bit_cast(u4, hv);
+    orow[8 * b + 4 + c] = __builtin_bit_cast(u4, lv);
+  }
+}
+
+// XCD-aware tile order (as rbf_gemm.hip): linear workgroup id L runs on XCD
+// L % 8; chunks of 64 tiles (8 x 8 tile blocks) are dealt so that an XCD's
+// consecutive tiles share panels in its L2.  A bijection on the grid.
+__device__ __forceinline__ void xcd_tile(int64_t& tx, int64_t& ty) {
+  const int64_t tm = gridDim.x, tn = gridDim.y, total = tm * tn;
+  const int64_t L = blockIdx.x + (int64_t)blockIdx.y * tm;
+  constexpr int64_t CH = 64, GM = 8;
+  const int64_t full = total / (8 * CH) * (8 * CH);
+  int64_t T = L;
+  if (L < full) {
+    const int64_t xcd = L % 8, local = L / 8;
+    T = ((local / CH) * 8 + xcd) * CH + local % CH;
+  }
+  const int64_t first_m = (T / (GM * tn)) * GM;
+  const int64_t gm = min(GM, tm - first_m);
+  const int64_t in = T - first_m * tn;
+  tx = first_m + in % gm;
+  ty = in / gm;
+}
+
+enum SplitEpi { SPLIT_STORE = 0, SPLIT_ROWS = 1 };
+
+template <int EPI, int WM>
+__global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
+    float gamma, float* __restrict__ out, int64_t ldo, int sym, const int32_t* __restrict__ a_rows,
+    const int32_t* __restrict__ out_rows, const int32_t* __restrict__ m_dev) {
+  constexpr int WN = 8 / WM, TM = 32 * WM, TN = 64 * WN, ROWS = TM + TN;
+  constexpr int CH = ROWS * 8;                   // 16-B chunks per stage
+  constexpr int NL = CH / kSplitThreads;         // chunks per thread
+  static_assert(CH % kSplitThreads == 0, "whole chunks per thread");
+  int64_t tx, ty;
+  xcd_tile(tx, ty);
+  if (EPI == SPLIT_ROWS) M = *m_dev;
+  if (EPI == SPLIT_STORE && sym && ty < tx) return;
+  if (EPI == SPLIT_ROWS && tx * TM >= M) return;  // uniform: no barrier reached
+  __shared__ u4 lds[2][CH];
+  __shared__ float s_asq[TM];
+  __shared__ int32_t s_ash[TM], s_orow[TM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t m0 = tx * TM, n0 = ty * TN;
+  const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
+
+  if (tid < TM) {
+    const int64_t row = m0 + tid;
+    const int64_t ar = EPI == SPLIT_ROWS ? (int64_t)a_rows[min(row, M - 1)] : min(row, M - 1);
+    s_asq[tid] = Asq[ar];
+    s_ash[tid] = Ash[ar];
+    s_orow[tid] = EPI == SPLIT_ROWS ? (row < M ? out_rows[row] : -1) : 0;
+  }
+
+  // staging: chunk id = tid + 512 i -> stage row id >> 3 (A rows, then B rows), chunk id & 7
+  const u4* src[NL];
+  int dst[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int id = tid + kSplitThreads * i, r = id >> 3, c = id & 7;
+    int64_t grow;
+    const u4* base;
+    if (r < TM) {
+      const int64_t row = m0 + r;  // rows past M: read a valid row (never stored)
+      grow = EPI == SPLIT_ROWS ? (int64_t)a_rows[min(row, M - 1)] : row;
+      base = A;
+    } else {
+      grow = n0 + (r - TM);
+      base = B;
+    }
+    src[i] = base + grow * rstride + c;
+    dst[i] = r * 8 + (c ^ ((r >> 1) & 7));
+  }
+  u4 st[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) st[i] = src[i][0];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) lds[0][dst[i]] = st[i];
+  __syncthreads();
+
+  f16v H[2], P[2], Q[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+
+  // operand rows of this lane: A row wm*32 + (lane&31), B rows TM + wn*64 + 32 j + (lane&31)
+  const int sw = ((lane & 31) >> 1) & 7, hl = lane >> 5;
+  const int ra = (wm * 32 + (lane & 31)) * 8;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * 8, rb1 = rb0 + 32 * 8;
+  const bool live = EPI != SPLIT_ROWS || m0 + wm * 32 < M;  // ROWS: a wave whose rows all lie past M only stages
+  int cur = 0;
+  for (int kt = 0; kt < nkb; ++kt) {
+    const bool more = kt + 1 < nkb;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < NL; ++i) st[i] = src[i][(int64_t)(kt + 1) * 8];
+    }
+    if (live) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int ch = (2 * kb + hl) ^ sw, cl = (4 + 2 * kb + hl) ^ sw;
+        const h8 ah = __builtin_bit_cast(h8, lds[cur][ra + ch]);
+        const h8 al = __builtin_bit_cast(h8, lds[cur][ra + cl]);
+        const h8 bh0 = __builtin_bit_cast(h8, lds[cur][rb0 + ch]);
+        const h8 bl0 = __builtin_bit_cast(h8, lds[cur][rb0 + cl]);
+        const h8 bh1 = __builtin_bit_cast(h8, lds[cur][rb1 + ch]);
+        const h8 bl1 = __builtin_bit_cast(h8, lds[cur][rb1 + cl]);
+        H[0] = mfma32_f16(ah, bh0, H[0]);
+        H[1] = mfma32_f16(ah, bh1, H[1]);
+        P[0] = mfma32_f16(ah, bl0, P[0]);
+        P[1] = mfma32_f16(ah, bl1, P[1]);
+        Q[0] = mfma32_f16(al, bh0, Q[0]);
+        Q[1] = mfma32_f16(al, bh1, Q[1]);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < NL; ++i) lds[cur ^ 1][dst[i]] = st[i];
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (!live) return;
+
+  // ---- epilogue: K = exp(-g max(|a|^2 + |b|^2 - 2 dot, 0)), dot = 2^-(sa+sb) (H + (P + Q)) ----
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+    const bool cok = col < N;
+    const float bsq = cok ? Bsq[col] : 0.f;
+    const int bsh = cok ? Bsh[col] : 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
+      const float kv = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+      if (EPI == SPLIT_ROWS) {
+        const int32_t orow = s_orow[lr];
+        if (orow >= 0 && cok) out[(int64_t)orow * ldo + col] = kv;
+      } else {
+        const int64_t row = m0 + lr;
+        if (row < M && cok) out[row * ldo + col] = kv;
+        H[j][r] = kv;  // kept for the transposed store
+      }
+    }
+  }
+  if (EPI == SPLIT_STORE && sym && ty != tx) {
+    // transposed tile: a lane holds 4 consecutive rows per group -> 16-B stores out[col][row .. row+3]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (col >= M) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = m0 + wm * 32 + 8 * q + 4 * hl;
+        float* dst = out + col * ldo + row;
+        if (row + 3 < N) {
+          f4 v;
+          v.x = H[j][4 * q + 0];
+          v.y = H[j][4 * q + 1];
+          v.z = H[j][4 * q + 2];
+          v.w = H[j][4 * q + 3];
+          *(f4*)dst = v;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (row + c < N) dst[c] = H[j][4 * q + c];
+        }
+      }
+    }
+  }
+}
+
+}  // namespace dev
+
+namespace launch {
+
+int64_t split_row_u4(int dp) { return (int64_t)((dp + 31) / 32) * 8; }
+
+int64_t split_pad_rows(int64_t rows) { return (rows + 255) / 256 * 256 + 256; }
+
+void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, int32_t* shift, hipStream_t s) {
+  if (rows <= 0) return;
+  const int nkb = (dp + 31) / 32;
+  dev::split_rows_kernel<<<dim3((unsigned)((rows + 3) / 4)), 256, 0, s>>>(x, rows, dp, ldx, (dev::u4*)out, shift,
+                                                                          nkb);
+  post_launch("split_rows_f16", s);
+}
+
+void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
+                          const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
+                          int64_t ldo, hipStream_t s, bool symmetric) {
+  if (M <= 0 || N <= 0) return;
+  DPSVM_CHECK(!symmetric || (A == B && Asq == Bsq && Ash == Bsh && M == N && ldo % 4 == 0),
+              "rbf_gemm_store_split: symmetric mode needs B == A, N == M");
+  const int64_t tm = (M + 127) / 128, tn = (N + 127) / 128;
+  DPSVM_CHECK(tn < 65536, "rbf_gemm_store_split: N too large for grid.y");
+  dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4><<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
+      (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
+      symmetric ? 1 : 0, nullptr, nullptr, nullptr);
+  post_launch("rbf_gemm_store_split", s);
+}
+
+void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq, const int32_t* a_rows,
+                            const int32_t* m_dev, int64_t M_max, const void* B, const int32_t* Bsh, const float* Bsq,
+                            int64_t N, int dp, float gamma, float* lines, const int32_t* out_rows, int64_t ldl,
+                            hipStream_t s) {
+  if (M_max <= 0 || N <= 0) return;
+  const int64_t tm = (M_max + 63) / 64, tn = (N + 255) / 256;
+  DPSVM_CHECK(tn < 65536, "rbf_rows_indexed_split: N too large for grid.y");
+  dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 2><<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
+      (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
+      a_rows, out_rows, m_dev);
+  post_launch("rbf_rows_indexed_split", s);
+}
+
+}  // namespace launch
+}  // namespace dpsvm

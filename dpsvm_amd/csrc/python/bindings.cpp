@@ -198,6 +198,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_t_halve", &SolverParams::ws_t_halve)
       .def_readwrite("ws_clip_fallback", &SolverParams::ws_clip_fallback)
       .def_readwrite("ws_block", &SolverParams::ws_block)
+      .def_readwrite("gram_precision", &SolverParams::gram_precision)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
       .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });
 
@@ -407,6 +408,7 @@ PYBIND11_MODULE(_C, m) {
         d["census"] = i.census;
         d["engine_note"] = i.engine_note;
         d["ws_wss"] = i.ws_wss;
+        d["gram"] = i.gram;
         return d;
       })
       .def("solve", [](GpuSolver& s, const Checkpoint* resume, py::object progress) {
@@ -489,9 +491,15 @@ PYBIND11_MODULE(_C, m) {
                         rows, (void*)stream);
   });
   m.def("k_rbf_rows_indexed", [](uintptr_t x, uintptr_t xsq, int64_t n, int ld, uintptr_t rows, int m_, float gamma,
-                                 uintptr_t out, int64_t out_ld, uintptr_t out_rows, uintptr_t stream) {
+                                 uintptr_t out, int64_t out_ld, uintptr_t out_rows, uintptr_t stream, bool split) {
     kernels::rbf_rows_indexed((const float*)x, (const float*)xsq, n, ld, (const int*)rows, m_, gamma, (float*)out,
-                              out_ld, (const int*)out_rows, (void*)stream);
+                              out_ld, (const int*)out_rows, (void*)stream, split);
+  }, py::arg("x"), py::arg("xsq"), py::arg("n"), py::arg("ld"), py::arg("rows"), py::arg("m"), py::arg("gamma"),
+        py::arg("out"), py::arg("out_ld"), py::arg("out_rows"), py::arg("stream"), py::arg("split") = false);
+  m.def("k_rbf_gram_split", [](uintptr_t a, uintptr_t asq, int64_t m_, uintptr_t b, uintptr_t bsq, int64_t n, int ld,
+                               float gamma, uintptr_t out, int64_t out_ld, bool sym, uintptr_t stream) {
+    kernels::rbf_gram_split((const float*)a, (const float*)asq, m_, (const float*)b, (const float*)bsq, n, ld, gamma,
+                            (float*)out, out_ld, sym, (void*)stream);
   });
   m.def("k_fused_select", [](uintptr_t f, uintptr_t alpha, uintptr_t y, int64_t n, float C, int rows, uintptr_t out,
                              uintptr_t stream) {

@@ -136,6 +136,12 @@ int even_block(const SolverParams& p) {
   return std::max(2, (std::max(1, p.graph_block) + 1) / 2 * 2);
 }
 
+// The split GEMMs' fp16 operands of every x row this rank holds (part of the
+// Gram / first-round work, so inside the timed region of every solve).
+void split_x(GpuSolver::Impl& m) {
+  if (m.gram_split) launch::split_rows_f16(m.x, m.x_rows, m.dp, m.dp, m.xs, m.xsh, m.stream);
+}
+
 // Dense engines: the whole Gram shard K[i][j] (i over all n rows, j over the
 // local rows) by one MFMA GEMM inside the timed region.
 struct DenseBase : Engine {
@@ -143,8 +149,14 @@ struct DenseBase : Engine {
   void gram(GpuSolver::Impl& m, SolveResult& res) {
     trace::Range gram_range("dpsvm/gram_gemm");
     gram_timer.start(m.stream);
+    split_x(m);
     if (!m.replicated) {
       gram_panels(m);
+    } else if (m.gram_split) {
+      const bool sym = m.off == 0 && m.nl == m.n;
+      const size_t ru = (size_t)launch::split_row_u4(m.dp) * 16;
+      launch::rbf_gemm_store_split(m.xs, m.xsh, m.xsq, m.n, (const uint8_t*)m.xs + (size_t)m.off * ru, m.xsh + m.off,
+                                   m.xsq + m.off, m.nl, m.dp, m.gamma, m.lines, m.ldl, m.stream, sym);
     } else {
       // one rank holds the whole (symmetric) Gram: compute half, mirror the rest
       const bool sym = m.off == 0 && m.nl == m.n;
@@ -161,9 +173,12 @@ struct DenseBase : Engine {
   // element is the same MFMA k-sequence as in the replicated launch
   // (bit-identical Gram).  One panel of X lives at a time.
   static void gram_panels(GpuSolver::Impl& m) {
-    const int64_t prow = round_up(m.ldl, 128) + 128;
+    const int64_t prow = round_up(m.ldl, 128) + 512;
     size_t tb = 0;
     float* panel = dmalloc<float>((size_t)prow * m.dp, &tb);
+    const size_t ru = (size_t)launch::split_row_u4(m.dp) * 16;
+    void* pxs = m.gram_split ? (void*)dmalloc<uint8_t>((size_t)prow * ru, &tb) : nullptr;
+    int32_t* pxsh = m.gram_split ? dmalloc<int32_t>((size_t)prow, &tb) : nullptr;
     HIP_CHECK(hipMemsetAsync(panel, 0, (size_t)prow * m.dp * 4, m.stream));
     std::vector<float> host;
     for (int r = 0; r < m.world; ++r) {
@@ -181,11 +196,19 @@ struct DenseBase : Engine {
           HIP_CHECK(hipMemcpyAsync(panel, host.data(), bytes, hipMemcpyHostToDevice, m.stream));
         }
       }
-      launch::rbf_gemm_store(panel, m.xsq + s.offset, s.size, m.dp, m.x, m.xsq + m.off, m.nl, m.dp, m.dp, m.gamma,
-                             m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);
+      if (m.gram_split) {
+        launch::split_rows_f16(panel, prow, m.dp, m.dp, pxs, pxsh, m.stream);
+        launch::rbf_gemm_store_split(pxs, pxsh, m.xsq + s.offset, s.size, m.xs, m.xsh, m.xsq + m.off, m.nl, m.dp,
+                                     m.gamma, m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);
+      } else {
+        launch::rbf_gemm_store(panel, m.xsq + s.offset, s.size, m.dp, m.x, m.xsq + m.off, m.nl, m.dp, m.dp, m.gamma,
+                               m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);
+      }
     }
     HIP_CHECK(hipStreamSynchronize(m.stream));
     (void)hipFree(panel);
+    if (pxs) (void)hipFree(pxs);
+    if (pxsh) (void)hipFree(pxsh);
   }
   // record "no pending pair" in buffer 1 + the initial keys (published to the
   // exchange when there is one, else all-reduced when collectives run)
@@ -413,6 +436,24 @@ struct WsRounds : Base {
   static void miss_rows(GpuSolver::Impl& m, const WsArgs& w) {
     const int64_t mmax = (int64_t)w.blocks * w.q_max;
     const float* B = m.x + (size_t)(m.off - m.args.x_row0) * m.dp;  // the owned rows
+    if (m.gram_split) {
+      const size_t ru = (size_t)launch::split_row_u4(m.dp) * 16;
+      const void* Bs = (const uint8_t*)m.xs + (size_t)(m.off - m.args.x_row0) * ru;
+      const int32_t* Bsh = m.xsh + (m.off - m.args.x_row0);
+      if (m.replicated) {
+        launch::rbf_rows_indexed_split(m.xs, m.xsh, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), mmax, Bs, Bsh,
+                                       m.xsq + m.off, m.nl, m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl,
+                                       m.stream);
+      } else {
+        launch::ws_pack_rows(m.x, m.off, m.nl, m.dp, m.xsq, m.wsctrl, (int)mmax, m.wsxq, m.wsxqsq, m.stream);
+        ws_allreduce_rows(m, mmax);
+        launch::split_rows_f16(m.wsxq, mmax, m.dp, m.dp, m.wsxs, m.wsxsh, m.stream);
+        launch::rbf_rows_indexed_split(m.wsxs, m.wsxsh, m.wsxqsq, m.wsiota, m.wsctrl_n_miss(), mmax, Bs, Bsh,
+                                       m.xsq + m.off, m.nl, m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl,
+                                       m.stream);
+      }
+      return;
+    }
     if (m.replicated) {
       launch::rbf_rows_indexed(m.x, m.xsq, m.wsctrl_miss_row(), m.wsctrl_n_miss(), mmax, B, m.xsq + m.off, m.nl,
                                m.dp, m.gamma, m.lines, m.wsctrl_miss_line(), m.ldl, m.stream);
@@ -488,6 +529,7 @@ struct WsDense final : WsRounds<DenseBase, false> {
 struct WsCache final : WsRounds<Engine, true> {
   EngineKind kind() const override { return EngineKind::WsCache; }
   void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult&) override {
+    split_x(m);
     seed_rounds(m, iter0, b_hi, b_lo);
   }
 };

@@ -102,6 +102,14 @@ struct GpuSolver::Impl {
   float* wssub = nullptr;          // q_max x q_max sub-Gram + [3][kWsMax] f / alpha / y of the working set
   float *wsxq = nullptr, *wsxqsq = nullptr;  // partitioned X, cache mode: the misses' X rows / norms
   int32_t* wsiota = nullptr;                  //   (their GEMM row indices: 0..q_max-1)
+  // fp16 split operands of the GEMMs (rbf_gemm_split.hip), rebuilt by every
+  // solve inside the timed region: xs / xsh = the x_rows rows of x; wsxs /
+  // wsxsh = the packed misses of partitioned ws-cache rounds
+  bool gram_split = false;
+  void* xs = nullptr;
+  int32_t* xsh = nullptr;
+  void* wsxs = nullptr;
+  int32_t* wsxsh = nullptr;
   std::vector<uint8_t> h_wscand;   // host staging of the per-round collectives (host communicators)
   std::vector<float> h_wssub, h_wsxq;
   std::vector<uint8_t> h_wspart;

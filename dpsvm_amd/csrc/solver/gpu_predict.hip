@@ -388,15 +388,60 @@ void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const
   launch::rbf_gemm_store(a, asq, m, ld, b, bsq, n, ld, ld, gamma, out, out_ld, (hipStream_t)stream, symmetric);
 }
 
+namespace {
+// split rows (rbf_gemm_split.hip) of `rows` fp32 rows of x, in a fresh buffer
+struct SplitRows {
+  void* planes = nullptr;
+  int32_t* shift = nullptr;
+  SplitRows(const float* x, int64_t rows, int ld, hipStream_t s) {
+    const int64_t pr = launch::split_pad_rows(rows);
+    const size_t bytes = (size_t)pr * launch::split_row_u4(ld) * 16;
+    size_t tb = 0;
+    planes = dmalloc<uint8_t>(bytes, &tb);
+    shift = dmalloc<int32_t>((size_t)pr, &tb);
+    HIP_CHECK(hipMemsetAsync(planes, 0, bytes, s));
+    HIP_CHECK(hipMemsetAsync(shift, 0, (size_t)pr * 4, s));
+    launch::split_rows_f16(x, rows, ld, ld, planes, shift, s);
+  }
+  ~SplitRows() {
+    (void)hipFree(planes);
+    (void)hipFree(shift);
+  }
+};
+}  // namespace
+
+void rbf_gram_split(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
+                    float gamma, float* out, int64_t out_ld, bool symmetric, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  SplitRows sa(a, m, ld, s);
+  if (symmetric) {
+    launch::rbf_gemm_store_split(sa.planes, sa.shift, asq, m, sa.planes, sa.shift, asq, n, ld, gamma, out, out_ld, s,
+                                 true);
+    HIP_CHECK(hipStreamSynchronize(s));
+    return;
+  }
+  SplitRows sb(b, n, ld, s);
+  launch::rbf_gemm_store_split(sa.planes, sa.shift, asq, m, sb.planes, sb.shift, bsq, n, ld, gamma, out, out_ld, s,
+                               false);
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
 void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const int* rows, int m, float gamma,
-                      float* out, int64_t out_ld, const int* out_rows, void* stream) {
+                      float* out, int64_t out_ld, const int* out_rows, void* stream, bool split) {
   DPSVM_CHECK(ld % 16 == 0 && m >= 0 && m <= 4096, "rbf_rows_indexed: ld multiple of 16, m <= 4096");
   hipStream_t s = (hipStream_t)stream;
   size_t tb = 0;
   int32_t* md = dmalloc<int32_t>(1, &tb);
   HIP_CHECK(hipMemcpyAsync(md, &m, 4, hipMemcpyHostToDevice, s));
-  launch::rbf_rows_indexed(x, xsq, rows, md, m, x, xsq, n, ld, gamma, out, out_rows, out_ld, s);
-  HIP_CHECK(hipStreamSynchronize(s));
+  if (split) {
+    SplitRows sx(x, n, ld, s);
+    launch::rbf_rows_indexed_split(sx.planes, sx.shift, xsq, rows, md, m, sx.planes, sx.shift, xsq, n, ld, gamma, out,
+                                   out_rows, out_ld, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+  } else {
+    launch::rbf_rows_indexed(x, xsq, rows, md, m, x, xsq, n, ld, gamma, out, out_rows, out_ld, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
   (void)hipFree(md);
 }
 

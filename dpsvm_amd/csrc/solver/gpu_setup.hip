@@ -38,7 +38,7 @@ GpuSolver::Impl::~Impl() {
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
                     (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wsdfs, (void*)wsdalpha, (void*)wspart,
-                    (void*)wsxq, (void*)wsxqsq, (void*)wsiota})
+                    (void*)wsxq, (void*)wsxqsq, (void*)wsiota, xs, (void*)xsh, wsxs, (void*)wsxsh})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
   if (hlines_h) (void)hipHostFree(hlines_h);
@@ -325,6 +325,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     m.h_records.assign((size_t)rb * m.world, 0);
   }
   m.h_partials.assign((size_t)2 * m.G, kKeyNone);
+  // fp16 split operands of x for the split GEMMs (allocated before the cache is
+  // sized from the free memory; released below if the engine runs f32 GEMMs)
+  DPSVM_CHECK(m.p.gram_precision >= 0 && m.p.gram_precision <= 2, "gram_precision must be 0 (auto), 1 (f32) or 2 (split)");
+  const bool maybe_ws = m.p.solver == 2 || (m.p.solver == 0 && n >= kWsAutoRows);
+  if (m.p.gram_precision == 2 || (m.p.gram_precision == 0 && maybe_ws)) {
+    m.xs = dmalloc<uint8_t>((size_t)m.x_rows * launch::split_row_u4(m.dp) * 16, &m.bytes);
+    m.xsh = dmalloc<int32_t>((size_t)m.x_rows, &m.bytes);
+  }
   HIP_CHECK(hipStreamSynchronize(m.stream));
 
   // ---- kernel-row cache sizing (288 GB HBM: the Gram shard is usually resident) ----
@@ -576,6 +584,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     a.plru_meta = nullptr;
     a.plru_stride = 0;
   }
+  // split GEMMs: the working-set engines (auto), or every dense Gram (split);
+  // the pair-at-a-time cache engines compute rows in their own f32 X pass
+  m.gram_split = m.xs && (m.working_set() || (m.p.gram_precision == 2 && m.dense));
+  if (m.xs && !m.gram_split) {
+    (void)hipFree(m.xs);
+    (void)hipFree(m.xsh);
+    m.xs = nullptr;
+    m.xsh = nullptr;
+  }
+  m.info.gram = m.gram_split ? "split-f16" : "f32";
   if (m.working_set()) {
     WsArgs& w = m.wsa;
     w = WsArgs{};
@@ -676,6 +694,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       m.wsxq = dmalloc<float>((size_t)rows * m.dp, &m.bytes);
       m.wsxqsq = dmalloc<float>((size_t)rows, &m.bytes);
       m.wsiota = dmalloc<int32_t>((size_t)rows, &m.bytes);
+      if (m.gram_split) {
+        m.wsxs = dmalloc<uint8_t>((size_t)rows * launch::split_row_u4(m.dp) * 16, &m.bytes);
+        m.wsxsh = dmalloc<int32_t>((size_t)rows, &m.bytes);
+      }
       std::vector<int32_t> io((size_t)rows);
       for (int64_t i = 0; i < rows; ++i) io[i] = (int32_t)i;
       HIP_CHECK(hipMemcpyAsync(m.wsiota, io.data(), io.size() * 4, hipMemcpyHostToDevice, m.stream));

@@ -121,6 +121,9 @@ class SVCConfig:
     ws_t_halve: float = 0.9         # multi-block: a round damped below this t halves the block count
     ws_clip_fallback: bool = True   # multi-block, independent clipping: one block per round after a clip
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
+    # Gram / kernel-row GEMM arithmetic: auto (split for the working-set engines, f32 for the pair engines),
+    # f32 (f32-input MFMA), split (fp16 MFMA over hi/lo split operands: fp32 accuracy, 3/16 of the MFMA time)
+    gram: str = "auto"
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -186,6 +189,7 @@ class SVCConfig:
         p.ws_clip_fallback = int(bool(self.ws_clip_fallback))
         p.ws_block = int(self.ws_block)
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
+        p.gram_precision = _pick({"auto": 0, "f32": 1, "split": 2}, self.gram, "gram")
         return p
 
     def device_kind(self) -> tuple[str, int]:

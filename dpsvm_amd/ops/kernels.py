@@ -37,9 +37,10 @@ def row_sqnorm(x: torch.Tensor) -> torch.Tensor:
     return out[: x.shape[0]]
 
 
-def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0) -> torch.Tensor:
+def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0, split: bool = False) -> torch.Tensor:
     """Gram block K[i, j] = exp(-gamma |a_i - b_j|^2) with the dense-mode MFMA
-    GEMM (32x32x2 f32, fused exp).  b=None: the symmetric Gram of a, computed
+    GEMM (32x32x2 f32, fused exp; split=True: fp16 MFMA over hi/lo split
+    operands, rbf_gemm_split.hip).  b=None: the symmetric Gram of a, computed
     as upper-triangle tiles plus their mirrored transposes."""
     C = load()
     sym = b is None
@@ -56,8 +57,9 @@ def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0)
     n = m if sym else b.shape[0]
     ld = (n + 127) // 128 * 128
     out = torch.full((m, ld), float("nan"), device=a.device)
-    C.k_rbf_gram(ap.data_ptr(), asq.data_ptr(), m, bp.data_ptr(), bsq.data_ptr(), n, dp, float(gamma),
-                 out.data_ptr(), ld, sym, _stream(a))
+    fn = C.k_rbf_gram_split if split else C.k_rbf_gram
+    fn(ap.data_ptr(), asq.data_ptr(), m, bp.data_ptr(), bsq.data_ptr(), n, dp, float(gamma), out.data_ptr(), ld, sym,
+       _stream(a))
     return out[:, :n]
 
 
@@ -150,10 +152,12 @@ def xpass_rows(x: torch.Tensor, keys, gamma: float, rows_per_group: int = 256) -
     return out[:, :n]
 
 
-def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_lines: int = 0) -> torch.Tensor:
+def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_lines: int = 0,
+                     split: bool = False) -> torch.Tensor:
     """The working-set cache engine's row GEMM (rbf_gemm EPI_ROWS: A rows by
     index, output rows to their lines, M read on the device): lines
-    [n_lines][n] with line out_lines[i] = K(x_rows[i], x_j)."""
+    [n_lines][n] with line out_lines[i] = K(x_rows[i], x_j).  split=True: the
+    fp16 split-operand kernel (rbf_gemm_split.hip)."""
     C = load()
     rows = [int(r) for r in rows]
     m = len(rows)
@@ -168,7 +172,7 @@ def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_line
     ld = (n + 127) // 128 * 128
     out = torch.full((n_lines, ld), float("nan"), device=x.device)
     C.k_rbf_rows_indexed(xp.data_ptr(), xsq.data_ptr(), n, dp, rd.data_ptr(), m, float(gamma), out.data_ptr(), ld,
-                         od.data_ptr(), _stream(x))
+                         od.data_ptr(), _stream(x), bool(split))
     return out[:, :n]
 
 

@@ -1,0 +1,83 @@
+"""The fp16 split-operand RBF GEMM (kernels/rbf_gemm_split.hip) vs a float64
+reference and vs the f32-MFMA GEMM (rbf_gemm.hip): same accuracy class, and
+bit-identical values under operand swap (symmetric Gram == full Gram ==
+indexed rows), which the sharded and cache-mode working-set engines rely on."""
+import numpy as np
+import pytest
+import torch
+
+from dpsvm_amd.utils.datasets import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dpsvm_amd.ops import kernels
+
+    return kernels
+
+
+def _ref(a, b, gamma):
+    a = a.astype(np.float64)
+    b = b.astype(np.float64)
+    d2 = (a * a).sum(1)[:, None] + (b * b).sum(1)[None, :] - 2 * a @ b.T
+    return np.exp(-gamma * np.maximum(d2, 0))
+
+
+@pytest.mark.parametrize("name,n,d,gamma", [("mnist", 1500, 784, 0.25), ("covtype", 1300, 54, 0.5),
+                                            ("blobs", 700, 1100, 1.0 / 1100)])
+def test_split_gram_matches_float64_like_f32_kernel(K, name, n, d, gamma):
+    kw = dict(n=n, seed=3, d=d) if name == "blobs" else dict(n=n, seed=3)
+    X, _ = synthetic(name, **kw)
+    x = torch.from_numpy(X).cuda()
+    ref = _ref(X, X, gamma)
+    k32 = K.rbf_gram(x, None, gamma).cpu().numpy()
+    k16 = K.rbf_gram(x, None, gamma, split=True).cpu().numpy()
+    e32 = np.abs(k32 - ref).max()
+    e16 = np.abs(k16 - ref).max()
+    assert e16 <= max(3 * e32, 2e-6), (e16, e32)
+    assert np.isfinite(k16).all()
+
+
+def test_split_gram_operand_swap_bit_identical(K):
+    X, _ = synthetic("mnist", n=1000, seed=4)
+    Y, _ = synthetic("mnist", n=777, seed=5)
+    x, yv = torch.from_numpy(X).cuda(), torch.from_numpy(Y).cuda()
+    sym = K.rbf_gram(x, None, 0.25, split=True)
+    full = K.rbf_gram(x, x.clone(), 0.25, split=True)
+    assert torch.equal(sym, full)
+    assert torch.equal(sym, sym.T)
+    ab = K.rbf_gram(x, yv, 0.25, split=True)
+    ba = K.rbf_gram(yv, x, 0.25, split=True)
+    assert torch.equal(ab, ba.T)
+
+
+def test_split_rows_indexed_equals_split_gram_rows(K):
+    X, _ = synthetic("mnist", n=1200, seed=6)
+    x = torch.from_numpy(X).cuda()
+    full = K.rbf_gram(x, None, 0.25, split=True)
+    rows = [5, 1199, 0, 640, 641, 77, 333, 1024] + list(range(100, 160))
+    lines = list(range(len(rows)))[::-1]
+    got = K.rbf_rows_indexed(x, rows, 0.25, out_lines=lines, split=True)
+    for r, ln in zip(rows, lines):
+        assert torch.equal(got[ln], full[r]), r
+
+
+def test_split_gram_extreme_row_scales(K):
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((300, 40)).astype(np.float32)
+    X[0] = 0.0                      # zero row
+    X[1] *= 1e-20                   # tiny row
+    X[2] *= 1e15                    # huge row
+    X[3, :5] = [1e6, 1e-6, -3.0, 0.0, 2.5e-30]  # wide range inside a row
+    x = torch.from_numpy(X).cuda()
+    g = 1e-3
+    k16 = K.rbf_gram(x, None, g, split=True).cpu().numpy()
+    k32 = K.rbf_gram(x, None, g).cpu().numpy()
+    ref = _ref(X, X, g)
+    assert np.isfinite(k16).all()
+    assert np.abs(k16 - ref).max() <= max(3 * np.abs(k32 - ref).max(), 2e-6)
+    assert k16[0, 0] == 1.0 and k16[1, 1] == 1.0
