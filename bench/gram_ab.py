@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--d", type=int, default=784)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="")
+    ap.add_argument("--only", default="", choices=["", "f32", "split"])
     args = ap.parse_args()
     C = load()
     X, _ = synthetic("mnist", n=args.n, seed=1)
@@ -45,6 +46,8 @@ def main():
     flops = 2.0 * 128 * 128 * dp * tiles * (tiles + 1) / 2  # upper tiles incl. the diagonal
     sub = np.random.default_rng(0).choice(n, 2048, replace=False)
     for name, fn in (("f32", C.k_rbf_gram), ("split", C.k_rbf_gram_split)):
+        if args.only and name != args.only:
+            continue
         ts = []
         for r in range(args.reps + 1):
             torch.cuda.synchronize()

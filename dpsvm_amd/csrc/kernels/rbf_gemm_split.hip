@@ -34,6 +34,8 @@
 // reads (16 rows, one chunk) hit 16 distinct bank quads.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dpsvm/common.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
@@ -110,16 +112,22 @@ __device__ __forceinline__ void xcd_tile(int64_t& tx, int64_t& ty) {
 
 enum SplitEpi { SPLIT_STORE = 0, SPLIT_ROWS = 1 };
 
-template <int EPI, int WM>
+// KB: 32-wide k blocks per LDS stage (1: 128-B LDS rows, chunk index XOR
+// (row >> 1) & 7; 2: 256-B rows, XOR row & 15 — both leave every ds_read_b128
+// lane group of the operand reads on 16 distinct bank quads).
+// ABL (diagnostics only, DPSVM_SPLIT_ABLATE): 1 = no global stores (a runtime
+// condition never true, gamma < 0, keeps the epilogue's math), 2 = no mirrored stores
+template <int EPI, int WM, int KB, int ABL = 0>
 __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
     float gamma, float* __restrict__ out, int64_t ldo, int sym, const int32_t* __restrict__ a_rows,
     const int32_t* __restrict__ out_rows, const int32_t* __restrict__ m_dev) {
   constexpr int WN = 8 / WM, TM = 32 * WM, TN = 64 * WN, ROWS = TM + TN;
-  constexpr int CH = ROWS * 8;                   // 16-B chunks per stage
+  constexpr int CPR = 8 * KB;                    // 16-B chunks per row and stage
+  constexpr int CH = ROWS * CPR;                 // chunks per stage
   constexpr int NL = CH / kSplitThreads;         // chunks per thread
-  static_assert(CH % kSplitThreads == 0, "whole chunks per thread");
+  static_assert(CH % kSplitThreads == 0 && (KB == 1 || KB == 2), "whole chunks per thread");
   int64_t tx, ty;
   xcd_tile(tx, ty);
   if (EPI == SPLIT_ROWS) M = *m_dev;
@@ -133,6 +141,7 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
   const int wm = wave / WN, wn = wave % WN;
   const int64_t m0 = tx * TM, n0 = ty * TN;
   const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
+  const int nst = (nkb + KB - 1) / KB;       // stages
 
   if (tid < TM) {
     const int64_t row = m0 + tid;
@@ -142,12 +151,12 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
     s_orow[tid] = EPI == SPLIT_ROWS ? (row < M ? out_rows[row] : -1) : 0;
   }
 
-  // staging: chunk id = tid + 512 i -> stage row id >> 3 (A rows, then B rows), chunk id & 7
+  // staging: chunk id = tid + 512 i -> stage row id / CPR (A rows, then B rows), chunk id % CPR
   const u4* src[NL];
   int dst[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int id = tid + kSplitThreads * i, r = id >> 3, c = id & 7;
+    const int id = tid + kSplitThreads * i, r = id / CPR, c = id % CPR;
     int64_t grow;
     const u4* base;
     if (r < TM) {
@@ -159,11 +168,22 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
       base = B;
     }
     src[i] = base + grow * rstride + c;
-    dst[i] = r * 8 + (c ^ ((r >> 1) & 7));
+    dst[i] = r * CPR + (c ^ (KB == 1 ? (r >> 1) & 7 : r & 15));
   }
-  u4 st[NL];
+  // chunk i of a stage belongs to k block (i % CPR) / 8 of it: the last stage
+  // of an odd block count computes its first block only, and its chunks of the
+  // missing block re-read the block before (an address select, not a branch
+  // around the load: hipcc would wait vmcnt(0) at every such branch)
+  auto load = [&](u4* st, int kt) {
 #pragma unroll
-  for (int i = 0; i < NL; ++i) st[i] = src[i][0];
+    for (int i = 0; i < NL; ++i) {
+      const int blk = ((tid + kSplitThreads * i) % CPR) >> 3;
+      const int64_t o = (int64_t)kt * CPR - ((KB > 1 && kt * KB + blk >= nkb) ? 8 : 0);
+      st[i] = src[i][o];
+    }
+  };
+  u4 st[NL];
+  load(st, 0);
 #pragma unroll
   for (int i = 0; i < NL; ++i) lds[0][dst[i]] = st[i];
   __syncthreads();
@@ -175,33 +195,34 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
     for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
 
   // operand rows of this lane: A row wm*32 + (lane&31), B rows TM + wn*64 + 32 j + (lane&31)
-  const int sw = ((lane & 31) >> 1) & 7, hl = lane >> 5;
-  const int ra = (wm * 32 + (lane & 31)) * 8;
-  const int rb0 = (TM + wn * 64 + (lane & 31)) * 8, rb1 = rb0 + 32 * 8;
+  const int sw = KB == 1 ? ((lane & 31) >> 1) & 7 : lane & 15, hl = lane >> 5;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
   const bool live = EPI != SPLIT_ROWS || m0 + wm * 32 < M;  // ROWS: a wave whose rows all lie past M only stages
   int cur = 0;
-  for (int kt = 0; kt < nkb; ++kt) {
-    const bool more = kt + 1 < nkb;
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < NL; ++i) st[i] = src[i][(int64_t)(kt + 1) * 8];
-    }
+  for (int kt = 0; kt < nst; ++kt) {
+    const bool more = kt + 1 < nst;
+    if (more) load(st, kt + 1);
     if (live) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        const int ch = (2 * kb + hl) ^ sw, cl = (4 + 2 * kb + hl) ^ sw;
-        const h8 ah = __builtin_bit_cast(h8, lds[cur][ra + ch]);
-        const h8 al = __builtin_bit_cast(h8, lds[cur][ra + cl]);
-        const h8 bh0 = __builtin_bit_cast(h8, lds[cur][rb0 + ch]);
-        const h8 bl0 = __builtin_bit_cast(h8, lds[cur][rb0 + cl]);
-        const h8 bh1 = __builtin_bit_cast(h8, lds[cur][rb1 + ch]);
-        const h8 bl1 = __builtin_bit_cast(h8, lds[cur][rb1 + cl]);
-        H[0] = mfma32_f16(ah, bh0, H[0]);
-        H[1] = mfma32_f16(ah, bh1, H[1]);
-        P[0] = mfma32_f16(ah, bl0, P[0]);
-        P[1] = mfma32_f16(ah, bl1, P[1]);
-        Q[0] = mfma32_f16(al, bh0, Q[0]);
-        Q[1] = mfma32_f16(al, bh1, Q[1]);
+      for (int blk = 0; blk < KB; ++blk) {
+        if (KB > 1 && kt * KB + blk >= nkb) break;  // uniform
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int ch = (8 * blk + 2 * ks + hl) ^ sw, cl = (8 * blk + 4 + 2 * ks + hl) ^ sw;
+          const h8 ah = __builtin_bit_cast(h8, lds[cur][ra + ch]);
+          const h8 al = __builtin_bit_cast(h8, lds[cur][ra + cl]);
+          const h8 bh0 = __builtin_bit_cast(h8, lds[cur][rb0 + ch]);
+          const h8 bl0 = __builtin_bit_cast(h8, lds[cur][rb0 + cl]);
+          const h8 bh1 = __builtin_bit_cast(h8, lds[cur][rb1 + ch]);
+          const h8 bl1 = __builtin_bit_cast(h8, lds[cur][rb1 + cl]);
+          H[0] = mfma32_f16(ah, bh0, H[0]);
+          H[1] = mfma32_f16(ah, bh1, H[1]);
+          P[0] = mfma32_f16(ah, bl0, P[0]);
+          P[1] = mfma32_f16(ah, bl1, P[1]);
+          Q[0] = mfma32_f16(al, bh0, Q[0]);
+          Q[1] = mfma32_f16(al, bh1, Q[1]);
+        }
       }
     }
     if (more) {
@@ -214,48 +235,75 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
   if (!live) return;
 
   // ---- epilogue: K = exp(-g max(|a|^2 + |b|^2 - 2 dot, 0)), dot = 2^-(sa+sb) (H + (P + Q)) ----
+  // (all values first, into H; then the stores: unpredicated for interior tiles)
+  float asq_r[16];
+  int ash_r[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    asq_r[r] = s_asq[lr];
+    ash_r[r] = s_ash[lr];
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
-    const bool cok = col < N;
-    const float bsq = cok ? Bsq[col] : 0.f;
-    const int bsh = cok ? Bsh[col] : 0;
+    const int64_t cc = col < N ? col : N - 1;
+    const float bsq = Bsq[cc];
+    const int bsh = Bsh[cc];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
-      const float kv = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
-      if (EPI == SPLIT_ROWS) {
-        const int32_t orow = s_orow[lr];
-        if (orow >= 0 && cok) out[(int64_t)orow * ldo + col] = kv;
-      } else {
-        const int64_t row = m0 + lr;
-        if (row < M && cok) out[row * ldo + col] = kv;
-        H[j][r] = kv;  // kept for the transposed store
+      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(ash_r[r] + bsh));
+      H[j][r] = rbf_from_dot(asq_r[r], bsq, dot, gamma);
+    }
+  }
+  const bool interior = m0 + TM <= M && n0 + TN <= N;
+  if (EPI == SPLIT_ROWS) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int32_t orow = s_orow[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+        if (orow >= 0 && (interior || col < N)) out[(int64_t)orow * ldo + col] = H[j][r];
+      }
+    }
+    return;
+  }
+  if (ABL != 1 || gamma < 0.f) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+        if (interior || (row < M && col < N)) out[row * ldo + col] = H[j][r];
       }
     }
   }
-  if (EPI == SPLIT_STORE && sym && ty != tx) {
+  if (EPI == SPLIT_STORE && sym && ty != tx && ABL == 0) {
     // transposed tile: a lane holds 4 consecutive rows per group -> 16-B stores out[col][row .. row+3]
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
-      if (col >= M) continue;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t row = m0 + wm * 32 + 8 * q + 4 * hl;
         float* dst = out + col * ldo + row;
-        if (row + 3 < N) {
-          f4 v;
-          v.x = H[j][4 * q + 0];
-          v.y = H[j][4 * q + 1];
-          v.z = H[j][4 * q + 2];
-          v.w = H[j][4 * q + 3];
+        f4 v;
+        v.x = H[j][4 * q + 0];
+        v.y = H[j][4 * q + 1];
+        v.z = H[j][4 * q + 2];
+        v.w = H[j][4 * q + 3];
+        if (interior) {
           *(f4*)dst = v;
-        } else {
+        } else if (col < M) {
+          if (row + 3 < N) {
+            *(f4*)dst = v;
+          } else {
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (row + c < N) dst[c] = H[j][4 * q + c];
+            for (int c = 0; c < 4; ++c)
+              if (row + c < N) dst[c] = v[c];
+          }
         }
       }
     }
@@ -286,7 +334,19 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
               "rbf_gemm_store_split: symmetric mode needs B == A, N == M");
   const int64_t tm = (M + 127) / 128, tn = (N + 127) / 128;
   DPSVM_CHECK(tn < 65536, "rbf_gemm_store_split: N too large for grid.y");
-  dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4><<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
+  static const int ablate = [] {
+    const char* e = std::getenv("DPSVM_SPLIT_ABLATE");  // diagnostics (bench/gram_ab.py)
+    return e ? atoi(e) : 0;
+  }();
+  static const int kb = [] {
+    const char* e = std::getenv("DPSVM_SPLIT_KB");  // diagnostics: k blocks per stage (A/B)
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  auto kern = kb == 1 ? dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 1, 0>
+              : ablate == 1 ? dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 2, 1>
+              : ablate == 2 ? dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 2, 2>
+                            : dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 2, 0>;
+  kern<<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
       (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
       symmetric ? 1 : 0, nullptr, nullptr, nullptr);
   post_launch("rbf_gemm_store_split", s);
@@ -299,7 +359,7 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
   if (M_max <= 0 || N <= 0) return;
   const int64_t tm = (M_max + 63) / 64, tn = (N + 255) / 256;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed_split: N too large for grid.y");
-  dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 2><<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
+  dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 2, 1><<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
       (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
       a_rows, out_rows, m_dev);
   post_launch("rbf_rows_indexed_split", s);
