@@ -86,6 +86,10 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   SolverParams p = p0;
   p.checkpoint_every = 0;  // phases are not checkpointed (the final state is)
   if (p.solver == 0) p.solver = 2;  // the phases are parts of a large problem: working-set rounds at any size
+  // the inactive rows' gradient comes from the f32 predict GEMM: the phases'
+  // kernel values must be the same f32 MFMA values (split-GEMM values differ
+  // by ~1e-5, which C-sized alpha changes turn into gradient drift)
+  if (p.gram_precision == 0) p.gram_precision = 1;
   const float gamma = resolve_gamma(p.gamma, d);
   p.gamma = gamma;
   const float C = p.C;

@@ -1,0 +1,67 @@
+"""Rank death on the GPU path: with
+DPSVM_FAULT=exit@K:1 rank 1's process dies mid-solve; the surviving rank must
+fail on its own within 60 s (the in-kernel peer exchange gives up and the
+solve raises), and the in-process multi-rank CLI must exit non-zero."""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_dead_rank_process_survivor_fails_within_60s():
+    port = _free_port()
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_RANK=str(r), DPSVM_FORCE_DEVICE="0", DPSVM_FAULT="exit@2000:1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_fault_worker.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=150)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    assert procs[1].returncode == 3, outs[1][-2000:]  # the injected death
+    assert procs[0].returncode != 0, outs[0][-2000:]
+    assert "rank 0: error" in outs[0], outs[0][-2000:]
+    # process start-up (torch import, device init, setup) included
+    assert elapsed < 90, elapsed
+
+
+def test_dead_rank_in_process_cli_exits_nonzero(tmp_path):
+    exe = os.path.join(ROOT, "bin", "svmTrain")
+    if not os.path.exists(exe):
+        pytest.skip("bin/svmTrain not built")
+    env = dict(os.environ, DPSVM_FAULT="exit@2000:1")
+    t0 = time.time()
+    r = subprocess.run([exe, "-a", "784", "-x", "12000", "--synthetic", "mnist", "-c", "10", "-g", "0.25", "-m",
+                        str(tmp_path / "m.txt"), "--ranks", "2", "--solver", "ws", "--dp", "shard",
+                        "--xch-timeout", "15"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert time.time() - t0 < 60

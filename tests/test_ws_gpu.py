@@ -520,11 +520,12 @@ def test_shrinking_reaches_the_stop_test_on_the_whole_problem(clip):
     unique optimum) matches the unshrunk solve."""
     X, y = synthetic("covtype", n=30000, seed=8)
     C_, g = 64.0, 0.25
-    kw = dict(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", solver="ws")
+    kw = dict(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", solver="ws", max_iter=5_000_000)
     full = SVC(**kw).fit(X, y)
     shr = SVC(shrink=True, **kw).fit(X, y)
     assert shr.setup_info_["iteration"] == "ws+shrinking" and shr.stats_["shrink_phases"] >= 2
-    assert shr.converged_ and full.converged_
+    assert full.converged_, (full.status_, full.n_iter_, full.stats_)
+    assert shr.converged_, (shr.status_, shr.n_iter_, shr.stats_)
     gap = _kkt_gap(X, y, shr.alpha_, C_, g)
     print(f"{clip}: phases {shr.stats_['shrink_phases']} gap {gap:.2e} b {shr.b_:.5f} vs {full.b_:.5f} "
           f"nsv {shr.n_support_} vs {full.n_support_} steps {shr.n_iter_} vs {full.n_iter_}")
