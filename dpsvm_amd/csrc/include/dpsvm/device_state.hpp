@@ -263,10 +263,11 @@ constexpr int64_t kWsAutoRows = 50000;   // solver auto: working-set engines fro
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor
 // t = min(1, g'd / d'Qd) of the dual (smo_ws.hip "multi-block rounds")
-constexpr int kWsMaxBlocks = 8;
-constexpr int kWsMaxAll = kWsMaxBlocks * kWsMax;  // union capacity (1536)
+constexpr int kWsMaxBlocks = 16;                  // blocks per round (P x q_max <= kWsMaxAll)
+constexpr int kWsAutoBlocks = 16;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
+constexpr int kWsMaxAll = 8 * kWsMax;             // union capacity (1536 rows)
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
-constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: kWsMaxBlocks from this many rows on
+constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
 
 struct alignas(16) WsCtrl {
   int64_t iter;      // pair updates applied so far

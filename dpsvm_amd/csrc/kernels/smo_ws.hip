@@ -1812,7 +1812,7 @@ void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
 }
 
 void ws_merge_multi(const WsArgs& a, hipStream_t s) {
-  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && !a.xpeer && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
+  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.blocks * a.q_max <= kWsMaxAll && !a.xpeer && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
                   (!a.cache || ws_cache_multi_supported(a.L, a.blocks, a.q_max)),
               "ws_merge_multi: multi-block rounds need the collectives, <= 256 candidate lists, an even q_max and "
               "(cache mode) L >= 2 P q_max + 4096 lines");

@@ -425,6 +425,8 @@ struct WsRounds : Base {
   static WsArgs one_block(const GpuSolver::Impl& m) {
     WsArgs w = m.wsa;
     w.blocks = 1;
+    w.q_max = m.ws_q1;  // ws_size rows (the multi-block rounds may use smaller blocks)
+    w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * w.q_max;
     w.aux = m.wssub + (size_t)w.q_max * w.q_max;
     w.aux_stride = kWsMax;
     // the one-block engine's set turnover (multi-block rounds replace the

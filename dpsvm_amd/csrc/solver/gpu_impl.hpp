@@ -94,6 +94,7 @@ struct GpuSolver::Impl {
   int64_t Gf = 0, RBf = 0;         // fused / persistent geometry: workgroups, rows per workgroup
   // working-set engine (smo_ws.hip): round control record, candidate keys
   WsArgs wsa{};
+  int ws_q1 = 0;                    // the one-block rounds' q_max (multi-block rounds may use smaller blocks)
   WsCtrl* wsctrl = nullptr;
   uint64_t* wscand = nullptr;
   float* wsdfs = nullptr;           // multi-block rounds: d_f [nl], d_alpha [n], line-search partials [G][2]

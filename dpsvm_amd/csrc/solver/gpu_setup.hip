@@ -501,11 +501,22 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool multi_comm = m.world == 1 || m.comm->device_memory() || m.p.exchange == 1;
   // ws_blocks auto (0): every block from kWsAutoBlocksRows rows on (the round's
   // fixed cost is amortised over P sub-problems; small problems need few rounds)
-  const int want_blocks = m.p.ws_blocks > 0 ? m.p.ws_blocks : (n >= kWsAutoBlocksRows ? kWsMaxBlocks : 1);
+  // auto: kWsAutoBlocks (16) blocks of kWsMaxAll / 16 = 96 rows (the union
+  // capacity over more, smaller sub-problems: each round's pair steps run on
+  // twice the workgroups; headline 0.0341 vs 0.0371 s at 8 x 192, same rounds,
+  // profiles/r3_blocks16_ab.txt), never larger than ws_size; the one-block
+  // rounds the adaptive count falls back to keep ws_size rows
+  const int auto_q = std::min(ws_q, kWsMaxAll / kWsAutoBlocks) & ~1;
+  const bool blocks_auto = m.p.ws_blocks == 0;
+  const int want_blocks = !blocks_auto ? m.p.ws_blocks
+                                       : (n >= kWsAutoBlocksRows ? std::min(kWsAutoBlocks, kWsMaxAll / auto_q) : 1);
+  const int mb_q = blocks_auto ? auto_q : ws_q;  // rows per block of the multi-block rounds
+  DPSVM_CHECK(want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
+              "ws_blocks x ws_size must be <= " + std::to_string(kWsMaxAll) + " (the round's union capacity)");
   // ws-cache takes them too when its cache holds the union's lines plus the
   // victim window (L >= 2 P q_max + 4096; agreed: L follows each device's free memory)
-  const bool wsc_multi = wsc_fits_pre && launch::ws_cache_multi_supported(m.L, want_blocks, ws_q);
-  bool multi_ok = want_blocks > 1 && (ws_cand || wsc_multi) && ws_q % 2 == 0 &&
+  const bool wsc_multi = wsc_fits_pre && launch::ws_cache_multi_supported(m.L, want_blocks, mb_q);
+  bool multi_ok = want_blocks > 1 && (ws_cand || wsc_multi) && mb_q % 2 == 0 &&
                   (int64_t)ws_G * m.world <= kWsMaxGroups && m.p.exchange != 2 && multi_comm;
   if (m.world > 1) multi_ok = m.all_agree(multi_ok, m.comm, m.world);
   // Residency of the ws peer exchange: gather workgroup a of every rank spins
@@ -647,15 +658,20 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.max_iter = m.p.max_iter;
     // multi-block rounds (adaptive block count, smo_ws.hip)
     w.blocks = 1;
+    m.ws_q1 = ws_q;
     if (want_blocks > 1) {
-      if (multi_ok && !m.xch) w.blocks = want_blocks;
+      if (multi_ok && !m.xch) {
+        w.blocks = want_blocks;
+        w.q_max = mb_q;
+        w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * mb_q;
+      }
       else if (m.p.ws_blocks > 1) m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
                                  "ws_blocks > 1 needs an even ws_size, <= 256 candidate lists over the collectives "
                                  "and (ws-cache) >= 2 P ws_size + 4096 lines: one block per round";
     }
     // multi-block rounds replace the whole union each round by default (measured on the
     // headline at P = 8: 3/4 q new 0.0506 s, all new 0.0493 s; profiles/r2_ws_blocks_sweep.txt)
-    if (w.blocks > 1 && m.p.ws_new <= 0) w.n_new = ws_q;
+    if (w.blocks > 1 && m.p.ws_new <= 0) w.n_new = w.q_max;
     w.rank = m.rank;
     w.aux_stride = w.blocks * kWsMax;
     // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)
@@ -664,13 +680,15 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // sub-Gram [q_max][q_max] then aux [f | alpha | y]: the first q_max^2 + kWsMax
     // floats are the per-round sum all-reduce at world > 1
     // (multi-block: P sub-Grams, then P aux blocks)
-    const size_t sub_floats = (size_t)w.blocks * ((size_t)ws_q * ws_q + 3 * kWsMax);
+    // (the one-block rounds' view: ws_size rows, gpu_engines.hip one_block)
+    const size_t sub_floats = std::max((size_t)w.blocks * ((size_t)w.q_max * w.q_max + 3 * kWsMax),
+                                       (size_t)ws_q * ws_q + 3 * kWsMax);
     m.wssub = dmalloc<float>(sub_floats, &m.bytes);
     HIP_CHECK(hipMemsetAsync(m.wssub, 0, sub_floats * 4, m.stream));
     w.cand = m.wscand;
     w.cand_out = m.wscand + (size_t)m.rank * w.G * 2 * kWsCand;
     w.subg = m.wssub;
-    w.aux = m.wssub + (size_t)w.blocks * ws_q * ws_q;
+    w.aux = m.wssub + (size_t)w.blocks * w.q_max * w.q_max;
     if (w.blocks > 1) {
       m.wsdfs = dmalloc<float>((size_t)m.nl, &m.bytes);
       m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
@@ -690,7 +708,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       w.xtimeout_ticks = (int64_t)(std::max(1e-6, m.p.xch_timeout_s) * 1e8);
     }
     if (w.cache && !m.replicated) {
-      const int64_t rows = (int64_t)w.blocks * ws_q;  // the round's misses at most
+      const int64_t rows = std::max<int64_t>((int64_t)w.blocks * w.q_max, ws_q);  // the round's misses at most
       m.wsxq = dmalloc<float>((size_t)rows * m.dp, &m.bytes);
       m.wsxqsq = dmalloc<float>((size_t)rows, &m.bytes);
       m.wsiota = dmalloc<int32_t>((size_t)rows, &m.bytes);
