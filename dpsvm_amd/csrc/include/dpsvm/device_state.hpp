@@ -252,7 +252,8 @@ constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..
 // candidates.  ~10^5 dependent pair steps then cost an LDS round trip each
 // instead of a grid-wide exchange.
 constexpr int kWsMax = 192;          // working-set capacity: q x q fp32 sub-Gram in LDS (147 KiB)
-constexpr int kWsCand = 4;           // candidates per side per selection workgroup
+constexpr int kWsCand = 8;           // candidates per side per selection workgroup (list capacity)
+constexpr int kWsCand1 = 4;          // ... of them read by the one-block merge and the peer exchange
 constexpr int kWsSelThreads = 256;   // selection / f-update workgroup
 constexpr int kWsMaxGroups = 256;    // selection workgroups per rank
 constexpr int kWsListsPerThread = 4; // candidate lists a merge thread folds into one (<= 1024 lists over ranks)
@@ -263,9 +264,9 @@ constexpr int64_t kWsAutoRows = 50000;   // solver auto: working-set engines fro
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor
 // t = min(1, g'd / d'Qd) of the dual (smo_ws.hip "multi-block rounds")
-constexpr int kWsMaxBlocks = 16;                  // blocks per round (P x q_max <= kWsMaxAll)
-constexpr int kWsAutoBlocks = 16;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
-constexpr int kWsMaxAll = 8 * kWsMax;             // union capacity (1536 rows)
+constexpr int kWsMaxBlocks = 32;                  // blocks per round (P x q_max <= kWsMaxAll)
+constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
+constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: the top 1536 of each side)
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
 
@@ -341,7 +342,7 @@ struct WsArgs {
   uint64_t* stamps;    // DPSVM_STAMPS diagnostics: s_memrealtime per phase, ring of kStampRing rounds
   // in-kernel peer exchange of the rounds (world > 1; nullptr: the communicator's
   // collectives).  Every rank's receive buffer (uncached, IPC-mapped by its
-  // peers; smo_ws.hip "peer exchange"): [2 parity][G_all][2 kWsCand][2] candidate
+  // peers; smo_ws.hip "peer exchange"): [2 parity][G_all][2 kWsCand1][2] candidate
   // granules, then from word xsub [2 parity][q_max][q_max + 1] sub-Gram rows with
   // the row's f in the last column
   uint64_t* const* xpeer;
@@ -362,7 +363,7 @@ struct WsArgs {
 };
 // u64 words of the working-set exchange region (both parities)
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {
-  return 2 * G_all * 4 * kWsCand + 2 * q_max * (q_max + 1);
+  return 2 * G_all * 4 * kWsCand1 + 2 * q_max * (q_max + 1);
 }
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;

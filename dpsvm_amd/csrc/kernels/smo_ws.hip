@@ -41,7 +41,7 @@ namespace dpsvm {
 namespace dev {
 
 constexpr int kWsGatherThreads = 256;
-constexpr int kWsMaxCand = kWsMaxGroups * kWsCand;  // per side
+constexpr int kWsMaxCand = kWsMaxGroups * kWsCand1;  // per side, one-block merge
 constexpr int kWsHash = 1024;                        // LDS hash slots per side (load factor <= 0.19)
 
 // Phase stamps (DPSVM_STAMPS), ring slot = round: ws_gather workgroup 0
@@ -229,7 +229,7 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
 // launch and no host step).  Round R = c->outer uses parity R & 1 and granule
 // tag xtag(R + 1) (xch.hpp: 16-bit tag << 48 | 48-bit payload, one aligned
 // 8-byte system-scope store — never torn, the data is the flag).  Producers:
-// each ws_select workgroup stores its 2 x kWsCand keys (two granules each: bits
+// each ws_select workgroup stores its 2 x kWsCand1 keys (two granules each: bits
 // 63..16, 15..0) into slot rank * G + b of EVERY rank's buffer; gather workgroup
 // a stores the sub-Gram entries (a, b) of the columns b its rank owns, and the
 // row's f when it owns row a, into row a of every rank's buffer.  Consumers
@@ -243,7 +243,7 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
 // kCommFail on this rank, and its peers time out the same way.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int64_t ws_xcand(const WsArgs& a, int par, int slot) {
-  return ((int64_t)par * a.G_all + slot) * (4 * kWsCand);
+  return ((int64_t)par * a.G_all + slot) * (4 * kWsCand1);
 }
 
 __device__ __forceinline__ int64_t ws_xrow(const WsArgs& a, int par, int row) {
@@ -252,7 +252,7 @@ __device__ __forceinline__ int64_t ws_xrow(const WsArgs& a, int par, int row) {
 
 __device__ __forceinline__ bool ws_tag_ok(uint64_t g, uint64_t t) { return (g >> 48) == (t >> 48); }
 
-// a <- the kWsCand smallest of the two ascending lists a, b (unique keys):
+// a <- the kWsCand1 smallest of the two ascending lists a, b (unique keys):
 // min(a[i], b[3 - i]) is a bitonic sequence of the 4 smallest, two
 // compare-exchange stages sort it
 __device__ __forceinline__ void ws_cx(uint64_t& x, uint64_t& y) {
@@ -261,8 +261,8 @@ __device__ __forceinline__ void ws_cx(uint64_t& x, uint64_t& y) {
   y = hi;
 }
 
-__device__ __forceinline__ void ws_top4_merge(uint64_t (&a)[kWsCand], const uint64_t (&b)[kWsCand]) {
-  static_assert(kWsCand == 4, "4-entry bitonic merge");
+__device__ __forceinline__ void ws_top4_merge(uint64_t (&a)[kWsCand1], const uint64_t (&b)[kWsCand1]) {
+  static_assert(kWsCand1 == 4, "4-entry bitonic merge");
 #pragma unroll
   for (int i = 0; i < 4; ++i) a[i] = a[i] < b[3 - i] ? a[i] : b[3 - i];
   ws_cx(a[0], a[2]);
@@ -539,7 +539,9 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
   // wave 0 merges the four lists; the owner of a winner drops it (keys are
   // unique: the global index is in the low bits)
   const int lane = tid & 63, wave = tid >> 6;
-  for (int round = 0; round < kWsCand && part == 0; ++round) {
+  // multi-block merges read kWsCand keys per list, the one-block merge kWsCand1
+  const int nc = a.blocks > 1 ? kWsCand : kWsCand1;
+  for (int round = 0; round < nc && part == 0; ++round) {
     uint64_t mu = kKeyNone, ml = kKeyNone;
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
@@ -561,18 +563,21 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
   __syncthreads();
   if (threadIdx.x < 64) {
     constexpr int W = kWsSelThreads / 64;
-    uint64_t eu = lane < W * kWsCand ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
-    uint64_t el = lane < W * kWsCand ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
+    const bool have = lane < W * kWsCand && lane % kWsCand < nc;  // the waves' nc entries
+    uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
+    uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
     uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
-    uint64_t pu[kWsCand], pl[kWsCand];  // uniform: every lane holds the lists
-    for (int round = 0; round < kWsCand; ++round) {
+    uint64_t pu[kWsCand1], pl[kWsCand1];  // uniform: every lane holds the first kWsCand1
+    for (int round = 0; round < nc; ++round) {
       const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
       if (lane == 0) {
         out[round] = mu;
         out[kWsCand + round] = ml;
       }
-      pu[round] = mu;
-      pl[round] = ml;
+      if (round < kWsCand1) {
+        pu[round] = mu;
+        pl[round] = ml;
+      }
       if (eu == mu) eu = kKeyNone;
       if (el == ml) el = kKeyNone;
     }
@@ -580,11 +585,11 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
       uint64_t* dst = a.xpeer[lane] + ws_xcand(a, (int)(c->outer & 1), a.xrank * a.G + blockIdx.x);
       const uint64_t t = xtag((uint32_t)c->outer + 1u);
 #pragma unroll
-      for (int r = 0; r < kWsCand; ++r) {
+      for (int r = 0; r < kWsCand1; ++r) {
         xch_store<true>(dst + 2 * r, t | (pu[r] >> 16));
         xch_store<true>(dst + 2 * r + 1, t | (pu[r] & 0xffffull));
-        xch_store<true>(dst + 2 * kWsCand + 2 * r, t | (pl[r] >> 16));
-        xch_store<true>(dst + 2 * kWsCand + 2 * r + 1, t | (pl[r] & 0xffffull));
+        xch_store<true>(dst + 2 * kWsCand1 + 2 * r, t | (pl[r] >> 16));
+        xch_store<true>(dst + 2 * kWsCand1 + 2 * r + 1, t | (pl[r] & 0xffffull));
       }
     }
   }
@@ -627,32 +632,32 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   // ---- every candidate list in registers: thread t holds lists t, t + 256,
   // ... (up to kWsListsPerThread, merged to one sorted top-kWsCand list per side:
   // the same as one selection workgroup over their rows) ----
-  uint64_t lu[kWsCand], ll[kWsCand];
+  uint64_t lu[kWsCand1], ll[kWsCand1];
 #pragma unroll
-  for (int r = 0; r < kWsCand; ++r) lu[r] = ll[r] = kKeyNone;
+  for (int r = 0; r < kWsCand1; ++r) lu[r] = ll[r] = kKeyNone;
   bool ok = true;
   const uint64_t xt = xtag((uint32_t)r_now + 1u);
   for (int j = 0; j < kWsListsPerThread; ++j) {
     const int slot = tid + j * kWsGatherThreads;
     if (slot >= G) break;
-    uint64_t cu[kWsCand], cl[kWsCand];
+    uint64_t cu[kWsCand1], cl[kWsCand1];
     if (a.xpeer == nullptr) {
 #pragma unroll
-      for (int r = 0; r < kWsCand; ++r) {
+      for (int r = 0; r < kWsCand1; ++r) {
         cu[r] = a.cand[(size_t)slot * 2 * kWsCand + r];
         cl[r] = a.cand[(size_t)slot * 2 * kWsCand + kWsCand + r];
       }
     } else {
       // peer exchange: poll slot `slot` of this rank's buffer
       const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, slot);
-      uint64_t g[4 * kWsCand];
+      uint64_t g[4 * kWsCand1];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (true) {
 #pragma unroll
-        for (int i = 0; i < 4 * kWsCand; ++i) g[i] = xch_load<true>(e + i);
+        for (int i = 0; i < 4 * kWsCand1; ++i) g[i] = xch_load<true>(e + i);
         bool all = true;
 #pragma unroll
-        for (int i = 0; i < 4 * kWsCand; ++i) all &= ws_tag_ok(g[i], xt);
+        for (int i = 0; i < 4 * kWsCand1; ++i) all &= ws_tag_ok(g[i], xt);
         if (all) break;
         if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
           ok = false;
@@ -662,14 +667,14 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
       }
       constexpr uint64_t m48 = (1ull << 48) - 1;
 #pragma unroll
-      for (int r = 0; r < kWsCand; ++r) {
+      for (int r = 0; r < kWsCand1; ++r) {
         cu[r] = ((g[2 * r] & m48) << 16) | (g[2 * r + 1] & 0xffffull);
-        cl[r] = ((g[2 * kWsCand + 2 * r] & m48) << 16) | (g[2 * kWsCand + 2 * r + 1] & 0xffffull);
+        cl[r] = ((g[2 * kWsCand1 + 2 * r] & m48) << 16) | (g[2 * kWsCand1 + 2 * r + 1] & 0xffffull);
       }
     }
     if (j == 0) {
 #pragma unroll
-      for (int r = 0; r < kWsCand; ++r) {
+      for (int r = 0; r < kWsCand1; ++r) {
         lu[r] = cu[r];
         ll[r] = cl[r];
       }
@@ -713,11 +718,11 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   // so a cut only ever drops rows of the boundary class. ----
   const int half = (want + 1) / 2;
   const int Gl = min(G, kWsGatherThreads);  // lists held (one merged list per thread)
-  const int d = min(kWsCand - 1, (half + Gl - 1) / Gl - 1);
+  const int d = min(kWsCand1 - 1, (half + Gl - 1) / Gl - 1);
   const int m = (half + d) / (d + 1);
   uint64_t hd[2] = {lu[0], ll[0]};
 #pragma unroll
-  for (int r = 1; r < kWsCand; ++r) {
+  for (int r = 1; r < kWsCand1; ++r) {
     hd[0] = r == d ? lu[r] : hd[0];
     hd[1] = r == d ? ll[r] : hd[1];
   }
@@ -763,7 +768,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
 #pragma unroll
   for (int sd = 0; sd < 2; ++sd) {
 #pragma unroll
-    for (int r = 0; r < kWsCand; ++r) {
+    for (int r = 0; r < kWsCand1; ++r) {
       const uint64_t k = sd ? ll[r] : lu[r];
       if (k == kKeyNone || k == gmin[sd]) continue;
       const uint32_t pre = (uint32_t)(k >> 48);
@@ -780,7 +785,7 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
     int oA = 1 + (int)((pofs >> (24 * sd)) & 4095), oB = 1 + totA + (int)((pofs >> (24 * sd + 12)) & 4095);
     S[sd] = 1 + totA + totB;
 #pragma unroll
-    for (int r = 0; r < kWsCand; ++r) {
+    for (int r = 0; r < kWsCand1; ++r) {
       const uint64_t k = sd ? ll[r] : lu[r];
       if (k == kKeyNone) continue;
       if (k == gmin[sd]) {
@@ -1096,15 +1101,15 @@ __device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
   return off + pre;
 }
 
-// ONE workgroup: every candidate key of both sides sorted (bitonic, 1024 per
-// side), the stop test, then the union: up rank r / low rank r interleaved
-// (most violating first, a row's first position wins), then the newest rows
-// of the previous union.  Union position i goes to block ((i / 2) mod P): each
-// block gets up / low pairs, block 0 the global extremes (so a round always
-// holds the maximal violating pair and makes progress).
-constexpr int kMH = 2048;  // merge hash slots per side (load <= 0.28)
-constexpr int kWsWindowMulti = 4096;  // cache mode: CLOCK victim window of the multi-block merge
-__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 21; }
+// ONE workgroup: every candidate key of both sides sorted (bitonic, 2048 per
+// side, two per thread), the stop test, then the union: up rank r / low rank r
+// interleaved (most violating first, a row's first position wins), then the
+// newest rows of the previous union.  Union position i goes to block
+// ((i / 2) mod P): each block gets up / low pairs, block 0 the global extremes
+// (so a round always holds the maximal violating pair and makes progress).
+constexpr int kMH = 4096;  // merge hash slots per side (load <= 0.38)
+constexpr int kWsWindowMulti = 8192;  // cache mode: CLOCK victim window of the multi-block merge
+__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 20; }
 __device__ __forceinline__ void mh_insert(int32_t* keys, int32_t* vals, int32_t idx, int32_t v) {
   uint32_t h = mh_hash(idx);
   while (true) {
@@ -1128,14 +1133,17 @@ __device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* v
 }
 
 __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
+  constexpr int T = kWsMergeThreads;
   constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
-  static_assert(NK == kWsMergeThreads, "one key per thread and side");
-  static_assert(kWsMaxAll <= 2 * kWsMergeThreads, "previous union: two rows per thread");
+  constexpr int U = kWsMaxAll / T;            // previous-union rows per thread
+  static_assert(NK == 2 * T, "two keys per thread and side: elements tid and tid + T");
+  static_assert(kWsMaxAll % T == 0 && U <= 3, "previous union: <= 3 rows per thread (scan counts <= 3)");
+  static_assert(kMH >= kWsMaxAll && kWsWindowMulti == 8 * T, "cache-mode aliases of the hash tables / sort keys");
   __shared__ uint64_t s_k[2][NK];
   __shared__ int32_t s_hash[4][kMH];
   __shared__ int32_t s_keep[kWsMaxAll + 2];
   __shared__ int32_t s_idx[kWsMaxAll];
-  __shared__ int s_wsum[kWsMergeThreads / 64];
+  __shared__ int s_wsum[T / 64];
   __shared__ int s_qb[kWsMaxBlocks];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x;
@@ -1150,44 +1158,69 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   const int P = max(1, min(c->p_act, a.blocks)), Qmax = P * a.q_max;
   const int q_prev = c->uq[par ^ 1];
   const int want = q_prev == 0 ? Qmax : min(P * a.n_new, Qmax);
-  // the previous union, newest first: thread t holds rows 2t, 2t + 1
-  const int32_t pidx0 = 2 * tid < q_prev ? c->uidx[par ^ 1][2 * tid] : -1;
-  const int32_t pidx1 = 2 * tid + 1 < q_prev ? c->uidx[par ^ 1][2 * tid + 1] : -1;
-  // key t of each side in thread t's registers (list t / 4, rank t % 4)
-  uint64_t v0, v1;
-  {
-    const int l = tid / kWsCand, r = tid % kWsCand;
-    v0 = l < G ? a.cand[(size_t)l * 2 * kWsCand + r] : kKeyNone;
-    v1 = l < G ? a.cand[(size_t)l * 2 * kWsCand + kWsCand + r] : kKeyNone;
+  // the previous union, newest first: thread t holds rows U t .. U t + U - 1
+  int32_t pidx[U];
+#pragma unroll
+  for (int h = 0; h < U; ++h) pidx[h] = U * tid + h < q_prev ? c->uidx[par ^ 1][U * tid + h] : -1;
+  // keys e = tid and e = tid + T of each side (list e / kWsCand, rank e % kWsCand)
+  uint64_t v[2][2];  // [side][element]
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T, l = e / kWsCand, r = e % kWsCand;
+    v[0][x] = l < G ? a.cand[(size_t)l * 2 * kWsCand + r] : kKeyNone;
+    v[1][x] = l < G ? a.cand[(size_t)l * 2 * kWsCand + kWsCand + r] : kKeyNone;
   }
   if (tid < kWsMaxBlocks) s_qb[tid] = 0;
-  for (int t = tid; t < 4 * kMH; t += kWsMergeThreads) (&s_hash[0][0])[t] = -1;
+  for (int t = tid; t < 4 * kMH; t += T) (&s_hash[0][0])[t] = -1;
   if (lead) WS_STAMP(20);
-  // bitonic sort of both sides, element e in thread e: partner distances < 64
-  // exchange by wave shuffles (no barrier: 45 of the 55 stages), the others
-  // through LDS
+  // bitonic sort of both sides over NK = 2T elements: partner e ^ j lives in
+  // the same half (thread tid ^ j) for j < T — wave shuffles below 64, LDS
+  // above — and in the same thread for j == T
   for (int k = 2; k <= NK; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      uint64_t p0, p1;
-      if (j >= 64) {
-        s_k[0][tid] = v0;
-        s_k[1][tid] = v1;
+      uint64_t p[2][2];
+      if (j == T) {
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          p[sd][0] = v[sd][1];
+          p[sd][1] = v[sd][0];
+        }
+      } else if (j >= 64) {
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          s_k[sd][tid] = v[sd][0];
+          s_k[sd][tid + T] = v[sd][1];
+        }
         __syncthreads();
-        p0 = s_k[0][tid ^ j];
-        p1 = s_k[1][tid ^ j];
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          p[sd][0] = s_k[sd][tid ^ j];
+          p[sd][1] = s_k[sd][(tid ^ j) + T];
+        }
         __syncthreads();
       } else {
-        p0 = __shfl_xor(v0, j);
-        p1 = __shfl_xor(v1, j);
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          p[sd][0] = __shfl_xor(v[sd][0], j);
+          p[sd][1] = __shfl_xor(v[sd][1], j);
+        }
       }
-      const bool keep_min = ((tid & k) == 0) == ((tid & j) == 0);
-      v0 = keep_min ? (p0 < v0 ? p0 : v0) : (p0 > v0 ? p0 : v0);
-      v1 = keep_min ? (p1 < v1 ? p1 : v1) : (p1 > v1 ? p1 : v1);
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int e = tid + x * T;
+        const bool keep_min = ((e & k) == 0) == ((e & j) == 0);
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd)
+          v[sd][x] = keep_min ? (p[sd][x] < v[sd][x] ? p[sd][x] : v[sd][x]) : (p[sd][x] > v[sd][x] ? p[sd][x] : v[sd][x]);
+      }
     }
     if (k == 64 && lead) WS_STAMP(21);
   }
-  s_k[0][tid] = v0;
-  s_k[1][tid] = v1;
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+    s_k[sd][tid] = v[sd][0];
+    s_k[sd][tid + T] = v[sd][1];
+  }
   __syncthreads();
   if (lead) WS_STAMP(11);
   const uint64_t gu = s_k[0][0], gl = s_k[1][0];
@@ -1213,50 +1246,77 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   int32_t* hv_u = s_hash[1];
   int32_t* hk_l = s_hash[2];
   int32_t* hv_l = s_hash[3];
-  const int half = (want + 1) / 2;
-  const uint64_t ku = tid < half ? v0 : kKeyNone, kl = tid < half ? v1 : kKeyNone;
-  if (ku != kKeyNone) mh_insert(hk_u, hv_u, (int32_t)key_index(ku), tid);
-  if (kl != kKeyNone) mh_insert(hk_l, hv_l, (int32_t)key_index(kl), tid);
+  const int half = (want + 1) / 2;  // <= kWsMaxAll / 2 = T + T / 2 ranks per side
+  uint64_t ku[2], kl[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T;
+    ku[x] = e < half ? v[0][x] : kKeyNone;
+    kl[x] = e < half ? v[1][x] : kKeyNone;
+    if (ku[x] != kKeyNone) mh_insert(hk_u, hv_u, (int32_t)key_index(ku[x]), e);
+    if (kl[x] != kKeyNone) mh_insert(hk_l, hv_l, (int32_t)key_index(kl[x]), e);
+  }
   __syncthreads();
   if (lead) WS_STAMP(12);
-  bool kp0 = false, kp1 = false;
-  if (ku != kKeyNone) {
-    const int rl = mh_find(hk_l, hv_l, (int32_t)key_index(ku));
-    kp0 = !(rl >= 0 && rl < tid);
+  // rank e keeps its up row unless the low side has it at a smaller rank, its
+  // low row unless the up side has it at a rank <= e (the up copy comes first)
+  bool kpu[2] = {false, false}, kpl[2] = {false, false};
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T;
+    if (ku[x] != kKeyNone) {
+      const int rl = mh_find(hk_l, hv_l, (int32_t)key_index(ku[x]));
+      kpu[x] = !(rl >= 0 && rl < e);
+    }
+    if (kl[x] != kKeyNone) {
+      const int ru = mh_find(hk_u, hv_u, (int32_t)key_index(kl[x]));
+      kpl[x] = !(ru >= 0 && ru <= e);
+    }
   }
-  if (kl != kKeyNone) {
-    const int ru = mh_find(hk_u, hv_u, (int32_t)key_index(kl));
-    kp1 = !(ru >= 0 && ru <= tid);
-  }
-  int kept = 0;
-  const int slot0 = block_scan_merge((int)kp0 + (int)kp1, s_wsum, &kept);
+  // union order: ranks 0 .. T - 1 (element 0 of threads in order), then ranks
+  // T .. (element 1): two scans
+  int tot0 = 0, tot1 = 0;
+  const int slot0 = block_scan_merge((int)kpu[0] + (int)kpl[0], s_wsum, &tot0);
+  const int slot1 = tot0 + block_scan_merge((int)kpu[1] + (int)kpl[1], s_wsum, &tot1);
+  const int kept = tot0 + tot1;
   const int n_chosen = min(kept, want);
-  if (tid < half) {
-    const int s0 = slot0, s1 = slot0 + (int)kp0;
-    const bool c0 = kp0 && s0 < want, c1 = kp1 && s1 < want;
-    s_keep[2 * tid] = c0 ? s0 : -1;
-    s_keep[2 * tid + 1] = c1 ? s1 : -1;
-    if (c0) s_idx[s0] = (int32_t)key_index(ku);
-    if (c1) s_idx[s1] = (int32_t)key_index(kl);
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T;
+    if (e < half) {
+      const int su = x == 0 ? slot0 : slot1, sl = su + (int)kpu[x];
+      const bool cu = kpu[x] && su < want, cl = kpl[x] && sl < want;
+      s_keep[2 * e] = cu ? su : -1;
+      s_keep[2 * e + 1] = cl ? sl : -1;
+      if (cu) s_idx[su] = (int32_t)key_index(ku[x]);
+      if (cl) s_idx[sl] = (int32_t)key_index(kl[x]);
+    }
   }
   __syncthreads();
   if (lead) WS_STAMP(13);
   // previous-union rows not chosen again keep their order after the new rows
   // (uniform skip when the new rows already fill the union)
-  bool pk0 = false, pk1 = false;
-  if (n_chosen < Qmax && pidx0 >= 0) {
-    const int ru = mh_find(hk_u, hv_u, pidx0), rl = mh_find(hk_l, hv_l, pidx0);
-    pk0 = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
-  }
-  if (n_chosen < Qmax && pidx1 >= 0) {
-    const int ru = mh_find(hk_u, hv_u, pidx1), rl = mh_find(hk_l, hv_l, pidx1);
-    pk1 = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+  bool pk[U];
+  int npk = 0;
+#pragma unroll
+  for (int h = 0; h < U; ++h) {
+    pk[h] = false;
+    if (n_chosen < Qmax && pidx[h] >= 0) {
+      const int ru = mh_find(hk_u, hv_u, pidx[h]), rl = mh_find(hk_l, hv_l, pidx[h]);
+      pk[h] = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+    }
+    npk += (int)pk[h];
   }
   int ptotal = 0;
   if (n_chosen < Qmax) {  // uniform
-    const int pslot = block_scan_merge((int)pk0 + (int)pk1, s_wsum, &ptotal);
-    if (pk0 && n_chosen + pslot < Qmax) s_idx[n_chosen + pslot] = pidx0;
-    if (pk1 && n_chosen + pslot + (int)pk0 < Qmax) s_idx[n_chosen + pslot + (int)pk0] = pidx1;
+    int at = n_chosen + block_scan_merge(npk, s_wsum, &ptotal);
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      if (pk[h]) {
+        if (at < Qmax) s_idx[at] = pidx[h];
+        ++at;
+      }
+    }
   }
   const int Q = min(Qmax, n_chosen + ptotal);
   __syncthreads();
@@ -1268,17 +1328,18 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     // while the round uses them); all misses at once (prefix scans), their
     // rows computed next by one row GEMM.  Setup guarantees
     // L >= 2 Qmax + kWsWindowMulti, so the window holds >= n_miss free lines. ----
-    int32_t* s_pin = (int32_t*)&s_k[0][0];  // the sort keys are dead: 4096 words
-    int32_t* s_victim = s_hash[0];         // the hash tables too: 2 x 2048 words
+    int32_t* s_pin = (int32_t*)&s_k[0][0];  // the sort keys are dead: 8192 words
+    int32_t* s_victim = s_hash[0];         // the hash tables too: kMH words each
     int32_t* s_line = s_hash[1];
     const int L = a.L, hand = c->hand;
     const int W = min(L, kWsWindowMulti);
-    for (int w = tid; w < kWsWindowMulti; w += kWsMergeThreads) s_pin[w] = 0;
+    for (int w = tid; w < kWsWindowMulti; w += T) s_pin[w] = 0;
     __syncthreads();
-    int32_t ln[2] = {-1, -1};
+    int32_t ln[U];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int u = tid + h * kWsMergeThreads;
+    for (int h = 0; h < U; ++h) {
+      ln[h] = -1;
+      const int u = tid + h * T;
       if (u < Q) {
         ln[h] = a.slot_of[s_idx[u]];
         if (ln[h] >= 0) {
@@ -1288,12 +1349,18 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
       }
     }
     __syncthreads();
-    const bool m0 = tid < Q && ln[0] < 0, m1 = tid + kWsMergeThreads < Q && ln[1] < 0;
-    int n_miss = 0;
-    const int mrank = block_scan_merge<2>((int)m0 + (int)m1, s_wsum, &n_miss);
-    // free window slots 4t .. 4t + 3 in window order
-    constexpr int SPT = kWsWindowMulti / kWsMergeThreads;
-    static_assert(SPT == 4, "four window slots per merge thread");
+    // misses in union order: element h of every thread is union row tid + h T,
+    // so one scan per h
+    int mrank[U], n_miss = 0;
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      const bool mh = tid + h * T < Q && ln[h] < 0;
+      int tot = 0;
+      mrank[h] = n_miss + block_scan_merge<1>((int)mh, s_wsum, &tot);
+      n_miss += tot;
+    }
+    // free window slots SPT t .. SPT t + SPT - 1 in window order
+    constexpr int SPT = kWsWindowMulti / T;
     bool fr[SPT];
     int nf = 0;
 #pragma unroll
@@ -1302,7 +1369,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
       nf += (int)fr[k];
     }
     int n_free = 0;
-    const int frank = block_scan_merge<3>(nf, s_wsum, &n_free);
+    const int frank = block_scan_merge<4>(nf, s_wsum, &n_free);
     int at = frank, last_used = -1;
 #pragma unroll
     for (int k = 0; k < SPT; ++k) {
@@ -1317,19 +1384,19 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     __syncthreads();
     if (last_used >= 0 && frank < n_miss && at >= n_miss) c->hand = (hand + last_used + 1) % L;  // the last victim
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int u = tid + h * kWsMergeThreads;
+    for (int h = 0; h < U; ++h) {
+      const int u = tid + h * T;
       if (u < Q && ln[h] < 0) {
-        const int r = mrank + (h == 1 ? (int)m0 : 0);
+        const int r = mrank[h];
         const int32_t row = s_idx[u];
-        const int32_t v = s_victim[r];
-        const int32_t old = a.key_of[v];
+        const int32_t vl = s_victim[r];
+        const int32_t old = a.key_of[vl];
         if (old >= 0) a.slot_of[old] = -1;  // evicted (never a member: members' lines are pinned)
-        a.key_of[v] = row;
-        a.slot_of[row] = v;
+        a.key_of[vl] = row;
+        a.slot_of[row] = vl;
         c->miss_row[r] = row;
-        c->miss_line[r] = v;
-        ln[h] = v;
+        c->miss_line[r] = vl;
+        ln[h] = vl;
       }
       if (u < Q) s_line[u] = ln[h];
     }
@@ -1340,7 +1407,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     }
     __syncthreads();
   }
-  for (int u = tid; u < Q; u += kWsMergeThreads) {
+  for (int u = tid; u < Q; u += T) {
     const int32_t row = s_idx[u];
     c->uidx[par][u] = row;
     const int pi = u >> 1, b = pi % P, la = 2 * (pi / P) + (u & 1);
@@ -1359,6 +1426,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     WS_STAMP(2);
   }
 }
+
 
 // P x q_max workgroups: workgroup p q_max + a gathers row a of block p's
 // sub-Gram (block p's columns) and the row's f / alpha / y

@@ -704,7 +704,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     if (m.xch) {
       w.xpeer = m.xpeer_d;
       w.xrank = m.rank;
-      w.xsub = 2 * (int64_t)w.G_all * 4 * kWsCand;
+      w.xsub = 2 * (int64_t)w.G_all * 4 * kWsCand1;
       w.xtimeout_ticks = (int64_t)(std::max(1e-6, m.p.xch_timeout_s) * 1e8);
     }
     if (w.cache && !m.replicated) {

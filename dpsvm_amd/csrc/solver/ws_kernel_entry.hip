@@ -67,7 +67,7 @@ WsMergeProbe ws_merge_multi_probe(const std::vector<uint64_t>& cand, int G, int 
                                   int n_new, float eps, const std::vector<int32_t>& prev_union, int64_t iter,
                                   int64_t max_iter) {
   DPSVM_CHECK(G >= 1 && G <= kWsMaxGroups && (int64_t)cand.size() == (int64_t)G * 2 * kWsCand,
-              "ws_merge_multi_probe: cand must be [G][2][4] with G <= 256");
+              "ws_merge_multi_probe: cand must be [G][2][kWsCand = 8] with G <= 256");
   DPSVM_CHECK(blocks >= 2 && blocks <= kWsMaxBlocks && q_max >= 2 && q_max <= kWsMax && q_max % 2 == 0,
               "ws_merge_multi_probe: 2 <= blocks <= 16, even q_max <= 192");
   DPSVM_CHECK((int64_t)prev_union.size() <= (int64_t)blocks * q_max, "ws_merge_multi_probe: previous union too long");

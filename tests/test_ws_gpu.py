@@ -494,21 +494,21 @@ def test_ws_adaptive_blocks_fall_back_to_one_block_rounds(clip):
 @pytest.mark.parametrize("clip", ["independent", "box"])
 def test_ws_cache_multi_block_bit_identical_to_resident_gram(clip):
     """Multi-block rounds on the kernel-row cache: the union's lines come from
-    a 4096-line CLOCK window (misses computed by one row GEMM per round).  The
+    an 8192-line CLOCK window (misses computed by one row GEMM per round).  The
     K values and the round arithmetic are the dense engine's, so the trajectory
     — including the adaptive block count — is bit-identical to ws-dense with the
     same blocks, with a cache small enough to evict."""
-    X, y = synthetic("mnist", n=9000, seed=12)
+    X, y = synthetic("mnist", n=14000, seed=12)
     kw = dict(C=10.0, gamma=0.25, eps=1e-3, clip=clip, device="cuda", solver="ws", ws_blocks=4, ws_size=64)
     dense = SVC(**kw).fit(X, y)
-    cache = SVC(force_cache=True, cache_lines=4700, **kw).fit(X, y)
+    cache = SVC(force_cache=True, cache_lines=9000, **kw).fit(X, y)
     assert dense.setup_info_["iteration"] == "ws-dense" and cache.setup_info_["iteration"] == "ws-cache"
     assert "ws_blocks" not in cache.setup_info_.get("engine_note", "")
     assert cache.stats_["ws_blocks"] == 4
     assert cache.converged_ and cache.n_iter_ == dense.n_iter_ and cache.n_rounds_ == dense.n_rounds_
     assert np.array_equal(cache.alpha_, dense.alpha_) and cache.b_ == dense.b_
     assert cache.stats_["ws_blocks_end"] == dense.stats_["ws_blocks_end"]
-    assert cache.stats_["rows_computed"] > 4700  # more rows than lines: evictions happened
+    assert cache.stats_["rows_computed"] > 9000  # more rows than lines: evictions happened
 
 
 @pytest.mark.parametrize("clip", ["box", "independent"])

@@ -14,6 +14,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 NONE = np.uint64((1 << 64) - 1)
+KC = 8   # candidates per side per selection workgroup (device_state.hpp kWsCand)
+KC1 = 4  # ... produced for (and read by) the one-block rounds (kWsCand1)
 
 
 @pytest.fixture(scope="module")
@@ -55,7 +57,7 @@ def in_low(a, y, C):
 
 # ---------------------------------------------------------------- merge
 def merge_model(cand, blocks, p_act, q_max, n_new, eps, prev):
-    c = np.asarray(cand, dtype=np.uint64).reshape(-1, 2, 4)
+    c = np.asarray(cand, dtype=np.uint64).reshape(-1, 2, KC)
     up, low = np.sort(c[:, 0, :].ravel()), np.sort(c[:, 1, :].ravel())
     b_hi, b_lo = key_value(up[0])[()], -key_value(low[0])[()]
     if up[0] == NONE or low[0] == NONE:
@@ -91,7 +93,7 @@ def merge_model(cand, blocks, p_act, q_max, n_new, eps, prev):
 
 
 def crafted_candidates(rng, G, n_rows, ties=True):
-    """G lists of up to 4 keys per side: rows are free (both sides), up-only or
+    """G lists of up to KC keys per side: rows are free (both sides), up-only or
     low-only; several rows share f values (ties break by index)."""
     rows = rng.choice(200000, size=n_rows, replace=False)
     f = rng.normal(size=n_rows).astype(np.float32)
@@ -99,11 +101,11 @@ def crafted_candidates(rng, G, n_rows, ties=True):
         f[: n_rows // 10] = f[0]
     kind = rng.integers(0, 3, size=n_rows)  # 0 free, 1 up only, 2 low only
     owner = rng.integers(0, G, size=n_rows)
-    cand = np.full((G, 2, 4), NONE, dtype=np.uint64)
+    cand = np.full((G, 2, KC), NONE, dtype=np.uint64)
     for g in range(G):
         sel = np.nonzero(owner == g)[0]
-        ups = np.sort(make_key(f[sel][kind[sel] != 2], rows[sel][kind[sel] != 2]))[:4]
-        lows = np.sort(make_key(-f[sel][kind[sel] != 1], rows[sel][kind[sel] != 1]))[:4]
+        ups = np.sort(make_key(f[sel][kind[sel] != 2], rows[sel][kind[sel] != 2]))[:KC]
+        lows = np.sort(make_key(-f[sel][kind[sel] != 1], rows[sel][kind[sel] != 1]))[:KC]
         cand[g, 0, : len(ups)] = ups
         cand[g, 1, : len(lows)] = lows
     return cand, rows
@@ -111,11 +113,12 @@ def crafted_candidates(rng, G, n_rows, ties=True):
 
 @pytest.mark.parametrize("G,blocks,p_act,n_prev,n_new", [(256, 8, 8, 0, 192), (256, 8, 4, 300, 96),
                                                         (37, 8, 8, 1000, 192), (200, 4, 1, 150, 144),
-                                                        (256, 2, 2, 64, 40)])
+                                                        (256, 2, 2, 64, 40), (256, 32, 32, 0, 96),
+                                                        (256, 32, 16, 2500, 48), (240, 16, 16, 900, 96)])
 def test_ws_merge_multi_matches_model(K, G, blocks, p_act, n_prev, n_new):
     rng = np.random.default_rng(G * 31 + blocks + p_act + n_prev)
     q_max = 192 if blocks == 8 else 96
-    cand, rows = crafted_candidates(rng, G, 3000)
+    cand, rows = crafted_candidates(rng, G, 3000 if blocks <= 8 else 12000)
     # previous union: half of it rows the merge picks again (dropped from the
     # retained tail), half rows it does not
     prev = np.concatenate([rng.choice(rows, size=n_prev // 2, replace=False),
@@ -140,9 +143,10 @@ def test_ws_merge_multi_stop_test_and_empty_side(K):
     cand, _ = crafted_candidates(rng, 16, 200, ties=False)
     up_min = key_value(np.sort(cand[:, 0, :].ravel())[0])[()]
     # every low key at -(b_hi + eps): b_lo = b_hi + eps <= b_hi + 2 eps -> converged
-    low = make_key(np.full(16 * 4, -(up_min + np.float32(1e-3)), dtype=np.float32), np.arange(10**6, 10**6 + 64))
+    low = make_key(np.full(16 * KC, -(up_min + np.float32(1e-3)), dtype=np.float32),
+                   np.arange(10**6, 10**6 + 16 * KC))
     c2 = cand.copy()
-    c2[:, 1, :] = np.sort(low).reshape(16, 4)
+    c2[:, 1, :] = np.sort(low).reshape(16, KC)
     got = K.ws_merge_multi(c2, 8, 192, 192, 1e-3)
     assert got["done"] == 1 and got["b_hi"] == up_min
     c3 = cand.copy()
@@ -344,16 +348,16 @@ def rbf(X, gamma):
     return np.exp(-gamma * d2)
 
 
-def candidates_model(f, a, y, C, G, rpt):
-    out = np.full((G, 2, 4), NONE, dtype=np.uint64)
+def candidates_model(f, a, y, C, G, rpt, nc=KC):
+    out = np.full((G, 2, nc), NONE, dtype=np.uint64)
     n = len(f)
     for b in range(G):
         lo, hi = b * rpt * 256, min(n, (b + 1) * rpt * 256)
         j = np.arange(lo, hi)
         if len(j) == 0:
             continue
-        u = np.sort(make_key(f[j][in_up(a[j], y[j], C)], j[in_up(a[j], y[j], C)]))[:4]
-        l_ = np.sort(make_key(-f[j][in_low(a[j], y[j], C)], j[in_low(a[j], y[j], C)]))[:4]
+        u = np.sort(make_key(f[j][in_up(a[j], y[j], C)], j[in_up(a[j], y[j], C)]))[:nc]
+        l_ = np.sort(make_key(-f[j][in_low(a[j], y[j], C)], j[in_low(a[j], y[j], C)]))[:nc]
         out[b, 0, : len(u)] = u
         out[b, 1, : len(l_)] = l_
     return out
@@ -436,7 +440,7 @@ def test_ws_select_two_pass_line_search_matches_model(K, target, P, p_act):
     assert got["n_damped"] == int(damped)
     assert got["p_act"] == (min(p_act, max(1, P // 2)) if damped else p_act)
     assert got["p1_round"] == (1 if damped and got["p_act"] == 1 else 0)
-    cand = np.asarray(got["cand"], dtype=np.uint64).reshape(G, 2, 4)
+    cand = np.asarray(got["cand"], dtype=np.uint64).reshape(G, 2, KC)  # multi-block kernels: KC per side
     np.testing.assert_array_equal(cand, candidates_model(got["f"], got["alpha"], y, C, G, rpt))
 
 
@@ -460,8 +464,8 @@ def test_ws_select_one_pass_matches_model(K):
     want_f = f + gram.astype(np.float64).T @ coef.astype(np.float64)
     np.testing.assert_allclose(got["f"], want_f, rtol=1e-5, atol=1e-5)
     np.testing.assert_array_equal(got["alpha"], a)
-    cand = np.asarray(got["cand"], dtype=np.uint64).reshape(G, 2, 4)
-    np.testing.assert_array_equal(cand, candidates_model(got["f"], a, y, C, G, rpt))
+    cand = np.asarray(got["cand"], dtype=np.uint64).reshape(G, 2, KC)[:, :, :KC1]  # one block: KC1 per side
+    np.testing.assert_array_equal(cand, candidates_model(got["f"], a, y, C, G, rpt, nc=KC1))
 
 
 @pytest.mark.parametrize("clip", ["independent", "box"])
