@@ -22,7 +22,8 @@ rank count: tests/test_ws_gpu.py sharded-vs-replicated tests).
 import json
 import sys
 
-PASS1_US = 50.0   # f-update pass 1 at P = 1 (profiles/r2_ws_blocks8_phase_stamps.json: ~50 us)
+PASS1_US = 50.0   # f-update pass 1 at P = 1 when the inputs carry no stamp of it (round-2 value)
+UNION = 3072      # rows per round (device_state.hpp kWsMaxAll); blocks of UNION / P rows, <= 192
 
 
 def main() -> int:
@@ -31,10 +32,11 @@ def main() -> int:
     r = m["round_us"]
     rounds = m["local"]["rounds"]
     blocks = m["local"]["blocks"][0]
-    q = 192
+    q = min(192, UNION // max(1, blocks)) if blocks > 1 else 192
     ar_bytes = blocks * (q * q + 192) * 4
     fixed = r["merge"] + r["gather"] + r["load_subgram"] + r["solve"]
-    rows_part = PASS1_US + r["select_pass2"]
+    pass1 = r.get("pass1_start_to_pass2_start") or PASS1_US
+    rows_part = pass1 + r["select_pass2"]
     gaps = max(0.0, r["period"] - fixed - rows_part)
     print(f"inputs: {path}")
     print(f"  measured: rounds {rounds}, round period {r['period']} us = redundant {fixed:.1f} (merge, gather, "

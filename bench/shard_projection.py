@@ -8,7 +8,8 @@
      RCCL communicator (force_collectives, captured in the round graph): the
      launch cost of the three collectives per round without any transfer;
   3. one rank's Gram slab K(all n rows, n / P owned columns) for P = 1, 2, 4, 8
-     (the non-symmetric MFMA GEMM a sharded rank runs);
+     (the non-symmetric split-operand MFMA GEMM a sharded rank runs, incl. the
+     fp16 split of its operands);
   4. the round anatomy from in-kernel stamps (DPSVM_STAMPS): which phases are
      per-rank redundant (merge, gather, solve) and which scale with n / P (the
      two f-update passes).
@@ -73,12 +74,12 @@ def main() -> int:
     slabs = {}
     for P in (1, 2, 4, 8):
         cols = xt[: (a.samples + P - 1) // P]
-        K.rbf_gram(xt, cols, 0.25)  # warm
+        K.rbf_gram(xt, cols, 0.25, split=True)  # warm
         torch.cuda.synchronize()
         ts = []
         for _ in range(a.reps):
             t0 = time.perf_counter()
-            K.rbf_gram(xt, cols, 0.25)
+            K.rbf_gram(xt, cols, 0.25, split=True)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         slabs[P] = round(min(ts), 6)

@@ -539,8 +539,9 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
   // wave 0 merges the four lists; the owner of a winner drops it (keys are
   // unique: the global index is in the low bits)
   const int lane = tid & 63, wave = tid >> 6;
-  // multi-block merges read kWsCand keys per list, the one-block merge kWsCand1
-  const int nc = a.blocks > 1 ? kWsCand : kWsCand1;
+  // multi-block merges read kWsCand keys per list (MODE 2: every multi-block
+  // round, the seed included), the one-block merge kWsCand1 (MODE 0)
+  constexpr int nc = MODE == 0 ? kWsCand1 : kWsCand;
   for (int round = 0; round < nc && part == 0; ++round) {
     uint64_t mu = kKeyNone, ml = kKeyNone;
 #pragma unroll
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
   __syncthreads();
   if (threadIdx.x < 64) {
     constexpr int W = kWsSelThreads / 64;
-    const bool have = lane < W * kWsCand && lane % kWsCand < nc;  // the waves' nc entries
+    const bool have = lane < W * kWsCand && (nc == kWsCand || lane % kWsCand < nc);  // the waves' nc entries
     uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
     uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
     uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
