@@ -117,23 +117,24 @@ enum SplitEpi { SPLIT_STORE = 0, SPLIT_ROWS = 1 };
 // lane group of the operand reads on 16 distinct bank quads).
 // ABL (diagnostics only, DPSVM_SPLIT_ABLATE): 1 = no global stores (a runtime
 // condition never true, gamma < 0, keeps the epilogue's math), 2 = no mirrored stores
-template <int EPI, int WM, int KB, int ABL = 0>
-__global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
+// WM x WN waves (default 8 waves); a workgroup tile of 32 WM rows x 64 WN columns.
+template <int EPI, int WM, int KB, int ABL = 0, int WN = 8 / WM>
+__global__ __launch_bounds__(64 * WM * WN, 1) void rbf_gemm_split_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
     float gamma, float* __restrict__ out, int64_t ldo, int sym, const int32_t* __restrict__ a_rows,
     const int32_t* __restrict__ out_rows, const int32_t* __restrict__ m_dev) {
-  constexpr int WN = 8 / WM, TM = 32 * WM, TN = 64 * WN, ROWS = TM + TN;
+  constexpr int THREADS = 64 * WM * WN, TM = 32 * WM, TN = 64 * WN, ROWS = TM + TN;
   constexpr int CPR = 8 * KB;                    // 16-B chunks per row and stage
   constexpr int CH = ROWS * CPR;                 // chunks per stage
-  constexpr int NL = CH / kSplitThreads;         // chunks per thread
-  static_assert(CH % kSplitThreads == 0 && (KB == 1 || KB == 2), "whole chunks per thread");
+  constexpr int NL = (CH + THREADS - 1) / THREADS;  // chunks per thread (the last one: a spare LDS slot)
+  static_assert((KB == 1 || KB == 2) && THREADS >= TM, "stage geometry");
   int64_t tx, ty;
   xcd_tile(tx, ty);
   if (EPI == SPLIT_ROWS) M = *m_dev;
   if (EPI == SPLIT_STORE && sym && ty < tx) return;
   if (EPI == SPLIT_ROWS && tx * TM >= M) return;  // uniform: no barrier reached
-  __shared__ u4 lds[2][CH];
+  __shared__ u4 lds[2][CH + 1];  // + a spare slot for the staging remainder
   __shared__ float s_asq[TM];
   __shared__ int32_t s_ash[TM], s_orow[TM];
 
@@ -151,12 +152,13 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
     s_orow[tid] = EPI == SPLIT_ROWS ? (row < M ? out_rows[row] : -1) : 0;
   }
 
-  // staging: chunk id = tid + 512 i -> stage row id / CPR (A rows, then B rows), chunk id % CPR
+  // staging: chunk id = tid + THREADS i -> stage row id / CPR (A rows, then B
+  // rows), chunk id % CPR; ids past the stage load a valid chunk into the spare slot
   const u4* src[NL];
   int dst[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int id = tid + kSplitThreads * i, r = id / CPR, c = id % CPR;
+    const int idr = tid + THREADS * i, spare = idr >= CH, id = spare ? 0 : idr, r = id / CPR, c = id % CPR;
     int64_t grow;
     const u4* base;
     if (r < TM) {
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
       base = B;
     }
     src[i] = base + grow * rstride + c;
-    dst[i] = r * CPR + (c ^ (KB == 1 ? (r >> 1) & 7 : r & 15));
+    dst[i] = spare ? CH : r * CPR + (c ^ (KB == 1 ? (r >> 1) & 7 : r & 15));
   }
   // chunk i of a stage belongs to k block (i % CPR) / 8 of it: the last stage
   // of an odd block count computes its first block only, and its chunks of the
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(kSplitThreads, 1) void rbf_gemm_split_kernel(
   auto load = [&](u4* st, int kt) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      const int blk = ((tid + kSplitThreads * i) % CPR) >> 3;
+      const int blk = ((tid + THREADS * i) % CPR) >> 3;
       const int64_t o = (int64_t)kt * CPR - ((KB > 1 && kt * KB + blk >= nkb) ? 8 : 0);
       st[i] = src[i][o];
     }
@@ -357,9 +359,13 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
                             int64_t N, int dp, float gamma, float* lines, const int32_t* out_rows, int64_t ldl,
                             hipStream_t s) {
   if (M_max <= 0 || N <= 0) return;
-  const int64_t tm = (M_max + 63) / 64, tn = (N + 255) / 256;
+  // 192 x 128 tiles (12 waves): a one-block round's misses (<= 192 rows) are
+  // one tile row, so every column panel of B — all of this rank's rows, the
+  // bytes that bound this GEMM — is read from HBM once per round (64-row
+  // tiles read it once per 64 misses)
+  const int64_t tm = (M_max + 191) / 192, tn = (N + 127) / 128;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed_split: N too large for grid.y");
-  dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 2, 1><<<dim3((unsigned)tm, (unsigned)tn), dev::kSplitThreads, 0, s>>>(
+  dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 6, 1, 0, 2><<<dim3((unsigned)tm, (unsigned)tn), 768, 0, s>>>(
       (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
       a_rows, out_rows, m_dev);
   post_launch("rbf_rows_indexed_split", s);
