@@ -28,7 +28,7 @@ def main() -> int:
     ap.add_argument("--ws-size", type=int, default=192)
     ap.add_argument("--ws-new", type=int, default=0)
     ap.add_argument("--ws-rel", type=float, default=0.3)
-    ap.add_argument("--ws-blocks", type=int, default=1)
+    ap.add_argument("--ws-blocks", type=int, default=0, help="0: the library default (adaptive multi-block)")
     ap.add_argument("--max-iter", type=int, default=10**7)
     ap.add_argument("--cache-lines", type=int, default=0)
     ap.add_argument("--force-cache", action="store_true")
@@ -59,11 +59,12 @@ def main() -> int:
         "select_candidates_us": us(s[:, 7] - s[:, 10]),
         "select_end_to_gather_us": us(s[:, 1] - s[:, 7]),
         "merge_us": us(s[:, 2] - s[:, 1]),
+        **({"rank_and_merge_us": us(s[:, 2] - s[:, 21])} if a.ws_blocks != 1 else {}),
         "merge_phases_us": ({"lists_and_stop_test": us(s[:, 11] - s[:, 1]), "radix_thresholds": us(s[:, 12] - s[:, 11]),
                              "class_compaction": us(s[:, 13] - s[:, 12]), "hash_dedup": us(s[:, 14] - s[:, 13]),
-                             "previous_set": us(s[:, 2] - s[:, 14])} if a.ws_blocks <= 1 else
-                            {"loads_and_hash_init": us(s[:, 20] - s[:, 1]), "sort_k_le_64": us(s[:, 21] - s[:, 20]),
-                             "sort_k_gt_64": us(s[:, 11] - s[:, 21]), "lists_and_sort": us(s[:, 11] - s[:, 1]), "stop_test_hash_insert": us(s[:, 12] - s[:, 11]),
+                             "previous_set": us(s[:, 2] - s[:, 14])} if a.ws_blocks == 1 else
+                            {"rank_kernel_to_merge": us(s[:, 1] - s[:, 21]), "sorted_loads_hash_init": us(s[:, 20] - s[:, 1]),
+                             "to_sorted_keys": us(s[:, 11] - s[:, 1]), "stop_test_hash_insert": us(s[:, 12] - s[:, 11]),
                              "dedup_compaction": us(s[:, 13] - s[:, 12]), "previous_union": us(s[:, 14] - s[:, 13]),
                              "block_assignment": us(s[:, 2] - s[:, 14])}),
         "gather_rows_us": us(s[:, 8] - s[:, 2]),

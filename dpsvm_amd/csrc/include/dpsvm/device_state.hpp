@@ -360,6 +360,7 @@ struct WsArgs {
   int32_t wss;         // sub-problem pair selection: 1 first order (the reference's), 2 second order (WSS2)
   float t_halve;       // multi-block: a round damped to t < t_halve halves the block count
   int32_t clip_fallback;  // multi-block, independent clipping: a clip event drops to one block (1) or not (0)
+  uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
 };
 // u64 words of the working-set exchange region (both parities)
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {

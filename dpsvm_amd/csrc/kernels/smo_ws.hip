@@ -1133,6 +1133,57 @@ __device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* v
   return -1;
 }
 
+// ws_rank: the multi-block merge's sort, spread over a grid of 2 sides x
+// kRankChunks workgroups instead of one workgroup's bitonic network (29 of the
+// merge's 41 us at 3,072-row unions, profiles/r3_ws_stamps_32x96.json).  A
+// key's position in its side's ascending order is the number of keys below it:
+// real keys are unique (the global row index is in the low bits), so these
+// counts are a permutation of [0, n_real); the absent keys (kKeyNone) fill the
+// tail.  Each workgroup holds its side's NK keys in LDS and ranks KPW of them,
+// SUB threads per key each counting over every SUB-th key pair (the SUB lanes of
+// one key read 8 consecutive 16-B pairs: no bank conflict, broadcast over keys).
+constexpr int kRankThreads = 256;
+constexpr int kRankChunks = 64;
+__global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
+  constexpr int NK = kWsMaxGroups * kWsCand;
+  constexpr int KPW = NK / kRankChunks, SUB = kRankThreads / KPW, PAIRS = NK / (2 * SUB);
+  static_assert(NK % kRankChunks == 0 && kRankThreads % KPW == 0 && SUB == 8 && NK % (2 * SUB) == 0, "rank geometry");
+  __shared__ uint64_t s_k[NK];
+  __shared__ int s_real[kRankThreads / 64];
+  const WsCtrl* c = a.ctrl;
+  if (c->done != kRunning) return;
+  const int side = blockIdx.x / kRankChunks, chunk = blockIdx.x % kRankChunks, tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) WS_STAMP(21);
+  const int G = a.G_all;
+  int real = 0;
+  for (int e = tid; e < NK; e += kRankThreads) {
+    const int l = e / kWsCand, r = e % kWsCand;
+    const uint64_t k = l < G ? a.cand[(size_t)l * 2 * kWsCand + side * kWsCand + r] : kKeyNone;
+    s_k[e] = k;
+    real += k != kKeyNone ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) real += __shfl_xor(real, o);
+  if ((tid & 63) == 0) s_real[tid >> 6] = real;
+  __syncthreads();
+  int n_real = 0;
+#pragma unroll
+  for (int w = 0; w < kRankThreads / 64; ++w) n_real += s_real[w];
+  const int e = chunk * KPW + tid / SUB, sub = tid % SUB;
+  const uint64_t k = s_k[e];
+  int cnt = 0;
+#pragma unroll 8
+  for (int i = 0; i < PAIRS; ++i) {
+    const int e2 = 2 * (sub + SUB * i);
+    cnt += (s_k[e2] < k ? 1 : 0) + (s_k[e2 + 1] < k ? 1 : 0);
+  }
+#pragma unroll
+  for (int o = 1; o < SUB; o <<= 1) cnt += __shfl_xor(cnt, o);
+  uint64_t* out = a.sorted + (size_t)side * NK;
+  if (sub == 0 && k != kKeyNone) out[cnt] = k;
+  if (tid < KPW && chunk * KPW + tid >= n_real) out[chunk * KPW + tid] = kKeyNone;
+}
+
 __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
   constexpr int T = kWsMergeThreads;
   constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
@@ -1163,60 +1214,16 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   int32_t pidx[U];
 #pragma unroll
   for (int h = 0; h < U; ++h) pidx[h] = U * tid + h < q_prev ? c->uidx[par ^ 1][U * tid + h] : -1;
-  // keys e = tid and e = tid + T of each side (list e / kWsCand, rank e % kWsCand)
+  // keys e = tid and e = tid + T of each side, in ascending order (ws_rank)
   uint64_t v[2][2];  // [side][element]
 #pragma unroll
   for (int x = 0; x < 2; ++x) {
-    const int e = tid + x * T, l = e / kWsCand, r = e % kWsCand;
-    v[0][x] = l < G ? a.cand[(size_t)l * 2 * kWsCand + r] : kKeyNone;
-    v[1][x] = l < G ? a.cand[(size_t)l * 2 * kWsCand + kWsCand + r] : kKeyNone;
+    v[0][x] = a.sorted[tid + x * T];
+    v[1][x] = a.sorted[NK + tid + x * T];
   }
   if (tid < kWsMaxBlocks) s_qb[tid] = 0;
   for (int t = tid; t < 4 * kMH; t += T) (&s_hash[0][0])[t] = -1;
   if (lead) WS_STAMP(20);
-  // bitonic sort of both sides over NK = 2T elements: partner e ^ j lives in
-  // the same half (thread tid ^ j) for j < T — wave shuffles below 64, LDS
-  // above — and in the same thread for j == T
-  for (int k = 2; k <= NK; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      uint64_t p[2][2];
-      if (j == T) {
-#pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          p[sd][0] = v[sd][1];
-          p[sd][1] = v[sd][0];
-        }
-      } else if (j >= 64) {
-#pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          s_k[sd][tid] = v[sd][0];
-          s_k[sd][tid + T] = v[sd][1];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          p[sd][0] = s_k[sd][tid ^ j];
-          p[sd][1] = s_k[sd][(tid ^ j) + T];
-        }
-        __syncthreads();
-      } else {
-#pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          p[sd][0] = __shfl_xor(v[sd][0], j);
-          p[sd][1] = __shfl_xor(v[sd][1], j);
-        }
-      }
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const int e = tid + x * T;
-        const bool keep_min = ((e & k) == 0) == ((e & j) == 0);
-#pragma unroll
-        for (int sd = 0; sd < 2; ++sd)
-          v[sd][x] = keep_min ? (p[sd][x] < v[sd][x] ? p[sd][x] : v[sd][x]) : (p[sd][x] > v[sd][x] ? p[sd][x] : v[sd][x]);
-      }
-    }
-    if (k == 64 && lead) WS_STAMP(21);
-  }
 #pragma unroll
   for (int sd = 0; sd < 2; ++sd) {
     s_k[sd][tid] = v[sd][0];
@@ -1885,6 +1892,9 @@ void ws_merge_multi(const WsArgs& a, hipStream_t s) {
                   (!a.cache || ws_cache_multi_supported(a.L, a.blocks, a.q_max)),
               "ws_merge_multi: multi-block rounds need the collectives, <= 256 candidate lists, an even q_max and "
               "(cache mode) L >= 2 P q_max + 4096 lines");
+  DPSVM_CHECK(a.sorted != nullptr, "ws_merge_multi: no sort buffer");
+  dev::ws_rank_kernel<<<2 * dev::kRankChunks, dev::kRankThreads, 0, s>>>(a);
+  post_launch("ws_rank", s);
   dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
   post_launch("ws_merge_multi", s);
 }

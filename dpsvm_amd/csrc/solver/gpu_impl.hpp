@@ -100,6 +100,7 @@ struct GpuSolver::Impl {
   float* wsdfs = nullptr;           // multi-block rounds: d_f [nl], d_alpha [n], line-search partials [G][2]
   float* wsdalpha = nullptr;
   double* wspart = nullptr;
+  uint64_t* wssorted = nullptr;     // multi-block merge: candidate keys per side, ascending
   float* wssub = nullptr;          // q_max x q_max sub-Gram + [3][kWsMax] f / alpha / y of the working set
   float *wsxq = nullptr, *wsxqsq = nullptr;  // partitioned X, cache mode: the misses' X rows / norms
   int32_t* wsiota = nullptr;                  //   (their GEMM row indices: 0..q_max-1)

@@ -37,7 +37,7 @@ GpuSolver::Impl::~Impl() {
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
-                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wsdfs, (void*)wsdalpha, (void*)wspart,
+                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wsdfs, (void*)wsdalpha, (void*)wspart, (void*)wssorted,
                     (void*)wsxq, (void*)wsxqsq, (void*)wsiota, xs, (void*)xsh, wsxs, (void*)wsxsh})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
@@ -693,6 +693,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       m.wsdfs = dmalloc<float>((size_t)m.nl, &m.bytes);
       m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
       m.wspart = dmalloc<double>((size_t)2 * w.G_all, &m.bytes);
+      m.wssorted = dmalloc<uint64_t>((size_t)2 * kWsMaxGroups * kWsCand, &m.bytes);
+      w.sorted = m.wssorted;
       HIP_CHECK(hipMemsetAsync(m.wsdalpha, 0, (size_t)n * 4, m.stream));
       w.dfs = m.wsdfs;
       w.dalpha = m.wsdalpha;

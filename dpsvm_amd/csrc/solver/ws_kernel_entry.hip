@@ -92,6 +92,7 @@ WsMergeProbe ws_merge_multi_probe(const std::vector<uint64_t>& cand, int G, int 
   a.eps = eps;
   a.max_iter = max_iter;
   a.ctrl = dc;
+  a.sorted = st.up(std::vector<uint64_t>(), (size_t)2 * kWsMaxGroups * kWsCand);
   launch::ws_merge_multi(a, st.s);
   const WsCtrl o = download(dc, 1, st.s)[0];
   WsMergeProbe r;
