@@ -268,6 +268,7 @@ constexpr int kWsMaxBlocks = 32;                  // blocks per round (P x q_max
 constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
 constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: the top 1536 of each side)
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
+constexpr int kWsMaxPass1Splits = 16;             // multi-block f-update pass 1: list slices over workgroups
 constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
 
 struct alignas(16) WsCtrl {
@@ -360,6 +361,7 @@ struct WsArgs {
   int32_t wss;         // sub-problem pair selection: 1 first order (the reference's), 2 second order (WSS2)
   float t_halve;       // multi-block: a round damped to t < t_halve halves the block count
   int32_t clip_fallback;  // multi-block, independent clipping: a clip event drops to one block (1) or not (0)
+  int32_t ks;          // multi-block pass 1: list slices over workgroups (dfs [ks][nl], part [G_all][ks][2])
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
 };
 // u64 words of the working-set exchange region (both parities)

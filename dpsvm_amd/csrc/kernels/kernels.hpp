@@ -70,6 +70,7 @@ void xch_ping(uint64_t* const* peers, int rank, int world, int64_t ping_off, uin
 // ws_select (f update, next candidates)
 bool ws_supported(int64_t nl_max, int world, int q_max);
 void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt);
+int ws_pass1_splits(int G);  // multi-block pass 1: workgroups per selection group
 void ws_select(const WsArgs& a, hipStream_t s);
 // multi-block rounds: pass 1 (d_f + line-search partials), pass 2 (apply, candidates); at
 // world > 1 the partials are all-gathered between them
@@ -112,6 +113,9 @@ void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, c
 int64_t split_row_u4(int dp);
 int64_t split_pad_rows(int64_t rows);
 void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, int32_t* shift, hipStream_t s);
+// split STORE GEMM variant: 0 auto (persistent when dp > 128), 1 tile per workgroup, 2 persistent
+int split_gemm_variant();
+void set_split_gemm_variant(int v);
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
                           int64_t ldo, hipStream_t s, bool symmetric = false);

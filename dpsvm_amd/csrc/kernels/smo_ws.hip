@@ -310,7 +310,7 @@ __device__ __forceinline__ float ws_line_search(const WsArgs& a, int P) {
   if (P <= 1) return 1.f;
   const int lane = threadIdx.x & 63;
   double q = 0.0, g = 0.0;
-  for (int k = lane; k < a.G_all; k += 64) {  // every rank's partials (all-gathered)
+  for (int k = lane; k < a.G_all * max(1, a.ks); k += 64) {  // every rank's partials (all-gathered)
     q += a.part[2 * k];
     g += a.part[2 * k + 1];
   }
@@ -377,8 +377,13 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
     }
   }
   __syncthreads();
-  // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers
-  const int64_t base = (int64_t)blockIdx.x * a.rpt * kWsSelThreads + tid;
+  // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers.
+  // MODE 1 runs KS = a.ks workgroups per row group, each over its KS-th of the
+  // changed-row list (pass 1 fills the device when G is small: 30 groups per rank at
+  // 8 ranks on the headline); pass 2 sums the KS partial changes in slice order.
+  const int KS = MODE == 1 ? max(1, a.ks) : 1;
+  const int grp = MODE == 1 ? (int)(blockIdx.x % a.G) : (int)blockIdx.x, ksi = MODE == 1 ? (int)(blockIdx.x / a.G) : 0;
+  const int64_t base = (int64_t)grp * a.rpt * kWsSelThreads + tid;
   float f[RPT];
   bool has[RPT];
 #pragma unroll
@@ -392,8 +397,8 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
 #pragma unroll
     for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
     if constexpr (MODE != 2) {
-    const int per = (na + PARTS - 1) / PARTS;
-    const int k_lo = part * per, k_hi = min(na, k_lo + per);
+    const int per = (na + PARTS * KS - 1) / (PARTS * KS);
+    const int k_lo = min(na, (ksi * PARTS + part) * per), k_hi = min(na, k_lo + per);
     for (int k0 = k_lo; k0 < k_hi; k0 += CH) {
       float kv[CH][RPT];
 #pragma unroll
@@ -434,12 +439,12 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
       for (int r = 0; r < RPT; ++r) {
         if (has[r] && part == 0) {
           const int64_t j = base + r * kWsSelThreads;
-          a.dfs[j] = acc[r];
+          a.dfs[(int64_t)ksi * a.nl + j] = acc[r];
           const float dj = a.dalpha[a.off + j];
           if (dj != 0.f) {
             const double cj = (double)dj * (double)a.y[a.off + j];
-            sq += cj * (double)acc[r];
-            sg -= cj * (double)f[r];
+            sq += cj * (double)acc[r];  // d'Qd is linear in the KS partial changes
+            if (ksi == 0) sg -= cj * (double)f[r];
           }
         }
       }
@@ -458,8 +463,9 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
           tq += s_red[0][k];
           tg += s_red[1][k];
         }
-        a.part[2 * ((int64_t)a.rank * a.G + blockIdx.x)] = tq;
-        a.part[2 * ((int64_t)a.rank * a.G + blockIdx.x) + 1] = tg;
+        const int64_t slot = ((int64_t)a.rank * a.G + grp) * KS + ksi;
+        a.part[2 * slot] = tq;
+        a.part[2 * slot + 1] = tg;
         if (blockIdx.x == 0) WS_STAMP(23);
       }
       return;
@@ -496,7 +502,11 @@ __global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_ker
       for (int r = 0; r < RPT; ++r) {
         if (has[r] && part == 0) {
           const int64_t j = base + r * kWsSelThreads;
-          const float d = a.dfs[j];
+          float d = a.dfs[j];
+          for (int k = 1; k < a.ks; ++k) {
+#pragma clang fp contract(off)
+            d = d + a.dfs[(int64_t)k * a.nl + j];
+          }
           acc[r] = t == 1.f ? d : t * d;
           const float dj = a.dalpha[a.off + j];
           if (dj != 0.f) {
@@ -1842,6 +1852,13 @@ __global__ __launch_bounds__(256) void ws_pack_rows_kernel(const float* __restri
 
 namespace launch {
 
+int ws_pass1_splits(int G) {
+  // >= ~2 workgroups per CU of a 256-CU device for the f-update pass 1 (its
+  // list slices are summed in slice order: every rank uses the same G, so the
+  // same count)
+  return std::max(1, std::min(kWsMaxPass1Splits, (512 + G - 1) / std::max(1, G)));
+}
+
 void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt) {
   // every rank the same geometry (sized for the largest shard); the merge reads
   // world * G <= 1024 candidate lists (kWsListsPerThread per merge thread), so
@@ -1862,7 +1879,7 @@ bool ws_supported(int64_t nl_max, int world, int q_max) {
 
 template <int MODE>
 static void ws_select_mode(const WsArgs& a, hipStream_t s) {
-  const dim3 grid(a.G);
+  const dim3 grid(a.G * (MODE == 1 ? std::max(1, a.ks) : 1));
   auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 4 ? 4 : rpt <= 16 ? 2 : 1)); };
   if (a.rpt <= 1) dev::ws_select_kernel<1, MODE><<<grid, threads(1), 0, s>>>(a);
   else if (a.rpt <= 2) dev::ws_select_kernel<2, MODE><<<grid, threads(2), 0, s>>>(a);

@@ -333,7 +333,7 @@ void ws_allgather_cand(GpuSolver::Impl& m) {
 // multi-block rounds at world > 1: every rank's line-search partials
 void ws_allgather_part(GpuSolver::Impl& m) {
   if (!m.collectives()) return;
-  const size_t bytes = (size_t)m.wsa.G * 2 * sizeof(double);
+  const size_t bytes = (size_t)m.wsa.G * std::max(1, m.wsa.ks) * 2 * sizeof(double);
   uint8_t* all = (uint8_t*)m.wsa.part;
   if (m.comm->device_memory()) {
     m.comm->allgather(all + (size_t)m.rank * bytes, all, bytes, m.stream);

@@ -690,9 +690,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.subg = m.wssub;
     w.aux = m.wssub + (size_t)w.blocks * w.q_max * w.q_max;
     if (w.blocks > 1) {
-      m.wsdfs = dmalloc<float>((size_t)m.nl, &m.bytes);
+      w.ks = launch::ws_pass1_splits(w.G);
+      m.wsdfs = dmalloc<float>((size_t)w.ks * m.nl, &m.bytes);
       m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
-      m.wspart = dmalloc<double>((size_t)2 * w.G_all, &m.bytes);
+      m.wspart = dmalloc<double>((size_t)2 * w.G_all * w.ks, &m.bytes);
       m.wssorted = dmalloc<uint64_t>((size_t)2 * kWsMaxGroups * kWsCand, &m.bytes);
       w.sorted = m.wssorted;
       HIP_CHECK(hipMemsetAsync(m.wsdalpha, 0, (size_t)n * 4, m.stream));

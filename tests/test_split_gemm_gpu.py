@@ -81,3 +81,27 @@ def test_split_gram_extreme_row_scales(K):
     assert np.isfinite(k16).all()
     assert np.abs(k16 - ref).max() <= max(3 * np.abs(k32 - ref).max(), 2e-6)
     assert k16[0, 0] == 1.0 and k16[1, 1] == 1.0
+
+
+@pytest.mark.parametrize("n,m,d", [(1000, 777, 784), (4133, 2300, 300), (2600, 129, 1024)])
+def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
+    """The persistent, cross-tile pipelined STORE GEMM (the default for dp > 128)
+    runs the tile kernel's MFMA sequence per tile: the same bits, symmetric
+    (upper tiles + mirrored stores) and plain, with partial edge tiles."""
+    from dpsvm_amd._native import load
+
+    C = load()
+    rng = np.random.default_rng(n)
+    x = torch.from_numpy(rng.random((n, d), dtype=np.float32)).cuda()
+    y = torch.from_numpy(rng.standard_normal((m, d), dtype=np.float32)).cuda()
+    g = 1.0 / d
+    try:
+        C.k_set_split_gemm_variant(1)
+        ref_sym, ref_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
+        C.k_set_split_gemm_variant(2)
+        got_sym, got_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
+    finally:
+        C.k_set_split_gemm_variant(0)
+    assert torch.equal(got_sym, ref_sym)
+    assert torch.equal(got_xy, ref_xy)
+    assert torch.isfinite(got_sym).all() and torch.isfinite(got_xy).all()
