@@ -17,7 +17,13 @@ plus the rank's Gram slab K(all rows, n / P columns) (measured at P = 1..8).
 The rounds are the one-GPU count (the trajectory is bit-identical at any
 rank count: tests/test_ws_gpu.py sharded-vs-replicated tests).
 
-  python bench/project_shard.py [profiles/r3_shard_projection_inputs_1gpu.json]
+  python bench/project_shard.py [inputs.json] [pass1_probe.jsonl]
+
+With a pass-1 probe file (bench/pass1_probe.py: the multi-block f-update pass 1
+measured alone at a rank's shard shape, 60000 x 60000 / P, with the workgroup
+split the solver picks, ws_pass1_splits) pass 1 at P > 1 is that measurement
+instead of the one-rank time / P — pass 1 does not divide by P (few selection
+groups per rank: profiles/r3_pass1_probe.txt).
 """
 import json
 import sys
@@ -26,8 +32,23 @@ PASS1_US = 50.0   # f-update pass 1 at P = 1 when the inputs carry no stamp of i
 UNION = 3072      # rows per round (device_state.hpp kWsMaxAll); blocks of UNION / P rows, <= 192
 
 
+def pass1_splits(G: int) -> int:
+    return max(1, min(16, 256 // max(1, G)))  # kernels ws_pass1_splits
+
+
+def probe_pass1(path):
+    """{P: pass-1 us} at the shard shapes of the probe (the solver's split)"""
+    out = {}
+    for line in open(path):
+        r = json.loads(line)
+        if r["rows"] == 60000 and r["ks"] == pass1_splits(r["G"]):
+            out[60000 // r["cols"]] = r["pass1_us_median"]
+    return out
+
+
 def main() -> int:
     path = sys.argv[1] if len(sys.argv) > 1 else "profiles/r3_shard_projection_inputs_1gpu.json"
+    probe = probe_pass1(sys.argv[2]) if len(sys.argv) > 2 else {}
     m = json.load(open(path))
     r = m["round_us"]
     rounds = m["local"]["rounds"]
@@ -37,6 +58,8 @@ def main() -> int:
     fixed = r["merge"] + r["gather"] + r["load_subgram"] + r["solve"]
     pass1 = r.get("pass1_start_to_pass2_start") or PASS1_US
     rows_part = pass1 + r["select_pass2"]
+    if probe:
+        print(f"  pass 1 measured at the shard shapes (bench/pass1_probe.py): {probe} us; one rank {pass1:.1f} us")
     gaps = max(0.0, r["period"] - fixed - rows_part)
     print(f"inputs: {path}")
     print(f"  measured: rounds {rounds}, round period {r['period']} us = redundant {fixed:.1f} (merge, gather, "
@@ -54,7 +77,8 @@ def main() -> int:
                 row.append(m["local"]["s"])
                 continue
             coll = 3 * L + 2 * (P - 1) / P * ar_bytes / (B * 1e3)  # bytes / (GB/s) -> us
-            per_round = fixed + rows_part / P + gaps + coll
+            p1 = probe.get(P, pass1 / P)
+            per_round = fixed + p1 + r["select_pass2"] / P + gaps + coll
             row.append(gram + rounds * per_round * 1e-6)
         print(f"{L:>6} {B:>7} | " + " | ".join(f"{v:.4f}  " for v in row))
     return 0

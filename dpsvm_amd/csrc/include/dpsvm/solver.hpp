@@ -200,12 +200,14 @@ struct WsSelectProbe {
   int G = 0, rpt = 0, p_act = 0, n_damped = 0, nonfinite = 0;
   float t = 1.f;
   int64_t p1_round = 0;
+  std::vector<float> pass1_us;  // reps > 0: event times of repeated pass-1 launches
 };
 WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t ldg, const std::vector<float>& f,
                               const std::vector<float>& alpha, const std::vector<float>& y,
                               const std::vector<float>& dalpha, const std::vector<int32_t>& apply_line,
                               const std::vector<float>& apply_coef, const std::vector<int32_t>& nab, int blocks,
-                              int p_round, int p_act, int q_max, float C, int64_t outer);
+                              int p_round, int p_act, int q_max, float C, int64_t outer, int ks = 0,
+                              int reps = 0);
 }  // namespace kernels
 
 int device_count();

@@ -543,6 +543,155 @@ __global__ __launch_bounds__(kPersistThreads, 1) void rbf_gemm_split_persist_ker
   store_mirror();
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA STORE GEMM: the tile kernel's MFMA sequence (128 x 128 tile, 8 waves
+// of 32 x 64, k blocks in order: bit-identical Gram) with the operands staged
+// by global_load_lds_dwordx4 into FOUR 32-k buffers, three blocks in flight
+// ahead of the one being multiplied.  Per k block: a counted vmcnt retires the
+// block's own DMA (never vmcnt(0) inside the loop), one raw s_barrier (the DMA
+// has landed everywhere, and every wave is done with the buffer the next DMA
+// overwrites), the DMA of block kb + 3, then 2 k16 steps of 6 MFMAs.  The
+// register-staged kernels above wait for each stage's loads before the next
+// stage can start (one stage of prefetch: a 0.3-0.6 us stage against a 1-2 us
+// L2-miss latency).  An LDS-DMA wave instruction writes 1 KiB lane-linearly (8
+// rows x 128 B): the bank swizzle of the operand reads (chunk c of row r at
+// position c ^ ((r >> 1) & 7)) moves to the per-lane SOURCE address.  All LDS
+// in one array (row data after the buffers): a second __shared__ object makes
+// hipcc wait vmcnt(0) before the operand reads.
+// ---------------------------------------------------------------------------
+constexpr int kGldsThreads = 512;
+__global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
+    float gamma, float* __restrict__ out, int64_t ldo, int sym) {
+  constexpr int WN = 2, TM = 128, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 4;
+  int64_t tx, ty;
+  xcd_tile(tx, ty);
+  if (sym && ty < tx) return;
+  __shared__ u4 lds[NB * BUF + 2 * ROWS / 4];  // 4 operand buffers, then |x|^2 [ROWS] and shifts [ROWS]
+  float* s_sq = (float*)(lds + NB * BUF);
+  int32_t* s_sh = (int32_t*)(lds + NB * BUF) + ROWS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t m0 = tx * TM, n0 = ty * TN;
+  const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
+
+  if (tid < ROWS) {
+    const int64_t ri = tid < TM ? min(m0 + tid, M - 1) : min(n0 + (tid - TM), N - 1);
+    s_sq[tid] = tid < TM ? Asq[ri] : Bsq[ri];
+    s_sh[tid] = tid < TM ? Ash[ri] : Bsh[ri];
+  }
+  // DMA sources: wave w fills rows 32 w + 8 i + (lane >> 3), i = 0..3 (waves 0-3: A rows,
+  // 4-7: B rows); lane position p = lane & 7 takes global chunk p ^ ((row >> 1) & 7)
+  const u4* src[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 32 * wave + 8 * i + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    src[i] = r < TM ? A + (m0 + r) * rstride + c : B + (n0 + (r - TM)) * rstride + c;
+  }
+  auto dma = [&](int kb) {
+    u4* dst = lds + (kb & (NB - 1)) * BUF + 32 * wave * CPR;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
+                                       (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+  };
+  __syncthreads();  // row data written (no DMA in flight yet)
+  dma(0);
+  if (nkb > 1) dma(1);
+  if (nkb > 2) dma(2);
+
+  f16v H[2], P[2], Q[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  for (int kb = 0; kb < nkb; ++kb) {
+    // retire block kb's DMA: the blocks after it (up to 2) may stay in flight
+    const int ahead = min(2, nkb - 1 - kb);
+    if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kb + 3 < nkb) dma(kb + 3);  // into the buffer of block kb - 1 (every wave is past it)
+    const u4* buf = lds + (kb & (NB - 1)) * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+      const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
+      const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
+      const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+      const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+      const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
+      const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
+      H[0] = mfma32_f16(ah, bh0, H[0]);
+      H[1] = mfma32_f16(ah, bh1, H[1]);
+      P[0] = mfma32_f16(ah, bl0, P[0]);
+      P[1] = mfma32_f16(ah, bl1, P[1]);
+      Q[0] = mfma32_f16(al, bh0, Q[0]);
+      Q[1] = mfma32_f16(al, bh1, Q[1]);
+    }
+  }
+
+  // ---- epilogue (as the tile kernel) ----
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cb = TM + wn * 64 + 32 * j + (lane & 31);
+    const float bsq = s_sq[cb];
+    const int bsh = s_sh[cb];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_sh[lr] + bsh));
+      H[j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
+    }
+  }
+  const bool interior = m0 + TM <= M && n0 + TN <= N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (interior || (row < M && col < N)) out[row * ldo + col] = H[j][r];
+    }
+  }
+  if (sym && ty != tx) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = m0 + wm * 32 + 8 * q + 4 * hl;
+        float* dst = out + col * ldo + row;
+        f4 v;
+        v.x = H[j][4 * q + 0];
+        v.y = H[j][4 * q + 1];
+        v.z = H[j][4 * q + 2];
+        v.w = H[j][4 * q + 3];
+        if (interior) {
+          *(f4*)dst = v;
+        } else if (col < M) {
+          if (row + 3 < N) {
+            *(f4*)dst = v;
+          } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (row + c < N) dst[c] = v[c];
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace dev
 
 namespace launch {
@@ -553,7 +702,7 @@ int g_split_variant = -1;
 
 int split_gemm_variant() {
   if (g_split_variant < 0) {
-    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // diagnostics: 1 = tile-per-workgroup kernel, 2 = persistent
+    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 2 persistent, 3 (= 0) LDS-DMA
     g_split_variant = e ? atoi(e) : 0;
   }
   return g_split_variant;
@@ -589,8 +738,16 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     const char* e = std::getenv("DPSVM_SPLIT_KB");  // diagnostics: k blocks per stage (A/B)
     return e && atoi(e) == 1 ? 1 : 2;
   }();
-  if (split_gemm_variant() != 1 && ablate == 0 && kb == 2 && (dp + 31) / 32 > 4 && tm * tn < (1ll << 31)) {
-    // persistent, cross-tile pipelined (default); one workgroup per CU, a multiple of 8
+  const int variant = split_gemm_variant();
+  if ((variant == 0 || variant == 3) && ablate == 0 && kb == 2) {  // default: LDS-DMA, three k blocks in flight
+    dev::rbf_gemm_split_glds_kernel<<<dim3((unsigned)tm, (unsigned)tn), dev::kGldsThreads, 0, s>>>(
+        (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
+        symmetric ? 1 : 0);
+    post_launch("rbf_gemm_split_glds", s);
+    return;
+  }
+  if (variant == 2 && ablate == 0 && kb == 2 && (dp + 31) / 32 > 4 && tm * tn < (1ll << 31)) {
+    // persistent, cross-tile pipelined; one workgroup per CU, a multiple of 8
     static const int cus = [] {
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);

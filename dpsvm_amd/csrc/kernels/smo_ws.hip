@@ -1853,10 +1853,14 @@ __global__ __launch_bounds__(256) void ws_pack_rows_kernel(const float* __restri
 namespace launch {
 
 int ws_pass1_splits(int G) {
-  // >= ~2 workgroups per CU of a 256-CU device for the f-update pass 1 (its
-  // list slices are summed in slice order: every rank uses the same G, so the
-  // same count)
-  return std::max(1, std::min(kWsMaxPass1Splits, (512 + G - 1) / std::max(1, G)));
+  // about one pass-1 workgroup per CU of the 256-CU device: the selection
+  // geometry gives a rank of P only G = ceil(60000 / P / 256) groups on the
+  // headline (30 at P = 8), and pass 1 is then bound by the few CUs issuing
+  // loads — 3,072 changed rows x 7,500 columns: 114 us with 30 workgroups, 38 us
+  // with 240; with 60,000 columns 235 workgroups beat 470 / 705 (158 vs 167 /
+  // 189 us; profiles/r3_pass1_probe.txt).  Every rank uses the same G, so the
+  // same slice count and the same summation order.
+  return std::max(1, std::min(kWsMaxPass1Splits, 256 / std::max(1, G)));
 }
 
 void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt) {

@@ -497,7 +497,7 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("xsq"), py::arg("n"), py::arg("ld"), py::arg("rows"), py::arg("m"), py::arg("gamma"),
         py::arg("out"), py::arg("out_ld"), py::arg("out_rows"), py::arg("stream"), py::arg("split") = false);
   m.def("k_set_split_gemm_variant", [](int v) { launch::set_split_gemm_variant(v); },
-        "split STORE GEMM: 0 auto (persistent when dp > 128), 1 tile per workgroup, 2 persistent (tests / A/B)");
+        "split STORE GEMM: 0 auto (= 3), 1 tile per workgroup, 2 persistent register-staged, 3 LDS-DMA (tests / A/B)");
   m.def("k_split_gemm_variant", []() { return launch::split_gemm_variant(); });
   m.def("k_rbf_gram_split", [](uintptr_t a, uintptr_t asq, int64_t m_, uintptr_t b, uintptr_t bsq, int64_t n, int ld,
                                float gamma, uintptr_t out, int64_t out_ld, bool sym, uintptr_t stream) {
@@ -548,10 +548,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("k_ws_select", [vi](const F32& gram, int64_t L, int64_t ldg, const F32& f, const F32& alpha, const F32& y,
                             const F32& dalpha, const I32& lines, const F32& coef, const I32& nab, int blocks,
-                            int p_round, int p_act, int q_max, float C, int64_t outer) {
+                            int p_round, int p_act, int q_max, float C, int64_t outer, int ks, int reps) {
     const auto r = kernels::ws_select_probe(from_np(gram), L, ldg, from_np(f), from_np(alpha), from_np(y),
                                             from_np(dalpha), vi(lines), from_np(coef), vi(nab), blocks, p_round, p_act,
-                                            q_max, C, outer);
+                                            q_max, C, outer, ks, reps);
     py::dict d;
     d["f"] = to_np(r.f);
     d["alpha"] = to_np(r.alpha);
@@ -562,12 +562,15 @@ PYBIND11_MODULE(_C, m) {
     d["G"] = r.G;
     d["rpt"] = r.rpt;
     d["t"] = r.t;
+    d["pass1_us"] = r.pass1_us;
     d["p_act"] = r.p_act;
     d["n_damped"] = r.n_damped;
     d["p1_round"] = r.p1_round;
     d["nonfinite"] = r.nonfinite;
     return d;
-  });
+  }, py::arg("gram"), py::arg("L"), py::arg("ldg"), py::arg("f"), py::arg("alpha"), py::arg("y"), py::arg("dalpha"),
+        py::arg("lines"), py::arg("coef"), py::arg("nab"), py::arg("blocks"), py::arg("p_round"), py::arg("p_act"),
+        py::arg("q_max"), py::arg("C"), py::arg("outer"), py::arg("ks") = 0, py::arg("reps") = 0);
   m.def("make_key", [](float f, uint32_t idx) { return make_key(f, idx); });
   m.def("key_value", [](uint64_t k) { return key_value(k); });
   m.def("key_index", [](uint64_t k) { return key_index(k); });

@@ -197,7 +197,7 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
                               const std::vector<float>& alpha, const std::vector<float>& y,
                               const std::vector<float>& dalpha, const std::vector<int32_t>& apply_line,
                               const std::vector<float>& apply_coef, const std::vector<int32_t>& nab, int blocks,
-                              int p_round, int p_act, int q_max, float C, int64_t outer) {
+                              int p_round, int p_act, int q_max, float C, int64_t outer, int ks, int reps) {
   const int64_t n = (int64_t)f.size();
   DPSVM_CHECK(n >= 1 && (int64_t)alpha.size() == n && (int64_t)y.size() == n && (int64_t)dalpha.size() == n,
               "ws_select_probe: f / alpha / y / dalpha of n rows");
@@ -241,8 +241,9 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
   a.alpha = st.up(alpha, (size_t)n);
   a.y = st.up(y, (size_t)n);
   a.dalpha = st.up(dalpha, (size_t)n);
-  a.dfs = st.up(std::vector<float>(), (size_t)n);
-  a.part = st.up(std::vector<double>(), (size_t)2 * G);
+  a.ks = std::max(1, ks);
+  a.dfs = st.up(std::vector<float>(), (size_t)n * a.ks);
+  a.part = st.up(std::vector<double>(), (size_t)2 * G * a.ks);
   a.cand = a.cand_out = st.up(std::vector<uint64_t>(), (size_t)G * 2 * kWsCand);
   a.n = a.nl = n;
   a.off = 0;
@@ -255,16 +256,33 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
   a.blocks = blocks;
   a.t_halve = 0.9f;
   a.clip_fallback = 1;
+  WsSelectProbe r;
+  if (blocks > 1 && reps > 0) {
+    // timing (bench/pass1_probe.py): pass 1 only reads the state, so it can repeat
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    for (int i = 0; i < reps; ++i) {
+      HIP_CHECK(hipEventRecord(e0, st.s));
+      launch::ws_select_pass(a, 1, st.s);
+      HIP_CHECK(hipEventRecord(e1, st.s));
+      HIP_CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      r.pass1_us.push_back(1e3 * ms);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
   launch::ws_select(a, st.s);  // blocks > 1: pass 1 then pass 2
   const WsCtrl o = download(a.ctrl, 1, st.s)[0];
-  WsSelectProbe r;
   r.G = G;
   r.rpt = rpt;
   r.f = download(a.f, (size_t)n, st.s);
   r.alpha = download(a.alpha, (size_t)n, st.s);
   r.dalpha = download(a.dalpha, (size_t)n, st.s);
-  r.dfs = download(a.dfs, (size_t)n, st.s);
-  r.part = download(a.part, (size_t)2 * G, st.s);
+  r.dfs = download(a.dfs, (size_t)n, st.s);  // slice 0 (all of it at ks = 1)
+  r.part = download(a.part, (size_t)2 * G * a.ks, st.s);
   r.cand = download(a.cand_out, (size_t)G * 2 * kWsCand, st.s);
   r.t = o.t_last;
   r.p_act = o.p_act;

@@ -85,9 +85,9 @@ def test_split_gram_extreme_row_scales(K):
 
 @pytest.mark.parametrize("n,m,d", [(1000, 777, 784), (4133, 2300, 300), (2600, 129, 1024)])
 def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
-    """The persistent, cross-tile pipelined STORE GEMM (the default for dp > 128)
-    runs the tile kernel's MFMA sequence per tile: the same bits, symmetric
-    (upper tiles + mirrored stores) and plain, with partial edge tiles."""
+    """The persistent, cross-tile pipelined STORE GEMM and the LDS-DMA GEMM run
+    the tile kernel's MFMA sequence per tile: the same bits, symmetric (upper
+    tiles + mirrored stores) and plain, with partial edge tiles."""
     from dpsvm_amd._native import load
 
     C = load()
@@ -98,10 +98,13 @@ def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
     try:
         C.k_set_split_gemm_variant(1)
         ref_sym, ref_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
-        C.k_set_split_gemm_variant(2)
-        got_sym, got_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
+        got = {}
+        for v in (2, 3):  # persistent pipelined; LDS-DMA with three k blocks in flight
+            C.k_set_split_gemm_variant(v)
+            got[v] = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
     finally:
         C.k_set_split_gemm_variant(0)
-    assert torch.equal(got_sym, ref_sym)
-    assert torch.equal(got_xy, ref_xy)
-    assert torch.isfinite(got_sym).all() and torch.isfinite(got_xy).all()
+    for v, (got_sym, got_xy) in got.items():
+        assert torch.equal(got_sym, ref_sym), v
+        assert torch.equal(got_xy, ref_xy), v
+        assert torch.isfinite(got_sym).all() and torch.isfinite(got_xy).all()

@@ -444,6 +444,33 @@ def test_ws_select_two_pass_line_search_matches_model(K, target, P, p_act):
     np.testing.assert_array_equal(cand, candidates_model(got["f"], got["alpha"], y, C, G, rpt))
 
 
+@pytest.mark.parametrize("ks", [2, 5])
+def test_ws_select_pass1_list_slices_match_model(K, ks):
+    """Pass 1 split into ks slices of the changed-row list per selection group
+    (ws_pass1_splits: a rank's shard of a sharded run has few groups): the
+    partials still sum to d'Qd and g'd, pass 2 sums the slices' changes, and f
+    after the round matches the model and the one-slice kernel."""
+    rng = np.random.default_rng(40 + ks)
+    n, C, q_max, P = 3000, 2.0, 96, 4
+    gram, f, a_new, y, dal, ch = select_state(rng, n, C, 160)
+    c = dal.astype(np.float64) * y
+    d_f = gram.astype(np.float64).T @ c
+    q = float(np.sum(c[ch] * d_f[ch]))
+    g = -float(np.sum(c[ch] * f.astype(np.float64)[ch]))
+    nab = [40] * P
+    kw = dict(q_max=q_max)
+    got = K.ws_select(gram, f, a_new, y, dal, ch, c[ch].astype(np.float32), nab, C, ks=ks, **kw)
+    one = K.ws_select(gram, f, a_new, y, dal, ch, c[ch].astype(np.float32), nab, C, ks=1, **kw)
+    part = np.asarray(got["part"]).reshape(got["G"] * ks, 2)
+    assert part[:, 0].sum() == pytest.approx(q, rel=1e-4)
+    assert part[:, 1].sum() == pytest.approx(g, rel=1e-6, abs=1e-9)
+    assert got["t"] == pytest.approx(float(line_search_rule(part[:, 0].sum(), part[:, 1].sum(), P)), rel=1e-6)
+    assert got["t"] == pytest.approx(one["t"], rel=1e-5)
+    np.testing.assert_allclose(got["f"], f + np.float32(got["t"]) * d_f, rtol=1e-4, atol=3e-5)
+    np.testing.assert_allclose(got["f"], one["f"], rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(got["alpha"], one["alpha"], rtol=1e-5, atol=1e-6 * C)
+
+
 def test_ws_select_one_pass_matches_model(K):
     rng = np.random.default_rng(3)
     n, C = 70000, 1.0  # 2 rows per selection thread
