@@ -692,6 +692,231 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent LDS-DMA STORE GEMM: the LDS-DMA kernel's k loop, one 512-thread
+// workgroup per CU walking tiles as the persistent kernel does, so that a
+// tile's Gram stores (128 KiB per tile with the mirror: 4.2 of the tile
+// kernel's 13.6 ms, profiles/r3_split_gemm_headline_ab.txt) drain while the
+// next tile multiplies.  Order at a tile boundary: the next tile's row data
+// (plain loads, issued while no DMA is in flight), the epilogue math, a
+// barrier, the next tile's first three DMAs, THEN this tile's stores — so the
+// next tile's first three waits count the stores as younger than their DMA:
+// vmcnt(8 + S) with S the store instructions each lane issued (interior tiles:
+// exactly 32 direct + 8 mirrored, unpredicated; edge tiles store predicated and
+// drain with vmcnt(0)).  From block 3 on the stores are older than the block's
+// DMA and vmcnt(8) retires them too.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_persist_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
+    float gamma, float* __restrict__ out, int64_t ldo, int sym, int tm, int tn) {
+  constexpr int WN = 2, TM = 128, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 4;
+  __shared__ u4 lds[NB * BUF + 4 * ROWS / 4];  // 4 operand buffers, then per tile parity |x|^2 [ROWS], shifts [ROWS]
+  float* s_sq0 = (float*)(lds + NB * BUF);
+  int32_t* s_sh0 = (int32_t*)(lds + NB * BUF) + 2 * ROWS;
+
+  const int total = tm * tn, G = gridDim.x;
+  auto valid = [&](int L, int& x, int& y) {
+    xcd_tile_of32(L, tm, tn, x, y);
+    return !(sym && y < x);
+  };
+  int tx = 0, ty = 0, L = blockIdx.x;
+  while (L < total && !valid(L, tx, ty)) L += G;
+  if (L >= total) return;  // uniform: no barrier reached
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t rstride = (int64_t)nkb * 8;
+  int64_t m0 = (int64_t)tx * TM, n0 = (int64_t)ty * TN;
+
+  // DMA geometry (as rbf_gemm_split_glds_kernel): row 32 w + 8 i + (lane >> 3)
+  int srow[4], schunk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    srow[i] = 32 * wave + 8 * i + (lane >> 3);
+    schunk[i] = (lane & 7) ^ ((srow[i] >> 1) & 7);
+  }
+  const u4* src[4];
+  auto set_src = [&](int64_t a0, int64_t b0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      src[i] = srow[i] < TM ? A + (a0 + srow[i]) * rstride + schunk[i] : B + (b0 + (srow[i] - TM)) * rstride + schunk[i];
+  };
+  auto dma = [&](int kb) {
+    u4* dst = lds + (kb & (NB - 1)) * BUF + 32 * wave * CPR;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
+                                       (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+  };
+  auto row_data = [&](int64_t a0, int64_t b0, float& q, int32_t& h) {
+    if (tid < ROWS) {
+      const int64_t ri = tid < TM ? min(a0 + tid, M - 1) : min(b0 + (tid - TM), N - 1);
+      q = tid < TM ? Asq[ri] : Bsq[ri];
+      h = tid < TM ? Ash[ri] : Bsh[ri];
+    }
+  };
+  {
+    float q = 0.f;
+    int32_t h = 0;
+    row_data(m0, n0, q, h);
+    if (tid < ROWS) {
+      s_sq0[tid] = q;
+      s_sh0[tid] = h;
+    }
+  }
+  __syncthreads();  // row data of tile 0 (no DMA in flight yet)
+  set_src(m0, n0);
+  dma(0);
+  if (nkb > 1) dma(1);
+  if (nkb > 2) dma(2);
+
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  int par = 0;
+  int pend = 0;  // store instructions each lane issued after the current tile's first DMAs (0, 32 or 40)
+  f16v H[2], P[2], Q[2];
+  while (true) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int ahead = min(2, nkb - 1 - kb);
+      // the previous tile's stores sit between the DMAs of blocks 2 and 3
+      const int st = kb < 3 ? pend : 0;
+      if (ahead == 2) {
+        if (st == 40) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+        else if (st == 32) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else if (ahead == 1) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // never with pending stores: nkb >= 5 (launcher)
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kb + 3 < nkb) dma(kb + 3);
+      const u4* buf = lds + (kb & (NB - 1)) * BUF;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+        const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
+        const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
+        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+        const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
+        const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
+        H[0] = mfma32_f16(ah, bh0, H[0]);
+        H[1] = mfma32_f16(ah, bh1, H[1]);
+        P[0] = mfma32_f16(ah, bl0, P[0]);
+        P[1] = mfma32_f16(ah, bl1, P[1]);
+        Q[0] = mfma32_f16(al, bh0, Q[0]);
+        Q[1] = mfma32_f16(al, bh1, Q[1]);
+      }
+    }
+    // ---- tile boundary (no DMA in flight: the last block waited vmcnt(0)) ----
+    int nL = L + G, ntx = tx, nty = ty;
+    while (nL < total && !valid(nL, ntx, nty)) nL += G;
+    const bool has_next = nL < total;
+    const int64_t nm0 = (int64_t)ntx * TM, nn0 = (int64_t)nty * TN;
+    float nq = 0.f;
+    int32_t nh = 0;
+    if (has_next) row_data(nm0, nn0, nq, nh);
+    const float* s_sq = s_sq0 + par * ROWS;
+    const int32_t* s_sh = s_sh0 + par * ROWS;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cb = TM + wn * 64 + 32 * j + (lane & 31);
+      const float bsq = s_sq[cb];
+      const int bsh = s_sh[cb];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_sh[lr] + bsh));
+        H[j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
+      }
+    }
+    if (has_next && tid < ROWS) {
+      s_sq0[(par ^ 1) * ROWS + tid] = nq;
+      s_sh0[(par ^ 1) * ROWS + tid] = nh;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done with the operand buffers of this tile
+    asm volatile("" ::: "memory");
+    if (has_next) {
+      set_src(nm0, nn0);
+      dma(0);
+      dma(1);
+      dma(2);
+    }
+    asm volatile("" ::: "memory");  // the stores stay behind the DMAs
+    const bool interior = m0 + TM <= M && n0 + TN <= N;
+    const bool mirror = sym && ty != tx;
+    if (interior) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) out[row * ldo + n0 + wn * 64 + 32 * j + (lane & 31)] = H[j][r];
+      }
+      if (mirror) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f4 v;
+            v.x = H[j][4 * q + 0];
+            v.y = H[j][4 * q + 1];
+            v.z = H[j][4 * q + 2];
+            v.w = H[j][4 * q + 3];
+            *(f4*)(out + col * ldo + m0 + wm * 32 + 8 * q + 4 * hl) = v;
+          }
+        }
+      }
+      pend = mirror ? 40 : 32;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+          if (row < M && col < N) out[row * ldo + col] = H[j][r];
+        }
+      }
+      if (mirror) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int64_t row = m0 + wm * 32 + 8 * q + 4 * hl;
+            float* dst = out + col * ldo + row;
+            if (col < M) {
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                if (row + c < N) dst[c] = H[j][4 * q + c];
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // predicated stores: drained here
+      pend = 0;
+    }
+    if (!has_next) break;
+    L = nL;
+    tx = ntx;
+    ty = nty;
+    m0 = nm0;
+    n0 = nn0;
+    par ^= 1;
+  }
+}
+
 }  // namespace dev
 
 namespace launch {
@@ -702,7 +927,7 @@ int g_split_variant = -1;
 
 int split_gemm_variant() {
   if (g_split_variant < 0) {
-    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 2 persistent, 3 (= 0) LDS-DMA
+    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 2 persistent, 3 LDS-DMA, 4 persistent LDS-DMA
     g_split_variant = e ? atoi(e) : 0;
   }
   return g_split_variant;
@@ -739,7 +964,23 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     return e && atoi(e) == 1 ? 1 : 2;
   }();
   const int variant = split_gemm_variant();
-  if ((variant == 0 || variant == 3) && ablate == 0 && kb == 2) {  // default: LDS-DMA, three k blocks in flight
+  if ((variant == 0 || variant == 4) && ablate == 0 && (dp + 31) / 32 >= 5 && tm * tn < (1ll << 31)) {
+    // default: persistent LDS-DMA, one workgroup per CU (a multiple of 8)
+    static const int cus4 = [] {
+      int dev = 0, n = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return std::max(8, n / 8 * 8);
+    }();
+    const int64_t tiles = symmetric ? tm * (tm + 1) / 2 : tm * tn;
+    const int grid = (int)std::min<int64_t>(cus4, (tiles + 7) / 8 * 8);
+    dev::rbf_gemm_split_glds_persist_kernel<<<dim3((unsigned)grid), dev::kGldsThreads, 0, s>>>(
+        (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
+        symmetric ? 1 : 0, (int)tm, (int)tn);
+    post_launch("rbf_gemm_split_glds_persist", s);
+    return;
+  }
+  if ((variant == 0 || variant == 3) && ablate == 0 && kb == 2) {  // LDS-DMA, three k blocks in flight (dp <= 128 by default)
     dev::rbf_gemm_split_glds_kernel<<<dim3((unsigned)tm, (unsigned)tn), dev::kGldsThreads, 0, s>>>(
         (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
         symmetric ? 1 : 0);

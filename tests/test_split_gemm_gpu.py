@@ -99,7 +99,7 @@ def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
         C.k_set_split_gemm_variant(1)
         ref_sym, ref_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
         got = {}
-        for v in (2, 3):  # persistent pipelined; LDS-DMA with three k blocks in flight
+        for v in (2, 3, 4):  # persistent pipelined; LDS-DMA (three k blocks in flight); persistent LDS-DMA
             C.k_set_split_gemm_variant(v)
             got[v] = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
     finally:
