@@ -917,6 +917,128 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_persist_k
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA ROWS GEMM (ws-cache: a round's missing kernel rows).  A = up to 192
+// rows gathered by index (the round's misses), B = the rank's rows streamed
+// from HBM once per round (one 192-row tile row, as the register-staged ROWS
+// kernel), output rows to their cache lines.  12 waves of 32 x 64; three 40 KiB
+// buffers of 32-k blocks (A 192 + B 128 rows), two in flight; every wave
+// issues exactly 4 DMA instructions per block (40 real 1 KiB pieces + 8 into
+// a scratch slot), so one counted vmcnt(4) retires a block.  Waves whose 32
+// rows all lie past the miss count only stage.  Same MFMA sequence per output
+// as every split kernel: bit-identical lines.  Measured equal to the
+// register-staged ROWS kernel (500k x 1024: 3.728 vs 3.712 s): that GEMM streams
+// the rank's X panel at HBM speed already, so it stays the default.
+// ---------------------------------------------------------------------------
+constexpr int kRowsGldsThreads = 768;
+__global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
+    const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
+    const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb, float gamma,
+    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
+  constexpr int WN = 2, TM = 192, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
+  constexpr int PIECES = ROWS / 8, WAVES = kRowsGldsThreads / 64, PER = (PIECES + WAVES - 1) / WAVES;
+  static_assert(PER == 4, "4 DMA pieces per wave and block");
+  const int64_t M = *m_dev;
+  const int64_t tx = blockIdx.x, ty = blockIdx.y;
+  const int64_t m0 = tx * TM, n0 = ty * TN;
+  if (m0 >= M) return;  // uniform: no barrier reached
+  __shared__ u4 lds[NB * BUF + 64 + 2 * TM / 4 + TM / 4];  // buffers, DMA scratch, |a|^2, shifts, out lines
+  u4* scratch = lds + NB * BUF;
+  float* s_asq = (float*)(lds + NB * BUF + 64);
+  int32_t* s_ash = (int32_t*)(lds + NB * BUF + 64) + TM;
+  int32_t* s_orow = (int32_t*)(lds + NB * BUF + 64) + 2 * TM;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t rstride = (int64_t)nkb * 8;
+  if (tid < TM) {
+    const int64_t row = m0 + tid;
+    const int64_t ar = (int64_t)a_rows[min(row, M - 1)];
+    s_asq[tid] = Asq[ar];
+    s_ash[tid] = Ash[ar];
+    s_orow[tid] = row < M ? out_rows[row] : -1;
+  }
+  // piece id = wave + WAVES * i (i < 4); pieces >= PIECES land in the scratch slot
+  const u4* src[PER];
+  int dsto[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int pc = wave + WAVES * i;
+    const bool real = pc < PIECES;
+    const int r = (real ? pc : 0) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t grow = r < TM ? (int64_t)a_rows[min(m0 + r, M - 1)] : n0 + (r - TM);
+    src[i] = (r < TM ? A : B) + grow * rstride + c;
+    dsto[i] = real ? pc * 8 * CPR : -1;
+  }
+  auto dma = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      u4* dst = dsto[i] >= 0 ? lds + (kb % NB) * BUF + dsto[i] : scratch;
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  __syncthreads();
+  dma(0);
+  if (nkb > 1) dma(1);
+
+  f16v H[2], P[2], Q[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+  const bool live = m0 + wm * 32 < M;
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kb + 2 < nkb) dma(kb + 2);  // into the buffer of block kb - 1
+    if (live) {
+      const u4* buf = lds + (kb % NB) * BUF;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+        const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
+        const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
+        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+        const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
+        const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
+        H[0] = mfma32_f16(ah, bh0, H[0]);
+        H[1] = mfma32_f16(ah, bh1, H[1]);
+        P[0] = mfma32_f16(ah, bl0, P[0]);
+        P[1] = mfma32_f16(ah, bl1, P[1]);
+        Q[0] = mfma32_f16(al, bh0, Q[0]);
+        Q[1] = mfma32_f16(al, bh1, Q[1]);
+      }
+    }
+  }
+  if (!live) return;
+  const bool interior = n0 + TN <= N;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+    const int64_t cc = col < N ? col : N - 1;
+    const float bsq = Bsq[cc];
+    const int bsh = Bsh[cc];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
+      const float v = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+      const int32_t orow = s_orow[lr];
+      if (orow >= 0 && (interior || col < N)) out[(int64_t)orow * ldo + col] = v;
+    }
+  }
+}
+
 }  // namespace dev
 
 namespace launch {
@@ -934,6 +1056,20 @@ int split_gemm_variant() {
 }
 
 void set_split_gemm_variant(int v) { g_split_variant = v; }
+
+namespace {
+int g_rows_variant = -1;
+}
+
+int rows_gemm_variant() {
+  if (g_rows_variant < 0) {
+    const char* e = std::getenv("DPSVM_ROWS_GEMM");  // A/B: 0 / 1 register-staged ROWS kernel, 2 LDS-DMA
+    g_rows_variant = e ? atoi(e) : 0;
+  }
+  return g_rows_variant;
+}
+
+void set_rows_gemm_variant(int v) { g_rows_variant = v; }
 
 int64_t split_row_u4(int dp) { return (int64_t)((dp + 31) / 32) * 8; }
 
@@ -1024,6 +1160,13 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
   // tiles read it once per 64 misses)
   const int64_t tm = (M_max + 191) / 192, tn = (N + 127) / 128;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed_split: N too large for grid.y");
+  if (rows_gemm_variant() == 2) {  // LDS-DMA, two 32-k blocks in flight (measured equal: HBM-bound on B, r3_rows_glds_ab.txt)
+    dev::rbf_rows_split_glds_kernel<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
+        (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
+        ldl, out_rows);
+    post_launch("rbf_rows_split_glds", s);
+    return;
+  }
   dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 6, 1, 0, 2><<<dim3((unsigned)tm, (unsigned)tn), 768, 0, s>>>(
       (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
       a_rows, out_rows, m_dev);

@@ -55,13 +55,23 @@ def test_split_gram_operand_swap_bit_identical(K):
     assert torch.equal(ab, ba.T)
 
 
-def test_split_rows_indexed_equals_split_gram_rows(K):
+@pytest.mark.parametrize("variant,extra", [(0, 0), (2, 0), (2, 340)])
+def test_split_rows_indexed_equals_split_gram_rows(K, variant, extra):
+    """The ws-cache row GEMM (0: register-staged, the default; 2: LDS-DMA) gives
+    the Gram's rows bit for bit, for a partial 192-row tile and (extra) several."""
+    from dpsvm_amd._native import load
+
+    C = load()
     X, _ = synthetic("mnist", n=1200, seed=6)
     x = torch.from_numpy(X).cuda()
     full = K.rbf_gram(x, None, 0.25, split=True)
-    rows = [5, 1199, 0, 640, 641, 77, 333, 1024] + list(range(100, 160))
+    rows = [5, 1199, 0, 640, 641, 77, 333, 1024] + list(range(100, 160)) + list(range(700, 700 + extra))
     lines = list(range(len(rows)))[::-1]
-    got = K.rbf_rows_indexed(x, rows, 0.25, out_lines=lines, split=True)
+    try:
+        C.k_set_rows_gemm_variant(variant)
+        got = K.rbf_rows_indexed(x, rows, 0.25, out_lines=lines, split=True)
+    finally:
+        C.k_set_rows_gemm_variant(0)
     for r, ln in zip(rows, lines):
         assert torch.equal(got[ln], full[r]), r
 
