@@ -109,9 +109,9 @@ def parse(argv=None):
                     help="sub-problem pair choice: 1 first order (the reference's rule), 2 second order (WSS2), "
                          "0 auto (second order when the kernel couples rows); default: the library's (auto)")
     ap.add_argument("--ws-blocks", type=int, default=0,
-                    help="ws-dense: up to P sub-problems solved per round on separate workgroups, combined by a "
-                         "line search (1..8; 0 = the library default: 8 from 50k rows, halved after every damped "
-                         "round)")
+                    help="up to P sub-problems solved per round on separate workgroups, combined by a line search "
+                         "(1..32; 0 = the library default: 32 blocks of 96 rows from 50k rows, halved after every "
+                         "damped round)")
     ap.add_argument("--eta", default="x", choices=["x", "gram"],
                     help="pair-at-a-time engines: K(hi, lo) of eta from the two X rows (default) or the resident Gram")
     ap.add_argument("--gram", default="auto", choices=["auto", "f32", "split"],

@@ -41,6 +41,7 @@ struct Options {
   bool legacy_model = false;  // write/read the seq format (no b line)
   bool quiet = false;
   bool skip_accuracy = false;
+  bool shrink = false;        // one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking)
 };
 
 inline void usage_train(const char* prog, bool seq) {
@@ -85,8 +86,9 @@ inline void usage_train(const char* prog, bool seq) {
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
                "   --ws-wss 1|2        :  sub-problem pair choice: 1 first order (reference), 2 second order\n"
-               "   --ws-blocks P       :  ws-dense: up to P sub-problems per round on P workgroups (1..8; default 0 = auto:\n"
-               "                          8 from 50k rows, halved after every damped round)\n"
+               "   --ws-blocks P       :  up to P sub-problems per round on P workgroups (1..32; default 0 = auto:\n"
+               "                          32 blocks of 96 rows from 50k rows, halved after every damped round)\n"
+               "   --shrink            :  one GPU: LIBSVM-style shrinking (phases on the rows that can still violate)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --gram auto|f32|split :  Gram / kernel-row GEMMs: f32-input MFMA, or fp16 MFMA over hi/lo split\n"
                "                          operands (fp32 accuracy); auto = split for the ws engines\n"
@@ -108,7 +110,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
     OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL, OPT_WSBLOCKS,
-    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM
+    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM, OPT_SHRINK
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -142,6 +144,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {"ws-wss", required_argument, 0, OPT_WSWSS}, {"gram", required_argument, 0, OPT_GRAM},
+      {"shrink", no_argument, 0, OPT_SHRINK},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -188,6 +191,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_LEGG: o.legacy_gamma = true; break;
       case OPT_QUIET: o.quiet = true; break;
       case OPT_SKIPACC: o.skip_accuracy = true; break;
+      case OPT_SHRINK: o.shrink = true; break;
       case OPT_VERBOSE: o.p.verbose = true; break;
       case OPT_PERSIST: {
         const std::string v = optarg;

@@ -80,6 +80,21 @@ int main(int argc, char** argv) {
           return;
         }
         const int dev = (o.ranks > 0 || world == 1) ? o.device : r;
+        if (o.shrink) {
+          // one GPU: shrinking phases, each a device solver on the active rows
+          // (solver/gpu_shrink.cpp); training accuracy by the GPU predictor
+          if (world > 1) fail("--shrink runs on one GPU");
+          std::cout << "SETUP DONE\n";
+          extras.engine = "ws+shrinking";
+          results[r] = solve_shrinking(o.p, dev, ds.x.data(), n, d, ds.y.data(), resume.get(), prog);
+          const double ta0 = cli::now_s();
+          if (!o.skip_accuracy) {
+            GpuPredictor pred(make_model(ds, results[r].alpha, results[r].b, o.p.gamma), dev);
+            accs[r] = accuracy_from_decision(pred.decision(ds.x.data(), n, d), ds.y.data(), n);
+          }
+          extras.t_accuracy = cli::now_s() - ta0;
+          return;
+        }
         GpuSolver solver(o.p, comm, dev);
         GpuSetupInfo info = solver.setup(ds.x.data(), n, n, d, ds.y.data());
         if (world > 1) comm->barrier();

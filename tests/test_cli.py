@@ -140,3 +140,28 @@ def test_svmtrain_gpu_matches_cpu_and_svmtest(tmp_path, bin_dir):
     assert r.returncode == 0, r.stderr
     acc = float([l for l in r.stdout.split("\n") if "accuracy" in l.lower()][-1].split()[-1])
     assert abs(acc - outs["gpu"][2]) < 2e-3  # the predictor reproduces the trainer's accuracy
+
+
+@pytest.mark.gpu
+def test_svmtrain_shrink_matches_plain_box(tmp_path, bin_dir):
+    """svmTrain --shrink (one GPU, LIBSVM-style shrinking phases) reaches the
+    same joint-box optimum as the plain device run: reference stdout lines, b
+    and the support-set size within the stop tolerance's reach."""
+    import json
+
+    outs = {}
+    for mode in ("plain", "shrink"):
+        m = str(tmp_path / f"model_{mode}.txt")
+        js = str(tmp_path / f"metrics_{mode}.json")
+        cmd = [os.path.join(bin_dir, "svmTrain"), "-a", "54", "-x", "20000", "--synthetic", "covtype", "-c", "32",
+               "-g", "0.03125", "-e", "0.001", "-n", "10000000", "--clip", "box", "-m", m, "--metrics-json", js]
+        r = run(cmd + (["--shrink"] if mode == "shrink" else []))
+        assert r.returncode == 0, r.stderr
+        for line in ("SETUP DONE", "Converged at iteration number:", "Training accuracy:"):
+            assert line in r.stdout, (line, r.stdout)
+        outs[mode] = json.load(open(js))
+    p, s = outs["plain"], outs["shrink"]
+    assert p["converged"] and s["converged"]
+    assert s["engine"] == "ws+shrinking"
+    assert abs(p["b"] - s["b"]) < 2e-2
+    assert abs(p["n_sv"] - s["n_sv"]) <= max(5, p["n_sv"] // 50)
