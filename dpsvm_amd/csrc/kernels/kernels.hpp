@@ -113,13 +113,10 @@ void rbf_rows_indexed(const float* X, const float* Xsq, const int32_t* a_rows, c
 int64_t split_row_u4(int dp);
 int64_t split_pad_rows(int64_t rows);
 void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, int32_t* shift, hipStream_t s);
-// split STORE GEMM variant: 0 auto (4 when dp > 128, else 3), 1 tile per workgroup, 2 persistent register-staged,
-// 3 LDS-DMA, 4 persistent LDS-DMA
+// split STORE GEMM variant: 0 auto (4 when dp > 128, else 3), 1 register-staged tile per workgroup, 3 LDS-DMA,
+// 4 persistent LDS-DMA
 int split_gemm_variant();
 void set_split_gemm_variant(int v);
-// split ROWS GEMM (ws-cache misses): 0 auto (= 1), 1 register-staged, 2 LDS-DMA
-int rows_gemm_variant();
-void set_rows_gemm_variant(int v);
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
                           int64_t ldo, hipStream_t s, bool symmetric = false);

@@ -334,216 +334,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void rbf_gemm_split_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Persistent STORE GEMM (the Gram): one 512-thread workgroup per CU walks the
-// tiles L = blockIdx.x, blockIdx.x + gridDim.x, ... of the XCD-aware order
-// (gridDim.x a multiple of 8: a workgroup's tiles stay on its XCD; symmetric:
-// lower tiles skipped).  The k stages of consecutive tiles form ONE pipeline:
-//   - the last stage of tile t loads stage 0 of tile t + 1 (an address select,
-//     no branch around the loads), so no tile starts with an exposed load;
-//   - tile t's results (exp applied: 32 values per lane) stay in registers and
-//     are stored during the first two stages of tile t + 1, where the MFMAs of
-//     the new tile cover them — the tile-per-workgroup kernel above stalls the
-//     CU on every tile's stores and first load (4.2 of its 13.6 ms are stores,
-//     profiles/r3_split_gemm_headline_ab.txt);
-//   - each tile's row data (|a|^2, shifts, |b|^2) goes to LDS at its first
-//     stage (double buffered by tile parity) and is read by its epilogue.
-// Same MFMA sequence per tile as the kernel above (KB = 2, 128 x 128): bit-
-// identical Gram.  Needs >= 3 stages (dp > 128); smaller dp uses the kernel above.
-// ---------------------------------------------------------------------------
-constexpr int kPersistThreads = 512;
-__global__ __launch_bounds__(kPersistThreads, 1) void rbf_gemm_split_persist_kernel(
-    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
-    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
-    float gamma, float* __restrict__ out, int64_t ldo, int sym, int tm, int tn) {
-  constexpr int WM = 4, WN = 2, KB = 2, THREADS = kPersistThreads, TM = 128, TN = 128, ROWS = TM + TN;
-  constexpr int CPR = 8 * KB, CH = ROWS * CPR, NL = CH / THREADS;
-  static_assert(CH % THREADS == 0 && NL == 8 && THREADS / CPR == 32, "stage geometry: chunk i of a thread is row r0 + 32 i");
-  __shared__ u4 lds[2][CH];
-  __shared__ float s_sq[2][ROWS];    // per tile parity: |a|^2 of the TM rows, then |b|^2 of the TN columns
-  __shared__ int32_t s_sh[2][ROWS];  // the rows' / columns' split shifts
-
-  const int total = tm * tn, G = gridDim.x;
-  auto valid = [&](int L, int& tx, int& ty) {
-    xcd_tile_of32(L, tm, tn, tx, ty);
-    return !(sym && ty < tx);
-  };
-  auto next_tile = [&](int L, int& tx, int& ty) {
-    for (L += G; L < total; L += G)
-      if (valid(L, tx, ty)) return L;
-    return total;
-  };
-  int tx = 0, ty = 0, L = blockIdx.x;
-  while (L < total && !valid(L, tx, ty)) L += G;
-  if (L >= total) return;  // uniform: no barrier reached
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
-  const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
-  const int nst = (nkb + KB - 1) / KB;
-  // staging: chunk tid + 512 i = row r0 + 32 i (A rows for i < 4, B rows after), chunk c
-  const int r0 = tid / CPR, c = tid % CPR, blk_c = c >> 3;
-  const int dst0 = r0 * CPR + (c ^ (r0 & 15));  // + 32 CPR i (r & 15 does not change)
-  const u4* srcA;
-  const u4* srcB;
-  auto set_src = [&](int64_t m0, int64_t n0) {
-    srcA = A + (m0 + r0) * rstride + c;
-    srcB = B + (n0 + r0) * rstride + c;
-  };
-  u4 st[NL];
-  auto load = [&](int kt) {
-    // the last stage of an odd block count re-reads the block before for its missing block
-    const int64_t o = (int64_t)kt * CPR - ((kt * KB + blk_c >= nkb) ? 8 : 0);
-#pragma unroll
-    for (int i = 0; i < NL; ++i)
-      st[i] = i < NL / 2 ? srcA[o + (int64_t)32 * i * rstride] : srcB[o + (int64_t)32 * (i - NL / 2) * rstride];
-  };
-  auto put = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NL; ++i) lds[buf][dst0 + 32 * CPR * i] = st[i];
-  };
-
-  int64_t m0 = (int64_t)tx * TM, n0 = (int64_t)ty * TN;
-  set_src(m0, n0);
-  load(0);
-  put(0);
-  __syncthreads();
-
-  const int sw = lane & 15;
-  const int ra = (wm * 32 + (lane & 31)) * CPR;
-  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
-  f16v H[2], P[2], Q[2];
-  float R[2][16];  // the previous tile's results
-  int64_t pm0 = 0, pn0 = 0;
-  bool pmirror = false, pint = false;
-
-  auto mfma_stage = [&](int cur, int kt) {
-#pragma unroll
-    for (int blk = 0; blk < KB; ++blk) {
-      if (kt * KB + blk >= nkb) break;  // uniform
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ch = (8 * blk + 2 * ks + hl) ^ sw, cl = (8 * blk + 4 + 2 * ks + hl) ^ sw;
-        const h8 ah = __builtin_bit_cast(h8, lds[cur][ra + ch]);
-        const h8 al = __builtin_bit_cast(h8, lds[cur][ra + cl]);
-        const h8 bh0 = __builtin_bit_cast(h8, lds[cur][rb0 + ch]);
-        const h8 bl0 = __builtin_bit_cast(h8, lds[cur][rb0 + cl]);
-        const h8 bh1 = __builtin_bit_cast(h8, lds[cur][rb1 + ch]);
-        const h8 bl1 = __builtin_bit_cast(h8, lds[cur][rb1 + cl]);
-        H[0] = mfma32_f16(ah, bh0, H[0]);
-        H[1] = mfma32_f16(ah, bh1, H[1]);
-        P[0] = mfma32_f16(ah, bl0, P[0]);
-        P[1] = mfma32_f16(ah, bl1, P[1]);
-        Q[0] = mfma32_f16(al, bh0, Q[0]);
-        Q[1] = mfma32_f16(al, bh1, Q[1]);
-      }
-    }
-  };
-  // the previous tile's stores, in two halves (stage 0: direct, stage 1: mirrored)
-  auto store_direct = [&]() {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t row = pm0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int64_t col = pn0 + wn * 64 + 32 * j + (lane & 31);
-        if (pint || (row < M && col < N)) out[row * ldo + col] = R[j][r];
-      }
-    }
-  };
-  auto store_mirror = [&]() {
-    if (!pmirror) return;  // uniform
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = pn0 + wn * 64 + 32 * j + (lane & 31);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t row = pm0 + wm * 32 + 8 * q + 4 * hl;
-        float* d = out + col * ldo + row;
-        f4 v;
-        v.x = R[j][4 * q + 0];
-        v.y = R[j][4 * q + 1];
-        v.z = R[j][4 * q + 2];
-        v.w = R[j][4 * q + 3];
-        if (pint) {
-          *(f4*)d = v;
-        } else if (col < M) {
-          if (row + 3 < N) {
-            *(f4*)d = v;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (row + e < N) d[e] = v[e];
-          }
-        }
-      }
-    }
-  };
-
-  int tpar = 0, cur = 0;
-  bool have_prev = false;
-  while (true) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
-    int ntx = tx, nty = ty;
-    const int Ln = next_tile(L, ntx, nty);
-    const bool has_next = Ln < total;
-    // the tile's row data -> LDS (read by its epilogue, after >= 2 barriers)
-    float rsq = 0.f;
-    int32_t rsh = 0;
-    if (tid < ROWS) {
-      const int64_t ri = tid < TM ? m0 + tid : n0 + (tid - TM);
-      const int64_t rc = tid < TM ? min(ri, M - 1) : min(ri, N - 1);
-      rsq = tid < TM ? Asq[rc] : Bsq[rc];
-      rsh = tid < TM ? Ash[rc] : Bsh[rc];
-    }
-    for (int kt = 0; kt < nst; ++kt) {
-      const bool more = kt + 1 < nst;
-      if (!more) set_src(has_next ? (int64_t)ntx * TM : m0, has_next ? (int64_t)nty * TN : n0);  // the next tile's stage 0
-      load(more ? kt + 1 : 0);
-      if (kt == 0 && have_prev) store_direct();
-      if (kt == 1 && have_prev) store_mirror();
-      mfma_stage(cur, kt);
-      if (kt == 0 && tid < ROWS) {
-        s_sq[tpar][tid] = rsq;
-        s_sh[tpar][tid] = rsh;
-      }
-      put(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    }
-    // epilogue: R = exp(-g max(|a|^2 + |b|^2 - 2 dot, 0)), dot = 2^-(sa+sb) (H + (P + Q))
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cb = TM + wn * 64 + 32 * j + (lane & 31);
-      const float bsq = s_sq[tpar][cb];
-      const int bsh = s_sh[tpar][cb];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_sh[tpar][lr] + bsh));
-        R[j][r] = rbf_from_dot(s_sq[tpar][lr], bsq, dot, gamma);
-      }
-    }
-    pm0 = m0;
-    pn0 = n0;
-    pmirror = sym && ty != tx;
-    pint = m0 + TM <= M && n0 + TN <= N;
-    have_prev = true;
-    if (!has_next) break;  // uniform
-    L = Ln;
-    tx = ntx;
-    ty = nty;
-    m0 = (int64_t)tx * TM;
-    n0 = (int64_t)ty * TN;
-    tpar ^= 1;
-  }
-  store_direct();
-  store_mirror();
-}
-
-// ---------------------------------------------------------------------------
 // LDS-DMA STORE GEMM: the tile kernel's MFMA sequence (128 x 128 tile, 8 waves
 // of 32 x 64, k blocks in order: bit-identical Gram) with the operands staged
 // by global_load_lds_dwordx4 into FOUR 32-k buffers, three blocks in flight
@@ -917,128 +707,6 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_persist_k
   }
 }
 
-// ---------------------------------------------------------------------------
-// LDS-DMA ROWS GEMM (ws-cache: a round's missing kernel rows).  A = up to 192
-// rows gathered by index (the round's misses), B = the rank's rows streamed
-// from HBM once per round (one 192-row tile row, as the register-staged ROWS
-// kernel), output rows to their cache lines.  12 waves of 32 x 64; three 40 KiB
-// buffers of 32-k blocks (A 192 + B 128 rows), two in flight; every wave
-// issues exactly 4 DMA instructions per block (40 real 1 KiB pieces + 8 into
-// a scratch slot), so one counted vmcnt(4) retires a block.  Waves whose 32
-// rows all lie past the miss count only stage.  Same MFMA sequence per output
-// as every split kernel: bit-identical lines.  Measured equal to the
-// register-staged ROWS kernel (500k x 1024: 3.728 vs 3.712 s): that GEMM streams
-// the rank's X panel at HBM speed already, so it stays the default.
-// ---------------------------------------------------------------------------
-constexpr int kRowsGldsThreads = 768;
-__global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kernel(
-    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
-    const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
-    const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb, float gamma,
-    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
-  constexpr int WN = 2, TM = 192, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
-  constexpr int PIECES = ROWS / 8, WAVES = kRowsGldsThreads / 64, PER = (PIECES + WAVES - 1) / WAVES;
-  static_assert(PER == 4, "4 DMA pieces per wave and block");
-  const int64_t M = *m_dev;
-  const int64_t tx = blockIdx.x, ty = blockIdx.y;
-  const int64_t m0 = tx * TM, n0 = ty * TN;
-  if (m0 >= M) return;  // uniform: no barrier reached
-  __shared__ u4 lds[NB * BUF + 64 + 2 * TM / 4 + TM / 4];  // buffers, DMA scratch, |a|^2, shifts, out lines
-  u4* scratch = lds + NB * BUF;
-  float* s_asq = (float*)(lds + NB * BUF + 64);
-  int32_t* s_ash = (int32_t*)(lds + NB * BUF + 64) + TM;
-  int32_t* s_orow = (int32_t*)(lds + NB * BUF + 64) + 2 * TM;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
-  const int64_t rstride = (int64_t)nkb * 8;
-  if (tid < TM) {
-    const int64_t row = m0 + tid;
-    const int64_t ar = (int64_t)a_rows[min(row, M - 1)];
-    s_asq[tid] = Asq[ar];
-    s_ash[tid] = Ash[ar];
-    s_orow[tid] = row < M ? out_rows[row] : -1;
-  }
-  // piece id = wave + WAVES * i (i < 4); pieces >= PIECES land in the scratch slot
-  const u4* src[PER];
-  int dsto[PER];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int pc = wave + WAVES * i;
-    const bool real = pc < PIECES;
-    const int r = (real ? pc : 0) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int64_t grow = r < TM ? (int64_t)a_rows[min(m0 + r, M - 1)] : n0 + (r - TM);
-    src[i] = (r < TM ? A : B) + grow * rstride + c;
-    dsto[i] = real ? pc * 8 * CPR : -1;
-  }
-  auto dma = [&](int kb) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      u4* dst = dsto[i] >= 0 ? lds + (kb % NB) * BUF + dsto[i] : scratch;
-      __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    }
-  };
-  __syncthreads();
-  dma(0);
-  if (nkb > 1) dma(1);
-
-  f16v H[2], P[2], Q[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
-  const bool live = m0 + wm * 32 < M;
-  const int sw = ((lane & 31) >> 1) & 7;
-  const int ra = (wm * 32 + (lane & 31)) * CPR;
-  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
-  for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kb + 2 < nkb) dma(kb + 2);  // into the buffer of block kb - 1
-    if (live) {
-      const u4* buf = lds + (kb % NB) * BUF;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
-        const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
-        const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
-        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
-        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
-        const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
-        const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
-        H[0] = mfma32_f16(ah, bh0, H[0]);
-        H[1] = mfma32_f16(ah, bh1, H[1]);
-        P[0] = mfma32_f16(ah, bl0, P[0]);
-        P[1] = mfma32_f16(ah, bl1, P[1]);
-        Q[0] = mfma32_f16(al, bh0, Q[0]);
-        Q[1] = mfma32_f16(al, bh1, Q[1]);
-      }
-    }
-  }
-  if (!live) return;
-  const bool interior = n0 + TN <= N;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
-    const int64_t cc = col < N ? col : N - 1;
-    const float bsq = Bsq[cc];
-    const int bsh = Bsh[cc];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
-      const float v = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
-      const int32_t orow = s_orow[lr];
-      if (orow >= 0 && (interior || col < N)) out[(int64_t)orow * ldo + col] = v;
-    }
-  }
-}
-
 }  // namespace dev
 
 namespace launch {
@@ -1049,27 +717,13 @@ int g_split_variant = -1;
 
 int split_gemm_variant() {
   if (g_split_variant < 0) {
-    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 2 persistent, 3 LDS-DMA, 4 persistent LDS-DMA
+    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 3 LDS-DMA, 4 persistent LDS-DMA
     g_split_variant = e ? atoi(e) : 0;
   }
   return g_split_variant;
 }
 
 void set_split_gemm_variant(int v) { g_split_variant = v; }
-
-namespace {
-int g_rows_variant = -1;
-}
-
-int rows_gemm_variant() {
-  if (g_rows_variant < 0) {
-    const char* e = std::getenv("DPSVM_ROWS_GEMM");  // A/B: 0 / 1 register-staged ROWS kernel, 2 LDS-DMA
-    g_rows_variant = e ? atoi(e) : 0;
-  }
-  return g_rows_variant;
-}
-
-void set_rows_gemm_variant(int v) { g_rows_variant = v; }
 
 int64_t split_row_u4(int dp) { return (int64_t)((dp + 31) / 32) * 8; }
 
@@ -1123,22 +777,6 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     post_launch("rbf_gemm_split_glds", s);
     return;
   }
-  if (variant == 2 && ablate == 0 && kb == 2 && (dp + 31) / 32 > 4 && tm * tn < (1ll << 31)) {
-    // persistent, cross-tile pipelined; one workgroup per CU, a multiple of 8
-    static const int cus = [] {
-      int dev = 0, n = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      return std::max(8, n / 8 * 8);
-    }();
-    const int64_t tiles = symmetric ? tm * (tm + 1) / 2 : tm * tn;
-    const int grid = (int)std::min<int64_t>(cus, (tiles + 7) / 8 * 8);
-    dev::rbf_gemm_split_persist_kernel<<<dim3((unsigned)grid), dev::kPersistThreads, 0, s>>>(
-        (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
-        symmetric ? 1 : 0, (int)tm, (int)tn);
-    post_launch("rbf_gemm_split_persist", s);
-    return;
-  }
   auto kern = kb == 1 ? dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 1, 0>
               : ablate == 1 ? dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 2, 1>
               : ablate == 2 ? dev::rbf_gemm_split_kernel<dev::SPLIT_STORE, 4, 2, 2>
@@ -1160,13 +798,6 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
   // tiles read it once per 64 misses)
   const int64_t tm = (M_max + 191) / 192, tn = (N + 127) / 128;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed_split: N too large for grid.y");
-  if (rows_gemm_variant() == 2) {  // LDS-DMA, two 32-k blocks in flight (measured equal: HBM-bound on B, r3_rows_glds_ab.txt)
-    dev::rbf_rows_split_glds_kernel<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
-        (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
-        ldl, out_rows);
-    post_launch("rbf_rows_split_glds", s);
-    return;
-  }
   dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 6, 1, 0, 2><<<dim3((unsigned)tm, (unsigned)tn), 768, 0, s>>>(
       (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
       a_rows, out_rows, m_dev);

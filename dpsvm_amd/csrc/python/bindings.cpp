@@ -497,10 +497,8 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("xsq"), py::arg("n"), py::arg("ld"), py::arg("rows"), py::arg("m"), py::arg("gamma"),
         py::arg("out"), py::arg("out_ld"), py::arg("out_rows"), py::arg("stream"), py::arg("split") = false);
   m.def("k_set_split_gemm_variant", [](int v) { launch::set_split_gemm_variant(v); },
-        "split STORE GEMM: 0 auto (4, or 3 when dp <= 128), 1 tile per workgroup, 2 persistent register-staged, 3 LDS-DMA, 4 persistent LDS-DMA (tests / A/B)");
+        "split STORE GEMM: 0 auto (4, or 3 when dp <= 128), 1 register-staged tile per workgroup, 3 LDS-DMA, 4 persistent LDS-DMA (tests / A/B)");
   m.def("k_split_gemm_variant", []() { return launch::split_gemm_variant(); });
-  m.def("k_set_rows_gemm_variant", [](int v) { launch::set_rows_gemm_variant(v); },
-        "split ROWS GEMM (ws-cache misses): 0 auto (= 1), 1 register-staged, 2 LDS-DMA (tests / A/B)");
   m.def("k_rbf_gram_split", [](uintptr_t a, uintptr_t asq, int64_t m_, uintptr_t b, uintptr_t bsq, int64_t n, int ld,
                                float gamma, uintptr_t out, int64_t out_ld, bool sym, uintptr_t stream) {
     kernels::rbf_gram_split((const float*)a, (const float*)asq, m_, (const float*)b, (const float*)bsq, n, ld, gamma,

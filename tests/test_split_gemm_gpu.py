@@ -55,23 +55,16 @@ def test_split_gram_operand_swap_bit_identical(K):
     assert torch.equal(ab, ba.T)
 
 
-@pytest.mark.parametrize("variant,extra", [(0, 0), (2, 0), (2, 340)])
-def test_split_rows_indexed_equals_split_gram_rows(K, variant, extra):
-    """The ws-cache row GEMM (0: register-staged, the default; 2: LDS-DMA) gives
-    the Gram's rows bit for bit, for a partial 192-row tile and (extra) several."""
-    from dpsvm_amd._native import load
-
-    C = load()
+@pytest.mark.parametrize("extra", [0, 340])
+def test_split_rows_indexed_equals_split_gram_rows(K, extra):
+    """The ws-cache row GEMM gives the Gram's rows bit for bit, for a partial
+    192-row tile and (extra) several tile rows."""
     X, _ = synthetic("mnist", n=1200, seed=6)
     x = torch.from_numpy(X).cuda()
     full = K.rbf_gram(x, None, 0.25, split=True)
     rows = [5, 1199, 0, 640, 641, 77, 333, 1024] + list(range(100, 160)) + list(range(700, 700 + extra))
     lines = list(range(len(rows)))[::-1]
-    try:
-        C.k_set_rows_gemm_variant(variant)
-        got = K.rbf_rows_indexed(x, rows, 0.25, out_lines=lines, split=True)
-    finally:
-        C.k_set_rows_gemm_variant(0)
+    got = K.rbf_rows_indexed(x, rows, 0.25, out_lines=lines, split=True)
     for r, ln in zip(rows, lines):
         assert torch.equal(got[ln], full[r]), r
 
@@ -95,9 +88,9 @@ def test_split_gram_extreme_row_scales(K):
 
 @pytest.mark.parametrize("n,m,d", [(1000, 777, 784), (4133, 2300, 300), (2600, 129, 1024)])
 def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
-    """The persistent, cross-tile pipelined STORE GEMM and the LDS-DMA GEMM run
-    the tile kernel's MFMA sequence per tile: the same bits, symmetric (upper
-    tiles + mirrored stores) and plain, with partial edge tiles."""
+    """The LDS-DMA STORE GEMMs (tile per workgroup, persistent) run the
+    register-staged tile kernel's MFMA sequence per tile: the same bits,
+    symmetric (upper tiles + mirrored stores) and plain, with partial edge tiles."""
     from dpsvm_amd._native import load
 
     C = load()
@@ -109,7 +102,7 @@ def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
         C.k_set_split_gemm_variant(1)
         ref_sym, ref_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
         got = {}
-        for v in (2, 3, 4):  # persistent pipelined; LDS-DMA (three k blocks in flight); persistent LDS-DMA
+        for v in (3, 4):  # LDS-DMA (three k blocks in flight); persistent LDS-DMA
             C.k_set_split_gemm_variant(v)
             got[v] = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
     finally:
