@@ -127,6 +127,11 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
 // Decision values: dec[i] = sum_j coef[j] K(A_i, B_j) - b   (B = SVs, coef = alpha*y)
 //   partial: scratch [splits][M_pad] (returned by predict_scratch_floats)
 int64_t predict_scratch_floats(int64_t M, int64_t N);
+// the split-operand decision GEMM behind rbf_predict (dp >= 128; DPSVM_PREDICT=f32 forces the f32 kernel):
+// f32 A / B split into stream-ordered scratch, partial [<= max_splits][ldp] (unused splits zeroed)
+void rbf_predict_split(const float* A, const float* Asq, int64_t M, int lda, const float* B, const float* Bsq,
+                       const float* coef, int64_t N, int ldb, int dp, float gamma, float* partial, int64_t ldp,
+                       int max_splits, hipStream_t s);
 void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                  const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
                  float b, float* partial, float* dec, const float* y, int32_t* correct,

@@ -23,6 +23,9 @@
 // (k l>>5, col l&31); C reg r of lane l -> (row (r&3)+8(r>>2)+4(l>>5), col l&31).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
+
 #include "dpsvm/common.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
@@ -367,9 +370,18 @@ void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const flo
     splits = predict_splits(M, N);
     const int per = (int)((tn + splits - 1) / splits);
     splits = (int)((tn + per - 1) / per);
-    dev::rbf_gemm_kernel<dev::EPI_PREDICT><<<dim3((unsigned)tm, (unsigned)splits), dev::GEMM_THREADS, 0, s>>>(
-        A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, partial, ldp, coef, per, 0);
-    post_launch("rbf_predict", s);
+    static const bool f32_only = [] {
+      const char* e = std::getenv("DPSVM_PREDICT");  // A/B: f32 = the f32-input MFMA decision GEMM
+      return e && std::string(e) == "f32";
+    }();
+    if (!f32_only && dp >= 128) {
+      // split-operand fp16 MFMA with LDS-DMA staging (fp32 accuracy, rbf_gemm_split.hip)
+      rbf_predict_split(A, Asq, M, lda, B, Bsq, coef, N, ldb, dp, gamma, partial, ldp, splits, s);
+    } else {
+      dev::rbf_gemm_kernel<dev::EPI_PREDICT><<<dim3((unsigned)tm, (unsigned)splits), dev::GEMM_THREADS, 0, s>>>(
+          A, Asq, M, lda, B, Bsq, N, ldb, dp, gamma, partial, ldp, coef, per, 0);
+      post_launch("rbf_predict", s);
+    }
   } else {
     HIP_CHECK(hipMemsetAsync(partial, 0, sizeof(float) * ldp, s));
   }

@@ -707,6 +707,146 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_persist_k
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decision GEMM on split operands (predict: training accuracy, GpuPredictor,
+// svmTest, the shrinking phases' gradient update): dec_i = sum_j coef_j K(A_i,
+// B_j) with A = query rows, B = support vectors.  A workgroup owns 128 query
+// rows and a range of SV tiles; the (SV tile, k block) sequence is ONE LDS-DMA
+// pipeline (the LDS-DMA STORE kernel's staging: four 32-k buffers, three blocks
+// in flight across tile boundaries — the query panel is the same for every SV
+// tile), and each SV tile's 128 x 128 kernel block is folded into per-row sums
+// in registers (no store).  Partial sums per SV split: partial[split][row].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kGldsThreads, 1) void rbf_predict_split_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq,
+    const float* __restrict__ coef, int64_t N, int nkb, float gamma, float* __restrict__ partial, int64_t ldp,
+    int per) {
+  constexpr int WN = 2, TM = 128, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 4;
+  __shared__ u4 lds[NB * BUF + 2 * TM / 4];
+  float* s_asq = (float*)(lds + NB * BUF);
+  int32_t* s_ash = (int32_t*)(lds + NB * BUF) + TM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int64_t tn_all = (N + TN - 1) / TN;
+  const int64_t t0 = (int64_t)blockIdx.y * per, t1 = min(t0 + per, tn_all);
+  float* out = partial + (int64_t)blockIdx.y * ldp + m0;
+  if (t0 >= t1) {  // uniform: an empty split contributes zeros
+    if (tid < TM) out[tid] = 0.f;
+    return;
+  }
+  const int64_t rstride = (int64_t)nkb * 8;
+  if (tid < TM) {
+    const int64_t ri = min(m0 + tid, M - 1);
+    s_asq[tid] = Asq[ri];
+    s_ash[tid] = Ash[ri];
+  }
+  const u4* src[4];
+  bool isb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 32 * wave + 8 * i + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    isb[i] = r >= TM;
+    src[i] = r < TM ? A + (m0 + r) * rstride + c : B + (t0 * TN + (r - TM)) * rstride + c;
+  }
+  const int64_t nblk = (t1 - t0) * nkb;
+  auto dma = [&](int64_t g) {
+    const int64_t t = g / nkb, kb = g - t * nkb;
+    u4* dst = lds + (g & (NB - 1)) * BUF + 32 * wave * CPR;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(src[i] + (isb[i] ? t * TN * rstride : 0) + kb * 8),
+          (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+  };
+  __syncthreads();
+  dma(0);
+  if (nblk > 1) dma(1);
+  if (nblk > 2) dma(2);
+
+  f16v H[2], P[2], Q[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+  float acc[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  int kb = 0;
+  int64_t t = t0;
+  for (int64_t g = 0; g < nblk; ++g) {
+    const int64_t ahead = min((int64_t)2, nblk - 1 - g);
+    if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (g + 3 < nblk) dma(g + 3);
+    const u4* buf = lds + (g & (NB - 1)) * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+      const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
+      const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
+      const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+      const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+      const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
+      const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
+      H[0] = mfma32_f16(ah, bh0, H[0]);
+      H[1] = mfma32_f16(ah, bh1, H[1]);
+      P[0] = mfma32_f16(ah, bl0, P[0]);
+      P[1] = mfma32_f16(ah, bl1, P[1]);
+      Q[0] = mfma32_f16(al, bh0, Q[0]);
+      Q[1] = mfma32_f16(al, bh1, Q[1]);
+    }
+    if (++kb == nkb) {  // the SV tile is complete: fold its kernel block into the row sums
+      const int64_t n0 = t * TN;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+        const int64_t cc = col < N ? col : N - 1;
+        const float cf = col < N ? coef[cc] : 0.f;
+        const float bsq = Bsq[cc];
+        const int bsh = Bsh[cc];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
+          acc[r] += cf * rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+          H[j][r] = P[j][r] = Q[j][r] = 0.f;
+        }
+      }
+      kb = 0;
+      ++t;
+    }
+  }
+  // the 32 columns of a lane group, then the two column waves through LDS
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = acc[r];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    acc[r] = v;
+  }
+  __syncthreads();  // every wave is past its last operand read (no DMA in flight)
+  float* red = (float*)lds;  // [WN][TM]
+  if ((lane & 31) == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wn * TM + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = acc[r];
+  }
+  __syncthreads();
+  if (tid < TM) out[tid] = red[tid] + red[TM + tid];
+}
+
 }  // namespace dev
 
 namespace launch {
@@ -726,6 +866,41 @@ int split_gemm_variant() {
 void set_split_gemm_variant(int v) { g_split_variant = v; }
 
 int64_t split_row_u4(int dp) { return (int64_t)((dp + 31) / 32) * 8; }
+
+void rbf_predict_split(const float* A, const float* Asq, int64_t M, int lda, const float* B, const float* Bsq,
+                       const float* coef, int64_t N, int ldb, int dp, float gamma, float* partial, int64_t ldp,
+                       int max_splits, hipStream_t s) {
+  // both operands split into stream-ordered scratch (rows padded: the kernel reads whole 128-row tiles)
+  const int nkb = (dp + 31) / 32;
+  const int64_t pa = split_pad_rows(M), pb = split_pad_rows(N), ru = split_row_u4(dp) * 16;
+  void *a_pl = nullptr, *b_pl = nullptr;
+  int32_t *a_sh = nullptr, *b_sh = nullptr;
+  HIP_CHECK(hipMallocAsync(&a_pl, (size_t)(pa * ru), s));
+  HIP_CHECK(hipMallocAsync(&b_pl, (size_t)(pb * ru), s));
+  HIP_CHECK(hipMallocAsync((void**)&a_sh, (size_t)pa * 4, s));
+  HIP_CHECK(hipMallocAsync((void**)&b_sh, (size_t)pb * 4, s));
+  HIP_CHECK(hipMemsetAsync(a_pl, 0, (size_t)(pa * ru), s));
+  HIP_CHECK(hipMemsetAsync(b_pl, 0, (size_t)(pb * ru), s));
+  HIP_CHECK(hipMemsetAsync(a_sh, 0, (size_t)pa * 4, s));
+  HIP_CHECK(hipMemsetAsync(b_sh, 0, (size_t)pb * 4, s));
+  split_rows_f16(A, M, dp, lda, a_pl, a_sh, s);
+  split_rows_f16(B, N, dp, ldb, b_pl, b_sh, s);
+  const int64_t tm = (M + 127) / 128, tn = (N + 127) / 128;
+  // ~2 workgroups per CU of a 256-CU device, at most the scratch's splits
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>({(int64_t)max_splits, tn, (512 + tm - 1) / tm}));
+  const int per = (int)((tn + splits - 1) / splits);
+  splits = (tn + per - 1) / per;
+  dev::rbf_predict_split_kernel<<<dim3((unsigned)tm, (unsigned)splits), dev::kGldsThreads, 0, s>>>(
+      (const dev::u4*)a_pl, a_sh, Asq, M, (const dev::u4*)b_pl, b_sh, Bsq, coef, N, nkb, gamma, partial, ldp, per);
+  post_launch("rbf_predict_split", s);
+  // zero the splits the reduce reads beyond the launched ones
+  if (splits < max_splits)
+    HIP_CHECK(hipMemsetAsync(partial + splits * ldp, 0, (size_t)(max_splits - splits) * ldp * 4, s));
+  HIP_CHECK(hipFreeAsync(a_pl, s));
+  HIP_CHECK(hipFreeAsync(b_pl, s));
+  HIP_CHECK(hipFreeAsync(a_sh, s));
+  HIP_CHECK(hipFreeAsync(b_sh, s));
+}
 
 int64_t split_pad_rows(int64_t rows) { return (rows + 255) / 256 * 256 + 256; }
 
