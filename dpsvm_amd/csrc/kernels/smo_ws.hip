@@ -342,10 +342,15 @@ constexpr int ws_parts() {
 // f_j over the changed rows j, c_j = d_alpha_j y_j), MODE 2 takes
 // t = min(1, g'd / d'Qd) from the partials (fixed order: every workgroup the
 // same t), applies f += t d_f and alpha = alpha_new - (1 - t) d_alpha, then
-// selects the candidates.
+// selects the candidates.  Pass 2 walks no list: one partition, 256 threads.
 template <int RPT, int MODE>
-__global__ __launch_bounds__(kWsSelThreads * ws_parts<RPT>()) void ws_select_kernel(WsArgs a) {
-  constexpr int PARTS = ws_parts<RPT>();
+constexpr int ws_sel_parts() {
+  return MODE == 2 ? 1 : ws_parts<RPT>();
+}
+
+template <int RPT, int MODE>
+__global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void ws_select_kernel(WsArgs a) {
+  constexpr int PARTS = ws_sel_parts<RPT, MODE>();
   constexpr int CH = RPT >= 32 ? 1 : RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
   constexpr int LMAX = MODE == 1 ? kWsMaxAll : MODE == 0 ? kWsMax : 1;
   __shared__ int32_t s_idx[LMAX];  // lines of the changed rows
@@ -1884,7 +1889,7 @@ bool ws_supported(int64_t nl_max, int world, int q_max) {
 template <int MODE>
 static void ws_select_mode(const WsArgs& a, hipStream_t s) {
   const dim3 grid(a.G * (MODE == 1 ? std::max(1, a.ks) : 1));
-  auto threads = [](int rpt) { return dim3(kWsSelThreads * (rpt <= 4 ? 4 : rpt <= 16 ? 2 : 1)); };
+  auto threads = [](int rpt) { return dim3(MODE == 2 ? kWsSelThreads : kWsSelThreads * (rpt <= 4 ? 4 : rpt <= 16 ? 2 : 1)); };
   if (a.rpt <= 1) dev::ws_select_kernel<1, MODE><<<grid, threads(1), 0, s>>>(a);
   else if (a.rpt <= 2) dev::ws_select_kernel<2, MODE><<<grid, threads(2), 0, s>>>(a);
   else if (a.rpt <= 4) dev::ws_select_kernel<4, MODE><<<grid, threads(4), 0, s>>>(a);
