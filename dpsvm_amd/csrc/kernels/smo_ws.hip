@@ -1491,8 +1491,9 @@ __device__ __forceinline__ float sel_lanes(float a, float b, uint64_t m) {
   return r;
 }
 
-__device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, int lane, float C, float (&fu)[3],
-                                         float (&fl)[3]) {
+template <int NS>
+__device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, int lane, float C, float (&fu)[NS],
+                                         float (&fl)[NS]) {
   const float INF = __builtin_inff();
   // the operands are uniform: each test as a wave mask (all ones or zero; wave
   // 0 runs with a full exec mask) keeps the set logic on the scalar unit
@@ -1508,7 +1509,7 @@ __device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, 
   const int s = pos >> 6;
   (void)lane;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < NS; ++k) {
     const uint64_t w = s == k ? bit : 0ull;
     fu[k] = sel_lanes(fu[k], nu, w);
     fl[k] = sel_lanes(fl[k], nl, w);
@@ -1587,6 +1588,14 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
   return (int)r;
 }
 
+__device__ __forceinline__ int ws_argpos(const float (&x)[2], float v) {
+  const uint64_t m0 = __ballot(x[0] == v), m1 = __ballot(x[1] == v);
+  const uint32_t r0 = sff1_u64(m0), r1 = sff1_u64(m1) | 64u;
+  uint32_t r;
+  asm volatile("s_min_u32 %0, %1, %2" : "=s"(r) : "s"(r0), "s"(r1));
+  return (int)r;
+}
+
 // kFull: q_max == kWsMax, the three 64-row slots fill a sub-Gram row (stride
 // 192): row reads need no clamp (columns q..191 hold zeros) and take immediate
 // LDS offsets
@@ -1595,8 +1604,11 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
 // I_low row with f_lo > b_hi that maximises (f_lo - b_hi)^2 / eta(hi, lo) —
 // the pair whose step gains the most dual objective — instead of argmax f.
 // The stop test stays the reference's first-order one (b_lo = max f over I_low).
-template <bool kBox, bool kFull, bool kMulti, bool kW2>
+// NS: 64-row slots per lane (3 for q_max <= 192, 2 for q_max <= 128 — the
+// multi-block rounds' 96-row blocks: a third less work per pair step)
+template <bool kBox, bool kFull, bool kMulti, bool kW2, int NS = 3>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
+  static_assert(NS == 3 || (NS == 2 && !kFull), "slots");
   extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
   __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
   __shared__ int32_t s_idx[kWsMax], s_line[kWsMax];
@@ -1651,9 +1663,9 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const float INF = __builtin_inff();
   const float C = a.C;
   const float eps_in = fmaxf(a.eps_floor, a.rel_local * 0.5f * (b_lo - b_hi));
-  float fu[3], fl[3], yr[3], a0[3];
+  float fu[NS], fl[NS], yr[NS], a0[NS];
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < NS; ++s) {
     const int p = lane + 64 * s;
     const bool v = p < q;
     const float fv = v ? s_f[p] : 0.f;
@@ -1672,14 +1684,17 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   int inner = 0;
   bool bad = false, clipped_any = false;
   while (inner < cap) {
-    float mu = fminf(fminf(fu[0], fu[1]), fu[2]);
-    float ml = fminf(fminf(fl[0], fl[1]), fl[2]);
+    float mu = fminf(fu[0], fu[1]), ml = fminf(fl[0], fl[1]);
+    if constexpr (NS == 3) {
+      mu = fminf(mu, fu[2]);
+      ml = fminf(ml, fl[2]);
+    }
     wave_min2_f32(mu, ml);
     const float bh = mu;
     float bl = -ml;  // first order: b_lo = max f over I_low (also the stop test's)
     const int ph = ws_argpos(fu, mu);
     int pl = -1;
-    float kh[3], kl[3];
+    float kh[NS], kl[NS];
     if constexpr (!kW2) pl = ws_argpos(fl, ml);
     // one exit test: an empty side, the sub-problem's stop test, or NaN
     const bool open = (mu < INF) & (ml < INF) & (bl > bh + 2.0f * eps_in);
@@ -1688,21 +1703,23 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
         // hi's sub-Gram row first, then the gain of every violating I_low row
         // as a minimum of -gain (INF: not a candidate)
 #pragma unroll
-        for (int s = 0; s < 3; ++s) kh[s] = K[ph * ldk + (kFull ? lane + 64 * s : min(lane + 64 * s, q - 1))];
-        float g[3];
+        for (int s = 0; s < NS; ++s) kh[s] = K[ph * ldk + (kFull ? lane + 64 * s : min(lane + 64 * s, q - 1))];
+        float g[NS];
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
+        for (int s = 0; s < NS; ++s) {
           const float dv = -fl[s] - bh;
           float eta = (1.0f + 1.0f) - 2.0f * kh[s];
           eta = eta >= a.tau ? eta : a.tau;
           g[s] = ((fl[s] < INF) & (dv > 0.f)) ? -(dv * dv) * __builtin_amdgcn_rcpf(eta) : INF;
         }
-        float gm = fminf(fminf(g[0], g[1]), g[2]), gm2 = gm;
+        float gm = fminf(g[0], g[1]);
+        if constexpr (NS == 3) gm = fminf(gm, g[2]);
+        float gm2 = gm;
         wave_min2_f32(gm, gm2);
         pl = gm < INF ? ws_argpos(g, gm) : -1;
         if (pl >= 0) {
           const int sl = pl >> 6;
-          bl = -readlane_f32(sl == 0 ? fl[0] : sl == 1 ? fl[1] : fl[2], pl & 63);  // f of the chosen lo
+          bl = -readlane_f32(sl == 0 ? fl[0] : (NS == 2 || sl == 1) ? fl[1] : fl[NS - 1], pl & 63);  // f of the chosen lo
         }
       }
     }
@@ -1715,7 +1732,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     const float a_hi = s_a[ph], y_hi = s_y[ph], a_lo = s_a[pl], y_lo = s_y[pl];
     const float khl = K[ph * ldk + pl], klh = K[pl * ldk + ph], khh = K[ph * ldk + ph], kll = K[pl * ldk + pl];
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
+    for (int s = 0; s < NS; ++s) {
       const int p = kFull ? lane + 64 * s : min(lane + 64 * s, q - 1);
       if constexpr (!kW2) kh[s] = K[ph * ldk + p];
       kl[s] = K[pl * ldk + p];
@@ -1725,7 +1742,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     if (kMulti && !kBox) clipped_any |= clipped;
     float f_lo_new, f_hi_new;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
+    for (int s = 0; s < NS; ++s) {
       float dl;
       {
 #pragma clang fp contract(off)
@@ -1752,7 +1769,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   // ---- commit: alphas, the changed rows for the f update, control, status ----
   int n_apply = 0;
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < NS; ++s) {
     const int p = lane + 64 * s;
     const float an = p < q ? s_a[p] : 0.f;
     const bool nz = p < q && an != a0[s];
@@ -1972,12 +1989,20 @@ void ws_solve(const WsArgs& a, hipStream_t s) {
       dev::ws_solve_kernel<true, false, true, W2>, dev::ws_solve_kernel<true, true, true, W2>
   static const Fn fns[16] = {WS_SOLVE_FNS(false), WS_SOLVE_FNS(true)};
 #undef WS_SOLVE_FNS
+  // two slots per lane when q_max <= 128 (never kFull)
+#define WS_SOLVE_FNS2(W2)                                                                                        \
+  dev::ws_solve_kernel<false, false, false, W2, 2>, dev::ws_solve_kernel<true, false, false, W2, 2>,            \
+      dev::ws_solve_kernel<false, false, true, W2, 2>, dev::ws_solve_kernel<true, false, true, W2, 2>
+  static const Fn fns2[8] = {WS_SOLVE_FNS2(false), WS_SOLVE_FNS2(true)};
+#undef WS_SOLVE_FNS2
   const int v = (w2 ? 8 : 0) + (multi ? 4 : 0) + (box ? 2 : 0) + (full ? 1 : 0);
-  const Fn fn = fns[v];
+  const bool two = a.q_max <= 128;
+  const Fn fn = two ? fns2[(w2 ? 4 : 0) + (multi ? 2 : 0) + (box ? 1 : 0)] : fns[v];
   // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
   static size_t attr[16] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024,
                             64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
-  size_t& at = attr[v];
+  static size_t attr2[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
+  size_t& at = two ? attr2[(w2 ? 4 : 0) + (multi ? 2 : 0) + (box ? 1 : 0)] : attr[v];
   if (lds > at) {
     HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     at = lds;
