@@ -1155,14 +1155,15 @@ __device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* v
 // real keys are unique (the global row index is in the low bits), so these
 // counts are a permutation of [0, n_real); the absent keys (kKeyNone) fill the
 // tail.  Each workgroup holds its side's NK keys in LDS and ranks KPW of them,
-// SUB threads per key each counting over every SUB-th key pair (the SUB lanes of
-// one key read 8 consecutive 16-B pairs: no bank conflict, broadcast over keys).
-constexpr int kRankThreads = 256;
+// SUB = 16 threads per key each counting over every SUB-th key pair (the SUB
+// lanes of one key read 16 consecutive 16-B pairs: no bank conflict, broadcast
+// over keys).
+constexpr int kRankThreads = 512;
 constexpr int kRankChunks = 64;
 __global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
   constexpr int NK = kWsMaxGroups * kWsCand;
   constexpr int KPW = NK / kRankChunks, SUB = kRankThreads / KPW, PAIRS = NK / (2 * SUB);
-  static_assert(NK % kRankChunks == 0 && kRankThreads % KPW == 0 && SUB == 8 && NK % (2 * SUB) == 0, "rank geometry");
+  static_assert(NK % kRankChunks == 0 && kRankThreads % KPW == 0 && SUB == 16 && NK % (2 * SUB) == 0, "rank geometry");
   __shared__ uint64_t s_k[NK];
   __shared__ int s_real[kRankThreads / 64];
   const WsCtrl* c = a.ctrl;
