@@ -369,12 +369,23 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
       s_idx[k] = c->apply_line[k];
       s_coef[k] = c->apply_coef[k];
     }
-  } else if constexpr (MODE == 1) {
-    // the blocks' apply segments, concatenated in block order
+  }
+  // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers.
+  // MODE 1 runs KS = a.ks workgroups per row group, each over its KS-th of the
+  // changed-row list (pass 1 fills the device when G is small: 30 groups per rank at
+  // 8 ranks on the headline); pass 2 sums the KS partial changes in slice order.
+  const int KS = MODE == 1 ? max(1, a.ks) : 1;
+  const int grp = MODE == 1 ? (int)(blockIdx.x % a.G) : (int)blockIdx.x, ksi = MODE == 1 ? (int)(blockIdx.x / a.G) : 0;
+  if constexpr (MODE == 1) {
+    // the blocks' apply segments, concatenated in block order; this workgroup
+    // loads only its slice [e_lo, e_hi) of the list (at their list positions)
+    const int per_wg = PARTS * ((na + PARTS * KS - 1) / (PARTS * KS));
+    const int e_lo = min(na, ksi * per_wg), e_hi = min(na, e_lo + per_wg);
     int at = 0;
-    for (int p = 0; p < a.blocks; ++p) {
+    for (int p = 0; p < a.blocks && at < e_hi; ++p) {
       const int nb = c->nab[p];
-      for (int k = threadIdx.x; k < nb; k += kWsSelThreads * PARTS) {
+      const int k0 = max(0, e_lo - at), k1 = min(nb, e_hi - at);
+      for (int k = k0 + threadIdx.x; k < k1; k += kWsSelThreads * PARTS) {
         s_idx[at + k] = c->apply_line[p * a.q_max + k];
         s_coef[at + k] = c->apply_coef[p * a.q_max + k];
       }
@@ -382,12 +393,6 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
     }
   }
   __syncthreads();
-  // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers.
-  // MODE 1 runs KS = a.ks workgroups per row group, each over its KS-th of the
-  // changed-row list (pass 1 fills the device when G is small: 30 groups per rank at
-  // 8 ranks on the headline); pass 2 sums the KS partial changes in slice order.
-  const int KS = MODE == 1 ? max(1, a.ks) : 1;
-  const int grp = MODE == 1 ? (int)(blockIdx.x % a.G) : (int)blockIdx.x, ksi = MODE == 1 ? (int)(blockIdx.x / a.G) : 0;
   const int64_t base = (int64_t)grp * a.rpt * kWsSelThreads + tid;
   float f[RPT];
   bool has[RPT];
