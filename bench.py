@@ -3,8 +3,11 @@
 even/odd shape (60000 x 784, RBF, C=10, gamma=0.25) — BASELINE.json's metric.
 
   python bench.py --gpus N --steps K --warmup W
-  (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
-          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+  (N > 1: either under python -m torch.distributed.run --nnodes=1
+          --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py
+          --gpus N ..., or plain `bench.py --gpus N`, which starts those N
+          ranks itself before touching the GPU and relays rank 0's line; a
+          rank count other than N is an error, never a silent downgrade)
 
 One "step" = one complete training run from alpha = 0 to convergence: state
 init, the resident Gram shard (MFMA GEMM) and the device-resident SMO loop —
@@ -135,8 +138,90 @@ def parse(argv=None):
     return a
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _visible_devices() -> int:
+    """Device count WITHOUT initialising the GPU (torch.cuda.device_count()
+    does not on this image; is_available() would)."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def spawn_ranks(a, argv) -> int:
+    """``--gpus N`` (N > 1) outside a torch.distributed launch: start the N
+    ranks ourselves — one process per GPU over torch.distributed.run, the
+    replacement of the reference's ``mpirun -np P`` (Makefile:74) — and relay
+    rank 0's JSON line.  Runs BEFORE anything touches the GPU (this process
+    never initialises HIP, and it never exec()s: the ranks are children).
+    Fails non-zero when a rank fails, no JSON line arrives, or the line does
+    not report N ranks — never a silent one-rank downgrade."""
+    import subprocess
+
+    n = a.gpus
+    if a.device != "cpu":
+        have = _visible_devices()
+        shared = os.environ.get("DPSVM_FORCE_DEVICE")
+        if (a.device == "cuda" or have > 0) and have < n and not shared:
+            print(f"[bench] --gpus {n} but only {have} visible device(s); set DPSVM_FORCE_DEVICE=<id> "
+                  f"to rehearse {n} ranks sharing one device", file=sys.stderr)
+            return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["DPSVM_BENCH_SPAWNED"] = str(n)
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *argv]
+    print(f"[bench] spawning {n} ranks: {' '.join(cmd[2:])}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    result = None
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{"):
+            try:
+                result = json.loads(s)
+            except ValueError:
+                print(line, end="", file=sys.stderr)
+                continue
+        else:
+            print(line, end="", file=sys.stderr, flush=True)  # rank chatter: keep stdout one JSON line
+    rc = proc.wait()
+    if rc != 0:
+        print(f"[bench] a rank failed (torch.distributed.run exit {rc})", file=sys.stderr)
+        return rc if rc > 0 else 1
+    if result is None:
+        print("[bench] no JSON line from rank 0", file=sys.stderr)
+        return 1
+    if int(result.get("n_gpus", 0)) != n:
+        print(f"[bench] rank 0 reported n_gpus={result.get('n_gpus')} for --gpus {n}", file=sys.stderr)
+        return 1
+    result["launcher"] = "bench.py spawned torch.distributed.run"
+    line = json.dumps(result)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
 def main(argv=None) -> int:
-    a = parse(argv)
+    raw_argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(raw_argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a, raw_argv)
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -162,8 +247,9 @@ def main(argv=None) -> int:
         if on_gpu:
             torch.cuda.synchronize()
 
-    if ctx.world != a.gpus and ctx.rank == 0:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
+    if ctx.world != a.gpus:
+        # never benchmark a different rank count than asked for
+        raise SystemExit(f"[bench] --gpus {a.gpus} but WORLD_SIZE={ctx.world}")
     n_ranks = ctx.world
 
     X, y = synthetic(a.data, n=a.samples, d=a.features, seed=a.seed)

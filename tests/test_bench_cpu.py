@@ -47,3 +47,30 @@ def test_bench_multirank_launch_contract():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4" and out["converged"]
     assert out["steps"] == 1 and out["warmup"] == 1 and out["value"] > 0
+
+
+def test_bench_spawns_its_own_ranks():
+    """``bench.py --gpus N`` without a launcher starts the N ranks itself
+    (torch.distributed.run child, never an exec) and relays rank 0's line."""
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--samples", "2000",
+             "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.strip().split("\n") if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["converged"]
+    assert out["launcher"].startswith("bench.py spawned")
+
+
+def test_bench_refuses_missing_devices_and_rank_mismatch():
+    # --device cuda with fewer visible devices than --gpus: a clear non-zero exit, no silent downgrade
+    env = dict(os.environ)
+    env.pop("DPSVM_FORCE_DEVICE", None)
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cuda",
+             "--samples", "500"], env=env)
+    assert r.returncode == 2 and "visible device" in r.stderr
+    # launched with a different rank count than --gpus: refused
+    env["WORLD_SIZE"], env["RANK"], env["LOCAL_RANK"] = "1", "0", "0"
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+             "--samples", "500"], env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
