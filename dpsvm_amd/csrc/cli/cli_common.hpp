@@ -79,14 +79,16 @@ inline void usage_train(const char* prog, bool seq) {
                "   --rows-per-group N  :  rows per workgroup of the fused/persistent engines (multiple of 256)\n"
                "   --xch-poll-batch N --xch-sleep N --xch-stride N --xch-mem auto|uncached|coarse\n"
                "   --xch-timeout S     :  give-up bound of one in-kernel exchange poll (default 120)\n"
-               "   --watchdog S        :  host bound on one block of iterations (default 1800)\n"
+               "   --watchdog S        :  host bound on one block of iterations (default 0 = auto: 1800 s,\n"
+               "                          adaptive to the block time with several ranks)\n"
                "   --census-groups N   :  residency census grid of the persistent engines (tests)\n"
                "   --no-verify-ranks   :  skip the cross-rank alpha digest (world > 1)\n"
                "   --solver S          :  auto (ws from 50k rows, else smo) | smo (pair-at-a-time engines) | ws (working-set rounds)\n"
                "   --ws-size N         :  working-set rows of the ws engine (<= 192, default 192)\n"
                "   --ws-new N --ws-rel R --ws-inner N --ws-block N :  ws engine round parameters\n"
                "   --ws-wss 1|2        :  sub-problem pair choice: 1 first order (reference), 2 second order\n"
-               "   --ws-blocks P       :  up to P sub-problems per round on P workgroups (1..32; default 0 = auto:\n"
+               "   --ws-blocks P       :  up to P sub-problems per round on P workgroups (1..32, P x ws-size <= 3072;\n"
+               "                          default 0 = auto:\n"
                "                          32 blocks of 96 rows from 50k rows, halved after every damped round)\n"
                "   --shrink            :  one GPU: LIBSVM-style shrinking (phases on the rows that can still violate)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"

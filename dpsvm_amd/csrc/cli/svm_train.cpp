@@ -121,9 +121,16 @@ int main(int argc, char** argv) {
         first_fail.compare_exchange_strong(none, r);
         // abort EVERY rank's communicator: peers blocked in a collective (or a
         // captured round graph) on a dead rank return now instead of at their
-        // watchdog, and fail with "communicator aborted"
+        // watchdog, and fail with "communicator aborted".  Only a REQUEST for
+        // the other ranks' communicators: each owning thread carries it out
+        // (RCCL: ncclCommAbort on the thread that enqueues, never under it)
         if (world > 1)
-          for (auto& c : comms) c->abort();
+          for (int q = 0; q < world; ++q) {
+            if (q == r)
+              comms[q]->abort();
+            else
+              comms[q]->request_abort();
+          }
       }
     };
     if (world == 1) {
@@ -133,7 +140,21 @@ int main(int argc, char** argv) {
       for (int r = 0; r < world; ++r) ts.emplace_back(rank_main, r);
       for (auto& t : ts) t.join();
     }
-    if (first_fail.load() >= 0) std::rethrow_exception(errs[first_fail.load()]);
+    if (first_fail.load() >= 0) {
+      // the peers' errors are consequences (aborted communicators): report
+      // them after the root cause, which is what the process fails with
+      for (int q = 0; q < world; ++q) {
+        if (q == first_fail.load() || !errs[q]) continue;
+        try {
+          std::rethrow_exception(errs[q]);
+        } catch (const std::exception& e) {
+          std::cerr << "svmTrain: rank " << q << " (after rank " << first_fail.load() << " failed): " << e.what()
+                    << "\n";
+        }
+      }
+      std::cerr << "svmTrain: rank " << first_fail.load() << " failed first (root cause)\n";
+      std::rethrow_exception(errs[first_fail.load()]);
+    }
 
     SolveResult& r0 = results[0];
     cli::print_outcome(r0, o.p.eps);

@@ -6,7 +6,9 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
+#include <thread>
 
 #include "dpsvm/comm.hpp"
 #include "dpsvm/common.hpp"
@@ -43,59 +45,87 @@ class RcclComm final : public Communicator {
   bool device_memory() const override { return true; }
   std::string name() const override { return "rccl"; }
 
+  // Every collective runs under mu_ with the handle checked inside the lock,
+  // so an abort can never free the communicator between the check and the
+  // enqueue; ncclCommAbort itself only ever runs on the thread that issues the
+  // collectives (abort() / a pending request seen by live() or async_error()).
   void allreduce_min_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    std::lock_guard<std::mutex> lk(mu_);
     RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclMin, live(), s));
   }
   void allreduce_sum_f64(double* buf, size_t count, hipStream_t s) override {
+    std::lock_guard<std::mutex> lk(mu_);
     RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, live(), s));
   }
   void allreduce_sum_f32(float* buf, size_t count, hipStream_t s) override {
+    std::lock_guard<std::mutex> lk(mu_);
     RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, live(), s));
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    std::lock_guard<std::mutex> lk(mu_);
     RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, live(), s));
   }
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+    std::lock_guard<std::mutex> lk(mu_);
     RCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, live(), s));
   }
   void barrier() override {
     HIP_CHECK(hipSetDevice(device_));
-    RCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, live(), bstream_));
-    HIP_CHECK(hipStreamSynchronize(bstream_));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      RCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, live(), bstream_));
+    }
+    // bounded by the same abort path as the solver's waits: a peer that died
+    // before the barrier makes this rank fail once someone requests the abort
+    while (true) {
+      hipError_t q = hipStreamQuery(bstream_);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) HIP_CHECK(q);
+      std::string err = async_error();
+      if (!err.empty()) ::dpsvm::fail("RCCL barrier failed on rank " + std::to_string(rank_) + ": " + err);
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
   std::string async_error() override {
-    if (aborted_.load()) return "communicator aborted";
     std::lock_guard<std::mutex> lk(mu_);
+    if (abort_req_.load() && comm_) abort_locked();
     if (!comm_) return "communicator aborted";
     ncclResult_t e = ncclSuccess;
     if (ncclCommGetAsyncError(comm_, &e) != ncclSuccess) return "ncclCommGetAsyncError failed";
     return e == ncclSuccess ? std::string() : std::string(ncclGetErrorString(e));
   }
-  // Immediate: ncclCommAbort raises the communicator's abort flag, which its
-  // in-flight kernels poll, so a collective blocked on a dead peer ends now
-  // (the solver's wait loop then sees async_error() and fails) instead of when
-  // the watchdog fires.  Safe from any thread; the handle is gone afterwards
-  // and every later call fails with "communicator aborted".
+  // Owning thread: ncclCommAbort raises the communicator's abort flag, which
+  // its in-flight kernels poll, so a collective blocked on a dead peer ends now
+  // (the solver's wait loop then fails) instead of when the watchdog fires.
+  // Every later call fails with "communicator aborted"; a hipGraph holding
+  // this communicator's nodes must not be launched again (the solver checks
+  // async_error() before every block).
   void abort() override {
-    if (aborted_.exchange(true)) return;
+    abort_req_.store(true);
     std::lock_guard<std::mutex> lk(mu_);
-    if (comm_) {
-      (void)hipSetDevice(device_);
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-    }
+    if (comm_) abort_locked();
   }
+  // Other threads: only the request (ncclCommAbort racing the owner's
+  // enqueue would free the handle under it).
+  void request_abort() override { abort_req_.store(true); }
 
  private:
+  void abort_locked() {
+    (void)hipSetDevice(device_);
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+  // with mu_ held
   ncclComm_t live() {
-    if (aborted_.load()) ::dpsvm::fail("RCCL communicator aborted (rank " + std::to_string(rank_) + ")");
+    if (abort_req_.load() && comm_) abort_locked();
+    if (!comm_) ::dpsvm::fail("RCCL communicator aborted (rank " + std::to_string(rank_) + ")");
     return comm_;
   }
   ncclComm_t comm_ = nullptr;
   int rank_, world_, device_;
   void* scratch_ = nullptr;
   hipStream_t bstream_ = nullptr;
-  std::atomic<bool> aborted_{false};
+  std::atomic<bool> abort_req_{false};
   std::mutex mu_;
 };
 

@@ -41,9 +41,17 @@ class Communicator {
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t stream) = 0;
   virtual void broadcast(void* buf, size_t bytes, int root, hipStream_t stream) = 0;
   virtual void barrier() = 0;
-  // RCCL: poll async errors (watchdog); others: no-op
+  // RCCL: poll async errors (watchdog); others: no-op.  Called by the thread
+  // that issues this communicator's collectives; it also carries out an abort
+  // requested by another thread (request_abort), so a peer's failure ends a
+  // collective blocked on it.
   virtual std::string async_error() { return {}; }
+  // abort NOW, from the thread that issues this communicator's collectives
   virtual void abort() {}
+  // any thread (e.g. a failed rank thread for its peers): ask for an abort;
+  // the owning thread performs it at its next collective or async_error()
+  // poll.  Host communicators abort at once (their abort is thread-safe).
+  virtual void request_abort() { abort(); }
 };
 
 std::unique_ptr<Communicator> make_local_comm();

@@ -50,6 +50,9 @@ enum class ClipMode : int {
   Box = 1,          // LIBSVM-style joint [L,H] box, keeps sum(alpha*y) = 0
 };
 
+// host bound on one block of iterations when SolverParams::watchdog_s is 0 (auto)
+constexpr double kWatchdogDefaultS = 1800.0;
+
 struct SolverParams {
   float C = 1.0f;
   float gamma = -1.0f;        // <0 -> 1/d (reference uses integer 1/d == 0)
@@ -97,7 +100,8 @@ struct SolverParams {
   int xch_stride = 4;         // u64 slots per exchange entry (>= 4; larger pads entries apart)
   int xch_mem = 0;            // receive buffer: 0 auto (uncached when world > 1), 1 uncached, 2 coarse
   double xch_timeout_s = 120.0;  // give-up bound of one in-kernel poll loop (then status 5)
-  double watchdog_s = 1800.0;    // host bound on one block of iterations
+  double watchdog_s = 0.0;       // host bound on one block of iterations (s); 0 = auto: 1800, and at
+                                 // world > 1 adaptive (120 s for the first blocks, then 50x the slowest)
   // residency census of the persistent engines (tests: a grid of this many
   // workgroups instead of the engine's, > the device's capacity forces the
   // fallback to the one-launch-per-iteration engine)
@@ -118,8 +122,8 @@ struct SolverParams {
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
   int ws_new = 0;             // rows replaced per round (0: 3 ws_size / 4)
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
-  int ws_blocks = 0;          // ws-dense: up to P disjoint q-row sub-problems per round (1..8; 0 auto = 8 from 50k
-                              // rows).  Adaptive: halved after every damped round (coupled blocks), 1 after an
+  int ws_blocks = 0;          // working-set engines: up to P disjoint q-row sub-problems per round (1..32,
+                              // P x ws_size <= 3072; 0 auto = 32 blocks of 96 rows from 50k rows, else 1).  Adaptive: halved after every damped round (coupled blocks), 1 after an
                               // independent-clip event, then the one-block round kernels (smo_ws.hip)
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_wss = 0;             // sub-problem pair choice: 1 the reference's first-order rule (max f over I_low),

@@ -10,6 +10,11 @@
 //                        must fail (bounded exchange polls, collective errors,
 //                        watchdog) instead of hanging, and the last checkpoint
 //                        resumes the run (any rank count).
+//   DPSVM_FAULT=throw@K:R rank R's solve throws (its thread / process stays
+//                        alive) at the first block boundary at/after iteration
+//                        K: in-process ranks (svmTrain --ranks / -p) must
+//                        abort their peers' communicators and report rank R's
+//                        error as the root cause.
 //   DPSVM_VERIFY=1       after solve: alpha in [0, C], f recomputed from alpha,
 //                        and the cross-rank alpha digest (the digest alone runs
 //                        by default at world > 1: SolverParams::verify_ranks).
@@ -66,13 +71,17 @@ inline int64_t fault_nan_iter() {
 }
 
 // DPSVM_FAULT=exit@K:R -> K when this is rank R, else -1
-inline int64_t fault_exit_iter(int rank) {
+inline int64_t fault_rank_iter(const char* kind, int rank) {
   const char* e = std::getenv("DPSVM_FAULT");
-  if (!e || strncmp(e, "exit@", 5) != 0) return -1;
-  const char* c = strchr(e + 5, ':');
+  const size_t k = strlen(kind);
+  if (!e || strncmp(e, kind, k) != 0) return -1;
+  const char* c = strchr(e + k, ':');
   if (!c || atoi(c + 1) != rank) return -1;
-  return atoll(e + 5);
+  return atoll(e + k);
 }
+inline int64_t fault_exit_iter(int rank) { return fault_rank_iter("exit@", rank); }
+// DPSVM_FAULT=throw@K:R -> K when this is rank R, else -1
+inline int64_t fault_throw_iter(int rank) { return fault_rank_iter("throw@", rank); }
 
 inline bool verify_enabled() {
   const char* e = std::getenv("DPSVM_VERIFY");

@@ -68,19 +68,22 @@ void GpuSolver::Impl::init_ctrl(int64_t iter0, float b_hi, float b_lo) {
 void GpuSolver::Impl::wait_event(hipEvent_t e) {
   // bounded wait with async-error polling (SURVEY §5.3 watchdog)
   auto t0 = Clock::now();
-  const double limit = wd_limit > 0.0 ? wd_limit : p.watchdog_s;
+  const double limit = wd_limit > 0.0 ? wd_limit : (p.watchdog_s > 0.0 ? p.watchdog_s : kWatchdogDefaultS);
   int spins = 0;
   while (true) {
     hipError_t q = hipEventQuery(e);
-    if (q == hipSuccess) return;
-    if (q != hipErrorNotReady) HIP_CHECK(q);
+    if (q != hipSuccess && q != hipErrorNotReady) HIP_CHECK(q);
     if (world > 1) {
+      // also after a completed event: kernels of an aborted communicator exit
+      // and their events complete, and the next block must not relaunch a
+      // graph whose collective nodes point at the freed communicator
       std::string err = comm->async_error();
       if (!err.empty()) {
         comm->abort();
         fail("collective failed on rank " + std::to_string(rank) + ": " + err);
       }
     }
+    if (q == hipSuccess) return;
     if (secs_since(t0) > limit) {
       if (world > 1) comm->abort();
       fail("watchdog: SMO block did not finish within " + std::to_string(limit) + " s");
@@ -501,17 +504,18 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool multi_comm = m.world == 1 || m.comm->device_memory() || m.p.exchange == 1;
   // ws_blocks auto (0): every block from kWsAutoBlocksRows rows on (the round's
   // fixed cost is amortised over P sub-problems; small problems need few rounds)
-  // auto: kWsAutoBlocks (16) blocks of kWsMaxAll / 16 = 96 rows (the union
+  // auto: kWsAutoBlocks (32) blocks of kWsMaxAll / 32 = 96 rows (the union
   // capacity over more, smaller sub-problems: each round's pair steps run on
-  // twice the workgroups; headline 0.0341 vs 0.0371 s at 8 x 192, same rounds,
-  // profiles/r3_blocks16_ab.txt), never larger than ws_size; the one-block
+  // more workgroups; headline 0.0308 vs 0.0371 s at 8 x 192,
+  // profiles/r3_union3072_ab.txt), never larger than ws_size; the one-block
   // rounds the adaptive count falls back to keep ws_size rows
   const int auto_q = std::min(ws_q, kWsMaxAll / kWsAutoBlocks) & ~1;
   const bool blocks_auto = m.p.ws_blocks == 0;
   const int want_blocks = !blocks_auto ? m.p.ws_blocks
                                        : (n >= kWsAutoBlocksRows ? std::min(kWsAutoBlocks, kWsMaxAll / auto_q) : 1);
   const int mb_q = blocks_auto ? auto_q : ws_q;  // rows per block of the multi-block rounds
-  DPSVM_CHECK(want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
+  // (only where working-set rounds can run: solver=smo or a small problem ignores ws_blocks)
+  DPSVM_CHECK(!(ws_cand || wsc_cand) || want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
               "ws_blocks x ws_size must be <= " + std::to_string(kWsMaxAll) + " (the round's union capacity)");
   // ws-cache takes them too when its cache holds the union's lines plus the
   // victim window (L >= 2 P q_max + 4096; agreed: L follows each device's free memory)

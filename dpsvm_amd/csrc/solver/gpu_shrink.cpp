@@ -84,7 +84,8 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   DPSVM_CHECK(n >= 2 && d >= 1, "solve_shrinking: need at least 2 samples and 1 feature");
   const double t_start = now();
   SolverParams p = p0;
-  p.checkpoint_every = 0;  // phases are not checkpointed (the final state is)
+  p.checkpoint_every = 0;  // the phases' own solvers do not checkpoint: the whole problem's state is
+                          // written after every phase instead (write_phase_checkpoint)
   if (p.solver == 0) p.solver = 2;  // the phases are parts of a large problem: working-set rounds at any size
   // the inactive rows' gradient comes from the f32 predict GEMM: the phases'
   // kernel values must be the same f32 MFMA values (split-GEMM values differ
@@ -200,6 +201,23 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     const Extremes e = extremes(f, alpha, y.data(), C);
     res.b_hi = e.b_hi;
     res.b_lo = e.b_lo;
+    if (!p0.checkpoint_path.empty()) {
+      // the whole problem after this phase (alpha, exact f): resumable by any
+      // solver, with or without shrinking
+      Checkpoint wck;
+      wck.n = n;
+      wck.d = d;
+      wck.C = p.C;
+      wck.gamma = gamma;
+      wck.eps = p.eps;
+      wck.clip = (int)p.clip;
+      wck.iter = iters;
+      wck.b_hi = e.b_hi;
+      wck.b_lo = e.b_lo;
+      wck.alpha = alpha;
+      wck.f = f;
+      write_checkpoint(p0.checkpoint_path, wck);
+    }
     const bool open = e.ok && gap_open(e.b_hi, e.b_lo, p.eps);
     if (p.verbose)
       fprintf(stderr, "[dpsvm] shrink phase %d: %lld active rows, %lld pair steps, global gap %g (status %d)\n",

@@ -120,6 +120,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   trace::Range loop_range("dpsvm/solve");
   const int64_t fault_iter = trace::fault_nan_iter();
   const int64_t exit_iter = trace::fault_exit_iter(m.outer_rank);
+  const int64_t throw_iter = trace::fault_throw_iter(m.outer_rank);
   bool fault_done = false;
   auto t0 = Clock::now();
   m.engine->seed(m, iter0, b_hi0, b_lo0, res);
@@ -129,10 +130,15 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   int64_t last_ck = iter0, last_log = iter0;
   SmoStatus st{};
   // watchdog at world > 1: the first blocks (the seed's Gram GEMM, graph
-  // instantiation) get min(watchdog_s, kWatchdogFirstS); later ones 50x the
+  // instantiation) get kWatchdogFirstS; later ones 50x the
   // slowest block seen, at least kWatchdogFloorS — a peer that died mid-solve
   // (a collective that never completes) fails this rank within seconds
+  // (only when the user left watchdog_s at 0 = auto: an explicit bound is used as given)
   constexpr double kWatchdogFirstS = 120.0, kWatchdogFloorS = 20.0;
+  struct WdReset {  // wd_limit must not outlive this solve (exceptions included)
+    double& v;
+    ~WdReset() { v = 0.0; }
+  } wd_reset{m.wd_limit};
   auto t_prev = Clock::now();
   double blk_max = 0.0;
   int n_timed = 0;
@@ -140,9 +146,9 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     m.engine->run_block(m, B);
     HIP_CHECK(hipEventRecord(m.ev[blocks & 1], m.stream));
     if (blocks > 0) {
-      if (m.world > 1)
-        m.wd_limit = n_timed >= 2 ? std::min(m.p.watchdog_s, std::max(kWatchdogFloorS, 50.0 * blk_max))
-                                  : std::min(m.p.watchdog_s, kWatchdogFirstS);
+      if (m.world > 1 && !(m.p.watchdog_s > 0.0))
+        m.wd_limit = n_timed >= 2 ? std::min(kWatchdogDefaultS, std::max(kWatchdogFloorS, 50.0 * blk_max))
+                                  : kWatchdogFirstS;
       m.wait_event(m.ev[(blocks - 1) & 1]);
       {
         const auto now = Clock::now();
@@ -167,6 +173,13 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
         fflush(stderr);
         _exit(3);
       }
+      if (throw_iter >= 0 && st.iter >= throw_iter) {
+        // DPSVM_FAULT=throw@K:R: this rank's solve fails, its thread lives on;
+        // drain its own stream first (nothing of this rank stays in flight)
+        (void)hipStreamSynchronize(m.stream);
+        fail("fault injection: rank " + std::to_string(m.outer_rank) + " throws at iteration " +
+             std::to_string(st.iter));
+      }
       if (fault_iter >= 0 && !fault_done && st.iter >= fault_iter) {
         // DPSVM_FAULT=nan@K: poison f[0]; lands between two enqueued blocks
         static const float qnan = std::nanf("");
@@ -187,7 +200,6 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
     DPSVM_CHECK(blocks <= max_blocks + 2, "SMO loop did not terminate (internal error)");
   }
   m.wait_event(m.ev[blocks & 1]);  // the overshoot block (early-exit kernels)
-  m.wd_limit = 0.0;
   HIP_CHECK(hipStreamSynchronize(m.stream));
   res.t_solve = secs_since(t0);
   res.t_gram = m.engine->gram_seconds();

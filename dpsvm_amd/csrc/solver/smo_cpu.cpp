@@ -181,6 +181,7 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
   std::vector<uint64_t> th_hi(T), th_lo(T);
   const int64_t fault_iter = trace::fault_nan_iter();
   const int64_t exit_iter = trace::fault_exit_iter(rank);
+  const int64_t throw_iter = trace::fault_throw_iter(rank);
   trace::Range loop_range("dpsvm/smo_loop_cpu");
   auto t0 = Clock::now();
   int64_t iter = iter0;
@@ -272,6 +273,8 @@ SolveResult solve_cpu(const Dataset& ds, const SolverParams& p, Communicator* co
       fflush(stderr);
       _exit(3);
     }
+    if (throw_iter >= 0 && iter >= throw_iter)  // DPSVM_FAULT=throw@K:R: this rank's solve fails
+      fail("fault injection: rank " + std::to_string(rank) + " throws at iteration " + std::to_string(iter));
     if (fault_iter >= 0 && iter == fault_iter && nl > 0) {  // DPSVM_FAULT
       f[0] = std::nanf("");
       keys_ready = false;

@@ -99,7 +99,7 @@ class SVCConfig:
     xch_stride: int = 4
     xch_mem: str = "auto"           # auto | uncached | coarse
     xch_timeout_s: float = 120.0    # give-up bound of one in-kernel poll (then the solve fails)
-    watchdog_s: float = 1800.0
+    watchdog_s: float = 0.0  # 0: auto (1800 s; adaptive to the block time at world > 1)
     census_groups: int = 0          # residency census grid (tests)
     verify_ranks: bool = True       # cross-rank alpha digest after each solve (world > 1)
     # solver: auto (ws from 50k rows, else smo) | smo (pair-at-a-time engines, the reference's trajectory) |
@@ -109,7 +109,8 @@ class SVCConfig:
     ws_size: int = 192              # working-set rows (<= 192)
     ws_new: int = 0                 # rows replaced per round (0: 3 ws_size / 4)
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
-    # ws-dense: up to P sub-problems per round (1..8; 0 auto = 8 from 50k rows, else 1); adaptive — halved
+    # working-set engines: up to P sub-problems per round (1..32, P x ws_size <= 3072; 0 auto = 32 blocks of
+    # 96 rows from 50k rows, else 1); adaptive — halved
     # after every damped round (coupled blocks), then the one-block round kernels (smo_ws.hip)
     ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)

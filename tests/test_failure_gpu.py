@@ -1,7 +1,9 @@
 """Rank death on the GPU path: with
 DPSVM_FAULT=exit@K:1 rank 1's process dies mid-solve; the surviving rank must
 fail on its own within 60 s (the in-kernel peer exchange gives up and the
-solve raises), and the in-process multi-rank CLI must exit non-zero."""
+solve raises).  In-process ranks (svmTrain --ranks / -p) whose rank 1 THROWS
+(DPSVM_FAULT=throw@K:1, thread alive) must abort the peer's communicator and
+report rank 1's error as the root cause."""
 import os
 import socket
 import subprocess
@@ -54,14 +56,38 @@ def test_dead_rank_process_survivor_fails_within_60s():
     assert elapsed < 90, elapsed
 
 
-def test_dead_rank_in_process_cli_exits_nonzero(tmp_path):
+def _cli_throw(tmp_path, extra):
     exe = os.path.join(ROOT, "bin", "svmTrain")
     if not os.path.exists(exe):
         pytest.skip("bin/svmTrain not built")
-    env = dict(os.environ, DPSVM_FAULT="exit@2000:1")
+    env = dict(os.environ, DPSVM_FAULT="throw@2000:1")
     t0 = time.time()
     r = subprocess.run([exe, "-a", "784", "-x", "12000", "--synthetic", "mnist", "-c", "10", "-g", "0.25", "-m",
-                        str(tmp_path / "m.txt"), "--ranks", "2", "--solver", "ws", "--dp", "shard",
-                        "--xch-timeout", "15"], capture_output=True, text=True, timeout=120, env=env)
-    assert r.returncode != 0
-    assert time.time() - t0 < 60
+                        str(tmp_path / "m.txt"), "--solver", "ws", "--dp", "shard", *extra],
+                       capture_output=True, text=True, timeout=120, env=env)
+    return r, time.time() - t0
+
+
+def test_thread_rank_throw_cli_reports_root_cause(tmp_path):
+    """DPSVM_FAULT=throw@K:1 inside rank 1's solve thread (process alive): the
+    CLI aborts rank 0's communicator, rank 0 leaves its blocked collective
+    through the abort, and the process exits non-zero with rank 1's error."""
+    r, dt = _cli_throw(tmp_path, ["--ranks", "2", "--xch-timeout", "15"])
+    assert r.returncode != 0 and dt < 60, (r.returncode, dt, r.stderr[-2000:])
+    err = r.stderr
+    assert "rank 1 failed first (root cause)" in err, err[-2000:]
+    assert "fault injection: rank 1 throws" in err.strip().splitlines()[-1], err[-2000:]
+    assert "rank 0 (after rank 1 failed)" in err and "aborted" in err, err[-2000:]
+
+
+def test_rccl_rank_throw_cli_reports_root_cause(tmp_path):
+    """The same over RCCL (-p 2, one GPU per rank thread): rank 0's owning
+    thread carries out the requested ncclCommAbort and fails."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    r, dt = _cli_throw(tmp_path, ["-p", "2"])
+    assert r.returncode != 0 and dt < 60, (r.returncode, dt, r.stderr[-2000:])
+    err = r.stderr
+    assert "rank 1 failed first (root cause)" in err, err[-2000:]
+    assert "fault injection: rank 1 throws" in err.strip().splitlines()[-1], err[-2000:]
+    assert "rank 0 (after rank 1 failed)" in err and "aborted" in err, err[-2000:]
