@@ -49,13 +49,16 @@ LIB_SOURCES = [
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/rbf_gemm_split.hip",
+    "kernels/rbf_gram_wide.hip",
     "kernels/smo_fused.hip",
     "kernels/microbench.hip",
     "kernels/compact.hip",
     "kernels/smo_fused_lru.hip",
     "kernels/smo_persist.hip",
     "kernels/smo_persist_lru.hip",
-    "kernels/smo_ws.hip",
+    "kernels/ws_select.hip",
+    "kernels/ws_merge.hip",
+    "kernels/ws_solve.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",

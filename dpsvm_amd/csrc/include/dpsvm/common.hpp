@@ -116,7 +116,7 @@ struct SolverParams {
   // GEMM (docs/DESIGN.md "Multi-GPU").
   int dp_policy = 0;
   // solver: 0 auto, 1 pair-at-a-time SMO engines (the reference's trajectory),
-  // 2 working-set rounds (ws engine, smo_ws.hip: the reference's pair rule on
+  // 2 working-set rounds (ws engine, ws_*.hip: the reference's pair rule on
   // a q-row sub-problem in LDS, the same global stop test)
   int solver = 0;
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
@@ -124,7 +124,7 @@ struct SolverParams {
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
   int ws_blocks = 0;          // working-set engines: up to P disjoint q-row sub-problems per round (1..32,
                               // P x ws_size <= 3072; 0 auto = 32 blocks of 96 rows from 50k rows, else 1).  Adaptive: halved after every damped round (coupled blocks), 1 after an
-                              // independent-clip event, then the one-block round kernels (smo_ws.hip)
+                              // independent-clip event, then the one-block round kernels (ws_*.hip)
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_wss = 0;             // sub-problem pair choice: 1 the reference's first-order rule (max f over I_low),
                               // 2 second order (WSS2: max (f_lo - b_hi)^2 / eta); the stop test is unchanged;

@@ -45,7 +45,7 @@ enum class EngineKind : int32_t {
   PersistCache = 2,  // kernel-row cache, persistent kernel, private cache metadata
   FusedCache = 3,    // kernel-row cache, one launch per iteration (+ host spill tier)
   Chain = 4,         // rows / step / finalize kernels + collective (partitioned X fallback)
-  WsDense = 5,       // Gram resident, working-set rounds (sub-problem in LDS, smo_ws.hip)
+  WsDense = 5,       // Gram resident, working-set rounds (sub-problem in LDS, ws_*.hip)
   WsCache = 6,       // kernel-row cache, working-set rounds (the set's missing rows by one MFMA GEMM)
 };
 inline const char* engine_name(EngineKind k) {
@@ -243,7 +243,7 @@ struct SmoArgs {
 };
 constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..16}, {key bits 15..0, alpha}
 
-// ---- working-set engine (smo_ws.hip) ----
+// ---- working-set engine (ws_*.hip) ----
 // Decomposition around the reference's pair update: each round selects a
 // working set of q rows (the most violating of I_up / I_low plus the newest
 // part of the previous set), one workgroup solves the q-row sub-problem with
@@ -263,7 +263,7 @@ constexpr int64_t kWsAutoRows = 50000;   // solver auto: working-set engines fro
 // multi-block rounds (ws_blocks = P > 1, ws-dense at world 1): a round selects
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor
-// t = min(1, g'd / d'Qd) of the dual (smo_ws.hip "multi-block rounds")
+// t = min(1, g'd / d'Qd) of the dual (ws_*.hip "multi-block rounds")
 constexpr int kWsMaxBlocks = 32;                  // blocks per round (P x q_max <= kWsMaxAll)
 constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
 constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: the top 1536 of each side)
@@ -343,7 +343,7 @@ struct WsArgs {
   uint64_t* stamps;    // DPSVM_STAMPS diagnostics: s_memrealtime per phase, ring of kStampRing rounds
   // in-kernel peer exchange of the rounds (world > 1; nullptr: the communicator's
   // collectives).  Every rank's receive buffer (uncached, IPC-mapped by its
-  // peers; smo_ws.hip "peer exchange"): [2 parity][G_all][2 kWsCand1][2] candidate
+  // peers; ws_*.hip "peer exchange"): [2 parity][G_all][2 kWsCand1][2] candidate
   // granules, then from word xsub [2 parity][q_max][q_max + 1] sub-Gram rows with
   // the row's f in the last column
   uint64_t* const* xpeer;

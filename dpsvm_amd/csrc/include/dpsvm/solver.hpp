@@ -158,7 +158,7 @@ void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* 
 void fused_select(const float* f, const float* alpha, const float* y, int64_t n, float C, int rows_per_group,
                   uint64_t* keys_out, void* stream);
 
-// ---- working-set kernels (smo_ws.hip), one launch each on crafted state
+// ---- working-set kernels (ws_*.hip), one launch each on crafted state
 // (host vectors in and out; ws_kernel_entry.hip).  Reference counterparts:
 // the selection / update functors svmTrain.cu:41-137, the pair rule
 // svmTrainMain.cpp:255-299. ----

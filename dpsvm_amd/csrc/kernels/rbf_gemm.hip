@@ -8,7 +8,7 @@
 //   ROWS    : STORE with row indirection — A row i is X row a_rows[i], output
 //             row i goes to line out_rows[i], M read on the device (*m_dev):
 //             the kernel rows of a working set's cache misses in one launch
-//             (the working-set cache engine, smo_ws.hip).
+//             (the working-set cache engine, ws_*.hip).
 //             Replaces the reference's n x (cublasSgemv + thrust::transform_reduce)
 //             launches (svmTrain.cu:633-665, K12/K13).
 //

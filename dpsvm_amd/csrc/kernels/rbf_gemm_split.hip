@@ -40,20 +40,14 @@
 #include "dpsvm/common.hpp"
 #include "device_util.hpp"
 #include "kernels.hpp"
+#include "split_util.hpp"
 #include "../runtime/hip_check.hpp"
 
 namespace dpsvm {
 namespace dev {
 
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-
 constexpr int kSplitThreads = 512;
 constexpr int kSplitShiftTarget = 15;  // largest |x| scaled into [2^14, 2^15)
-
-__device__ __forceinline__ f16v mfma32_f16(h8 a, h8 b, f16v c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
 
 // One wave per row: shift[r] and the h / l planes of row r (columns past dp
 // are zero).
@@ -106,23 +100,6 @@ __device__ __forceinline__ void xcd_tile_of(int64_t L, int64_t tm, int64_t tn, i
   const int64_t first_m = (T / (GM * tn)) * GM;
   const int64_t gm = min(GM, tm - first_m);
   const int64_t in = T - first_m * tn;
-  tx = first_m + in % gm;
-  ty = in / gm;
-}
-
-// the same order in 32-bit arithmetic (the persistent kernel: tm * tn < 2^31)
-__device__ __forceinline__ void xcd_tile_of32(int L, int tm, int tn, int& tx, int& ty) {
-  const int total = tm * tn;
-  constexpr int CH = 64, GM = 8;
-  const int full = total / (8 * CH) * (8 * CH);
-  int T = L;
-  if (L < full) {
-    const int xcd = L % 8, local = L / 8;
-    T = ((local / CH) * 8 + xcd) * CH + local % CH;
-  }
-  const int first_m = (T / (GM * tn)) * GM;
-  const int gm = min(GM, tm - first_m);
-  const int in = T - first_m * tn;
   tx = first_m + in % gm;
   ty = in / gm;
 }
@@ -929,6 +906,10 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     return e && atoi(e) == 1 ? 1 : 2;
   }();
   const int variant = split_gemm_variant();
+  if (variant == 5 && ablate == 0 && rbf_gram_wide_supported(M, N, dp, ldo)) {
+    rbf_gram_wide(A, Ash, Asq, M, B, Bsh, Bsq, N, dp, gamma, out, ldo, s, symmetric);
+    return;
+  }
   if ((variant == 0 || variant == 4) && ablate == 0 && (dp + 31) / 32 >= 5 && tm * tn < (1ll << 31)) {
     // default: persistent LDS-DMA, one workgroup per CU (a multiple of 8)
     static const int cus4 = [] {

@@ -1,0 +1,970 @@
+// Working-set engine, merge and gather: the stop test and the next working
+// set from every workgroup's candidate lists (one-block: ws_gather / ws_merge;
+// multi-block: ws_rank + ws_merge_multi, the union of P blocks), the cache
+// mode's line assignment, and the sub-Gram rows of the set (ws_gather*).
+// Round structure and shared helpers: ws_common.hpp.
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "ws_common.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+// ---------------------------------------------------------------------------
+// the merge: stop test and the new working set (one 256-thread workgroup;
+// identical result in every workgroup that runs it).  Returns false when the
+// run stopped (done is then set by workgroup 0).  s_idx[0..*q) = the set,
+// newest first; *b_hi / *b_lo = the global selection.
+// ---------------------------------------------------------------------------
+__device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out, float* bh_out, float* bl_out) {
+  __shared__ int s_hist[2][256];
+  __shared__ int s_sel[2][2];
+  __shared__ int s_thr[2];
+  __shared__ uint64_t s_wsum64[4];
+  __shared__ uint64_t s_sv[2][kWsMaxCand];
+  __shared__ int32_t s_hash[4][kWsHash];  // up keys, up ranks, low keys, low ranks
+  __shared__ int32_t s_keep[2 * kWsMax];  // per interleaved position: final slot or -1
+  __shared__ uint64_t s_scr[8];
+  __shared__ int s_wsum[4];
+  const int tid = threadIdx.x;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  if (c->done != kRunning) {
+    // a round ended the run (max_iter / no pair): its changes were applied by
+    // the ws_select that followed it; nothing may be applied twice
+    if (lead) c->n_apply = 0;
+    return false;
+  }
+  const int G = a.G_all;
+  const int64_t r_now = c->outer;
+  const int par = (int)(r_now & 1);
+  const int q_prev = c->q[par ^ 1];
+  const int want = q_prev == 0 ? a.q_max : min(a.n_new, a.q_max);
+  // the previous set's row (read at the end) in the same load batch as the
+  // candidate lists: one global round trip fewer on the merge's serial path
+  const int32_t pidx_pre = tid < q_prev ? c->idx[par ^ 1][tid] : -1;
+
+  // ---- every candidate list in registers: thread t holds lists t, t + 256,
+  // ... (up to kWsListsPerThread, merged to one sorted top-kWsCand list per side:
+  // the same as one selection workgroup over their rows) ----
+  uint64_t lu[kWsCand1], ll[kWsCand1];
+#pragma unroll
+  for (int r = 0; r < kWsCand1; ++r) lu[r] = ll[r] = kKeyNone;
+  bool ok = true;
+  const uint64_t xt = xtag((uint32_t)r_now + 1u);
+  for (int j = 0; j < kWsListsPerThread; ++j) {
+    const int slot = tid + j * kWsGatherThreads;
+    if (slot >= G) break;
+    uint64_t cu[kWsCand1], cl[kWsCand1];
+    if (a.xpeer == nullptr) {
+#pragma unroll
+      for (int r = 0; r < kWsCand1; ++r) {
+        cu[r] = a.cand[(size_t)slot * 2 * kWsCand + r];
+        cl[r] = a.cand[(size_t)slot * 2 * kWsCand + kWsCand + r];
+      }
+    } else {
+      // peer exchange: poll slot `slot` of this rank's buffer
+      const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, slot);
+      uint64_t g[4 * kWsCand1];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {
+#pragma unroll
+        for (int i = 0; i < 4 * kWsCand1; ++i) g[i] = xch_load<true>(e + i);
+        bool all = true;
+#pragma unroll
+        for (int i = 0; i < 4 * kWsCand1; ++i) all &= ws_tag_ok(g[i], xt);
+        if (all) break;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      constexpr uint64_t m48 = (1ull << 48) - 1;
+#pragma unroll
+      for (int r = 0; r < kWsCand1; ++r) {
+        cu[r] = ((g[2 * r] & m48) << 16) | (g[2 * r + 1] & 0xffffull);
+        cl[r] = ((g[2 * kWsCand1 + 2 * r] & m48) << 16) | (g[2 * kWsCand1 + 2 * r + 1] & 0xffffull);
+      }
+    }
+    if (j == 0) {
+#pragma unroll
+      for (int r = 0; r < kWsCand1; ++r) {
+        lu[r] = cu[r];
+        ll[r] = cl[r];
+      }
+    } else {
+      ws_top4_merge(lu, cu);
+      ws_top4_merge(ll, cl);
+    }
+  }
+  if (a.xpeer != nullptr && !__syncthreads_and(ok)) {
+    ws_comm_fail(a, c);
+    return false;
+  }
+  // ---- global minima (stop test) ----
+  uint64_t gu = lu[0], gl = ll[0];
+  block_min2_u64<kWsGatherThreads>(gu, gl, s_scr);
+  const float b_hi = key_value(gu), b_lo = -key_value(gl);
+  if (lead) WS_STAMP(11);
+  const int64_t it0 = c->iter;
+  int stop = kRunning;
+  if (c->nonfinite) stop = kNonFinite;
+  else if (gu == kKeyNone || gl == kKeyNone) stop = kNoPair;
+  else if (!isfinite(b_hi) || !isfinite(b_lo)) stop = kNonFinite;
+  else if (!(b_lo > b_hi + 2.0f * a.eps)) stop = kConverged;
+  else if (it0 >= a.max_iter) stop = kMaxIter;
+  if (stop != kRunning) {
+    if (lead) {
+      c->done = stop;
+      c->n_apply = 0;  // applied by the last ws_select already
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+      ws_status(a.status, c);
+    }
+    return false;
+  }
+
+  // ---- per side, a 16-bit key prefix T: the rows whose prefix is <= T hold
+  // >= m depth-d list entries, hence >= m (d + 1) >= ceil(want / 2)
+  // candidates.  Two 8-bit radix passes over the depth-d entries (LDS
+  // histograms): no sort.  The new rows are then taken by class — the global
+  // extreme first, prefix < T, prefix == T — each class in list (row) order,
+  // so a cut only ever drops rows of the boundary class. ----
+  const int half = (want + 1) / 2;
+  const int Gl = min(G, kWsGatherThreads);  // lists held (one merged list per thread)
+  const int d = min(kWsCand1 - 1, (half + Gl - 1) / Gl - 1);
+  const int m = (half + d) / (d + 1);
+  uint64_t hd[2] = {lu[0], ll[0]};
+#pragma unroll
+  for (int r = 1; r < kWsCand1; ++r) {
+    hd[0] = r == d ? lu[r] : hd[0];
+    hd[1] = r == d ? ll[r] : hd[1];
+  }
+  for (int t = tid; t < 4 * kWsHash; t += kWsGatherThreads) (&s_hash[0][0])[t] = -1;
+  s_hist[0][tid] = 0;
+  s_hist[1][tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd)
+    if (hd[sd] != kKeyNone) atomicAdd(&s_hist[sd][(int)(hd[sd] >> 56)], 1);
+  __syncthreads();
+  if (tid < 128) {  // wave 0: up side, wave 1: low side
+    const int sd = tid >> 6;
+    int below = 0;
+    const int b1 = wave_find_bin(s_hist[sd], m, &below);
+    if ((tid & 63) == 0) {
+      s_sel[sd][0] = b1;
+      s_sel[sd][1] = below;
+    }
+  }
+  __syncthreads();
+  s_hist[0][tid] = 0;
+  s_hist[1][tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd)
+    if (hd[sd] != kKeyNone && s_sel[sd][0] >= 0 && (int)(hd[sd] >> 56) == s_sel[sd][0])
+      atomicAdd(&s_hist[sd][(int)(hd[sd] >> 48) & 255], 1);
+  __syncthreads();
+  if (tid < 128) {
+    const int sd = tid >> 6;
+    int below = 0;
+    const int b1 = s_sel[sd][0];
+    const int b2 = b1 >= 0 ? wave_find_bin(s_hist[sd], m - s_sel[sd][1], &below) : -1;
+    if ((tid & 63) == 0) s_thr[sd] = b1 >= 0 && b2 >= 0 ? (b1 << 8) | b2 : 0xFFFF;  // too few: every row
+  }
+  __syncthreads();
+  if (lead) WS_STAMP(12);
+  const uint32_t T[2] = {(uint32_t)s_thr[0], (uint32_t)s_thr[1]};
+  const uint64_t gmin[2] = {gu, gl};
+  // class counts per thread (the global extreme is placed first, separately)
+  uint64_t packed = 0;  // 12-bit fields: [up A, up B, low A, low B]
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+#pragma unroll
+    for (int r = 0; r < kWsCand1; ++r) {
+      const uint64_t k = sd ? ll[r] : lu[r];
+      if (k == kKeyNone || k == gmin[sd]) continue;
+      const uint32_t pre = (uint32_t)(k >> 48);
+      if (pre < T[sd]) packed += 1ull << (24 * sd);
+      else if (pre == T[sd]) packed += 1ull << (24 * sd + 12);
+    }
+  }
+  uint64_t ptot = 0;
+  const uint64_t pofs = block_scan_fields(packed, s_wsum64, &ptot);
+  int S[2];
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+    const int totA = (int)((ptot >> (24 * sd)) & 4095), totB = (int)((ptot >> (24 * sd + 12)) & 4095);
+    int oA = 1 + (int)((pofs >> (24 * sd)) & 4095), oB = 1 + totA + (int)((pofs >> (24 * sd + 12)) & 4095);
+    S[sd] = 1 + totA + totB;
+#pragma unroll
+    for (int r = 0; r < kWsCand1; ++r) {
+      const uint64_t k = sd ? ll[r] : lu[r];
+      if (k == kKeyNone) continue;
+      if (k == gmin[sd]) {
+        s_sv[sd][0] = k;
+        continue;
+      }
+      const uint32_t pre = (uint32_t)(k >> 48);
+      if (pre < T[sd]) s_sv[sd][oA++] = k;
+      else if (pre == T[sd]) s_sv[sd][oB++] = k;
+    }
+  }
+  __syncthreads();
+
+  if (lead) WS_STAMP(13);
+  // ---- the new working set ----
+  int32_t* hk_u = s_hash[0];
+  int32_t* hv_u = s_hash[1];
+  int32_t* hk_l = s_hash[2];
+  int32_t* hv_l = s_hash[3];
+  if (tid < want) {
+    if (tid < S[0]) ws_hash_insert(hk_u, hv_u, (int32_t)key_index(s_sv[0][tid]), tid);
+    if (tid < S[1]) ws_hash_insert(hk_l, hv_l, (int32_t)key_index(s_sv[1][tid]), tid);
+  }
+  __syncthreads();
+  // interleaved positions 2r (up rank r), 2r + 1 (low rank r); a row's first
+  // position wins; thread t owns positions 2t and 2t + 1
+  bool kp[2] = {false, false};
+  int32_t ki[2] = {-1, -1};
+  if (tid < want) {
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      const uint64_t kk = tid < S[sd] ? s_sv[sd][tid] : kKeyNone;
+      if (kk != kKeyNone) {
+        ki[sd] = (int32_t)key_index(kk);
+        if (sd == 0) {
+          const int rl = ws_hash_find(hk_l, hv_l, ki[sd]);
+          kp[sd] = !(rl >= 0 && rl < tid);
+        } else {
+          const int ru = ws_hash_find(hk_u, hv_u, ki[sd]);
+          kp[sd] = !(ru >= 0 && ru <= tid);
+        }
+      }
+    }
+  }
+  int kept = 0;
+  const int slot0 = block_scan_small256((int)kp[0] + (int)kp[1], s_wsum, &kept);
+  const int n_chosen = min(kept, want);
+  if (tid < want) {
+    const int s0 = slot0, s1 = slot0 + (int)kp[0];
+    const bool c0 = kp[0] && s0 < want, c1 = kp[1] && s1 < want;
+    s_keep[2 * tid] = c0 ? s0 : -1;
+    s_keep[2 * tid + 1] = c1 ? s1 : -1;
+    if (c0) s_idx[s0] = ki[0];
+    if (c1) s_idx[s1] = ki[1];
+  }
+  __syncthreads();
+  if (lead) WS_STAMP(14);
+  // the previous set (newest first): rows not chosen again, up to q_max
+  bool pk = false;
+  int32_t pidx = -1;
+  if (tid < q_prev) {
+    pidx = pidx_pre;
+    const int ru = ws_hash_find(hk_u, hv_u, pidx);
+    const int rl = ws_hash_find(hk_l, hv_l, pidx);
+    pk = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+  }
+  int ptotal = 0;
+  const int pslot = block_scan_small256((int)pk, s_wsum, &ptotal);
+  if (pk && n_chosen + pslot < a.q_max) s_idx[n_chosen + pslot] = pidx;
+  const int q = min(a.q_max, n_chosen + ptotal);
+  __syncthreads();
+  *q_out = q;
+  *bh_out = b_hi;
+  *bl_out = b_lo;
+  return true;
+}
+
+// Row ra of the q_max-stride sub-Gram from line `line` (K(idx_ra, off + j) at
+// line[j]), plus the row's f / alpha / y.  A rank fills only the columns (and
+// the f) of rows it owns and zeros the rest, so at world > 1 one sum all-reduce
+// assembles the exact matrix (each entry has exactly one owner).  Rows ra >= q
+// are zeroed.
+__device__ __forceinline__ void ws_gather_row(const WsArgs& a, WsCtrl* c, const int32_t* s_idx, int q, int ra,
+                                              const float* line) {
+  const int tid = threadIdx.x;
+  float* dst = a.subg + (size_t)ra * a.q_max;
+  if (ra >= q) {
+    for (int b = tid; b < a.q_max; b += kWsGatherThreads) dst[b] = 0.f;
+    if (tid == 0) a.aux[ra] = 0.f;
+    return;
+  }
+  const int64_t lo = a.off, hi = a.off + a.nl;
+  if (a.xpeer != nullptr) {
+    // peer exchange: push the owned entries of row ra (+ its f) to every rank,
+    // then poll this rank's copy of the row (q_max <= 192 < 256: one column per
+    // thread, the last thread takes f)
+    const int64_t R = c->outer;
+    const uint64_t t = xtag((uint32_t)R + 1u);
+    const int64_t row = ws_xrow(a, (int)(R & 1), ra);
+    constexpr int kF = kWsGatherThreads - 1;
+    const int64_t gi = s_idx[ra];
+    if (tid < q) {
+      const int64_t gj = s_idx[tid];
+      if (gj >= lo && gj < hi) {
+        const uint64_t v = t | __float_as_uint(line[gj - lo]);
+        for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + tid, v);
+      }
+    } else if (tid == kF && gi >= lo && gi < hi) {
+      const uint64_t v = t | __float_as_uint(a.f[gi - lo]);
+      for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + a.q_max, v);
+    }
+    bool ok = true;
+    const int col = tid < q ? tid : tid == kF ? a.q_max : -1;
+    if (col >= 0) {
+      const uint64_t* g = a.xpeer[a.xrank] + row + col;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t v = xch_load<true>(g);
+      while (!ws_tag_ok(v, t)) {
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = xch_load<true>(g);
+      }
+      const float fv = __uint_as_float((uint32_t)v);
+      if (tid == kF) a.aux[ra] = fv;
+      else dst[tid] = fv;
+    } else if (tid < a.q_max) {
+      dst[tid] = 0.f;
+    }
+    if (tid == 0) {
+      a.aux[a.aux_stride + ra] = a.alpha[gi];
+      a.aux[2 * a.aux_stride + ra] = a.y[gi];
+    }
+    if (!__syncthreads_and(ok)) ws_comm_fail(a, c);
+    return;
+  }
+  for (int b = tid; b < a.q_max; b += kWsGatherThreads) {
+    const int64_t gj = b < q ? (int64_t)s_idx[b] : -1;
+    dst[b] = gj >= lo && gj < hi ? line[gj - lo] : 0.f;
+  }
+  if (tid == 0) {
+    const int64_t gi = s_idx[ra];
+    a.aux[ra] = gi >= lo && gi < hi ? a.f[gi - lo] : 0.f;
+    a.aux[a.aux_stride + ra] = a.alpha[gi];
+    a.aux[2 * a.aux_stride + ra] = a.y[gi];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ws_gather (dense mode): the merge in every workgroup + one sub-Gram row per
+// workgroup (row a: q random columns of Gram row idx_a — one load per thread;
+// the whole grid issues the scattered reads a single CU could not)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  if (lead) WS_STAMP(1);
+  const int par = (int)(c->outer & 1);
+  int q = 0;
+  float b_hi = 0.f, b_lo = 0.f;
+  if (!ws_merge(a, c, s_idx, &q, &b_hi, &b_lo)) return;
+  if (lead) WS_STAMP(2);
+  if (blockIdx.x == 0) {
+    for (int t = tid; t < q; t += kWsGatherThreads) {
+      c->idx[par][t] = s_idx[t];
+      c->line[par][t] = s_idx[t];  // the resident Gram: line i is row i
+    }
+    if (tid == 0) {
+      c->q[par] = q;
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+    }
+  }
+  ws_gather_row(a, c, s_idx, q, blockIdx.x, blockIdx.x < q ? a.gram + (int64_t)s_idx[blockIdx.x] * a.ldg : nullptr);
+  if (lead) WS_STAMP(8);
+}
+
+// ---------------------------------------------------------------------------
+// cache mode, round part 1 — ws_merge (ONE workgroup): the merge, then lines
+// for the members: a member's row is cached (slot_of) or takes a victim line.
+// Victims come from a window of up to 512 lines after the CLOCK hand, skipping
+// lines that hold a member (pinned while the round uses them); all misses are
+// assigned at once (one prefix scan), their rows computed next by one GEMM.
+// ---------------------------------------------------------------------------
+constexpr int kWsWindow = 512;
+
+__global__ __launch_bounds__(kWsGatherThreads) void ws_merge_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  __shared__ int32_t s_line[kWsMax];
+  __shared__ int32_t s_pin[kWsWindow];
+  __shared__ int32_t s_victim[kWsMax];
+  __shared__ int s_wsum[4];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  if (tid == 0) WS_STAMP(1);
+  const int par = (int)(c->outer & 1);
+  int q = 0;
+  float b_hi = 0.f, b_lo = 0.f;
+  if (!ws_merge(a, c, s_idx, &q, &b_hi, &b_lo)) return;
+  if (tid == 0) WS_STAMP(2);
+  const int L = a.L, hand = c->hand;
+  const int W = min(L, kWsWindow);
+  for (int w = tid; w < kWsWindow; w += kWsGatherThreads) s_pin[w] = 0;
+  __syncthreads();
+  int32_t my_line = -1, my_row = -1;
+  if (tid < q) {
+    my_row = s_idx[tid];
+    my_line = a.slot_of[my_row];
+    if (my_line >= 0) {
+      const int o = (my_line - hand + L) % L;
+      if (o < W) s_pin[o] = 1;
+    }
+  }
+  __syncthreads();
+  int n_miss = 0;
+  const bool miss = tid < q && my_line < 0;
+  const int mrank = block_scan_small256((int)miss, s_wsum, &n_miss);
+  // free window slots 2t, 2t + 1 in window order
+  const bool f0 = 2 * tid < W && !s_pin[2 * tid], f1 = 2 * tid + 1 < W && !s_pin[2 * tid + 1];
+  int n_free = 0;
+  const int frank = block_scan_small256((int)f0 + (int)f1, s_wsum, &n_free);
+  int last_used = -1;
+  if (f0 && frank < n_miss) {
+    s_victim[frank] = (hand + 2 * tid) % L;
+    last_used = 2 * tid;
+  }
+  if (f1 && frank + (int)f0 < n_miss) {
+    s_victim[frank + (int)f0] = (hand + 2 * tid + 1) % L;
+    last_used = 2 * tid + 1;
+  }
+  __syncthreads();
+  if (miss) {  // n_free >= W - q >= n_miss whenever L >= q + 256 (setup guarantees L >= 2 q_max + 512)
+    const int32_t ln = s_victim[mrank];
+    const int32_t old = a.key_of[ln];
+    if (old >= 0) a.slot_of[old] = -1;  // evicted (never a member: members' lines are pinned)
+    a.key_of[ln] = my_row;
+    a.slot_of[my_row] = ln;
+    my_line = ln;
+    c->miss_row[mrank] = my_row;
+    c->miss_line[mrank] = ln;
+  }
+  if (tid < q) {
+    c->idx[par][tid] = my_row;
+    c->line[par][tid] = my_line;
+  }
+  if (n_miss > 0 && last_used >= 0 && (frank + (int)f0 + (int)f1 >= n_miss) && (frank < n_miss))
+    c->hand = (hand + last_used + 1) % L;  // the thread holding the last victim
+  if (tid == 0) {
+    c->q[par] = q;
+    c->b_hi = b_hi;
+    c->b_lo = b_lo;
+    c->n_miss = n_miss;
+    c->rows_computed += n_miss;
+    c->row_hits += q - n_miss;
+  }
+}
+
+// cache mode, round part 3 — ws_gather_lines (q_max workgroups): row a of the
+// sub-Gram from member a's line, its alpha / y / f
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  if (c->done != kRunning) return;
+  const int par = (int)(c->outer & 1);
+  const int q = c->q[par];
+  const int ra = blockIdx.x;
+  if (ra >= q) {
+    ws_gather_row(a, c, s_idx, q, ra, nullptr);
+    return;
+  }
+  for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][t];
+  __syncthreads();
+  ws_gather_row(a, c, s_idx, q, ra, a.gram + (int64_t)c->line[par][ra] * a.ldg);
+  if (tid == 0 && ra == 0) WS_STAMP(8);
+}
+
+// ---------------------------------------------------------------------------
+// multi-block rounds (a.blocks = P > 1; ws-dense at world 1).  The grid-wide
+// work of a round (merge, f update, candidates) is shared by P sub-problems
+// solved at once on P workgroups (the one-wave solve leaves the other CUs
+// idle): ws_merge_multi picks up to P q_max rows, ws_gather_multi their P
+// diagonal q x q blocks, ws_solve<kMulti> one block per workgroup, and the
+// two-pass ws_select applies the combined step with the exact line search.
+// ---------------------------------------------------------------------------
+// exclusive prefix of counts 0 .. 2^BITS - 1 over kWsMergeThreads threads in
+// thread order (bit-plane ballots)
+template <int BITS = 2>
+__device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  int pre = 0, wtot = 0;
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const uint64_t m = __ballot((v >> b) & 1);
+    pre += __popcll(m & below) << b;
+    wtot += __popcll(m) << b;
+  }
+  if (lane == 0) wsum[wave] = wtot;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWsMergeThreads / 64; ++w) {
+    off += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off + pre;
+}
+
+// ONE workgroup: every candidate key of both sides sorted (bitonic, 2048 per
+// side, two per thread), the stop test, then the union: up rank r / low rank r
+// interleaved (most violating first, a row's first position wins), then the
+// newest rows of the previous union.  Union position i goes to block
+// ((i / 2) mod P): each block gets up / low pairs, block 0 the global extremes
+// (so a round always holds the maximal violating pair and makes progress).
+constexpr int kMH = 4096;  // merge hash slots per side (load <= 0.38)
+constexpr int kWsWindowMulti = 8192;  // cache mode: CLOCK victim window of the multi-block merge
+__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 20; }
+__device__ __forceinline__ void mh_insert(int32_t* keys, int32_t* vals, int32_t idx, int32_t v) {
+  uint32_t h = mh_hash(idx);
+  while (true) {
+    const int32_t old = atomicCAS(keys + h, -1, idx);
+    if (old == -1) {
+      vals[h] = v;
+      return;
+    }
+    h = (h + 1) & (kMH - 1);
+  }
+}
+__device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* vals, int32_t idx) {
+  uint32_t h = mh_hash(idx);
+  for (int probe = 0; probe < kMH; ++probe) {
+    const int32_t k = keys[h];
+    if (k == idx) return vals[h];
+    if (k == -1) return -1;
+    h = (h + 1) & (kMH - 1);
+  }
+  return -1;
+}
+
+// ws_rank: the multi-block merge's sort, spread over a grid of 2 sides x
+// kRankChunks workgroups instead of one workgroup's bitonic network (29 of the
+// merge's 41 us at 3,072-row unions, profiles/r3_ws_stamps_32x96.json).  A
+// key's position in its side's ascending order is the number of keys below it:
+// real keys are unique (the global row index is in the low bits), so these
+// counts are a permutation of [0, n_real); the absent keys (kKeyNone) fill the
+// tail.  Each workgroup holds its side's NK keys in LDS and ranks KPW of them,
+// SUB = 16 threads per key each counting over every SUB-th key pair (the SUB
+// lanes of one key read 16 consecutive 16-B pairs: no bank conflict, broadcast
+// over keys).
+constexpr int kRankThreads = 512;
+constexpr int kRankChunks = 64;
+__global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
+  constexpr int NK = kWsMaxGroups * kWsCand;
+  constexpr int KPW = NK / kRankChunks, SUB = kRankThreads / KPW, PAIRS = NK / (2 * SUB);
+  static_assert(NK % kRankChunks == 0 && kRankThreads % KPW == 0 && SUB == 16 && NK % (2 * SUB) == 0, "rank geometry");
+  __shared__ uint64_t s_k[NK];
+  __shared__ int s_real[kRankThreads / 64];
+  const WsCtrl* c = a.ctrl;
+  if (c->done != kRunning) return;
+  const int side = blockIdx.x / kRankChunks, chunk = blockIdx.x % kRankChunks, tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) WS_STAMP(21);
+  const int G = a.G_all;
+  int real = 0;
+  for (int e = tid; e < NK; e += kRankThreads) {
+    const int l = e / kWsCand, r = e % kWsCand;
+    const uint64_t k = l < G ? a.cand[(size_t)l * 2 * kWsCand + side * kWsCand + r] : kKeyNone;
+    s_k[e] = k;
+    real += k != kKeyNone ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) real += __shfl_xor(real, o);
+  if ((tid & 63) == 0) s_real[tid >> 6] = real;
+  __syncthreads();
+  int n_real = 0;
+#pragma unroll
+  for (int w = 0; w < kRankThreads / 64; ++w) n_real += s_real[w];
+  const int e = chunk * KPW + tid / SUB, sub = tid % SUB;
+  const uint64_t k = s_k[e];
+  int cnt = 0;
+#pragma unroll 8
+  for (int i = 0; i < PAIRS; ++i) {
+    const int e2 = 2 * (sub + SUB * i);
+    cnt += (s_k[e2] < k ? 1 : 0) + (s_k[e2 + 1] < k ? 1 : 0);
+  }
+#pragma unroll
+  for (int o = 1; o < SUB; o <<= 1) cnt += __shfl_xor(cnt, o);
+  uint64_t* out = a.sorted + (size_t)side * NK;
+  if (sub == 0 && k != kKeyNone) out[cnt] = k;
+  if (tid < KPW && chunk * KPW + tid >= n_real) out[chunk * KPW + tid] = kKeyNone;
+}
+
+__global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
+  constexpr int T = kWsMergeThreads;
+  constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
+  constexpr int U = kWsMaxAll / T;            // previous-union rows per thread
+  static_assert(NK == 2 * T, "two keys per thread and side: elements tid and tid + T");
+  static_assert(kWsMaxAll % T == 0 && U <= 3, "previous union: <= 3 rows per thread (scan counts <= 3)");
+  static_assert(kMH >= kWsMaxAll && kWsWindowMulti == 8 * T, "cache-mode aliases of the hash tables / sort keys");
+  __shared__ uint64_t s_k[2][NK];
+  __shared__ int32_t s_hash[4][kMH];
+  __shared__ int32_t s_keep[kWsMaxAll + 2];
+  __shared__ int32_t s_idx[kWsMaxAll];
+  __shared__ int s_wsum[T / 64];
+  __shared__ int s_qb[kWsMaxBlocks];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x;
+  const bool lead = tid == 0;
+  if (c->done != kRunning) {
+    if (lead) c->n_apply = 0;  // applied by the last ws_select already
+    return;
+  }
+  if (lead) WS_STAMP(1);
+  const int G = a.G_all;
+  const int par = (int)(c->outer & 1);
+  const int P = max(1, min(c->p_act, a.blocks)), Qmax = P * a.q_max;
+  const int q_prev = c->uq[par ^ 1];
+  const int want = q_prev == 0 ? Qmax : min(P * a.n_new, Qmax);
+  // the previous union, newest first: thread t holds rows U t .. U t + U - 1
+  int32_t pidx[U];
+#pragma unroll
+  for (int h = 0; h < U; ++h) pidx[h] = U * tid + h < q_prev ? c->uidx[par ^ 1][U * tid + h] : -1;
+  // keys e = tid and e = tid + T of each side, in ascending order (ws_rank)
+  uint64_t v[2][2];  // [side][element]
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    v[0][x] = a.sorted[tid + x * T];
+    v[1][x] = a.sorted[NK + tid + x * T];
+  }
+  if (tid < kWsMaxBlocks) s_qb[tid] = 0;
+  for (int t = tid; t < 4 * kMH; t += T) (&s_hash[0][0])[t] = -1;
+  if (lead) WS_STAMP(20);
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+    s_k[sd][tid] = v[sd][0];
+    s_k[sd][tid + T] = v[sd][1];
+  }
+  __syncthreads();
+  if (lead) WS_STAMP(11);
+  const uint64_t gu = s_k[0][0], gl = s_k[1][0];
+  const float b_hi = key_value(gu), b_lo = -key_value(gl);
+  const int64_t it0 = c->iter;
+  int stop = kRunning;
+  if (c->nonfinite) stop = kNonFinite;
+  else if (gu == kKeyNone || gl == kKeyNone) stop = kNoPair;
+  else if (!isfinite(b_hi) || !isfinite(b_lo)) stop = kNonFinite;
+  else if (!(b_lo > b_hi + 2.0f * a.eps)) stop = kConverged;
+  else if (it0 >= a.max_iter) stop = kMaxIter;
+  if (stop != kRunning) {
+    if (lead) {
+      c->done = stop;
+      c->n_apply = 0;
+      c->b_hi = b_hi;
+      c->b_lo = b_lo;
+      ws_status(a.status, c);
+    }
+    return;
+  }
+  int32_t* hk_u = s_hash[0];
+  int32_t* hv_u = s_hash[1];
+  int32_t* hk_l = s_hash[2];
+  int32_t* hv_l = s_hash[3];
+  const int half = (want + 1) / 2;  // <= kWsMaxAll / 2 = T + T / 2 ranks per side
+  uint64_t ku[2], kl[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T;
+    ku[x] = e < half ? v[0][x] : kKeyNone;
+    kl[x] = e < half ? v[1][x] : kKeyNone;
+    if (ku[x] != kKeyNone) mh_insert(hk_u, hv_u, (int32_t)key_index(ku[x]), e);
+    if (kl[x] != kKeyNone) mh_insert(hk_l, hv_l, (int32_t)key_index(kl[x]), e);
+  }
+  __syncthreads();
+  if (lead) WS_STAMP(12);
+  // rank e keeps its up row unless the low side has it at a smaller rank, its
+  // low row unless the up side has it at a rank <= e (the up copy comes first)
+  bool kpu[2] = {false, false}, kpl[2] = {false, false};
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T;
+    if (ku[x] != kKeyNone) {
+      const int rl = mh_find(hk_l, hv_l, (int32_t)key_index(ku[x]));
+      kpu[x] = !(rl >= 0 && rl < e);
+    }
+    if (kl[x] != kKeyNone) {
+      const int ru = mh_find(hk_u, hv_u, (int32_t)key_index(kl[x]));
+      kpl[x] = !(ru >= 0 && ru <= e);
+    }
+  }
+  // union order: ranks 0 .. T - 1 (element 0 of threads in order), then ranks
+  // T .. (element 1): two scans
+  int tot0 = 0, tot1 = 0;
+  const int slot0 = block_scan_merge((int)kpu[0] + (int)kpl[0], s_wsum, &tot0);
+  const int slot1 = tot0 + block_scan_merge((int)kpu[1] + (int)kpl[1], s_wsum, &tot1);
+  const int kept = tot0 + tot1;
+  const int n_chosen = min(kept, want);
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int e = tid + x * T;
+    if (e < half) {
+      const int su = x == 0 ? slot0 : slot1, sl = su + (int)kpu[x];
+      const bool cu = kpu[x] && su < want, cl = kpl[x] && sl < want;
+      s_keep[2 * e] = cu ? su : -1;
+      s_keep[2 * e + 1] = cl ? sl : -1;
+      if (cu) s_idx[su] = (int32_t)key_index(ku[x]);
+      if (cl) s_idx[sl] = (int32_t)key_index(kl[x]);
+    }
+  }
+  __syncthreads();
+  if (lead) WS_STAMP(13);
+  // previous-union rows not chosen again keep their order after the new rows
+  // (uniform skip when the new rows already fill the union)
+  bool pk[U];
+  int npk = 0;
+#pragma unroll
+  for (int h = 0; h < U; ++h) {
+    pk[h] = false;
+    if (n_chosen < Qmax && pidx[h] >= 0) {
+      const int ru = mh_find(hk_u, hv_u, pidx[h]), rl = mh_find(hk_l, hv_l, pidx[h]);
+      pk[h] = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
+    }
+    npk += (int)pk[h];
+  }
+  int ptotal = 0;
+  if (n_chosen < Qmax) {  // uniform
+    int at = n_chosen + block_scan_merge(npk, s_wsum, &ptotal);
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      if (pk[h]) {
+        if (at < Qmax) s_idx[at] = pidx[h];
+        ++at;
+      }
+    }
+  }
+  const int Q = min(Qmax, n_chosen + ptotal);
+  __syncthreads();
+  if (lead) WS_STAMP(14);
+  if (a.cache) {
+    // ---- kernel-row cache: a line for every union row.  A member's row is
+    // cached (slot_of) or takes a victim from the window of kWsWindowMulti
+    // lines after the CLOCK hand, skipping lines that hold a member (pinned
+    // while the round uses them); all misses at once (prefix scans), their
+    // rows computed next by one row GEMM.  Setup guarantees
+    // L >= 2 Qmax + kWsWindowMulti, so the window holds >= n_miss free lines. ----
+    int32_t* s_pin = (int32_t*)&s_k[0][0];  // the sort keys are dead: 8192 words
+    int32_t* s_victim = s_hash[0];         // the hash tables too: kMH words each
+    int32_t* s_line = s_hash[1];
+    const int L = a.L, hand = c->hand;
+    const int W = min(L, kWsWindowMulti);
+    for (int w = tid; w < kWsWindowMulti; w += T) s_pin[w] = 0;
+    __syncthreads();
+    int32_t ln[U];
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      ln[h] = -1;
+      const int u = tid + h * T;
+      if (u < Q) {
+        ln[h] = a.slot_of[s_idx[u]];
+        if (ln[h] >= 0) {
+          const int o = (ln[h] - hand + L) % L;
+          if (o < W) s_pin[o] = 1;
+        }
+      }
+    }
+    __syncthreads();
+    // misses in union order: element h of every thread is union row tid + h T,
+    // so one scan per h
+    int mrank[U], n_miss = 0;
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      const bool mh = tid + h * T < Q && ln[h] < 0;
+      int tot = 0;
+      mrank[h] = n_miss + block_scan_merge<1>((int)mh, s_wsum, &tot);
+      n_miss += tot;
+    }
+    // free window slots SPT t .. SPT t + SPT - 1 in window order
+    constexpr int SPT = kWsWindowMulti / T;
+    bool fr[SPT];
+    int nf = 0;
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      fr[k] = SPT * tid + k < W && !s_pin[SPT * tid + k];
+      nf += (int)fr[k];
+    }
+    int n_free = 0;
+    const int frank = block_scan_merge<4>(nf, s_wsum, &n_free);
+    int at = frank, last_used = -1;
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      if (fr[k]) {
+        if (at < n_miss) {
+          s_victim[at] = (hand + SPT * tid + k) % L;
+          last_used = SPT * tid + k;
+        }
+        ++at;
+      }
+    }
+    __syncthreads();
+    if (last_used >= 0 && frank < n_miss && at >= n_miss) c->hand = (hand + last_used + 1) % L;  // the last victim
+#pragma unroll
+    for (int h = 0; h < U; ++h) {
+      const int u = tid + h * T;
+      if (u < Q && ln[h] < 0) {
+        const int r = mrank[h];
+        const int32_t row = s_idx[u];
+        const int32_t vl = s_victim[r];
+        const int32_t old = a.key_of[vl];
+        if (old >= 0) a.slot_of[old] = -1;  // evicted (never a member: members' lines are pinned)
+        a.key_of[vl] = row;
+        a.slot_of[row] = vl;
+        c->miss_row[r] = row;
+        c->miss_line[r] = vl;
+        ln[h] = vl;
+      }
+      if (u < Q) s_line[u] = ln[h];
+    }
+    if (lead) {
+      c->n_miss = n_miss;
+      c->rows_computed += n_miss;
+      c->row_hits += Q - n_miss;
+    }
+    __syncthreads();
+  }
+  for (int u = tid; u < Q; u += T) {
+    const int32_t row = s_idx[u];
+    c->uidx[par][u] = row;
+    const int pi = u >> 1, b = pi % P, la = 2 * (pi / P) + (u & 1);
+    c->idx[par][b * a.q_max + la] = row;
+    c->line[par][b * a.q_max + la] = a.cache ? s_hash[1][u] : row;  // cache: s_line; dense: line i is row i
+    atomicMax(&s_qb[b], la + 1);
+  }
+  __syncthreads();
+  if (tid < a.blocks) c->qb[par][tid] = s_qb[tid];  // inactive blocks: 0 rows
+  if (lead) {
+    c->uq[par] = Q;
+    c->q[par] = Q;
+    c->p_round = P;
+    c->b_hi = b_hi;
+    c->b_lo = b_lo;
+    WS_STAMP(2);
+  }
+}
+
+
+// P x q_max workgroups: workgroup p q_max + a gathers row a of block p's
+// sub-Gram (block p's columns) and the row's f / alpha / y
+__global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArgs a) {
+  __shared__ int32_t s_idx[kWsMax];
+  WsCtrl* c = a.ctrl;
+  if (c->done != kRunning) return;
+  const int tid = threadIdx.x;
+  const int par = (int)(c->outer & 1);
+  const int p = (int)blockIdx.x / a.q_max, ra = (int)blockIdx.x % a.q_max;
+  const int q = c->qb[par][p];
+  WsArgs b = a;
+  b.subg = a.subg + (size_t)p * a.q_max * a.q_max;
+  b.aux = a.aux + (size_t)p * kWsMax;  // f / alpha / y of block p at stride aux_stride
+  if (ra >= q) {
+    ws_gather_row(b, c, s_idx, q, ra, nullptr);
+    return;
+  }
+  for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][p * a.q_max + t];
+  __syncthreads();
+  // the row's line (dense: the resident Gram's row itself)
+  const int64_t line = a.cache ? (int64_t)c->line[par][p * a.q_max + ra] : (int64_t)s_idx[ra];
+  ws_gather_row(b, c, s_idx, q, ra, a.gram + line * a.ldg);
+  if (tid == 0 && blockIdx.x == 0) WS_STAMP(8);
+}
+
+// The adaptive block count reached 1: the host switches to the one-block round
+// kernels at a block boundary (gpu_engines.hip).  Their merge retains the
+// previous set from idx[par ^ 1][0 .. q[par ^ 1]) in newest-first order, which
+// the multi-block merge kept as the union (uidx, uq): copy it over (at most
+// q_max rows, the newest).  One workgroup, stream-ordered between two rounds.
+__global__ __launch_bounds__(256) void ws_to_single_kernel(WsArgs a) {
+  WsCtrl* c = a.ctrl;
+  const int pp = (int)((c->outer + 1) & 1);  // the last round's parity (outer - 1) & 1
+  const int q = min(c->uq[pp], a.q_max);
+  for (int i = threadIdx.x; i < q; i += blockDim.x) c->idx[pp][i] = c->uidx[pp][i];
+  if (threadIdx.x == 0) c->q[pp] = q;
+}
+
+// Partitioned X, cache mode: the X rows of this round's cache misses, packed
+// for the row GEMM.  Block i < q_max: row i of the pack = X row miss_row[i]
+// when this rank owns it, else zeros — the sum all-reduce over ranks then
+// leaves every rank holding the exact rows (x + 0 + ... = x); rows past n_miss
+// are zeroed too (never read by the GEMM, kept finite).  xsq is global on
+// every rank: the packed norms are local.
+__global__ __launch_bounds__(256) void ws_pack_rows_kernel(const float* __restrict__ x, int64_t off, int64_t nl,
+                                                           int dp, const float* __restrict__ xsq,
+                                                           const WsCtrl* __restrict__ c, float* __restrict__ out,
+                                                           float* __restrict__ out_sq) {
+  const int i = blockIdx.x;
+  const int m = c->n_miss;
+  const int64_t row = i < m ? (int64_t)c->miss_row[i] : -1;
+  const bool own = row >= off && row < off + nl;
+  f4* dst = (f4*)(out + (size_t)i * dp);
+  const f4* src = (const f4*)(x + (size_t)(own ? row - off : 0) * dp);
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int k = threadIdx.x; k < dp / 4; k += blockDim.x) dst[k] = own ? src[k] : z;
+  if (threadIdx.x == 0) out_sq[i] = row >= 0 ? xsq[row] : 0.f;
+}
+
+}  // namespace dev
+
+namespace launch {
+
+void ws_merge_multi(const WsArgs& a, hipStream_t s) {
+  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.blocks * a.q_max <= kWsMaxAll && !a.xpeer && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
+                  (!a.cache || ws_cache_multi_supported(a.L, a.blocks, a.q_max)),
+              "ws_merge_multi: multi-block rounds need the collectives, <= 256 candidate lists, an even q_max and "
+              "(cache mode) L >= 2 P q_max + 4096 lines");
+  DPSVM_CHECK(a.sorted != nullptr, "ws_merge_multi: no sort buffer");
+  dev::ws_rank_kernel<<<2 * dev::kRankChunks, dev::kRankThreads, 0, s>>>(a);
+  post_launch("ws_rank", s);
+  dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
+  post_launch("ws_merge_multi", s);
+}
+
+void ws_gather(const WsArgs& a, hipStream_t s) {
+  if (a.blocks > 1) {
+    dev::ws_gather_multi_kernel<<<dim3(a.blocks * a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+    post_launch("ws_gather_multi", s);
+  } else if (a.cache) {
+    dev::ws_gather_lines_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+    post_launch("ws_gather_lines", s);
+  } else {
+    dev::ws_gather_kernel<<<dim3(a.q_max), dev::kWsGatherThreads, 0, s>>>(a);
+    post_launch("ws_gather", s);
+  }
+}
+
+void ws_merge(const WsArgs& a, hipStream_t s) {
+  dev::ws_merge_kernel<<<1, dev::kWsGatherThreads, 0, s>>>(a);
+  post_launch("ws_merge", s);
+}
+
+void ws_to_single(const WsArgs& a, hipStream_t s) {
+  dev::ws_to_single_kernel<<<1, 256, 0, s>>>(a);
+  post_launch("ws_to_single", s);
+}
+
+void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* xsq, const WsCtrl* ctrl, int q_max,
+                  float* out, float* out_sq, hipStream_t s) {
+  DPSVM_CHECK(dp % 16 == 0, "ws_pack_rows: dp must be a multiple of 16");
+  dev::ws_pack_rows_kernel<<<dim3(q_max), 256, 0, s>>>(x, off, nl, dp, xsq, ctrl, out, out_sq);
+  post_launch("ws_pack_rows", s);
+}
+
+bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max + dev::kWsWindow; }
+
+bool ws_cache_multi_supported(int64_t L, int blocks, int q_max) {
+  return L >= 2 * (int64_t)blocks * q_max + dev::kWsWindowMulti;
+}
+
+}  // namespace launch
+}  // namespace dpsvm

@@ -1,0 +1,373 @@
+// Working-set engine, selection pass (ws_select): the round's alpha changes
+// applied to every f_j — one pass, or the two passes around the multi-block
+// line search — then each workgroup's candidate keys per side.  Round
+// structure and shared helpers: ws_common.hpp.
+#include <hip/hip_runtime.h>
+
+#include "dpsvm/common.hpp"
+#include "dpsvm/device_state.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+#include "ws_common.hpp"
+#include "../runtime/hip_check.hpp"
+
+namespace dpsvm {
+namespace dev {
+
+// ---------------------------------------------------------------------------
+// ws_select: f update of the last round + per-workgroup candidates
+// ---------------------------------------------------------------------------
+// Threads of a workgroup: 256 rows (x RPT) times PARTS partitions of the
+// changed-row list.  Each partition sums its contiguous slice of the list in
+// list order; the slices combine in partition order — the rounding depends on
+// the list only (never on the grid or the rank count), and every thread has at
+// most ~48 Gram loads of one batch in flight instead of a chain of batches.
+template <int RPT>
+constexpr int ws_parts() {
+  // register budget: <= 4 waves per SIMD at RPT <= 4, 2 up to 16, 1 at 32 (2M rows on one GPU)
+  return RPT <= 4 ? 4 : RPT <= 16 ? 2 : 1;
+}
+
+// MODE 0: one pass (f += the round's change, then candidates).  Multi-block
+// rounds split it: MODE 1 computes the change d_f into a.dfs and per-workgroup
+// partial sums of the line search (d'Qd = sum_j c_j d_f_j and g'd = -sum_j c_j
+// f_j over the changed rows j, c_j = d_alpha_j y_j), MODE 2 takes
+// t = min(1, g'd / d'Qd) from the partials (fixed order: every workgroup the
+// same t), applies f += t d_f and alpha = alpha_new - (1 - t) d_alpha, then
+// selects the candidates.  Pass 2 walks no list: one partition, 256 threads.
+template <int RPT, int MODE>
+constexpr int ws_sel_parts() {
+  return MODE == 2 ? 1 : ws_parts<RPT>();
+}
+
+template <int RPT, int MODE>
+__global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void ws_select_kernel(WsArgs a) {
+  constexpr int PARTS = ws_sel_parts<RPT, MODE>();
+  constexpr int CH = RPT >= 32 ? 1 : RPT >= 8 ? 4 : 48 / RPT;  // Gram loads in flight per thread (vmcnt <= 63)
+  constexpr int LMAX = MODE == 1 ? kWsMaxAll : MODE == 0 ? kWsMax : 1;
+  __shared__ int32_t s_idx[LMAX];  // lines of the changed rows
+  __shared__ float s_coef[LMAX];
+  __shared__ double s_red[2][kWsSelThreads * PARTS / 64];
+  __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][PARTS > 1 ? kWsSelThreads * RPT : 1];
+  __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x & (kWsSelThreads - 1), part = threadIdx.x / kWsSelThreads;
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(MODE == 1 ? 22 : 6);  // pass 1: own slots (22, 23)
+  const int na = c->n_apply;
+  const int done = c->done;
+  if (na == 0 && (done != kRunning || MODE == 1)) return;
+  if constexpr (MODE == 0) {
+    for (int k = threadIdx.x; k < na; k += kWsSelThreads * PARTS) {
+      s_idx[k] = c->apply_line[k];
+      s_coef[k] = c->apply_coef[k];
+    }
+  }
+  // a workgroup owns a.rpt x 256 rows (ws_geometry); RPT (>= a.rpt) only sizes the registers.
+  // MODE 1 runs KS = a.ks workgroups per row group, each over its KS-th of the
+  // changed-row list (pass 1 fills the device when G is small: 30 groups per rank at
+  // 8 ranks on the headline); pass 2 sums the KS partial changes in slice order.
+  const int KS = MODE == 1 ? max(1, a.ks) : 1;
+  const int grp = MODE == 1 ? (int)(blockIdx.x % a.G) : (int)blockIdx.x, ksi = MODE == 1 ? (int)(blockIdx.x / a.G) : 0;
+  if constexpr (MODE == 1) {
+    // the blocks' apply segments, concatenated in block order; this workgroup
+    // loads only its slice [e_lo, e_hi) of the list (at their list positions)
+    const int per_wg = PARTS * ((na + PARTS * KS - 1) / (PARTS * KS));
+    const int e_lo = min(na, ksi * per_wg), e_hi = min(na, e_lo + per_wg);
+    int at = 0;
+    for (int p = 0; p < a.blocks && at < e_hi; ++p) {
+      const int nb = c->nab[p];
+      const int k0 = max(0, e_lo - at), k1 = min(nb, e_hi - at);
+      for (int k = k0 + threadIdx.x; k < k1; k += kWsSelThreads * PARTS) {
+        s_idx[at + k] = c->apply_line[p * a.q_max + k];
+        s_coef[at + k] = c->apply_coef[p * a.q_max + k];
+      }
+      at += nb;
+    }
+  }
+  __syncthreads();
+  const int64_t base = (int64_t)grp * a.rpt * kWsSelThreads + tid;
+  float f[RPT];
+  bool has[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int64_t j = base + (int64_t)r * kWsSelThreads;
+    has[r] = r < a.rpt && j < a.nl;
+    f[r] = has[r] && part == 0 ? a.f[j] : 0.f;
+  }
+  if (na > 0) {
+    float acc[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+    if constexpr (MODE != 2) {
+    const int per = (na + PARTS * KS - 1) / (PARTS * KS);
+    const int k_lo = min(na, (ksi * PARTS + part) * per), k_hi = min(na, k_lo + per);
+    for (int k0 = k_lo; k0 < k_hi; k0 += CH) {
+      float kv[CH][RPT];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int kk = min(k0 + u, k_hi - 1);
+        const float* row = a.gram + (int64_t)s_idx[kk] * a.ldg;
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) kv[u][r] = has[r] ? row[base + r * kWsSelThreads] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        if (k0 + u < k_hi) {
+          const float cc = s_coef[k0 + u];
+#pragma unroll
+          for (int r = 0; r < RPT; ++r) acc[r] = f_add1(acc[r], cc, kv[u][r]);
+        }
+      }
+    }
+    if (PARTS > 1) {
+      if (part > 0) {
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) s_part[part - 1][r * kWsSelThreads + tid] = acc[r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 1; p < PARTS; ++p) {
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+#pragma clang fp contract(off)
+          acc[r] = acc[r] + s_part[p - 1][r * kWsSelThreads + tid];
+        }
+      }
+    }
+    }  // MODE != 2
+    if constexpr (MODE == 1) {
+      double sq = 0.0, sg = 0.0;
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        if (has[r] && part == 0) {
+          const int64_t j = base + r * kWsSelThreads;
+          a.dfs[(int64_t)ksi * a.nl + j] = acc[r];
+          const float dj = a.dalpha[a.off + j];
+          if (dj != 0.f) {
+            const double cj = (double)dj * (double)a.y[a.off + j];
+            sq += cj * (double)acc[r];  // d'Qd is linear in the KS partial changes
+            if (ksi == 0) sg -= cj * (double)f[r];
+          }
+        }
+      }
+      // fixed-order block sums (butterfly per wave, waves in order)
+      sq = wave_sum_f64(sq);
+      sg = wave_sum_f64(sg);
+      const int w = threadIdx.x >> 6;
+      if ((threadIdx.x & 63) == 0) {
+        s_red[0][w] = sq;
+        s_red[1][w] = sg;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double tq = 0.0, tg = 0.0;
+        for (int k = 0; k < kWsSelThreads * PARTS / 64; ++k) {
+          tq += s_red[0][k];
+          tg += s_red[1][k];
+        }
+        const int64_t slot = ((int64_t)a.rank * a.G + grp) * KS + ksi;
+        a.part[2 * slot] = tq;
+        a.part[2 * slot + 1] = tg;
+        if (blockIdx.x == 0) WS_STAMP(23);
+      }
+      return;
+    }
+    if constexpr (MODE == 2) {
+      const int pr = c->p_round;  // written by this round's merge (p_act may change below)
+      const float t = ws_line_search(a, pr);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->t_last = t;
+        if (t < 1.f) {
+          // strongly coupled blocks: fewer from the next round on (the solve's
+          // commit may have set p_act = 1 already: an independent-clip event)
+          c->n_damped = c->n_damped + 1;
+          const int np = t < a.t_halve ? max(1, pr / 2) : pr;
+          if (np < c->p_act) c->p_act = np;
+          if (c->p_act == 1 && c->p1_round == 0) c->p1_round = c->outer;
+          ws_status(a.status, c);  // p1_round visible with the round that set it (gpu_engines.hip)
+        }
+      }
+      if (a.world > 1 && blockIdx.x == 0) {
+        // alpha is global on every rank: the changed rows this rank does not own
+        // (its threads below fix the owned ones before classifying them)
+        for (int p = 0; p < a.blocks; ++p) {
+          const int nb = c->nab[p];
+          for (int k = threadIdx.x; k < nb; k += kWsSelThreads * PARTS) {
+            const int64_t gi = c->apply_idx[p * a.q_max + k];
+            if (gi >= a.off && gi < a.off + a.nl) continue;
+            if (t < 1.f) a.alpha[gi] = clip01(a.alpha[gi] - (1.f - t) * a.dalpha[gi], 0.f, a.C);
+            a.dalpha[gi] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        if (has[r] && part == 0) {
+          const int64_t j = base + r * kWsSelThreads;
+          float d = a.dfs[j];
+          for (int k = 1; k < a.ks; ++k) {
+#pragma clang fp contract(off)
+            d = d + a.dfs[(int64_t)k * a.nl + j];
+          }
+          acc[r] = t == 1.f ? d : t * d;
+          const float dj = a.dalpha[a.off + j];
+          if (dj != 0.f) {
+            if (t < 1.f) a.alpha[a.off + j] = clip01(a.alpha[a.off + j] - (1.f - t) * dj, 0.f, a.C);
+            a.dalpha[a.off + j] = 0.f;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+#pragma clang fp contract(off)
+      f[r] = f[r] + acc[r];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (has[r] && part == 0) a.f[base + r * kWsSelThreads] = f[r];
+      bad |= has[r] && part == 0 && !isfinite(f[r]);
+    }
+    if (bad) atomicOr(&c->nonfinite, 1);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(10);
+  if (done != kRunning) return;  // uniform
+
+  // partition 0 (waves 0..3) classifies and extracts; the other waves idle to
+  // the one barrier below (no wave leaves before it)
+  uint64_t ku[RPT], kl[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    ku[r] = kl[r] = kKeyNone;
+    if (has[r] && part == 0) {
+      const int64_t gj = a.off + base + r * kWsSelThreads;
+      const float av = a.alpha[gj], yv = a.y[gj];
+      if (in_up(av, yv, a.C)) ku[r] = make_key(f[r], (uint32_t)gj);
+      if (in_low(av, yv, a.C)) kl[r] = make_key(-f[r], (uint32_t)gj);
+    }
+  }
+  // each wave's kWsCand smallest keys per side (DPP minima, no barrier), then
+  // wave 0 merges the four lists; the owner of a winner drops it (keys are
+  // unique: the global index is in the low bits)
+  const int lane = tid & 63, wave = tid >> 6;
+  // multi-block merges read kWsCand keys per list (MODE 2: every multi-block
+  // round, the seed included), the one-block merge kWsCand1 (MODE 0)
+  constexpr int nc = MODE == 0 ? kWsCand1 : kWsCand;
+  for (int round = 0; round < nc && part == 0; ++round) {
+    uint64_t mu = kKeyNone, ml = kKeyNone;
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      mu = ku[r] < mu ? ku[r] : mu;
+      ml = kl[r] < ml ? kl[r] : ml;
+    }
+    mu = wave_min_u64(mu);
+    ml = wave_min_u64(ml);
+    if (lane == 0) {
+      s_wc[wave][0][round] = mu;
+      s_wc[wave][1][round] = ml;
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (ku[r] == mu) ku[r] = kKeyNone;
+      if (kl[r] == ml) kl[r] = kKeyNone;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    constexpr int W = kWsSelThreads / 64;
+    const bool have = lane < W * kWsCand && (nc == kWsCand || lane % kWsCand < nc);  // the waves' nc entries
+    uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
+    uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
+    uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
+    uint64_t pu[kWsCand1], pl[kWsCand1];  // uniform: every lane holds the first kWsCand1
+    for (int round = 0; round < nc; ++round) {
+      const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
+      if (lane == 0) {
+        out[round] = mu;
+        out[kWsCand + round] = ml;
+      }
+      if (round < kWsCand1) {
+        pu[round] = mu;
+        pl[round] = ml;
+      }
+      if (eu == mu) eu = kKeyNone;
+      if (el == ml) el = kKeyNone;
+    }
+    if (a.xpeer != nullptr && lane < a.world) {  // lane p publishes to rank p
+      uint64_t* dst = a.xpeer[lane] + ws_xcand(a, (int)(c->outer & 1), a.xrank * a.G + blockIdx.x);
+      const uint64_t t = xtag((uint32_t)c->outer + 1u);
+#pragma unroll
+      for (int r = 0; r < kWsCand1; ++r) {
+        xch_store<true>(dst + 2 * r, t | (pu[r] >> 16));
+        xch_store<true>(dst + 2 * r + 1, t | (pu[r] & 0xffffull));
+        xch_store<true>(dst + 2 * kWsCand1 + 2 * r, t | (pl[r] >> 16));
+        xch_store<true>(dst + 2 * kWsCand1 + 2 * r + 1, t | (pl[r] & 0xffffull));
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(7);
+}
+
+}  // namespace dev
+
+namespace launch {
+
+int ws_pass1_splits(int G) {
+  // about one pass-1 workgroup per CU of the 256-CU device: the selection
+  // geometry gives a rank of P only G = ceil(60000 / P / 256) groups on the
+  // headline (30 at P = 8), and pass 1 is then bound by the few CUs issuing
+  // loads — 3,072 changed rows x 7,500 columns: 114 us with 30 workgroups, 38 us
+  // with 240; with 60,000 columns 235 workgroups beat 470 / 705 (158 vs 167 /
+  // 189 us; profiles/r3_pass1_probe.txt).  Every rank uses the same G, so the
+  // same slice count and the same summation order.
+  return std::max(1, std::min(kWsMaxPass1Splits, 256 / std::max(1, G)));
+}
+
+void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt) {
+  // every rank the same geometry (sized for the largest shard); the merge reads
+  // world * G <= 1024 candidate lists (kWsListsPerThread per merge thread), so
+  // up to 8 ranks keep 128-256 selection workgroups each
+  const int64_t gmax = std::max<int64_t>(
+      1, std::min<int64_t>(kWsMaxGroups, (int64_t)kWsListsPerThread * 256 / std::max(1, world)));
+  const int64_t g = std::max<int64_t>(1, std::min<int64_t>(gmax, (nl_max + kWsSelThreads - 1) / kWsSelThreads));
+  const int64_t r = (nl_max + g * kWsSelThreads - 1) / (g * kWsSelThreads);
+  *G = (int32_t)g;
+  *rpt = (int32_t)std::max<int64_t>(1, r);
+}
+
+bool ws_supported(int64_t nl_max, int world, int q_max) {
+  int32_t G = 0, rpt = 0;
+  ws_geometry(nl_max, world, &G, &rpt);
+  return q_max >= 2 && q_max <= kWsMax && rpt <= kWsMaxRPT && nl_max < (int64_t)1 << 31 && world <= kWsMaxGroups;
+}
+
+template <int MODE>
+static void ws_select_mode(const WsArgs& a, hipStream_t s) {
+  const dim3 grid(a.G * (MODE == 1 ? std::max(1, a.ks) : 1));
+  auto threads = [](int rpt) { return dim3(MODE == 2 ? kWsSelThreads : kWsSelThreads * (rpt <= 4 ? 4 : rpt <= 16 ? 2 : 1)); };
+  if (a.rpt <= 1) dev::ws_select_kernel<1, MODE><<<grid, threads(1), 0, s>>>(a);
+  else if (a.rpt <= 2) dev::ws_select_kernel<2, MODE><<<grid, threads(2), 0, s>>>(a);
+  else if (a.rpt <= 4) dev::ws_select_kernel<4, MODE><<<grid, threads(4), 0, s>>>(a);
+  else if (a.rpt <= 8) dev::ws_select_kernel<8, MODE><<<grid, threads(8), 0, s>>>(a);
+  else if (a.rpt <= 16) dev::ws_select_kernel<16, MODE><<<grid, threads(16), 0, s>>>(a);
+  else dev::ws_select_kernel<32, MODE><<<grid, threads(32), 0, s>>>(a);
+  post_launch("ws_select", s);
+}
+
+void ws_select(const WsArgs& a, hipStream_t s) {
+  if (a.blocks > 1) {
+    ws_select_mode<1>(a, s);  // d_f + line-search partials
+    ws_select_mode<2>(a, s);  // f += t d_f, candidates
+  } else {
+    ws_select_mode<0>(a, s);
+  }
+}
+
+void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
+  if (pass == 1) ws_select_mode<1>(a, s);
+  else ws_select_mode<2>(a, s);
+}
+
+}  // namespace launch
+}  // namespace dpsvm

@@ -15,7 +15,7 @@
 //                     (smo_kernels.hip): the partitioned-X fallback
 //   ws-dense          Gram resident; working-set rounds: one workgroup solves a
 //                     q-row sub-problem from an LDS sub-Gram, one grid pass
-//                     updates f and selects the next candidates (smo_ws.hip)
+//                     updates f and selects the next candidates (ws_*.hip)
 //   ws-cache          kernel-row cache; working-set rounds whose missing rows
 //                     come from one MFMA GEMM per round
 //
@@ -400,7 +400,7 @@ void capture_rounds(GpuSolver::Impl& m, int B, hipGraph_t* graph, hipGraphExec_t
   HIP_CHECK(hipGraphInstantiate(exec, *graph, nullptr, nullptr, 0));
 }
 
-// Working-set rounds (smo_ws.hip) on the resident Gram (ws-dense) or on a
+// Working-set rounds (ws_*.hip) on the resident Gram (ws-dense) or on a
 // kernel-row cache (ws-cache: the Gram does not fit HBM).  A round is
 //   [merge (+ cache mode: line assignment, one MFMA GEMM for the set's missing
 //   rows)] -> gather (sub-Gram rows) -> solve (LDS sub-problem) -> select (f

@@ -92,7 +92,7 @@ struct GpuSolver::Impl {
   std::string xch_diag;
   std::string xch_mem = "none";    // receive-buffer memory kind
   int64_t Gf = 0, RBf = 0;         // fused / persistent geometry: workgroups, rows per workgroup
-  // working-set engine (smo_ws.hip): round control record, candidate keys
+  // working-set engine (ws_*.hip): round control record, candidate keys
   WsArgs wsa{};
   int ws_q1 = 0;                    // the one-block rounds' q_max (multi-block rounds may use smaller blocks)
   WsCtrl* wsctrl = nullptr;

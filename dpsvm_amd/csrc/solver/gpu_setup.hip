@@ -488,7 +488,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool want_xch = (!ws_cand && !wsc_cand && m.dense && m.p.exchange != 1 && (m.world > 1 || m.p.exchange == 2)) ||
                         pdense_cand || plru_cand;
   // working-set engines at world > 1: the rounds' candidate lists and sub-Gram
-  // rows through the same kind of receive buffers (smo_ws.hip, "peer exchange")
+  // rows through the same kind of receive buffers (ws_*.hip, "peer exchange")
   const bool wsc_fits_pre = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
   int32_t ws_G = 0, ws_rpt = 0;
   if (ws_cand || wsc_cand) launch::ws_geometry(nl_max, m.world, &ws_G, &ws_rpt);
@@ -660,7 +660,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.tau = m.p.tau;
     w.clip = (int)m.p.clip;
     w.max_iter = m.p.max_iter;
-    // multi-block rounds (adaptive block count, smo_ws.hip)
+    // multi-block rounds (adaptive block count, ws_*.hip)
     w.blocks = 1;
     m.ws_q1 = ws_q;
     if (want_blocks > 1) {

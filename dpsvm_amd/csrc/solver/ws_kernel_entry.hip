@@ -1,4 +1,4 @@
-// Kernel-level test entry points of the working-set engine (smo_ws.hip): each
+// Kernel-level test entry points of the working-set engine (ws_*.hip): each
 // runs ONE kernel (or the two f-update passes) on crafted device state and
 // returns the state it leaves, so tests/test_kernels_gpu.py can check the
 // merge (sort, stop test, union, block assignment), the LDS pair loop and the

@@ -104,14 +104,14 @@ class SVCConfig:
     verify_ranks: bool = True       # cross-rank alpha digest after each solve (world > 1)
     # solver: auto (ws from 50k rows, else smo) | smo (pair-at-a-time engines, the reference's trajectory) |
     # ws (working-set rounds: the reference's pair rule on a q-row sub-problem
-    # in LDS, the same global stop test; smo_ws.hip)
+    # in LDS, the same global stop test; ws_*.hip)
     solver: str = "auto"
     ws_size: int = 192              # working-set rows (<= 192)
     ws_new: int = 0                 # rows replaced per round (0: 3 ws_size / 4)
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
     # working-set engines: up to P sub-problems per round (1..32, P x ws_size <= 3072; 0 auto = 32 blocks of
     # 96 rows from 50k rows, else 1); adaptive — halved
-    # after every damped round (coupled blocks), then the one-block round kernels (smo_ws.hip)
+    # after every damped round (coupled blocks), then the one-block round kernels (ws_*.hip)
     ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second

@@ -182,7 +182,7 @@ WS_CAND = 8  # candidates per side per selection workgroup (device_state.hpp kWs
 
 def ws_merge_multi(cand, blocks: int, q_max: int, n_new: int, eps: float, prev_union=(), p_act: int | None = None,
                    iteration: int = 0, max_iter: int = 1 << 40) -> dict:
-    """One launch of the multi-block merge (smo_ws.hip ws_merge_multi_kernel) on
+    """One launch of the multi-block merge (ws_*.hip ws_merge_multi_kernel) on
     crafted candidate lists ``cand`` [G][2][WS_CAND] (u64 keys, up then low; KEY_NONE
     for empty slots) and a previous union (newest first).  Returns the new
     union, the [blocks][q_max] block layout (-1 unused), rows per block, the

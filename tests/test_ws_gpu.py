@@ -1,4 +1,4 @@
-"""Working-set engine (solver="ws", smo_ws.hip) on MI355X.
+"""Working-set engine (solver="ws", ws_*.hip) on MI355X.
 
 The ws engine applies the reference's pair rule (svmTrainMain.cpp:255-299) to a
 q-row sub-problem per round, so its trajectory differs from the pair-at-a-time
@@ -353,7 +353,7 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine, n):
 @pytest.mark.parametrize("case", ["blobs", "mnist", "adult"])
 def test_ws_multi_block_rounds_reach_the_reference_optimum(case, clip, blocks):
     """ws_blocks = P: P disjoint sub-problems per round, the combined step scaled
-    by the exact line search (smo_ws.hip, multi-block rounds).  Coupled problems
+    by the exact line search (ws_*.hip, multi-block rounds).  Coupled problems
     (blobs, adult: K far from I) exercise t < 1; the stop test must hold on the
     exact float64 gradient and, with box clipping, the unique dual optimum must
     be reached."""

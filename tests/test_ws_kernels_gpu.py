@@ -1,4 +1,4 @@
-"""Kernel-level tests of the working-set engine (smo_ws.hip): each kernel runs
+"""Kernel-level tests of the working-set engine (ws_*.hip): each kernel runs
 once on crafted state (dpsvm_amd.ops.kernels.ws_*) and is checked against a
 numpy model of the same rule — the merge (sort, stop test, union with
 first-position-wins deduplication, previous-union retention, block
