@@ -343,12 +343,17 @@ struct WsArgs {
   uint64_t* stamps;    // DPSVM_STAMPS diagnostics: s_memrealtime per phase, ring of kStampRing rounds
   // in-kernel peer exchange of the rounds (world > 1; nullptr: the communicator's
   // collectives).  Every rank's receive buffer (uncached, IPC-mapped by its
-  // peers; ws_*.hip "peer exchange"): [2 parity][G_all][2 kWsCand1][2] candidate
-  // granules, then from word xsub [2 parity][q_max][q_max + 1] sub-Gram rows with
-  // the row's f in the last column
+  // peers; ws_common.hpp "peer exchange"): [2 parity][G_all][xcw] candidate
+  // granules (per side xcw / 4 keys of two granules: up at 0, low at xcw / 2),
+  // from word xsub [2 parity][xsub_rows][q_max + 1] sub-Gram rows with the row's
+  // f in the last column, and (multi-block rounds) from word xpart [2 parity]
+  // [G_all * ks][4] line-search partials (two doubles of two granules each)
   uint64_t* const* xpeer;
   int32_t xrank;
+  int32_t xcw;       // granules per candidate slot: 4 kWsCand1 (one-block engine) or 4 kWsCand (multi-block)
   int64_t xsub;
+  int64_t xsub_rows; // sub-Gram rows per parity (blocks x q_max of the widest view)
+  int64_t xpart;
   int64_t xtimeout_ticks;  // give-up bound of one poll (s_memrealtime, 100 MHz)
   // multi-block rounds (P = blocks > 1): subg / aux hold P blocks
   // ([P][q_max][q_max], [P][3][kWsMax]); the f update runs in two passes
@@ -364,9 +369,20 @@ struct WsArgs {
   int32_t ks;          // multi-block pass 1: list slices over workgroups (dfs [ks][nl], part [G_all][ks][2])
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
 };
-// u64 words of the working-set exchange region (both parities)
+// u64 words of the working-set exchange region (both parities): one-block
+// engine
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {
   return 2 * G_all * 4 * kWsCand1 + 2 * q_max * (q_max + 1);
+}
+// multi-block engine (P blocks of q rows; its one-block rounds use q1 rows):
+// candidates (kWsCand keys per side), line-search partials, sub-Gram rows
+constexpr int64_t ws_xch_cand_words_multi(int64_t G_all) { return 2 * G_all * 4 * kWsCand; }
+constexpr int64_t ws_xch_part_words(int64_t G_all, int64_t ks) { return 2 * G_all * ks * 4; }
+constexpr int64_t ws_xch_sub_words(int64_t P, int64_t q, int64_t q1) {
+  return 2 * ((P * q * (q + 1)) > (q1 * (q1 + 1)) ? P * q * (q + 1) : q1 * (q1 + 1));
+}
+constexpr int64_t ws_xch_words_multi(int64_t G_all, int64_t ks, int64_t P, int64_t q, int64_t q1) {
+  return ws_xch_cand_words_multi(G_all) + ws_xch_part_words(G_all, ks) + ws_xch_sub_words(P, q, q1);
 }
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;

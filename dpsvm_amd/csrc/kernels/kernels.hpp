@@ -81,6 +81,10 @@ void ws_solve(const WsArgs& a, hipStream_t s);
 // row GEMM; ws_gather then reads the sub-Gram from the members' lines
 void ws_merge(const WsArgs& a, hipStream_t s);
 // multi-block rounds (a.blocks > 1, ws-dense at one rank): the union merge before ws_gather
+// multi-block rounds over the peer exchange: every rank's candidate lists / line-search
+// partials from this rank's receive buffer into cand / part (the all-gathers' layout)
+void ws_xcollect_cand(const WsArgs& a, hipStream_t s);
+void ws_xcollect_part(const WsArgs& a, hipStream_t s);
 void ws_merge_multi(const WsArgs& a, hipStream_t s);
 // the adaptive block count reached 1: the last union becomes the one-block
 // kernels' previous set (run once, between two rounds)

@@ -246,14 +246,45 @@ __device__ __forceinline__ void ws_status(SmoStatus* s, const WsCtrl* c) {
 // kCommFail on this rank, and its peers time out the same way.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int64_t ws_xcand(const WsArgs& a, int par, int slot) {
-  return ((int64_t)par * a.G_all + slot) * (4 * kWsCand1);
+  return ((int64_t)par * a.G_all + slot) * a.xcw;
 }
 
 __device__ __forceinline__ int64_t ws_xrow(const WsArgs& a, int par, int row) {
-  return a.xsub + ((int64_t)par * a.q_max + row) * (a.q_max + 1);
+  return a.xsub + ((int64_t)par * a.xsub_rows + row) * (a.q_max + 1);
+}
+
+// multi-block rounds: slot k (= (rank G + group) ks + slice) of the line-search partials
+__device__ __forceinline__ int64_t ws_xpart(const WsArgs& a, int par, int64_t k) {
+  return a.xpart + ((int64_t)par * a.G_all * max(1, a.ks) + k) * 4;
 }
 
 __device__ __forceinline__ bool ws_tag_ok(uint64_t g, uint64_t t) { return (g >> 48) == (t >> 48); }
+
+// a 64-bit payload as two granules (bits 63..16, bits 15..0) and back
+__device__ __forceinline__ void ws_put64(uint64_t* dst, uint64_t t, uint64_t v) {
+  xch_store<true>(dst, t | (v >> 16));
+  xch_store<true>(dst + 1, t | (v & 0xffffull));
+}
+__device__ __forceinline__ uint64_t ws_get64(uint64_t g0, uint64_t g1) {
+  return ((g0 & ((1ull << 48) - 1)) << 16) | (g1 & 0xffffull);
+}
+
+// poll n consecutive granules of this rank's buffer until all carry tag t;
+// false after a.xtimeout_ticks (the caller fails the round)
+template <int N>
+__device__ __forceinline__ bool ws_poll(const WsArgs& a, const uint64_t* g, uint64_t t, uint64_t (&out)[N]) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = xch_load<true>(g + i);
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) all &= ws_tag_ok(out[i], t);
+    if (all) return true;
+    if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
 
 // a <- the kWsCand1 smallest of the two ascending lists a, b (unique keys):
 // min(a[i], b[3 - i]) is a bitonic sequence of the 4 smallest, two
@@ -281,6 +312,13 @@ __device__ __forceinline__ void ws_comm_fail(const WsArgs& a, WsCtrl* c) {
     c->n_apply = 0;  // nothing of this round is applied
     ws_status(a.status, c);
   }
+}
+
+// the same from any single thread (no threadIdx condition)
+__device__ __forceinline__ void ws_comm_fail_thread(const WsArgs& a, WsCtrl* c) {
+  c->done = kCommFail;
+  c->n_apply = 0;
+  ws_status(a.status, c);
 }
 
 // fixed-order wave sum (xor butterfly: every lane ends with the same bits)
@@ -313,7 +351,7 @@ __device__ __forceinline__ float ws_line_search(const WsArgs& a, int P) {
   if (P <= 1) return 1.f;
   const int lane = threadIdx.x & 63;
   double q = 0.0, g = 0.0;
-  for (int k = lane; k < a.G_all * max(1, a.ks); k += 64) {  // every rank's partials (all-gathered)
+  for (int k = lane; k < a.G_all * max(1, a.ks); k += 64) {  // every rank's partials (all-gathered / collected)
     q += a.part[2 * k];
     g += a.part[2 * k + 1];
   }

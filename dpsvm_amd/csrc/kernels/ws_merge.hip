@@ -67,28 +67,15 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
         cl[r] = a.cand[(size_t)slot * 2 * kWsCand + kWsCand + r];
       }
     } else {
-      // peer exchange: poll slot `slot` of this rank's buffer
+      // peer exchange: poll slot `slot` of this rank's buffer (up keys at 0,
+      // low keys at a.xcw / 2: ws_select's push)
       const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, slot);
-      uint64_t g[4 * kWsCand1];
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (true) {
-#pragma unroll
-        for (int i = 0; i < 4 * kWsCand1; ++i) g[i] = xch_load<true>(e + i);
-        bool all = true;
-#pragma unroll
-        for (int i = 0; i < 4 * kWsCand1; ++i) all &= ws_tag_ok(g[i], xt);
-        if (all) break;
-        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      constexpr uint64_t m48 = (1ull << 48) - 1;
+      uint64_t gu[2 * kWsCand1], gl[2 * kWsCand1];
+      ok = ok && ws_poll<2 * kWsCand1>(a, e, xt, gu) && ws_poll<2 * kWsCand1>(a, e + a.xcw / 2, xt, gl);
 #pragma unroll
       for (int r = 0; r < kWsCand1; ++r) {
-        cu[r] = ((g[2 * r] & m48) << 16) | (g[2 * r + 1] & 0xffffull);
-        cl[r] = ((g[2 * kWsCand1 + 2 * r] & m48) << 16) | (g[2 * kWsCand1 + 2 * r + 1] & 0xffffull);
+        cu[r] = ws_get64(gu[2 * r], gu[2 * r + 1]);
+        cl[r] = ws_get64(gl[2 * r], gl[2 * r + 1]);
       }
     }
     if (j == 0) {
@@ -551,6 +538,27 @@ __device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* v
   return -1;
 }
 
+// Multi-block rounds over the peer exchange: every rank's candidate lists
+// (pushed by pass 2 of the previous round into this rank's receive buffer) into
+// a.cand, the layout the all-gather leaves, so ws_rank reads them as from the
+// collective.  A few workgroups spin here instead of ws_rank's 128: ranks
+// sharing a device (rehearsals) must leave wave slots for each other's producers.
+constexpr int kXCollectThreads = 256;
+__global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsArgs a) {
+  WsCtrl* c = a.ctrl;
+  if (c->done != kRunning) return;
+  const int e = (int)(blockIdx.x * kXCollectThreads + threadIdx.x);  // (list, side, rank) key
+  bool ok = true;
+  if (e < a.G_all * 2 * kWsCand) {
+    const int l = e / (2 * kWsCand), side = (e / kWsCand) & 1, r = e % kWsCand;
+    uint64_t g[2];
+    ok = ws_poll<2>(a, a.xpeer[a.xrank] + ws_xcand(a, (int)(c->outer & 1), l) + side * (a.xcw / 2) + 2 * r,
+                    xtag((uint32_t)c->outer + 1u), g);
+    a.cand[e] = ok ? ws_get64(g[0], g[1]) : kKeyNone;
+  }
+  if (!ok) ws_comm_fail_thread(a, c);
+}
+
 // ws_rank: the multi-block merge's sort, spread over a grid of 2 sides x
 // kRankChunks workgroups instead of one workgroup's bitonic network (29 of the
 // merge's 41 us at 3,072-row unions, profiles/r3_ws_stamps_32x96.json).  A
@@ -868,6 +876,41 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArg
   WsArgs b = a;
   b.subg = a.subg + (size_t)p * a.q_max * a.q_max;
   b.aux = a.aux + (size_t)p * kWsMax;  // f / alpha / y of block p at stride aux_stride
+  if (a.xpeer != nullptr) {
+    // peer exchange: push the entries (ra, b) of the columns this rank owns and
+    // the row's f (when owned) into row p q_max + ra of every rank's buffer;
+    // ws_solve polls them (no workgroup of this kernel waits: rows past q need
+    // nothing, the solve zero-fills them).  alpha / y are global: local aux.
+    if (ra >= q) return;
+    for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][p * a.q_max + t];
+    __syncthreads();
+    const int64_t line = a.cache ? (int64_t)c->line[par][p * a.q_max + ra] : (int64_t)s_idx[ra];
+    const float* src = a.gram + line * a.ldg;
+    const int64_t lo = a.off, hi = a.off + a.nl, gi = s_idx[ra];
+    const uint64_t t = xtag((uint32_t)c->outer + 1u);
+    const int64_t row = ws_xrow(a, par, p * a.q_max + ra);
+    for (int col = tid; col <= q; col += kWsGatherThreads) {
+      uint64_t v;
+      int at;
+      if (col < q) {
+        const int64_t gj = s_idx[col];
+        if (gj < lo || gj >= hi) continue;
+        v = t | __float_as_uint(src[gj - lo]);
+        at = col;
+      } else {  // the row's f, last column
+        if (gi < lo || gi >= hi) continue;
+        v = t | __float_as_uint(a.f[gi - lo]);
+        at = a.q_max;
+      }
+      for (int r = 0; r < a.world; ++r) xch_store<true>(a.xpeer[r] + row + at, v);
+    }
+    if (tid == 0) {
+      b.aux[a.aux_stride + ra] = a.alpha[gi];
+      b.aux[2 * a.aux_stride + ra] = a.y[gi];
+    }
+    if (tid == 0 && blockIdx.x == 0) WS_STAMP(8);
+    return;
+  }
   if (ra >= q) {
     ws_gather_row(b, c, s_idx, q, ra, nullptr);
     return;
@@ -918,12 +961,20 @@ __global__ __launch_bounds__(256) void ws_pack_rows_kernel(const float* __restri
 
 namespace launch {
 
+void ws_xcollect_cand(const WsArgs& a, hipStream_t s) {
+  const int keys = a.G_all * 2 * kWsCand;
+  dev::ws_xcollect_cand_kernel<<<dim3((unsigned)((keys + dev::kXCollectThreads - 1) / dev::kXCollectThreads)),
+                                 dev::kXCollectThreads, 0, s>>>(a);
+  post_launch("ws_xcollect_cand", s);
+}
+
 void ws_merge_multi(const WsArgs& a, hipStream_t s) {
-  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.blocks * a.q_max <= kWsMaxAll && !a.xpeer && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
+  DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.blocks * a.q_max <= kWsMaxAll && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
                   (!a.cache || ws_cache_multi_supported(a.L, a.blocks, a.q_max)),
-              "ws_merge_multi: multi-block rounds need the collectives, <= 256 candidate lists, an even q_max and "
+              "ws_merge_multi: multi-block rounds need <= 256 candidate lists, an even q_max and "
               "(cache mode) L >= 2 P q_max + 4096 lines");
   DPSVM_CHECK(a.sorted != nullptr, "ws_merge_multi: no sort buffer");
+  DPSVM_CHECK(!a.xpeer || a.xcw >= 4 * kWsCand, "ws_merge_multi: peer exchange slots too narrow");
   dev::ws_rank_kernel<<<2 * dev::kRankChunks, dev::kRankThreads, 0, s>>>(a);
   post_launch("ws_rank", s);
   dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);

@@ -48,6 +48,7 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
   __shared__ int32_t s_idx[LMAX];  // lines of the changed rows
   __shared__ float s_coef[LMAX];
   __shared__ double s_red[2][kWsSelThreads * PARTS / 64];
+  __shared__ double s_red_tot[2];
   __shared__ float s_part[PARTS > 1 ? PARTS - 1 : 1][PARTS > 1 ? kWsSelThreads * RPT : 1];
   __shared__ uint64_t s_wc[kWsSelThreads / 64][2][kWsCand];
   WsCtrl* c = a.ctrl;
@@ -165,10 +166,22 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
           tq += s_red[0][k];
           tg += s_red[1][k];
         }
+        s_red_tot[0] = tq;
+        s_red_tot[1] = tg;
         const int64_t slot = ((int64_t)a.rank * a.G + grp) * KS + ksi;
         a.part[2 * slot] = tq;
         a.part[2 * slot + 1] = tg;
         if (blockIdx.x == 0) WS_STAMP(23);
+      }
+      __syncthreads();  // s_red_tot
+      if (a.xpeer != nullptr && threadIdx.x < 64 && (threadIdx.x >> 1) < a.world) {
+        // peer exchange: the slot's two doubles to every rank (lanes 2 p, 2 p + 1: rank p)
+        const int64_t slot = ((int64_t)a.rank * a.G + grp) * KS + ksi;
+        const int64_t R = c->outer;  // committed by this round's solve
+        const uint64_t t = xtag((uint32_t)R + 1u);
+        const int pr = threadIdx.x >> 1, h = threadIdx.x & 1;
+        const double v = h ? s_red_tot[1] : s_red_tot[0];
+        ws_put64(a.xpeer[pr] + ws_xpart(a, (int)(R & 1), slot) + 2 * h, t, (uint64_t)__double_as_longlong(v));
       }
       return;
     }
@@ -280,38 +293,62 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
     uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
     uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
     uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
-    uint64_t pu[kWsCand1], pl[kWsCand1];  // uniform: every lane holds the first kWsCand1
+    uint64_t pu[nc], pl[nc];  // uniform: every lane holds the list
     for (int round = 0; round < nc; ++round) {
       const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
       if (lane == 0) {
         out[round] = mu;
         out[kWsCand + round] = ml;
       }
-      if (round < kWsCand1) {
-        pu[round] = mu;
-        pl[round] = ml;
-      }
+      pu[round] = mu;
+      pl[round] = ml;
       if (eu == mu) eu = kKeyNone;
       if (el == ml) el = kKeyNone;
     }
-    if (a.xpeer != nullptr && lane < a.world) {  // lane p publishes to rank p
+    if (a.xpeer != nullptr && lane < a.world) {
+      // lane p publishes to rank p: the nc keys per side the merge of this
+      // engine reads (slot width a.xcw: up keys at 0, low keys at a.xcw / 2)
       uint64_t* dst = a.xpeer[lane] + ws_xcand(a, (int)(c->outer & 1), a.xrank * a.G + blockIdx.x);
       const uint64_t t = xtag((uint32_t)c->outer + 1u);
+      const int lo = a.xcw / 2;
 #pragma unroll
-      for (int r = 0; r < kWsCand1; ++r) {
-        xch_store<true>(dst + 2 * r, t | (pu[r] >> 16));
-        xch_store<true>(dst + 2 * r + 1, t | (pu[r] & 0xffffull));
-        xch_store<true>(dst + 2 * kWsCand1 + 2 * r, t | (pl[r] >> 16));
-        xch_store<true>(dst + 2 * kWsCand1 + 2 * r + 1, t | (pl[r] & 0xffffull));
+      for (int r = 0; r < nc; ++r) {
+        ws_put64(dst + 2 * r, t, pu[r]);
+        ws_put64(dst + lo + 2 * r, t, pl[r]);
       }
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(7);
 }
 
+// Multi-block rounds over the peer exchange: every rank's line-search partials
+// (pushed by pass 1 into this rank's receive buffer) into a.part, the layout the
+// all-gather leaves — pass 2 then reads them as from the collective.  Runs when
+// pass 1 ran (the round applies changes).
+__global__ __launch_bounds__(256) void ws_xcollect_part_kernel(WsArgs a) {
+  WsCtrl* c = a.ctrl;
+  if (c->n_apply == 0) return;  // pass 1 pushed nothing (or the run ended: n_apply = 0)
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= (int64_t)a.G_all * max(1, a.ks)) return;
+  const int64_t R = c->outer;  // committed by this round's solve, as pass 1 tagged it
+  uint64_t v[4];
+  if (ws_poll<4>(a, a.xpeer[a.xrank] + ws_xpart(a, (int)(R & 1), k), xtag((uint32_t)R + 1u), v)) {
+    a.part[2 * k] = __longlong_as_double((long long)ws_get64(v[0], v[1]));
+    a.part[2 * k + 1] = __longlong_as_double((long long)ws_get64(v[2], v[3]));
+  } else {
+    ws_comm_fail_thread(a, c);
+  }
+}
+
 }  // namespace dev
 
 namespace launch {
+
+void ws_xcollect_part(const WsArgs& a, hipStream_t s) {
+  const int64_t slots = (int64_t)a.G_all * std::max(1, a.ks);
+  dev::ws_xcollect_part_kernel<<<dim3((unsigned)((slots + 255) / 256)), 256, 0, s>>>(a);
+  post_launch("ws_xcollect_part", s);
+}
 
 int ws_pass1_splits(int G) {
   // about one pass-1 workgroup per CU of the 256-CU device: the selection

@@ -164,7 +164,38 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const int ib = blk * a.q_max;
   const float* subg = a.subg + (size_t)blk * ldk * ldk;
   const float* aux = a.aux + (size_t)blk * kWsMax;
-  {
+  bool xok = true;
+  if (kMulti && a.xpeer != nullptr) {
+    // peer exchange: block blk's rows a < q from this rank's receive buffer,
+    // entries (a, b < q) and f (last column) pushed by their owners
+    // (ws_gather_multi); columns q .. q_max - 1 are zeros
+    const int64_t R = c->outer;
+    const uint64_t t = xtag((uint32_t)R + 1u);
+    const uint64_t* mine = a.xpeer[a.xrank];
+    const int w = ldk + 1;
+    for (int e = tid; e < q * w; e += kWsSolveThreads) {
+      const int ra = e / w, col = e - ra * w;
+      if (col < ldk && col >= q) {
+        K[ra * ldk + col] = 0.f;
+        continue;
+      }
+      if (col > ldk) continue;
+      uint64_t v[1];
+      if (!xok || !ws_poll<1>(a, mine + ws_xrow(a, par, ib + ra) + col, t, v)) {
+        xok = false;
+        continue;
+      }
+      const float fv = __uint_as_float((uint32_t)v[0]);
+      if (col < ldk) K[ra * ldk + col] = fv;
+      else s_f[ra] = fv;
+    }
+    if (tid < q) {
+      s_a[tid] = aux[a.aux_stride + tid];
+      s_y[tid] = aux[2 * a.aux_stride + tid];
+      s_idx[tid] = c->idx[par][ib + tid];
+      s_line[tid] = c->line[par][ib + tid];
+    }
+  } else {
     // q rows of the q_max-stride sub-Gram into LDS (147 KiB at q = 192): 16-B
     // loads, four in flight per thread before their stores
     const int n = q * ldk;
@@ -194,7 +225,12 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       s_line[tid] = c->line[par][ib + tid];
     }
   }
-  __syncthreads();
+  bool xfail = false;
+  if (kMulti && a.xpeer != nullptr) xfail = !__syncthreads_and(xok);
+  else __syncthreads();
+  // a rank stopped publishing: this block takes no step; its commit below still
+  // counts it, and the round's last block keeps kCommFail
+  if (xfail && tid == 0) ws_comm_fail_thread(a, c);
   if (tid == 0) WS_STAMP(3);
   if (wave != 0) return;
 
@@ -218,7 +254,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     room = blk < pa ? room / pa + (blk < room % pa ? 1 : 0) : 0;
   }
   // uniform: in an SGPR, so the loop test is one scalar compare
-  const int cap = __builtin_amdgcn_readfirstlane((int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max));
+  const int cap = xfail ? 0 : __builtin_amdgcn_readfirstlane((int)(room < (int64_t)a.inner_max ? room : (int64_t)a.inner_max));
   int inner = 0;
   bool bad = false, clipped_any = false;
   while (inner < cap) {
@@ -368,7 +404,11 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
         c->p_act = 1;
         if (c->p1_round == 0) c->p1_round = c->outer;
       }
-      c->done = any_bad ? kNonFinite : tot_i == 0 ? kNoPair : (it0 + tot_i >= a.max_iter ? kMaxIter : kRunning);
+      if (__hip_atomic_load(&c->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kCommFail) {
+        c->n_apply = 0;  // a block's exchange poll gave up (peer exchange): the run ends here
+      } else {
+        c->done = any_bad ? kNonFinite : tot_i == 0 ? kNoPair : (it0 + tot_i >= a.max_iter ? kMaxIter : kRunning);
+      }
       ws_status(a.status, c);
     }
   }

@@ -332,7 +332,7 @@ void ws_allgather_cand(GpuSolver::Impl& m) {
 
 // multi-block rounds at world > 1: every rank's line-search partials
 void ws_allgather_part(GpuSolver::Impl& m) {
-  if (!m.collectives()) return;
+  if (!m.collectives() || m.wsa.xpeer) return;  // peer exchange: pushed by pass 1, polled by pass 2
   const size_t bytes = (size_t)m.wsa.G * std::max(1, m.wsa.ks) * 2 * sizeof(double);
   uint8_t* all = (uint8_t*)m.wsa.part;
   if (m.comm->device_memory()) {
@@ -429,6 +429,7 @@ struct WsRounds : Base {
     w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * w.q_max;
     w.aux = m.wssub + (size_t)w.q_max * w.q_max;
     w.aux_stride = kWsMax;
+    w.xsub_rows = w.q_max;  // peer exchange: the one-block layout of the sub-Gram rows (same region)
     // the one-block engine's set turnover (multi-block rounds replace the
     // whole union): 3/4 new rows, the newest quarter of the previous set kept
     w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, w.q_max) : 3 * w.q_max / 4);
@@ -467,6 +468,9 @@ struct WsRounds : Base {
     }
   }
   static void round(GpuSolver::Impl& m, const WsArgs& w) {
+    // multi-block rounds over the peer exchange: the candidate lists every rank
+    // pushed at the end of the previous round (or the seed), collected in-kernel
+    if (w.blocks > 1 && w.xpeer) launch::ws_xcollect_cand(w, m.stream);
     if (w.blocks > 1) launch::ws_merge_multi(w, m.stream);
     else if (kCache) launch::ws_merge(w, m.stream);  // ws-dense one-block rounds merge inside ws_gather
     if (kCache) miss_rows(m, w);
@@ -475,7 +479,8 @@ struct WsRounds : Base {
     launch::ws_solve(w, m.stream);
     if (w.blocks > 1) {
       launch::ws_select_pass(w, 1, m.stream);
-      ws_allgather_part(m);
+      if (w.xpeer) launch::ws_xcollect_part(w, m.stream);  // peer exchange: the partials pass 1 pushed
+      else ws_allgather_part(m);
       launch::ws_select_pass(w, 2, m.stream);
     } else {
       launch::ws_select(w, m.stream);

@@ -493,14 +493,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   int32_t ws_G = 0, ws_rpt = 0;
   if (ws_cand || wsc_cand) launch::ws_geometry(nl_max, m.world, &ws_G, &ws_rpt);
   // multi-block rounds (ws_blocks > 1): the union merge reads <= 256 candidate
-  // lists, an even q_max; at world > 1 over the collectives (their extra
-  // per-round all-gather of line-search partials has no peer-exchange form)
+  // lists, an even q_max.  At world > 1 they run over the in-kernel peer
+  // exchange (candidate lists, the P sub-Grams' owned entries and the
+  // line-search partials pushed into every rank's receive buffer: no collective
+  // per round) or, when that is unavailable, over the communicator's
+  // collectives (three per round; a device communicator, or exchange=allreduce)
   DPSVM_CHECK(m.p.ws_blocks >= 0 && m.p.ws_blocks <= kWsMaxBlocks,
               "ws_blocks must be 0 (auto) or 1.." + std::to_string(kWsMaxBlocks));
-  // host communicators stage every collective through host memory (three per
-  // round): there the one-block rounds over the in-kernel peer exchange are
-  // faster (2 processes on one GPU: 0.163 vs 0.198 s), so multi-block rounds at
-  // world > 1 need a device communicator (RCCL) or exchange=allreduce
   const bool multi_comm = m.world == 1 || m.comm->device_memory() || m.p.exchange == 1;
   // ws_blocks auto (0): every block from kWsAutoBlocksRows rows on (the round's
   // fixed cost is amortised over P sub-problems; small problems need few rounds)
@@ -520,30 +519,52 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // ws-cache takes them too when its cache holds the union's lines plus the
   // victim window (L >= 2 P q_max + 4096; agreed: L follows each device's free memory)
   const bool wsc_multi = wsc_fits_pre && launch::ws_cache_multi_supported(m.L, want_blocks, mb_q);
-  bool multi_ok = want_blocks > 1 && (ws_cand || wsc_multi) && mb_q % 2 == 0 &&
-                  (int64_t)ws_G * m.world <= kWsMaxGroups && m.p.exchange != 2 && multi_comm;
-  if (m.world > 1) multi_ok = m.all_agree(multi_ok, m.comm, m.world);
-  // Residency of the ws peer exchange: gather workgroup a of every rank spins
-  // until the same workgroup of every other rank has pushed its row, so with
-  // ranks sharing a device (rehearsals) the spinning gathers of the other
-  // ranks — (share - 1) x q_max workgroups, one per CU at worst — must leave a
-  // CU free for this rank's solve workgroup (q_max^2 floats of LDS), or the
-  // round deadlocks until the poll timeout.  On distinct devices share = 1.
-  // Refused (collectives instead) unless exchange=peer is explicit.
-  bool ws_xch_resident = true;
+  bool multi_elig = want_blocks > 1 && (ws_cand || wsc_multi) && mb_q % 2 == 0 &&
+                    (int64_t)ws_G * m.world <= kWsMaxGroups;
+  if (m.world > 1) multi_elig = m.all_agree(multi_elig, m.comm, m.world);
+  // Residency of the ws peer exchange with ranks sharing a device (rehearsals;
+  // on distinct devices share = 1).  One-block rounds: gather workgroup a of
+  // every rank spins until the same workgroup of every other rank has pushed its
+  // row, so the other ranks' spinning gathers — (share - 1) x q_max workgroups,
+  // one per CU at worst — must leave a CU free for this rank's solve workgroup.
+  // Multi-block rounds: no producer waits (selection and gather workgroups
+  // push); the spinning consumers of one rank are the two collect kernels (<= 16
+  // workgroups of 4 waves) and the solve (P workgroups of 16 waves), and the
+  // share ranks' solves plus one rank's full-size producer kernel (1024 waves)
+  // must fit the device's wave slots so every rank's producers still run.
+  bool ws_xch_resident = true, multi_xch_resident = true;
   if (m.world > 1) {
     const int share = max_device_sharing(m);  // collective
     int cus = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m.device));
     ws_xch_resident = m.all_agree((int64_t)(share - 1) * ws_q < (int64_t)cus, m.comm, m.world);
+    multi_xch_resident =
+        m.all_agree((int64_t)share * 16 * std::max(1, want_blocks) + 1024 <= (int64_t)cus * 32, m.comm, m.world);
     if (!ws_xch_resident && m.p.exchange != 2 && (ws_cand || wsc_fits_pre))
       m.info.engine_note = "ws peer exchange refused: " + std::to_string(share) + " ranks share a device (" +
                            std::to_string((share - 1) * ws_q) + " spinning gather workgroups >= " +
                            std::to_string(cus) + " CUs): collectives";
   }
-  const bool want_ws_xch = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives && !multi_ok &&
-                           (ws_xch_resident || m.p.exchange == 2) &&
-                           (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
+  const bool ws_peer_base = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives &&
+                            (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
+  // multi-block rounds over the peer exchange (partitioned X in cache mode sums
+  // the miss rows by an all-reduce: that engine keeps the collectives)
+  const int ks_mb = launch::ws_pass1_splits(ws_G);
+  bool multi_peer = false;
+  if (ws_peer_base && multi_elig && !(wsc_cand && !m.replicated) && (multi_xch_resident || m.p.exchange == 2)) {
+    const int64_t G_all = (int64_t)ws_G * m.world;
+    const bool ok = m.setup_exchange(ws_xch_words_multi(G_all, ks_mb, want_blocks, mb_q, ws_q));
+    DPSVM_CHECK(ok || m.p.exchange != 2,
+                "peer exchange requested (exchange=peer) but its self test failed (" + m.xch_diag + ")");
+    if (ok) {
+      m.xch = true;
+      multi_peer = true;
+    } else {
+      m.info.engine_note = "peer exchange refused: " + m.xch_diag + " (multi-block rounds use the collectives)";
+    }
+  }
+  const bool multi_ok = multi_elig && (multi_peer || (multi_comm && m.p.exchange != 2));
+  const bool want_ws_xch = ws_peer_base && !multi_ok && (ws_xch_resident || m.p.exchange == 2);
   if (want_ws_xch) {
     const bool ok = m.setup_exchange(ws_xch_words((int64_t)ws_G * m.world, ws_q));
     DPSVM_CHECK(ok || m.p.exchange != 2,
@@ -664,14 +685,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.blocks = 1;
     m.ws_q1 = ws_q;
     if (want_blocks > 1) {
-      if (multi_ok && !m.xch) {
+      if (multi_ok) {
         w.blocks = want_blocks;
         w.q_max = mb_q;
         w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * mb_q;
       }
       else if (m.p.ws_blocks > 1) m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") +
-                                 "ws_blocks > 1 needs an even ws_size, <= 256 candidate lists over the collectives "
-                                 "and (ws-cache) >= 2 P ws_size + 4096 lines: one block per round";
+                                 "ws_blocks > 1 needs an even ws_size, <= 256 candidate lists, the peer exchange or a "
+                                 "device communicator, and (ws-cache) >= 2 P ws_size + 4096 lines: one block per round";
     }
     // multi-block rounds replace the whole union each round by default (measured on the
     // headline at P = 8: 3/4 q new 0.0506 s, all new 0.0493 s; profiles/r2_ws_blocks_sweep.txt)
@@ -694,7 +715,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.subg = m.wssub;
     w.aux = m.wssub + (size_t)w.blocks * w.q_max * w.q_max;
     if (w.blocks > 1) {
-      w.ks = launch::ws_pass1_splits(w.G);
+      w.ks = ks_mb;
       m.wsdfs = dmalloc<float>((size_t)w.ks * m.nl, &m.bytes);
       m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
       m.wspart = dmalloc<double>((size_t)2 * w.G_all * w.ks, &m.bytes);
@@ -711,7 +732,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     if (m.xch) {
       w.xpeer = m.xpeer_d;
       w.xrank = m.rank;
-      w.xsub = 2 * (int64_t)w.G_all * 4 * kWsCand1;
+      if (w.blocks > 1) {  // ws_xch_words_multi: candidates (kWsCand keys a side), partials, sub-Gram rows
+        w.xcw = 4 * kWsCand;
+        w.xpart = ws_xch_cand_words_multi(w.G_all);
+        w.xsub = w.xpart + ws_xch_part_words(w.G_all, w.ks);
+        w.xsub_rows = (int64_t)w.blocks * w.q_max;  // the one-block view: its own q_max (gpu_engines.hip)
+      } else {  // ws_xch_words
+        w.xcw = 4 * kWsCand1;
+        w.xsub = 2 * (int64_t)w.G_all * 4 * kWsCand1;
+        w.xsub_rows = w.q_max;
+      }
       w.xtimeout_ticks = (int64_t)(std::max(1e-6, m.p.xch_timeout_s) * 1e8);
     }
     if (w.cache && !m.replicated) {

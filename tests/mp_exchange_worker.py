@@ -31,7 +31,8 @@ def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
            "exchange_mem": clf.setup_info_["exchange_mem"],
            "iters": int(clf.n_iter_), "rounds": int(getattr(clf, "n_rounds_", 0) or 0), "b": float(clf.b_),
-           "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest()}
+           "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest(),
+           "ws_blocks": int(clf.stats_.get("ws_blocks", 1) or 1), "engine_note": clf.setup_info_.get("engine_note", "")}
     with open(f"{out}.rank{ctx.rank}.json", "w") as f:
         json.dump(rec, f)
     del comm

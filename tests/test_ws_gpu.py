@@ -336,7 +336,8 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine, n):
         kw.update(force_cache=True, cache_lines=1500)
     if world > 2:
         kw.update(ws_size=64)
-    ref = _fit_threads(load(), world, X, y, **kw)
+    # host-staged collectives on the thread ranks (70k rows: multi-block rounds on both sides)
+    ref = _fit_threads(load(), world, X, y, exchange="allreduce", **kw)
     sha = hashlib.sha256(ref[0].alpha_.tobytes()).hexdigest()
     for k in range(world):
         assert res[k]["exchange"] == "peer" and res[k]["exchange_mem"] == "uncached"
@@ -346,6 +347,72 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine, n):
         assert res[k]["alpha_sha"] == sha
     if n > 6000:  # 2 x 137 selection workgroups: the merge folds two candidate lists per thread
         assert ref[0].setup_info_["groups"] * world > 256
+
+
+@pytest.mark.parametrize("clip", ["independent", "box"])
+@pytest.mark.parametrize("extra", [{}, {"force_cache": True, "cache_lines": 9000}])
+def test_ws_multi_block_peer_exchange_loopback_bit_identical(clip, extra):
+    """Multi-block rounds over the in-kernel peer exchange at world 1
+    (exchange="peer": loopback into the own receive buffer): the candidate
+    lists (ws_rank polls them), the P sub-Grams' entries and f (pushed by
+    ws_gather_multi, polled by ws_solve) and the line-search partials (pushed
+    by pass 1, polled by pass 2) — the same values as the direct path, so the
+    same trajectory bit for bit (coupled data: the adaptive count falls to one
+    block mid-run, so the one-block rounds of a multi-block engine's exchange
+    layout are covered too)."""
+    for case in ("mnist", "blobs"):
+        X, y = (synthetic("mnist", n=8000, seed=3) if case == "mnist"
+                else synthetic("blobs", n=6000, d=12, seed=41, sep=1.2))
+        kw = dict(C=10.0 if case == "mnist" else 2.0, gamma=0.25 if case == "mnist" else 0.15, eps=1e-3,
+                  clip=clip, device="cuda", solver="ws", ws_blocks=4, xch_timeout_s=30.0, **extra)
+        ref = SVC(**kw).fit(X, y)
+        got = SVC(exchange="peer", **kw).fit(X, y)
+        assert got.setup_info_["exchange"] == "loopback" and ref.setup_info_["exchange"] == "none"
+        assert got.stats_["ws_blocks"] == 4 and ref.stats_["ws_blocks"] == 4, got.setup_info_.get("engine_note")
+        assert got.setup_info_["iteration"] == ref.setup_info_["iteration"]
+        assert got.n_iter_ == ref.n_iter_ and got.n_rounds_ == ref.n_rounds_
+        assert np.array_equal(got.alpha_, ref.alpha_) and got.b_ == ref.b_
+        assert got.converged_
+
+
+@pytest.mark.parametrize("world,clip", [(2, "independent"), (2, "box"), (4, "box")])
+def test_ws_multi_block_peer_exchange_processes_one_gpu(tmp_path, world, clip):
+    """Sharded MULTI-BLOCK rounds with ranks as processes sharing the GPU (gloo
+    bootstrap, IPC-mapped uncached receive buffers): zero collectives per round
+    (candidates, sub-Gram entries and line-search partials pushed in-kernel),
+    bit-identical to the same rank count over host-staged collectives (thread
+    ranks, exchange=allreduce)."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from dpsvm_amd._native import load
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
+    out = tmp_path / f"wsm{world}"
+    port = 29720 + world + (5 if clip == "box" else 0)
+    knobs = {"ws_blocks": 4, "clip": clip}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), "ws", "6000", json.dumps(knobs)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    errs = "".join(open(f"{out}.rank{k}.err").read()[-1500:] for k in range(world)
+                   if os.path.exists(f"{out}.rank{k}.err"))
+    assert r.returncode == 0, errs + r.stderr[-2000:]
+    res = [json.load(open(f"{out}.rank{k}.json")) for k in range(world)]
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", solver="ws", dp="shard", ws_blocks=4, clip=clip)
+    ref = _fit_threads(load(), world, X, y, exchange="allreduce", **kw)
+    sha = hashlib.sha256(ref[0].alpha_.tobytes()).hexdigest()
+    assert ref[0].stats_["ws_blocks"] == 4
+    for k in range(world):
+        assert res[k]["exchange"] == "peer" and res[k]["ws_blocks"] == 4, res[k]
+        assert ref[k].setup_info_["exchange"] == "allreduce"
+        assert res[k]["iters"] == ref[0].n_iter_ and res[k]["rounds"] == ref[0].n_rounds_
+        assert res[k]["alpha_sha"] == sha
 
 
 @pytest.mark.parametrize("blocks", [2, 8])
