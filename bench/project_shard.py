@@ -81,6 +81,33 @@ def main() -> int:
             per_round = fixed + p1 + r["select_pass2"] / P + gaps + coll
             row.append(gram + rounds * per_round * 1e-6)
         print(f"{L:>6} {B:>7} | " + " | ".join(f"{v:.4f}  " for v in row))
+    px = m.get("peer_loopback")
+    if px:
+        # the default at world > 1: no collective per round.  MEASURED on one GPU:
+        # the exchange's kernel cost per round (loopback: pushes, two collect
+        # launches, the solve's polled loads).  ASSUMED: the extra latency of a
+        # store crossing xGMI before the consumer's poll sees it (three exchange
+        # points per round: candidates, sub-Gram rows, partials) and the link
+        # bandwidth for the pushed bytes (each rank sends its owned share of the
+        # P sub-Grams to every peer: ~ entries / P x (P - 1) x 8 B per link set)
+        ext = px["extra_us_per_round"]
+        sub_entries = blocks * q * q
+        print(f"PEER EXCHANGE (default): measured loopback cost {ext} us/round "
+              f"(same trajectory: {px['same_trajectory']}); ASSUMED xGMI store-to-poll latency X per exchange point "
+              f"(3 per round) and per-GPU injection bandwidth W for the pushed granules")
+        print(f"{'X us':>6} {'W GB/s':>7} | " + " | ".join(f"P={p:<2d} s" for p in (1, 2, 4, 8)))
+        for X, W in ((2, 300), (4, 150), (8, 64)):
+            row = []
+            for P in (1, 2, 4, 8):
+                if P == 1:
+                    row.append(m["local"]["s"])
+                    continue
+                sent = sub_entries / P * (P - 1) * 8  # bytes a rank pushes to its peers
+                xfer = 3 * X + sent / (W * 1e3)
+                p1 = probe.get(P, pass1 / P)
+                per_round = fixed + p1 + r["select_pass2"] / P + gaps + max(0.0, ext) + xfer
+                row.append(m["gram_slab_s"][str(P)] + rounds * per_round * 1e-6)
+            print(f"{X:>6} {W:>7} | " + " | ".join(f"{v:.4f}  " for v in row))
     return 0
 
 

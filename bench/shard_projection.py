@@ -68,6 +68,15 @@ def main() -> int:
                             "same_trajectory": bool(rc.n_iter_ == loc.n_iter_ and np.array_equal(rc.alpha_, loc.alpha_)),
                             "extra_us_per_round": round(1e6 * (t_rc - t_loc) / max(1, rc.n_rounds_), 2)}
     del comm
+    # the multi-block rounds over the in-kernel peer exchange at world 1
+    # (loopback: every push lands in the own receive buffer, the collect kernels
+    # and the solve poll it): the exchange's per-round kernel cost without xGMI
+    t_px, px = best(lambda: SVC(exchange="peer", xch_timeout_s=60.0, **kw).fit(X, y))
+    out["peer_loopback"] = {"s": round(t_px, 6), "rounds": px.n_rounds_, "steps": px.n_iter_,
+                            "exchange": px.setup_info_.get("exchange"),
+                            "blocks": int(px.stats_.get("ws_blocks", 1)),
+                            "same_trajectory": bool(px.n_iter_ == loc.n_iter_ and np.array_equal(px.alpha_, loc.alpha_)),
+                            "extra_us_per_round": round(1e6 * (t_px - t_loc) / max(1, px.n_rounds_), 2)}
 
     # one rank's Gram slab: K(all rows, n / P columns), non-symmetric GEMM
     xt = torch.tensor(X, device="cuda")

@@ -8,13 +8,17 @@
 // is the same order as the MFMA work it feeds.  A 256 x 128 tile moves 48 KiB
 // (48 pieces) for 192 MFMAs — half the DMA issue and half the L2 operand
 // traffic per MFMA.  Each of the 8 waves owns 64 x 64 outputs (2 x 2 MFMA
-// 32x32 tiles, three accumulators H / P / Q each: 192 accumulator registers,
-// two waves per SIMD).
+// 32x32 tiles, two accumulators each: 128 accumulator registers, two waves per
+// SIMD).
 //
-// Numerics: every output element is the same MFMA k-sequence (H, P, Q over the
-// k blocks in order) and the same epilogue as every split kernel, so the Gram
-// is bit-identical to rbf_gemm_split_glds_persist_kernel's (test:
-// test_split_gram_wide_bit_identical).
+// Numerics: H = sum h_a h_b as in every split kernel; the cross terms go to ONE
+// accumulator PQ, one MFMA per 8-wide k chunk with A' = [h_a | l_a] and
+// B' = [l_b | h_b] in the two K halves (h_a l_b + l_a h_b in one fp32 sum).
+// Swapping the operands swaps the two K halves of every such MFMA; the Gram's
+// bit symmetry K(i, j) == K(j, i) then rests on the MFMA's sum being invariant
+// under that swap, which bench/mfma_swap_probe.hip checks on the hardware.
+// The values differ from the three-accumulator kernels' by rounding only
+// (same products, fp32 sums).
 //
 // Symmetric mode on 256-row tiles: tile (tx, ty) covers the 128-row blocks
 // 2tx and 2tx + 1 of the rows and column block ty; it runs when ty >= 2tx.  A
@@ -76,9 +80,9 @@ __device__ __forceinline__ void quad_transpose4(float (&v)[4], int i) {
 }
 
 __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
-    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
-    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
-    float gamma, float* __restrict__ out, int64_t ldo, int sym, int tm, int tn) {
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int N, int nkb,
+    float gamma, float* __restrict__ out, int ldo, int sym, int tm, int tn) {
   constexpr int TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
   __shared__ u4 lds[NB * BUF + 4 * ROWS / 4];  // 3 operand buffers (144 KiB), then per tile parity |x|^2, shifts
   float* s_sq0 = (float*)(lds + NB * BUF);
@@ -96,7 +100,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5, qi = lane & 3;
   const int64_t rstride = (int64_t)nkb * 8;
-  int64_t m0 = (int64_t)tx * TM, n0 = (int64_t)ty * TN;
+  int m0 = tx * TM, n0 = ty * TN;
 
   // DMA geometry: wave w fills A rows 32 w + 8 i + (lane >> 3) (i = 0..3) and B
   // rows 16 w + 8 i + (lane >> 3) (i = 0..1); lane position p = lane & 7 takes
@@ -115,9 +119,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
   }
   const u4* srca;
   const u4* srcb;
-  auto set_src = [&](int64_t a0, int64_t b0) {
-    srca = A + (a0 + 32 * wave + l3) * rstride;
-    srcb = B + (b0 + 16 * wave + l3) * rstride;
+  auto set_src = [&](int a0, int b0) {
+    srca = A + (int64_t)(a0 + 32 * wave + l3) * rstride;
+    srcb = B + (int64_t)(b0 + 16 * wave + l3) * rstride;
   };
   auto dma = [&](int kb, int buf) {
     u4* dst = lds + buf * BUF;
@@ -132,9 +136,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
           (const void*)(srcb + (int64_t)(8 * i) * rstride + (int64_t)kb * 8 + bch[i]),
           (__attribute__((address_space(3))) void*)(dst + (TM + 16 * wave + 8 * i) * CPR), 16, 0, 0);
   };
-  auto row_data = [&](int64_t a0, int64_t b0, float& q, int32_t& h) {
+  auto row_data = [&](int a0, int b0, float& q, int32_t& h) {
     if (tid < ROWS) {
-      const int64_t ri = tid < TM ? min(a0 + tid, M - 1) : min(b0 + (tid - TM), N - 1);
+      const int ri = tid < TM ? min(a0 + tid, M - 1) : min(b0 + (tid - TM), N - 1);
       q = tid < TM ? Asq[ri] : Bsq[ri];
       h = tid < TM ? Ash[ri] : Bsh[ri];
     }
@@ -153,9 +157,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
   dma(0, 0);
   if (nkb > 1) dma(1, 1);
 
-  const int sw = ((lane & 31) >> 1) & 7;
-  const int ra0 = (wm * 64 + (lane & 31)) * CPR, ra1 = ra0 + 32 * CPR;
-  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
   int par = 0;
   int pend = 0;  // store instructions each lane issued after the current tile's first two DMAs (0, 16 or 32)
   f16v H[2][2], PQ[2][2];
@@ -184,6 +185,13 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
       asm volatile("" ::: "memory");
       if (kb + 2 < nkb) dma(kb + 2, cb == 0 ? 2 : cb - 1);  // the buffer of block kb - 1: every wave is past it
       const u4* buf = lds + cb * BUF;
+      // operand offsets recomputed per block from an opaque lane id (kept live
+      // across the loop they cost ~40 registers)
+      int klane = lane;
+      asm volatile("" : "+v"(klane));
+      const int sw = ((klane & 31) >> 1) & 7, hl = klane >> 5;
+      const int ra0 = (wm * 64 + (klane & 31)) * CPR, ra1 = ra0 + 32 * CPR;
+      const int rb0 = (TM + wn * 64 + (klane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
       // H: k16 steps, lane half hl supplies h chunk 2 ks + hl (k slots 8 hl ..)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -213,22 +221,28 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
     int nL = L + G, ntx = tx, nty = ty;
     while (nL < total && !valid(nL, ntx, nty)) nL += G;
     const bool has_next = nL < total;
-    const int64_t nm0 = (int64_t)ntx * TM, nn0 = (int64_t)nty * TN;
+    const int nm0 = ntx * TM, nn0 = nty * TN;
     float nq = 0.f;
     int32_t nh = 0;
     if (has_next) row_data(nm0, nn0, nq, nh);
     const float* s_sq = s_sq0 + par * ROWS;
     const int32_t* s_sh = s_sh0 + par * ROWS;
+    // the epilogue's lane-dependent offsets are recomputed per tile (an opaque
+    // copy of the lane id): hoisted out of the tile loop they would stay live
+    // across the k loop and push it past 256 registers
+    int elane = lane;
+    asm volatile("" : "+v"(elane));
+    const int ehl = elane >> 5, eqi = elane & 3;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const int cbr = TM + wn * 64 + 32 * b + (lane & 31);
+      const int cbr = TM + wn * 64 + 32 * b + (elane & 31);
       const float bsq = s_sq[cbr];
       const int bsh = s_sh[cbr];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int lr = wm * 64 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const int lr = wm * 64 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * ehl;
           const float dot = ldexpf(H[a][b][r] + PQ[a][b][r], -(s_sh[lr] + bsh));
           H[a][b][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
         }
@@ -249,7 +263,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
     // this wave's 128-row block and what it stores
     const int rblk = 2 * tx + (wm >> 1);
     const bool direct = !sym || ty >= rblk, mirror = sym && ty > rblk;
-    const int64_t wr0 = m0 + wm * 64, wc0 = n0 + wn * 64;  // the wave's 64 x 64 outputs
+    const int wr0 = m0 + wm * 64, wc0 = n0 + wn * 64;  // the wave's 64 x 64 outputs
     const bool interior = wr0 + 64 <= M && wc0 + 64 <= N && nkb >= 3;
     if (interior) {
       if (mirror) {  // transposed: a lane's 4 consecutive rows -> 16 B of out[col][row ..]
@@ -257,7 +271,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
         for (int a = 0; a < 2; ++a)
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
-            const int64_t col = wc0 + 32 * b + (lane & 31);
+            const int col = wc0 + 32 * b + (elane & 31);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               f4 v;
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
               v.y = H[a][b][4 * g + 1];
               v.z = H[a][b][4 * g + 2];
               v.w = H[a][b][4 * g + 3];
-              *(f4*)(out + col * ldo + wr0 + 32 * a + 8 * g + 4 * hl) = v;
+              *(f4*)(out + (int64_t)col * ldo + wr0 + 32 * a + 8 * g + 4 * ehl) = v;
             }
           }
       }
@@ -277,15 +291,15 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               float v[4] = {H[a][b][4 * g + 0], H[a][b][4 * g + 1], H[a][b][4 * g + 2], H[a][b][4 * g + 3]};
-              quad_transpose4(v, qi);
-              const int64_t row = wr0 + 32 * a + 8 * g + 4 * hl + qi;
-              const int64_t col = wc0 + 32 * b + ((lane & 31) & ~3);
+              quad_transpose4(v, eqi);
+              const int row = wr0 + 32 * a + 8 * g + 4 * ehl + eqi;
+              const int col = wc0 + 32 * b + ((elane & 31) & ~3);
               f4 o;
               o.x = v[0];
               o.y = v[1];
               o.z = v[2];
               o.w = v[3];
-              *(f4*)(out + row * ldo + col) = o;
+              *(f4*)(out + (int64_t)row * ldo + col) = o;
             }
       }
       pend = (direct ? 16 : 0) + (mirror ? 16 : 0);
@@ -295,10 +309,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
         for (int a = 0; a < 2; ++a)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int64_t row = wr0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            const int row = wr0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * ehl;
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
-              const int64_t col = wc0 + 32 * b + (lane & 31);
+              const int col = wc0 + 32 * b + (elane & 31);
               if (row < M && col < N) out[row * ldo + col] = H[a][b][r];
             }
           }
@@ -308,14 +322,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void rbf_gram_wide_kernel(
         for (int a = 0; a < 2; ++a)
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
-            const int64_t col = wc0 + 32 * b + (lane & 31);
+            const int col = wc0 + 32 * b + (elane & 31);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              const int64_t row = wr0 + 32 * a + 8 * g + 4 * hl;
+              const int row = wr0 + 32 * a + 8 * g + 4 * ehl;
               if (col < M) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                  if (row + c < N) out[col * ldo + row + c] = H[a][b][4 * g + c];
+                  if (row + c < N) out[(int64_t)col * ldo + row + c] = H[a][b][4 * g + c];
               }
             }
           }
@@ -357,8 +371,8 @@ void rbf_gram_wide(const void* A, const int32_t* Ash, const float* Asq, int64_t 
   const int64_t tiles = symmetric ? tm * tn / 2 + tm : tm * tn;  // an upper bound of the valid tiles
   const int grid = (int)std::min<int64_t>(cus8, (tiles + 7) / 8 * 8);
   dev::rbf_gram_wide_kernel<<<dim3((unsigned)grid), dev::kWideThreads, 0, s>>>(
-      (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
-      symmetric ? 1 : 0, (int)tm, (int)tn);
+      (const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B, Bsh, Bsq, (int)N, (dp + 31) / 32, gamma, out,
+      (int)ldo, symmetric ? 1 : 0, (int)tm, (int)tn);
   post_launch("rbf_gram_wide", s);
 }
 
