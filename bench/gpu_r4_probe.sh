@@ -1,9 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-hipcc --offload-arch=gfx950 -O3 bench/mfma_swap_probe.hip -o /tmp/mfma_swap_probe 2>/dev/null &&
-timeout -k 5 60 /tmp/mfma_swap_probe 4096 49 0 > gpurun_out/r4_mfma_swap_probe.txt &&
-timeout -k 5 60 /tmp/mfma_swap_probe 4096 1 0 >> gpurun_out/r4_mfma_swap_probe.txt &&
-timeout -k 5 60 /tmp/mfma_swap_probe 4096 49 1 >> gpurun_out/r4_mfma_swap_probe.txt &&
+
+timeout -k 5 60 bin/mfma_swap_probe 4096 49 0 > gpurun_out/r4_mfma_swap_probe.txt &&
+timeout -k 5 60 bin/mfma_swap_probe 4096 1 0 >> gpurun_out/r4_mfma_swap_probe.txt &&
+timeout -k 5 60 bin/mfma_swap_probe 4096 49 1 >> gpurun_out/r4_mfma_swap_probe.txt &&
 cat gpurun_out/r4_mfma_swap_probe.txt &&
 DPSVM_SPLIT_GEMM=4 timeout -k 10 120 python3 bench/gram_ab.py --only split > gpurun_out/r4_gram_v4.txt 2>&1 &&
 DPSVM_SPLIT_GEMM=5 timeout -k 10 120 python3 bench/gram_ab.py --only split > gpurun_out/r4_gram_v5.txt 2>&1 &&

@@ -49,7 +49,6 @@ LIB_SOURCES = [
     "kernels/smo_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/rbf_gemm_split.hip",
-    "kernels/rbf_gram_wide.hip",
     "kernels/smo_fused.hip",
     "kernels/microbench.hip",
     "kernels/compact.hip",

@@ -118,14 +118,9 @@ int64_t split_row_u4(int dp);
 int64_t split_pad_rows(int64_t rows);
 void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, int32_t* shift, hipStream_t s);
 // split STORE GEMM variant: 0 auto (4 when dp > 128, else 3), 1 register-staged tile per workgroup, 3 LDS-DMA,
-// 4 persistent LDS-DMA, 5 persistent 256 x 128 tiles (rbf_gram_wide.hip)
+// 4 persistent LDS-DMA
 int split_gemm_variant();
 void set_split_gemm_variant(int v);
-// 256 x 128-tile persistent split Gram GEMM (rbf_gram_wide.hip): the same values bit for bit
-bool rbf_gram_wide_supported(int64_t M, int64_t N, int dp, int64_t ldo);
-void rbf_gram_wide(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B, const int32_t* Bsh,
-                   const float* Bsq, int64_t N, int dp, float gamma, float* out, int64_t ldo, hipStream_t s,
-                   bool symmetric);
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
                           int64_t ldo, hipStream_t s, bool symmetric = false);

@@ -906,10 +906,6 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     return e && atoi(e) == 1 ? 1 : 2;
   }();
   const int variant = split_gemm_variant();
-  if (variant == 5 && ablate == 0 && rbf_gram_wide_supported(M, N, dp, ldo)) {
-    rbf_gram_wide(A, Ash, Asq, M, B, Bsh, Bsq, N, dp, gamma, out, ldo, s, symmetric);
-    return;
-  }
   if ((variant == 0 || variant == 4) && ablate == 0 && (dp + 31) / 32 >= 5 && tm * tn < (1ll << 31)) {
     // default: persistent LDS-DMA, one workgroup per CU (a multiple of 8)
     static const int cus4 = [] {

@@ -1,5 +1,5 @@
 // Device helpers shared by the split-operand fp16 MFMA GEMMs
-// (rbf_gemm_split.hip, rbf_gram_wide.hip): operand vector types, the
+// (rbf_gemm_split.hip): operand vector types, the
 // 32x32x16 f16 MFMA and the XCD-aware persistent tile order.
 #pragma once
 
