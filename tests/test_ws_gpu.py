@@ -350,7 +350,7 @@ def test_ws_peer_exchange_processes_one_gpu(tmp_path, world, engine, n):
 
 
 @pytest.mark.parametrize("clip", ["independent", "box"])
-@pytest.mark.parametrize("extra", [{}, {"force_cache": True, "cache_lines": 9000}])
+@pytest.mark.parametrize("extra", [{}, {"force_cache": True, "cache_lines": 11000}])
 def test_ws_multi_block_peer_exchange_loopback_bit_identical(clip, extra):
     """Multi-block rounds over the in-kernel peer exchange at world 1
     (exchange="peer": loopback into the own receive buffer): the candidate
@@ -360,9 +360,11 @@ def test_ws_multi_block_peer_exchange_loopback_bit_identical(clip, extra):
     same trajectory bit for bit (coupled data: the adaptive count falls to one
     block mid-run, so the one-block rounds of a multi-block engine's exchange
     layout are covered too)."""
+    # (ws-cache multi-block rounds need L >= 2 P q + 8192 lines: 12,000 rows, 11,000 lines)
+    n = 12000 if extra else 8000
     for case in ("mnist", "blobs"):
-        X, y = (synthetic("mnist", n=8000, seed=3) if case == "mnist"
-                else synthetic("blobs", n=6000, d=12, seed=41, sep=1.2))
+        X, y = (synthetic("mnist", n=n, seed=3) if case == "mnist"
+                else synthetic("blobs", n=n, d=12, seed=41, sep=1.2))
         kw = dict(C=10.0 if case == "mnist" else 2.0, gamma=0.25 if case == "mnist" else 0.15, eps=1e-3,
                   clip=clip, device="cuda", solver="ws", ws_blocks=4, xch_timeout_s=30.0, **extra)
         ref = SVC(**kw).fit(X, y)
