@@ -32,6 +32,7 @@ def main() -> int:
     ap.add_argument("--max-iter", type=int, default=10**7)
     ap.add_argument("--cache-lines", type=int, default=0)
     ap.add_argument("--force-cache", action="store_true")
+    ap.add_argument("--exchange", default="auto", help="peer: the in-kernel exchange at world 1 (loopback)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "ws_stamps")
@@ -41,7 +42,8 @@ def main() -> int:
 
     X, y = synthetic(a.data, n=a.samples, d=a.features)
     clf = SVC(C=a.C, gamma=a.gamma, eps=1e-3, device="cuda", solver="ws", ws_size=a.ws_size, ws_new=a.ws_new,
-              ws_rel=a.ws_rel, ws_blocks=a.ws_blocks, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache).fit(X, y)
+              ws_rel=a.ws_rel, ws_blocks=a.ws_blocks, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache,
+              exchange=a.exchange, xch_timeout_s=60.0).fit(X, y)
     raw = np.fromfile(path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
     rounds = min(clf.n_rounds_, 4096)
     s = raw[2:rounds]
@@ -75,6 +77,17 @@ def main() -> int:
         "solve_end_to_next_select_us": us(nxt - s[:, 4]),
         "round_period_us": us(np.diff(s[:, 6])),
     }
+    if (s[:, 15] > 0).all():  # multi-block peer exchange: the two collect kernels (workgroup 0)
+        res["exchange"] = clf.setup_info_.get("exchange")
+        res["peer_phases_us"] = {
+            "pass2_end_to_collect_cand": us(s[:, 15] - s[:, 7]),
+            "collect_cand_wg0": us(s[:, 16] - s[:, 15]),
+            "collect_cand_to_rank": us(s[:, 21] - s[:, 16]),
+            "pass1_wg0": us(s[:, 23] - s[:, 22]),
+            "pass1_to_collect_part": us(s[:, 17] - s[:, 23]),
+            "collect_part_wg0": us(s[:, 19] - s[:, 17]),
+            "collect_part_to_pass2": us(s[:, 6] - s[:, 19]),
+        }
     if (s[:, 18] > 0).any():  # experimental per-phase core-clock cycle sums (s_memtime)
         st = np.maximum(1, s[:, 5])
         res["cycles_per_step"] = {k: float(np.median(s[:, 12 + i] / st)) for i, k in enumerate(

@@ -547,6 +547,7 @@ constexpr int kXCollectThreads = 256;
 __global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsArgs a) {
   WsCtrl* c = a.ctrl;
   if (c->done != kRunning) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(15);
   const int e = (int)(blockIdx.x * kXCollectThreads + threadIdx.x);  // (list, side, rank) key
   bool ok = true;
   if (e < a.G_all * 2 * kWsCand) {
@@ -557,6 +558,7 @@ __global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsAr
     a.cand[e] = ok ? ws_get64(g[0], g[1]) : kKeyNone;
   }
   if (!ok) ws_comm_fail_thread(a, c);
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(16);
 }
 
 // ws_rank: the multi-block merge's sort, spread over a grid of 2 sides x

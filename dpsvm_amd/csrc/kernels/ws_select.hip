@@ -328,6 +328,7 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
 __global__ __launch_bounds__(256) void ws_xcollect_part_kernel(WsArgs a) {
   WsCtrl* c = a.ctrl;
   if (c->n_apply == 0) return;  // pass 1 pushed nothing (or the run ended: n_apply = 0)
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(17);
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= (int64_t)a.G_all * max(1, a.ks)) return;
   const int64_t R = c->outer;  // committed by this round's solve, as pass 1 tagged it
@@ -338,6 +339,7 @@ __global__ __launch_bounds__(256) void ws_xcollect_part_kernel(WsArgs a) {
   } else {
     ws_comm_fail_thread(a, c);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(19);
 }
 
 }  // namespace dev

@@ -169,25 +169,48 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     // peer exchange: block blk's rows a < q from this rank's receive buffer,
     // entries (a, b < q) and f (last column) pushed by their owners
     // (ws_gather_multi); columns q .. q_max - 1 are zeros
+    // A thread's granules are loaded in batches of kB (all in flight: one
+    // latency of the uncached buffer per batch), then only the ones not yet
+    // tagged are re-polled — a per-entry poll loop paid one round trip each.
     const int64_t R = c->outer;
     const uint64_t t = xtag((uint32_t)R + 1u);
-    const uint64_t* mine = a.xpeer[a.xrank];
-    const int w = ldk + 1;
-    for (int e = tid; e < q * w; e += kWsSolveThreads) {
-      const int ra = e / w, col = e - ra * w;
-      if (col < ldk && col >= q) {
-        K[ra * ldk + col] = 0.f;
-        continue;
+    const uint64_t* rows = a.xpeer[a.xrank] + ws_xrow(a, par, ib);  // row ra at + ra * (ldk + 1)
+    const int w = ldk + 1, n_e = q * w;
+    constexpr int kB = 16;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int e0 = 0; e0 < n_e && xok; e0 += kB * kWsSolveThreads) {
+      uint64_t v[kB];
+      uint32_t need = 0;  // bit k: entry e0 + tid + k * threads still to land
+#pragma unroll
+      for (int k = 0; k < kB; ++k) {
+        const int e = e0 + tid + k * kWsSolveThreads;
+        const int col = e - (e / w) * w;
+        const bool want = e < n_e && (col < q || col == ldk);
+        v[k] = want ? xch_load<true>(rows + e) : t;
+        need |= want ? 1u << k : 0u;
       }
-      if (col > ldk) continue;
-      uint64_t v[1];
-      if (!xok || !ws_poll<1>(a, mine + ws_xrow(a, par, ib + ra) + col, t, v)) {
-        xok = false;
-        continue;
+      while (true) {
+#pragma unroll
+        for (int k = 0; k < kB; ++k)
+          if (((need >> k) & 1u) && ws_tag_ok(v[k], t)) need &= ~(1u << k);
+        if (need == 0) break;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
+          xok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < kB; ++k)
+          if ((need >> k) & 1u) v[k] = xch_load<true>(rows + e0 + tid + k * kWsSolveThreads);
       }
-      const float fv = __uint_as_float((uint32_t)v[0]);
-      if (col < ldk) K[ra * ldk + col] = fv;
-      else s_f[ra] = fv;
+#pragma unroll
+      for (int k = 0; k < kB; ++k) {
+        const int e = e0 + tid + k * kWsSolveThreads;
+        if (e >= n_e) break;
+        const int ra = e / w, col = e - ra * w;
+        if (col < ldk) K[ra * ldk + col] = col < q ? __uint_as_float((uint32_t)v[k]) : 0.f;
+        else s_f[ra] = __uint_as_float((uint32_t)v[k]);
+      }
     }
     if (tid < q) {
       s_a[tid] = aux[a.aux_stride + tid];
