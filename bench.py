@@ -46,6 +46,9 @@ PRESETS = {
     "adult": dict(data="adult", samples=32561, features=123, C=100.0, gamma=0.5, eps=1e-3, max_iter=150000),
     "covtype": dict(data="covtype", samples=581012, features=54, C=2048.0, gamma=0.03125, eps=1e-3,
                     max_iter=3000000),
+    # Makefile:77 (run_cover): the first 500,000 covtype rows
+    "covtype-ref": dict(data="covtype", samples=500000, features=54, C=2048.0, gamma=0.03125, eps=1e-3,
+                        max_iter=3000000),
     "synthetic-2m": dict(data="uniform", samples=2000000, features=1024, C=1.0, gamma=1.0 / 1024, eps=1e-3,
                          max_iter=3000000),
 }
@@ -104,8 +107,9 @@ def parse(argv=None):
     ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
     ap.add_argument("--ws-block", type=int, default=32)
     ap.add_argument("--ws-t-halve", type=float, default=None, help="multi-block: damped rounds below this t halve P")
-    ap.add_argument("--shrink", action="store_true",
-                    help="one GPU: LIBSVM-style shrinking as problem reduction (phases on the active rows)")
+    ap.add_argument("--shrink", default="auto", choices=["auto", "on", "off"],
+                    help="one GPU: LIBSVM-style shrinking as problem reduction (phases on the active rows); "
+                         "auto (the library's default): on when the whole Gram is not resident (C.shrink_auto)")
     ap.add_argument("--ws-no-clip-fallback", action="store_true",
                     help="multi-block, independent clipping: keep the blocks after a clip event")
     ap.add_argument("--ws-wss", type=int, default=None, choices=[0, 1, 2],
@@ -280,10 +284,12 @@ def main(argv=None) -> int:
         print(f"[bench] iter {it} b_hi {bh:.6g} b_lo {bl:.6g} gap {bl - bh:.3g} {el:.1f} s "
               f"hits {hits} misses {misses}", file=sys.stderr, flush=True)
 
-    if on_gpu and a.shrink:
+    if on_gpu and a.shrink == "on" and n_ranks > 1:
+        raise SystemExit("--shrink on runs on one GPU")
+    use_shrink = on_gpu and n_ranks == 1 and (
+        a.shrink == "on" or (a.shrink == "auto" and C.shrink_auto(params, X.shape[0], X.shape[1], ctx.local_rank)))
+    if use_shrink:
         # shrinking phases (one GPU): every phase sets its solver up inside the timed run
-        if n_ranks > 1:
-            raise SystemExit("--shrink runs on one GPU")
         solver = None
         info = {"device_name": C.device_name(ctx.local_rank), "x_replicated": True, "iteration": "ws+shrinking"}
         run = lambda: C.solve_shrinking(X, y, params, ctx.local_rank, None,  # noqa: E731
@@ -480,6 +486,7 @@ def main(argv=None) -> int:
             "poll_batch": info.get("poll_batch", 0),
             "census": info.get("census", "n/a"),
             "engine_note": info.get("engine_note", ""),
+            "shrink": {"mode": a.shrink, "on": bool(use_shrink), "phases": int(res.get("shrink_phases", 0))},
             "shard_check": shard_check,
             "dp_autotune": dp_choice,
             "reference_check": ref_check,

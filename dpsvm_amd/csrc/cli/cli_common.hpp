@@ -41,7 +41,7 @@ struct Options {
   bool legacy_model = false;  // write/read the seq format (no b line)
   bool quiet = false;
   bool skip_accuracy = false;
-  bool shrink = false;        // one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking)
+  int shrink = 0;             // one GPU, shrinking phases (solve_shrinking): 0 auto (shrink_auto), 1 off, 2 on
 };
 
 inline void usage_train(const char* prog, bool seq) {
@@ -90,7 +90,8 @@ inline void usage_train(const char* prog, bool seq) {
                "   --ws-blocks P       :  up to P sub-problems per round on P workgroups (1..32, P x ws-size <= 3072;\n"
                "                          default 0 = auto:\n"
                "                          32 blocks of 96 rows from 50k rows, halved after every damped round)\n"
-               "   --shrink            :  one GPU: LIBSVM-style shrinking (phases on the rows that can still violate)\n"
+               "   --shrink[=auto|on|off] :  one GPU: LIBSVM-style shrinking (phases on the rows that can still\n"
+               "                         violate; auto, the default: on when the whole Gram is not resident)\n"
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --gram auto|f32|split :  Gram / kernel-row GEMMs: f32-input MFMA, or fp16 MFMA over hi/lo split\n"
                "                          operands (fp32 accuracy); auto = split for the ws engines\n"
@@ -146,7 +147,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {"ws-wss", required_argument, 0, OPT_WSWSS}, {"gram", required_argument, 0, OPT_GRAM},
-      {"shrink", no_argument, 0, OPT_SHRINK},
+      {"shrink", optional_argument, 0, OPT_SHRINK},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -193,7 +194,12 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       case OPT_LEGG: o.legacy_gamma = true; break;
       case OPT_QUIET: o.quiet = true; break;
       case OPT_SKIPACC: o.skip_accuracy = true; break;
-      case OPT_SHRINK: o.shrink = true; break;
+      case OPT_SHRINK: {
+        const std::string v = optarg ? optarg : "on";
+        if (v != "auto" && v != "off" && v != "on") usage_train(argv[0], seq);
+        o.shrink = v == "on" ? 2 : v == "off" ? 1 : 0;
+        break;
+      }
       case OPT_VERBOSE: o.p.verbose = true; break;
       case OPT_PERSIST: {
         const std::string v = optarg;

@@ -80,10 +80,10 @@ int main(int argc, char** argv) {
           return;
         }
         const int dev = (o.ranks > 0 || world == 1) ? o.device : r;
-        if (o.shrink) {
+        if (o.shrink == 2 && world > 1) fail("--shrink runs on one GPU");
+        if (world == 1 && (o.shrink == 2 || (o.shrink == 0 && shrink_auto(o.p, n, d, dev)))) {
           // one GPU: shrinking phases, each a device solver on the active rows
           // (solver/gpu_shrink.cpp); training accuracy by the GPU predictor
-          if (world > 1) fail("--shrink runs on one GPU");
           std::cout << "SETUP DONE\n";
           extras.engine = "ws+shrinking";
           results[r] = solve_shrinking(o.p, dev, ds.x.data(), n, d, ds.y.data(), resume.get(), prog);

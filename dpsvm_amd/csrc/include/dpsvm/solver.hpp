@@ -112,6 +112,13 @@ class GpuSolver {
 SolveResult solve_shrinking(const SolverParams& p, int device, const float* x, int64_t n, int d, const float* y,
                             const Checkpoint* resume = nullptr, const ProgressFn& progress = {});
 
+// shrink="auto" (library, svmTrain and bench default): shrinking phases where
+// they pay — one GPU, working-set rounds, and a Gram that does not fit the
+// device's cache budget (the ws-cache regime: covtype-shape 581k x 54).  On a
+// resident Gram (the headline) a phase only adds setup work; measured in
+// profiles/r4_shrink_auto_*.txt.
+bool shrink_auto(const SolverParams& p, int64_t n, int d, int device);
+
 // Stand-alone GPU predictor (svmTest GPU path): model SVs resident on device,
 // decision values of a host or device matrix via the MFMA predict kernel.
 class GpuPredictor {

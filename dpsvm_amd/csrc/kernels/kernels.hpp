@@ -136,6 +136,8 @@ int64_t predict_scratch_floats(int64_t M, int64_t N);
 void rbf_predict_split(const float* A, const float* Asq, int64_t M, int lda, const float* B, const float* Bsq,
                        const float* coef, int64_t N, int ldb, int dp, float gamma, float* partial, int64_t ldp,
                        int max_splits, hipStream_t s);
+// which decision GEMM rbf_predict runs for this dp: the split-operand one (dp >= 128) or the f32 one
+bool predict_uses_split(int dp);
 void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                  const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
                  float b, float* partial, float* dec, const float* y, int32_t* correct,

@@ -357,6 +357,14 @@ int64_t predict_scratch_floats(int64_t M, int64_t N) {
   return (int64_t)predict_splits(M, std::max<int64_t>(N, 1)) * round_up(std::max<int64_t>(M, 1), dev::BM);
 }
 
+bool predict_uses_split(int dp) {
+  static const bool f32_only = [] {
+    const char* e = std::getenv("DPSVM_PREDICT");  // A/B: f32 = the f32-input MFMA decision GEMM
+    return e && std::string(e) == "f32";
+  }();
+  return !f32_only && dp >= 128;
+}
+
 void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                  const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
                  float b, float* partial, float* dec, const float* y, int32_t* correct,
@@ -370,11 +378,7 @@ void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const flo
     splits = predict_splits(M, N);
     const int per = (int)((tn + splits - 1) / splits);
     splits = (int)((tn + per - 1) / per);
-    static const bool f32_only = [] {
-      const char* e = std::getenv("DPSVM_PREDICT");  // A/B: f32 = the f32-input MFMA decision GEMM
-      return e && std::string(e) == "f32";
-    }();
-    if (!f32_only && dp >= 128) {
+    if (predict_uses_split(dp)) {
       // split-operand fp16 MFMA with LDS-DMA staging (fp32 accuracy, rbf_gemm_split.hip)
       rbf_predict_split(A, Asq, M, lda, B, Bsq, coef, N, ldb, dp, gamma, partial, ldp, splits, s);
     } else {

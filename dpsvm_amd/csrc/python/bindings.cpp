@@ -368,6 +368,9 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(to_np(r.alpha), result_dict(r));
   }, py::arg("x"), py::arg("y"), py::arg("params"), py::arg("device") = 0, py::arg("resume") = nullptr,
      py::arg("progress") = py::none());
+  m.def("shrink_auto", [](const SolverParams& p, int64_t n, int d, int device) { return shrink_auto(p, n, d, device); },
+        py::arg("params"), py::arg("n"), py::arg("d"), py::arg("device") = 0,
+        "shrink='auto': shrinking phases where they pay (one GPU, working-set rounds, Gram not resident)");
 
   py::class_<GpuSolver, std::shared_ptr<GpuSolver>>(m, "GpuSolver")
       .def(py::init([](const SolverParams& p, std::shared_ptr<Communicator> comm, int device) {

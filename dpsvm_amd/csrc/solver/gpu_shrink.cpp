@@ -28,8 +28,12 @@
 #include <cmath>
 #include <cstdio>
 
+#include <hip/hip_runtime.h>
+
 #include "dpsvm/device_state.hpp"
 #include "dpsvm/solver.hpp"
+#include "../kernels/kernels.hpp"
+#include "../runtime/hip_check.hpp"
 
 namespace dpsvm {
 
@@ -87,10 +91,13 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   p.checkpoint_every = 0;  // the phases' own solvers do not checkpoint: the whole problem's state is
                           // written after every phase instead (write_phase_checkpoint)
   if (p.solver == 0) p.solver = 2;  // the phases are parts of a large problem: working-set rounds at any size
-  // the inactive rows' gradient comes from the f32 predict GEMM: the phases'
-  // kernel values must be the same f32 MFMA values (split-GEMM values differ
-  // by ~1e-5, which C-sized alpha changes turn into gradient drift)
-  if (p.gram_precision == 0) p.gram_precision = 1;
+  // the inactive rows' gradient comes from the predict GEMM: the phases' kernel
+  // values must be the ones it computes (f32 MFMA and split-operand values
+  // differ by ~1e-5, which C-sized alpha changes turn into gradient drift) —
+  // the split GEMMs when the predictor runs split (dp >= 128: 5x the f32 GEMM's
+  // speed for the phases' row GEMMs, which was round 3's 2x loss on
+  // synthetic-2m), the f32 MFMA otherwise
+  if (p.gram_precision == 0) p.gram_precision = launch::predict_uses_split((d + 15) / 16 * 16) ? 0 : 1;
   const float gamma = resolve_gamma(p.gamma, d);
   p.gamma = gamma;
   const float C = p.C;
@@ -257,6 +264,22 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   res.t_solve = now() - t_start;
   res.shrink_phases = phases;
   return res;
+}
+
+bool shrink_auto(const SolverParams& p, int64_t n, int d, int device) {
+  (void)d;
+  if (p.solver == 1) return false;                       // solver=smo: the reference's trajectory
+  if (p.solver == 0 && n < kWsAutoRows) return false;    // auto below 50k rows: the pair engines
+  if (p.force_cache) return false;                     // an explicit engine request (tests, probes)
+  HIP_CHECK(hipSetDevice(device));
+  size_t freeb = 0, totalb = 0;
+  HIP_CHECK(hipMemGetInfo(&freeb, &totalb));
+  // the setup's cache budget (gpu_setup.hip): the Gram is resident when every
+  // line (>= n floats, padded to 256 rows) fits it
+  double budget = p.cache_frac * (double)freeb - 256.0 * 1024 * 1024;
+  if (p.cache_mb > 0) budget = std::min(budget, p.cache_mb * 1024.0 * 1024.0);
+  const double ld = (double)((n + 255) / 256 * 256);
+  return (double)n * ld * 4.0 > budget;
 }
 
 }  // namespace dpsvm

@@ -117,14 +117,23 @@ class SVCConfig:
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
     ws_block: int = 32              # rounds per hipGraph block
     # one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking: phases on the rows that can
-    # still violate, the rest of the gradient updated by one predict GEMM per phase)
-    shrink: bool = False
+    # still violate, the rest of the gradient updated by one predict GEMM per phase).  auto: on where it
+    # pays — one GPU, working-set rounds, the whole Gram not resident (C.shrink_auto) | on | off
+    shrink: str = "auto"
     ws_t_halve: float = 0.9         # multi-block: a round damped below this t halves the block count
     ws_clip_fallback: bool = True   # multi-block, independent clipping: one block per round after a clip
     eta: str = "x"                  # pair engines' K(hi, lo): x (from the X rows) | gram (resident Gram)
     # Gram / kernel-row GEMM arithmetic: auto (split for the working-set engines, f32 for the pair engines),
     # f32 (f32-input MFMA), split (fp16 MFMA over hi/lo split operands: fp32 accuracy, 3/16 of the MFMA time)
     gram: str = "auto"
+
+    def shrink_mode(self) -> str:
+        s = self.shrink
+        if s is True or s is False:
+            return "on" if s else "off"
+        if s not in ("auto", "on", "off"):
+            raise ValueError(f"shrink must be auto, on or off (got {s!r})")
+        return s
 
     def resolved_gamma(self, d: int) -> float:
         return float(self.gamma) if self.gamma is not None and self.gamma >= 0 else 1.0 / float(d)
@@ -242,6 +251,10 @@ class SVC:
             return s.astype(np.float32)
         return np.where(s > 0, self.classes_[-1], self.classes_[0])
 
+    def _use_shrink(self, p, n: int, d: int, dev: int) -> bool:
+        mode = self.config.shrink_mode()
+        return mode == "on" or (mode == "auto" and bool(load().shrink_auto(p, n, d, dev)))
+
     # ------------------------------------------------------------------ fit
     def fit(self, X, y, comm=None, resume=None, progress: Optional[Callable] = None,
             rank_rows: Optional[int] = None) -> "SVC":
@@ -265,7 +278,7 @@ class SVC:
         kind, dev = cfg.device_kind()
         self.device_ = f"{kind}:{dev}" if kind == "cuda" else "cpu"
         t0 = time.perf_counter()
-        if kind == "cuda" and cfg.shrink and comm is None and rank_rows is None:
+        if kind == "cuda" and comm is None and rank_rows is None and self._use_shrink(p, n, d, dev):
             alpha, info = C.solve_shrinking(X, ys, p, dev, ck, progress)
             self.setup_info_ = {"iteration": "ws+shrinking", "device_name": C.device_name(dev), "n_local": n,
                                 "x_replicated": True, "engine_note": f"{info['shrink_phases']} shrinking phases"}
