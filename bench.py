@@ -127,6 +127,9 @@ def parse(argv=None):
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
     ap.add_argument("--cache-groups", type=int, default=256)
     ap.add_argument("--force-cache", action="store_true")
+    ap.add_argument("--engines", default="production", choices=["production", "all"],
+                    help="all: also the quarantined pair-at-a-time cache / partitioned-X engines (A/B probes; "
+                         "--host-cache-lines needs it)")
     ap.add_argument("--xch-poll-batch", type=int, default=0)
     ap.add_argument("--xch-mem", default="auto", choices=["auto", "uncached", "coarse"])
     ap.add_argument("--xch-timeout", type=float, default=None,
@@ -262,7 +265,7 @@ def main(argv=None) -> int:
                     x_mode=a.x_mode, graph_block=a.graph_block, host_cache_lines=a.host_cache_lines,
                     exchange=a.exchange, persist=a.persist, persist_block=a.persist_block,
                     dp="replicate" if a.dp == "measure" else a.dp,
-                    rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache,
+                    rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache, engines=a.engines,
                     xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
                     ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, ws_blocks=a.ws_blocks, ws_inner=a.ws_inner, eta=a.eta,
                     gram=a.gram,

@@ -74,7 +74,9 @@ inline void usage_train(const char* prog, bool seq) {
                "   --exchange MODE     :  per-iteration keys: auto | allreduce | peer (in-kernel, xGMI)\n"
                "   --dp MODE           :  data parallelism at world > 1: auto | shard | replicate\n"
                "   --force-cache       :  kernel-row cache mode even when the Gram fits\n"
-               "   --cache-engine E    :  cache mode, one launch per iteration: fused | chain\n"
+               "   --cache-engine E    :  cache mode, one launch per iteration: fused | chain (--engines all)\n"
+               "   --engines E         :  production (default) | all: also the quarantined pair-at-a-time cache /\n"
+               "                         partitioned-X engines (tests, A/B probes; --host-cache-lines needs it)\n"
                "   --cache-groups N    :  cache mode workgroups per rank (default 256)\n"
                "   --rows-per-group N  :  rows per workgroup of the fused/persistent engines (multiple of 256)\n"
                "   --xch-poll-batch N --xch-sleep N --xch-stride N --xch-mem auto|uncached|coarse\n"
@@ -113,7 +115,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
     OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL, OPT_WSBLOCKS,
-    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM, OPT_SHRINK
+    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM, OPT_SHRINK, OPT_ENGINES
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -147,7 +149,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {"ws-wss", required_argument, 0, OPT_WSWSS}, {"gram", required_argument, 0, OPT_GRAM},
-      {"shrink", optional_argument, 0, OPT_SHRINK},
+      {"shrink", optional_argument, 0, OPT_SHRINK}, {"engines", required_argument, 0, OPT_ENGINES},
       {0, 0, 0, 0}};
   while (true) {
     int idx = 0;
@@ -225,6 +227,12 @@ inline Options parse_train(int argc, char** argv, bool seq) {
         const std::string v = optarg;
         if (v != "fused" && v != "chain") usage_train(argv[0], seq);
         o.p.cache_engine = v == "chain" ? 1 : 0;
+        break;
+      }
+      case OPT_ENGINES: {
+        const std::string v = optarg;
+        if (v != "production" && v != "all") usage_train(argv[0], seq);
+        o.p.engines = v == "all" ? 1 : 0;
         break;
       }
       case OPT_CGROUPS: o.p.cache_groups = atoi(optarg); break;

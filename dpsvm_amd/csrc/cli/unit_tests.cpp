@@ -208,6 +208,7 @@ static void test_gpu() {
   SolveResult rc = solve_cpu(ds, p);
   for (int mode = 0; mode < 3; ++mode) {
     SolverParams pg = p;
+    pg.engines = 1;                       // the pair-at-a-time cache / partitioned engines (quarantined)
     if (mode == 1) pg.cache_lines = 64;   // LRU + speculation
     if (mode == 2) pg.x_mode = 2;         // partitioned records, LRU
     GpuSolver s(pg, nullptr, 0);

@@ -92,6 +92,10 @@ struct SolverParams {
   //      every choice is a parameter, none comes from the environment) ----
   bool force_cache = false;   // kernel-row cache mode even when the Gram shard fits
   int cache_engine = 0;       // cache mode, one launch per iteration: 0 fused kernel, 1 rows/step/finalize chain
+  // 0 production (kEngineTable: ws-dense, ws-cache, persistent-dense, fused-dense), 1 all — also the
+  // quarantined pair-at-a-time engines for a Gram that is not resident or an X that is partitioned
+  // (kQuarantineTable: persistent-cache, fused-cache, chain; tests and A/B probes only)
+  int engines = 0;
   int cache_groups = 256;     // cache mode: workgroups per rank (one per CU: the X pass wants every CU)
   int rows_per_group = 0;     // rows per workgroup of the fused / persistent engines (0 auto; multiple of 256)
   // peer exchange (in-kernel key exchange of the fused / persistent engines)

@@ -68,11 +68,17 @@ struct EngineFacts {
   bool dense = false;             // Gram resident
   bool cache_replicated = false;  // Gram not resident, X replicated (the pair cache engines' X pass)
   bool persistent = false;        // in-kernel exchange set up and its candidate's geometry fits
+  bool quarantine = false;        // engines=all: the quarantined rows may match
 };
 
 // The engine choice: first matching row wins.  `use` is the path that reaches
 // the row (docs/DESIGN.md §2 lists the same table).  A persistent row whose
 // grid then fails the co-residency census drops to the fused row below it.
+// Production: the four rows of kEngineTable.  The pair-at-a-time engines for a
+// Gram that is not resident or an X that is partitioned (kQuarantineTable) are
+// reached only with SolverParams::engines = 1 (tests, A/B probes): with 288 GB
+// per GPU the Gram of the pair engines' problems (< 50k rows) is resident, and
+// ws-cache is 5-10x faster on the problems whose Gram is not.
 struct EngineRule {
   EngineKind kind;
   bool (*when)(const EngineFacts&);
@@ -87,17 +93,24 @@ inline constexpr EngineRule kEngineTable[] = {
      "default below 50k rows (solver auto) or solver=smo: the reference's trajectory"},
     {EngineKind::FusedDense, [](const EngineFacts& f) { return f.dense; },
      "fallback of persistent-dense (census or exchange self-test failed, persist=off, forced collectives)"},
-    {EngineKind::PersistCache, [](const EngineFacts& f) { return f.cache_replicated && f.persistent; },
-     "pair-at-a-time in cache mode: solver=smo, or a cache too small for ws-cache"},
-    {EngineKind::FusedCache, [](const EngineFacts& f) { return f.cache_replicated; },
-     "fallback of persistent-cache; host spill tier (host_cache_lines); persist=off"},
-    {EngineKind::Chain, [](const EngineFacts&) { return true; },
-     "pair-at-a-time with X partitioned (x_mode=partitioned, solver=smo or below 50k rows); cache_engine=chain"},
 };
-inline EngineKind choose_engine(const EngineFacts& f) {
+inline constexpr EngineRule kQuarantineTable[] = {
+    {EngineKind::PersistCache, [](const EngineFacts& f) { return f.cache_replicated && f.persistent; },
+     "engines=all: pair-at-a-time in cache mode (solver=smo, or a cache too small for ws-cache)"},
+    {EngineKind::FusedCache, [](const EngineFacts& f) { return f.cache_replicated; },
+     "engines=all: fallback of persistent-cache; host spill tier (host_cache_lines); persist=off"},
+    {EngineKind::Chain, [](const EngineFacts&) { return true; },
+     "engines=all: pair-at-a-time with X partitioned (x_mode=partitioned, solver=smo); cache_engine=chain"},
+};
+// false: no production row matches and the quarantined rows are off (the
+// setup reports why: the configuration needs engines=all)
+inline bool choose_engine(const EngineFacts& f, EngineKind* out) {
   for (const EngineRule& r : kEngineTable)
-    if (r.when(f)) return r.kind;
-  return EngineKind::Chain;
+    if (r.when(f)) return *out = r.kind, true;
+  if (f.quarantine)
+    for (const EngineRule& r : kQuarantineTable)
+      if (r.when(f)) return *out = r.kind, true;
+  return false;
 }
 
 // Written by smo_finalize, read by the next iteration's kernels.

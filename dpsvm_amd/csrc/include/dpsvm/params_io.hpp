@@ -38,6 +38,7 @@ void for_each_param(SolverParams& p, F&& f) {
   f("persist_block", p.persist_block);
   f("force_cache", p.force_cache);
   f("cache_engine", p.cache_engine);
+  f("engines", p.engines);
   f("cache_groups", p.cache_groups);
   f("rows_per_group", p.rows_per_group);
   f("xch_poll_batch", p.xch_poll_batch);

@@ -176,6 +176,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("persist_block", &SolverParams::persist_block)
       .def_readwrite("force_cache", &SolverParams::force_cache)
       .def_readwrite("cache_engine", &SolverParams::cache_engine)
+      .def_readwrite("engines", &SolverParams::engines)
       .def_readwrite("cache_groups", &SolverParams::cache_groups)
       .def_readwrite("rows_per_group", &SolverParams::rows_per_group)
       .def_readwrite("xch_poll_batch", &SolverParams::xch_poll_batch)
@@ -217,22 +218,29 @@ PYBIND11_MODULE(_C, m) {
                     [](Checkpoint& c, F32 a) { c.alpha = from_np(a); })
       .def_property("f", [](const Checkpoint& c) { return to_np(c.f); },
                     [](Checkpoint& c, F32 a) { c.f = from_np(a); });
-  // the device solver's engine choice (device_state.hpp kEngineTable), for docs and tests
-  m.def("engine_table", []() {
+  // the device solver's engine choice (device_state.hpp kEngineTable, then
+  // kQuarantineTable with engines=all), for docs and tests
+  m.def("engine_table", [](bool quarantine) {
     std::vector<std::pair<std::string, std::string>> out;
     for (const EngineRule& r : kEngineTable) out.emplace_back(engine_name(r.kind), r.use);
+    if (quarantine)
+      for (const EngineRule& r : kQuarantineTable) out.emplace_back(engine_name(r.kind), r.use);
     return out;
-  });
-  m.def("choose_engine", [](bool ws_dense, bool ws_cache, bool dense, bool cache_replicated, bool persistent) {
+  }, py::arg("quarantine") = false);
+  m.def("choose_engine", [](bool ws_dense, bool ws_cache, bool dense, bool cache_replicated, bool persistent,
+                            bool quarantine) -> py::object {
     EngineFacts f;
     f.ws_dense = ws_dense;
     f.ws_cache = ws_cache;
     f.dense = dense;
     f.cache_replicated = cache_replicated;
     f.persistent = persistent;
-    return std::string(engine_name(choose_engine(f)));
+    f.quarantine = quarantine;
+    EngineKind k;
+    if (!choose_engine(f, &k)) return py::none();
+    return py::str(engine_name(k));
   }, py::arg("ws_dense") = false, py::arg("ws_cache") = false, py::arg("dense") = false,
-        py::arg("cache_replicated") = false, py::arg("persistent") = false);
+        py::arg("cache_replicated") = false, py::arg("persistent") = false, py::arg("quarantine") = false);
   m.def("write_checkpoint", &write_checkpoint, py::arg("path"), py::arg("ck"));
   m.def("read_checkpoint", &read_checkpoint, py::arg("path"));
 

@@ -331,7 +331,13 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // fp16 split operands of x for the split GEMMs (allocated before the cache is
   // sized from the free memory; released below if the engine runs f32 GEMMs)
   DPSVM_CHECK(m.p.gram_precision >= 0 && m.p.gram_precision <= 2, "gram_precision must be 0 (auto), 1 (f32) or 2 (split)");
-  const bool maybe_ws = m.p.solver == 2 || (m.p.solver == 0 && n >= kWsAutoRows);
+  DPSVM_CHECK(m.p.engines == 0 || m.p.engines == 1, "engines must be 0 (production) or 1 (all)");
+  DPSVM_CHECK(m.p.engines == 1 || (m.p.host_cache_lines == 0 && m.p.cache_engine == 0),
+              "host_cache_lines and cache_engine=chain run on the quarantined pair-at-a-time cache engines: "
+              "set engines=all (tests, A/B probes)");
+  // production engines, solver auto: the working-set engines also below
+  // kWsAutoRows rows when the Gram is not resident or X is partitioned
+  const bool maybe_ws = m.p.solver == 2 || (m.p.solver == 0 && (n >= kWsAutoRows || m.p.engines == 0));
   if (m.p.gram_precision == 2 || (m.p.gram_precision == 0 && maybe_ws)) {
     m.xs = dmalloc<uint8_t>((size_t)m.x_rows * launch::split_row_u4(m.dp) * 16, &m.bytes);
     m.xsh = dmalloc<int32_t>((size_t)m.x_rows, &m.bytes);
@@ -353,10 +359,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // solver auto: the working-set engines from kWsAutoRows rows on (the pair-at-a-time
   // engines follow the reference's trajectory exactly and win on small problems;
   // on 500k-2M rows ws is 5-10x faster: profiles/r2_*_converged.json)
-  const bool want_ws = m.p.solver == 2 || (m.p.solver == 0 && n >= kWsAutoRows);
+  const bool gram_fits = m.all_agree(want_lines >= n && !m.p.force_cache, m.comm, m.world);
+  const bool want_ws = m.p.solver == 2 ||
+                       (m.p.solver == 0 && (n >= kWsAutoRows || (m.p.engines == 0 && (!gram_fits || !m.replicated))));
   const bool ws_ok = want_ws && launch::ws_supported(nl_max, m.world, ws_q);
-  m.dense = (m.replicated || ws_ok) && want_lines >= n && !m.p.force_cache;
-  m.dense = m.all_agree(m.dense, m.comm, m.world);  // free memory can differ per device
+  m.dense = (m.replicated || ws_ok) && gram_fits;  // agreed: free memory can differ per device
   if (m.dense) {
     m.RBf = geo_dense.first;
     m.Gf = geo_dense.second;
@@ -372,7 +379,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 &&
                         (!m.replicated || launch::smo_fused_lru_supported(m.dp));
   if (want_ws && !ws_ok)
-    m.info.engine_note = "ws engines need <= " + std::to_string(kWsMaxRPT) + " rows per selection thread: SMO engine used";
+    m.info.engine_note = "ws engines need <= " + std::to_string(kWsMaxRPT) + " rows per selection thread";
   const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
                          launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
@@ -590,14 +597,20 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   }
   const bool wsc_fits = wsc_cand && launch::ws_cache_supported(m.L, ws_q);
   if (wsc_cand && !wsc_fits)
-    m.info.engine_note = "ws-cache needs >= " + std::to_string(2 * ws_q + 512) + " lines: SMO cache engine used";
+    m.info.engine_note = "ws-cache needs >= " + std::to_string(2 * ws_q + 512) + " lines";
   EngineFacts facts;
   facts.ws_dense = ws_cand;
   facts.ws_cache = wsc_fits;
   facts.dense = m.dense;
   facts.cache_replicated = fused_lru_ok;
   facts.persistent = (m.dense ? pdense_cand : plru_cand) && m.xch;
-  m.kind = choose_engine(facts);
+  facts.quarantine = m.p.engines == 1;
+  if (!choose_engine(facts, &m.kind)) {
+    std::string why = m.p.solver == 1 ? "solver=smo (pair-at-a-time) needs the resident Gram and replicated X"
+                                      : "no working-set engine fits this configuration";
+    if (!m.info.engine_note.empty()) why += " (" + m.info.engine_note + ")";
+    DPSVM_CHECK(false, why + "; the pair-at-a-time cache / partitioned-X engines are quarantined: set engines=all");
+  }
   if (m.persistent() && !m.census(m.kind)) {
     DPSVM_CHECK(m.p.persist != 2, "persistent engine requested (persist=on) but its grid is not co-resident (" +
                                       m.info.engine_note + ")");

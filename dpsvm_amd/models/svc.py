@@ -92,6 +92,10 @@ class SVCConfig:
     dp: str = "auto"                # world > 1: auto | shard (rows split) | replicate (every rank solves it all)
     force_cache: bool = False       # kernel-row cache mode even when the Gram fits
     cache_engine: str = "fused"     # cache mode, one launch per iteration: fused | chain
+    # production (ws-dense, ws-cache, persistent-dense, fused-dense) | all: also the quarantined
+    # pair-at-a-time engines for a non-resident Gram / partitioned X (persistent-cache, fused-cache, chain;
+    # host_cache_lines and cache_engine=chain need it) — tests and A/B probes (device_state.hpp kQuarantineTable)
+    engines: str = "production"
     cache_groups: int = 256         # cache mode workgroups per rank
     rows_per_group: int = 0         # rows per workgroup of the fused/persistent engines (0 auto; multiple of 256)
     xch_poll_batch: int = 0         # peer exchange: publications per lane per poll round (0 auto)
@@ -176,6 +180,7 @@ class SVCConfig:
         p.dp_policy = _pick(_DP, self.dp, "dp")
         p.force_cache = bool(self.force_cache)
         p.cache_engine = _pick(_CACHE_ENGINE, self.cache_engine, "cache_engine")
+        p.engines = _pick({"production": 0, "all": 1}, self.engines, "engines")
         p.cache_groups = int(self.cache_groups)
         if self.rows_per_group % 256:
             raise ValueError("rows_per_group must be a multiple of 256")

@@ -18,7 +18,7 @@ def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
     ctx = init_distributed(device="cuda")
     comm = make_comm(ctx, "gloo")
     X, y = synthetic("covtype", n=n, seed=2)
-    extra = {"cache_lines": 256} if engine == "persistent-cache" else {}
+    extra = {"cache_lines": 256, "engines": "all"} if engine == "persistent-cache" else {}
     if engine.startswith("ws"):  # working-set rounds, rows sharded (candidates + sub-Gram rows in-kernel)
         extra = {"solver": "ws", "dp": "shard"}
         if engine == "ws-cache":

@@ -1,6 +1,7 @@
 """The device solver's engine choice is one table (device_state.hpp kEngineTable,
-evaluated by choose_engine() in gpu_setup.hip); docs/DESIGN.md §2 lists the same
-rows.  CPU only: the table is host code."""
+evaluated by choose_engine() in gpu_setup.hip; kQuarantineTable after it only
+with engines=all); docs/DESIGN.md §2 lists the same rows.  CPU only: the table
+is host code."""
 import os
 import re
 
@@ -9,21 +10,31 @@ import pytest
 C = pytest.importorskip("dpsvm_amd._C")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRODUCTION = ["ws-dense", "ws-cache", "persistent-dense", "fused-dense"]
+QUARANTINE = ["persistent-cache", "fused-cache", "chain"]
+
+
+def _doc_rows(doc, start, stop):
+    sec = doc[doc.index(start):doc.index(stop)]
+    rows = re.findall(r"^\| ([a-z-]+)(?: \(§[^)]*\))? \|", sec, flags=re.M)
+    return [r for r in rows if r != "engine"]
 
 
 def test_engine_table_matches_design_doc():
     table = C.engine_table()
-    names = [n for n, _ in table]
-    assert names == ["ws-dense", "ws-cache", "persistent-dense", "fused-dense", "persistent-cache", "fused-cache",
-                     "chain"]
+    assert [n for n, _ in table] == PRODUCTION  # <= 4 production rows
+    full = C.engine_table(quarantine=True)
+    assert [n for n, _ in full] == PRODUCTION + QUARANTINE
     with open(os.path.join(ROOT, "docs", "DESIGN.md")) as fh:
         doc = fh.read()
-    sec = doc[doc.index("**Engine choice**"):doc.index("## 2a.")]
-    doc_rows = re.findall(r"^\| ([a-z-]+)(?: \(§[^)]*\))? \|", sec, flags=re.M)
-    doc_rows = [r for r in doc_rows if r != "engine"]
-    assert doc_rows == names, "DESIGN.md §2 engine table out of sync with kEngineTable"
-    for _, use in table:
+    assert _doc_rows(doc, "**Engine choice**", "**Quarantined rows**") == PRODUCTION, \
+        "DESIGN.md §2 engine table out of sync with kEngineTable"
+    assert _doc_rows(doc, "**Quarantined rows**", "## 2a.") == QUARANTINE, \
+        "DESIGN.md §2 quarantine table out of sync with kQuarantineTable"
+    for _, use in full:
         assert use
+    for _, use in full[len(PRODUCTION):]:
+        assert use.startswith("engines=all")
 
 
 @pytest.mark.parametrize("facts,want", [
@@ -31,10 +42,16 @@ def test_engine_table_matches_design_doc():
     (dict(ws_cache=True, cache_replicated=True, persistent=True), "ws-cache"),
     (dict(dense=True, persistent=True), "persistent-dense"),
     (dict(dense=True), "fused-dense"),
-    (dict(cache_replicated=True, persistent=True), "persistent-cache"),
-    (dict(cache_replicated=True), "fused-cache"),
-    (dict(), "chain"),
-    (dict(persistent=True), "chain"),
+    (dict(cache_replicated=True, persistent=True), None),
+    (dict(cache_replicated=True), None),
+    (dict(), None),
+    (dict(cache_replicated=True, persistent=True, quarantine=True), "persistent-cache"),
+    (dict(cache_replicated=True, quarantine=True), "fused-cache"),
+    (dict(quarantine=True), "chain"),
+    (dict(persistent=True, quarantine=True), "chain"),
+    (dict(ws_cache=True, cache_replicated=True, quarantine=True), "ws-cache"),
 ])
 def test_choose_engine_first_match(facts, want):
+    """None: no production row matches — the setup refuses the configuration
+    and names engines=all"""
     assert C.choose_engine(**facts) == want

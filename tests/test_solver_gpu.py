@@ -9,10 +9,19 @@ import numpy as np
 import pytest
 import torch
 
-from dpsvm_amd import SVC, load_model
+from dpsvm_amd import SVC as _SVC
+from dpsvm_amd import load_model
 from dpsvm_amd.utils.datasets import synthetic
 
 pytestmark = pytest.mark.gpu
+
+
+def SVC(*args, **kw):
+    """this module covers every device engine: the quarantined pair-at-a-time
+    cache / partitioned-X engines included (engines=all; the production rows
+    come first in the choice, so dense problems run the same engines)"""
+    kw.setdefault("engines", "all")
+    return _SVC(*args, **kw)
 
 
 @pytest.fixture(scope="module", autouse=True)

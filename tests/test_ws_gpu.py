@@ -128,10 +128,35 @@ def test_ws_cache_engine_bit_identical_to_resident_gram(case):
 
 
 def test_ws_cache_engine_small_cache_refused_cleanly():
+    """A cache below ws-cache's 2 q + 512 lines: the production engines refuse
+    it with the reason; engines=all falls back to the (quarantined) pair cache
+    engines."""
     X, y = synthetic("adult", n=3000, seed=1)
-    s = SVC(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300).fit(X, y)
+    kw = dict(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300)
+    with pytest.raises(Exception, match="ws-cache needs .*engines=all"):
+        SVC(**kw).fit(X, y)
+    s = SVC(engines="all", **kw).fit(X, y)
     assert s.setup_info_["iteration"] in ("persistent-cache", "fused-cache")
     assert "ws-cache needs" in s.setup_info_["engine_note"]
+
+
+def test_production_engines_route_small_cache_problems_to_ws():
+    """Production engines, solver auto below 50k rows: the pair-at-a-time
+    engines only with the resident Gram; a Gram that is not resident (here a
+    capped cache) runs ws-cache, and solver=smo there is refused with the
+    reason (the pair cache engines are quarantined behind engines=all)."""
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    dense = SVC(**kw).fit(X, y)
+    assert dense.setup_info_["iteration"] == "persistent-dense"
+    cap = SVC(force_cache=True, cache_lines=2000, **kw).fit(X, y)
+    assert cap.setup_info_["iteration"] == "ws-cache" and cap.converged_
+    assert abs(cap.b_ - dense.b_) < 1e-2
+    with pytest.raises(Exception, match="solver=smo .*engines=all"):
+        SVC(solver="smo", force_cache=True, cache_lines=2000, **kw).fit(X, y)
+    pair = SVC(solver="smo", force_cache=True, cache_lines=2000, engines="all", **kw).fit(X, y)
+    assert pair.setup_info_["iteration"] == "persistent-cache"
+    assert pair.converged_ and abs(pair.b_ - dense.b_) < 1e-2
 
 
 def _fit_threads(native, world, X, y, **kw):
