@@ -137,6 +137,7 @@ def parse(argv=None):
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--log-every", type=int, default=0,
                     help="rank 0 prints b_hi / b_lo / gap every N pair steps (long big-config runs)")
+    ap.add_argument("--verbose", action="store_true", help="solver diagnostics on stderr (engine, shrink phases)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     for k, v in PRESETS[a.config].items():
@@ -276,6 +277,7 @@ def main(argv=None) -> int:
     params = cfg.to_native(X.shape[1])
     if ctx.rank == 0:
         params.log_every = a.log_every
+        params.verbose = a.verbose
     # auto: RCCL, or gloo on EVERY rank when the RCCL bootstrap fails on any
     # rank (agreed over the host group, dpsvm_amd.parallel.make_comm); the
     # per-iteration exchange is in-kernel either way
@@ -287,16 +289,16 @@ def main(argv=None) -> int:
         print(f"[bench] iter {it} b_hi {bh:.6g} b_lo {bl:.6g} gap {bl - bh:.3g} {el:.1f} s "
               f"hits {hits} misses {misses}", file=sys.stderr, flush=True)
 
-    if on_gpu and a.shrink == "on" and n_ranks > 1:
-        raise SystemExit("--shrink on runs on one GPU")
-    use_shrink = on_gpu and n_ranks == 1 and (
-        a.shrink == "on" or (a.shrink == "auto" and C.shrink_auto(params, X.shape[0], X.shape[1], ctx.local_rank)))
+    sh_comm = comm if n_ranks > 1 else None
+    use_shrink = on_gpu and (a.shrink == "on" or (
+        a.shrink == "auto" and C.shrink_auto(params, X.shape[0], X.shape[1], ctx.local_rank, sh_comm)))
     if use_shrink:
-        # shrinking phases (one GPU): every phase sets its solver up inside the timed run
+        # shrinking phases: every phase sets its (multi-rank) solver up inside the timed run
         solver = None
-        info = {"device_name": C.device_name(ctx.local_rank), "x_replicated": True, "iteration": "ws+shrinking"}
+        info = {"device_name": C.device_name(ctx.local_rank), "x_replicated": True, "iteration": "ws+shrinking",
+                "dp_policy": f"per phase ({a.dp})" if n_ranks > 1 else "none"}
         run = lambda: C.solve_shrinking(X, y, params, ctx.local_rank, None,  # noqa: E731
-                                        progress if a.log_every else None)
+                                        progress if (a.log_every and ctx.rank == 0) else None, sh_comm)
     elif on_gpu:
         solver = C.GpuSolver(params, comm, ctx.local_rank)
         info = solver.setup(X, X.shape[0], y)

@@ -4,11 +4,12 @@
 set -o pipefail
 mkdir -p gpurun_out
 B="python3 -u bench.py --no-accuracy --reference-check off"
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_ws_gpu.py tests/test_cli.py -k "small_cache or production_engines or shrink" > gpurun_out/r4sh_pytest.log 2>&1 &&
 timeout -k 10 300 $B --steps 3 --warmup 1 > gpurun_out/r4sh_headline.json 2> gpurun_out/r4sh_headline.err &&
-timeout -k 10 300 $B --config covtype --clip box --steps 1 --warmup 0 --log-every 5000000 > gpurun_out/r4sh_covbox_auto.json 2> gpurun_out/r4sh_covbox_auto.err &&
+timeout -k 10 300 $B --config covtype --clip box --steps 1 --warmup 0 --log-every 5000000 --verbose > gpurun_out/r4sh_covbox_auto.json 2> gpurun_out/r4sh_covbox_auto.err &&
 timeout -k 10 200 $B --config covtype-ref --steps 1 --warmup 0 --log-every 5000000 > gpurun_out/r4sh_covref_auto.json 2> gpurun_out/r4sh_covref_auto.err &&
 timeout -k 10 200 $B --config covtype-ref --shrink off --steps 1 --warmup 0 --log-every 5000000 > gpurun_out/r4sh_covref_off.json 2> gpurun_out/r4sh_covref_off.err &&
-timeout -k 10 400 $B --config synthetic-2m --steps 1 --warmup 0 --log-every 1000000 > gpurun_out/r4sh_syn2m_auto.json 2> gpurun_out/r4sh_syn2m_auto.err &&
+timeout -k 10 400 $B --config synthetic-2m --steps 1 --warmup 0 --log-every 1000000 --verbose > gpurun_out/r4sh_syn2m_auto.json 2> gpurun_out/r4sh_syn2m_auto.err &&
 timeout -k 10 400 $B --config synthetic-2m --shrink off --steps 1 --warmup 0 --log-every 1000000 > gpurun_out/r4sh_syn2m_off.json 2> gpurun_out/r4sh_syn2m_off.err
 rc=$?
 python3 - <<'PY'

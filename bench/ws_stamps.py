@@ -33,6 +33,7 @@ def main() -> int:
     ap.add_argument("--cache-lines", type=int, default=0)
     ap.add_argument("--force-cache", action="store_true")
     ap.add_argument("--exchange", default="auto", help="peer: the in-kernel exchange at world 1 (loopback)")
+    ap.add_argument("--clip", default="independent", choices=["independent", "box"])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "ws_stamps")
@@ -43,7 +44,7 @@ def main() -> int:
     X, y = synthetic(a.data, n=a.samples, d=a.features)
     clf = SVC(C=a.C, gamma=a.gamma, eps=1e-3, device="cuda", solver="ws", ws_size=a.ws_size, ws_new=a.ws_new,
               ws_rel=a.ws_rel, ws_blocks=a.ws_blocks, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache,
-              exchange=a.exchange, xch_timeout_s=60.0).fit(X, y)
+              exchange=a.exchange, xch_timeout_s=60.0, clip=a.clip, shrink="off").fit(X, y)
     raw = np.fromfile(path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
     rounds = min(clf.n_rounds_, 4096)
     s = raw[2:rounds]

@@ -80,13 +80,15 @@ int main(int argc, char** argv) {
           return;
         }
         const int dev = (o.ranks > 0 || world == 1) ? o.device : r;
-        if (o.shrink == 2 && world > 1) fail("--shrink runs on one GPU");
-        if (world == 1 && (o.shrink == 2 || (o.shrink == 0 && shrink_auto(o.p, n, d, dev)))) {
-          // one GPU: shrinking phases, each a device solver on the active rows
-          // (solver/gpu_shrink.cpp); training accuracy by the GPU predictor
-          std::cout << "SETUP DONE\n";
-          extras.engine = "ws+shrinking";
-          results[r] = solve_shrinking(o.p, dev, ds.x.data(), n, d, ds.y.data(), resume.get(), prog);
+        if (o.shrink == 2 || (o.shrink == 0 && shrink_auto(o.p, n, d, dev, world > 1 ? comm : nullptr))) {
+          // shrinking phases, each a (multi-rank) device solver on the active
+          // rows (solver/gpu_shrink.cpp); training accuracy by the GPU predictor
+          if (r == 0) {
+            std::cout << "SETUP DONE\n";
+            extras.engine = "ws+shrinking";
+          }
+          results[r] = solve_shrinking(o.p, dev, ds.x.data(), n, d, ds.y.data(), resume.get(), prog,
+                                       world > 1 ? comm : nullptr);
           const double ta0 = cli::now_s();
           if (!o.skip_accuracy) {
             GpuPredictor pred(make_model(ds, results[r].alpha, results[r].b, o.p.gamma), dev);

@@ -96,6 +96,9 @@ class GpuSolver {
   // after solve(): this rank's gradient f_j = sum_i alpha_i y_i K(i, j) - y_j
   // as the solver maintained it (its local rows)
   std::vector<float> gradient() const;
+  // after solve(): the whole gradient on every rank (the shards all-gathered;
+  // a collective at world > 1)
+  std::vector<float> gradient_all();
   const GpuSetupInfo& info() const;
   struct Impl;
 
@@ -103,21 +106,24 @@ class GpuSolver {
   std::unique_ptr<Impl> impl_;
 };
 
-// Shrinking (LIBSVM's heuristic, as problem reduction; one device): phases of
-// the device solver on the active rows only — free alphas and bounded ones that
-// can still violate (f below b_lo on the up side, above b_hi on the low side) —
-// each to its own stop test, then the inactive rows' gradient is brought up to
-// date by one predict GEMM over the phase's alpha changes and the reference's
-// stop test is evaluated on the whole problem.  x, y: host, all n rows.
+// Shrinking (LIBSVM's heuristic, as problem reduction): phases of the device
+// solver on the active rows only — free alphas and bounded ones that can still
+// violate (f below b_lo on the up side, above b_hi on the low side) — each to
+// its own stop test, then the inactive rows' gradient is brought up to date by
+// one predict GEMM over the phase's alpha changes and the reference's stop
+// test is evaluated on the whole problem.  x, y: host, all n rows (on every
+// rank).  comm (world > 1): every rank calls; a phase is a multi-rank solve
+// (dp policy of p), the inactive-row update split over the ranks.
 SolveResult solve_shrinking(const SolverParams& p, int device, const float* x, int64_t n, int d, const float* y,
-                            const Checkpoint* resume = nullptr, const ProgressFn& progress = {});
+                            const Checkpoint* resume = nullptr, const ProgressFn& progress = {},
+                            Communicator* comm = nullptr);
 
 // shrink="auto" (library, svmTrain and bench default): shrinking phases where
 // they pay — one GPU, working-set rounds, and a Gram that does not fit the
 // device's cache budget (the ws-cache regime: covtype-shape 581k x 54).  On a
 // resident Gram (the headline) a phase only adds setup work; measured in
 // profiles/r4_shrink_auto_*.txt.
-bool shrink_auto(const SolverParams& p, int64_t n, int d, int device);
+bool shrink_auto(const SolverParams& p, int64_t n, int d, int device, Communicator* comm = nullptr);
 
 // Stand-alone GPU predictor (svmTest GPU path): model SVs resident on device,
 // decision values of a host or device matrix via the MFMA predict kernel.

@@ -363,7 +363,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("progress") = py::none());
 
   m.def("solve_shrinking", [](F32 x, F32 y, const SolverParams& p, int device, const Checkpoint* resume,
-                              py::object progress) {
+                              py::object progress, std::shared_ptr<Communicator> comm) {
     int64_t n = 0;
     int d = 0;
     check_xy(x, y, n, d);
@@ -371,14 +371,17 @@ PYBIND11_MODULE(_C, m) {
     SolveResult r;
     {
       py::gil_scoped_release rel;
-      r = solve_shrinking(p, device, x.data(), n, d, y.data(), resume, prog);
+      r = solve_shrinking(p, device, x.data(), n, d, y.data(), resume, prog, comm.get());
     }
     return py::make_tuple(to_np(r.alpha), result_dict(r));
   }, py::arg("x"), py::arg("y"), py::arg("params"), py::arg("device") = 0, py::arg("resume") = nullptr,
-     py::arg("progress") = py::none());
-  m.def("shrink_auto", [](const SolverParams& p, int64_t n, int d, int device) { return shrink_auto(p, n, d, device); },
-        py::arg("params"), py::arg("n"), py::arg("d"), py::arg("device") = 0,
-        "shrink='auto': shrinking phases where they pay (one GPU, working-set rounds, Gram not resident)");
+     py::arg("progress") = py::none(), py::arg("comm") = nullptr);
+  m.def("shrink_auto", [](const SolverParams& p, int64_t n, int d, int device, std::shared_ptr<Communicator> comm) {
+          py::gil_scoped_release rel;
+          return shrink_auto(p, n, d, device, comm.get());
+        }, py::arg("params"), py::arg("n"), py::arg("d"), py::arg("device") = 0, py::arg("comm") = nullptr,
+        "shrink='auto': shrinking phases where they pay (working-set rounds, the whole Gram not resident on "
+        "one device; agreed over comm)");
 
   py::class_<GpuSolver, std::shared_ptr<GpuSolver>>(m, "GpuSolver")
       .def(py::init([](const SolverParams& p, std::shared_ptr<Communicator> comm, int device) {

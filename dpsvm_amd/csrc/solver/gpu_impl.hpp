@@ -179,6 +179,7 @@ struct GpuSolver::Impl {
 
   // ---- gpu_solve.hip ----
   void snapshot(const SmoStatus& st);
+  std::vector<float> gather_f();
 };
 
 namespace gpu {

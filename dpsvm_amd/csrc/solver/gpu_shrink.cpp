@@ -1,4 +1,5 @@
-// Shrinking for the device solver (one GPU), as problem reduction.
+// Shrinking for the device solver, as problem reduction (one GPU, or every
+// rank of a communicator running the same phases on its share).
 //
 // LIBSVM's shrinking heuristic in the reference's f-notation (f_j = sum_i
 // alpha_i y_i K(i, j) - y_j, b_hi = min f over I_up, b_lo = max f over I_low;
@@ -23,6 +24,12 @@
 // is evaluated on the whole problem.  Phase 0 solves the whole problem to a
 // loose tolerance; the last phase, if the shrunk ones keep failing the global
 // test, solves the whole problem to eps.
+//
+// With a communicator (world > 1, X replicated): every rank runs this host
+// loop on identical state.  A phase is one multi-rank GpuSolver (rows sharded
+// or replicated by the dp policy), its gradient all-gathered; the inactive
+// rows' update is split over the ranks (each predicts its slice of them) and
+// all-gathered, so every rank continues from the same bits.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -77,6 +84,55 @@ std::vector<float> gather_rows(const float* x, int d, const std::vector<int64_t>
 
 double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
+// MIN over ranks of a flag (every rank must call)
+bool comm_all(Communicator* comm, bool mine) {
+  if (!comm || comm->size() == 1) return mine;
+  uint64_t v = mine ? 1ull : 0ull;
+  if (comm->device_memory()) {
+    uint64_t* d = nullptr;
+    hipStream_t st = nullptr;
+    HIP_CHECK(hipStreamCreate(&st));
+    HIP_CHECK(hipMalloc((void**)&d, 8));
+    HIP_CHECK(hipMemcpy(d, &v, 8, hipMemcpyHostToDevice));
+    comm->allreduce_min_u64(d, 1, st);
+    HIP_CHECK(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    (void)hipFree(d);
+    (void)hipStreamDestroy(st);
+  } else {
+    comm->allreduce_min_u64(&v, 1, nullptr);
+  }
+  return v == 1ull;
+}
+
+// every rank's slice shard_of(n, r, world) of a length-n vector, all-gathered
+// into `out` (each rank filled only its own slice)
+void comm_allgather_slices(Communicator* comm, std::vector<float>& out) {
+  const int world = comm->size(), rank = comm->rank();
+  const int64_t n = (int64_t)out.size(), ld = (n + world - 1) / world;
+  const Shard me = shard_of(n, rank, world);
+  std::vector<float> loc((size_t)ld, 0.f), all((size_t)ld * world);
+  std::copy(out.begin() + me.offset, out.begin() + me.offset + me.size, loc.begin());
+  if (comm->device_memory()) {
+    float* gb = nullptr;
+    hipStream_t st = nullptr;
+    HIP_CHECK(hipStreamCreate(&st));
+    HIP_CHECK(hipMalloc((void**)&gb, (size_t)ld * world * 4));
+    HIP_CHECK(hipMemcpy(gb + (size_t)rank * ld, loc.data(), (size_t)ld * 4, hipMemcpyHostToDevice));
+    comm->allgather(gb + (size_t)rank * ld, gb, (size_t)ld * 4, st);
+    HIP_CHECK(hipMemcpyAsync(all.data(), gb, all.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    (void)hipFree(gb);
+    (void)hipStreamDestroy(st);
+  } else {
+    comm->allgather(loc.data(), all.data(), (size_t)ld * 4, nullptr);
+  }
+  for (int r = 0; r < world; ++r) {
+    const Shard s = shard_of(n, r, world);
+    std::copy(all.begin() + (size_t)r * ld, all.begin() + (size_t)r * ld + s.size, out.begin() + s.offset);
+  }
+}
+
 constexpr float kPhase0EpsScale = 50.f;   // phase 0: the whole problem to 50 eps
 constexpr double kShrinkMaxFrac = 0.6;    // shrink only if the active set is at most 60% of the rows
 constexpr int kMaxPhases = 8;             // then the whole problem to eps
@@ -84,8 +140,11 @@ constexpr int kMaxPhases = 8;             // then the whole problem to eps
 }  // namespace
 
 SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, int64_t n, int d, const float* y_in,
-                            const Checkpoint* resume, const ProgressFn& progress) {
+                            const Checkpoint* resume, const ProgressFn& progress, Communicator* comm) {
   DPSVM_CHECK(n >= 2 && d >= 1, "solve_shrinking: need at least 2 samples and 1 feature");
+  const int world = comm ? comm->size() : 1, rank = comm ? comm->rank() : 0;
+  DPSVM_CHECK(world == 1 || p0.x_mode != 2, "solve_shrinking: every rank holds X (x_mode partitioned is not supported)");
+  if (world == 1) comm = nullptr;
   const double t_start = now();
   SolverParams p = p0;
   p.checkpoint_every = 0;  // the phases' own solvers do not checkpoint: the whole problem's state is
@@ -119,7 +178,7 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     for (int64_t j = 0; j < n; ++j) f[j] = -y[j];
 
   SolveResult res;
-  res.world = 1;
+  res.world = world;
   int phases = 0;
   int64_t rounds = 0, rows_computed = 0;
   double t_gram = 0.0;
@@ -160,11 +219,12 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     if (have_f || phases > 0) ck.f = all ? f : fa;  // else recomputed from alpha by the solver
     std::vector<float> a_new, f_new;
     SolveResult r;
+    const double t_phase = now();
     {
-      GpuSolver s(sp, nullptr, device);
+      GpuSolver s(sp, comm, device);
       s.setup(xp, na, na, d, all ? y.data() : ya.data());
       r = s.solve((phases == 0 && !resume) ? nullptr : &ck, progress);
-      f_new = s.gradient();
+      f_new = s.gradient_all();
     }  // the phase's device memory is released before the next phase
     ++phases;
     iters = r.iters;
@@ -194,10 +254,18 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
       for (int64_t j = 0; j < n; ++j)
         if (!is_act[j]) inact.push_back(j);
       if (!changed.empty() && !inact.empty()) {
-        dm.x = gather_rows(x, d, changed);
-        const std::vector<float> xi = gather_rows(x, d, inact);
-        GpuPredictor pr(dm, device);
-        const std::vector<float> df = pr.decision(xi.data(), (int64_t)inact.size(), d);
+        // this rank's slice of the inactive rows (all of them at world 1)
+        std::vector<float> df((size_t)inact.size(), 0.f);
+        const Shard sl = shard_of((int64_t)inact.size(), rank, world);
+        if (sl.size > 0) {
+          dm.x = gather_rows(x, d, changed);
+          const std::vector<int64_t> mine(inact.begin() + sl.offset, inact.begin() + sl.offset + sl.size);
+          const std::vector<float> xi = gather_rows(x, d, mine);
+          GpuPredictor pr(dm, device);
+          const std::vector<float> dfl = pr.decision(xi.data(), sl.size, d);
+          std::copy(dfl.begin(), dfl.end(), df.begin() + sl.offset);
+        }
+        if (comm) comm_allgather_slices(comm, df);
         for (size_t k = 0; k < inact.size(); ++k) f[inact[k]] += df[k];
       }
       for (int64_t k = 0; k < na; ++k) {
@@ -208,7 +276,7 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     const Extremes e = extremes(f, alpha, y.data(), C);
     res.b_hi = e.b_hi;
     res.b_lo = e.b_lo;
-    if (!p0.checkpoint_path.empty()) {
+    if (!p0.checkpoint_path.empty() && rank == 0) {
       // the whole problem after this phase (alpha, exact f): resumable by any
       // solver, with or without shrinking
       Checkpoint wck;
@@ -226,9 +294,12 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
       write_checkpoint(p0.checkpoint_path, wck);
     }
     const bool open = e.ok && gap_open(e.b_hi, e.b_lo, p.eps);
-    if (p.verbose)
-      fprintf(stderr, "[dpsvm] shrink phase %d: %lld active rows, %lld pair steps, global gap %g (status %d)\n",
-              phases, (long long)na, (long long)iters, (double)(e.b_lo - e.b_hi), r.status);
+    if (p.verbose && rank == 0)
+      fprintf(stderr,
+              "[dpsvm] shrink phase %d: %lld active rows, %lld rounds, %lld pair steps, %.3f s (solve %.3f s), "
+              "global gap %g (status %d)\n",
+              phases, (long long)na, (long long)r.outer, (long long)iters, now() - t_phase, r.t_solve,
+              (double)(e.b_lo - e.b_hi), r.status);
     if (!e.ok) {
       res.status = kNoPair;
       break;
@@ -266,11 +337,15 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   return res;
 }
 
-bool shrink_auto(const SolverParams& p, int64_t n, int d, int device) {
+bool shrink_auto(const SolverParams& p, int64_t n, int d, int device, Communicator* comm) {
   (void)d;
   if (p.solver == 1) return false;                       // solver=smo: the reference's trajectory
   if (p.solver == 0 && n < kWsAutoRows) return false;    // auto below 50k rows: the pair engines
   if (p.force_cache) return false;                     // an explicit engine request (tests, probes)
+  if (comm && comm->size() > 1) {
+    if (p.x_mode == 2) return false;                     // the phases need X on every rank
+    return !comm_all(comm, !shrink_auto(p, n, d, device, nullptr));  // any rank short of memory: shrink
+  }
   HIP_CHECK(hipSetDevice(device));
   size_t freeb = 0, totalb = 0;
   HIP_CHECK(hipMemGetInfo(&freeb, &totalb));

@@ -43,6 +43,13 @@ void GpuSolver::Impl::snapshot(const SmoStatus& st) {
       ck.alpha[q.i_hi] = q.a_hi;
     }
   }
+  ck.f = gather_f();
+  // replicated solve: every rank holds everything, the caller's rank 0 writes
+  if (rank == 0 && outer_rank == 0) write_checkpoint(p.checkpoint_path, ck);
+}
+
+// every rank: the whole gradient (the solve's f shards all-gathered)
+std::vector<float> GpuSolver::Impl::gather_f() {
   std::vector<float> floc((size_t)ldl, 0.f), fall((size_t)ldl * world);
   HIP_CHECK(hipMemcpy(floc.data(), f, nl * 4, hipMemcpyDeviceToHost));
   if (world > 1) {
@@ -60,13 +67,17 @@ void GpuSolver::Impl::snapshot(const SmoStatus& st) {
   } else {
     fall = floc;
   }
-  ck.f.assign((size_t)n, 0.f);
+  std::vector<float> out((size_t)n, 0.f);
   for (int r = 0; r < world; ++r) {
     Shard s = shard_of(n, r, world);
-    std::copy(fall.begin() + (size_t)r * ldl, fall.begin() + (size_t)r * ldl + s.size, ck.f.begin() + s.offset);
+    std::copy(fall.begin() + (size_t)r * ldl, fall.begin() + (size_t)r * ldl + s.size, out.begin() + s.offset);
   }
-  // replicated solve: every rank holds everything, the caller's rank 0 writes
-  if (rank == 0 && outer_rank == 0) write_checkpoint(p.checkpoint_path, ck);
+  return out;
+}
+
+std::vector<float> GpuSolver::gradient_all() {
+  HIP_CHECK(hipSetDevice(impl_->device));
+  return impl_->gather_f();
 }
 
 SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progress) {

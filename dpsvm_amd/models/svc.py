@@ -256,9 +256,10 @@ class SVC:
             return s.astype(np.float32)
         return np.where(s > 0, self.classes_[-1], self.classes_[0])
 
-    def _use_shrink(self, p, n: int, d: int, dev: int) -> bool:
+    def _use_shrink(self, p, n: int, d: int, dev: int, comm=None) -> bool:
+        """collective at world > 1 (every rank calls; agreed)"""
         mode = self.config.shrink_mode()
-        return mode == "on" or (mode == "auto" and bool(load().shrink_auto(p, n, d, dev)))
+        return mode == "on" or (mode == "auto" and bool(load().shrink_auto(p, n, d, dev, comm)))
 
     # ------------------------------------------------------------------ fit
     def fit(self, X, y, comm=None, resume=None, progress: Optional[Callable] = None,
@@ -283,8 +284,8 @@ class SVC:
         kind, dev = cfg.device_kind()
         self.device_ = f"{kind}:{dev}" if kind == "cuda" else "cpu"
         t0 = time.perf_counter()
-        if kind == "cuda" and comm is None and rank_rows is None and self._use_shrink(p, n, d, dev):
-            alpha, info = C.solve_shrinking(X, ys, p, dev, ck, progress)
+        if kind == "cuda" and rank_rows is None and self._use_shrink(p, n, d, dev, comm):
+            alpha, info = C.solve_shrinking(X, ys, p, dev, ck, progress, comm)
             self.setup_info_ = {"iteration": "ws+shrinking", "device_name": C.device_name(dev), "n_local": n,
                                 "x_replicated": True, "engine_note": f"{info['shrink_phases']} shrinking phases"}
             self._solver = None

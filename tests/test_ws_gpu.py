@@ -615,8 +615,8 @@ def test_shrinking_reaches_the_stop_test_on_the_whole_problem(clip):
     X, y = synthetic("covtype", n=30000, seed=8)
     C_, g = 64.0, 0.25
     kw = dict(C=C_, gamma=g, eps=1e-3, clip=clip, device="cuda", solver="ws", max_iter=5_000_000)
-    full = SVC(**kw).fit(X, y)
-    shr = SVC(shrink=True, **kw).fit(X, y)
+    full = SVC(shrink="off", **kw).fit(X, y)
+    shr = SVC(shrink="on", **kw).fit(X, y)
     assert shr.setup_info_["iteration"] == "ws+shrinking" and shr.stats_["shrink_phases"] >= 2
     assert full.converged_, (full.status_, full.n_iter_, full.stats_)
     assert shr.converged_, (shr.status_, shr.n_iter_, shr.stats_)
@@ -628,3 +628,28 @@ def test_shrinking_reaches_the_stop_test_on_the_whole_problem(clip):
     if clip == "box":
         assert abs(shr.b_ - full.b_) < 2e-2
         assert abs(shr.n_support_ - full.n_support_) <= max(5, full.n_support_ // 50)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shrinking_multi_rank(world):
+    """Shrinking phases over a communicator (ranks as threads sharing the GPU):
+    each phase is a rows-sharded multi-rank solve, the inactive rows' update is
+    split over the ranks and all-gathered — every rank ends on the same alpha
+    bits, at the one-rank optimum (box clipping: unique), through the same
+    number of phases' stop tests on the whole problem."""
+    from dpsvm_amd._native import load
+
+    X, y = synthetic("covtype", n=20000, seed=8)
+    C_, g = 64.0, 0.25
+    kw = dict(C=C_, gamma=g, eps=1e-3, clip="box", device="cuda", solver="ws", shrink="on", dp="shard",
+              max_iter=5_000_000)
+    one = SVC(**kw).fit(X, y)
+    outs = _fit_threads(load(), world, X, y, **kw)
+    for o in outs:
+        assert o.setup_info_["iteration"] == "ws+shrinking" and o.converged_
+        assert np.array_equal(o.alpha_, outs[0].alpha_) and o.b_ == outs[0].b_
+        assert o.stats_["shrink_phases"] >= 2 and o.stats_["world"] == world
+    assert one.converged_
+    assert abs(outs[0].b_ - one.b_) < 2e-2
+    assert abs(outs[0].n_support_ - one.n_support_) <= max(5, one.n_support_ // 50)
+    assert _kkt_gap(X, y, outs[0].alpha_, C_, g) < 2e-3 + 5e-4
