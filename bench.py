@@ -491,7 +491,8 @@ def main(argv=None) -> int:
             "poll_batch": info.get("poll_batch", 0),
             "census": info.get("census", "n/a"),
             "engine_note": info.get("engine_note", ""),
-            "shrink": {"mode": a.shrink, "on": bool(use_shrink), "phases": int(res.get("shrink_phases", 0))},
+            "shrink": {"mode": a.shrink, "on": bool(use_shrink), "phases": int(res.get("shrink_phases", 0)),
+                       "phase_log": res.get("phase_log", "")},
             "shard_check": shard_check,
             "dp_autotune": dp_choice,
             "reference_check": ref_check,

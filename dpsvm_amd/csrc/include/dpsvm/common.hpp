@@ -168,6 +168,8 @@ struct SolveResult {
   int ws_blocks = 1, ws_blocks_end = 1;
   int64_t ws_p1_round = 0, ws_damped = 0;
   int shrink_phases = 0;       // solve_shrinking: device solves on the (active) rows
+  // solve_shrinking: one entry per phase, "rows engine/dp_policy exchange rounds seconds" (';'-separated)
+  std::string phase_log;
   bool converged() const { return status == 1; }
 };
 

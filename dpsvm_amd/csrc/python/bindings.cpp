@@ -123,6 +123,7 @@ py::dict result_dict(const SolveResult& r) {
   d["ws_p1_round"] = r.ws_p1_round;
   d["ws_damped"] = r.ws_damped;
   d["shrink_phases"] = r.shrink_phases;
+  d["phase_log"] = r.phase_log;
   d["host_cache_lines"] = r.host_cache_lines;
   d["cache_lines"] = r.cache_lines;
   d["world"] = r.world;

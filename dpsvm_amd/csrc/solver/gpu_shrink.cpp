@@ -220,13 +220,21 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     std::vector<float> a_new, f_new;
     SolveResult r;
     const double t_phase = now();
+    std::string phase_engine;
     {
       GpuSolver s(sp, comm, device);
-      s.setup(xp, na, na, d, all ? y.data() : ya.data());
+      const GpuSetupInfo si = s.setup(xp, na, na, d, all ? y.data() : ya.data());
+      phase_engine = si.iteration + "/" + (world > 1 ? si.dp_policy : std::string("local")) +
+                     (world > 1 ? " " + si.exchange : std::string());
       r = s.solve((phases == 0 && !resume) ? nullptr : &ck, progress);
       f_new = s.gradient_all();
     }  // the phase's device memory is released before the next phase
     ++phases;
+    {
+      char buf[64];
+      snprintf(buf, sizeof(buf), " %lld %.3f", (long long)r.outer, now() - t_phase);
+      res.phase_log += (res.phase_log.empty() ? "" : ";") + std::to_string(na) + " " + phase_engine + buf;
+    }
     iters = r.iters;
     rounds += r.outer;
     rows_computed += r.rows_computed;
