@@ -293,12 +293,15 @@ def main(argv=None) -> int:
     use_shrink = on_gpu and (a.shrink == "on" or (
         a.shrink == "auto" and C.shrink_auto(params, X.shape[0], X.shape[1], ctx.local_rank, sh_comm)))
     if use_shrink:
-        # shrinking phases: every phase sets its (multi-rank) solver up inside the timed run
+        # shrinking phases: the whole-problem solver is set up here, untimed, as the
+        # plain solver is (X upload, cache sizing); every shrunk phase sets its
+        # (multi-rank) solver up inside the timed run
         solver = None
-        info = {"device_name": C.device_name(ctx.local_rank), "x_replicated": True, "iteration": "ws+shrinking",
-                "dp_policy": f"per phase ({a.dp})" if n_ranks > 1 else "none"}
-        run = lambda: C.solve_shrinking(X, y, params, ctx.local_rank, None,  # noqa: E731
-                                        progress if (a.log_every and ctx.rank == 0) else None, sh_comm)
+        shr = C.ShrinkingSolver(params, sh_comm, ctx.local_rank)
+        info = shr.setup(X, y)
+        if n_ranks > 1:
+            info["dp_policy"] = f"per phase ({a.dp}; whole problem: {info['dp_policy']})"
+        run = lambda: shr.solve(None, progress if (a.log_every and ctx.rank == 0) else None)  # noqa: E731
     elif on_gpu:
         solver = C.GpuSolver(params, comm, ctx.local_rank)
         info = solver.setup(X, X.shape[0], y)
@@ -492,6 +495,7 @@ def main(argv=None) -> int:
             "census": info.get("census", "n/a"),
             "engine_note": info.get("engine_note", ""),
             "shrink": {"mode": a.shrink, "on": bool(use_shrink), "phases": int(res.get("shrink_phases", 0)),
+                       "whole_problem_engine": info.get("phase0_engine"),
                        "phase_log": res.get("phase_log", "")},
             "shard_check": shard_check,
             "dp_autotune": dp_choice,

@@ -71,6 +71,8 @@ def main() -> int:
                              "dedup_compaction": us(s[:, 13] - s[:, 12]), "previous_union": us(s[:, 14] - s[:, 13]),
                              "block_assignment": us(s[:, 2] - s[:, 14])}),
         "gather_rows_us": us(s[:, 8] - s[:, 2]),
+        **({"merged_to_gather_entry_us": us(s[:, 9] - s[:, 2]), "gather_kernel_us": us(s[:, 8] - s[:, 9])}
+           if (s[:, 9] > 0).all() else {}),
         "gather_end_to_solve_us": us(s[:, 0] - s[:, 8]),
         "load_subgram_us": us(s[:, 3] - s[:, 0]),
         "solve_us": us(s[:, 4] - s[:, 3]),

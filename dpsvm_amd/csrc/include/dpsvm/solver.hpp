@@ -99,6 +99,8 @@ class GpuSolver {
   // after solve(): the whole gradient on every rank (the shards all-gathered;
   // a collective at world > 1)
   std::vector<float> gradient_all();
+  // the stop tolerance of the next solve() (kernel arguments updated, captured graphs rebuilt)
+  void set_eps(float eps);
   const GpuSetupInfo& info() const;
   struct Impl;
 
@@ -118,6 +120,22 @@ SolveResult solve_shrinking(const SolverParams& p, int device, const float* x, i
                             const Checkpoint* resume = nullptr, const ProgressFn& progress = {},
                             Communicator* comm = nullptr);
 
+// The same, with the whole-problem solver set up once (X upload, cache or Gram
+// sizing: the setup a plain solve does before its timed region) and kept for
+// every whole-problem phase and every solve(); the shrunk phases' solvers use
+// the memory it leaves (cache_frac).  x, y (host) must outlive the object.
+class ShrinkingSolver {
+ public:
+  ShrinkingSolver(const SolverParams& p, Communicator* comm, int device);
+  ~ShrinkingSolver();
+  GpuSetupInfo setup(const float* x, int64_t n, int d, const float* y);
+  SolveResult solve(const Checkpoint* resume = nullptr, const ProgressFn& progress = {});
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+};
+
 // shrink="auto" (library, svmTrain and bench default): shrinking phases where
 // they pay — one GPU, working-set rounds, and a Gram that does not fit the
 // device's cache budget (the ws-cache regime: covtype-shape 581k x 54).  On a
@@ -129,7 +147,8 @@ bool shrink_auto(const SolverParams& p, int64_t n, int d, int device, Communicat
 // decision values of a host or device matrix via the MFMA predict kernel.
 class GpuPredictor {
  public:
-  GpuPredictor(const Model& m, int device);
+  // precision: 0 auto (split-operand GEMM from 128 padded features), 1 f32-input MFMA, 2 split-operand
+  GpuPredictor(const Model& m, int device, int precision = 0);
   ~GpuPredictor();
   std::vector<float> decision(const float* x_host, int64_t n, int d);
   // device pointers, stream = hipStream_t as void*

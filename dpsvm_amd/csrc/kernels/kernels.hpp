@@ -138,10 +138,11 @@ void rbf_predict_split(const float* A, const float* Asq, int64_t M, int lda, con
                        int max_splits, hipStream_t s);
 // which decision GEMM rbf_predict runs for this dp: the split-operand one (dp >= 128) or the f32 one
 bool predict_uses_split(int dp);
+// precision: 0 auto (predict_uses_split), 1 the f32-input MFMA GEMM, 2 the split-operand GEMM (any dp)
 void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                  const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
                  float b, float* partial, float* dec, const float* y, int32_t* correct,
-                 hipStream_t s);
+                 hipStream_t s, int precision = 0);
 
 // SV compaction: idx_out[k] = i for the k-th alpha[i] > 0 (index order)
 // scratch: >= compact_scratch_ints(n) ints; count written to *count_dev

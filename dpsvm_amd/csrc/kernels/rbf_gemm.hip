@@ -368,7 +368,7 @@ bool predict_uses_split(int dp) {
 void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const float* B,
                  const float* Bsq, const float* coef, int64_t N, int ldb, int dp, float gamma,
                  float b, float* partial, float* dec, const float* y, int32_t* correct,
-                 hipStream_t s) {
+                 hipStream_t s, int precision) {
   if (M <= 0) return;
   DPSVM_CHECK(dp % 16 == 0, "rbf_predict: dp must be a multiple of 16");
   const int64_t ldp = round_up(M, dev::BM);
@@ -378,7 +378,7 @@ void rbf_predict(const float* A, const float* Asq, int64_t M, int lda, const flo
     splits = predict_splits(M, N);
     const int per = (int)((tn + splits - 1) / splits);
     splits = (int)((tn + per - 1) / per);
-    if (predict_uses_split(dp)) {
+    if (precision == 2 || (precision == 0 && predict_uses_split(dp))) {
       // split-operand fp16 MFMA with LDS-DMA staging (fp32 accuracy, rbf_gemm_split.hip)
       rbf_predict_split(A, Asq, M, lda, B, Bsq, coef, N, ldb, dp, gamma, partial, ldp, splits, s);
     } else {

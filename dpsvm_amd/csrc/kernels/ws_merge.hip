@@ -872,6 +872,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArg
   WsCtrl* c = a.ctrl;
   if (c->done != kRunning) return;
   const int tid = threadIdx.x;
+  if (tid == 0 && blockIdx.x == 0) WS_STAMP(9);  // after ws-cache's miss-row GEMM (stamps 2 -> 9)
   const int par = (int)(c->outer & 1);
   const int p = (int)blockIdx.x / a.q_max, ra = (int)blockIdx.x % a.q_max;
   const int q = c->qb[par][p];

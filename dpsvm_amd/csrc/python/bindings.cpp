@@ -130,6 +130,35 @@ py::dict result_dict(const SolveResult& r) {
   return d;
 }
 
+py::dict setup_dict(const GpuSetupInfo& i) {
+  py::dict d;
+  d["device"] = i.device;
+  d["device_name"] = i.device_name;
+  d["n"] = i.n;
+  d["n_local"] = i.n_local;
+  d["offset"] = i.offset;
+  d["d"] = i.d;
+  d["dp"] = i.dp;
+  d["x_replicated"] = i.x_replicated;
+  d["iteration"] = i.iteration;
+  d["exchange"] = i.exchange;
+  d["exchange_mem"] = i.exchange_mem;
+  d["cache_lines"] = i.cache_lines;
+  d["blocks"] = i.blocks;
+  d["bytes_device"] = i.bytes_device;
+  d["dp_policy"] = i.dp_policy;
+  d["rows_per_group"] = i.rows_per_group;
+  d["groups"] = i.groups;
+  d["poll_batch"] = i.poll_batch;
+  d["cus"] = i.cus;
+  d["blocks_per_cu"] = i.blocks_per_cu;
+  d["census"] = i.census;
+  d["engine_note"] = i.engine_note;
+  d["ws_wss"] = i.ws_wss;
+  d["gram"] = i.gram;
+  return d;
+}
+
 ProgressFn wrap_progress(py::object cb) {
   if (cb.is_none()) return {};
   py::function fn = cb;
@@ -399,32 +428,7 @@ PYBIND11_MODULE(_C, m) {
           py::gil_scoped_release r;
           i = s.setup(x.data(), x.shape(0), n, (int)x.shape(1), y.data());
         }
-        py::dict d;
-        d["device"] = i.device;
-        d["device_name"] = i.device_name;
-        d["n"] = i.n;
-        d["n_local"] = i.n_local;
-        d["offset"] = i.offset;
-        d["d"] = i.d;
-        d["dp"] = i.dp;
-        d["x_replicated"] = i.x_replicated;
-        d["iteration"] = i.iteration;
-        d["exchange"] = i.exchange;
-        d["exchange_mem"] = i.exchange_mem;
-        d["cache_lines"] = i.cache_lines;
-        d["blocks"] = i.blocks;
-        d["bytes_device"] = i.bytes_device;
-        d["dp_policy"] = i.dp_policy;
-        d["rows_per_group"] = i.rows_per_group;
-        d["groups"] = i.groups;
-        d["poll_batch"] = i.poll_batch;
-        d["cus"] = i.cus;
-        d["blocks_per_cu"] = i.blocks_per_cu;
-        d["census"] = i.census;
-        d["engine_note"] = i.engine_note;
-        d["ws_wss"] = i.ws_wss;
-        d["gram"] = i.gram;
-        return d;
+        return setup_dict(i);
       })
       .def("solve", [](GpuSolver& s, const Checkpoint* resume, py::object progress) {
         auto prog = wrap_progress(progress);
@@ -454,8 +458,49 @@ PYBIND11_MODULE(_C, m) {
         return to_np(out);
       });
 
+  // shrinking phases with the whole-problem solver set up once (setup() outside
+  // a timed region, as GpuSolver's); keeps X / y and the communicator alive
+  struct PyShrink {
+    std::shared_ptr<Communicator> comm;
+    std::unique_ptr<ShrinkingSolver> s;
+    F32 x, y;
+  };
+  py::class_<PyShrink, std::shared_ptr<PyShrink>>(m, "ShrinkingSolver")
+      .def(py::init([](const SolverParams& p, std::shared_ptr<Communicator> comm, int device) {
+             auto h = std::make_shared<PyShrink>();
+             h->comm = comm;
+             h->s.reset(new ShrinkingSolver(p, comm.get(), device));
+             return h;
+           }),
+           py::arg("params"), py::arg("comm") = nullptr, py::arg("device") = 0)
+      .def("setup", [](PyShrink& h, F32 x, F32 y) {
+        int64_t n = 0;
+        int d = 0;
+        check_xy(x, y, n, d);
+        h.x = x;
+        h.y = y;
+        GpuSetupInfo i;
+        {
+          py::gil_scoped_release r;
+          i = h.s->setup(h.x.data(), n, d, h.y.data());
+        }
+        py::dict out = setup_dict(i);
+        out["phase0_engine"] = i.iteration;
+        out["iteration"] = "ws+shrinking";
+        return out;
+      }, py::arg("x"), py::arg("y"))
+      .def("solve", [](PyShrink& h, const Checkpoint* resume, py::object progress) {
+        auto prog = wrap_progress(progress);
+        SolveResult r;
+        {
+          py::gil_scoped_release rel;
+          r = h.s->solve(resume, prog);
+        }
+        return py::make_tuple(to_np(r.alpha), result_dict(r));
+      }, py::arg("resume") = nullptr, py::arg("progress") = py::none());
+
   py::class_<GpuPredictor, std::shared_ptr<GpuPredictor>>(m, "GpuPredictor")
-      .def(py::init<const Model&, int>(), py::arg("model"), py::arg("device") = 0)
+      .def(py::init<const Model&, int, int>(), py::arg("model"), py::arg("device") = 0, py::arg("precision") = 0)
       .def("decision", [](GpuPredictor& p, F32 x) {
         if (x.ndim() != 2) throw py::value_error("x must be 2-D");
         std::vector<float> out;

@@ -209,6 +209,7 @@ std::vector<float> GpuSolver::decision(const SolveResult& r, const float* xh, in
 struct GpuPredictor::Impl {
   int device = 0;
   int d = 0, dp = 0;
+  int precision = 0;  // launch::rbf_predict's: 0 auto, 1 f32, 2 split
   float gamma = 0.f, b = 0.f;
   int64_t nsv = 0;
   float *sv = nullptr, *svsq = nullptr, *coef = nullptr;
@@ -220,9 +221,11 @@ struct GpuPredictor::Impl {
   }
 };
 
-GpuPredictor::GpuPredictor(const Model& mdl, int device) : impl_(new Impl) {
+GpuPredictor::GpuPredictor(const Model& mdl, int device, int precision) : impl_(new Impl) {
   auto& m = *impl_;
+  DPSVM_CHECK(precision >= 0 && precision <= 2, "GpuPredictor: precision must be 0 (auto), 1 (f32) or 2 (split)");
   m.device = device;
+  m.precision = precision;
   HIP_CHECK(hipSetDevice(device));
   HIP_CHECK(hipStreamCreateWithFlags(&m.stream, hipStreamNonBlocking));
   m.d = std::max(1, mdl.d);
@@ -272,7 +275,7 @@ std::vector<float> GpuPredictor::decision(const float* xh, int64_t nt, int d) {
     HIP_CHECK(hipMemsetAsync(dsq, 0, cpad * 4, m.stream));
     launch::row_sqnorm(dx, rows, m.dp, m.dp, dsq, m.stream);
     launch::rbf_predict(dx, dsq, rows, m.dp, m.sv, m.svsq, m.coef, m.nsv, m.dp, m.dp, m.gamma, m.b, part, ddec,
-                        nullptr, nullptr, m.stream);
+                        nullptr, nullptr, m.stream, m.precision);
     HIP_CHECK(hipMemcpyAsync(out.data() + r0, ddec, rows * 4, hipMemcpyDeviceToHost, m.stream));
   }
   HIP_CHECK(hipStreamSynchronize(m.stream));
@@ -292,7 +295,7 @@ void GpuPredictor::decision_device(const float* x_dev, int64_t nt, int d, int ld
   HIP_CHECK(hipMemsetAsync(dsq, 0, pad * 4, s));
   launch::row_sqnorm(x_dev, nt, m.dp, ld, dsq, s);
   launch::rbf_predict(x_dev, dsq, nt, ld, m.sv, m.svsq, m.coef, m.nsv, m.dp, m.dp, m.gamma, m.b, part, out_dev,
-                      nullptr, nullptr, s);
+                      nullptr, nullptr, s, m.precision);
   HIP_CHECK(hipStreamSynchronize(s));
   (void)hipFree(dsq);
   (void)hipFree(part);

@@ -110,6 +110,25 @@ GpuSolver::GpuSolver(const SolverParams& p, Communicator* comm, int device) : im
 }
 
 GpuSolver::~GpuSolver() = default;
+
+void GpuSolver::set_eps(float eps) {
+  auto& m = *impl_;
+  DPSVM_CHECK(eps > 0.f && std::isfinite(eps), "set_eps: eps must be > 0");
+  if (eps == m.p.eps) return;
+  HIP_CHECK(hipSetDevice(m.device));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  m.p.eps = eps;
+  m.args.eps = eps;
+  m.wsa.eps = eps;
+  m.wsa.eps_floor = m.p.ws_rel * eps;
+  // the captured graphs hold the old kernel arguments: recaptured by the next solve
+  if (m.gexec) (void)hipGraphExecDestroy(m.gexec);
+  if (m.graph) (void)hipGraphDestroy(m.graph);
+  if (m.gexec1) (void)hipGraphExecDestroy(m.gexec1);
+  if (m.graph1) (void)hipGraphDestroy(m.graph1);
+  m.gexec = m.gexec1 = nullptr;
+  m.graph = m.graph1 = nullptr;
+}
 const GpuSetupInfo& GpuSolver::info() const { return impl_->info; }
 
 namespace {

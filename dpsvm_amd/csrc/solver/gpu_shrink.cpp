@@ -34,6 +34,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <memory>
 
 #include <hip/hip_runtime.h>
 
@@ -105,6 +106,43 @@ bool comm_all(Communicator* comm, bool mine) {
   return v == 1ull;
 }
 
+// This rank's slice of X resident on the device for the inactive rows' update
+// (uploaded once: no host gather of the inactive rows per phase), with the
+// decision buffer and a stream.
+struct XSlice {
+  int device = 0, dp = 0;
+  Shard s;
+  float* x = nullptr;
+  float* out = nullptr;
+  hipStream_t st = nullptr;
+  XSlice(const float* xh, int64_t n, int d, int dev, int rank, int world) : device(dev), dp(pad_features(d)) {
+    s = shard_of(n, rank, world);
+    HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const int64_t rows = (s.size + 127) / 128 * 128 + 128;  // whole 128-row tiles for the GEMM
+    HIP_CHECK(hipMalloc((void**)&x, (size_t)rows * dp * 4));
+    HIP_CHECK(hipMalloc((void**)&out, (size_t)rows * 4));
+    HIP_CHECK(hipMemsetAsync(x, 0, (size_t)rows * dp * 4, st));
+    if (s.size > 0)
+      HIP_CHECK(hipMemcpy2DAsync(x, (size_t)dp * 4, xh + (size_t)s.offset * d, (size_t)d * 4, (size_t)d * 4,
+                                 (size_t)s.size, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+  }
+  ~XSlice() {
+    (void)hipSetDevice(device);
+    if (x) (void)hipFree(x);
+    if (out) (void)hipFree(out);
+    if (st) (void)hipStreamDestroy(st);
+  }
+  // df[s.offset ..) = sum_i dm.alpha_i dm.y_i K(x_i, x_j) for this rank's rows j
+  void update(const Model& dm, int d, int precision, std::vector<float>& df) {
+    if (s.size == 0) return;
+    GpuPredictor pr(dm, device, precision);
+    pr.decision_device(x, s.size, d, dp, out, st);
+    HIP_CHECK(hipMemcpy(df.data() + s.offset, out, (size_t)s.size * 4, hipMemcpyDeviceToHost));
+  }
+};
+
 // every rank's slice shard_of(n, r, world) of a length-n vector, all-gathered
 // into `out` (each rank filled only its own slice)
 void comm_allgather_slices(Communicator* comm, std::vector<float>& out) {
@@ -139,29 +177,71 @@ constexpr int kMaxPhases = 8;             // then the whole problem to eps
 
 }  // namespace
 
-SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, int64_t n, int d, const float* y_in,
-                            const Checkpoint* resume, const ProgressFn& progress, Communicator* comm) {
-  DPSVM_CHECK(n >= 2 && d >= 1, "solve_shrinking: need at least 2 samples and 1 feature");
-  const int world = comm ? comm->size() : 1, rank = comm ? comm->rank() : 0;
-  DPSVM_CHECK(world == 1 || p0.x_mode != 2, "solve_shrinking: every rank holds X (x_mode partitioned is not supported)");
-  if (world == 1) comm = nullptr;
-  const double t_start = now();
-  SolverParams p = p0;
-  p.checkpoint_every = 0;  // the phases' own solvers do not checkpoint: the whole problem's state is
-                          // written after every phase instead (write_phase_checkpoint)
-  if (p.solver == 0) p.solver = 2;  // the phases are parts of a large problem: working-set rounds at any size
+struct ShrinkingSolver::Impl {
+  SolverParams p0, p;
+  Communicator* comm = nullptr;
+  int device = 0, world = 1, rank = 0;
+  const float* x = nullptr;
+  int64_t n = 0;
+  int d = 0;
+  float gamma = 0.f;
+  std::vector<float> y;
+  std::unique_ptr<GpuSolver> whole;  // every whole-problem phase (set up once)
+  GpuSetupInfo info;
+  std::unique_ptr<XSlice> xsl;  // this rank's X rows on the device, from the first shrunk phase on
+};
+
+ShrinkingSolver::ShrinkingSolver(const SolverParams& p0, Communicator* comm, int device) : impl_(new Impl) {
+  auto& m = *impl_;
+  m.world = comm ? comm->size() : 1;
+  m.rank = comm ? comm->rank() : 0;
+  DPSVM_CHECK(m.world == 1 || p0.x_mode != 2, "shrinking: every rank holds X (x_mode partitioned is not supported)");
+  m.comm = m.world > 1 ? comm : nullptr;
+  m.device = device;
+  m.p0 = p0;
+  m.p = p0;
+  m.p.checkpoint_every = 0;  // the phases' own solvers do not checkpoint: the whole problem's state is
+                             // written after every phase instead
+  if (m.p.solver == 0) m.p.solver = 2;  // the phases are parts of a large problem: working-set rounds at any size
   // the inactive rows' gradient comes from the predict GEMM: the phases' kernel
-  // values must be the ones it computes (f32 MFMA and split-operand values
-  // differ by ~1e-5, which C-sized alpha changes turn into gradient drift) —
-  // the split GEMMs when the predictor runs split (dp >= 128: 5x the f32 GEMM's
-  // speed for the phases' row GEMMs, which was round 3's 2x loss on
-  // synthetic-2m), the f32 MFMA otherwise
-  if (p.gram_precision == 0) p.gram_precision = launch::predict_uses_split((d + 15) / 16 * 16) ? 0 : 1;
-  const float gamma = resolve_gamma(p.gamma, d);
-  p.gamma = gamma;
+  // values must come from the same arithmetic (f32 MFMA and split-operand
+  // values differ by ~1e-5, which C-sized alpha changes turn into gradient
+  // drift) — auto: the split GEMMs for both (the working-set engines' default:
+  // round 3 ran the phases on the f32 GEMMs, 2x slower on synthetic-2m and
+  // 1.4x per round on covtype's miss rows)
+  if (m.p.gram_precision == 0) m.p.gram_precision = 2;
+}
+
+ShrinkingSolver::~ShrinkingSolver() = default;
+
+GpuSetupInfo ShrinkingSolver::setup(const float* x, int64_t n, int d, const float* y_in) {
+  auto& m = *impl_;
+  DPSVM_CHECK(n >= 2 && d >= 1, "shrinking: need at least 2 samples and 1 feature");
+  m.x = x;
+  m.n = n;
+  m.d = d;
+  m.gamma = resolve_gamma(m.p.gamma, d);
+  m.p.gamma = m.gamma;
+  m.y.resize((size_t)n);
+  for (int64_t j = 0; j < n; ++j) m.y[j] = y_in[j] > 0 ? 1.f : -1.f;
+  m.xsl.reset();
+  m.whole.reset();
+  m.whole.reset(new GpuSolver(m.p, m.comm, m.device));
+  m.info = m.whole->setup(x, n, n, d, m.y.data());
+  return m.info;
+}
+
+SolveResult ShrinkingSolver::solve(const Checkpoint* resume, const ProgressFn& progress) {
+  auto& m = *impl_;
+  DPSVM_CHECK(m.whole != nullptr, "ShrinkingSolver::solve before setup");
+  const SolverParams& p = m.p;
+  const int64_t n = m.n;
+  const int d = m.d, world = m.world, rank = m.rank;
+  const float* x = m.x;
+  const float gamma = m.gamma;
   const float C = p.C;
-  std::vector<float> y((size_t)n);
-  for (int64_t j = 0; j < n; ++j) y[j] = y_in[j] > 0 ? 1.f : -1.f;
+  const std::vector<float>& y = m.y;
+  const double t_start = now();
   std::vector<float> alpha((size_t)n, 0.f), f((size_t)n);
   int64_t iters = 0;
   bool have_f = false;
@@ -187,11 +267,9 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   while (true) {
     const bool all = act.empty() || (int64_t)act.size() == n;
     const int64_t na = all ? n : (int64_t)act.size();
-    SolverParams sp = p;
     // phase 0 (every row, the first time): a loose tolerance; later phases to eps
-    if (phases == 0 && !full_to_eps && (have_f || !resume)) sp.eps = p.eps * kPhase0EpsScale;
+    const float eps_ph = (phases == 0 && !full_to_eps && (have_f || !resume)) ? p.eps * kPhase0EpsScale : p.eps;
     std::vector<float> xa, ya, aa, fa;
-    const float* xp = x;
     if (!all) {
       xa = gather_rows(x, d, act);
       ya.resize((size_t)na);
@@ -202,7 +280,6 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
         aa[k] = alpha[act[k]];
         fa[k] = f[act[k]];
       }
-      xp = xa.data();
     }
     const Extremes e0 = extremes(all ? f : fa, all ? alpha : aa, all ? y.data() : ya.data(), C);
     Checkpoint ck;
@@ -210,25 +287,39 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     ck.d = d;
     ck.C = p.C;
     ck.gamma = gamma;
-    ck.eps = sp.eps;
+    ck.eps = eps_ph;
     ck.clip = (int)p.clip;
     ck.iter = iters;
     ck.b_hi = e0.b_hi;
     ck.b_lo = e0.b_lo;
     ck.alpha = all ? alpha : aa;
     if (have_f || phases > 0) ck.f = all ? f : fa;  // else recomputed from alpha by the solver
-    std::vector<float> a_new, f_new;
+    const Checkpoint* ckp = (phases == 0 && !resume) ? nullptr : &ck;
+    std::vector<float> f_new;
     SolveResult r;
     const double t_phase = now();
+    double t_set = 0.0, t_grad = 0.0;
     std::string phase_engine;
-    {
-      GpuSolver s(sp, comm, device);
-      const GpuSetupInfo si = s.setup(xp, na, na, d, all ? y.data() : ya.data());
-      phase_engine = si.iteration + "/" + (world > 1 ? si.dp_policy : std::string("local")) +
-                     (world > 1 ? " " + si.exchange : std::string());
-      r = s.solve((phases == 0 && !resume) ? nullptr : &ck, progress);
+    if (all) {
+      // the whole problem: the solver set up once (setup())
+      m.whole->set_eps(eps_ph);
+      r = m.whole->solve(ckp, progress);
+      const double tg = now();
+      f_new = m.whole->gradient_all();
+      t_grad = now() - tg;
+      phase_engine = m.info.iteration + "/" + (world > 1 ? m.info.dp_policy + " " + m.info.exchange : std::string("local"));
+    } else {
+      SolverParams sp = p;
+      sp.eps = eps_ph;
+      GpuSolver s(sp, m.comm, m.device);
+      const GpuSetupInfo si = s.setup(xa.data(), na, na, d, ya.data());
+      t_set = now() - t_phase;
+      phase_engine = si.iteration + "/" + (world > 1 ? si.dp_policy + " " + si.exchange : std::string("local"));
+      r = s.solve(ckp, progress);
+      const double tg = now();
       f_new = s.gradient_all();
-    }  // the phase's device memory is released before the next phase
+      t_grad = now() - tg;
+    }  // a shrunk phase's device memory is released before the next phase
     ++phases;
     {
       char buf[64];
@@ -239,11 +330,13 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
     rounds += r.outer;
     rows_computed += r.rows_computed;
     t_gram += r.t_gram;
+    double t_upd = 0.0;
     if (all) {
       alpha = r.alpha;
       f = f_new;
     } else {
       // the inactive rows' gradient: one predict GEMM over the phase's changes
+      const double tu = now();
       Model dm;
       dm.gamma = gamma;
       dm.b = 0.f;
@@ -257,34 +350,27 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
         }
       std::vector<char> is_act((size_t)n, 0);
       for (int64_t j : act) is_act[j] = 1;
-      std::vector<int64_t> inact;
-      inact.reserve((size_t)(n - na));
-      for (int64_t j = 0; j < n; ++j)
-        if (!is_act[j]) inact.push_back(j);
-      if (!changed.empty() && !inact.empty()) {
-        // this rank's slice of the inactive rows (all of them at world 1)
-        std::vector<float> df((size_t)inact.size(), 0.f);
-        const Shard sl = shard_of((int64_t)inact.size(), rank, world);
-        if (sl.size > 0) {
-          dm.x = gather_rows(x, d, changed);
-          const std::vector<int64_t> mine(inact.begin() + sl.offset, inact.begin() + sl.offset + sl.size);
-          const std::vector<float> xi = gather_rows(x, d, mine);
-          GpuPredictor pr(dm, device);
-          const std::vector<float> dfl = pr.decision(xi.data(), sl.size, d);
-          std::copy(dfl.begin(), dfl.end(), df.begin() + sl.offset);
-        }
-        if (comm) comm_allgather_slices(comm, df);
-        for (size_t k = 0; k < inact.size(); ++k) f[inact[k]] += df[k];
+      if (!changed.empty() && na < n) {
+        // the change's contribution at every row of this rank's slice of X
+        // (device-resident; the active rows' values are unused), all-gathered
+        if (!m.xsl) m.xsl.reset(new XSlice(x, n, d, m.device, rank, world));
+        dm.x = gather_rows(x, d, changed);
+        std::vector<float> df((size_t)n, 0.f);
+        m.xsl->update(dm, d, p.gram_precision, df);
+        if (m.comm) comm_allgather_slices(m.comm, df);
+        for (int64_t j = 0; j < n; ++j)
+          if (!is_act[j]) f[j] += df[j];
       }
       for (int64_t k = 0; k < na; ++k) {
         alpha[act[k]] = r.alpha[k];
         f[act[k]] = f_new[k];
       }
+      t_upd = now() - tu;
     }
     const Extremes e = extremes(f, alpha, y.data(), C);
     res.b_hi = e.b_hi;
     res.b_lo = e.b_lo;
-    if (!p0.checkpoint_path.empty() && rank == 0) {
+    if (!m.p0.checkpoint_path.empty() && rank == 0) {
       // the whole problem after this phase (alpha, exact f): resumable by any
       // solver, with or without shrinking
       Checkpoint wck;
@@ -299,15 +385,15 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
       wck.b_lo = e.b_lo;
       wck.alpha = alpha;
       wck.f = f;
-      write_checkpoint(p0.checkpoint_path, wck);
+      write_checkpoint(m.p0.checkpoint_path, wck);
     }
     const bool open = e.ok && gap_open(e.b_hi, e.b_lo, p.eps);
     if (p.verbose && rank == 0)
       fprintf(stderr,
-              "[dpsvm] shrink phase %d: %lld active rows, %lld rounds, %lld pair steps, %.3f s (solve %.3f s), "
-              "global gap %g (status %d)\n",
-              phases, (long long)na, (long long)r.outer, (long long)iters, now() - t_phase, r.t_solve,
-              (double)(e.b_lo - e.b_hi), r.status);
+              "[dpsvm] shrink phase %d: %lld active rows, %lld rounds, %lld pair steps, %.3f s (setup %.3f, "
+              "solve %.3f, gradient %.3f, inactive update %.3f s), global gap %g (status %d)\n",
+              phases, (long long)na, (long long)r.outer, (long long)iters, now() - t_phase, t_set, r.t_solve, t_grad,
+              t_upd, (double)(e.b_lo - e.b_hi), r.status);
     if (!e.ok) {
       res.status = kNoPair;
       break;
@@ -343,6 +429,13 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   res.t_solve = now() - t_start;
   res.shrink_phases = phases;
   return res;
+}
+
+SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, int64_t n, int d, const float* y_in,
+                            const Checkpoint* resume, const ProgressFn& progress, Communicator* comm) {
+  ShrinkingSolver s(p0, comm, device);
+  s.setup(x, n, d, y_in);
+  return s.solve(resume, progress);
 }
 
 bool shrink_auto(const SolverParams& p, int64_t n, int d, int device, Communicator* comm) {

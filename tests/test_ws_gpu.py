@@ -146,7 +146,7 @@ def test_production_engines_route_small_cache_problems_to_ws():
     capped cache) runs ws-cache, and solver=smo there is refused with the
     reason (the pair cache engines are quarantined behind engines=all)."""
     X, y = synthetic("covtype", n=6000, seed=2)
-    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda")
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", clip="box")  # box: one optimum for both engines
     dense = SVC(**kw).fit(X, y)
     assert dense.setup_info_["iteration"] == "persistent-dense"
     cap = SVC(force_cache=True, cache_lines=2000, **kw).fit(X, y)
