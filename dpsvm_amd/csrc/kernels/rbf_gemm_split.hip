@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "dpsvm/common.hpp"
 #include "device_util.hpp"
@@ -456,6 +457,271 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
         }
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA ROWS GEMM: a working-set round's cache misses (up to 192 indexed A
+// rows, a_rows[0 .. *m_dev)) against all of this rank's B rows, K written to
+// the misses' cache lines.  The register-staged ROWS kernel above waits for
+// each 32-k stage's loads before the next can start, so on synthetic-2m
+// (K = 1024, 2M B rows: the 8 GB split X panel per round) it ran at 2.3 TB/s of
+// B bytes and 3.5 ms per round (profiles/r4_big_inputs).  Here the operands of
+// a 192 x 128 tile go through three 32-k LDS buffers by global_load_lds_dwordx4
+// (40 KiB each; the row data after them in the same array), the next block's
+// DMA in flight while a block is multiplied; the waves are the ROWS kernel's
+// (6 x 2, 32 x 64 each) with its MFMA sequence and epilogue, so the rows are
+// bit-identical to it (and to the Gram kernels').  Ten waves issue the DMA: 40
+// wave instructions of 8 rows x 128 B per block, 4 per wave.
+// ---------------------------------------------------------------------------
+constexpr int kRowsGldsThreads = 768;
+__global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
+    const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
+    const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb, float gamma,
+    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
+  constexpr int WN = 2, TM = 192, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
+  constexpr int DMA_WAVES = ROWS / 32;  // 10: each fills 32 rows (4 instructions of 8 rows)
+  int64_t tx, ty;
+  xcd_tile(tx, ty);
+  const int M = *m_dev;
+  if (tx * TM >= M) return;  // uniform: no barrier reached
+  __shared__ u4 lds[NB * BUF + (3 * TM + 2 * TN) / 4];
+  float* s_asq = (float*)(lds + NB * BUF);
+  int32_t* s_ash = (int32_t*)(s_asq + TM);
+  int32_t* s_orow = s_ash + TM;
+  float* s_bsq = (float*)(s_orow + TM);
+  int32_t* s_bsh = (int32_t*)(s_bsq + TN);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t m0 = tx * TM, n0 = ty * TN;
+  const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
+  if (tid < TM) {
+    const int64_t row = m0 + tid;
+    const int64_t ar = a_rows[min(row, (int64_t)M - 1)];
+    s_asq[tid] = Asq[ar];
+    s_ash[tid] = Ash[ar];
+    s_orow[tid] = row < M ? out_rows[row] : -1;
+  } else if (tid < TM + TN) {
+    const int64_t cc = min(n0 + (tid - TM), N - 1);
+    s_bsq[tid - TM] = Bsq[cc];
+    s_bsh[tid - TM] = Bsh[cc];
+  }
+  // DMA sources: wave w < 10 fills stage rows 32 w + 8 i + (lane >> 3); lane
+  // position p = lane & 7 takes global chunk p ^ ((row >> 1) & 7) (the read
+  // swizzle); A rows past M re-read a valid row (never stored)
+  const u4* src[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = min(32 * wave + 8 * i + (lane >> 3), ROWS - 1);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t grow = r < TM ? (int64_t)a_rows[min(m0 + r, (int64_t)M - 1)] : n0 + (r - TM);
+    src[i] = (r < TM ? A : B) + grow * rstride + c;
+  }
+  const bool dma_wave = wave < DMA_WAVES;
+  auto dma = [&](int kb) {
+    u4* dst = lds + (kb % NB) * BUF + 32 * wave * CPR;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
+                                       (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+  };
+  __syncthreads();  // row data written (no DMA in flight yet)
+  if (dma_wave) {
+    dma(0);
+    if (nkb > 1) dma(1);
+  }
+
+  f16v H[2], P[2], Q[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  const bool live = m0 + wm * 32 < M;  // a wave whose rows all lie past M only stages
+  for (int kb = 0; kb < nkb; ++kb) {
+    // retire block kb's DMA (block kb + 1 may stay in flight)
+    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (dma_wave && kb + 2 < nkb) dma(kb + 2);  // into the buffer of block kb - 1 (every wave is past it)
+    if (live) {
+      const u4* buf = lds + (kb % NB) * BUF;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+        const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
+        const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
+        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+        const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
+        const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
+        H[0] = mfma32_f16(ah, bh0, H[0]);
+        H[1] = mfma32_f16(ah, bh1, H[1]);
+        P[0] = mfma32_f16(ah, bl0, P[0]);
+        P[1] = mfma32_f16(ah, bl1, P[1]);
+        Q[0] = mfma32_f16(al, bh0, Q[0]);
+        Q[1] = mfma32_f16(al, bh1, Q[1]);
+      }
+    }
+  }
+  if (!live) return;
+
+  // ---- epilogue (the ROWS kernel's): K = exp(-g max(|a|^2 + |b|^2 - 2 dot, 0)) ----
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cb = wn * 64 + 32 * j + (lane & 31);
+    const float bsq = s_bsq[cb];
+    const int bsh = s_bsh[cb];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
+      H[j][r] = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+    }
+  }
+  const bool interior = n0 + TN <= N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int32_t orow = s_orow[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (orow >= 0 && (interior || col < N)) out[(int64_t)orow * ldo + col] = H[j][r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent small-K ROWS GEMM (nkb <= 2 k blocks: d <= 64, covtype's 54
+// features).  There a tile is two k blocks of MFMA work against 24-98 KiB of
+// operand and store traffic, so a tile-per-workgroup grid is a chain of
+// latencies (load, multiply, store) per tile.  Here one 768-thread workgroup
+// per CU walks the 192 x 64 tiles of its grid stride: the 192 A rows of its
+// tile row (<= 48 KiB) are staged into LDS once, the B column tiles (64 rows,
+// and their |x|^2 / shifts) stream through two LDS buffers by LDS-DMA, the next
+// tile's DMA issued before this tile's multiply, so its latency hides under
+// the multiply, the epilogue and the stores.  MFMA sequence and epilogue as
+// the ROWS kernels: bit-identical rows.
+// ---------------------------------------------------------------------------
+constexpr int kRowsPersistThreads = 768;
+template <int NKB>
+__global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
+    const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
+    const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, float gamma,
+    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
+  // 12 waves of 32 x 32 (one MFMA tile, three accumulators): a 192 x 64 tile
+  constexpr int WN = 2, TM = 192, TN = 64, CPR = 8;
+  constexpr int ABUF = TM * NKB * CPR, BBUF = TN * NKB * CPR;  // u4
+  const int M = *m_dev;
+  const int tn = (int)((N + TN - 1) / TN), tm = (M + TM - 1) / TM, total = tm * tn;
+  int L = blockIdx.x;
+  if (L >= total) return;  // uniform
+  __shared__ u4 lds[ABUF + 2 * BBUF + (2 * 2 * TN) / 4 + (3 * TM) / 4];
+  u4* s_a = lds;
+  u4* s_b = lds + ABUF;                                   // [2][NKB * TN rows][CPR]
+  float* s_bsq = (float*)(lds + ABUF + 2 * BBUF);         // [2][TN], then s_bsh [2][TN]
+  int32_t* s_bsh = (int32_t*)(s_bsq + 2 * TN);
+  float* s_asq = (float*)(s_bsh + 2 * TN);
+  int32_t* s_ash = (int32_t*)(s_asq + TM);
+  int32_t* s_orow = s_ash + TM;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  constexpr int64_t rstride = (int64_t)NKB * 8;
+  constexpr int BWAVES = TN * NKB / 32;  // waves 0 .. BWAVES - 1: the B rows (32 k-rows each); wave 10: |x|^2, shifts
+  // B DMA of column tile ty into buffer b
+  auto dma = [&](int ty, int b) {
+    const int64_t n0 = (int64_t)ty * TN;
+    if (wave < BWAVES) {
+      u4* dst = s_b + b * BBUF + 32 * wave * CPR;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 32 * wave + 8 * i + (lane >> 3), kb = q / TN, r = q % TN;
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        __builtin_amdgcn_global_load_lds((const void*)(B + (n0 + r) * rstride + kb * 8 + c),
+                                         (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+      }
+    } else if (wave == 10) {
+      const int64_t cc = min(n0 + lane, N - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Bsq + cc),
+                                       (__attribute__((address_space(3))) void*)(s_bsq + b * TN), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Bsh + cc),
+                                       (__attribute__((address_space(3))) void*)(s_bsh + b * TN), 4, 0, 0);
+    }
+  };
+  dma(L % tn, 0);
+  int ltx = -1, buf = 0;
+  const int sw = ((lane & 31) >> 1) & 7;
+  for (; L < total; L += gridDim.x) {
+    const int tx = L / tn, ty = L % tn;
+    const int64_t m0 = (int64_t)tx * TM, n0 = (int64_t)ty * TN;
+    if (tx != ltx) {
+      // the A rows of this tile row (plain loads: the first tile, or a new tile
+      // row of a multi-block round's misses); every wave is past the old rows
+      __syncthreads();
+      for (int id = tid; id < TM * NKB * CPR; id += kRowsPersistThreads) {
+        const int kb = id / (TM * CPR), r = (id / CPR) % TM, c = id % CPR;
+        const int64_t ar = a_rows[min(m0 + r, (int64_t)M - 1)];
+        s_a[(kb * TM + r) * CPR + (c ^ ((r >> 1) & 7))] = A[ar * rstride + kb * 8 + c];
+      }
+      if (tid < TM) {
+        const int64_t row = m0 + tid;
+        const int64_t ar = a_rows[min(row, (int64_t)M - 1)];
+        s_asq[tid] = Asq[ar];
+        s_ash[tid] = Ash[ar];
+        s_orow[tid] = row < M ? out_rows[row] : -1;
+      }
+      ltx = tx;
+    }
+    const bool live = m0 + wm * 32 < M;
+    // this tile's DMA has landed (and the previous tile's stores)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (L + (int)gridDim.x < total) dma((L + gridDim.x) % tn, buf ^ 1);  // every wave is past buffer buf ^ 1
+    if (live) {
+      f16v H, P, Q;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) H[r] = P[r] = Q[r] = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb) {
+        const int ra = ((kb * TM) + wm * 32 + (lane & 31)) * CPR;
+        const int rb = (buf * BBUF) + (kb * TN + wn * 32 + (lane & 31)) * CPR;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+          const h8 ah = __builtin_bit_cast(h8, s_a[ra + ch]);
+          const h8 al = __builtin_bit_cast(h8, s_a[ra + cl]);
+          const h8 bh = __builtin_bit_cast(h8, s_b[rb + ch]);
+          const h8 bl = __builtin_bit_cast(h8, s_b[rb + cl]);
+          H = mfma32_f16(ah, bh, H);
+          P = mfma32_f16(ah, bl, P);
+          Q = mfma32_f16(al, bh, Q);
+        }
+      }
+      const int cb = wn * 32 + (lane & 31);
+      const float bsq = s_bsq[buf * TN + cb];
+      const int bsh = s_bsh[buf * TN + cb];
+      const int64_t col = n0 + cb;
+      const bool ok = col < N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const float dot = ldexpf(H[r] + (P[r] + Q[r]), -(s_ash[lr] + bsh));
+        const float v = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+        const int32_t orow = s_orow[lr];
+        if (orow >= 0 && ok) out[(int64_t)orow * ldo + col] = v;
+      }
+    }
+    buf ^= 1;
   }
 }
 
@@ -950,9 +1216,38 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
   // tiles read it once per 64 misses)
   const int64_t tm = (M_max + 191) / 192, tn = (N + 127) / 128;
   DPSVM_CHECK(tn < 65536, "rbf_rows_indexed_split: N too large for grid.y");
-  dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 6, 1, 0, 2><<<dim3((unsigned)tm, (unsigned)tn), 768, 0, s>>>(
-      (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
-      a_rows, out_rows, m_dev);
+  static const bool reg_staged = [] {  // A/B: DPSVM_ROWS_KERNEL=reg, the register-staged ROWS kernel
+    const char* e = std::getenv("DPSVM_ROWS_KERNEL");
+    return e && std::string(e) == "reg";
+  }();
+  const int nkb = (dp + 31) / 32;
+  static const bool no_persist = [] {  // A/B: DPSVM_ROWS_KERNEL=glds, the tile-per-workgroup LDS-DMA kernel
+    const char* e = std::getenv("DPSVM_ROWS_KERNEL");
+    return e && std::string(e) == "glds";
+  }();
+  if (!reg_staged && !no_persist && nkb <= 2) {
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      HIP_CHECK(hipGetDevice(&dev));
+      HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+      return std::max(1, n);
+    }();
+    const int64_t grid = std::min<int64_t>(tm * tn, cus);
+    if (nkb == 1)
+      dev::rbf_rows_split_persist_kernel<1><<<dim3((unsigned)grid), dev::kRowsPersistThreads, 0, s>>>(
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, gamma, lines, ldl, out_rows);
+    else
+      dev::rbf_rows_split_persist_kernel<2><<<dim3((unsigned)grid), dev::kRowsPersistThreads, 0, s>>>(
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, gamma, lines, ldl, out_rows);
+  } else if (reg_staged) {
+    dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 6, 1, 0, 2><<<dim3((unsigned)tm, (unsigned)tn), 768, 0, s>>>(
+        (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
+        a_rows, out_rows, m_dev);
+  } else {
+    dev::rbf_rows_split_glds_kernel<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
+        (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
+        ldl, out_rows);
+  }
   post_launch("rbf_rows_indexed_split", s);
 }
 

@@ -285,9 +285,10 @@ class SVC:
         self.device_ = f"{kind}:{dev}" if kind == "cuda" else "cpu"
         t0 = time.perf_counter()
         if kind == "cuda" and rank_rows is None and self._use_shrink(p, n, d, dev, comm):
-            alpha, info = C.solve_shrinking(X, ys, p, dev, ck, progress, comm)
-            self.setup_info_ = {"iteration": "ws+shrinking", "device_name": C.device_name(dev), "n_local": n,
-                                "x_replicated": True, "engine_note": f"{info['shrink_phases']} shrinking phases"}
+            shr = C.ShrinkingSolver(p, comm, dev)
+            self.setup_info_ = shr.setup(X, ys)  # the whole-problem phases' solver; iteration "ws+shrinking"
+            alpha, info = shr.solve(ck, progress)
+            self.setup_info_["engine_note"] = f"{info['shrink_phases']} shrinking phases: {info['phase_log']}"
             self._solver = None
         elif kind == "cuda":
             solver = C.GpuSolver(p, comm, dev)

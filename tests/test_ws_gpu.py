@@ -260,7 +260,7 @@ def test_ws_engine_large_n_rows_per_thread(n):
     X, y = synthetic("blobs", n=n, d=d, seed=3, sep=10.0)  # well separated: few SVs
     C_, g = 1.0, 0.125
     # solver auto picks the working-set engines from 50k rows on
-    s = SVC(C=C_, gamma=g, eps=1e-3, device="cuda", max_iter=200000).fit(X, y)
+    s = SVC(C=C_, gamma=g, eps=1e-3, device="cuda", max_iter=200000, shrink="off").fit(X, y)
     rpt = s.setup_info_["rows_per_group"] // 256
     if n > 1_000_000:
         assert s.setup_info_["iteration"] == "ws-cache" and rpt == 17  # RPT=32 kernel
