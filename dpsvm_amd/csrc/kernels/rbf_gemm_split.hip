@@ -602,12 +602,15 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
 // features).  There a tile is two k blocks of MFMA work against 24-98 KiB of
 // operand and store traffic, so a tile-per-workgroup grid is a chain of
 // latencies (load, multiply, store) per tile.  Here one 768-thread workgroup
-// per CU walks the 192 x 64 tiles of its grid stride: the 192 A rows of its
-// tile row (<= 48 KiB) are staged into LDS once, the B column tiles (64 rows,
-// and their |x|^2 / shifts) stream through two LDS buffers by LDS-DMA, the next
+// per CU walks the tiles of its grid stride (64 x 192 up to 192 x 64 by the
+// miss count): the A rows of its tile row (<= 48 KiB) are staged into LDS
+// once, the B column tiles (and their |x|^2 / shifts) stream through two LDS buffers by LDS-DMA, the next
 // tile's DMA issued before this tile's multiply, so its latency hides under
-// the multiply, the epilogue and the stores.  MFMA sequence and epilogue as
-// the ROWS kernels: bit-identical rows.
+// the multiply, the epilogue and the stores; a wave then waits with vmcnt(16)
+// (its 16 stores of the tile before are younger than that DMA), so the stores
+// drain under the next tile instead of being waited for (every live lane
+// stores exactly 16 values: rows past M and columns past N go to a scratch
+// line).  MFMA sequence and epilogue as the ROWS kernels: bit-identical rows.
 // ---------------------------------------------------------------------------
 constexpr int kRowsPersistThreads = 768;
 template <int NKB>
@@ -615,49 +618,59 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
     const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
     const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, float gamma,
-    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
-  // 12 waves of 32 x 32 (one MFMA tile, three accumulators): a 192 x 64 tile
-  constexpr int WN = 2, TM = 192, TN = 64, CPR = 8;
-  constexpr int ABUF = TM * NKB * CPR, BBUF = TN * NKB * CPR;  // u4
+    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows, float* __restrict__ trash) {
+  // 12 waves of 32 x 32 (one MFMA tile, three accumulators each), laid out by
+  // the round's miss count M: WM x WN = 2 x 6 (64 x 192 tiles) up to 64
+  // misses, 4 x 3 (128 x 96) up to 128, else 6 x 2 (192 x 64) — the fewest,
+  // widest tiles that cover the live rows (a tile's cost is mostly latency)
+  constexpr int CPR = 8, TMX = 192, TNX = 192;
+  constexpr int ABUF = TMX * NKB * CPR, BBUF = TNX * NKB * CPR;  // u4
   const int M = *m_dev;
+  const int WM = M <= 64 ? 2 : M <= 128 ? 4 : 6, WN = 12 / WM, TM = 32 * WM, TN = 32 * WN;
   const int tn = (int)((N + TN - 1) / TN), tm = (M + TM - 1) / TM, total = tm * tn;
   int L = blockIdx.x;
   if (L >= total) return;  // uniform
-  __shared__ u4 lds[ABUF + 2 * BBUF + (2 * 2 * TN) / 4 + (3 * TM) / 4];
-  u4* s_a = lds;
-  u4* s_b = lds + ABUF;                                   // [2][NKB * TN rows][CPR]
-  float* s_bsq = (float*)(lds + ABUF + 2 * BBUF);         // [2][TN], then s_bsh [2][TN]
-  int32_t* s_bsh = (int32_t*)(s_bsq + 2 * TN);
-  float* s_asq = (float*)(s_bsh + 2 * TN);
-  int32_t* s_ash = (int32_t*)(s_asq + TM);
-  int32_t* s_orow = s_ash + TM;
+  __shared__ u4 lds[ABUF + 2 * BBUF + (2 * 2 * TNX) / 4 + (3 * TMX) / 4];
+  u4* s_a = lds;                                          // [NKB][TM rows][CPR]
+  u4* s_b = lds + ABUF;                                   // [2][NKB][TN rows][CPR]
+  float* s_bsq = (float*)(lds + ABUF + 2 * BBUF);         // [2][TNX], then s_bsh [2][TNX]
+  int32_t* s_bsh = (int32_t*)(s_bsq + 2 * TNX);
+  float* s_asq = (float*)(s_bsh + 2 * TNX);
+  int32_t* s_ash = (int32_t*)(s_asq + TMX);
+  int32_t* s_orow = s_ash + TMX;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
   constexpr int64_t rstride = (int64_t)NKB * 8;
-  constexpr int BWAVES = TN * NKB / 32;  // waves 0 .. BWAVES - 1: the B rows (32 k-rows each); wave 10: |x|^2, shifts
-  // B DMA of column tile ty into buffer b
+  const int nb = TN * NKB / 8, nv = (TN + 63) / 64;  // B-row DMA instructions; |x|^2 (and shift) ones per tile
+  // B DMA of column tile ty into buffer b: instruction i (8 k-rows x 128 B) by
+  // wave i % 12, then the |x|^2 / shift dwords by the waves after
   auto dma = [&](int ty, int b) {
     const int64_t n0 = (int64_t)ty * TN;
-    if (wave < BWAVES) {
-      u4* dst = s_b + b * BBUF + 32 * wave * CPR;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = 32 * wave + 8 * i + (lane >> 3), kb = q / TN, r = q % TN;
+    for (int i = wave; i < nb + 2 * nv; i += 12) {
+      if (i < nb) {
+        const int q = 8 * i + (lane >> 3), kb = q / TN, r = q % TN;
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         __builtin_amdgcn_global_load_lds((const void*)(B + (n0 + r) * rstride + kb * 8 + c),
-                                         (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(s_b + b * BBUF + 8 * i * CPR),
+                                         16, 0, 0);
+      } else {
+        const int v = i - nb, part = v % nv;
+        const int64_t cc = min(n0 + 64 * part + lane, N - 1);
+        if (v < nv)
+          __builtin_amdgcn_global_load_lds((const void*)(Bsq + cc),
+                                           (__attribute__((address_space(3))) void*)(s_bsq + b * TNX + 64 * part), 4,
+                                           0, 0);
+        else
+          __builtin_amdgcn_global_load_lds((const void*)(Bsh + cc),
+                                           (__attribute__((address_space(3))) void*)(s_bsh + b * TNX + 64 * part), 4,
+                                           0, 0);
       }
-    } else if (wave == 10) {
-      const int64_t cc = min(n0 + lane, N - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Bsq + cc),
-                                       (__attribute__((address_space(3))) void*)(s_bsq + b * TN), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Bsh + cc),
-                                       (__attribute__((address_space(3))) void*)(s_bsh + b * TN), 4, 0, 0);
     }
   };
   dma(L % tn, 0);
   int ltx = -1, buf = 0;
+  bool stored = false;  // this wave's 16 stores of the previous tile are younger than the pending DMA
   const int sw = ((lane & 31) >> 1) & 7;
   for (; L < total; L += gridDim.x) {
     const int tx = L / tn, ty = L % tn;
@@ -679,10 +692,12 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
         s_orow[tid] = row < M ? out_rows[row] : -1;
       }
       ltx = tx;
+      stored = false;  // those loads were waited for: nothing older is outstanding
     }
     const bool live = m0 + wm * 32 < M;
-    // this tile's DMA has landed (and the previous tile's stores)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this tile's DMA has landed; the previous tile's stores may still drain
+    if (stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -708,8 +723,8 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
         }
       }
       const int cb = wn * 32 + (lane & 31);
-      const float bsq = s_bsq[buf * TN + cb];
-      const int bsh = s_bsh[buf * TN + cb];
+      const float bsq = s_bsq[buf * TNX + cb];
+      const int bsh = s_bsh[buf * TNX + cb];
       const int64_t col = n0 + cb;
       const bool ok = col < N;
 #pragma unroll
@@ -718,9 +733,13 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
         const float dot = ldexpf(H[r] + (P[r] + Q[r]), -(s_ash[lr] + bsh));
         const float v = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
         const int32_t orow = s_orow[lr];
-        if (orow >= 0 && ok) out[(int64_t)orow * ldo + col] = v;
+        // exactly 16 stores per lane (the vmcnt(16) above): rows past M and
+        // columns past N go to the scratch line
+        float* dst = (orow >= 0 && ok) ? out + (int64_t)orow * ldo + col : trash + lane;
+        *dst = v;
       }
     }
+    stored = live;
     buf ^= 1;
   }
 }
@@ -1232,13 +1251,20 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
       HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
       return std::max(1, n);
     }();
+    static float* trash = [] {  // the scratch line of the fixed-count stores (64 floats, never read)
+      float* t = nullptr;
+      HIP_CHECK(hipMalloc((void**)&t, 64 * sizeof(float)));
+      return t;
+    }();
     const int64_t grid = std::min<int64_t>(tm * tn, cus);
     if (nkb == 1)
       dev::rbf_rows_split_persist_kernel<1><<<dim3((unsigned)grid), dev::kRowsPersistThreads, 0, s>>>(
-          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, gamma, lines, ldl, out_rows);
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, gamma, lines, ldl, out_rows,
+          trash);
     else
       dev::rbf_rows_split_persist_kernel<2><<<dim3((unsigned)grid), dev::kRowsPersistThreads, 0, s>>>(
-          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, gamma, lines, ldl, out_rows);
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, gamma, lines, ldl, out_rows,
+          trash);
   } else if (reg_staged) {
     dev::rbf_gemm_split_kernel<dev::SPLIT_ROWS, 6, 1, 0, 2><<<dim3((unsigned)tm, (unsigned)tn), 768, 0, s>>>(
         (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
