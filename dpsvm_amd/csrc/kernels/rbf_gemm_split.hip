@@ -475,6 +475,9 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
 // wave instructions of 8 rows x 128 B per block, 4 per wave.
 // ---------------------------------------------------------------------------
 constexpr int kRowsGldsThreads = 768;
+// BAUX: cache policy of the B operand's DMA (2 = nt: streamed once per round,
+// kept from evicting the A rows every tile re-reads from L2)
+template <int BAUX>
 __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
     const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
@@ -520,12 +523,20 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
     src[i] = (r < TM ? A : B) + grow * rstride + c;
   }
   const bool dma_wave = wave < DMA_WAVES;
+  const bool b_wave = 32 * wave >= TM;  // waves 6 .. 9 stage B rows only (TM = 192 = 6 x 32)
   auto dma = [&](int kb) {
     u4* dst = lds + (kb % NB) * BUF + 32 * wave * CPR;
+    if (b_wave) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
-                                       (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
+                                         (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, BAUX);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
+                                         (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+    }
   };
   __syncthreads();  // row data written (no DMA in flight yet)
   if (dma_wave) {
@@ -1270,9 +1281,18 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
         (const dev::u4*)X, Xsh, Xsq, M_max, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl, 0,
         a_rows, out_rows, m_dev);
   } else {
-    dev::rbf_rows_split_glds_kernel<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
-        (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
-        ldl, out_rows);
+    static const bool b_cached = [] {  // A/B: DPSVM_ROWS_BNT=0 streams B with the default cache policy
+      const char* e = std::getenv("DPSVM_ROWS_BNT");
+      return e && std::string(e) == "0";
+    }();
+    if (b_cached)
+      dev::rbf_rows_split_glds_kernel<0><<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
+          ldl, out_rows);
+    else
+      dev::rbf_rows_split_glds_kernel<2><<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
+          ldl, out_rows);
   }
   post_launch("rbf_rows_indexed_split", s);
 }
