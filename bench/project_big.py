@@ -14,7 +14,7 @@ replicated when it does), from one-GPU measurements:
   * the in-kernel peer exchange's own per-round cost at the same shape, loopback
     at world 1 (profiles/r4_big_inputs/runs.jsonl: peer vs local);
   * the shrinking phases of the one-GPU run (rows, rounds, seconds:
-    profiles/r4_shrink_auto_final_1gpu.jsonl phase_log);
+    profiles/r4_big_configs_final_1gpu.jsonl phase_log);
   * ASSUMED: X us extra latency per exchange point of a store crossing xGMI
     (3 points per round) — the one input no single GPU can measure.
 
@@ -48,25 +48,32 @@ def kernel_round_us(path, rounds):
 
 
 def runs():
-    rs = [json.loads(line) for line in open(f"{INP}/runs.jsonl") if line.strip()]
-    return [r for r in rs if "value" in r]
+    """profiles/r4_big_inputs/runs.jsonl, in order: covtype capped solve with the
+    loopback peer exchange and its local twin (the same kernels: their
+    difference is the exchange's cost), covtype local with the round-4 ROWS
+    kernel, synthetic-2m local (same), the covtype P = 8 slab probe"""
+    return [json.loads(line) for line in open(f"{INP}/runs.jsonl") if line.strip()]
 
 
 def main() -> int:
     rs = runs()
-    cov_local = next(r for r in rs if r["preset"] == "covtype" and r["exchange"] == "none")
-    cov_peer = next(r for r in rs if r["preset"] == "covtype" and r["exchange"] == "loopback")
-    syn_local = next(r for r in rs if r["preset"] == "synthetic-2m")
-    fin = [json.loads(line) for line in open("profiles/r4_shrink_auto_final_1gpu.jsonl") if line.strip()]
-    cov_shr = next(r for r in fin if r["preset"] == "covtype" and r["params"].get("ws_rel", 0.3) > 0.2)
-    syn_shr = next(r for r in fin if r["preset"] == "synthetic-2m")
-    ext = 1e6 * (cov_peer["value"] - cov_local["value"]) / cov_local["rounds"]
+    cov_peer, cov_local_old, cov_local, syn_local = rs[0], rs[1], rs[2], rs[3]
+    slab = rs[4]["slab"]["8"]
+    assert cov_peer["exchange"] == "loopback" and cov_local_old["exchange"] == "none"
+    fin = [json.loads(line) for line in open("profiles/r4_big_configs_final_1gpu.jsonl") if line.strip()]
+    cov_shr = next(r for r in fin if r["preset"] == "covtype" and r["shrink"]["on"])
+    syn_shr = next(r for r in fin if r["preset"] == "synthetic-2m" and r["shrink"]["on"])
+    ext = 1e6 * (cov_peer["value"] - cov_local_old["value"]) / cov_local_old["rounds"]
     print(f"measured loopback peer-exchange cost at covtype shape: {ext:.1f} us/round "
-          f"({cov_peer['value']:.3f} vs {cov_local['value']:.3f} s, {cov_local['rounds']} rounds)")
+          f"({cov_peer['value']:.3f} vs {cov_local_old['value']:.3f} s, {cov_local_old['rounds']} rounds)")
+    print(f"measured covtype dense Gram slab at P = 8 (K(581012 rows, 72627 columns), {slab['gb']} GB): "
+          f"{slab['s']} s - the P = 8 whole-problem phase may run ws-dense; projected as ws-cache "
+          f"(its miss-row GEMM / P): an upper bound")
+    cov_run, syn_run = cov_local, syn_local
     shapes = []
     for name, run, stats, shr, n, d in (
-            ("covtype box 581k x 54", cov_local, f"{INP}/covtype_box_2M_steps_kernel_stats.csv", cov_shr, 581012, 54),
-            ("synthetic-2m 2M x 1024", syn_local, f"{INP}/synthetic2m_120k_steps_kernel_stats.csv", syn_shr, 2000000,
+            ("covtype box 581k x 54", cov_run, f"{INP}/covtype_box_2M_steps_kernel_stats.csv", cov_shr, 581012, 54),
+            ("synthetic-2m 2M x 1024", syn_run, f"{INP}/synthetic2m_120k_steps_kernel_stats.csv", syn_shr, 2000000,
              1024)):
         k = kernel_round_us(stats, run["rounds"])
         period = 1e6 * run["value"] / run["rounds"]
