@@ -756,6 +756,164 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 }
 
 // ---------------------------------------------------------------------------
+// Wide-wave LDS-DMA STORE GEMM (variant 5): 256 x 128 tiles, 8 waves of
+// 64 x 64 (2 x 2 MFMA tiles, three accumulators each: 192 accumulator
+// registers at two waves per SIMD).  The 32 x 64 waves of the kernels above
+// read 6 KiB of LDS operands per 6 MFMAs; with the DMA's 32 KiB of LDS writes
+// per k block the LDS port needs ~167 B/clk per CU against 128 (PMC: ~35% MFMA
+// busy).  A 64 x 64 wave reads 8 KiB per 12 MFMAs: ~114 B/clk with the DMA, so
+// the MFMA pipe, not the LDS port, sets the pace.  Same per-element k order
+// (H, P, Q over the k blocks in order): bit-identical to the other kernels.
+// Symmetric mode: tile (tx, ty) covers 128-row blocks 2 tx and 2 tx + 1 of
+// column block ty; computed when ty >= 2 tx, each block above the diagonal
+// also stored transposed (the diagonal-straddling tile's lower block is
+// written twice with the same bits).  Three 48 KiB buffers of 32 k, one block
+// in flight while one is multiplied.
+// ---------------------------------------------------------------------------
+constexpr int kW64Threads = 512;
+__global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
+    float gamma, float* __restrict__ out, int64_t ldo, int sym) {
+  constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
+  int64_t tx, ty;
+  xcd_tile(tx, ty);
+  if (sym && ty < 2 * tx) return;  // uniform: both 128-row blocks below the diagonal
+  __shared__ u4 lds[NB * BUF + 2 * ROWS / 4];  // 3 operand buffers, then |x|^2 [ROWS] and shifts [ROWS]
+  float* s_sq = (float*)(lds + NB * BUF);
+  int32_t* s_sh = (int32_t*)(lds + NB * BUF) + ROWS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t m0 = tx * TM, n0 = ty * TN;
+  const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
+  if (tid < ROWS) {
+    const int64_t ri = tid < TM ? min(m0 + tid, M - 1) : min(n0 + (tid - TM), N - 1);
+    s_sq[tid] = tid < TM ? Asq[ri] : Bsq[ri];
+    s_sh[tid] = tid < TM ? Ash[ri] : Bsh[ri];
+  }
+  // DMA: wave w fills stage rows 48 w + 8 i + (lane >> 3), i = 0..5; lane
+  // position p = lane & 7 takes global chunk p ^ ((row >> 1) & 7).  An 8-row
+  // group is all A or all B rows: a wave-uniform base (SGPRs) plus a 32-bit
+  // lane offset keeps the addressing out of the 256 registers the 192
+  // accumulators leave room in
+  const u4* base[6];
+  uint32_t off[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int g = __builtin_amdgcn_readfirstlane(48 * wave + 8 * i);  // first row of the group (uniform)
+    const int r = g + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    base[i] = g < TM ? A + (m0 + g) * rstride : B + (n0 + (g - TM)) * rstride;
+    off[i] = (uint32_t)((lane >> 3) * rstride + c);
+  }
+  auto dma = [&](int kb) {
+    u4* dst = lds + (kb % NB) * BUF + 48 * wave * CPR;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(base[i] + (int64_t)kb * 8 + off[i]),
+                                       (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+  };
+  __syncthreads();  // row data written (no DMA in flight yet)
+  dma(0);
+  if (nkb > 1) dma(1);
+
+  f16v H[2][2], P[2][2], Q[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) H[i][j][r] = P[i][j][r] = Q[i][j][r] = 0.f;
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra0 = (wm * 64 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
+  for (int kb = 0; kb < nkb; ++kb) {
+    // retire block kb's DMA (block kb + 1 may stay in flight)
+    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kb + 2 < nkb) dma(kb + 2);  // into the buffer of block kb - 1 (every wave is past it)
+    const u4* buf = lds + (kb % NB) * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+      // hi x hi, then hi x lo (the A hi fragments die), then lo x hi: at most
+      // six operand fragments live
+      const h8 ah0 = __builtin_bit_cast(h8, buf[ra0 + ch]);
+      const h8 ah1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + ch]);
+      const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+      const h8 bh1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + ch]);
+      H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
+      const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+      const h8 bl1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + cl]);
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      const h8 al0 = __builtin_bit_cast(h8, buf[ra0 + cl]);
+      const h8 al1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + cl]);
+      Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
+    }
+  }
+
+  // ---- epilogue (as the tile kernel), one 32 x 32 MFMA tile at a time:
+  // values, direct stores, transposed stores (its P / Q registers die early) ----
+  const bool interior = m0 + TM <= M && n0 + TN <= N;
+  // this wave's 64 rows lie in 128-row block 2 tx + (wm >> 1): transposed store above the diagonal
+  const bool mirror = sym && ty > 2 * tx + (wm >> 1);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cb = TM + wn * 64 + 32 * j + (lane & 31);
+    const float bsq = s_sq[cb];
+    const int bsh = s_sh[cb];
+    const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(s_sh[lr] + bsh));
+        H[i][j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
+        const int64_t row = m0 + lr;
+        if (interior || (row < M && col < N)) out[row * ldo + col] = H[i][j][r];
+      }
+      if (mirror) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t row = m0 + wm * 64 + 32 * i + 8 * q + 4 * hl;
+          float* dst = out + col * ldo + row;
+          f4 v;
+          v.x = H[i][j][4 * q + 0];
+          v.y = H[i][j][4 * q + 1];
+          v.z = H[i][j][4 * q + 2];
+          v.w = H[i][j][4 * q + 3];
+          if (interior) {
+            *(f4*)dst = v;
+          } else if (col < M) {
+            if (row + 3 < N) {
+              *(f4*)dst = v;
+            } else {
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                if (row + c < N) dst[c] = v[c];
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent LDS-DMA STORE GEMM: the LDS-DMA kernel's k loop, one 512-thread
 // workgroup per CU walking tiles as the persistent kernel does, so that a
 // tile's Gram stores (128 KiB per tile with the mirror: 4.2 of the tile
@@ -1130,7 +1288,7 @@ int g_split_variant = -1;
 
 int split_gemm_variant() {
   if (g_split_variant < 0) {
-    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 3 LDS-DMA, 4 persistent LDS-DMA
+    const char* e = std::getenv("DPSVM_SPLIT_GEMM");  // A/B: 1 tile kernel, 3 LDS-DMA, 4 persistent LDS-DMA, 5 wide-wave
     g_split_variant = e ? atoi(e) : 0;
   }
   return g_split_variant;
@@ -1202,6 +1360,17 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     return e && atoi(e) == 1 ? 1 : 2;
   }();
   const int variant = split_gemm_variant();
+  // default from 5 k blocks: the wide-wave LDS-DMA kernel (60000^2 x 784
+  // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
+  // bit-identical; profiles/r4_w64_gram_ab.txt)
+  if ((variant == 5 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0) {
+    const int64_t tm2 = (M + 255) / 256;
+    dev::rbf_gemm_split_w64_kernel<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
+        (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
+        symmetric ? 1 : 0);
+    post_launch("rbf_gemm_split_w64", s);
+    return;
+  }
   if ((variant == 0 || variant == 4) && ablate == 0 && (dp + 31) / 32 >= 5 && tm * tn < (1ll << 31)) {
     // default: persistent LDS-DMA, one workgroup per CU (a multiple of 8)
     static const int cus4 = [] {

@@ -102,7 +102,7 @@ def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
         C.k_set_split_gemm_variant(1)
         ref_sym, ref_xy = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
         got = {}
-        for v in (3, 4):  # LDS-DMA (three k blocks in flight); persistent LDS-DMA
+        for v in (3, 4, 5):  # LDS-DMA (three k blocks in flight); persistent LDS-DMA; wide-wave 256 x 128
             C.k_set_split_gemm_variant(v)
             got[v] = K.rbf_gram(x, None, g, split=True), K.rbf_gram(x, y, g, split=True)
     finally:
