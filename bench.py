@@ -469,6 +469,9 @@ def main(argv=None) -> int:
                           "one_block_from_round": int(res.get("ws_p1_round", 0)),
                           "damped_rounds": int(res.get("ws_damped", 0))},
             "converged": bool(res["converged"]),
+            **({"note": "stopped at the iteration cap: an unconverged working-set model is not the reference's "
+                        "pair-at-a-time iterate at the same cap (raise --max-iter to converge)"}
+               if int(res["status"]) == 2 and int(res.get("outer", 0)) > 0 else {}),
             "n_sv": nsv,
             "b": res["b"],
             "b_hi": res.get("b_hi"),

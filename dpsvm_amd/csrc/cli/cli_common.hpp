@@ -383,6 +383,13 @@ inline void print_outcome(const SolveResult& r, float eps) {
               << r.ws_blocks << (r.ws_blocks_end != r.ws_blocks ? " -> " + std::to_string(r.ws_blocks_end) : "")
               << ")\n";
   if (r.status == 4) std::cout << "WARNING: non-finite b_hi/b_lo encountered; training stopped\n";
+  if (r.outer > 0 && r.status == 2) {
+    // a capped, unconverged working-set solve is not the reference's iterate at that cap
+    std::cerr << "warning: stopped at the iteration cap with gap " << (r.b_lo - r.b_hi) << " > 2 eps: the "
+              << "working-set rounds' unconverged model differs from the reference's pair-at-a-time iterate at the "
+              << "same cap; raise --max-iter (-n) to converge, or --solver smo for the reference's trajectory "
+              << "(with --engines all when the Gram is not resident)\n";
+  }
   std::cout << "b: " << r.b << "\n";
 }
 

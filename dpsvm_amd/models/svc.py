@@ -311,6 +311,13 @@ class SVC:
         self.fit_time_ = float(info["t_solve"])
         self.setup_time_ = float(info["t_setup"])
         self.stats_ = dict(info)
+        if self.status_ == 2 and self.n_rounds_ > 0:
+            import warnings
+
+            warnings.warn(f"stopped at max_iter with gap {info['b_lo'] - info['b_hi']:.3g} > 2 eps: an unconverged "
+                          "working-set model differs from the reference's pair-at-a-time iterate at the same cap; "
+                          "raise max_iter to converge, or solver='smo' for the reference's trajectory (engines='all' "
+                          "when the Gram is not resident)", RuntimeWarning, stacklevel=2)
         self.gamma_ = p.gamma
         self.n_features_in_ = d
         self._X_train, self._y_train = (X, ys) if rank_rows is None else (None, None)
