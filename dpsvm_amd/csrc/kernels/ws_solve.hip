@@ -71,26 +71,24 @@ __device__ __forceinline__ PairUpdate ws_pair_step(float a_hi, float a_lo, float
   const float s = y_lo * y_hi;
   float a_lo_new = a_lo + (y_lo * (bh - bl)) * r;
   float a_hi_new;
-  if (kBox && !same) {
-    float L, H, hL, hH;
-    if (y_hi != y_lo) {
-      const float dl = a_lo - a_hi;
-      L = dl > 0.f ? dl : 0.f;
-      hL = dl > 0.f ? 0.f : -1.f;
-      H = C + dl < C ? C + dl : C;
-      hH = C + dl < C ? C : -1.f;
-    } else {
-      const float sm = a_lo + a_hi;
-      L = sm - C > 0.f ? sm - C : 0.f;
-      hL = sm - C > 0.f ? C : -1.f;
-      H = sm < C ? sm : C;
-      hH = sm < C ? 0.f : -1.f;
-    }
+  if (kBox) {
+    // branch-free (every branch of the one-wave loop is a fetch bubble): both
+    // box geometries and the same-row case computed, the pair's uniform
+    // labels / positions select — the same values the branches produced
+    const float dl = a_lo - a_hi, sm = a_lo + a_hi;
+    const bool diff = y_hi != y_lo;
+    const float L = diff ? (dl > 0.f ? dl : 0.f) : (sm - C > 0.f ? sm - C : 0.f);
+    const float hL = diff ? (dl > 0.f ? 0.f : -1.f) : (sm - C > 0.f ? C : -1.f);
+    const float H = diff ? (C + dl < C ? C + dl : C) : (sm < C ? sm : C);
+    const float hH = diff ? (C + dl < C ? C : -1.f) : (sm < C ? 0.f : -1.f);
     const bool atL = a_lo_new <= L, atH = !atL && a_lo_new >= H;
-    a_lo_new = atL ? L : (atH ? H : a_lo_new);
+    const float lo_box = atL ? L : (atH ? H : a_lo_new);
     const float snap = atL ? hL : (atH ? hH : -1.f);
-    a_hi_new = snap >= 0.f ? snap : a_hi + (s * (a_lo - a_lo_new));
-    a_hi_new = clip01(a_hi_new, 0.0f, C);
+    const float hi_box = clip01(snap >= 0.f ? snap : a_hi + (s * (a_lo - lo_box)), 0.0f, C);
+    const float hi_same = clip01(a_hi + (s * (a_lo - a_lo_new)), 0.0f, C);
+    const float lo_same = clip01(a_lo_new, 0.0f, C);
+    a_lo_new = same ? lo_same : lo_box;
+    a_hi_new = same ? hi_same : hi_box;
   } else {
     a_hi_new = a_hi + (s * (a_lo - a_lo_new));
     const float lo_raw = a_lo_new, hi_raw = a_hi_new;
@@ -307,7 +305,11 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
           const float dv = -fl[s] - bh;
           float eta = (1.0f + 1.0f) - 2.0f * kh[s];
           eta = eta >= a.tau ? eta : a.tau;
-          g[s] = ((fl[s] < INF) & (dv > 0.f)) ? -(dv * dv) * __builtin_amdgcn_rcpf(eta) : INF;
+          // on every lane, then a select: hipcc made each slot's conditional
+          // reciprocal an exec-masked branch (three per step)
+          float gv = -(dv * dv) * __builtin_amdgcn_rcpf(eta);
+          asm volatile("" : "+v"(gv));
+          g[s] = ((fl[s] < INF) & (dv > 0.f)) ? gv : INF;
         }
         float gm = fminf(g[0], g[1]);
         if constexpr (NS == 3) gm = fminf(gm, g[2]);
