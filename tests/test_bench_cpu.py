@@ -74,3 +74,21 @@ def test_bench_refuses_missing_devices_and_rank_mismatch():
     r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
              "--samples", "500"], env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_bench_presets_and_shrink_flag():
+    """BASELINE configs as bench presets: covtype-ref is Makefile:77's run_cover
+    recipe (500,000 rows, C=2048, gamma=0.03125, eps 1e-3, 3M cap); shrink is
+    auto by default (on only where the whole Gram is not resident, GPU) and
+    accepts on / off."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = bench.parse(["--config", "covtype-ref"])
+    assert (a.samples, a.features, a.C, a.gamma, a.eps, a.max_iter) == (500000, 54, 2048.0, 0.03125, 1e-3, 3000000)
+    assert a.shrink == "auto" and a.engines == "production"
+    assert bench.parse(["--shrink", "off"]).shrink == "off"
+    full = bench.parse(["--config", "covtype"])
+    assert full.samples == 581012 and full.data == a.data == "covtype"
