@@ -124,7 +124,7 @@ struct SolverParams {
   // a q-row sub-problem in LDS, the same global stop test)
   int solver = 0;
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
-  int ws_new = 0;             // rows replaced per round (0: 3 ws_size / 4)
+  int ws_new = 0;             // rows replaced per one-block round (0: auto, ws_new_auto in device_state.hpp)
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
   int ws_blocks = 0;          // working-set engines: up to P disjoint q-row sub-problems per round (1..32,
                               // P x ws_size <= 3072; 0 auto = 32 blocks of 96 rows from 50k rows, else 1).  Adaptive: halved after every damped round (coupled blocks), 1 after an

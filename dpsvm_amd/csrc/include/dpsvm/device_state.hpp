@@ -113,6 +113,19 @@ inline bool choose_engine(const EngineFacts& f, EngineKind* out) {
   return false;
 }
 
+// Rows a one-block working-set round replaces (ws_new = 0: auto): all q with
+// >= 128 padded features, 3/4 of the set (the newest quarter kept) below.
+// Measured with full replacement: synthetic-2m 2M x 1024 47.9 -> 44.4 s,
+// mnist-parity 0.0226 -> 0.0219 s, adult (solver=ws) 0.207 -> 0.191 s;
+// covtype (54 features, strongly coupled at C = 2048) stalls without retained
+// rows and keeps 3/4 (profiles/r4_ws_new_ab.txt, r4_ws_param_sweep_1gpu.txt).
+// A function of the shape only, so ws-dense and ws-cache (and every rank) take
+// the same sets: the cache engine stays bit-identical to the dense one.
+inline int ws_new_auto(int ws_new, int q, int dp) {
+  const int n = ws_new > 0 ? (ws_new < q ? ws_new : q) : (dp >= 128 ? q : 3 * q / 4);
+  return n > 2 ? n : 2;
+}
+
 // Written by smo_finalize, read by the next iteration's kernels.
 struct alignas(16) SmoCtrl {
   int32_t iter;        // SMO updates applied so far

@@ -431,8 +431,8 @@ struct WsRounds : Base {
     w.aux_stride = kWsMax;
     w.xsub_rows = w.q_max;  // peer exchange: the one-block layout of the sub-Gram rows (same region)
     // the one-block engine's set turnover (multi-block rounds replace the
-    // whole union): 3/4 new rows, the newest quarter of the previous set kept
-    w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, w.q_max) : 3 * w.q_max / 4);
+    // whole union): ws_new_auto (device_state.hpp)
+    w.n_new = ws_new_auto(m.p.ws_new, w.q_max, m.dp);
     return w;
   }
   // cache mode: the kernel rows of the round's misses (<= blocks x q_max rows), one GEMM

@@ -685,7 +685,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // >= 2 new rows: the global maximal violating pair (up rank 0, low rank 0)
     // is always in the set, so every round makes progress
     // defaults measured on the MNIST-shape headline (profiles/r2_ws_param_sweep.txt)
-    w.n_new = std::max(2, m.p.ws_new > 0 ? std::min(m.p.ws_new, ws_q) : 3 * ws_q / 4);
+    w.n_new = ws_new_auto(m.p.ws_new, ws_q, m.dp);
     w.inner_max = m.p.ws_inner > 0 ? m.p.ws_inner : 4 * ws_q;
     DPSVM_CHECK(m.p.ws_wss >= 0 && m.p.ws_wss <= 2, "ws_wss must be 0 (auto), 1 (first order) or 2 (second order)");
     if (m.p.ws_wss > 0) {

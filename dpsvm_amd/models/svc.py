@@ -111,7 +111,7 @@ class SVCConfig:
     # in LDS, the same global stop test; ws_*.hip)
     solver: str = "auto"
     ws_size: int = 192              # working-set rows (<= 192)
-    ws_new: int = 0                 # rows replaced per round (0: 3 ws_size / 4)
+    ws_new: int = 0                 # rows replaced per one-block round (0: auto, ws_size from 128 padded features, else 3/4)
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
     # working-set engines: up to P sub-problems per round (1..32, P x ws_size <= 3072; 0 auto = 32 blocks of
     # 96 rows from 50k rows, else 1); adaptive — halved
