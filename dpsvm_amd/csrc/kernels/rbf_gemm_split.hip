@@ -771,6 +771,7 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 // in flight while one is multiplied.
 // ---------------------------------------------------------------------------
 constexpr int kW64Threads = 512;
+template <int NT>  // 1: non-temporal Gram stores (the 14.4 GB the headline writes do not evict operand panels)
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
@@ -884,7 +885,10 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
         const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(s_sh[lr] + bsh));
         H[i][j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
         const int64_t row = m0 + lr;
-        if (interior || (row < M && col < N)) out[row * ldo + col] = H[i][j][r];
+        if (interior || (row < M && col < N)) {
+          if constexpr (NT) __builtin_nontemporal_store(H[i][j][r], out + row * ldo + col);
+          else out[row * ldo + col] = H[i][j][r];
+        }
       }
       if (mirror) {
 #pragma unroll
@@ -896,16 +900,13 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
           v.y = H[i][j][4 * q + 1];
           v.z = H[i][j][4 * q + 2];
           v.w = H[i][j][4 * q + 3];
-          if (interior) {
-            *(f4*)dst = v;
+          if (interior || (col < M && row + 3 < N)) {
+            if constexpr (NT) __builtin_nontemporal_store(v, (f4*)dst);
+            else *(f4*)dst = v;
           } else if (col < M) {
-            if (row + 3 < N) {
-              *(f4*)dst = v;
-            } else {
 #pragma unroll
-              for (int c = 0; c < 4; ++c)
-                if (row + c < N) dst[c] = v[c];
-            }
+            for (int c = 0; c < 4; ++c)
+              if (row + c < N) dst[c] = v[c];
           }
         }
       }
@@ -1364,8 +1365,13 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   if ((variant == 5 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0) {
+    static const int nt = [] {
+      const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal
+      return e ? atoi(e) : 0;
+    }();
     const int64_t tm2 = (M + 255) / 256;
-    dev::rbf_gemm_split_w64_kernel<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
+    auto kern = nt ? dev::rbf_gemm_split_w64_kernel<1> : dev::rbf_gemm_split_w64_kernel<0>;
+    kern<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
         (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
         symmetric ? 1 : 0);
     post_launch("rbf_gemm_split_w64", s);
