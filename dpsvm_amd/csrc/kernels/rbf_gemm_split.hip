@@ -771,7 +771,9 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 // in flight while one is multiplied.
 // ---------------------------------------------------------------------------
 constexpr int kW64Threads = 512;
-template <int NT>  // 1: non-temporal Gram stores (the 14.4 GB the headline writes do not evict operand panels)
+// NT 1: non-temporal Gram stores (measured slower, profiles/r4_gram_nt_store_ab.txt);
+// NT 2: diagnostics only — stores skipped unless a value is NaN (the store-free time)
+template <int NT>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
@@ -885,12 +887,13 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
         const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(s_sh[lr] + bsh));
         H[i][j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
         const int64_t row = m0 + lr;
+        if (NT == 2 && !(H[i][j][r] != H[i][j][r])) continue;
         if (interior || (row < M && col < N)) {
-          if constexpr (NT) __builtin_nontemporal_store(H[i][j][r], out + row * ldo + col);
+          if constexpr (NT == 1) __builtin_nontemporal_store(H[i][j][r], out + row * ldo + col);
           else out[row * ldo + col] = H[i][j][r];
         }
       }
-      if (mirror) {
+      if (mirror && NT != 2) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int64_t row = m0 + wm * 64 + 32 * i + 8 * q + 4 * hl;
@@ -901,7 +904,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
           v.z = H[i][j][4 * q + 2];
           v.w = H[i][j][4 * q + 3];
           if (interior || (col < M && row + 3 < N)) {
-            if constexpr (NT) __builtin_nontemporal_store(v, (f4*)dst);
+            if constexpr (NT == 1) __builtin_nontemporal_store(v, (f4*)dst);
             else *(f4*)dst = v;
           } else if (col < M) {
 #pragma unroll
@@ -1366,11 +1369,12 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   if ((variant == 5 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0) {
     static const int nt = [] {
-      const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal
+      const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
       return e ? atoi(e) : 0;
     }();
     const int64_t tm2 = (M + 255) / 256;
-    auto kern = nt ? dev::rbf_gemm_split_w64_kernel<1> : dev::rbf_gemm_split_w64_kernel<0>;
+    auto kern = nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
+                : nt ? dev::rbf_gemm_split_w64_kernel<1> : dev::rbf_gemm_split_w64_kernel<0>;
     kern<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
         (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
         symmetric ? 1 : 0);
