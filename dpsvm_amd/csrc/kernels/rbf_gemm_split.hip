@@ -873,6 +873,50 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
   const bool interior = m0 + TM <= M && n0 + TN <= N;
   // this wave's 64 rows lie in 128-row block 2 tx + (wm >> 1): transposed store above the diagonal
   const bool mirror = sym && ty > 2 * tx + (wm >> 1);
+  if (NT == 0 && interior && ldo <= (1 << 21)) {
+    // interior tile (all but the last row / column of tiles): no bounds tests,
+    // so no branch per value; |x|^2 and shifts read as 4-row vectors (one LDS
+    // round trip per 4 values); stores at 32-bit offsets from uniform bases
+    // (the generic loop below waited out one LDS round trip per value)
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    float* const ob = out + m0 * ldo + n0;  // direct block
+    float* const mb = out + n0 * ldo + m0;  // mirrored block
+    const uint32_t ld = (uint32_t)ldo;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = wn * 64 + 32 * j + (lane & 31);
+      const float bsq = s_sq[TM + cl];
+      const int bsh = s_sh[TM + cl];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int lr0 = wm * 64 + 32 * i + 4 * hl;  // value r sits on row lr0 + 8 (r >> 2) + (r & 3)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
+          const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(ash[e] + bsh));
+            H[i][j][r] = rbf_from_dot(asq[e], bsq, dot, gamma);
+            ob[(uint32_t)(lr0 + 8 * g + e) * ld + (uint32_t)cl] = H[i][j][r];
+          }
+        }
+        if (mirror) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f4 v;
+            v.x = H[i][j][4 * q + 0];
+            v.y = H[i][j][4 * q + 1];
+            v.z = H[i][j][4 * q + 2];
+            v.w = H[i][j][4 * q + 3];
+            *(f4*)(mb + (uint32_t)cl * ld + (uint32_t)(lr0 + 8 * q)) = v;
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int cb = TM + wn * 64 + 32 * j + (lane & 31);
