@@ -105,7 +105,7 @@ def parse(argv=None):
     ap.add_argument("--ws-new", type=int, default=0)
     ap.add_argument("--ws-rel", type=float, default=0.3)
     ap.add_argument("--ws-inner", type=int, default=0, help="pair steps per block and round at most (0: 4 ws_size)")
-    ap.add_argument("--ws-block", type=int, default=32)
+    ap.add_argument("--ws-block", type=int, default=8)
     ap.add_argument("--ws-t-halve", type=float, default=None, help="multi-block: damped rounds below this t halve P")
     ap.add_argument("--shrink", default="auto", choices=["auto", "on", "off"],
                     help="one GPU: LIBSVM-style shrinking as problem reduction (phases on the active rows); "

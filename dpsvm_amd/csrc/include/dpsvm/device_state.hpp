@@ -296,6 +296,7 @@ constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: 
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 constexpr int kWsMaxPass1Splits = 16;             // multi-block f-update pass 1: list slices over workgroups
 constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
+constexpr int64_t kWsSwitchRounds = 32;           // multi-block -> one-block graph switch granularity (rounds)
 
 struct alignas(16) WsCtrl {
   int64_t iter;      // pair updates applied so far

@@ -504,7 +504,14 @@ struct WsRounds : Base {
   }
   void observe(GpuSolver::Impl& m, const SmoStatus& st, int64_t blocks_done) override {
     if (single || m.wsa.blocks <= 1 || st.ws_p1_round <= 0) return;
-    if (st.ws_p1_round > blocks_done * this->block(m.p)) return;  // set by the block in flight: next time
+    // the switch to the one-block graph happens on kWsSwitchRounds boundaries
+    // only, with what the host knew one such span earlier — the rounds the
+    // 32-round graph blocks switched at, whatever the graph block size (short
+    // blocks end a solve sooner after convergence without moving a trajectory)
+    const int64_t B = this->block(m.p), next = (blocks_done + 1) * B;  // first round after the block in flight
+    const int64_t span = std::max<int64_t>(B, kWsSwitchRounds);
+    if (next % span != 0) return;
+    if (st.ws_p1_round > next - span) return;  // set by a later round: next boundary
     single = true;
     const WsArgs w = one_block(m);
     launch::ws_to_single(w, m.stream);

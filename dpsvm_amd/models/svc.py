@@ -119,7 +119,7 @@ class SVCConfig:
     ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
-    ws_block: int = 32              # rounds per hipGraph block
+    ws_block: int = 8               # rounds per hipGraph block
     # one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking: phases on the rows that can
     # still violate, the rest of the gradient updated by one predict GEMM per phase).  auto: on where it
     # pays — one GPU, working-set rounds, the whole Gram not resident (C.shrink_auto) | on | off
