@@ -909,92 +909,63 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     }
   }
 
-  // ---- epilogue (as the tile kernel), one 32 x 32 MFMA tile at a time:
-  // values, direct stores, transposed stores (its P / Q registers die early) ----
-  const bool interior = m0 + TM <= M && n0 + TN <= N;
-  // this wave's 64 rows lie in 128-row block 2 tx + (wm >> 1): transposed store above the diagonal
-  const bool mirror = sym && ty > 2 * tx + (wm >> 1);
-  if (NT == 0 && interior && ldo <= (1 << 21)) {
-    // interior tile (all but the last row / column of tiles): no bounds tests,
-    // so no branch per value; |x|^2 and shifts read as 4-row vectors (one LDS
-    // round trip per 4 values); stores at 32-bit offsets from uniform bases
-    // (the generic loop below waited out one LDS round trip per value)
-    typedef int i4v __attribute__((ext_vector_type(4)));
-    float* const ob = out + m0 * ldo + n0;  // direct block
-    float* const mb = out + n0 * ldo + m0;  // mirrored block
-    const uint32_t ld = (uint32_t)ldo;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int cl = wn * 64 + 32 * j + (lane & 31);
-      const float bsq = s_sq[TM + cl];
-      const int bsh = s_sh[TM + cl];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int lr0 = wm * 64 + 32 * i + 4 * hl;  // value r sits on row lr0 + 8 (r >> 2) + (r & 3)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
-          const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * g);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(ash[e] + bsh));
-            H[i][j][r] = rbf_from_dot(asq[e], bsq, dot, gamma);
-            ob[(uint32_t)(lr0 + 8 * g + e) * ld + (uint32_t)cl] = H[i][j][r];
-          }
-        }
-        if (mirror) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            f4 v;
-            v.x = H[i][j][4 * q + 0];
-            v.y = H[i][j][4 * q + 1];
-            v.z = H[i][j][4 * q + 2];
-            v.w = H[i][j][4 * q + 3];
-            *(f4*)(mb + (uint32_t)cl * ld + (uint32_t)(lr0 + 8 * q)) = v;
-          }
-        }
-      }
-    }
-    return;
-  }
+  // ---- epilogue, one 32 x 32 MFMA tile at a time: values, direct stores,
+  // transposed stores.  ONE code path for interior and edge tiles: a second,
+  // interior-only copy (round 4) made the compiler spill 396 B of the live
+  // accumulators to scratch (175 scratch instructions).  |x|^2 and shifts are
+  // read as 4-row vectors (one LDS round trip per 4 values), stores go to
+  // 32-bit offsets from uniform tile bases (host: ldo < 2^24) under a row /
+  // column mask that is all-true on interior tiles ----
+  typedef int i4v __attribute__((ext_vector_type(4)));
+  const bool mirror = sym && ty > 2 * tx + (wm >> 1);  // this wave's 64 rows lie in 128-row block 2 tx + (wm >> 1)
+  float* const ob = out + m0 * ldo + n0;  // direct block
+  float* const mb = out + n0 * ldo + m0;  // mirrored block (symmetric: M == N)
+  const uint32_t ld = (uint32_t)ldo;
+  const int rlim = (int)min<int64_t>(M - m0, TM);  // tile rows inside [0, M)
+  const int clim = (int)min<int64_t>(N - n0, TN);  // tile columns inside [0, N)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int cb = TM + wn * 64 + 32 * j + (lane & 31);
-    const float bsq = s_sq[cb];
-    const int bsh = s_sh[cb];
-    const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+    const int cl = wn * 64 + 32 * j + (lane & 31);
+    const bool okc = cl < clim;
+    const float bsq = s_sq[TM + cl];
+    const int bsh = s_sh[TM + cl];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      const int lr0 = wm * 64 + 32 * i + 4 * hl;  // value r sits on row lr0 + 8 (r >> 2) + (r & 3)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int lr = wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(s_sh[lr] + bsh));
-        H[i][j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
-        const int64_t row = m0 + lr;
-        if (NT == 2 && !(H[i][j][r] != H[i][j][r])) continue;
-        if (interior || (row < M && col < N)) {
-          if constexpr (NT == 1) __builtin_nontemporal_store(H[i][j][r], out + row * ldo + col);
-          else out[row * ldo + col] = H[i][j][r];
+      for (int g = 0; g < 4; ++g) {
+        const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
+        const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e, lr = lr0 + 8 * g + e;
+          const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(ash[e] + bsh));
+          H[i][j][r] = rbf_from_dot(asq[e], bsq, dot, gamma);
+          if (NT == 2 && !(H[i][j][r] != H[i][j][r])) continue;
+          if (okc && lr < rlim) {
+            float* dst = ob + ((uint32_t)lr * ld + (uint32_t)cl);
+            if constexpr (NT == 1) __builtin_nontemporal_store(H[i][j][r], dst);
+            else *dst = H[i][j][r];
+          }
         }
       }
       if (mirror && NT != 2) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int64_t row = m0 + wm * 64 + 32 * i + 8 * q + 4 * hl;
-          float* dst = out + col * ldo + row;
+          const int lr = lr0 + 8 * q;
+          float* dst = mb + ((uint32_t)cl * ld + (uint32_t)lr);
           f4 v;
           v.x = H[i][j][4 * q + 0];
           v.y = H[i][j][4 * q + 1];
           v.z = H[i][j][4 * q + 2];
           v.w = H[i][j][4 * q + 3];
-          if (interior || (col < M && row + 3 < N)) {
+          if (okc && lr + 3 < rlim) {
             if constexpr (NT == 1) __builtin_nontemporal_store(v, (f4*)dst);
             else *(f4*)dst = v;
-          } else if (col < M) {
+          } else if (okc) {
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-              if (row + c < N) dst[c] = v[c];
+              if (lr + c < rlim) dst[c] = v[c];
           }
         }
       }
@@ -1452,7 +1423,8 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // default from 5 k blocks: the wide-wave LDS-DMA kernel (60000^2 x 784
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
-  if ((variant == 5 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0) {
+  // (32-bit store offsets inside a 256 x 128 tile: ldo < 2^24)
+  if ((variant == 5 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 && ldo < (1ll << 24)) {
     static const int nt = [] {
       const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
       return e ? atoi(e) : 0;
