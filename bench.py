@@ -187,6 +187,13 @@ def spawn_ranks(a, argv) -> int:
             return 2
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if os.environ.get("DPSVM_FORCE_DEVICE"):
+        # rehearsal: N ranks share one device.  With HIP's default of 4 hardware
+        # queues per process, 8 processes oversubscribe the device's queues and the
+        # scheduler time-slices them: a round's spinning consumers then wait out
+        # whole quanta for a descheduled peer's pushes (8-rank headline 2.30 s
+        # vs 0.065 s with 2 queues each, profiles/r5_rehearsal_queues_1gpu.txt)
+        env.setdefault("GPU_MAX_HW_QUEUES", "2")
     env["DPSVM_BENCH_SPAWNED"] = str(n)
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
@@ -363,6 +370,7 @@ def main(argv=None) -> int:
                            "b": s_res["b"], "smo_loop_s": round(float(s_res["t_solve"]), 6),
                            "gram_gemm_s": round(float(s_res.get("t_gram", 0.0)), 6),
                            "engine": s_info.get("iteration"), "exchange": s_info.get("exchange"),
+                           "ws_exchange": s_info.get("ws_exchange"), "engine_note": s_info.get("engine_note", ""),
                            "exchange_mem": s_info.get("exchange_mem"),
                            "geometry": f"{s_info.get('rows_per_group')}x{s_info.get('groups')}",
                            "us_per_iter": round(1e6 * float(s_res["t_solve"]) / max(1, int(s_res["iters"])), 3),
@@ -435,6 +443,15 @@ def main(argv=None) -> int:
                          np.sign(d_ws) == np.sign(d_ref))), "rows_compared": int(len(rows))}
         del r_solver
 
+    policy = info.get("dp_policy", "shard")
+    if n_ranks > 1 and dp_choice is None:
+        # always both data-parallel policies' times at N > 1 where measured: the
+        # sharded time next to a replicated one (a replicated solve is not a
+        # scaling point), the timed run's own time for the policy it used
+        dp_choice = {"replicate_s": round(per_run, 6) if policy == "replicate" else None,
+                     "shard_s": (round(per_run, 6) if policy != "replicate" else
+                                 (shard_check or {}).get("s")),
+                     "chosen": "replicate" if policy == "replicate" else "shard"}
     if ctx.rank == 0:
         # the reference publishes numbers for the MNIST config only (README.md:23)
         headline = a.config == "mnist" and a.data == "mnist" and a.samples == 60000 and a.features == 784
@@ -461,7 +478,11 @@ def main(argv=None) -> int:
                 "model": f"RBF C-SVM, modified SMO (C={a.C:g}, gamma={a.gamma:g}, tol={a.eps:g})",
                 "global_batch": a.samples,
                 "seq_len": a.features,
-                "parallelism": f"dp{n_ranks}",
+                # dpN-shard: the rows split over N ranks (each rank a shard of f, Gram
+                # columns / cache lines); replicateN: every rank solves the whole
+                # problem (no communication; NOT a strong-scaling point)
+                "parallelism": ("dp1" if n_ranks == 1 else
+                                f"replicate{n_ranks}" if policy == "replicate" else f"dp{n_ranks}-shard"),
             },
             "iterations": int(res["iters"]),
             "rounds": int(res.get("outer", 0)),
@@ -491,6 +512,8 @@ def main(argv=None) -> int:
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
             "exchange": info.get("exchange", "none"),
+            # working-set rounds: peer (in-kernel pushes) | collectives | loopback | none
+            "ws_exchange": info.get("ws_exchange", "none"),
             "exchange_mem": info.get("exchange_mem", "none"),
             "dp_policy": info.get("dp_policy", "shard"),
             "geometry": f"{info.get('rows_per_group', 0)}x{info.get('groups', 0)}",

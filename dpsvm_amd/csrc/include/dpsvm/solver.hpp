@@ -68,6 +68,10 @@ struct GpuSetupInfo {
   std::string iteration;  // engine: "persistent-dense" | "fused-dense" | "persistent-cache" | "fused-cache" | "chain"
   std::string exchange;   // per-iteration key exchange: "none" | "allreduce" | "peer" | "loopback" (1 rank)
   std::string exchange_mem = "none";  // peer exchange receive buffer: "uncached" (across devices) | "coarse"
+  // working-set engines: how a round's candidate lists, sub-Gram entries and
+  // line-search partials cross ranks — "peer" (in-kernel pushes, no collective),
+  // "collectives" (all-gather / sum all-reduce per round), "none" (one rank)
+  std::string ws_exchange = "none";
   std::string dp_policy = "shard";    // "shard" (rows split over ranks) | "replicate" (every rank solves it all)
   int64_t rows_per_group = 0, groups = 0;  // fused / persistent geometry
   int poll_batch = 0;                 // publications per lane per poll round (peer exchange)

@@ -54,29 +54,16 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
   uint64_t lu[kWsCand1], ll[kWsCand1];
 #pragma unroll
   for (int r = 0; r < kWsCand1; ++r) lu[r] = ll[r] = kKeyNone;
-  bool ok = true;
-  const uint64_t xt = xtag((uint32_t)r_now + 1u);
   for (int j = 0; j < kWsListsPerThread; ++j) {
     const int slot = tid + j * kWsGatherThreads;
     if (slot >= G) break;
+    // every rank's lists: all-gathered, or (peer exchange) collected from this
+    // rank's receive buffer by ws_xcollect_cand — the merge never spins
     uint64_t cu[kWsCand1], cl[kWsCand1];
-    if (a.xpeer == nullptr) {
 #pragma unroll
-      for (int r = 0; r < kWsCand1; ++r) {
-        cu[r] = a.cand[(size_t)slot * 2 * kWsCand + r];
-        cl[r] = a.cand[(size_t)slot * 2 * kWsCand + kWsCand + r];
-      }
-    } else {
-      // peer exchange: poll slot `slot` of this rank's buffer (up keys at 0,
-      // low keys at a.xcw / 2: ws_select's push)
-      const uint64_t* e = a.xpeer[a.xrank] + ws_xcand(a, par, slot);
-      uint64_t gu[2 * kWsCand1], gl[2 * kWsCand1];
-      ok = ok && ws_poll<2 * kWsCand1>(a, e, xt, gu) && ws_poll<2 * kWsCand1>(a, e + a.xcw / 2, xt, gl);
-#pragma unroll
-      for (int r = 0; r < kWsCand1; ++r) {
-        cu[r] = ws_get64(gu[2 * r], gu[2 * r + 1]);
-        cl[r] = ws_get64(gl[2 * r], gl[2 * r + 1]);
-      }
+    for (int r = 0; r < kWsCand1; ++r) {
+      cu[r] = a.cand[(size_t)slot * 2 * kWsCand + r];
+      cl[r] = a.cand[(size_t)slot * 2 * kWsCand + kWsCand + r];
     }
     if (j == 0) {
 #pragma unroll
@@ -88,10 +75,6 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
       ws_top4_merge(lu, cu);
       ws_top4_merge(ll, cl);
     }
-  }
-  if (a.xpeer != nullptr && !__syncthreads_and(ok)) {
-    ws_comm_fail(a, c);
-    return false;
   }
   // ---- global minima (stop test) ----
   uint64_t gu = lu[0], gl = ll[0];
@@ -274,8 +257,10 @@ __device__ bool ws_merge(const WsArgs& a, WsCtrl* c, int32_t* s_idx, int* q_out,
 // the f) of rows it owns and zeros the rest, so at world > 1 one sum all-reduce
 // assembles the exact matrix (each entry has exactly one owner).  Rows ra >= q
 // are zeroed.
+// Peer exchange: xr is the row's slot in the receive buffers (block p's row
+// ra of a multi-block round: p q_max + ra).
 __device__ __forceinline__ void ws_gather_row(const WsArgs& a, WsCtrl* c, const int32_t* s_idx, int q, int ra,
-                                              const float* line) {
+                                              const float* line, int xr) {
   const int tid = threadIdx.x;
   float* dst = a.subg + (size_t)ra * a.q_max;
   if (ra >= q) {
@@ -285,49 +270,33 @@ __device__ __forceinline__ void ws_gather_row(const WsArgs& a, WsCtrl* c, const 
   }
   const int64_t lo = a.off, hi = a.off + a.nl;
   if (a.xpeer != nullptr) {
-    // peer exchange: push the owned entries of row ra (+ its f) to every rank,
-    // then poll this rank's copy of the row (q_max <= 192 < 256: one column per
-    // thread, the last thread takes f)
+    // peer exchange: push the owned entries of row ra (+ its f) into row ra of
+    // every rank's receive buffer and return — ws_solve polls the rows (push
+    // only: no gather workgroup waits for a peer, so ranks sharing a device
+    // never park q_max spinning workgroups on it).  alpha / y are global: local aux.
     const int64_t R = c->outer;
     const uint64_t t = xtag((uint32_t)R + 1u);
-    const int64_t row = ws_xrow(a, (int)(R & 1), ra);
-    constexpr int kF = kWsGatherThreads - 1;
+    const int64_t row = ws_xrow(a, (int)(R & 1), xr);
     const int64_t gi = s_idx[ra];
-    if (tid < q) {
-      const int64_t gj = s_idx[tid];
-      if (gj >= lo && gj < hi) {
-        const uint64_t v = t | __float_as_uint(line[gj - lo]);
-        for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + tid, v);
+    for (int col = tid; col <= q; col += kWsGatherThreads) {
+      uint64_t v;
+      int at;
+      if (col < q) {
+        const int64_t gj = s_idx[col];
+        if (gj < lo || gj >= hi) continue;
+        v = t | __float_as_uint(line[gj - lo]);
+        at = col;
+      } else {  // the row's f, last column
+        if (gi < lo || gi >= hi) continue;
+        v = t | __float_as_uint(a.f[gi - lo]);
+        at = a.q_max;
       }
-    } else if (tid == kF && gi >= lo && gi < hi) {
-      const uint64_t v = t | __float_as_uint(a.f[gi - lo]);
-      for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + a.q_max, v);
-    }
-    bool ok = true;
-    const int col = tid < q ? tid : tid == kF ? a.q_max : -1;
-    if (col >= 0) {
-      const uint64_t* g = a.xpeer[a.xrank] + row + col;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint64_t v = xch_load<true>(g);
-      while (!ws_tag_ok(v, t)) {
-        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > a.xtimeout_ticks) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        v = xch_load<true>(g);
-      }
-      const float fv = __uint_as_float((uint32_t)v);
-      if (tid == kF) a.aux[ra] = fv;
-      else dst[tid] = fv;
-    } else if (tid < a.q_max) {
-      dst[tid] = 0.f;
+      for (int p = 0; p < a.world; ++p) xch_store<true>(a.xpeer[p] + row + at, v);
     }
     if (tid == 0) {
       a.aux[a.aux_stride + ra] = a.alpha[gi];
       a.aux[2 * a.aux_stride + ra] = a.y[gi];
     }
-    if (!__syncthreads_and(ok)) ws_comm_fail(a, c);
     return;
   }
   for (int b = tid; b < a.q_max; b += kWsGatherThreads) {
@@ -369,7 +338,8 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
       c->b_lo = b_lo;
     }
   }
-  ws_gather_row(a, c, s_idx, q, blockIdx.x, blockIdx.x < q ? a.gram + (int64_t)s_idx[blockIdx.x] * a.ldg : nullptr);
+  ws_gather_row(a, c, s_idx, q, blockIdx.x, blockIdx.x < q ? a.gram + (int64_t)s_idx[blockIdx.x] * a.ldg : nullptr,
+                blockIdx.x);
   if (lead) WS_STAMP(8);
 }
 
@@ -464,12 +434,12 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_lines_kernel(WsArg
   const int q = c->q[par];
   const int ra = blockIdx.x;
   if (ra >= q) {
-    ws_gather_row(a, c, s_idx, q, ra, nullptr);
+    ws_gather_row(a, c, s_idx, q, ra, nullptr, ra);
     return;
   }
   for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][t];
   __syncthreads();
-  ws_gather_row(a, c, s_idx, q, ra, a.gram + (int64_t)c->line[par][ra] * a.ldg);
+  ws_gather_row(a, c, s_idx, q, ra, a.gram + (int64_t)c->line[par][ra] * a.ldg, ra);
   if (tid == 0 && ra == 0) WS_STAMP(8);
 }
 
@@ -549,13 +519,21 @@ __global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsAr
   if (c->done != kRunning) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(15);
   const int e = (int)(blockIdx.x * kXCollectThreads + threadIdx.x);  // (list, side, rank) key
+  // keys per side the previous round's selection pushed: kWsCand by pass 2 of a
+  // multi-block round (and the seed), kWsCand1 by a one-block round — also in the
+  // one-block rounds of a multi-block engine, whose slots stay kWsCand wide
+  const int nk = a.blocks > 1 ? kWsCand : kWsCand1;
   bool ok = true;
   if (e < a.G_all * 2 * kWsCand) {
     const int l = e / (2 * kWsCand), side = (e / kWsCand) & 1, r = e % kWsCand;
-    uint64_t g[2];
-    ok = ws_poll<2>(a, a.xpeer[a.xrank] + ws_xcand(a, (int)(c->outer & 1), l) + side * (a.xcw / 2) + 2 * r,
-                    xtag((uint32_t)c->outer + 1u), g);
-    a.cand[e] = ok ? ws_get64(g[0], g[1]) : kKeyNone;
+    if (r < nk) {
+      uint64_t g[2];
+      ok = ws_poll<2>(a, a.xpeer[a.xrank] + ws_xcand(a, (int)(c->outer & 1), l) + side * (a.xcw / 2) + 2 * r,
+                      xtag((uint32_t)c->outer + 1u), g);
+      a.cand[e] = ok ? ws_get64(g[0], g[1]) : kKeyNone;
+    } else {
+      a.cand[e] = kKeyNone;  // not pushed (the one-block merge reads kWsCand1 keys a side)
+    }
   }
   if (!ok) ws_comm_fail_thread(a, c);
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(16);
@@ -879,50 +857,16 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_multi_kernel(WsArg
   WsArgs b = a;
   b.subg = a.subg + (size_t)p * a.q_max * a.q_max;
   b.aux = a.aux + (size_t)p * kWsMax;  // f / alpha / y of block p at stride aux_stride
-  if (a.xpeer != nullptr) {
-    // peer exchange: push the entries (ra, b) of the columns this rank owns and
-    // the row's f (when owned) into row p q_max + ra of every rank's buffer;
-    // ws_solve polls them (no workgroup of this kernel waits: rows past q need
-    // nothing, the solve zero-fills them).  alpha / y are global: local aux.
-    if (ra >= q) return;
-    for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][p * a.q_max + t];
-    __syncthreads();
-    const int64_t line = a.cache ? (int64_t)c->line[par][p * a.q_max + ra] : (int64_t)s_idx[ra];
-    const float* src = a.gram + line * a.ldg;
-    const int64_t lo = a.off, hi = a.off + a.nl, gi = s_idx[ra];
-    const uint64_t t = xtag((uint32_t)c->outer + 1u);
-    const int64_t row = ws_xrow(a, par, p * a.q_max + ra);
-    for (int col = tid; col <= q; col += kWsGatherThreads) {
-      uint64_t v;
-      int at;
-      if (col < q) {
-        const int64_t gj = s_idx[col];
-        if (gj < lo || gj >= hi) continue;
-        v = t | __float_as_uint(src[gj - lo]);
-        at = col;
-      } else {  // the row's f, last column
-        if (gi < lo || gi >= hi) continue;
-        v = t | __float_as_uint(a.f[gi - lo]);
-        at = a.q_max;
-      }
-      for (int r = 0; r < a.world; ++r) xch_store<true>(a.xpeer[r] + row + at, v);
-    }
-    if (tid == 0) {
-      b.aux[a.aux_stride + ra] = a.alpha[gi];
-      b.aux[2 * a.aux_stride + ra] = a.y[gi];
-    }
-    if (tid == 0 && blockIdx.x == 0) WS_STAMP(8);
-    return;
-  }
+  if (a.xpeer != nullptr && ra >= q) return;  // peer exchange: ws_solve zero-fills rows past q
   if (ra >= q) {
-    ws_gather_row(b, c, s_idx, q, ra, nullptr);
+    ws_gather_row(b, c, s_idx, q, ra, nullptr, p * a.q_max + ra);
     return;
   }
   for (int t = tid; t < q; t += kWsGatherThreads) s_idx[t] = c->idx[par][p * a.q_max + t];
   __syncthreads();
   // the row's line (dense: the resident Gram's row itself)
   const int64_t line = a.cache ? (int64_t)c->line[par][p * a.q_max + ra] : (int64_t)s_idx[ra];
-  ws_gather_row(b, c, s_idx, q, ra, a.gram + line * a.ldg);
+  ws_gather_row(b, c, s_idx, q, ra, a.gram + line * a.ldg, p * a.q_max + ra);
   if (tid == 0 && blockIdx.x == 0) WS_STAMP(8);
 }
 

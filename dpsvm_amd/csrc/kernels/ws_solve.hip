@@ -14,6 +14,9 @@
 namespace dpsvm {
 namespace dev {
 
+// peer exchange: sub-Gram granules in flight per solve thread and poll batch
+constexpr int kWsSolvePollBatch = 10;
+
 // ---------------------------------------------------------------------------
 // ws_solve: the sub-problem on wave 0
 // ---------------------------------------------------------------------------
@@ -163,18 +166,18 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const float* subg = a.subg + (size_t)blk * ldk * ldk;
   const float* aux = a.aux + (size_t)blk * kWsMax;
   bool xok = true;
-  if (kMulti && a.xpeer != nullptr) {
+  if (a.xpeer != nullptr) {
     // peer exchange: block blk's rows a < q from this rank's receive buffer,
-    // entries (a, b < q) and f (last column) pushed by their owners
-    // (ws_gather_multi); columns q .. q_max - 1 are zeros
-    // A thread's granules are loaded in batches of kB (all in flight: one
-    // latency of the uncached buffer per batch), then only the ones not yet
-    // tagged are re-polled — a per-entry poll loop paid one round trip each.
+    // entries (a, b < q) and f (last column) pushed by their owners (the gather
+    // kernels push and return: the solve is the round's only sub-Gram consumer);
+    // columns q .. q_max - 1 are zeros.  A thread's granules are loaded in
+    // batches of kB (all in flight: one latency of the uncached buffer per
+    // batch), then only the ones not yet tagged are re-polled.
     const int64_t R = c->outer;
     const uint64_t t = xtag((uint32_t)R + 1u);
     const uint64_t* rows = a.xpeer[a.xrank] + ws_xrow(a, par, ib);  // row ra at + ra * (ldk + 1)
     const int w = ldk + 1, n_e = q * w;
-    constexpr int kB = 16;
+    constexpr int kB = kWsSolvePollBatch;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (int e0 = 0; e0 < n_e && xok; e0 += kB * kWsSolveThreads) {
       uint64_t v[kB];
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     }
   }
   bool xfail = false;
-  if (kMulti && a.xpeer != nullptr) xfail = !__syncthreads_and(xok);
+  if (a.xpeer != nullptr) xfail = !__syncthreads_and(xok);
   else __syncthreads();
   // a rank stopped publishing: this block takes no step; its commit below still
   // counts it, and the round's last block keeps kCommFail
@@ -392,10 +395,14 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   if (lane == 0 && !kMulti) {
     WS_STAMP(4);
     if (a.stamps) a.stamps[(size_t)(c->outer % kStampRing) * 2 * kStampSlots + 5] = (uint64_t)inner;
-    c->n_apply = n_apply;
     c->iter = it0 + inner;
     c->outer = c->outer + 1;
-    c->done = bad ? kNonFinite : inner == 0 ? kNoPair : (it0 + inner >= a.max_iter ? kMaxIter : kRunning);
+    if (xfail) {
+      c->n_apply = 0;  // the exchange poll gave up (peer exchange): the run ends here, kCommFail kept
+    } else {
+      c->n_apply = n_apply;
+      c->done = bad ? kNonFinite : inner == 0 ? kNoPair : (it0 + inner >= a.max_iter ? kMaxIter : kRunning);
+    }
     ws_status(a.status, c);
   }
   if (lane == 0 && kMulti) {

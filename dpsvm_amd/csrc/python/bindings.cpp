@@ -143,6 +143,7 @@ py::dict setup_dict(const GpuSetupInfo& i) {
   d["iteration"] = i.iteration;
   d["exchange"] = i.exchange;
   d["exchange_mem"] = i.exchange_mem;
+  d["ws_exchange"] = i.ws_exchange;
   d["cache_lines"] = i.cache_lines;
   d["blocks"] = i.blocks;
   d["bytes_device"] = i.bytes_device;

@@ -468,9 +468,10 @@ struct WsRounds : Base {
     }
   }
   static void round(GpuSolver::Impl& m, const WsArgs& w) {
-    // multi-block rounds over the peer exchange: the candidate lists every rank
-    // pushed at the end of the previous round (or the seed), collected in-kernel
-    if (w.blocks > 1 && w.xpeer) launch::ws_xcollect_cand(w, m.stream);
+    // peer exchange: the candidate lists every rank pushed at the end of the
+    // previous round (or the seed), collected in-kernel by a few workgroups (the
+    // merge then reads them as from the all-gather and never spins)
+    if (w.xpeer) launch::ws_xcollect_cand(w, m.stream);
     if (w.blocks > 1) launch::ws_merge_multi(w, m.stream);
     else if (kCache) launch::ws_merge(w, m.stream);  // ws-dense one-block rounds merge inside ws_gather
     if (kCache) miss_rows(m, w);

@@ -549,27 +549,24 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                     (int64_t)ws_G * m.world <= kWsMaxGroups;
   if (m.world > 1) multi_elig = m.all_agree(multi_elig, m.comm, m.world);
   // Residency of the ws peer exchange with ranks sharing a device (rehearsals;
-  // on distinct devices share = 1).  One-block rounds: gather workgroup a of
-  // every rank spins until the same workgroup of every other rank has pushed its
-  // row, so the other ranks' spinning gathers — (share - 1) x q_max workgroups,
-  // one per CU at worst — must leave a CU free for this rank's solve workgroup.
-  // Multi-block rounds: no producer waits (selection and gather workgroups
-  // push); the spinning consumers of one rank are the two collect kernels (<= 16
-  // workgroups of 4 waves) and the solve (P workgroups of 16 waves), and the
-  // share ranks' solves plus one rank's full-size producer kernel (1024 waves)
-  // must fit the device's wave slots so every rank's producers still run.
-  bool ws_xch_resident = true, multi_xch_resident = true;
+  // on distinct devices share = 1).  No producer ever waits: selection, gather
+  // and pass-1 workgroups push into every rank's receive buffer and return.  The
+  // spinning consumers of one rank are the collect kernels (<= 16 workgroups of
+  // 4 waves) and the solve (one workgroup of 16 waves per block), so the share
+  // ranks' consumers plus one rank's full-size producer kernel (1024 waves) must
+  // fit the device's wave slots for every rank's producers to keep running —
+  // one-block and multi-block rounds alike.
+  bool xch_resident = true;
   if (m.world > 1) {
     const int share = max_device_sharing(m);  // collective
     int cus = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m.device));
-    ws_xch_resident = m.all_agree((int64_t)(share - 1) * ws_q < (int64_t)cus, m.comm, m.world);
-    multi_xch_resident =
-        m.all_agree((int64_t)share * 16 * std::max(1, want_blocks) + 1024 <= (int64_t)cus * 32, m.comm, m.world);
-    if (!ws_xch_resident && m.p.exchange != 2 && (ws_cand || wsc_fits_pre))
+    const int64_t waves = (int64_t)share * (64 + 16 * std::max(1, want_blocks)) + 1024;
+    xch_resident = m.all_agree(waves <= (int64_t)cus * 32, m.comm, m.world);
+    if (!xch_resident && m.p.exchange != 2 && (ws_cand || wsc_fits_pre))
       m.info.engine_note = "ws peer exchange refused: " + std::to_string(share) + " ranks share a device (" +
-                           std::to_string((share - 1) * ws_q) + " spinning gather workgroups >= " +
-                           std::to_string(cus) + " CUs): collectives";
+                           std::to_string(waves) + " spinning + producer waves > " + std::to_string(cus * 32) +
+                           " wave slots): collectives";
   }
   const bool ws_peer_base = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives &&
                             (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
@@ -577,7 +574,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // the miss rows by an all-reduce: that engine keeps the collectives)
   const int ks_mb = launch::ws_pass1_splits(ws_G);
   bool multi_peer = false;
-  if (ws_peer_base && multi_elig && !(wsc_cand && !m.replicated) && (multi_xch_resident || m.p.exchange == 2)) {
+  if (ws_peer_base && multi_elig && !(wsc_cand && !m.replicated) && (xch_resident || m.p.exchange == 2)) {
     const int64_t G_all = (int64_t)ws_G * m.world;
     const bool ok = m.setup_exchange(ws_xch_words_multi(G_all, ks_mb, want_blocks, mb_q, ws_q));
     DPSVM_CHECK(ok || m.p.exchange != 2,
@@ -590,7 +587,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     }
   }
   const bool multi_ok = multi_elig && (multi_peer || (multi_comm && m.p.exchange != 2));
-  const bool want_ws_xch = ws_peer_base && !multi_ok && (ws_xch_resident || m.p.exchange == 2);
+  const bool want_ws_xch = ws_peer_base && !multi_ok && (xch_resident || m.p.exchange == 2);
   if (want_ws_xch) {
     const bool ok = m.setup_exchange(ws_xch_words((int64_t)ws_G * m.world, ws_q));
     DPSVM_CHECK(ok || m.p.exchange != 2,
@@ -796,6 +793,12 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   m.info.exchange_mem = m.xch ? m.xch_mem : "none";
   m.info.exchange = m.xch ? (m.world > 1 ? "peer" : "loopback")
                           : (m.world > 1 || m.p.force_collectives ? "allreduce" : "none");
+  if (m.working_set()) {
+    m.info.ws_exchange = m.wsa.xpeer ? (m.world > 1 ? "peer" : "loopback")
+                                     : (m.collectives() ? "collectives" : "none");
+    // partitioned X in cache mode also sums each round's packed miss rows
+    if (m.wsa.xpeer && m.ws_round_collectives()) m.info.ws_exchange += "+rows-allreduce";
+  }
   m.info.rows_per_group = m.working_set() ? (int64_t)m.wsa.rpt * kWsSelThreads : m.fused() ? m.RBf : kStepRows;
   m.info.groups = m.working_set() ? m.wsa.G : m.fused() ? m.Gf : m.G;
   m.info.poll_batch = m.xch && !m.working_set() ? launch::poll_batch(a) : 0;

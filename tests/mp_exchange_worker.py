@@ -32,7 +32,9 @@ def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
            "exchange_mem": clf.setup_info_["exchange_mem"],
            "iters": int(clf.n_iter_), "rounds": int(getattr(clf, "n_rounds_", 0) or 0), "b": float(clf.b_),
            "alpha_sha": hashlib.sha256(clf.alpha_.tobytes()).hexdigest(),
-           "ws_blocks": int(clf.stats_.get("ws_blocks", 1) or 1), "engine_note": clf.setup_info_.get("engine_note", "")}
+           "ws_blocks": int(clf.stats_.get("ws_blocks", 1) or 1), "engine_note": clf.setup_info_.get("engine_note", ""),
+           "ws_exchange": clf.setup_info_.get("ws_exchange", "none"),
+           "ws_p1_round": int(clf.stats_.get("ws_p1_round", 0) or 0)}
     with open(f"{out}.rank{ctx.rank}.json", "w") as f:
         json.dump(rec, f)
     del comm

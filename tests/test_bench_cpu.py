@@ -45,7 +45,8 @@ def test_bench_multirank_launch_contract():
     lines = [l for l in r.stdout.strip().split("\n") if l.startswith("{")]
     assert len(lines) == 1, lines
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4" and out["converged"]
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4-shard" and out["converged"]
+    assert out["dp_autotune"]["shard_s"] == out["value"] and out["dp_autotune"]["chosen"] == "shard"
     assert out["steps"] == 1 and out["warmup"] == 1 and out["value"] > 0
 
 
@@ -58,7 +59,7 @@ def test_bench_spawns_its_own_ranks():
     lines = [l for l in r.stdout.strip().split("\n") if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["converged"]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2-shard" and out["converged"]
     assert out["launcher"].startswith("bench.py spawned")
 
 

@@ -442,6 +442,52 @@ def test_ws_multi_block_peer_exchange_processes_one_gpu(tmp_path, world, clip):
         assert res[k]["alpha_sha"] == sha
 
 
+@pytest.mark.parametrize("clip", ["independent", "box"])
+@pytest.mark.parametrize("knobs", [{"ws_blocks": 4}, {"ws_blocks": 1}])
+def test_ws_peer_exchange_eight_processes_one_gpu(tmp_path, clip, knobs):
+    """EIGHT ranks as processes sharing the GPU (the rank count of the 8-GPU
+    node) at the default working-set size: every producer pushes and returns,
+    only the collect kernels and the solve poll, so eight ranks' spinning
+    consumers leave the device room for every rank's producers.  Multi-block
+    rounds on covtype-shape data fall to one block mid-run (damped rounds), so
+    the one-block rounds of a multi-block engine run over the exchange too.
+    Bit-identical to the same 8 ranks over host-staged collectives, in both
+    clipping modes."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from dpsvm_amd._native import load
+
+    world = 8
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
+    out = tmp_path / "ws8"
+    port = 29760 + (1 if clip == "box" else 0) + (2 if knobs["ws_blocks"] > 1 else 0)
+    kn = dict(knobs, clip=clip)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), "ws", "6000", json.dumps(kn)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    errs = "".join(open(f"{out}.rank{k}.err").read()[-1500:] for k in range(world)
+                   if os.path.exists(f"{out}.rank{k}.err"))
+    assert r.returncode == 0, errs + r.stderr[-2000:]
+    res = [json.load(open(f"{out}.rank{k}.json")) for k in range(world)]
+    X, y = synthetic("covtype", n=6000, seed=2)
+    kw = dict(C=4.0, gamma=0.5, eps=1e-3, device="cuda", solver="ws", dp="shard", **kn)
+    ref = _fit_threads(load(), world, X, y, exchange="allreduce", **kw)
+    sha = hashlib.sha256(ref[0].alpha_.tobytes()).hexdigest()
+    for k in range(world):
+        assert res[k]["ws_exchange"] == "peer" and res[k]["engine_note"] == "", res[k]
+        assert ref[k].setup_info_["ws_exchange"] == "collectives"
+        assert res[k]["iters"] == ref[0].n_iter_ and res[k]["rounds"] == ref[0].n_rounds_
+        assert res[k]["alpha_sha"] == sha
+    if knobs["ws_blocks"] > 1:  # the one-block switch ran under the peer exchange
+        assert res[0]["ws_blocks"] == 4 and res[0]["ws_p1_round"] > 0, res[0]
+
+
 @pytest.mark.parametrize("blocks", [2, 8])
 @pytest.mark.parametrize("clip", ["independent", "box"])
 @pytest.mark.parametrize("case", ["blobs", "mnist", "adult"])
