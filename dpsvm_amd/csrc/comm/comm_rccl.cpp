@@ -131,6 +131,29 @@ class RcclComm final : public Communicator {
 
 }  // namespace
 
+void sync_collective(Communicator* c, hipStream_t stream, const char* what, double limit_s) {
+  const double limit = limit_s > 0.0 ? limit_s : kWatchdogDefaultS;
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool multi = c != nullptr && c->size() > 1;
+  for (int spins = 0;; ++spins) {
+    const hipError_t q = hipStreamQuery(stream);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIP_CHECK(q);
+    if (multi) {
+      const std::string err = c->async_error();
+      if (!err.empty()) {
+        c->abort();
+        ::dpsvm::fail(std::string(what) + ": collective failed on rank " + std::to_string(c->rank()) + ": " + err);
+      }
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+      if (multi) c->abort();
+      ::dpsvm::fail(std::string(what) + ": collective did not finish within " + std::to_string(limit) + " s");
+    }
+    if (spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 std::vector<uint8_t> rccl_unique_id() {
   ncclUniqueId id;
   RCCL_CHECK(ncclGetUniqueId(&id));

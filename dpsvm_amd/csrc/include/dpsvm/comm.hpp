@@ -56,6 +56,13 @@ class Communicator {
 
 std::unique_ptr<Communicator> make_local_comm();
 
+// Wait for `stream` after a device communicator's collective, bounded: polls
+// the stream, the communicator's async error (which also carries out an abort
+// another rank thread requested: a collective blocked on a failed peer ends
+// instead of hanging the waiting rank forever) and a time limit (seconds;
+// <= 0: the watchdog default).  Fails (dpsvm::fail) with `what` on error.
+void sync_collective(Communicator* c, hipStream_t stream, const char* what, double limit_s = 0.0);
+
 // ThreadComm: create a group once, then hand comm(r) to thread r.
 class ThreadCommGroup {
  public:

@@ -15,6 +15,10 @@
 //                        K: in-process ranks (svmTrain --ranks / -p) must
 //                        abort their peers' communicators and report rank R's
 //                        error as the root cause.
+//   DPSVM_FAULT=throwphase@P:R  rank R throws right after shrinking phase P
+//                        (gpu_shrink.cpp): its peers are then blocked in the
+//                        phase boundary's collectives, which must end through
+//                        the abort (bounded waits, sync_collective).
 //   DPSVM_VERIFY=1       after solve: alpha in [0, C], f recomputed from alpha,
 //                        and the cross-rank alpha digest (the digest alone runs
 //                        by default at world > 1: SolverParams::verify_ranks).
@@ -82,6 +86,8 @@ inline int64_t fault_rank_iter(const char* kind, int rank) {
 inline int64_t fault_exit_iter(int rank) { return fault_rank_iter("exit@", rank); }
 // DPSVM_FAULT=throw@K:R -> K when this is rank R, else -1
 inline int64_t fault_throw_iter(int rank) { return fault_rank_iter("throw@", rank); }
+// DPSVM_FAULT=throwphase@P:R -> P when this is rank R, else -1
+inline int64_t fault_throw_phase(int rank) { return fault_rank_iter("throwphase@", rank); }
 
 inline bool verify_enabled() {
   const char* e = std::getenv("DPSVM_VERIFY");

@@ -205,7 +205,8 @@ struct DenseBase : Engine {
                                m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);
       }
     }
-    HIP_CHECK(hipStreamSynchronize(m.stream));
+    if (m.world > 1 && m.comm->device_memory()) sync_collective(m.comm, m.stream, "Gram panel broadcast");
+    else HIP_CHECK(hipStreamSynchronize(m.stream));
     (void)hipFree(panel);
     if (pxs) (void)hipFree(pxs);
     if (pxsh) (void)hipFree(pxsh);

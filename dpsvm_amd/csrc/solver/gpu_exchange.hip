@@ -17,7 +17,7 @@ using gpu::dmalloc;
 
 void GpuSolver::Impl::allreduce_keys(uint64_t* buf, int64_t count) {
   if (comm->device_memory()) {
-    comm->allreduce_min_u64(buf, (size_t)count, stream);
+    comm->allreduce_min_u64(buf, (size_t)count, stream);  // in the iteration stream (waits: wait_event)
   } else {
     if ((int64_t)h_partials.size() < count) h_partials.resize((size_t)count);
     HIP_CHECK(hipMemcpyAsync(h_partials.data(), buf, 8 * count, hipMemcpyDeviceToHost, stream));
@@ -38,7 +38,7 @@ void GpuSolver::Impl::allgather_bytes(const void* send, void* recv, size_t nbyte
     HIP_CHECK(hipMemcpy(d + nbytes * world, send, nbytes, hipMemcpyHostToDevice));
     comm->allgather(d + nbytes * world, d, nbytes, stream);
     HIP_CHECK(hipMemcpyAsync(recv, d, nbytes * world, hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
+    sync_collective(comm, stream, "setup all-gather");
     (void)hipFree(d);
   } else {
     comm->allgather(send, recv, nbytes, nullptr);
@@ -54,7 +54,7 @@ bool GpuSolver::Impl::all_agree(bool mine, Communicator* c, int w) {
     HIP_CHECK(hipMemcpy(d, &v, 8, hipMemcpyHostToDevice));
     c->allreduce_min_u64(d, 1, stream);
     HIP_CHECK(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
+    sync_collective(c, stream, "setup agreement");
     (void)hipFree(d);
   } else {
     c->allreduce_min_u64(&v, 1, nullptr);

@@ -60,7 +60,7 @@ static void build_svs(GpuSolver::Impl& m, const SolveResult& r, SvSet& s) {
         HIP_CHECK(hipMemcpy(dc, cnts.data(), m.world * 8, hipMemcpyHostToDevice));
         m.comm->allreduce_sum_f64(dc, m.world, m.stream);
         HIP_CHECK(hipMemcpyAsync(cnts.data(), dc, m.world * 8, hipMemcpyDeviceToHost, m.stream));
-        HIP_CHECK(hipStreamSynchronize(m.stream));
+        sync_collective(m.comm, m.stream, "SV count all-reduce");
         (void)hipFree(dc);
       } else {
         m.comm->allreduce_sum_f64(cnts.data(), m.world, nullptr);
@@ -91,7 +91,7 @@ static void build_svs(GpuSolver::Impl& m, const SolveResult& r, SvSet& s) {
       auto gather = [&](float* buf, int64_t elems) {
         if (m.comm->device_memory()) {
           m.comm->allgather(buf + (size_t)m.rank * elems, buf, elems * 4, m.stream);
-          HIP_CHECK(hipStreamSynchronize(m.stream));
+          sync_collective(m.comm, m.stream, "SV all-gather");
         } else {
           std::vector<float> h((size_t)elems * m.world);
           HIP_CHECK(hipMemcpy(h.data() + (size_t)m.rank * elems, buf + (size_t)m.rank * elems, elems * 4,
@@ -156,7 +156,7 @@ double GpuSolver::train_accuracy(const SolveResult& r) {
       HIP_CHECK(hipMemcpy(dt, &tot, 8, hipMemcpyHostToDevice));
       m.comm->allreduce_sum_f64(dt, 1, m.stream);
       HIP_CHECK(hipMemcpyAsync(&tot, dt, 8, hipMemcpyDeviceToHost, m.stream));
-      HIP_CHECK(hipStreamSynchronize(m.stream));
+      sync_collective(m.comm, m.stream, "accuracy all-reduce");
       (void)hipFree(dt);
     } else {
       m.comm->allreduce_sum_f64(&tot, 1, nullptr);

@@ -316,7 +316,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       float* gbuf = dmalloc<float>((size_t)m.ldl * m.world, &m.bytes);
       m.comm->allgather(loc, gbuf, m.ldl * 4, m.stream);
       HIP_CHECK(hipMemcpyAsync(all.data(), gbuf, all.size() * 4, hipMemcpyDeviceToHost, m.stream));
-      HIP_CHECK(hipStreamSynchronize(m.stream));
+      sync_collective(m.comm, m.stream, "norm all-gather");
       (void)hipFree(gbuf);
     } else {
       HIP_CHECK(hipMemcpyAsync(mine.data(), loc, m.ldl * 4, hipMemcpyDeviceToHost, m.stream));

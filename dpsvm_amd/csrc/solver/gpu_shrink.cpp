@@ -42,6 +42,7 @@
 #include "dpsvm/solver.hpp"
 #include "../kernels/kernels.hpp"
 #include "../runtime/hip_check.hpp"
+#include "../runtime/trace.hpp"
 
 namespace dpsvm {
 
@@ -97,7 +98,7 @@ bool comm_all(Communicator* comm, bool mine) {
     HIP_CHECK(hipMemcpy(d, &v, 8, hipMemcpyHostToDevice));
     comm->allreduce_min_u64(d, 1, st);
     HIP_CHECK(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    sync_collective(comm, st, "shrink agreement");
     (void)hipFree(d);
     (void)hipStreamDestroy(st);
   } else {
@@ -159,7 +160,7 @@ void comm_allgather_slices(Communicator* comm, std::vector<float>& out) {
     HIP_CHECK(hipMemcpy(gb + (size_t)rank * ld, loc.data(), (size_t)ld * 4, hipMemcpyHostToDevice));
     comm->allgather(gb + (size_t)rank * ld, gb, (size_t)ld * 4, st);
     HIP_CHECK(hipMemcpyAsync(all.data(), gb, all.size() * 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    sync_collective(comm, st, "inactive-row all-gather");
     (void)hipFree(gb);
     (void)hipStreamDestroy(st);
   } else {
@@ -326,6 +327,8 @@ SolveResult ShrinkingSolver::solve(const Checkpoint* resume, const ProgressFn& p
       snprintf(buf, sizeof(buf), " %lld %.3f", (long long)r.outer, now() - t_phase);
       res.phase_log += (res.phase_log.empty() ? "" : ";") + std::to_string(na) + " " + phase_engine + buf;
     }
+    if (trace::fault_throw_phase(m.rank) == phases)
+      fail("fault injection: rank " + std::to_string(m.rank) + " throws after shrink phase " + std::to_string(phases));
     iters = r.iters;
     rounds += r.outer;
     rows_computed += r.rows_computed;

@@ -59,7 +59,7 @@ std::vector<float> GpuSolver::Impl::gather_f() {
       HIP_CHECK(hipMemcpy(gb + (size_t)rank * ldl, f, ldl * 4, hipMemcpyDeviceToDevice));
       comm->allgather(gb + (size_t)rank * ldl, gb, ldl * 4, stream);
       HIP_CHECK(hipMemcpyAsync(fall.data(), gb, fall.size() * 4, hipMemcpyDeviceToHost, stream));
-      HIP_CHECK(hipStreamSynchronize(stream));
+      sync_collective(comm, stream, "gradient all-gather");
       (void)hipFree(gb);
     } else {
       comm->allgather(floc.data(), fall.data(), ldl * 4, nullptr);
@@ -261,7 +261,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
       HIP_CHECK(hipMemcpy(dk, hk, 16, hipMemcpyHostToDevice));
       c->allreduce_min_u64(dk, 2, m.stream);
       HIP_CHECK(hipMemcpyAsync(hk, dk, 16, hipMemcpyDeviceToHost, m.stream));
-      HIP_CHECK(hipStreamSynchronize(m.stream));
+      sync_collective(c, m.stream, "alpha digest all-reduce");
       (void)hipFree(dk);
     } else {
       c->allreduce_min_u64(hk, 2, nullptr);

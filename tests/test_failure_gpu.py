@@ -91,3 +91,38 @@ def test_rccl_rank_throw_cli_reports_root_cause(tmp_path):
     assert "rank 1 failed first (root cause)" in err, err[-2000:]
     assert "fault injection: rank 1 throws" in err.strip().splitlines()[-1], err[-2000:]
     assert "rank 0 (after rank 1 failed)" in err and "aborted" in err, err[-2000:]
+
+
+def _cli_throw_phase(tmp_path, extra):
+    exe = os.path.join(ROOT, "bin", "svmTrain")
+    if not os.path.exists(exe):
+        pytest.skip("bin/svmTrain not built")
+    env = dict(os.environ, DPSVM_FAULT="throwphase@1:1")
+    t0 = time.time()
+    r = subprocess.run([exe, "-a", "54", "-x", "20000", "--synthetic", "covtype", "-c", "4", "-g", "0.5", "-m",
+                        str(tmp_path / "m.txt"), "--shrink=on", "--clip", "box", *extra],
+                       capture_output=True, text=True, timeout=180, env=env)
+    return r, time.time() - t0
+
+
+def test_thread_rank_throw_at_shrink_boundary_reports_root_cause(tmp_path):
+    """DPSVM_FAULT=throwphase@1:1: rank 1 throws right after shrinking phase 1,
+    while rank 0 goes on into the phase boundary's collectives (agreement,
+    inactive-row gather) — it must leave them through the abort and the CLI
+    must report rank 1 as the root cause, not hang."""
+    r, dt = _cli_throw_phase(tmp_path, ["--ranks", "2", "--xch-timeout", "15"])
+    assert r.returncode != 0 and dt < 150, (r.returncode, dt, r.stderr[-2000:])
+    err = r.stderr
+    assert "rank 1 failed first (root cause)" in err, err[-2000:]
+    assert "throws after shrink phase 1" in err.strip().splitlines()[-1], err[-2000:]
+
+
+def test_rccl_rank_throw_at_shrink_boundary_reports_root_cause(tmp_path):
+    """The same over RCCL (-p 2): rank 0's waits on its device collectives are
+    bounded (sync_collective polls the communicator's abort), so the owning
+    thread leaves them once rank 1 failed."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    r, dt = _cli_throw_phase(tmp_path, ["-p", "2"])
+    assert r.returncode != 0 and dt < 150, (r.returncode, dt, r.stderr[-2000:])
+    assert "rank 1 failed first (root cause)" in r.stderr, r.stderr[-2000:]
