@@ -251,6 +251,10 @@ def main(argv=None) -> int:
     # (N > 1: the solver checks a cross-rank alpha digest after every run, so a
     # diverged run fails loudly instead of reporting a time)
     C = load()
+    if a.engines == "all":
+        from dpsvm_amd._native import load_quarantine
+
+        load_quarantine()  # the quarantined pair-at-a-time cache engines (plugin)
     ctx = init_distributed(device=a.device)
     on_gpu = ctx.device.startswith("cuda")
 

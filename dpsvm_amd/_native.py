@@ -51,6 +51,29 @@ def load(build_if_missing: bool = True):
     raise ImportError(f"dpsvm_amd native extension not built: {_ERR}. Run `python -m dpsvm_amd.build`.")
 
 
+_PAIRQ = None
+
+
+def load_quarantine():
+    """Load the plugin with the quarantined pair-at-a-time cache /
+    partitioned-X engines (libdpsvm_pairq.so, next to the module; it registers
+    them with the solver when loaded).  engines="all" needs it (tests, A/B
+    probes); the production module never does."""
+    global _PAIRQ
+    if _PAIRQ is not None:
+        return _PAIRQ
+    C = load()
+    import ctypes
+
+    path = os.path.join(os.path.dirname(os.path.abspath(C.__file__)), "libdpsvm_pairq.so")
+    if not os.path.exists(path):
+        raise ImportError(f"the pair-cache plugin is not built ({path}); run `python -m dpsvm_amd.build`")
+    _PAIRQ = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    if not C.quarantine_loaded():
+        raise ImportError(f"{path} loaded but did not register its engines")
+    return _PAIRQ
+
+
 def gpu_available() -> bool:
     """True when a HIP device is usable (via torch when present)."""
     try:

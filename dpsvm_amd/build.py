@@ -1,7 +1,9 @@
 """Build the native core for MI355X (gfx950) in-tree.
 
 Products (all git-ignored, shipped to the GPU box with the snapshot):
-  dpsvm_amd/_C<EXT_SUFFIX>   pybind11 module (solver, kernels, comm, I/O)
+  dpsvm_amd/_C<EXT_SUFFIX>   pybind11 module (solver, kernels, comm, I/O): the production engines
+  dpsvm_amd/libdpsvm_pairq.so  plugin: the quarantined pair-at-a-time cache / partitioned-X
+                             engines (loaded for engines="all"; linked into the CLIs)
   bin/svmTrain               distributed trainer CLI  (reference: svmTrainMain.cpp)
   bin/svmTest                predictor CLI            (reference: seq_test.cpp / Makefile:104)
   bin/svmSeq                 CPU trainer CLI          (reference: seq.cpp)
@@ -46,18 +48,24 @@ LIB_SOURCES = [
     "solver/gpu_predict.hip",
     "solver/ws_kernel_entry.hip",
     "solver/gpu_shrink.cpp",
-    "kernels/smo_kernels.hip",
+    "kernels/setup_kernels.hip",
     "kernels/rbf_gemm.hip",
     "kernels/rbf_gemm_split.hip",
     "kernels/smo_fused.hip",
     "kernels/microbench.hip",
     "kernels/compact.hip",
-    "kernels/smo_fused_lru.hip",
     "kernels/smo_persist.hip",
-    "kernels/smo_persist_lru.hip",
     "kernels/ws_select.hip",
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
+]
+# the quarantined engines (solver/gpu_engines_pairq.hip registers them): a plugin
+# library for the Python module, linked into the CLIs (svmTrain --engines all)
+PLUGIN_SOURCES = [
+    "kernels/smo_kernels.hip",
+    "kernels/smo_fused_lru.hip",
+    "kernels/smo_persist_lru.hip",
+    "solver/gpu_engines_pairq.hip",
 ]
 CLI = {
     "svmTrain": "cli/svm_train.cpp",
@@ -79,6 +87,10 @@ def ext_suffix() -> str:
 
 def module_path() -> Path:
     return PKG / ("_C" + ext_suffix())
+
+
+def plugin_path() -> Path:
+    return PKG / "libdpsvm_pairq.so"
 
 
 def _headers_mtime() -> float:
@@ -114,11 +126,12 @@ def _compile(src: Path, obj: Path, flags: list[str], extra: list[str], force: bo
     return f"compiled {src.name}"
 
 
-def _link(out: Path, objs: list[Path], shared: bool, flags: list[str]) -> None:
+def _link(out: Path, objs: list[Path], shared: bool, flags: list[str], extra: list[str] | None = None) -> None:
     out.parent.mkdir(parents=True, exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}"] + [str(o) for o in objs] + ["-o", str(out)]
     if shared:
-        cmd += ["-shared"]
+        cmd += ["-shared", f"-Wl,-soname,{out.name}"]
+    cmd += extra or []
     cmd += [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lpthread", f"-Wl,-rpath,{ROCM / 'lib'}"]
     # sanitizer runtimes: each -fsanitize= stays paired with the -Xarch_host before it
     for i, x in enumerate(flags[:-1]):
@@ -139,7 +152,7 @@ def build(jobs: int | None = None, force: bool = False, debug: bool = False, asa
     import pybind11
 
     py_inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
-    tasks = [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in LIB_SOURCES]
+    tasks = [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in LIB_SOURCES + PLUGIN_SOURCES]
     tasks.append((CSRC / BINDINGS, objdir / "bindings.o", py_inc + ["-fvisibility=hidden"]))
     if clis:
         tasks += [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in CLI.values()]
@@ -156,13 +169,21 @@ def build(jobs: int | None = None, force: bool = False, debug: bool = False, asa
         _link(mod, lib_objs + [objdir / "bindings.o"], True, flags)
         if verbose:
             print(f"linked {mod}")
+    # the plugin resolves the solver's symbols from the module it sits next to
+    plug_objs = [objdir / (s.replace("/", "_") + ".o") for s in PLUGIN_SOURCES]
+    plug = plugin_path() if not (debug or asan) else objdir / "libdpsvm_pairq.so"
+    newest_p = max([o.stat().st_mtime for o in plug_objs] + [mod.stat().st_mtime])
+    if force or not plug.exists() or plug.stat().st_mtime < newest_p:
+        _link(plug, plug_objs, True, flags, [str(mod), "-Wl,-rpath,$ORIGIN"])
+        if verbose:
+            print(f"linked {plug}")
     if clis:
         bindir = BIN if not (debug or asan) else objdir / "bin"
         for name, src in CLI.items():
             o = objdir / (src.replace("/", "_") + ".o")
             out = bindir / name
-            if force or not out.exists() or out.stat().st_mtime < max(newest, o.stat().st_mtime):
-                _link(out, lib_objs + [o], False, flags)
+            if force or not out.exists() or out.stat().st_mtime < max(newest, newest_p, o.stat().st_mtime):
+                _link(out, lib_objs + plug_objs + [o], False, flags)
                 if verbose:
                     print(f"linked {out}")
     return mod

@@ -82,6 +82,10 @@ struct GpuSetupInfo {
   std::string gram = "f32";           // Gram / kernel-row GEMM arithmetic: "f32" or "split-f16" (rbf_gemm_split.hip)
 };
 
+// true once the pair-cache plugin (libdpsvm_pairq.so, or the CLIs that link it)
+// registered the quarantined pair-at-a-time cache / partitioned-X engines
+bool quarantine_loaded();
+
 class GpuSolver {
  public:
   // x: host row-major [n_x][d] where n_x = n (replicated) or the rank's shard

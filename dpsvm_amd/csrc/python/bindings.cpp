@@ -251,6 +251,8 @@ PYBIND11_MODULE(_C, m) {
                     [](Checkpoint& c, F32 a) { c.f = from_np(a); });
   // the device solver's engine choice (device_state.hpp kEngineTable, then
   // kQuarantineTable with engines=all), for docs and tests
+  m.def("quarantine_loaded", []() { return quarantine_loaded(); },
+        "true once the pair-cache plugin (libdpsvm_pairq.so) registered the quarantined engines");
   m.def("engine_table", [](bool quarantine) {
     std::vector<std::pair<std::string, std::string>> out;
     for (const EngineRule& r : kEngineTable) out.emplace_back(engine_name(r.kind), r.use);

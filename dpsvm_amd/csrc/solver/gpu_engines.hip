@@ -7,12 +7,8 @@
 //                     keys exchanged in-kernel (smo_persist.hip)
 //   fused-dense       Gram resident; one launch per iteration, blocks of launches
 //                     replayed from a hipGraph (smo_fused.hip)
-//   persistent-cache  kernel-row cache; one launch per persist_block iterations,
-//                     private cache metadata per workgroup (smo_persist_lru.hip)
-//   fused-cache       kernel-row cache (+ pinned host tier); one launch per
-//                     iteration (smo_fused_lru.hip)
-//   chain             rows / step / [collective] / finalize per iteration
-//                     (smo_kernels.hip): the partitioned-X fallback
+//   (persistent-cache, fused-cache and chain — the quarantined pair-at-a-time
+//   cache / partitioned-X engines — live in the plugin gpu_engines_pairq.hip)
 //   ws-dense          Gram resident; working-set rounds: one workgroup solves a
 //                     q-row sub-problem from an LDS sub-Gram, one grid pass
 //                     updates f and selects the next candidates (ws_*.hip)
@@ -22,6 +18,8 @@
 // Reference per-iteration path: svmTrainMain.cpp:235-310 (host loop, >= 7
 // blocking host<->device round trips, one MPI Allgather).
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 
 #include "gpu_impl.hpp"
 #include "../runtime/timer.hpp"
@@ -33,39 +31,14 @@ namespace dpsvm {
 // synchronisation for device communicators).  Fused engines: iteration k of
 // a block reads partial buffer / record k^1 and writes k&1.
 void GpuSolver::Impl::enqueue_iteration(int k) {
-  if (fused()) {
+  if (kind == EngineKind::FusedDense) {
     const int wi = k & 1, ri = wi ^ 1;
-    uint64_t* pout = pf + (size_t)wi * 2 * Gf;
-    if (kind == EngineKind::FusedCache)
-      launch::smo_fused_lru(args, pf + (size_t)ri * 2 * Gf, pout, rcf + ri, rcf + wi, stream);
-    else
-      launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pout, rf + ri, rf + wi, stream);
-    if (collectives() && !xch) allreduce_keys(pout, 2 * Gf);
+    launch::smo_fused(args, 1, pf + (size_t)ri * 2 * Gf, pf + (size_t)wi * 2 * Gf, rf + ri, rf + wi, stream);
+    if (collectives() && !xch) allreduce_keys(pf + (size_t)wi * 2 * Gf, 2 * Gf);
     return;
   }
-  launch::smo_rows(args, stream);
-  launch::smo_step(args, stream);
-  if (collectives()) {
-    if (replicated) {
-      allreduce_keys(partials, 2 * G);
-    } else {
-      launch::smo_local_record(args, stream);
-      const size_t rb = (size_t)args.rec_bytes;
-      if (comm->device_memory()) {
-        comm->allgather(my_record, records, rb, stream);
-      } else {
-        HIP_CHECK(hipMemcpyAsync(h_records.data() + rank * rb, my_record, rb, hipMemcpyDeviceToHost, stream));
-        HIP_CHECK(hipStreamSynchronize(stream));
-        comm->allgather(h_records.data() + rank * rb, h_records.data(), rb, nullptr);
-        HIP_CHECK(hipMemcpyAsync(records, h_records.data(), rb * world, hipMemcpyHostToDevice, stream));
-      }
-    }
-  } else if (!replicated) {
-    // single-rank partitioned (tests): the local record is the whole world
-    launch::smo_local_record(args, stream);
-    HIP_CHECK(hipMemcpyAsync(records, my_record, args.rec_bytes, hipMemcpyDeviceToDevice, stream));
-  }
-  launch::smo_finalize(args, stream);
+  // fused-cache / chain: the quarantined pair-at-a-time engines (plugin)
+  gpu::need_quarantine("the fused-cache / chain iteration").enqueue_iteration(*this, k);
 }
 
 void GpuSolver::Impl::build_graph(int iters) {
@@ -86,55 +59,6 @@ void GpuSolver::Impl::build_graph(int iters) {
 
 namespace gpu {
 namespace {
-
-FusedRec seed_record(int64_t iter0, float b_hi, float b_lo) {
-  FusedRec r;
-  r.i_hi = r.i_lo = -1;  // no pending pair
-  r.a_hi = r.a_lo = 0.f;
-  r.iter = (int32_t)iter0;
-  r.done = kRunning;
-  r.b_hi = b_hi;
-  r.b_lo = b_lo;
-  return r;
-}
-
-Pending pending_of(const FusedRec& r) {
-  Pending q;
-  q.valid = true;
-  q.i_hi = r.i_hi;
-  q.i_lo = r.i_lo;
-  q.a_hi = r.a_hi;
-  q.a_lo = r.a_lo;
-  q.iter = r.iter;
-  q.b_hi = r.b_hi;
-  q.b_lo = r.b_lo;
-  return q;
-}
-
-// Blocks of launch-per-iteration engines: a hipGraph when the communicator is
-// stream-ordered (or absent), else eager launches.
-void run_launches(GpuSolver::Impl& m, int B) {
-  if (m.gexec) {
-    HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
-  } else {
-    for (int i = 0; i < B; ++i) m.enqueue_iteration(i);
-  }
-}
-
-void maybe_graph(GpuSolver::Impl& m, int B) {
-  const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
-  if (!graphs) return;
-  try {
-    m.build_graph(B);
-  } catch (const std::exception& e) {
-    if (m.p.verbose) fprintf(stderr, "[dpsvm] graph capture failed (%s); eager launches\n", e.what());
-  }
-}
-
-int even_block(const SolverParams& p) {
-  // fused engines ping-pong two buffers: the parity must survive graph replays
-  return std::max(2, (std::max(1, p.graph_block) + 1) / 2 * 2);
-}
 
 // The split GEMMs' fp16 operands of every x row this rank holds (part of the
 // Gram / first-round work, so inside the timed region of every solve).
@@ -248,65 +172,6 @@ struct FusedDense final : DenseBase {
     maybe_graph(m, block(m.p));
   }
   void run_block(GpuSolver::Impl& m, int B) override { run_launches(m, B); }
-};
-
-struct PersistCache final : Engine {
-  EngineKind kind() const override { return EngineKind::PersistCache; }
-  int block(const SolverParams& p) const override { return std::max(1, p.persist_block); }
-  void prepare(GpuSolver::Impl& m) override {  // every workgroup's private copy: empty cache, hand 0
-    launch::plru_init(m.plru_meta, m.args.plru_stride, m.Gf, m.n, m.L, m.stream);
-    HIP_CHECK(hipMemsetAsync(m.plru_stats, 0, 8 * sizeof(int64_t), m.stream));
-  }
-  void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult&) override {
-    const FusedRec r0 = seed_record(iter0, b_hi, b_lo);
-    HIP_CHECK(hipMemcpyAsync(m.rf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
-    launch::smo_fused(m.args, 0, nullptr, m.pf + 2 * m.Gf, m.rf + 1, nullptr, m.stream);
-  }
-  void run_block(GpuSolver::Impl& m, int B) override {
-    launch::smo_persist_lru(m.args, m.rf + 1, B, m.plru_stats, m.stream);
-  }
-  Pending pending(GpuSolver::Impl& m) override {
-    FusedRec r;
-    HIP_CHECK(hipMemcpy(&r, m.rf + 1, sizeof(r), hipMemcpyDeviceToHost));
-    return pending_of(r);
-  }
-};
-
-struct FusedCache final : Engine {
-  EngineKind kind() const override { return EngineKind::FusedCache; }
-  int block(const SolverParams& p) const override { return even_block(p); }
-  void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult&) override {
-    // record "no pending pair, empty cache" in buffer 1 + initial keys
-    FusedCacheRec r0;
-    memset(&r0, 0, sizeof(r0));
-    r0.i_hi = r0.i_lo = -1;
-    r0.iter = (int32_t)iter0;
-    r0.done = kRunning;
-    r0.b_hi = b_hi;
-    r0.b_lo = b_lo;
-    r0.hit_line[0] = r0.hit_line[1] = -1;
-    for (int q = 0; q < kNQ; ++q) r0.line[q] = r0.key[q] = r0.old[q] = r0.hline[q] = r0.hold[q] = -1;
-    HIP_CHECK(hipMemcpyAsync(m.rcf + 1, &r0, sizeof(r0), hipMemcpyHostToDevice, m.stream));
-    uint64_t* p1 = m.pf + 2 * m.Gf;
-    launch::smo_fused(m.args, 0, nullptr, p1, nullptr, nullptr, m.stream);
-    if (m.collectives()) m.allreduce_keys(p1, 2 * m.Gf);
-    maybe_graph(m, block(m.p));
-  }
-  void run_block(GpuSolver::Impl& m, int B) override { run_launches(m, B); }
-  Pending pending(GpuSolver::Impl& m) override {
-    FusedCacheRec r;
-    HIP_CHECK(hipMemcpy(&r, m.rcf + 1, sizeof(r), hipMemcpyDeviceToHost));
-    Pending q;
-    q.valid = true;
-    q.i_hi = r.i_hi;
-    q.i_lo = r.i_lo;
-    q.a_hi = r.a_hi;
-    q.a_lo = r.a_lo;
-    q.iter = r.iter;
-    q.b_hi = r.b_hi;
-    q.b_lo = r.b_lo;
-    return q;
-  }
 };
 
 // Per-round collectives of the working-set engines at world > 1 (or forced at
@@ -550,25 +415,37 @@ struct WsCache final : WsRounds<Engine, true> {
   }
 };
 
-struct Chain final : Engine {
-  EngineKind kind() const override { return EngineKind::Chain; }
-  int block(const SolverParams& p) const override { return std::max(1, p.graph_block); }
-  void seed(GpuSolver::Impl& m, int64_t, float, float, SolveResult&) override { maybe_graph(m, block(m.p)); }
-  void run_block(GpuSolver::Impl& m, int B) override { run_launches(m, B); }
-};
-
 }  // namespace
 
 std::unique_ptr<Engine> make_engine(EngineKind k) {
   switch (k) {
     case EngineKind::PersistDense: return std::make_unique<PersistDense>();
     case EngineKind::FusedDense: return std::make_unique<FusedDense>();
-    case EngineKind::PersistCache: return std::make_unique<PersistCache>();
-    case EngineKind::FusedCache: return std::make_unique<FusedCache>();
     case EngineKind::WsDense: return std::make_unique<WsDense>();
     case EngineKind::WsCache: return std::make_unique<WsCache>();
-    default: return std::make_unique<Chain>();
+    default: return need_quarantine("the pair-at-a-time cache / chain engines").make_engine(k);
   }
+}
+
+namespace {
+std::atomic<const QuarantineOps*> g_quarantine{nullptr};
+}
+
+void register_quarantine(const QuarantineOps* ops) { g_quarantine.store(ops); }
+
+const QuarantineOps* quarantine() { return g_quarantine.load(); }
+
+}  // namespace gpu
+
+bool quarantine_loaded() { return gpu::quarantine() != nullptr; }
+
+namespace gpu {
+
+const QuarantineOps& need_quarantine(const char* what) {
+  const QuarantineOps* q = g_quarantine.load();
+  DPSVM_CHECK(q != nullptr, std::string(what) + " live in the quarantined pair-cache plugin, which is not loaded "
+                                                "(engines=\"all\": dpsvm_amd._native.load_quarantine(), or the CLIs)");
+  return *q;
 }
 
 }  // namespace gpu

@@ -89,7 +89,7 @@ bool GpuSolver::Impl::setup_exchange(int64_t region_words) {
     DPSVM_CHECK(world <= 64, "peer exchange supports at most 64 ranks");
     launch::preload_fused_kernels(stream);
     launch::preload_persist_kernel(stream);
-    launch::preload_persist_lru_kernel(stream);
+    if (const gpu::QuarantineOps* qo = gpu::quarantine()) qo->preload(stream);  // pair-cache plugin loaded
     const size_t xbytes = (size_t)(xregion + ping_words) * 8;
     const bool want_uc = p.xch_mem == 1 || (p.xch_mem == 0 && world > 1);
     bool got_uc = false;
@@ -190,7 +190,8 @@ bool GpuSolver::Impl::census(EngineKind k) {
   const bool dense_k = k == EngineKind::PersistDense;
   int cus = 0;
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  const int per_cu = dense_k ? launch::smo_persist_blocks_per_cu(args) : launch::smo_persist_lru_blocks_per_cu(args);
+  const int per_cu = dense_k ? launch::smo_persist_blocks_per_cu(args)
+                             : gpu::need_quarantine("the persistent-cache census").persist_lru_blocks_per_cu(args);
   info.cus = cus;
   info.blocks_per_cu = per_cu;
   const int groups = p.census_groups > 0 ? p.census_groups : (int)Gf;
@@ -209,7 +210,7 @@ bool GpuSolver::Impl::census(EngineKind k) {
     // but ranks sharing a device (rehearsals) can have their queue time-sliced out
     a.census_ticks = (int64_t)(2.0 * 1e8);
     if (dense_k) launch::smo_persist_census(a, groups, stream);
-    else launch::smo_persist_lru_census(a, groups, stream);
+    else gpu::need_quarantine("the persistent-cache census").persist_lru_census(a, groups, stream);
     int32_t h[2] = {0, 0};
     HIP_CHECK(hipMemcpyAsync(h, words, 8, hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));

@@ -207,5 +207,80 @@ struct Engine {
 
 std::unique_ptr<Engine> make_engine(EngineKind k);
 
+// ---- helpers shared by the production engines (gpu_engines.hip) and the
+// quarantined pair-at-a-time cache / chain engines (gpu_engines_pairq.hip) ----
+inline FusedRec seed_record(int64_t iter0, float b_hi, float b_lo) {
+  FusedRec r;
+  r.i_hi = r.i_lo = -1;  // no pending pair
+  r.a_hi = r.a_lo = 0.f;
+  r.iter = (int32_t)iter0;
+  r.done = kRunning;
+  r.b_hi = b_hi;
+  r.b_lo = b_lo;
+  return r;
+}
+
+inline Pending pending_of(const FusedRec& r) {
+  Pending q;
+  q.valid = true;
+  q.i_hi = r.i_hi;
+  q.i_lo = r.i_lo;
+  q.a_hi = r.a_hi;
+  q.a_lo = r.a_lo;
+  q.iter = r.iter;
+  q.b_hi = r.b_hi;
+  q.b_lo = r.b_lo;
+  return q;
+}
+
+// Blocks of launch-per-iteration engines: a hipGraph when the communicator is
+// stream-ordered (or absent), else eager launches.
+inline void run_launches(GpuSolver::Impl& m, int B) {
+  if (m.gexec) {
+    HIP_CHECK(hipGraphLaunch(m.gexec, m.stream));
+  } else {
+    for (int i = 0; i < B; ++i) m.enqueue_iteration(i);
+  }
+}
+
+inline void maybe_graph(GpuSolver::Impl& m, int B) {
+  const bool graphs = m.p.use_graph && m.device_comm() && !m.p.sync_debug && !sync_debug_env();
+  if (!graphs) return;
+  try {
+    m.build_graph(B);
+  } catch (const std::exception& e) {
+    if (m.p.verbose) fprintf(stderr, "[dpsvm] graph capture failed (%s); eager launches\n", e.what());
+  }
+}
+
+inline int even_block(const SolverParams& p) {
+  // fused engines ping-pong two buffers: the parity must survive graph replays
+  return std::max(2, (std::max(1, p.graph_block) + 1) / 2 * 2);
+}
+
+// The pair-at-a-time cache / partitioned-X engines (persistent-cache,
+// fused-cache, chain: kQuarantineTable in device_state.hpp) are not part of
+// the production module: they live in a plugin (dpsvm_amd/_pairq*.so; linked
+// into the CLIs) that registers this table when it is loaded (engines="all").
+// Production code reaches them only through quarantine().
+struct QuarantineOps {
+  std::unique_ptr<Engine> (*make_engine)(EngineKind k);
+  void (*enqueue_iteration)(GpuSolver::Impl& m, int k);  // fused-cache / chain: one iteration
+  // facts of the engine choice (gpu_setup.hip) and residency (census)
+  bool (*fused_lru_supported)(int dp);
+  bool (*persist_lru_supported)(int dp, int fused_rows, int fused_G);
+  int64_t (*plru_stride_words)(int64_t n, int64_t L);
+  int (*persist_lru_blocks_per_cu)(const SmoArgs& a);
+  void (*persist_lru_census)(const SmoArgs& a, int groups, hipStream_t s);
+  void (*preload)(hipStream_t s);
+  // kernel-level test entry points (tests/test_kernels_gpu.py)
+  void (*smo_rows)(const SmoArgs& a, hipStream_t s);
+  void (*smo_step)(const SmoArgs& a, hipStream_t s);
+  void (*xpass_rows)(const SmoArgs& a, const int* keys, int n_new, hipStream_t s);
+};
+void register_quarantine(const QuarantineOps* ops);
+const QuarantineOps* quarantine();     // nullptr: the plugin is not loaded
+const QuarantineOps& need_quarantine(const char* what);  // fails loudly when not loaded
+
 }  // namespace gpu
 }  // namespace dpsvm

@@ -345,7 +345,7 @@ void rbf_rows(const float* x, const float* xsq, int64_t n, int ld, const float* 
   a.d = ld;
   a.G = (int32_t)((n + kStepRows - 1) / kStepRows);
   a.gamma = gamma;
-  launch::smo_rows(a, s);
+  gpu::need_quarantine("k_rbf_rows (smo_rows)").smo_rows(a, s);
   HIP_CHECK(hipStreamSynchronize(s));
   (void)hipFree(dc);
 }
@@ -369,7 +369,7 @@ void select_partials(const float* f, const float* alpha, const float* y, int64_t
   a.off = offset;
   a.C = C;
   a.G = (int32_t)((n + kStepRows - 1) / kStepRows);
-  launch::smo_step(a, s);
+  gpu::need_quarantine("k_select_partials (smo_step)").smo_step(a, s);
   HIP_CHECK(hipStreamSynchronize(s));
   (void)hipFree(dc);
   if (blocks_out) *blocks_out = a.G;
@@ -469,7 +469,7 @@ void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* 
   a.fused_rows = rows_per_group;
   a.fused_G = (int32_t)G;
   hipStream_t s = (hipStream_t)stream;
-  launch::xpass_rows(a, keys, nq, s);
+  gpu::need_quarantine("k_xpass_rows (xpass)").xpass_rows(a, keys, nq, s);
   HIP_CHECK(hipStreamSynchronize(s));
 }
 

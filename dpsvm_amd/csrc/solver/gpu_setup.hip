@@ -390,21 +390,27 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // engine candidates.  Persistent engines need the in-kernel exchange (set up
   // below) and a co-resident grid (census); the one-launch-per-iteration
   // engines are the fallbacks.
-  const bool fused_lru_ok = !m.dense && m.replicated && launch::smo_fused_lru_supported(m.dp) && m.p.cache_engine == 0;
+  // the pair-at-a-time cache engines are a plugin (gpu_engines_pairq.hip), present
+  // only when loaded (engines=all): production setups never pick them
+  const gpu::QuarantineOps* qo = gpu::quarantine();
+  DPSVM_CHECK(m.p.engines == 0 || qo != nullptr,
+              "engines=all needs the quarantined pair-cache plugin (dpsvm_amd._native.load_quarantine())");
+  const bool dp16 = m.dp >= 16 && m.dp % 16 == 0;  // the cache-mode X pass / row GEMM operand width
+  const bool fused_lru_ok = !m.dense && m.replicated && qo && qo->fused_lru_supported(m.dp) && m.p.cache_engine == 0;
   // working-set engines: the resident Gram (ws-dense), or a kernel-row cache
   // whose missing rows come from one GEMM per round (ws-cache); rows sharded
   // over ranks at world > 1 (per-round candidate all-gather + sub-Gram sum)
   const bool ws_cand = ws_ok && m.dense;
   const bool wsc_cand = ws_ok && !m.dense && m.p.host_cache_lines == 0 &&
-                        (!m.replicated || launch::smo_fused_lru_supported(m.dp));
+                        (!m.replicated || dp16);
   if (want_ws && !ws_ok)
     m.info.engine_note = "ws engines need <= " + std::to_string(kWsMaxRPT) + " rows per selection thread";
   const bool plru_cand = !wsc_cand && fused_lru_ok && m.p.host_cache_lines == 0 && m.p.persist != 1 && m.p.exchange != 1 &&
                          m.p.use_graph && !m.p.force_collectives &&
-                         launch::smo_persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
+                         qo->persist_lru_supported(m.dp, (int)m.RBf, (int)m.Gf);
   if (plru_cand) {
     // every workgroup's private metadata copy comes out of the line budget (upper bound: L = n)
-    const double meta_bytes = (double)m.Gf * launch::plru_stride_words(n, n) * 4.0;
+    const double meta_bytes = (double)m.Gf * qo->plru_stride_words(n, n) * 4.0;
     want_lines = std::min<int64_t>(want_lines, (int64_t)((budget - meta_bytes) / line_bytes));
   }
   const bool pdense_cand = !ws_cand && m.dense &&
@@ -641,7 +647,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     }
   }
   if (m.kind == EngineKind::PersistCache) {
-    a.plru_stride = launch::plru_stride_words(n, m.L);
+    a.plru_stride = gpu::need_quarantine("the persistent-cache engine").plru_stride_words(n, m.L);
     m.plru_meta = dmalloc<int32_t>((size_t)m.Gf * a.plru_stride, &m.bytes);
     m.plru_stats = dmalloc<int64_t>(8, &m.bytes);
     a.plru_meta = m.plru_meta;

@@ -17,7 +17,7 @@ from typing import Any, Callable, Optional
 
 import numpy as np
 
-from .._native import gpu_available, load
+from .._native import gpu_available, load, load_quarantine
 
 
 def _as_f32_2d(X) -> np.ndarray:
@@ -267,6 +267,8 @@ class SVC:
         """Train.  ``comm``: a native communicator (see dpsvm_amd.parallel) for
         multi-rank training; ``resume``: checkpoint path or native Checkpoint."""
         C = load()
+        if self.config.engines == "all" or self.config.host_cache_lines or self.config.cache_engine == "chain":
+            load_quarantine()  # the quarantined pair-at-a-time cache engines (plugin)
         X = _as_f32_2d(X)
         ys = self._encode(y)
         n, d = X.shape[0], X.shape[1]

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import torch
 
-from .._native import load
+from .._native import load, load_quarantine
 
 STEP_ROWS = 128
 
@@ -65,8 +65,9 @@ def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0,
 
 def rbf_rows(x: torch.Tensor, w: torch.Tensor, gamma: float) -> torch.Tensor:
     """K[q, j] = exp(-gamma |x_j - w_q|^2) for up to 16 query rows w (the
-    smo_rows MFMA 16x16x4 kernel)."""
+    smo_rows MFMA 16x16x4 kernel; quarantined pair-cache plugin)."""
     C = load()
+    load_quarantine()
     nq = w.shape[0]
     if not 1 <= nq <= 16:
         raise ValueError("1 <= len(w) <= 16")
@@ -85,8 +86,10 @@ def rbf_rows(x: torch.Tensor, w: torch.Tensor, gamma: float) -> torch.Tensor:
 
 
 def select_partials(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: float, offset: int = 0):
-    """Per-workgroup packed (b_hi, I_hi) / (-b_lo, I_lo) keys of smo_step."""
+    """Per-workgroup packed (b_hi, I_hi) / (-b_lo, I_lo) keys of smo_step
+    (quarantined pair-cache plugin)."""
     C = load()
+    load_quarantine()
     n = f.shape[0]
     g = (n + STEP_ROWS - 1) // STEP_ROWS
     part = torch.zeros(2 * g, device=f.device, dtype=torch.int64)
@@ -134,8 +137,9 @@ def compact_positive(alpha: torch.Tensor) -> torch.Tensor:
 def xpass_rows(x: torch.Tensor, keys, gamma: float, rows_per_group: int = 256) -> torch.Tensor:
     """The cache engines' X pass (xpass.hpp, v_mfma_f32_16x16x4_f32): rows
     K(x_keys[q], x_j) for up to 16 query rows, every workgroup filling its own
-    rows_per_group-row segment of each line."""
+    rows_per_group-row segment of each line; quarantined pair-cache plugin)."""
     C = load()
+    load_quarantine()
     keys = [int(k) for k in keys]
     if not 1 <= len(keys) <= 16:
         raise ValueError("1..16 query rows per X pass")

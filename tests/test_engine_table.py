@@ -55,3 +55,29 @@ def test_choose_engine_first_match(facts, want):
     """None: no production row matches — the setup refuses the configuration
     and names engines=all"""
     assert C.choose_engine(**facts) == want
+
+
+def test_quarantined_engines_are_a_plugin_not_the_production_module():
+    """The production module carries no code of the quarantined pair-at-a-time
+    cache / partitioned-X engines: their kernels and
+    engine classes live in libdpsvm_pairq.so, which registers them when loaded
+    (engines="all"); the CLIs link them in."""
+    import subprocess
+
+    from dpsvm_amd import build
+    from dpsvm_amd._native import load_quarantine
+
+    def defined(path):
+        out = subprocess.run(["nm", "-D", "--defined-only", "-C", str(path)], capture_output=True, text=True)
+        assert out.returncode == 0, out.stderr
+        return out.stdout
+
+    prod = defined(build.module_path())
+    for sym in ("smo_fused_lru_kernel", "smo_persist_lru_kernel", "smo_rows_kernel", "smo_finalize_kernel",
+                "launch::smo_fused_lru(", "launch::smo_persist_lru(", "launch::smo_rows("):
+        assert sym not in prod, f"{sym} is in the production module"
+    plug = defined(build.plugin_path())
+    for sym in ("launch::smo_fused_lru(", "launch::smo_persist_lru(", "launch::smo_rows("):
+        assert sym in plug
+    load_quarantine()
+    assert C.quarantine_loaded()
