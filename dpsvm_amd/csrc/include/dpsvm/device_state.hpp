@@ -393,7 +393,9 @@ struct WsArgs {
   int32_t wss;         // sub-problem pair selection: 1 first order (the reference's), 2 second order (WSS2)
   float t_halve;       // multi-block: a round damped to t < t_halve halves the block count
   int32_t clip_fallback;  // multi-block, independent clipping: a clip event drops to one block (1) or not (0)
-  int32_t ks;          // multi-block pass 1: list slices over workgroups (dfs [ks][nl], part [G_all][ks][2])
+  int32_t ks;          // multi-block pass 1: list slices over workgroups (dfs [ks][nl], part [world p1G][ks][2])
+  int32_t p1G;         // multi-block pass 1: column groups per rank (= G; the wide pass 1: ceil(nl_max / 1024))
+  int32_t p1v4;        // multi-block pass 1: 1 = wide column groups, 4 columns (16-B loads) per thread
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
 };
 // u64 words of the working-set exchange region (both parities): one-block
@@ -404,12 +406,13 @@ constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {
 // multi-block engine (P blocks of q rows; its one-block rounds use q1 rows):
 // candidates (kWsCand keys per side), line-search partials, sub-Gram rows
 constexpr int64_t ws_xch_cand_words_multi(int64_t G_all) { return 2 * G_all * 4 * kWsCand; }
-constexpr int64_t ws_xch_part_words(int64_t G_all, int64_t ks) { return 2 * G_all * ks * 4; }
+// (P1_all = world x p1G pass-1 groups: the selection groups, or the wide pass 1's)
+constexpr int64_t ws_xch_part_words(int64_t P1_all, int64_t ks) { return 2 * P1_all * ks * 4; }
 constexpr int64_t ws_xch_sub_words(int64_t P, int64_t q, int64_t q1) {
   return 2 * ((P * q * (q + 1)) > (q1 * (q1 + 1)) ? P * q * (q + 1) : q1 * (q1 + 1));
 }
-constexpr int64_t ws_xch_words_multi(int64_t G_all, int64_t ks, int64_t P, int64_t q, int64_t q1) {
-  return ws_xch_cand_words_multi(G_all) + ws_xch_part_words(G_all, ks) + ws_xch_sub_words(P, q, q1);
+constexpr int64_t ws_xch_words_multi(int64_t G_all, int64_t P1_all, int64_t ks, int64_t P, int64_t q, int64_t q1) {
+  return ws_xch_cand_words_multi(G_all) + ws_xch_part_words(P1_all, ks) + ws_xch_sub_words(P, q, q1);
 }
 constexpr int kStampRing = 4096;
 constexpr int kStampSlots = 12;

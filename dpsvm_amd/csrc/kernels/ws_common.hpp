@@ -253,9 +253,13 @@ __device__ __forceinline__ int64_t ws_xrow(const WsArgs& a, int par, int row) {
   return a.xsub + ((int64_t)par * a.xsub_rows + row) * (a.q_max + 1);
 }
 
-// multi-block rounds: slot k (= (rank G + group) ks + slice) of the line-search partials
+// multi-block rounds: the line-search partial slots of every rank, world x
+// p1G groups x ks slices; slot k = (rank p1G + group) ks + slice
+__device__ __forceinline__ int64_t ws_nparts(const WsArgs& a) {
+  return (int64_t)a.world * a.p1G * max(1, a.ks);
+}
 __device__ __forceinline__ int64_t ws_xpart(const WsArgs& a, int par, int64_t k) {
-  return a.xpart + ((int64_t)par * a.G_all * max(1, a.ks) + k) * 4;
+  return a.xpart + ((int64_t)par * ws_nparts(a) + k) * 4;
 }
 
 __device__ __forceinline__ bool ws_tag_ok(uint64_t g, uint64_t t) { return (g >> 48) == (t >> 48); }
@@ -351,7 +355,7 @@ __device__ __forceinline__ float ws_line_search(const WsArgs& a, int P) {
   if (P <= 1) return 1.f;
   const int lane = threadIdx.x & 63;
   double q = 0.0, g = 0.0;
-  for (int k = lane; k < a.G_all * max(1, a.ks); k += 64) {  // every rank's partials (all-gathered / collected)
+  for (int k = lane; k < ws_nparts(a); k += 64) {  // every rank's partials (all-gathered / collected)
     q += a.part[2 * k];
     g += a.part[2 * k + 1];
   }

@@ -168,7 +168,7 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
         }
         s_red_tot[0] = tq;
         s_red_tot[1] = tg;
-        const int64_t slot = ((int64_t)a.rank * a.G + grp) * KS + ksi;
+        const int64_t slot = ((int64_t)a.rank * a.p1G + grp) * KS + ksi;
         a.part[2 * slot] = tq;
         a.part[2 * slot + 1] = tg;
         if (blockIdx.x == 0) WS_STAMP(23);
@@ -176,7 +176,7 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
       __syncthreads();  // s_red_tot
       if (a.xpeer != nullptr && threadIdx.x < 64 && (threadIdx.x >> 1) < a.world) {
         // peer exchange: the slot's two doubles to every rank (lanes 2 p, 2 p + 1: rank p)
-        const int64_t slot = ((int64_t)a.rank * a.G + grp) * KS + ksi;
+        const int64_t slot = ((int64_t)a.rank * a.p1G + grp) * KS + ksi;
         const int64_t R = c->outer;  // committed by this round's solve
         const uint64_t t = xtag((uint32_t)R + 1u);
         const int pr = threadIdx.x >> 1, h = threadIdx.x & 1;
@@ -321,6 +321,128 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(7);
 }
 
+// Multi-block pass 1, wide layout (a.p1v4): the same sums as MODE 1 — d_f_j =
+// sum_k c_k K(k, j) over the round's changed rows, each partition over a
+// contiguous slice of the list in list order, partitions combined in order,
+// slices summed in order by pass 2 — but a workgroup owns 1024 columns and a
+// thread 4 adjacent ones (16-B row loads): each wave reads 1 KiB of a changed
+// Gram row per load instead of 256 B (HBM row-buffer locality of the scattered
+// rows), and p1G = ceil(nl_max / 1024) groups x ks list slices fill the device.
+constexpr int kP1Cols = 4 * kWsSelThreads;  // columns per workgroup
+__global__ __launch_bounds__(4 * kWsSelThreads) void ws_pass1_v4_kernel(WsArgs a) {
+  constexpr int PARTS = 4, CH = 12;  // 12 rows x 16 B in flight per thread
+  __shared__ int32_t s_idx[kWsMaxAll];
+  __shared__ float s_coef[kWsMaxAll];
+  __shared__ f4 s_part[PARTS - 1][kWsSelThreads];
+  __shared__ double s_red[2][4 * kWsSelThreads / 64];
+  __shared__ double s_red_tot[2];
+  WsCtrl* c = a.ctrl;
+  const int tid = threadIdx.x & (kWsSelThreads - 1), part = threadIdx.x / kWsSelThreads;
+  if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(22);
+  const int na = c->n_apply;
+  if (na == 0) return;
+  const int KS = max(1, a.ks);
+  const int grp = (int)(blockIdx.x % a.p1G), ksi = (int)(blockIdx.x / a.p1G);
+  {  // this workgroup's slice [e_lo, e_hi) of the blocks' concatenated apply segments
+    const int per_wg = PARTS * ((na + PARTS * KS - 1) / (PARTS * KS));
+    const int e_lo = min(na, ksi * per_wg), e_hi = min(na, e_lo + per_wg);
+    int at = 0;
+    for (int p = 0; p < a.blocks && at < e_hi; ++p) {
+      const int nb = c->nab[p];
+      const int k0 = max(0, e_lo - at), k1 = min(nb, e_hi - at);
+      for (int k = k0 + threadIdx.x; k < k1; k += 4 * kWsSelThreads) {
+        s_idx[at + k] = c->apply_line[p * a.q_max + k];
+        s_coef[at + k] = c->apply_coef[p * a.q_max + k];
+      }
+      at += nb;
+    }
+  }
+  __syncthreads();
+  const int64_t j0 = (int64_t)grp * kP1Cols + 4 * tid;
+  const bool has = j0 < a.nl;  // j0 + 4 <= round_up(nl, 4) <= ldg: the 16-B load stays in the row
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int per = (na + PARTS * KS - 1) / (PARTS * KS);
+  const int k_lo = min(na, (ksi * PARTS + part) * per), k_hi = min(na, k_lo + per);
+  for (int k0 = k_lo; k0 < k_hi; k0 += CH) {
+    f4 kv[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int kk = min(k0 + u, k_hi - 1);
+      const float* row = a.gram + (int64_t)s_idx[kk] * a.ldg;
+      kv[u] = has ? *(const f4*)(row + j0) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      if (k0 + u < k_hi) {
+        const float cc = s_coef[k0 + u];
+        acc.x = f_add1(acc.x, cc, kv[u].x);
+        acc.y = f_add1(acc.y, cc, kv[u].y);
+        acc.z = f_add1(acc.z, cc, kv[u].z);
+        acc.w = f_add1(acc.w, cc, kv[u].w);
+      }
+    }
+  }
+  if (part > 0) s_part[part - 1][tid] = acc;
+  __syncthreads();
+  double sq = 0.0, sg = 0.0;
+  if (part == 0) {
+#pragma unroll
+    for (int p = 1; p < PARTS; ++p) {
+#pragma clang fp contract(off)
+      const f4 o = s_part[p - 1][tid];
+      acc.x = acc.x + o.x;
+      acc.y = acc.y + o.y;
+      acc.z = acc.z + o.z;
+      acc.w = acc.w + o.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t j = j0 + e;
+      if (has && j < a.nl) {
+        a.dfs[(int64_t)ksi * a.nl + j] = acc[e];
+        const float dj = a.dalpha[a.off + j];
+        if (dj != 0.f) {
+          const double cj = (double)dj * (double)a.y[a.off + j];
+          sq += cj * (double)acc[e];  // d'Qd is linear in the KS partial changes
+          if (ksi == 0) sg -= cj * (double)a.f[j];
+        }
+      }
+    }
+  }
+  // fixed-order block sums (butterfly per wave, waves in order)
+  sq = wave_sum_f64(sq);
+  sg = wave_sum_f64(sg);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[0][w] = sq;
+    s_red[1][w] = sg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tq = 0.0, tg = 0.0;
+    for (int k = 0; k < 4 * kWsSelThreads / 64; ++k) {
+      tq += s_red[0][k];
+      tg += s_red[1][k];
+    }
+    s_red_tot[0] = tq;
+    s_red_tot[1] = tg;
+    const int64_t slot = ((int64_t)a.rank * a.p1G + grp) * KS + ksi;
+    a.part[2 * slot] = tq;
+    a.part[2 * slot + 1] = tg;
+    if (blockIdx.x == 0) WS_STAMP(23);
+  }
+  __syncthreads();  // s_red_tot
+  if (a.xpeer != nullptr && threadIdx.x < 64 && (threadIdx.x >> 1) < a.world) {
+    // peer exchange: the slot's two doubles to every rank (lanes 2 p, 2 p + 1: rank p)
+    const int64_t slot = ((int64_t)a.rank * a.p1G + grp) * KS + ksi;
+    const int64_t R = c->outer;  // committed by this round's solve
+    const uint64_t t = xtag((uint32_t)R + 1u);
+    const int pr = threadIdx.x >> 1, h = threadIdx.x & 1;
+    const double v = h ? s_red_tot[1] : s_red_tot[0];
+    ws_put64(a.xpeer[pr] + ws_xpart(a, (int)(R & 1), slot) + 2 * h, t, (uint64_t)__double_as_longlong(v));
+  }
+}
+
 // Multi-block rounds over the peer exchange: every rank's line-search partials
 // (pushed by pass 1 into this rank's receive buffer) into a.part, the layout the
 // all-gather leaves — pass 2 then reads them as from the collective.  Runs when
@@ -330,7 +452,7 @@ __global__ __launch_bounds__(256) void ws_xcollect_part_kernel(WsArgs a) {
   if (c->n_apply == 0) return;  // pass 1 pushed nothing (or the run ended: n_apply = 0)
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(17);
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= (int64_t)a.G_all * max(1, a.ks)) return;
+  if (k >= ws_nparts(a)) return;
   const int64_t R = c->outer;  // committed by this round's solve, as pass 1 tagged it
   uint64_t v[4];
   if (ws_poll<4>(a, a.xpeer[a.xrank] + ws_xpart(a, (int)(R & 1), k), xtag((uint32_t)R + 1u), v)) {
@@ -347,7 +469,7 @@ __global__ __launch_bounds__(256) void ws_xcollect_part_kernel(WsArgs a) {
 namespace launch {
 
 void ws_xcollect_part(const WsArgs& a, hipStream_t s) {
-  const int64_t slots = (int64_t)a.G_all * std::max(1, a.ks);
+  const int64_t slots = (int64_t)a.world * a.p1G * std::max(1, a.ks);
   dev::ws_xcollect_part_kernel<<<dim3((unsigned)((slots + 255) / 256)), 256, 0, s>>>(a);
   post_launch("ws_xcollect_part", s);
 }
@@ -396,7 +518,7 @@ static void ws_select_mode(const WsArgs& a, hipStream_t s) {
 
 void ws_select(const WsArgs& a, hipStream_t s) {
   if (a.blocks > 1) {
-    ws_select_mode<1>(a, s);  // d_f + line-search partials
+    ws_select_pass(a, 1, s);  // d_f + line-search partials
     ws_select_mode<2>(a, s);  // f += t d_f, candidates
   } else {
     ws_select_mode<0>(a, s);
@@ -404,9 +526,17 @@ void ws_select(const WsArgs& a, hipStream_t s) {
 }
 
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
-  if (pass == 1) ws_select_mode<1>(a, s);
-  else ws_select_mode<2>(a, s);
+  if (pass == 1 && a.p1v4) {
+    dev::ws_pass1_v4_kernel<<<dim3(a.p1G * std::max(1, a.ks)), 4 * kWsSelThreads, 0, s>>>(a);
+    post_launch("ws_pass1_v4", s);
+  } else if (pass == 1) {
+    ws_select_mode<1>(a, s);
+  } else {
+    ws_select_mode<2>(a, s);
+  }
 }
+
+int ws_pass1_v4_groups(int64_t nl_max) { return (int)std::max<int64_t>(1, (nl_max + dev::kP1Cols - 1) / dev::kP1Cols); }
 
 }  // namespace launch
 }  // namespace dpsvm

@@ -199,7 +199,7 @@ void ws_allgather_cand(GpuSolver::Impl& m) {
 // multi-block rounds at world > 1: every rank's line-search partials
 void ws_allgather_part(GpuSolver::Impl& m) {
   if (!m.collectives() || m.wsa.xpeer) return;  // peer exchange: pushed by pass 1, polled by pass 2
-  const size_t bytes = (size_t)m.wsa.G * std::max(1, m.wsa.ks) * 2 * sizeof(double);
+  const size_t bytes = (size_t)m.wsa.p1G * std::max(1, m.wsa.ks) * 2 * sizeof(double);
   uint8_t* all = (uint8_t*)m.wsa.part;
   if (m.comm->device_memory()) {
     m.comm->allgather(all + (size_t)m.rank * bytes, all, bytes, m.stream);

@@ -578,11 +578,19 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                             (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
   // multi-block rounds over the peer exchange (partitioned X in cache mode sums
   // the miss rows by an all-reduce: that engine keeps the collectives)
-  const int ks_mb = launch::ws_pass1_splits(ws_G);
+  // multi-block pass 1: the selection geometry (G groups of rpt x 256 columns),
+  // or the wide layout (1024-column groups, 16-B row loads; DPSVM_PASS1=v4|v1)
+  static const int pass1_env = [] {
+    const char* e = std::getenv("DPSVM_PASS1");
+    return e ? (std::string(e) == "v4" ? 1 : std::string(e) == "v1" ? 0 : -1) : -1;
+  }();
+  const bool p1v4 = pass1_env == 1;
+  const int p1G = p1v4 ? launch::ws_pass1_v4_groups(nl_max) : ws_G;
+  const int ks_mb = launch::ws_pass1_splits(p1G);
   bool multi_peer = false;
   if (ws_peer_base && multi_elig && !(wsc_cand && !m.replicated) && (xch_resident || m.p.exchange == 2)) {
     const int64_t G_all = (int64_t)ws_G * m.world;
-    const bool ok = m.setup_exchange(ws_xch_words_multi(G_all, ks_mb, want_blocks, mb_q, ws_q));
+    const bool ok = m.setup_exchange(ws_xch_words_multi(G_all, (int64_t)p1G * m.world, ks_mb, want_blocks, mb_q, ws_q));
     DPSVM_CHECK(ok || m.p.exchange != 2,
                 "peer exchange requested (exchange=peer) but its self test failed (" + m.xch_diag + ")");
     if (ok) {
@@ -681,6 +689,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.nl = m.nl;
     w.off = m.off;
     w.G = ws_G;
+    w.p1G = ws_G;  // multi-block rounds may take the wide pass-1 geometry below
     w.rpt = ws_rpt;
     w.world = m.world;
     w.G_all = w.G * m.world;
@@ -751,9 +760,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.aux = m.wssub + (size_t)w.blocks * w.q_max * w.q_max;
     if (w.blocks > 1) {
       w.ks = ks_mb;
+      w.p1G = p1G;
+      w.p1v4 = p1v4 ? 1 : 0;
       m.wsdfs = dmalloc<float>((size_t)w.ks * m.nl, &m.bytes);
       m.wsdalpha = dmalloc<float>((size_t)n, &m.bytes);
-      m.wspart = dmalloc<double>((size_t)2 * w.G_all * w.ks, &m.bytes);
+      m.wspart = dmalloc<double>((size_t)2 * w.world * w.p1G * w.ks, &m.bytes);
       m.wssorted = dmalloc<uint64_t>((size_t)2 * kWsMaxGroups * kWsCand, &m.bytes);
       w.sorted = m.wssorted;
       HIP_CHECK(hipMemsetAsync(m.wsdalpha, 0, (size_t)n * 4, m.stream));
@@ -770,7 +781,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       if (w.blocks > 1) {  // ws_xch_words_multi: candidates (kWsCand keys a side), partials, sub-Gram rows
         w.xcw = 4 * kWsCand;
         w.xpart = ws_xch_cand_words_multi(w.G_all);
-        w.xsub = w.xpart + ws_xch_part_words(w.G_all, w.ks);
+        w.xsub = w.xpart + ws_xch_part_words((int64_t)w.world * w.p1G, w.ks);
         w.xsub_rows = (int64_t)w.blocks * w.q_max;  // the one-block view: its own q_max (gpu_engines.hip)
       } else {  // ws_xch_words
         w.xcw = 4 * kWsCand1;

@@ -242,6 +242,7 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
   a.y = st.up(y, (size_t)n);
   a.dalpha = st.up(dalpha, (size_t)n);
   a.ks = std::max(1, ks);
+  a.p1G = G;
   a.dfs = st.up(std::vector<float>(), (size_t)n * a.ks);
   a.part = st.up(std::vector<double>(), (size_t)2 * G * a.ks);
   a.cand = a.cand_out = st.up(std::vector<uint64_t>(), (size_t)G * 2 * kWsCand);
