@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--ks", default="1,2,4,8,16")
     ap.add_argument("--changed", type=int, default=3072)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--wide", action="store_true", help="the wide pass 1 (ws_pass1_v4_kernel, the default)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from dpsvm_amd._native import load
@@ -46,10 +47,10 @@ def main() -> int:
         nab = np.full(blocks, q, dtype=np.int32)
         for ks in [int(v) for v in a.ks.split(",")]:
             r = C.k_ws_select(gram.reshape(-1), L, n, f, alpha, y, dalpha, lines, coef, nab, blocks, blocks, blocks, q,
-                              10.0, 1, ks=ks, reps=a.reps)
+                              10.0, 1, ks=ks, reps=a.reps, wide=a.wide)
             t = np.array(r["pass1_us"][2:])
             rec = {"cols": n, "rows": L, "changed": int(blocks * q), "G": int(r["G"]), "ks": ks,
-                   "workgroups": int(r["G"]) * ks, "pass1_us_median": round(float(np.median(t)), 2),
+                   "wide": bool(a.wide), "p1G": int(r["p1G"]), "workgroups": int(r["p1G"]) * ks, "pass1_us_median": round(float(np.median(t)), 2),
                    "pass1_us_min": round(float(t.min()), 2),
                    "GBps": round(blocks * q * n * 4 / (float(np.median(t)) * 1e-6) / 1e9, 1)}
             print(json.dumps(rec), flush=True)

@@ -238,6 +238,7 @@ struct WsSelectProbe {
   std::vector<double> part;      // [G][2] d'Qd, g'd partials (two-pass mode)
   std::vector<uint64_t> cand;    // [G][2][kWsCand]
   int G = 0, rpt = 0, p_act = 0, n_damped = 0, nonfinite = 0;
+  int p1G = 0;                   // pass-1 groups (= G; the wide pass 1: ceil(n / 1024)); part is [p1G][ks][2]
   float t = 1.f;
   int64_t p1_round = 0;
   std::vector<float> pass1_us;  // reps > 0: event times of repeated pass-1 launches
@@ -247,7 +248,7 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
                               const std::vector<float>& dalpha, const std::vector<int32_t>& apply_line,
                               const std::vector<float>& apply_coef, const std::vector<int32_t>& nab, int blocks,
                               int p_round, int p_act, int q_max, float C, int64_t outer, int ks = 0,
-                              int reps = 0);
+                              int reps = 0, bool wide = false);
 }  // namespace kernels
 
 int device_count();

@@ -72,6 +72,7 @@ bool ws_supported(int64_t nl_max, int world, int q_max);
 void ws_geometry(int64_t nl_max, int world, int32_t* G, int32_t* rpt);
 int ws_pass1_splits(int G);  // multi-block pass 1: workgroups per selection group
 int ws_pass1_v4_groups(int64_t nl_max);  // the wide pass 1: 1024-column groups per rank
+int ws_pass1_v4_splits(int p1G);         // ... and its list slices per group
 void ws_select(const WsArgs& a, hipStream_t s);
 // multi-block rounds: pass 1 (d_f + line-search partials), pass 2 (apply, candidates); at
 // world > 1 the partials are all-gathered between them

@@ -538,5 +538,9 @@ void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
 
 int ws_pass1_v4_groups(int64_t nl_max) { return (int)std::max<int64_t>(1, (nl_max + dev::kP1Cols - 1) / dev::kP1Cols); }
 
+// the wide pass 1's list slices: about one workgroup per CU (the headline at one
+// rank: 59 groups x 4 slices; a rank of 8: 8 groups x 32 slices)
+int ws_pass1_v4_splits(int p1G) { return std::max(1, std::min(2 * kWsMaxPass1Splits, 256 / std::max(1, p1G))); }
+
 }  // namespace launch
 }  // namespace dpsvm

@@ -34,7 +34,7 @@ __device__ __forceinline__ float sel_lanes(float a, float b, uint64_t m) {
 
 template <int NS>
 __device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, int lane, float C, float (&fu)[NS],
-                                         float (&fl)[NS], float (&ar)[NS]) {
+                                         float (&fl)[NS]) {
   const float INF = __builtin_inff();
   // the operands are uniform: each test as a wave mask (all ones or zero; wave
   // 0 runs with a full exec mask) keeps the set logic on the scalar unit
@@ -54,24 +54,7 @@ __device__ __forceinline__ void ws_place(int pos, float an, float yv, float fp, 
     const uint64_t w = s == k ? bit : 0ull;
     fu[k] = sel_lanes(fu[k], nu, w);
     fl[k] = sel_lanes(fl[k], nl, w);
-    ar[k] = sel_lanes(ar[k], an, w);  // the row's alpha lives in its owner lane's slot register
   }
-}
-
-// the value of working-set position pos = 64 s + l (s, l uniform) from the
-// slot registers: one readlane per slot, then a scalar select (no LDS trip)
-template <int NS>
-__device__ __forceinline__ float slot_lane(const float (&v)[NS], int s, int l) {
-  // the slot by v_cndmask from scalar all-lanes masks (shared by every value of
-  // the same position), then one readlane: 3 instructions per value (a readlane
-  // per slot plus a scalar select came out as ~8 with the VGPR round trips)
-  // (ballot masks: plain selects on one index let the compiler turn the slots
-  // into a scratch array indexed by s)
-  const uint64_t m1 = __ballot(s == 1), m2 = __ballot(s == 2);  // all lanes or none (wave 0: full exec)
-  float x = v[0];
-  if constexpr (NS == 3) x = sel_lanes(x, v[2], m2);
-  x = sel_lanes(x, v[1], m1);
-  return readlane_f32(x, l);
 }
 
 // The reference's pair update (svmTrainMain.cpp:282-295; pair_update in
@@ -166,7 +149,7 @@ template <bool kBox, bool kFull, bool kMulti, bool kW2, int NS = 3>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   static_assert(NS == 3 || (NS == 2 && !kFull), "slots");
   extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
-  __shared__ float s_a[kWsMax], s_y[kWsMax], s_f[kWsMax];
+  __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
   __shared__ int32_t s_idx[kWsMax], s_line[kWsMax];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -278,17 +261,13 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   const float INF = __builtin_inff();
   const float C = a.C;
   const float eps_in = fmaxf(a.eps_floor, a.rel_local * 0.5f * (b_lo - b_hi));
-  // per lane, slot s = working-set position lane + 64 s: f (as the I_up /
-  // I_low keys fu / fl), the label, the current and the round's first alpha —
-  // all in registers; the pair's values are read with readlane
-  float fu[NS], fl[NS], yr[NS], a0[NS], ar[NS];
+  float fu[NS], fl[NS], yr[NS], a0[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int p = lane + 64 * s;
     const bool v = p < q;
     const float fv = v ? s_f[p] : 0.f;
     a0[s] = v ? s_a[p] : 0.f;
-    ar[s] = a0[s];
     yr[s] = v ? s_y[p] : 1.f;
     fu[s] = v && in_up(a0[s], yr[s], C) ? fv : INF;
     fl[s] = v && in_low(a0[s], yr[s], C) ? -fv : INF;
@@ -350,20 +329,16 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       bad = open;  // a violating pair exists but no position matches it: NaN
       break;
     }
-    // the pair's rows of the sub-Gram: one batch of LDS reads; the pair's
-    // alphas / labels and its 2 x 2 block K(hi|lo, hi|lo) from registers
-    // (readlane of the owner lanes' slots: no second LDS round trip)
+    // every remaining LDS read of the step in one batch: the pair's alphas /
+    // labels, the 2 x 2 block K(hi|lo, hi|lo) and the sub-Gram rows
+    const float a_hi = s_a[ph], y_hi = s_y[ph], a_lo = s_a[pl], y_lo = s_y[pl];
+    const float khl = K[ph * ldk + pl], klh = K[pl * ldk + ph], khh = K[ph * ldk + ph], kll = K[pl * ldk + pl];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int p = kFull ? lane + 64 * s : min(lane + 64 * s, q - 1);
       if constexpr (!kW2) kh[s] = K[ph * ldk + p];
       kl[s] = K[pl * ldk + p];
     }
-    const int sh = ph >> 6, lh = ph & 63, slo = pl >> 6, llo = pl & 63;
-    const float a_hi = slot_lane(ar, sh, lh), y_hi = slot_lane(yr, sh, lh);
-    const float a_lo = slot_lane(ar, slo, llo), y_lo = slot_lane(yr, slo, llo);
-    const float khl = slot_lane(kh, slo, llo), khh = slot_lane(kh, sh, lh);
-    const float klh = slot_lane(kl, sh, lh), kll = slot_lane(kl, slo, llo);
     bool clipped = false;
     const PairUpdate up = ws_pair_step<kBox>(a_hi, a_lo, y_hi, y_lo, bh, bl, khl, C, a.tau, ph == pl, &clipped);
     if (kMulti && !kBox) clipped_any |= clipped;
@@ -385,8 +360,12 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       f_lo_new = bl + (up.c_hi * khl + up.c_lo * kll);
       f_hi_new = bh + (up.c_hi * khh + up.c_lo * klh);
     }
-    ws_place(pl, up.a_lo_new, y_lo, f_lo_new, lane, C, fu, fl, ar);
-    ws_place(ph, up.a_hi_new, y_hi, f_hi_new, lane, C, fu, fl, ar);  // hi written last (svmTrainMain.cpp:298-299)
+    ws_place(pl, up.a_lo_new, y_lo, f_lo_new, lane, C, fu, fl);
+    ws_place(ph, up.a_hi_new, y_hi, f_hi_new, lane, C, fu, fl);  // hi written last (svmTrainMain.cpp:298-299)
+    // lane 0 writes the pair's alphas, the other lanes a private scratch word
+    // each (no exec-mask branch in the loop, no bank conflict)
+    s_a[lane == 0 ? pl : kWsMax + lane] = up.a_lo_new;
+    s_a[lane == 0 ? ph : kWsMax + 64 + lane] = up.a_hi_new;
     ++inner;
   }
   // ---- commit: alphas, the changed rows for the f update, control, status ----
@@ -394,7 +373,7 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int p = lane + 64 * s;
-    const float an = p < q ? ar[s] : 0.f;
+    const float an = p < q ? s_a[p] : 0.f;
     const bool nz = p < q && an != a0[s];
     const uint64_t mk = __ballot(nz);
     const int at = n_apply + __popcll(mk & ((1ull << lane) - 1ull));

@@ -611,10 +611,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("k_ws_select", [vi](const F32& gram, int64_t L, int64_t ldg, const F32& f, const F32& alpha, const F32& y,
                             const F32& dalpha, const I32& lines, const F32& coef, const I32& nab, int blocks,
-                            int p_round, int p_act, int q_max, float C, int64_t outer, int ks, int reps) {
+                            int p_round, int p_act, int q_max, float C, int64_t outer, int ks, int reps, bool wide) {
     const auto r = kernels::ws_select_probe(from_np(gram), L, ldg, from_np(f), from_np(alpha), from_np(y),
                                             from_np(dalpha), vi(lines), from_np(coef), vi(nab), blocks, p_round, p_act,
-                                            q_max, C, outer, ks, reps);
+                                            q_max, C, outer, ks, reps, wide);
     py::dict d;
     d["f"] = to_np(r.f);
     d["alpha"] = to_np(r.alpha);
@@ -624,6 +624,7 @@ PYBIND11_MODULE(_C, m) {
     d["cand"] = r.cand;
     d["G"] = r.G;
     d["rpt"] = r.rpt;
+    d["p1G"] = r.p1G;
     d["t"] = r.t;
     d["pass1_us"] = r.pass1_us;
     d["p_act"] = r.p_act;
@@ -633,7 +634,8 @@ PYBIND11_MODULE(_C, m) {
     return d;
   }, py::arg("gram"), py::arg("L"), py::arg("ldg"), py::arg("f"), py::arg("alpha"), py::arg("y"), py::arg("dalpha"),
         py::arg("lines"), py::arg("coef"), py::arg("nab"), py::arg("blocks"), py::arg("p_round"), py::arg("p_act"),
-        py::arg("q_max"), py::arg("C"), py::arg("outer"), py::arg("ks") = 0, py::arg("reps") = 0);
+        py::arg("q_max"), py::arg("C"), py::arg("outer"), py::arg("ks") = 0, py::arg("reps") = 0,
+        py::arg("wide") = false);
   m.def("make_key", [](float f, uint32_t idx) { return make_key(f, idx); });
   m.def("key_value", [](uint64_t k) { return key_value(k); });
   m.def("key_index", [](uint64_t k) { return key_index(k); });

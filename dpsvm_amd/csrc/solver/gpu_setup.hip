@@ -578,15 +578,17 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                             (m.world > 1 || m.p.exchange == 2);  // exchange=peer at world 1: loopback (tests)
   // multi-block rounds over the peer exchange (partitioned X in cache mode sums
   // the miss rows by an all-reduce: that engine keeps the collectives)
-  // multi-block pass 1: the selection geometry (G groups of rpt x 256 columns),
-  // or the wide layout (1024-column groups, 16-B row loads; DPSVM_PASS1=v4|v1)
-  static const int pass1_env = [] {
+  // multi-block pass 1: the wide layout by default (1024-column groups, 16-B
+  // row loads: headline round 227.5 -> 212.9 us, 0.0257 -> 0.0248 s,
+  // profiles/r5_pass1_wide_ab.txt), or the selection geometry (G groups of
+  // rpt x 256 columns; DPSVM_PASS1=v1 for A/B runs)
+  static const bool p1_sel = [] {
     const char* e = std::getenv("DPSVM_PASS1");
-    return e ? (std::string(e) == "v4" ? 1 : std::string(e) == "v1" ? 0 : -1) : -1;
+    return e && std::string(e) == "v1";
   }();
-  const bool p1v4 = pass1_env == 1;
+  const bool p1v4 = !p1_sel;
   const int p1G = p1v4 ? launch::ws_pass1_v4_groups(nl_max) : ws_G;
-  const int ks_mb = launch::ws_pass1_splits(p1G);
+  const int ks_mb = p1v4 ? launch::ws_pass1_v4_splits(p1G) : launch::ws_pass1_splits(p1G);
   bool multi_peer = false;
   if (ws_peer_base && multi_elig && !(wsc_cand && !m.replicated) && (xch_resident || m.p.exchange == 2)) {
     const int64_t G_all = (int64_t)ws_G * m.world;

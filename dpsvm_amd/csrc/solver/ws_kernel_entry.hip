@@ -197,7 +197,8 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
                               const std::vector<float>& alpha, const std::vector<float>& y,
                               const std::vector<float>& dalpha, const std::vector<int32_t>& apply_line,
                               const std::vector<float>& apply_coef, const std::vector<int32_t>& nab, int blocks,
-                              int p_round, int p_act, int q_max, float C, int64_t outer, int ks, int reps) {
+                              int p_round, int p_act, int q_max, float C, int64_t outer, int ks, int reps,
+                              bool wide) {
   const int64_t n = (int64_t)f.size();
   DPSVM_CHECK(n >= 1 && (int64_t)alpha.size() == n && (int64_t)y.size() == n && (int64_t)dalpha.size() == n,
               "ws_select_probe: f / alpha / y / dalpha of n rows");
@@ -243,8 +244,12 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
   a.dalpha = st.up(dalpha, (size_t)n);
   a.ks = std::max(1, ks);
   a.p1G = G;
+  if (wide && blocks > 1) {  // the wide pass 1 (ws_pass1_v4_kernel)
+    a.p1v4 = 1;
+    a.p1G = launch::ws_pass1_v4_groups(n);
+  }
   a.dfs = st.up(std::vector<float>(), (size_t)n * a.ks);
-  a.part = st.up(std::vector<double>(), (size_t)2 * G * a.ks);
+  a.part = st.up(std::vector<double>(), (size_t)2 * a.p1G * a.ks);
   a.cand = a.cand_out = st.up(std::vector<uint64_t>(), (size_t)G * 2 * kWsCand);
   a.n = a.nl = n;
   a.off = 0;
@@ -283,7 +288,8 @@ WsSelectProbe ws_select_probe(const std::vector<float>& gram, int64_t L, int64_t
   r.alpha = download(a.alpha, (size_t)n, st.s);
   r.dalpha = download(a.dalpha, (size_t)n, st.s);
   r.dfs = download(a.dfs, (size_t)n, st.s);  // slice 0 (all of it at ks = 1)
-  r.part = download(a.part, (size_t)2 * G * a.ks, st.s);
+  r.part = download(a.part, (size_t)2 * a.p1G * a.ks, st.s);
+  r.p1G = a.p1G;
   r.cand = download(a.cand_out, (size_t)G * 2 * kWsCand, st.s);
   r.t = o.t_last;
   r.p_act = o.p_act;

@@ -220,13 +220,15 @@ def ws_solve(K, f, alpha, y, qb, q_max: int, C_: float, clip: str = "independent
 
 
 def ws_select(gram, f, alpha, y, dalpha, apply_lines, apply_coef, nab, C_: float, q_max: int = 192,
-              p_round: int | None = None, p_act: int | None = None, outer: int = 1, ks: int = 0) -> dict:
+              p_round: int | None = None, p_act: int | None = None, outer: int = 1, ks: int = 0,
+              wide: bool = False) -> dict:
     """The working-set f update + candidate selection (ws_select_kernel) on a
     dense gram [L][ldg >= n] (rows = lines).  len(nab) == 1: the one-pass
     kernel; more blocks: pass 1 (d_f, d'Qd / g'd partials) and pass 2 (line
     search t, f += t d_f, alpha = alpha_new - (1 - t) d_alpha, candidates).
     ks > 1: pass 1 split into ks list slices per selection group (dfs then
-    holds slice 0, part [G][ks][2])."""
+    holds slice 0, part [G][ks][2]).  wide: the wide pass 1 (1024-column
+    groups, 16-B row loads; part [p1G][ks][2])."""
     import numpy as np
 
     g = np.ascontiguousarray(np.asarray(gram, dtype=np.float32))
@@ -235,7 +237,7 @@ def ws_select(gram, f, alpha, y, dalpha, apply_lines, apply_coef, nab, C_: float
     return load().k_ws_select(g.reshape(-1), g.shape[0], g.shape[1], f32(f), f32(alpha), f32(y), f32(dalpha),
                               np.asarray(apply_lines, dtype=np.int32), f32(apply_coef), np.asarray(nab, dtype=np.int32),
                               P, P if p_round is None else p_round, P if p_act is None else p_act, q_max, float(C_),
-                              int(outer), ks=int(ks))
+                              int(outer), ks=int(ks), wide=bool(wide))
 
 
 def fused_select(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: float, rows_per_group: int = 256):

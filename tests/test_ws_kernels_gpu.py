@@ -524,3 +524,35 @@ def test_ws_solve_second_order_matches_model(K, clip):
     if got["steps"][0] < 4 * q_max:
         bh2, bl2 = extremes(fn, an, y, C)
         assert bl2 <= bh2 + 2 * eps_in + 1e-4
+
+
+@pytest.mark.parametrize("ks", [1, 3])
+def test_ws_select_wide_pass1_matches_model(K, ks):
+    """The wide pass 1 (ws_pass1_v4_kernel: 1024-column groups, four columns per
+    thread, 16-B row loads, ks list slices): d_f, the d'Qd / g'd partials and f
+    after pass 2 match the float64 model and the selection-geometry kernel;
+    n not a multiple of 1024 (the last group is partial)."""
+    rng = np.random.default_rng(70 + ks)
+    n, C, q_max, P = 3000, 2.0, 96, 4
+    gram, f, a_new, y, dal, ch = select_state(rng, n, C, 160)
+    c = dal.astype(np.float64) * y
+    d_f = gram.astype(np.float64).T @ c
+    q = float(np.sum(c[ch] * d_f[ch]))
+    g = -float(np.sum(c[ch] * f.astype(np.float64)[ch]))
+    nab = [40] * P
+    got = K.ws_select(gram, f, a_new, y, dal, ch, c[ch].astype(np.float32), nab, C, q_max=q_max, ks=ks, wide=True)
+    ref = K.ws_select(gram, f, a_new, y, dal, ch, c[ch].astype(np.float32), nab, C, q_max=q_max, ks=ks)
+    assert got["p1G"] == (n + 1023) // 1024
+    part = np.asarray(got["part"]).reshape(got["p1G"] * ks, 2)
+    assert part[:, 0].sum() == pytest.approx(q, rel=1e-4)
+    assert part[:, 1].sum() == pytest.approx(g, rel=1e-6, abs=1e-9)
+    if ks == 1:
+        np.testing.assert_allclose(got["dfs"], d_f, rtol=1e-4, atol=2e-5)
+    assert got["t"] == pytest.approx(float(line_search_rule(part[:, 0].sum(), part[:, 1].sum(), P)), rel=1e-6)
+    assert got["t"] == pytest.approx(ref["t"], rel=1e-5)
+    np.testing.assert_allclose(got["f"], f + np.float32(got["t"]) * d_f, rtol=1e-4, atol=3e-5)
+    np.testing.assert_allclose(got["f"], ref["f"], rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(got["alpha"], ref["alpha"], rtol=1e-5, atol=1e-6 * C)
+    G, rpt = got["G"], got["rpt"]
+    cand = np.asarray(got["cand"], dtype=np.uint64).reshape(G, 2, KC)
+    np.testing.assert_array_equal(cand, candidates_model(got["f"], got["alpha"], y, C, G, rpt))
