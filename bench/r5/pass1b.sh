@@ -16,3 +16,16 @@ for N in 4 8; do
   DPSVM_FORCE_DEVICE=0 timeout -k 10 400 python3 -u bench.py --gpus $N --dp shard --steps 3 --warmup 1 --no-accuracy --reference-check off --json-out gpurun_out/r5w_mp$N.json > gpurun_out/r5w_mp$N.log 2>&1 || { tail -20 gpurun_out/r5w_mp$N.log; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/r5w_mp$N.json')); print('shard $N ranks (one GPU)', d['value'], d['ws_exchange'], d['rounds'], d['converged'], d['b'])"
 done
+# blocks per round: 32 x 96 (default) vs 64 x 48 (one slot per lane in the solve)
+for B in 32 64 32 64; do
+  DPSVM_WS_AUTO_BLOCKS=$B timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 2 --reference-check off --no-accuracy --json-out gpurun_out/r5b_$B.json > gpurun_out/r5b_$B.log 2>&1 || { tail -20 gpurun_out/r5b_$B.log; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/r5b_$B.json')); print('blocks $B', d['value'], d['rounds'], d['iterations'], d['ws_blocks'], d['converged'], d['b'])" | tee -a gpurun_out/r5b_summary.txt
+done
+for cfg in mnist-parity mnist-makefile; do
+  for B in 32 64; do
+    DPSVM_WS_AUTO_BLOCKS=$B timeout -k 10 300 python3 -u bench.py --config $cfg --steps 5 --warmup 1 --reference-check off --no-accuracy --json-out gpurun_out/r5b_${cfg}_$B.json > gpurun_out/r5b_${cfg}_$B.log 2>&1 || { tail -20 gpurun_out/r5b_${cfg}_$B.log; exit 1; }
+    python3 -c "import json; d=json.load(open('gpurun_out/r5b_${cfg}_$B.json')); print('$cfg blocks $B', d['value'], d['rounds'], d['iterations'], d['ws_blocks'], d['converged'], d['b'])" | tee -a gpurun_out/r5b_summary.txt
+  done
+done
+DPSVM_WS_AUTO_BLOCKS=64 timeout -k 10 300 python3 -u bench/ws_stamps.py --out gpurun_out/r5b_stamps_64.json > /dev/null 2> gpurun_out/r5b_stamps_64.err || exit 1
+python3 -c "import json; d=json.load(open('gpurun_out/r5b_stamps_64.json')); print(d)" | tee -a gpurun_out/r5b_summary.txt

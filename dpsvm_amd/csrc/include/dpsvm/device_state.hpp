@@ -290,7 +290,7 @@ constexpr int64_t kWsAutoRows = 50000;   // solver auto: working-set engines fro
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor
 // t = min(1, g'd / d'Qd) of the dual (ws_*.hip "multi-block rounds")
-constexpr int kWsMaxBlocks = 32;                  // blocks per round (P x q_max <= kWsMaxAll)
+constexpr int kWsMaxBlocks = 64;                  // blocks per round (P x q_max <= kWsMaxAll)
 constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
 constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: the top 1536 of each side)
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup

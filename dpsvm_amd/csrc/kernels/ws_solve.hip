@@ -127,6 +127,10 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[3], float v) {
   return (int)r;
 }
 
+__device__ __forceinline__ int ws_argpos(const float (&x)[1], float v) {
+  return (int)sff1_u64(__ballot(x[0] == v));  // -1 (all ones) when none
+}
+
 __device__ __forceinline__ int ws_argpos(const float (&x)[2], float v) {
   const uint64_t m0 = __ballot(x[0] == v), m1 = __ballot(x[1] == v);
   const uint32_t r0 = sff1_u64(m0), r1 = sff1_u64(m1) | 64u;
@@ -144,10 +148,11 @@ __device__ __forceinline__ int ws_argpos(const float (&x)[2], float v) {
 // the pair whose step gains the most dual objective — instead of argmax f.
 // The stop test stays the reference's first-order one (b_lo = max f over I_low).
 // NS: 64-row slots per lane (3 for q_max <= 192, 2 for q_max <= 128 — the
-// multi-block rounds' 96-row blocks: a third less work per pair step)
+// multi-block rounds' 96-row blocks: a third less work per pair step — and 1
+// for blocks of <= 64 rows)
 template <bool kBox, bool kFull, bool kMulti, bool kW2, int NS = 3>
 __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
-  static_assert(NS == 3 || (NS == 2 && !kFull), "slots");
+  static_assert(NS == 3 || ((NS == 2 || NS == 1) && !kFull), "slots");
   extern __shared__ __attribute__((aligned(16))) float K[];  // q rows of the sub-Gram, stride q_max
   __shared__ float s_a[kWsMax + 128], s_y[kWsMax], s_f[kWsMax];  // s_a: + 2 x 64 scratch words
   __shared__ int32_t s_idx[kWsMax], s_line[kWsMax];
@@ -282,7 +287,11 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
   int inner = 0;
   bool bad = false, clipped_any = false;
   while (inner < cap) {
-    float mu = fminf(fu[0], fu[1]), ml = fminf(fl[0], fl[1]);
+    float mu = fu[0], ml = fl[0];
+    if constexpr (NS >= 2) {
+      mu = fminf(mu, fu[1]);
+      ml = fminf(ml, fl[1]);
+    }
     if constexpr (NS == 3) {
       mu = fminf(mu, fu[2]);
       ml = fminf(ml, fl[2]);
@@ -314,14 +323,15 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
           asm volatile("" : "+v"(gv));
           g[s] = ((fl[s] < INF) & (dv > 0.f)) ? gv : INF;
         }
-        float gm = fminf(g[0], g[1]);
+        float gm = g[0];
+        if constexpr (NS >= 2) gm = fminf(gm, g[1]);
         if constexpr (NS == 3) gm = fminf(gm, g[2]);
         float gm2 = gm;
         wave_min2_f32(gm, gm2);
         pl = gm < INF ? ws_argpos(g, gm) : -1;
         if (pl >= 0) {
           const int sl = pl >> 6;
-          bl = -readlane_f32(sl == 0 ? fl[0] : (NS == 2 || sl == 1) ? fl[1] : fl[NS - 1], pl & 63);  // f of the chosen lo
+          bl = -readlane_f32(sl == 0 || NS == 1 ? fl[0] : (NS == 2 || sl == 1) ? fl[1] : fl[NS - 1], pl & 63);  // f of the chosen lo
         }
       }
     }
@@ -467,14 +477,22 @@ void ws_solve(const WsArgs& a, hipStream_t s) {
       dev::ws_solve_kernel<false, false, true, W2, 2>, dev::ws_solve_kernel<true, false, true, W2, 2>
   static const Fn fns2[8] = {WS_SOLVE_FNS2(false), WS_SOLVE_FNS2(true)};
 #undef WS_SOLVE_FNS2
+  // one slot per lane when q_max <= 64 (blocks of the 64-block rounds)
+#define WS_SOLVE_FNS1(W2)                                                                                        \
+  dev::ws_solve_kernel<false, false, false, W2, 1>, dev::ws_solve_kernel<true, false, false, W2, 1>,            \
+      dev::ws_solve_kernel<false, false, true, W2, 1>, dev::ws_solve_kernel<true, false, true, W2, 1>
+  static const Fn fns1[8] = {WS_SOLVE_FNS1(false), WS_SOLVE_FNS1(true)};
+#undef WS_SOLVE_FNS1
   const int v = (w2 ? 8 : 0) + (multi ? 4 : 0) + (box ? 2 : 0) + (full ? 1 : 0);
-  const bool two = a.q_max <= 128;
-  const Fn fn = two ? fns2[(w2 ? 4 : 0) + (multi ? 2 : 0) + (box ? 1 : 0)] : fns[v];
+  const int v2 = (w2 ? 4 : 0) + (multi ? 2 : 0) + (box ? 1 : 0);
+  const bool one = a.q_max <= 64, two = !one && a.q_max <= 128;
+  const Fn fn = one ? fns1[v2] : two ? fns2[v2] : fns[v];
   // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
   static size_t attr[16] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024,
                             64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
   static size_t attr2[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
-  size_t& at = two ? attr2[(w2 ? 4 : 0) + (multi ? 2 : 0) + (box ? 1 : 0)] : attr[v];
+  static size_t attr1[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
+  size_t& at = one ? attr1[v2] : two ? attr2[v2] : attr[v];
   if (lds > at) {
     HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     at = lds;

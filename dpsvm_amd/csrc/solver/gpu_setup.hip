@@ -540,10 +540,15 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // more workgroups; headline 0.0308 vs 0.0371 s at 8 x 192,
   // profiles/r3_union3072_ab.txt), never larger than ws_size; the one-block
   // rounds the adaptive count falls back to keep ws_size rows
-  const int auto_q = std::min(ws_q, kWsMaxAll / kWsAutoBlocks) & ~1;
+  static const int auto_blocks = [] {  // A/B: DPSVM_WS_AUTO_BLOCKS (2 .. kWsMaxBlocks)
+    const char* e = std::getenv("DPSVM_WS_AUTO_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 2 && v <= kWsMaxBlocks ? v : kWsAutoBlocks;
+  }();
+  const int auto_q = std::min(ws_q, kWsMaxAll / auto_blocks) & ~1;
   const bool blocks_auto = m.p.ws_blocks == 0;
   const int want_blocks = !blocks_auto ? m.p.ws_blocks
-                                       : (n >= kWsAutoBlocksRows ? std::min(kWsAutoBlocks, kWsMaxAll / auto_q) : 1);
+                                       : (n >= kWsAutoBlocksRows ? std::min(auto_blocks, kWsMaxAll / auto_q) : 1);
   const int mb_q = blocks_auto ? auto_q : ws_q;  // rows per block of the multi-block rounds
   // (only where working-set rounds can run: solver=smo or a small problem ignores ws_blocks)
   DPSVM_CHECK(!(ws_cand || wsc_cand) || want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
