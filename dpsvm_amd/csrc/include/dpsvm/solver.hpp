@@ -109,6 +109,9 @@ class GpuSolver {
   std::vector<float> gradient_all();
   // the stop tolerance of the next solve() (kernel arguments updated, captured graphs rebuilt)
   void set_eps(float eps);
+  // free the kernel-row cache / resident Gram until the next solve() (which
+  // allocates it again): ShrinkingSolver lends its memory to a shrunk phase
+  void release_cache();
   const GpuSetupInfo& info() const;
   struct Impl;
 

@@ -562,6 +562,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("k_set_split_gemm_variant", [](int v) { launch::set_split_gemm_variant(v); },
         "split STORE GEMM: 0 auto (4, or 3 when dp <= 128), 1 register-staged tile per workgroup, 3 LDS-DMA, 4 persistent LDS-DMA (tests / A/B)");
   m.def("k_split_gemm_variant", []() { return launch::split_gemm_variant(); });
+  m.def("k_split_rows", [](uintptr_t x, int64_t rows, int dp, int ldx, uintptr_t out, uintptr_t shift,
+                           uintptr_t stream) {
+    launch::split_rows_f16((const float*)x, rows, dp, ldx, (void*)out, (int32_t*)shift, (hipStream_t)stream);
+  });
   m.def("k_rbf_gram_split", [](uintptr_t a, uintptr_t asq, int64_t m_, uintptr_t b, uintptr_t bsq, int64_t n, int ld,
                                float gamma, uintptr_t out, int64_t out_ld, bool sym, uintptr_t stream) {
     kernels::rbf_gram_split((const float*)a, (const float*)asq, m_, (const float*)b, (const float*)bsq, n, ld, gamma,

@@ -131,6 +131,24 @@ void GpuSolver::set_eps(float eps) {
 }
 const GpuSetupInfo& GpuSolver::info() const { return impl_->info; }
 
+void GpuSolver::release_cache() {
+  auto& m = *impl_;
+  if (!m.lines) return;
+  HIP_CHECK(hipSetDevice(m.device));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  // the captured graphs hold the lines' address: recaptured by the next solve
+  if (m.gexec) (void)hipGraphExecDestroy(m.gexec);
+  if (m.graph) (void)hipGraphDestroy(m.graph);
+  if (m.gexec1) (void)hipGraphExecDestroy(m.gexec1);
+  if (m.graph1) (void)hipGraphDestroy(m.graph1);
+  m.gexec = m.gexec1 = nullptr;
+  m.graph = m.graph1 = nullptr;
+  HIP_CHECK(hipFree(m.lines));
+  m.lines = nullptr;
+  m.args.lines = nullptr;
+  m.wsa.gram = nullptr;
+}
+
 namespace {
 
 // Fast geometry of the one-device persistent dense engine: <= 256 workgroups

@@ -312,6 +312,23 @@ SolveResult ShrinkingSolver::solve(const Checkpoint* resume, const ProgressFn& p
     } else {
       SolverParams sp = p;
       sp.eps = eps_ph;
+      {
+        // the whole-problem solver holds its cache (cache_frac of the device):
+        // when the phase's resident Gram (na x na / world columns) does not fit
+        // what is left, lend it that memory until the next whole phase (which
+        // allocates it again); agreed, so every rank's phase sees the same sizes
+        HIP_CHECK(hipSetDevice(m.device));
+        size_t freeb = 0, totalb = 0;
+        HIP_CHECK(hipMemGetInfo(&freeb, &totalb));
+        const int64_t cols = (na + world - 1) / world;
+        const double need = (double)na * (double)((cols + 255) / 256 * 256) * 4.0;
+        static const bool force_release = [] {  // tests: DPSVM_SHRINK_RELEASE=1 lends it for every phase
+          const char* e = std::getenv("DPSVM_SHRINK_RELEASE");
+          return e && e[0] == '1';
+        }();
+        const bool fits = need < p.cache_frac * (double)freeb - 512.0 * (1 << 20) && !force_release;
+        if (!comm_all(m.comm, fits)) m.whole->release_cache();
+      }
       GpuSolver s(sp, m.comm, m.device);
       const GpuSetupInfo si = s.setup(xa.data(), na, na, d, ya.data());
       t_set = now() - t_phase;
@@ -441,6 +458,21 @@ SolveResult solve_shrinking(const SolverParams& p0, int device, const float* x, 
   return s.solve(resume, progress);
 }
 
+namespace {
+// the setup's cache budget (gpu_setup.hip) on this device: is the Gram block
+// K(all n rows, cols columns) NOT resident?  (every line >= cols floats,
+// padded to 256)
+bool gram_exceeds_device(const SolverParams& p, int64_t n, int64_t cols, int device) {
+  HIP_CHECK(hipSetDevice(device));
+  size_t freeb = 0, totalb = 0;
+  HIP_CHECK(hipMemGetInfo(&freeb, &totalb));
+  double budget = p.cache_frac * (double)freeb - 256.0 * 1024 * 1024;
+  if (p.cache_mb > 0) budget = std::min(budget, p.cache_mb * 1024.0 * 1024.0);
+  const double ld = (double)((cols + 255) / 256 * 256);
+  return (double)n * ld * 4.0 > budget;
+}
+}  // namespace
+
 bool shrink_auto(const SolverParams& p, int64_t n, int d, int device, Communicator* comm) {
   (void)d;
   if (p.solver == 1) return false;                       // solver=smo: the reference's trajectory
@@ -448,17 +480,15 @@ bool shrink_auto(const SolverParams& p, int64_t n, int d, int device, Communicat
   if (p.force_cache) return false;                     // an explicit engine request (tests, probes)
   if (comm && comm->size() > 1) {
     if (p.x_mode == 2) return false;                     // the phases need X on every rank
-    return !comm_all(comm, !shrink_auto(p, n, d, device, nullptr));  // any rank short of memory: shrink
+    // a rank holds the columns of its row shard (dp shard; dp auto shards when
+    // the whole Gram does not fit one device) or the whole Gram (dp replicate):
+    // shrink only when that footprint is not resident on some rank's device
+    // (covtype-ref at 8 ranks: 500k x 62.5k columns, 125 GB a rank, resident)
+    const int64_t P = comm->size();
+    const int64_t cols = p.dp_policy == 2 ? n : (n + P - 1) / P;
+    return !comm_all(comm, !gram_exceeds_device(p, n, cols, device));  // any rank short of memory: shrink
   }
-  HIP_CHECK(hipSetDevice(device));
-  size_t freeb = 0, totalb = 0;
-  HIP_CHECK(hipMemGetInfo(&freeb, &totalb));
-  // the setup's cache budget (gpu_setup.hip): the Gram is resident when every
-  // line (>= n floats, padded to 256 rows) fits it
-  double budget = p.cache_frac * (double)freeb - 256.0 * 1024 * 1024;
-  if (p.cache_mb > 0) budget = std::min(budget, p.cache_mb * 1024.0 * 1024.0);
-  const double ld = (double)((n + 255) / 256 * 256);
-  return (double)n * ld * 4.0 > budget;
+  return gram_exceeds_device(p, n, n, device);
 }
 
 }  // namespace dpsvm

@@ -88,6 +88,12 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   res.cache_lines = m.L;
   auto ts0 = Clock::now();
 
+  if (!m.lines) {  // released (release_cache): the same L lines again, empty
+    size_t tb = 0;
+    m.lines = gpu::dmalloc<float>((size_t)m.L * m.ldl, &tb);
+    m.args.lines = m.lines;
+    m.wsa.gram = m.lines;
+  }
   // ---- state init (alpha = 0, f = -y, empty cache) or resume ----
   int64_t iter0 = 0;
   float b_hi0 = 0.f, b_lo0 = 0.f;

@@ -259,3 +259,24 @@ def fused_select(f: torch.Tensor, alpha: torch.Tensor, y: torch.Tensor, C_: floa
     C.k_fused_select(fp.data_ptr(), ap.data_ptr(), yp.data_ptr(), n, float(C_), rows_per_group, out.data_ptr(),
                      _stream(f))
     return out[: 2 * groups].view(groups, 2)
+
+
+def split_rows(x: torch.Tensor, rows: int, dp: int, ldx: int | None = None):
+    """The split GEMMs' operand preparation (split_rows_kernel): per row a
+    power-of-two shift s (largest |x| into [2^14, 2^15)) and the fp16 planes
+    h = fp16(x 2^s), l = fp16(x 2^s - h), laid out as ceil(dp / 32) blocks of
+    32 h then 32 l values.  ``x``: a flat float32 CUDA tensor holding the rows at
+    stride ``ldx`` >= dp, columns d .. dp - 1 zero (any stride / offset: the
+    kernel's 16-B path needs ldx % 4 == 0 and an aligned base, else it reads
+    element by element).  Returns
+    (planes [rows, blocks, 2, 32] float16, shift [rows] int32)."""
+    C = load()
+    ldx = ldx or dp
+    if ldx < dp or x.numel() < (rows - 1) * ldx + dp:
+        raise ValueError("split_rows: need ldx >= dp and (rows - 1) * ldx + dp elements")
+    nkb = (dp + 31) // 32
+    planes = torch.zeros(rows * nkb * 64, device=x.device, dtype=torch.float16)
+    shift = torch.zeros(rows, device=x.device, dtype=torch.int32)
+    C.k_split_rows(x.data_ptr(), rows, dp, ldx, planes.data_ptr(), shift.data_ptr(), _stream(x))
+    torch.cuda.synchronize(x.device)
+    return planes.view(rows, nkb, 2, 32), shift

@@ -111,3 +111,39 @@ def test_split_gram_persistent_bit_identical_to_tile_kernel(K, n, m, d):
         assert torch.equal(got_sym, ref_sym), v
         assert torch.equal(got_xy, ref_xy), v
         assert torch.isfinite(got_sym).all() and torch.isfinite(got_xy).all()
+
+
+def _split_model(X, dp):
+    """numpy model of split_rows_kernel: shift to [2^14, 2^15), fp16 hi / lo planes"""
+    rows, d = X.shape
+    nkb = (dp + 31) // 32
+    Xp = np.zeros((rows, nkb * 32), np.float32)
+    Xp[:, :d] = X
+    m = np.abs(X).max(1)
+    e = np.frexp(m)[1]
+    s = np.where((m > 0) & np.isfinite(m), 15 - e, 0).astype(np.int32)
+    v = np.ldexp(Xp, s[:, None]).astype(np.float32)
+    h = v.astype(np.float16)
+    lo = (v - h.astype(np.float32)).astype(np.float16)
+    planes = np.stack([h.reshape(rows, nkb, 32), lo.reshape(rows, nkb, 32)], axis=2)
+    return planes, s
+
+
+@pytest.mark.parametrize("d,ldx,offset", [(2200, 2208, 0), (1100, 1105, 0), (784, 784, 1), (3000, 3009, 3)])
+def test_split_rows_long_and_unaligned_rows(K, d, ldx, offset):
+    """split_rows_kernel beyond 2,048 columns (the loop that reloads from memory
+    past the register-held chunks) and with an odd row stride / a base pointer
+    off 16-B alignment (the element-by-element path): bit-identical to the
+    numpy model of the split."""
+    rng = np.random.default_rng(d + ldx + offset)
+    rows = 37
+    X = (rng.standard_normal((rows, d)) * np.exp(rng.uniform(-8, 8, (rows, 1)))).astype(np.float32)
+    buf = np.zeros(offset + rows * ldx, np.float32)
+    for r in range(rows):
+        buf[offset + r * ldx: offset + r * ldx + d] = X[r]
+    xt = torch.from_numpy(buf).cuda()
+    dp = (d + 15) // 16 * 16
+    planes, shift = K.split_rows(xt[offset:], rows, dp, ldx)
+    want_p, want_s = _split_model(X, dp)
+    np.testing.assert_array_equal(shift.cpu().numpy(), want_s)
+    np.testing.assert_array_equal(planes.cpu().numpy().view(np.uint16), want_p.view(np.uint16))

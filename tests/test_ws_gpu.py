@@ -699,3 +699,67 @@ def test_shrinking_multi_rank(world):
     assert abs(outs[0].b_ - one.b_) < 2e-2
     assert abs(outs[0].n_support_ - one.n_support_) <= max(5, one.n_support_ // 50)
     assert _kkt_gap(X, y, outs[0].alpha_, C_, g) < 2e-3 + 5e-4
+
+
+def test_shrink_auto_judges_the_rank_shard_not_the_whole_gram():
+    """shrink="auto" at world > 1 compares the per-rank Gram footprint of the
+    sharded solve (n x n / P columns) with the device budget, not the whole n x n
+    Gram: a cap that holds half of the headline's Gram but not
+    all of it shrinks at one rank and not at two (dp auto / shard), and still
+    shrinks at two with dp replicate."""
+    import threading
+
+    from dpsvm_amd import SVCConfig
+    from dpsvm_amd._native import load
+
+    C = load()
+    n, d = 60000, 784
+    out = {}
+    for world, dp in ((1, "auto"), (2, "auto"), (2, "replicate")):
+        p = SVCConfig(C=10.0, gamma=0.25, cache_mb=10000, dp=dp).to_native(d)  # 10 GB: 14.4 GB whole, 7.2 GB a shard
+        if world == 1:
+            out[(world, dp)] = [bool(C.shrink_auto(p, n, d, 0, None))]
+            continue
+        g = C.ThreadCommGroup(world)
+        comms = [g.comm(r) for r in range(world)]
+        res = [None] * world
+
+        def work(r):
+            res[r] = bool(C.shrink_auto(p, n, d, 0, comms[r]))
+
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        out[(world, dp)] = res
+    assert out[(1, "auto")] == [True]
+    assert out[(2, "auto")] == [False, False]
+    assert out[(2, "replicate")] == [True, True]
+
+
+def test_shrinking_lends_the_whole_solvers_cache_bit_identically(monkeypatch):
+    """A shrunk phase whose Gram does not fit the memory the whole-problem
+    solver leaves gets that solver's cache (release_cache; the next whole phase
+    allocates it again and recaptures its graphs).  Forced for every phase here
+    (DPSVM_SHRINK_RELEASE=1, read once per process: a fresh interpreter): the
+    run is bit-identical to one that keeps the cache."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    code = ("import json, sys, hashlib; sys.path.insert(0, %r)\n"
+            "from dpsvm_amd import SVC\nfrom dpsvm_amd.utils.datasets import synthetic\n"
+            "X, y = synthetic('covtype', n=30000, seed=8)\n"
+            "c = SVC(C=64.0, gamma=0.25, eps=1e-3, clip='box', device='cuda', solver='ws', max_iter=5_000_000,"
+            " shrink='on', force_cache=True, cache_lines=20000).fit(X, y)\n"
+            "print(json.dumps({'sha': hashlib.sha256(c.alpha_.tobytes()).hexdigest(), 'b': float(c.b_),"
+            " 'phases': int(c.stats_['shrink_phases']), 'conv': bool(c.converged_)}))\n"
+            % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    outs = []
+    for rel in ("0", "1"):
+        env = dict(os.environ, DPSVM_SHRINK_RELEASE=rel)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[0]["phases"] >= 2 and outs[0]["conv"]
+    assert outs[0] == outs[1]
