@@ -47,8 +47,21 @@ def probe_pass1(path):
 
 
 def main() -> int:
-    path = sys.argv[1] if len(sys.argv) > 1 else "profiles/r3_shard_projection_inputs_1gpu.json"
-    probe = probe_pass1(sys.argv[2]) if len(sys.argv) > 2 else {}
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("inputs", nargs="?", default="profiles/r3_shard_projection_inputs_1gpu.json")
+    ap.add_argument("probe", nargs="?", default=None)
+    ap.add_argument("--rehearsal", action="append", default=[],
+                    help="P:path of a bench/shard_stamps.py JSON of a P-rank run sharing ONE GPU: its measured "
+                         "exchange consumer cost per round replaces the assumed xGMI latency for that P")
+    a = ap.parse_args()
+    path = a.inputs
+    probe = probe_pass1(a.probe) if a.probe else {}
+    reh = {}
+    for spec in a.rehearsal:
+        P, f = spec.split(":", 1)
+        reh[int(P)] = json.load(open(f))
     m = json.load(open(path))
     r = m["round_us"]
     rounds = m["local"]["rounds"]
@@ -108,6 +121,29 @@ def main() -> int:
                 per_round = fixed + p1 + r["select_pass2"] / P + gaps + max(0.0, ext) + xfer
                 row.append(m["gram_slab_s"][str(P)] + rounds * per_round * 1e-6)
             print(f"{X:>6} {W:>7} | " + " | ".join(f"{v:.4f}  " for v in row))
+    if reh:
+        # MEASURED on ONE GPU with P ranks sharing it (bench/shard_stamps.py): the
+        # exchange consumers' time per round (candidate collect, partials collect,
+        # the solve's sub-Gram poll + load) — they wait for every rank's pushes,
+        # and on one device also for the other ranks' kernels: an upper bound of
+        # the exchange cost across P GPUs
+        print("PEER EXCHANGE, consumer cost per round MEASURED in one-GPU rehearsals (upper bound; no assumed latency)")
+        row = []
+        for P in (1, 2, 4, 8):
+            if P == 1:
+                row.append(f"{m['local']['s']:.4f}")
+                continue
+            if P not in reh:
+                row.append("   -   ")
+                continue
+            exch = reh[P]["exchange_consumer_us_per_round"]
+            p1 = probe.get(P, pass1 / P)
+            per_round = fixed - r["load_subgram"] + p1 + r["select_pass2"] / P + gaps + exch
+            row.append(f"{m['gram_slab_s'][str(P)] + rounds * per_round * 1e-6:.4f}")
+        print(f"{'':>14} | " + " | ".join(f"P={p} {v}" for p, v in zip((1, 2, 4, 8), row)))
+        for P, d in sorted(reh.items()):
+            print(f"  P={P}: consumer cost {d['exchange_consumer_us_per_round']} us/round "
+                  f"(median over {d['ranks']} ranks: {d['median_over_ranks']})")
     return 0
 
 
