@@ -36,7 +36,10 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "dpsvm/common.hpp"
 #include "device_util.hpp"
@@ -814,14 +817,23 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 constexpr int kW64Threads = 512;
 // NT 1: non-temporal Gram stores (measured slower, profiles/r4_gram_nt_store_ab.txt);
 // NT 2: diagnostics only — stores skipped unless a value is NaN (the store-free time)
+// tiles: nullptr = the whole tm x tn grid in the XCD order; else a compact
+// table of the tiles to compute (the symmetric Gram's upper tiles, host-built
+// in the XCD order: no workgroup is launched only to exit)
 template <int NT>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
-    float gamma, float* __restrict__ out, int64_t ldo, int sym) {
+    float gamma, float* __restrict__ out, int64_t ldo, int sym, const uint32_t* __restrict__ tiles) {
   constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
   int64_t tx, ty;
-  xcd_tile(tx, ty);
+  if (tiles) {
+    const uint32_t t = tiles[blockIdx.x];  // (tx << 16) | ty
+    tx = t >> 16;
+    ty = t & 0xffffu;
+  } else {
+    xcd_tile(tx, ty);
+  }
   if (sym && ty < 2 * tx) return;  // uniform: both 128-row blocks below the diagonal
   __shared__ u4 lds[NB * BUF + 2 * ROWS / 4];  // 3 operand buffers, then |x|^2 [ROWS] and shifts [ROWS]
   float* s_sq = (float*)(lds + NB * BUF);
@@ -1403,6 +1415,52 @@ void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, in
   post_launch("split_rows_f16", s);
 }
 
+namespace {
+// The symmetric Gram's upper tiles of the 256 x 128 wide-wave kernel (tile
+// (tx, ty) is needed when ty >= 2 tx) as a compact table in the XCD order of
+// xcd_tile_of (chunks of 64 tiles of 8 tile rows dealt round-robin to the 8
+// XCDs): built once per shape on the host, kept on the device.  The full grid
+// launched tm x tn workgroups of which half exited at once (55k of 110k on
+// the headline).
+struct TileTable {
+  uint32_t* dev = nullptr;
+  int64_t count = 0;
+};
+const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int64_t, int64_t>, TileTable> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({tm, tn});
+  if (it != cache.end()) return it->second;
+  // the needed tiles in the order xcd_tile_of's bijection visits them: groups of
+  // 8 tile rows, column by column, rows inside a column
+  std::vector<uint32_t> order;
+  constexpr int64_t GM = 8, CH = 64;
+  for (int64_t g0 = 0; g0 < tm; g0 += GM) {
+    const int64_t gm = std::min(GM, tm - g0);
+    for (int64_t ty = 0; ty < tn; ++ty)
+      for (int64_t tx = g0; tx < g0 + gm; ++tx)
+        if (ty >= 2 * tx) order.push_back((uint32_t)((tx << 16) | ty));
+  }
+  const int64_t total = (int64_t)order.size(), full = total / (8 * CH) * (8 * CH);
+  std::vector<uint32_t> tab((size_t)total);
+  for (int64_t L = 0; L < total; ++L) {  // workgroup L runs on XCD L % 8: XCD x takes chunks x, x + 8, ...
+    int64_t T = L;
+    if (L < full) {
+      const int64_t xcd = L % 8, local = L / 8;
+      T = ((local / CH) * 8 + xcd) * CH + local % CH;
+    }
+    tab[(size_t)L] = order[(size_t)T];
+  }
+  TileTable t;
+  t.count = total;
+  HIP_CHECK(hipMalloc((void**)&t.dev, (size_t)total * sizeof(uint32_t)));
+  HIP_CHECK(hipMemcpyAsync(t.dev, tab.data(), (size_t)total * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return cache.emplace(std::make_pair(tm, tn), t).first->second;
+}
+}  // namespace
+
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
                           int64_t ldo, hipStream_t s, bool symmetric) {
@@ -1432,9 +1490,19 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     const int64_t tm2 = (M + 255) / 256;
     auto kern = nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
                 : nt ? dev::rbf_gemm_split_w64_kernel<1> : dev::rbf_gemm_split_w64_kernel<0>;
-    kern<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
-        (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
-        symmetric ? 1 : 0);
+    static const bool compact = [] {  // A/B: DPSVM_GRAM_COMPACT=0 launches the full grid (half exit at once)
+      const char* e = std::getenv("DPSVM_GRAM_COMPACT");
+      return !(e && e[0] == '0');
+    }();
+    if (symmetric && compact && tm2 < 65536 && tn < 65536) {
+      const auto& tab = sym_tile_table(tm2, tn, s);
+      kern<<<dim3((unsigned)tab.count), dev::kW64Threads, 0, s>>>(
+          (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo, 1, tab.dev);
+    } else {
+      kern<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
+          (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
+          symmetric ? 1 : 0, nullptr);
+    }
     post_launch("rbf_gemm_split_w64", s);
     return;
   }
