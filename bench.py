@@ -192,8 +192,9 @@ def spawn_ranks(a, argv) -> int:
         # queues per process, 8 processes oversubscribe the device's queues and the
         # scheduler time-slices them: a round's spinning consumers then wait out
         # whole quanta for a descheduled peer's pushes (8-rank headline 2.30 s
-        # vs 0.065 s with 2 queues each, profiles/r5_rehearsal_queues_1gpu.txt)
-        env.setdefault("GPU_MAX_HW_QUEUES", "2")
+        # vs 0.065 s with 2 queues each, profiles/r5_rehearsal_queues_1gpu.txt).
+        # Overridden even when the environment sets it (the GPU boxes export 4)
+        env["GPU_MAX_HW_QUEUES"] = os.environ.get("DPSVM_REHEARSAL_HW_QUEUES", "2")
     env["DPSVM_BENCH_SPAWNED"] = str(n)
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),

@@ -44,7 +44,7 @@ case "$task" in
     exit $rc ;;
   mp)
     N=$1; shift
-    export DPSVM_FORCE_DEVICE=0 DPSVM_XCH_TIMEOUT_S=${DPSVM_XCH_TIMEOUT_S:-30} GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-2}
+    export DPSVM_FORCE_DEVICE=0 DPSVM_XCH_TIMEOUT_S=${DPSVM_XCH_TIMEOUT_S:-30} GPU_MAX_HW_QUEUES=${DPSVM_REHEARSAL_HW_QUEUES:-2}
     timeout -k 10 "$LIMIT" python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" \
       --master-addr 127.0.0.1 --master-port $((29600 + N)) bench.py --gpus "$N" --comm gloo "$@" \
       > "gpurun_out/mp${N}_$TAG.log" 2>&1
