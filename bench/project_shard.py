@@ -36,14 +36,24 @@ def pass1_splits(G: int) -> int:
     return max(1, min(16, 256 // max(1, G)))  # kernels ws_pass1_splits
 
 
+def pass1_v4_splits(p1G: int) -> int:
+    return max(1, min(32, 256 // max(1, p1G)))  # kernels ws_pass1_v4_splits
+
+
 def probe_pass1(path):
-    """{P: pass-1 us} at the shard shapes of the probe (the solver's split)"""
-    out = {}
+    """{P: pass-1 us} at the shard shapes of the probe, with the solver's split:
+    the wide pass 1 (the default since round 5) when the probe holds it, else
+    the selection-geometry pass 1"""
+    wide, sel = {}, {}
     for line in open(path):
         r = json.loads(line)
-        if r["rows"] == 60000 and r["ks"] == pass1_splits(r["G"]):
-            out[60000 // r["cols"]] = r["pass1_us_median"]
-    return out
+        if r["rows"] != 60000:
+            continue
+        if r.get("wide") and r["ks"] == pass1_v4_splits(r["p1G"]):
+            wide[60000 // r["cols"]] = r["pass1_us_median"]
+        elif not r.get("wide") and r["ks"] == pass1_splits(r["G"]):
+            sel[60000 // r["cols"]] = r["pass1_us_median"]
+    return wide or sel
 
 
 def main() -> int:
