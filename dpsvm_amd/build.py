@@ -58,6 +58,7 @@ LIB_SOURCES = [
     "kernels/ws_select.hip",
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
+    "kernels/ws_persist.hip",
 ]
 # the quarantined engines (solver/gpu_engines_pairq.hip registers them): a plugin
 # library for the Python module, linked into the CLIs (svmTrain --engines all)

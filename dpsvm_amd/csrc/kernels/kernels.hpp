@@ -79,6 +79,13 @@ void ws_select(const WsArgs& a, hipStream_t s);
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s);
 void ws_gather(const WsArgs& a, hipStream_t s);
 void ws_solve(const WsArgs& a, hipStream_t s);
+// persistent small-problem rounds (ws_persist.hip): `rounds` one-block rounds in
+// one launch of a.G co-resident workgroups; census: rounds = -1 on a.psync + 2
+bool ws_persist_supported(const WsArgs& a);
+size_t ws_persist_lds(const WsArgs& a);
+int ws_persist_blocks_per_cu(const WsArgs& a);
+void ws_persist_census(const WsArgs& a, hipStream_t s);
+void ws_persist(const WsArgs& a, int rounds, hipStream_t s);
 // cache mode: the merge + line assignment (one workgroup) runs before the
 // row GEMM; ws_gather then reads the sub-Gram from the members' lines
 void ws_merge(const WsArgs& a, hipStream_t s);

@@ -367,6 +367,10 @@ struct WsRounds : Base {
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
     ws_allgather_cand(m);
+    if (m.ws_persist) {  // persistent rounds (ws_persist.hip): no graph; arrivals == G x released rounds
+      HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 16, m.stream));
+      return;
+    }
     if (ws_graphs(m) && !m.gexec) capture_rounds(m, this->block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });
   }
   void observe(GpuSolver::Impl& m, const SmoStatus& st, int64_t blocks_done) override {
@@ -385,6 +389,10 @@ struct WsRounds : Base {
     if (ws_graphs(m) && !m.gexec1) capture_rounds(m, this->block(m.p), &m.graph1, &m.gexec1, [&] { round(m, w); });
   }
   void run_block(GpuSolver::Impl& m, int B) override {
+    if (m.ws_persist && !single) {
+      launch::ws_persist(m.wsa, B, m.stream);
+      return;
+    }
     hipGraphExec_t g = single ? m.gexec1 : m.gexec;
     if (g) {
       HIP_CHECK(hipGraphLaunch(g, m.stream));

@@ -37,7 +37,7 @@ GpuSolver::Impl::~Impl() {
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
-                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wsdfs, (void*)wsdalpha, (void*)wspart, (void*)wssorted,
+                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wspsync, (void*)wsdfs, (void*)wsdalpha, (void*)wspart, (void*)wssorted,
                     (void*)wsxq, (void*)wsxqsq, (void*)wsiota, xs, (void*)xsh, wsxs, (void*)wsxsh})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
@@ -213,6 +213,53 @@ int max_device_sharing(GpuSolver::Impl& m) {
     most = std::max(most, k);
   }
   return most;
+}
+
+// Persistent small-problem rounds (ws_persist.hip): ws-dense at one rank with
+// one block per round — auto up to kWsPersistAutoGroups selection groups (the
+// rounds of a small active set are launch- and merge-bound, a large set's are
+// f-update-bound).  Its grid spins on its own workgroups, so a census of the
+// kernel's own grid and resources comes first; a failed census keeps the graph.
+void ws_persist_setup(GpuSolver::Impl& m) {
+  WsArgs& w = m.wsa;
+  m.ws_persist = false;
+  w.psync = nullptr;
+  m.info.ws_rounds = "graph";
+  int mode = m.p.ws_persist;  // 0 auto, 1 on, 2 off
+  if (const char* e = std::getenv("DPSVM_WS_PERSIST")) mode = std::atoi(e);  // A/B runs
+  if (mode == 2 || m.kind != EngineKind::WsDense || m.world != 1 || w.blocks != 1 || w.off != 0) return;
+  if (mode == 0 && w.G > kWsPersistAutoGroups) return;
+  if (!m.wspsync) m.wspsync = dmalloc<int32_t>(4, &m.bytes);
+  w.psync = m.wspsync;
+  if (!launch::ws_persist_supported(w)) {
+    w.psync = nullptr;
+    return;
+  }
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m.device));
+  const int per_cu = launch::ws_persist_blocks_per_cu(w);
+  bool ok = per_cu >= 1 && w.G <= cus;
+  int32_t h[4] = {0, 0, 0, 0};
+  if (ok) {
+    HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 16, m.stream));
+    w.xtimeout_ticks = (int64_t)(2.0 * 1e8);  // census: 2 s
+    launch::ws_persist_census(w, m.stream);
+    HIP_CHECK(hipMemcpyAsync(h, m.wspsync, 16, hipMemcpyDeviceToHost, m.stream));
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    ok = h[3] == 0 && h[2] == w.G;
+  }
+  HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 16, m.stream));
+  if (!ok) {
+    m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") + "ws persistent rounds: census " +
+                          std::to_string(h[2]) + "/" + std::to_string(w.G) + " workgroups co-resident (" +
+                          std::to_string(per_cu) + " per CU): graph rounds";
+    w.psync = nullptr;
+    return;
+  }
+  // a round boundary waits microseconds; 10 s means the grid lost residency
+  w.xtimeout_ticks = (int64_t)(10.0 * 1e8);
+  m.ws_persist = true;
+  m.info.ws_rounds = "persistent";
 }
 
 }  // namespace
@@ -829,6 +876,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       HIP_CHECK(hipMemcpyAsync(m.wsiota, io.data(), io.size() * 4, hipMemcpyHostToDevice, m.stream));
       HIP_CHECK(hipStreamSynchronize(m.stream));
     }
+    ws_persist_setup(m);
   }
   m.engine = gpu::make_engine(m.kind);
   m.info.iteration = engine_name(m.kind);

@@ -119,7 +119,10 @@ class SVCConfig:
     ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
-    ws_block: int = 8               # rounds per hipGraph block
+    ws_block: int = 8               # rounds per hipGraph block (or per persistent-round launch)
+    # persistent small-problem rounds (one launch per ws_block rounds, ws_persist.hip): auto (one GPU, one
+    # block, resident Gram, <= 16,384 rows) | on (wherever supported) | off (a graph of launches per round)
+    ws_persist: str = "auto"
     # one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking: phases on the rows that can
     # still violate, the rest of the gradient updated by one predict GEMM per phase).  auto: on where it
     # pays — one GPU, working-set rounds, the whole Gram not resident (C.shrink_auto) | on | off
@@ -203,6 +206,7 @@ class SVCConfig:
         p.ws_t_halve = float(self.ws_t_halve)
         p.ws_clip_fallback = int(bool(self.ws_clip_fallback))
         p.ws_block = int(self.ws_block)
+        p.ws_persist = _pick({"auto": 0, "on": 1, "off": 2}, self.ws_persist, "ws_persist")
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         p.gram_precision = _pick({"auto": 0, "f32": 1, "split": 2}, self.gram, "gram")
         return p

@@ -25,6 +25,7 @@ SPILL_FREE = [
     "kernels/ws_select.hip",
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
+    "kernels/ws_persist.hip",
     "kernels/smo_persist.hip",
     "kernels/compact.hip",
 ]
