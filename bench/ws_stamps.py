@@ -20,11 +20,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def persistent_report(a, clf, raw, rounds) -> int:
     """persistent rounds (ws_persist.hip, workgroup 0): [0] round start, [1]
-    arrivals seen, [2] merged, [3] sub-Gram in LDS, [4] solved, then — in the
+    arrivals seen, [2] merged, [8] gather arrivals seen, [3] sub-Gram in LDS,
+    [4] solved, then — in the
     next slot — [6] release seen, [10] f updated, [7] candidates published"""
     s = raw[2:rounds - 1]
     nx = raw[3:rounds]  # the select phase that follows round r sits in slot r + 1
-    ok = (s[:, [0, 1, 2, 3, 4]] > 0).all(axis=1) & (nx[:, [6, 7, 10]] > 0).all(axis=1)
+    ok = (s[:, [0, 1, 2, 3, 4, 8]] > 0).all(axis=1) & (nx[:, [6, 7, 10]] > 0).all(axis=1)
     s, nx = s[ok], nx[ok]
     us = lambda v: np.round(np.median(v) * 0.01, 2)  # noqa: E731
     res = {
@@ -33,7 +34,8 @@ def persistent_report(a, clf, raw, rounds) -> int:
         "ws_rounds": "persistent", "steps_per_round_median": float(np.median(s[:, 5])),
         "arrival_wait_us": us(s[:, 1] - s[:, 0]),
         "merge_us": us(s[:, 2] - s[:, 1]),
-        "gather_subgram_to_lds_us": us(s[:, 3] - s[:, 2]),
+        "gather_and_arrivals_us": us(s[:, 8] - s[:, 2]),
+        "subgram_to_lds_us": us(s[:, 3] - s[:, 8]),
         "solve_us": us(s[:, 4] - s[:, 3]),
         "solve_per_step_us": float(np.round(np.median((s[:, 4] - s[:, 3]) / np.maximum(1, s[:, 5])) * 0.01, 3)),
         "commit_to_release_seen_us": us(nx[:, 6] - s[:, 4]),

@@ -133,8 +133,8 @@ struct SolverParams {
   int ws_wss = 0;             // sub-problem pair choice: 1 the reference's first-order rule (max f over I_low),
                               // 2 second order (WSS2: max (f_lo - b_hi)^2 / eta); the stop test is unchanged;
                               // 0 auto: second order when a row sample's mean off-diagonal K > 0.1
-  int ws_persist = 0;         // persistent small-problem rounds (ws_persist.hip): 0 auto (one rank, one block,
-                              // resident Gram, <= kWsPersistAutoGroups x 256 rows), 1 on where supported, 2 off
+  int ws_persist = 0;         // persistent one-block rounds (ws_persist.hip: one rank, resident Gram): 1 on where
+                              // supported; 0 auto and 2 off keep the graph of launches (measured faster)
   int ws_block = 8;           // rounds per hipGraph block (the host stops at most ~2 blocks past convergence;
                               // the one-block switch stays on 32-round boundaries: same trajectories)
   float ws_t_halve = 0.9f;    // multi-block: a round damped below this line-search factor halves the block count

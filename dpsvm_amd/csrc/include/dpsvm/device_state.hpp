@@ -296,8 +296,7 @@ constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: 
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 constexpr int kWsMaxPass1Splits = 16;             // multi-block f-update pass 1: list slices over workgroups
 constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
-constexpr int64_t kWsSwitchRounds = 32;
-constexpr int kWsPersistAutoGroups = 64;          // ws_persist auto: persistent rounds up to 64 x 256 rows           // multi-block -> one-block graph switch granularity (rounds)
+constexpr int64_t kWsSwitchRounds = 32;           // multi-block -> one-block graph switch granularity (rounds)
 
 struct alignas(16) WsCtrl {
   int64_t iter;      // pair updates applied so far
@@ -398,7 +397,8 @@ struct WsArgs {
   int32_t p1G;         // multi-block pass 1: column groups per rank (= G; the wide pass 1: ceil(nl_max / 1024))
   int32_t p1v4;        // multi-block pass 1: 1 = wide column groups, 4 columns (16-B loads) per thread
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
-  int32_t* psync;      // persistent rounds (ws_persist.hip): [0] arrivals, [1] rounds released, [2..3] census
+  int32_t* psync;      // persistent rounds (ws_persist.hip): [0] selection arrivals, [1] rounds released,
+                       // [2..3] census, [4] gather arrivals (8 words)
 };
 // u64 words of the working-set exchange region (both parities): one-block
 // engine

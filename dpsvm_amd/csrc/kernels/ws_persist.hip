@@ -3,30 +3,31 @@
 // G co-resident workgroups (one per CU, checked by a census at setup), with
 // the round's kernel boundaries replaced by two one-way signals:
 //
-//   workgroup 0   merge (stop test + next working set, ws_merge.hpp), the q x q
-//                 sub-Gram gathered from the Gram straight into LDS, the pair
-//                 loop on wave 0 and the commit (ws_solve.hpp) — then it
+//   every group   waits for the G selection arrivals of the previous round
+//                 (psync[0]), merges the candidate lists (stop test + next
+//                 working set, ws_merge.hpp — redundantly, as ws_gather does),
+//                 gathers rows grp, grp + G, ... of the q x q sub-Gram into
+//                 global memory and arrives (psync[4]);
+//   workgroup 0   waits for those G arrivals, loads the sub-Gram into LDS, runs
+//                 the pair loop on wave 0 and the commit (ws_solve.hpp), then
 //                 releases the round (psync[1] = rounds released);
 //   every group   waits for the release, applies the round's alpha changes to
 //                 its 256 columns of f and publishes its candidate lists (the
 //                 ws_select arithmetic: the same four list partitions summed in
 //                 the same order, so f, the candidates and the trajectory are
-//                 bit-identical to the graph of launches), then arrives
-//                 (psync[0] += 1); workgroup 0 waits for G arrivals before its
-//                 next merge.
+//                 bit-identical to the graph of launches), then arrives.
 //
 // The graph path spends ~29 us of a ~74 us round of the covtype-shape 7.5k-row
 // sub-problem outside the solve (four launches: select 9.3, merge 8.0, gather
 // and sub-Gram load 4.4, launch gaps ~6; profiles/r4_ws_stamps_cov7500*.json);
-// here the merge runs once (not in all q gather workgroups), the sub-Gram never
-// goes through global memory, and a round boundary is two agent-scope fences
-// plus an atomic.  Cross-workgroup data (f rows of the set, alpha, candidate
+// here a round boundary is an agent-scope fence pair plus an atomic per
+// signal (three per round).  Cross-workgroup data (f rows of the set, alpha, candidate
 // lists, the control record) moves under release / acquire fences at agent
 // scope (the XCDs' L2s are not coherent with each other).  Every wait is
 // bounded (a.xtimeout_ticks): a grid that is not co-resident ends the run with
 // kCommFail instead of hanging.  Stamps (DPSVM_STAMPS, workgroup 0): [0] round
-// start, [1] arrivals seen, [2] merged, [3] sub-Gram in LDS, [4] solved, [6]
-// release seen, [10] f updated, [7] candidates published.  Reference round:
+// start, [1] arrivals seen, [2] merged, [8] gather arrivals seen, [3] sub-Gram
+// in LDS, [4] solved, [6] release seen, [10] f updated, [7] candidates published.  Reference round:
 // svmTrainMain.cpp:235-310.
 #include <hip/hip_runtime.h>
 
@@ -95,58 +96,109 @@ __global__ __launch_bounds__(kWpThreads, 1) void ws_persist_kernel(WsArgs a, int
   const bool has = j < a.nl;
 
   for (int r = 0; r < rounds; ++r) {
-    // ================= workgroup 0: merge, sub-Gram, solve, commit =================
-    if (wg0) {
-      if (lead) WS_STAMP(0);
-      if (tid == 0) s_word[1] = r == 0 || wp_wait(sync, G * (gen0 + r), a.xtimeout_ticks) ? 1 : 0;
-      __syncthreads();
-      if (!s_word[1]) {
-        if (tid == 0) wp_fail(a, c);
-        break;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the groups' f, candidate lists
-      if (lead) WS_STAMP(1);
-      int q = 0;
-      float b_hi = 0.f, b_lo = 0.f;
-      WsMergeLds& L = *(WsMergeLds*)lds;
-      if (ws_merge(a, c, s_set, &q, &b_hi, &b_lo, L)) {  // ends with a barrier (L is dead after it)
-        if (lead) WS_STAMP(2);
-        const int par = (int)(c->outer & 1);
-        const int64_t it0 = c->iter;
-        const int ldk = a.q_max;
+    const int32_t gen = gen0 + r;  // rounds released before this one
+    // ---- every group: the previous round's selections are in (r = 0: the
+    // launch boundary), then the merge — redundantly, identical inputs and
+    // arithmetic, as in ws_gather: no group waits for a published set ----
+    if (wg0 && tid == 0) WS_STAMP(0);
+    if (tid == 0) s_word[1] = r == 0 || wp_wait(sync, G * gen, a.xtimeout_ticks) ? 1 : 0;
+    __syncthreads();
+    if (!s_word[1]) {
+      if (tid == 0) wp_fail(a, c);
+      break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every group's f and candidate lists
+    if (lead) WS_STAMP(1);
+    int q = 0;
+    float b_hi = 0.f, b_lo = 0.f;
+    const bool go = ws_merge(a, c, s_set, &q, &b_hi, &b_lo, *(WsMergeLds*)lds);  // ends with a barrier
+    const int par = (int)(c->outer & 1);
+    const int ldk = a.q_max;
+    if (go) {
+      if (lead) WS_STAMP(2);
+      if (wg0) {
         for (int t = tid; t < q; t += kWpThreads) {
-          const int32_t gi = s_set[t];
-          c->idx[par][t] = gi;
-          c->line[par][t] = gi;  // the resident Gram: line i is row i
-          s_line[t] = gi;
-          s_f[t] = a.f[gi];      // one rank: local row = global row
-          s_a[t] = a.alpha[gi];
-          s_y[t] = a.y[gi];
+          c->idx[par][t] = s_set[t];
+          c->line[par][t] = s_set[t];  // the resident Gram: line i is row i
         }
         if (tid == 0) {
           c->q[par] = q;
           c->b_hi = b_hi;
           c->b_lo = b_lo;
         }
-        // rows a < q of the q_max-stride sub-Gram (columns >= q zero): q random
-        // columns of each member's Gram row, 16 loads in flight per thread
+      }
+      // the sub-Gram rows ra = grp, grp + G, ... (q random columns of member
+      // ra's Gram row; columns q .. q_max - 1 zero) and their f / alpha / y,
+      // through global memory to workgroup 0 (the scattered reads of one CU
+      // would take ~30 us: the whole grid issues them)
+      const int my_rows = q > grp ? (q - grp + G - 1) / G : 0;
+      const int n = my_rows * ldk;
+      constexpr int U = 8;
+      for (int e0 = tid; e0 < n; e0 += U * kWpThreads) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * kWpThreads;
+          const int k = e / ldk, col = e - k * ldk;
+          const bool in = e < n && col < q;
+          v[u] = in ? a.gram[(int64_t)s_set[grp + k * G] * a.ldg + s_set[col]] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * kWpThreads;
+          const int k = e / ldk, col = e - k * ldk;
+          if (e < n) a.subg[(size_t)(grp + k * G) * ldk + col] = v[u];
+        }
+      }
+      for (int k = tid; k < my_rows; k += kWpThreads) {
+        const int ra = grp + k * G;
+        const int32_t gi = s_set[ra];
+        a.aux[ra] = a.f[gi];  // one rank: local row = global row
+        a.aux[a.aux_stride + ra] = a.alpha[gi];
+        a.aux[2 * a.aux_stride + ra] = a.y[gi];
+      }
+    }
+    // every group arrives (also when the run stopped: the counts stay G per round)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(sync + 4, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+
+    // ---- workgroup 0: the sub-Gram into LDS, the pair loop, the commit ----
+    if (wg0) {
+      if (go) {
+        if (tid == 0) s_word[1] = wp_wait(sync + 4, G * (gen + 1), a.xtimeout_ticks) ? 1 : 0;
+        __syncthreads();
+        if (!s_word[1]) {
+          if (tid == 0) wp_fail(a, c);
+          break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lead) WS_STAMP(8);
+        const int64_t it0 = c->iter;
         float* K = lds;
-        const int n = q * ldk;
-        constexpr int U = 16;
-        for (int e0 = tid; e0 < n; e0 += U * kWpThreads) {
-          float v[U];
+        if ((ldk & 3) == 0) {  // q rows x q_max: 16-B loads, four in flight per thread
+          const f4* src = (const f4*)a.subg;
+          f4* dst = (f4*)K;
+          const int n4 = q * ldk / 4;
+          for (int e = tid; e < n4; e += 4 * kWpThreads) {
+            f4 v[4];
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int e = e0 + u * kWpThreads;
-            const int ra = e / ldk, col = e - ra * ldk;
-            const bool in = e < n && col < q;
-            v[u] = in ? a.gram[(int64_t)s_set[ra] * a.ldg + s_set[col]] : 0.f;
-          }
+            for (int u = 0; u < 4; ++u) {
+              const int k = e + u * kWpThreads;
+              v[u] = src[k < n4 ? k : 0];
+            }
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int e = e0 + u * kWpThreads;
-            if (e < n) K[e] = v[u];
+            for (int u = 0; u < 4; ++u)
+              if (e + u * kWpThreads < n4) dst[e + u * kWpThreads] = v[u];
           }
+        } else {
+          for (int e = tid; e < q * ldk; e += kWpThreads) K[e] = a.subg[e];
+        }
+        for (int t = tid; t < q; t += kWpThreads) {
+          s_line[t] = s_set[t];
+          s_f[t] = a.aux[t];
+          s_a[t] = a.aux[a.aux_stride + t];
+          s_y[t] = a.aux[2 * a.aux_stride + t];
         }
         __syncthreads();
         if (lead) WS_STAMP(3);
@@ -158,9 +210,9 @@ __global__ __launch_bounds__(kWpThreads, 1) void ws_persist_kernel(WsArgs a, int
       // of this XCD's L2 before the round count moves
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(sync + 1, gen0 + r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(sync + 1, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      if (tid == 0) s_word[1] = wp_wait(sync + 1, gen0 + r + 1, a.xtimeout_ticks) ? 1 : 0;
+      if (tid == 0) s_word[1] = wp_wait(sync + 1, gen + 1, a.xtimeout_ticks) ? 1 : 0;
       __syncthreads();
       if (!s_word[1]) {
         if (tid == 0) wp_fail(a, c);
@@ -185,7 +237,7 @@ __global__ __launch_bounds__(kWpThreads, 1) void ws_persist_kernel(WsArgs a, int
       // list order, combined in partition order (ws_select.hip)
       const int per = (na + 3) / 4;
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      constexpr int CH = 12;  // x 4 partitions: 48 Gram loads in flight per thread
+      constexpr int CH = 15;  // x 4 partitions: 60 Gram loads in flight per thread (vmcnt <= 63)
       for (int s0 = 0; s0 < per; s0 += CH) {
         float kv[4][CH];
 #pragma unroll

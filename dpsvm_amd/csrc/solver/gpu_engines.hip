@@ -368,7 +368,7 @@ struct WsRounds : Base {
     launch::ws_select(m.wsa, m.stream);
     ws_allgather_cand(m);
     if (m.ws_persist) {  // persistent rounds (ws_persist.hip): no graph; arrivals == G x released rounds
-      HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 16, m.stream));
+      HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 32, m.stream));
       return;
     }
     if (ws_graphs(m) && !m.gexec) capture_rounds(m, this->block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });

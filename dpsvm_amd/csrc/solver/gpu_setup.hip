@@ -216,10 +216,14 @@ int max_device_sharing(GpuSolver::Impl& m) {
 }
 
 // Persistent small-problem rounds (ws_persist.hip): ws-dense at one rank with
-// one block per round — auto up to kWsPersistAutoGroups selection groups (the
-// rounds of a small active set are launch- and merge-bound, a large set's are
-// f-update-bound).  Its grid spins on its own workgroups, so a census of the
-// kernel's own grid and resources comes first; a failed census keeps the graph.
+// one block per round, on request (ws_persist = 1; auto keeps the graph: on the
+// covtype-shape 7.5k-row sub-problem a persistent round measured 88.3 us vs
+// 73.2 us for the graph of launches — an agent-scope signal costs what a
+// launch gap in a graph does, and a 256-thread workgroup per CU has a quarter
+// of the memory parallelism of the launches' 1024-thread workgroups for the
+// f update and the sub-Gram load; profiles/r5_ws_persist_ab.txt).  Its grid
+// spins on its own workgroups, so a census of the kernel's own grid and
+// resources comes first; a failed census keeps the graph.
 void ws_persist_setup(GpuSolver::Impl& m) {
   WsArgs& w = m.wsa;
   m.ws_persist = false;
@@ -228,8 +232,9 @@ void ws_persist_setup(GpuSolver::Impl& m) {
   int mode = m.p.ws_persist;  // 0 auto, 1 on, 2 off
   if (const char* e = std::getenv("DPSVM_WS_PERSIST")) mode = std::atoi(e);  // A/B runs
   if (mode == 2 || m.kind != EngineKind::WsDense || m.world != 1 || w.blocks != 1 || w.off != 0) return;
-  if (mode == 0 && w.G > kWsPersistAutoGroups) return;
-  if (!m.wspsync) m.wspsync = dmalloc<int32_t>(4, &m.bytes);
+  if (mode == 0) return;  // auto: the graph (measured faster, see above)
+  if (w.G > kWsMaxGroups) return;
+  if (!m.wspsync) m.wspsync = dmalloc<int32_t>(8, &m.bytes);
   w.psync = m.wspsync;
   if (!launch::ws_persist_supported(w)) {
     w.psync = nullptr;
@@ -241,14 +246,14 @@ void ws_persist_setup(GpuSolver::Impl& m) {
   bool ok = per_cu >= 1 && w.G <= cus;
   int32_t h[4] = {0, 0, 0, 0};
   if (ok) {
-    HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 16, m.stream));
+    HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 32, m.stream));
     w.xtimeout_ticks = (int64_t)(2.0 * 1e8);  // census: 2 s
     launch::ws_persist_census(w, m.stream);
     HIP_CHECK(hipMemcpyAsync(h, m.wspsync, 16, hipMemcpyDeviceToHost, m.stream));
     HIP_CHECK(hipStreamSynchronize(m.stream));
     ok = h[3] == 0 && h[2] == w.G;
   }
-  HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 16, m.stream));
+  HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 32, m.stream));
   if (!ok) {
     m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") + "ws persistent rounds: census " +
                           std::to_string(h[2]) + "/" + std::to_string(w.G) + " workgroups co-resident (" +

@@ -120,8 +120,8 @@ class SVCConfig:
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
     ws_block: int = 8               # rounds per hipGraph block (or per persistent-round launch)
-    # persistent small-problem rounds (one launch per ws_block rounds, ws_persist.hip): auto (one GPU, one
-    # block, resident Gram, <= 16,384 rows) | on (wherever supported) | off (a graph of launches per round)
+    # persistent one-block rounds (one launch per ws_block rounds, ws_persist.hip; one GPU, resident Gram):
+    # on | auto / off (a graph of launches per round: measured faster, profiles/r5_ws_persist_ab.txt)
     ws_persist: str = "auto"
     # one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking: phases on the rows that can
     # still violate, the rest of the gradient updated by one predict GEMM per phase).  auto: on where it

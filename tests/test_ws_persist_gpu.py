@@ -57,16 +57,16 @@ def test_persistent_rounds_bit_identical_to_graph_rounds(case):
         assert per.n_iter_ == 1234 and not per.converged_
 
 
-def test_persistent_rounds_auto_threshold_and_off():
-    """auto: persistent up to 64 selection groups (16,384 rows); larger
-    problems and ws_persist="off" keep the graph of launches"""
+def test_persistent_rounds_opt_in_and_multi_block_refusal():
+    """auto keeps the graph of launches (measured faster on MI355X,
+    profiles/r5_ws_persist_ab.txt); "on" takes the persistent rounds where
+    supported — one block per round: a multi-block engine keeps its graph"""
     X, y = synthetic("adult", n=2000, seed=9)
     kw = dict(C=1.0, gamma=0.05, eps=1e-3, device="cuda", solver="ws")
-    assert SVC(**kw).fit(X, y).setup_info_["ws_rounds"] == "persistent"
-    assert SVC(ws_persist="off", **kw).fit(X, y).setup_info_["ws_rounds"] == "graph"
-    Xb, yb = synthetic("adult", n=17000, seed=9)
-    big = SVC(ws_blocks=1, **kw).fit(Xb, yb)
-    assert big.setup_info_["ws_rounds"] == "graph" and big.converged_
+    assert SVC(**kw).fit(X, y).setup_info_["ws_rounds"] == "graph"
+    assert SVC(ws_persist="on", **kw).fit(X, y).setup_info_["ws_rounds"] == "persistent"
+    mb = SVC(ws_persist="on", ws_blocks=4, ws_size=96, **kw).fit(X, y)
+    assert mb.setup_info_["ws_rounds"] == "graph" and mb.converged_
 
 
 def test_persistent_rounds_repeated_solves_and_resume(tmp_path):
