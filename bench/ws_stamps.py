@@ -117,6 +117,10 @@ def main() -> int:
         "solve_end_to_next_select_us": us(nxt - s[:, 4]),
         "round_period_us": us(np.diff(s[:, 6])),
     }
+    if clf.setup_info_.get("ws_rows") == "recompute":  # ws_recompute.hip: select = the fused pass (6 -> 7)
+        res["ws_rows"] = "recompute"
+        for k in ("select_fupdate_us", "select_candidates_us"):
+            res.pop(k, None)
     if (s[:, 15] > 0).all():  # multi-block peer exchange: the two collect kernels (workgroup 0)
         res["exchange"] = clf.setup_info_.get("exchange")
         res["peer_phases_us"] = {

@@ -59,6 +59,7 @@ LIB_SOURCES = [
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
     "kernels/ws_persist.hip",
+    "kernels/ws_recompute.hip",
 ]
 # the quarantined engines (solver/gpu_engines_pairq.hip registers them): a plugin
 # library for the Python module, linked into the CLIs (svmTrain --engines all)

@@ -135,6 +135,8 @@ struct SolverParams {
                               // 0 auto: second order when a row sample's mean off-diagonal K > 0.1
   int ws_persist = 0;         // persistent one-block rounds (ws_persist.hip: one rank, resident Gram): 1 on where
                               // supported; 0 auto and 2 off keep the graph of launches (measured faster)
+  int ws_recompute = 0;       // ws-cache rounds without the row cache (ws_recompute.hip: kernel rows recomputed,
+                              // fused into the f update): 0 auto (one rank, one block, d <= 64 padded), 1 on, 2 off
   int ws_block = 8;           // rounds per hipGraph block (the host stops at most ~2 blocks past convergence;
                               // the one-block switch stays on 32-round boundaries: same trajectories)
   float ws_t_halve = 0.9f;    // multi-block: a round damped below this line-search factor halves the block count

@@ -80,6 +80,7 @@ struct GpuSetupInfo {
   std::string engine_note;            // why the engine was chosen / refused (fallbacks)
   int ws_wss = 0;                     // working-set engines: sub-problem pair choice (1 first, 2 second order)
   std::string ws_rounds = "none";     // working-set engines: "graph" (launches per round) or "persistent"
+  std::string ws_rows = "none";       // ws engines' kernel rows: "gram" (resident), "cache" (row cache), "recompute"
   std::string gram = "f32";           // Gram / kernel-row GEMM arithmetic: "f32" or "split-f16" (rbf_gemm_split.hip)
 };
 

@@ -157,6 +157,7 @@ py::dict setup_dict(const GpuSetupInfo& i) {
   d["engine_note"] = i.engine_note;
   d["ws_wss"] = i.ws_wss;
   d["ws_rounds"] = i.ws_rounds;
+  d["ws_rows"] = i.ws_rows;
   d["gram"] = i.gram;
   return d;
 }
@@ -232,6 +233,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_clip_fallback", &SolverParams::ws_clip_fallback)
       .def_readwrite("ws_block", &SolverParams::ws_block)
       .def_readwrite("ws_persist", &SolverParams::ws_persist)
+      .def_readwrite("ws_recompute", &SolverParams::ws_recompute)
       .def_readwrite("gram_precision", &SolverParams::gram_precision)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
       .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });

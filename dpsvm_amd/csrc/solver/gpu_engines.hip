@@ -334,6 +334,15 @@ struct WsRounds : Base {
     }
   }
   static void round(GpuSolver::Impl& m, const WsArgs& w) {
+    if (kCache && m.ws_recompute) {
+      // no row cache: merge + sub-Gram from the split X rows, the solve, then
+      // the selection pass with the changed rows' kernel rows recomputed inside
+      // the f update (ws_recompute.hip)
+      launch::ws_subgram_split(w, m.xs, m.xsh, m.xsq, m.dp, m.gamma, m.stream);
+      launch::ws_solve(w, m.stream);
+      launch::ws_fupdate_split(w, m.xs, m.xsh, m.xsq, m.dp, m.gamma, m.stream);
+      return;
+    }
     // peer exchange: the candidate lists every rank pushed at the end of the
     // previous round (or the seed), collected in-kernel by a few workgroups (the
     // merge then reads them as from the all-gather and never spins)

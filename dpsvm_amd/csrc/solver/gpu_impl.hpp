@@ -138,6 +138,8 @@ struct GpuSolver::Impl {
   // persistent small-problem rounds (ws_persist.hip): on after a passed census
   bool ws_persist = false;
   int32_t* wspsync = nullptr;
+  // ws-cache rounds with the kernel rows recomputed (ws_recompute.hip)
+  bool ws_recompute = false;
 
   ~Impl();
 

@@ -267,6 +267,22 @@ void ws_persist_setup(GpuSolver::Impl& m) {
   m.info.ws_rounds = "persistent";
 }
 
+// ws-cache without the cache (ws_recompute.hip): with short rows (d <= 64
+// padded) a round's kernel rows are cheaper to recompute inside the f update
+// than to write into cache lines and read back (covtype-shape 581k rows:
+// profiles/r5_ws_recompute_ab.txt).  One rank, one block per round.
+void ws_recompute_setup(GpuSolver::Impl& m) {
+  WsArgs& w = m.wsa;
+  m.ws_recompute = false;
+  m.info.ws_rows = m.kind == EngineKind::WsDense ? "gram" : "cache";
+  if (m.kind != EngineKind::WsCache) return;
+  int mode = m.p.ws_recompute;  // 0 auto, 1 on, 2 off
+  if (const char* e = std::getenv("DPSVM_WS_RECOMPUTE")) mode = std::atoi(e);  // A/B runs
+  if (mode == 2 || !m.gram_split || !launch::ws_recompute_supported(w, m.dp)) return;
+  m.ws_recompute = true;
+  m.info.ws_rows = "recompute";
+}
+
 }  // namespace
 
 GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int d, const float* yh) {
@@ -882,6 +898,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       HIP_CHECK(hipStreamSynchronize(m.stream));
     }
     ws_persist_setup(m);
+    ws_recompute_setup(m);
   }
   m.engine = gpu::make_engine(m.kind);
   m.info.iteration = engine_name(m.kind);

@@ -123,6 +123,9 @@ class SVCConfig:
     # persistent one-block rounds (one launch per ws_block rounds, ws_persist.hip; one GPU, resident Gram):
     # on | auto / off (a graph of launches per round: measured faster, profiles/r5_ws_persist_ab.txt)
     ws_persist: str = "auto"
+    # ws-cache rounds without the kernel-row cache (ws_recompute.hip: the round's kernel rows recomputed inside
+    # the f update, the sub-Gram straight from X): auto (one GPU, one block, d <= 64) | on | off
+    ws_recompute: str = "auto"
     # one GPU: LIBSVM-style shrinking as problem reduction (solve_shrinking: phases on the rows that can
     # still violate, the rest of the gradient updated by one predict GEMM per phase).  auto: on where it
     # pays — one GPU, working-set rounds, the whole Gram not resident (C.shrink_auto) | on | off
@@ -207,6 +210,7 @@ class SVCConfig:
         p.ws_clip_fallback = int(bool(self.ws_clip_fallback))
         p.ws_block = int(self.ws_block)
         p.ws_persist = _pick({"auto": 0, "on": 1, "off": 2}, self.ws_persist, "ws_persist")
+        p.ws_recompute = _pick({"auto": 0, "on": 1, "off": 2}, self.ws_recompute, "ws_recompute")
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         p.gram_precision = _pick({"auto": 0, "f32": 1, "split": 2}, self.gram, "gram")
         return p

@@ -26,6 +26,7 @@ SPILL_FREE = [
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
     "kernels/ws_persist.hip",
+    "kernels/ws_recompute.hip",
     "kernels/smo_persist.hip",
     "kernels/compact.hip",
 ]

@@ -119,9 +119,10 @@ def test_ws_cache_engine_bit_identical_to_resident_gram(case):
     X, y = synthetic(name, n=n, seed=5)
     kw = dict(C=C_, gamma=g, eps=1e-3, device="cuda", solver="ws")
     dense = SVC(**kw).fit(X, y)
-    cache = SVC(force_cache=True, cache_lines=lines, **kw).fit(X, y)
+    cache = SVC(force_cache=True, cache_lines=lines, ws_recompute="off", **kw).fit(X, y)
     assert dense.setup_info_["iteration"] == "ws-dense"
     assert cache.setup_info_["iteration"] == "ws-cache" and cache.setup_info_["cache_lines"] == lines
+    assert cache.setup_info_["ws_rows"] == "cache"
     assert cache.converged_ and cache.n_iter_ == dense.n_iter_ and cache.n_rounds_ == dense.n_rounds_
     assert np.array_equal(cache.alpha_, dense.alpha_) and cache.b_ == dense.b_
     assert cache.stats_["rows_computed"] > lines  # more rows than lines: evictions happened
