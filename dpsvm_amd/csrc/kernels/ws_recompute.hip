@@ -314,8 +314,11 @@ __global__ __launch_bounds__(kFupdThreads) void ws_fupdate_split_kernel(WsArgs a
 
 namespace launch {
 
+// (one-block rounds only: a multi-block ws-cache engine runs its multi-block
+// rounds on the row cache and its one-block rounds — after the adaptive count
+// reached 1 — without it)
 bool ws_recompute_supported(const WsArgs& a, int dp) {
-  return dp <= 64 && a.world == 1 && a.blocks == 1 && a.xpeer == nullptr && a.off == 0 && a.q_max <= kWsMax;
+  return dp <= 64 && a.world == 1 && a.xpeer == nullptr && a.off == 0 && a.q_max <= kWsMax;
 }
 
 void ws_subgram_split(const WsArgs& a, const void* xs, const int32_t* xsh, const float* xsq, int dp, float gamma,

@@ -334,7 +334,7 @@ struct WsRounds : Base {
     }
   }
   static void round(GpuSolver::Impl& m, const WsArgs& w) {
-    if (kCache && m.ws_recompute) {
+    if (kCache && m.ws_recompute && w.blocks == 1) {
       // no row cache: merge + sub-Gram from the split X rows, the solve, then
       // the selection pass with the changed rows' kernel rows recomputed inside
       // the f update (ws_recompute.hip)

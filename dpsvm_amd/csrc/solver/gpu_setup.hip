@@ -270,7 +270,8 @@ void ws_persist_setup(GpuSolver::Impl& m) {
 // ws-cache without the cache (ws_recompute.hip): with short rows (d <= 64
 // padded) a round's kernel rows are cheaper to recompute inside the f update
 // than to write into cache lines and read back (covtype-shape 581k rows:
-// profiles/r5_ws_recompute_ab.txt).  One rank, one block per round.
+// profiles/r5_ws_recompute_ab.txt).  One rank; the one-block rounds (a
+// multi-block engine's multi-block rounds keep the cache).
 void ws_recompute_setup(GpuSolver::Impl& m) {
   WsArgs& w = m.wsa;
   m.ws_recompute = false;

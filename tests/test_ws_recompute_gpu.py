@@ -75,3 +75,21 @@ def test_recompute_checkpoint_resume(tmp_path):
     assert not part.converged_
     res = SVC(**kw).fit(X, y, resume=ck)
     assert res.converged_ and abs(res.b_ - full.b_) < 1e-2 * max(1.0, abs(full.b_))
+
+
+def test_recompute_after_the_multi_block_switch():
+    """A multi-block ws-cache engine runs its multi-block rounds on the row
+    cache and, once the adaptive block count reached 1 (coupled covtype rows),
+    its one-block rounds without it — and still stops at the resident-Gram
+    optimum"""
+    X, y = synthetic("covtype", n=14000, d=54, seed=4)
+    base = dict(C=64.0, gamma=0.5, eps=1e-3, clip="box", device="cuda", solver="ws", ws_blocks=4, ws_size=96)
+    dense = SVC(**base).fit(X, y)
+    rec = SVC(force_cache=True, cache_lines=10000, **base).fit(X, y)  # >= 2 P q + 8192: multi-block ws-cache
+    assert rec.setup_info_["iteration"] == "ws-cache" and rec.setup_info_["ws_rows"] == "recompute"
+    print(f"blocks {rec.stats_.get('ws_blocks')} -> {rec.stats_.get('ws_blocks_end')}, rounds {rec.n_rounds_} vs "
+          f"{dense.n_rounds_}, b {rec.b_:.6f} vs {dense.b_:.6f}")
+    assert rec.stats_.get("ws_blocks") == 4 and rec.stats_.get("ws_blocks_end") == 1
+    assert rec.converged_
+    agree = float(np.mean(np.sign(rec.decision_function(X)) == np.sign(dense.decision_function(X))))
+    assert agree > 0.995 and abs(rec.b_ - dense.b_) < 1e-2 * max(1.0, abs(dense.b_))
