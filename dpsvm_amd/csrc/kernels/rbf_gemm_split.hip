@@ -817,8 +817,6 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 constexpr int kW64Threads = 512;
 // NT 1: non-temporal Gram stores (measured slower, profiles/r4_gram_nt_store_ab.txt);
 // NT 2: diagnostics only — stores skipped unless a value is NaN (the store-free time)
-// NT 3: diagnostics only — P and Q summed in one accumulator set (128 instead of
-// 192 accumulators; not bit-identical to the other split kernels)
 // tiles: nullptr = the whole tm x tn grid in the XCD order; else a compact
 // table of the tiles to compute (the symmetric Gram's upper tiles, host-built
 // in the XCD order: no workgroup is launched only to exit)
@@ -916,17 +914,10 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
       P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
       const h8 al0 = __builtin_bit_cast(h8, buf[ra0 + cl]);
       const h8 al1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + cl]);
-      if constexpr (NT == 3) {  // diagnostics: lo x hi into the hi x lo accumulators (128 accumulators, not bit-identical)
-        P[0][0] = mfma32_f16(al0, bh0, P[0][0]);
-        P[0][1] = mfma32_f16(al0, bh1, P[0][1]);
-        P[1][0] = mfma32_f16(al1, bh0, P[1][0]);
-        P[1][1] = mfma32_f16(al1, bh1, P[1][1]);
-      } else {
-        Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
-        Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
-        Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
-        Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
-      }
+      Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
     }
   }
 
@@ -960,8 +951,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e, lr = lr0 + 8 * g + e;
-          const float pq = NT == 3 ? P[i][j][r] : P[i][j][r] + Q[i][j][r];
-          const float dot = ldexpf(H[i][j][r] + pq, -(ash[e] + bsh));
+          const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(ash[e] + bsh));
           H[i][j][r] = rbf_from_dot(asq[e], bsq, dot, gamma);
           if (NT == 2 && !(H[i][j][r] != H[i][j][r])) continue;
           if (okc && lr < rlim) {
@@ -1498,8 +1488,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       return e ? atoi(e) : 0;
     }();
     const int64_t tm2 = (M + 255) / 256;
-    auto kern = nt == 3 ? dev::rbf_gemm_split_w64_kernel<3>
-                : nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
+    auto kern = nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
                 : nt ? dev::rbf_gemm_split_w64_kernel<1> : dev::rbf_gemm_split_w64_kernel<0>;
     static const bool compact = [] {  // A/B: DPSVM_GRAM_COMPACT=0 launches the full grid (half exit at once)
       const char* e = std::getenv("DPSVM_GRAM_COMPACT");
