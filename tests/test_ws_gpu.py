@@ -393,6 +393,8 @@ def test_ws_multi_block_peer_exchange_loopback_bit_identical(clip, extra):
                 else synthetic("blobs", n=n, d=12, seed=41, sep=1.2))
         kw = dict(C=10.0 if case == "mnist" else 2.0, gamma=0.25 if case == "mnist" else 0.15, eps=1e-3,
                   clip=clip, device="cuda", solver="ws", ws_blocks=4, xch_timeout_s=30.0, **extra)
+        if extra:  # the row cache on both sides (recompute rounds are a world-1, no-exchange mode)
+            kw["ws_recompute"] = "off"
         ref = SVC(**kw).fit(X, y)
         got = SVC(exchange="peer", **kw).fit(X, y)
         assert got.setup_info_["exchange"] == "loopback" and ref.setup_info_["exchange"] == "none"
