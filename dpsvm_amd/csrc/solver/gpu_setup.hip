@@ -176,6 +176,7 @@ bool distinct_devices(GpuSolver::Impl& m) {
 // to 96 rows (fixed stride, float64): how strongly the rows of a working set
 // couple — ~0 when K ~ I (MNIST-shape at gamma 0.25), ~0.85 for covtype-shape
 constexpr double kWsW2Coupling = 0.1;
+constexpr double kWsUncoupled = 1e-4;  // below: the blocks of a round are independent (64 blocks of 48 rows)
 double mean_offdiag_kernel(const float* xh, int64_t rows, int d, float gamma) {
   const int64_t s = std::min<int64_t>(96, rows);
   if (s < 2) return 0.0;
@@ -627,11 +628,22 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // more workgroups; headline 0.0308 vs 0.0371 s at 8 x 192,
   // profiles/r3_union3072_ab.txt), never larger than ws_size; the one-block
   // rounds the adaptive count falls back to keep ws_size rows
-  static const int auto_blocks = [] {  // A/B: DPSVM_WS_AUTO_BLOCKS (2 .. kWsMaxBlocks)
+  static const int auto_blocks_env = [] {  // A/B: DPSVM_WS_AUTO_BLOCKS (2 .. kWsMaxBlocks)
     const char* e = std::getenv("DPSVM_WS_AUTO_BLOCKS");
     const int v = e ? atoi(e) : 0;
-    return v >= 2 && v <= kWsMaxBlocks ? v : kWsAutoBlocks;
+    return v >= 2 && v <= kWsMaxBlocks ? v : 0;
   }();
+  // the coupling of a row sample (mean off-diagonal K, host, outside the timed
+  // region; read by the auto choices below and by the pair choice): where the
+  // kernel is numerically diagonal at working-set scale (MNIST-shape at gamma
+  // 0.25: 1.7e-9; the structured mnist-parity: 4.3e-3; covtype-shape 0.85) the
+  // blocks of a round do not interact, so kWsMaxBlocks blocks of 48 rows (one
+  // row per solve lane: cheaper pair steps) beat 32 of 96 (headline
+  // 0.0238-0.0240 vs 0.0241-0.0242 s); coupled data keeps 32 (mnist-parity
+  // 0.0206 s with 32, 0.0422 s with 64: damped rounds; profiles/r5_blocks_64_vs_32_ab.txt)
+  const double coupling = (ws_cand || wsc_cand) ? mean_offdiag_kernel(xh, n_x_rows, d, m.gamma) : 1.0;
+  const bool uncoupled = m.all_agree(coupling < kWsUncoupled, m.comm, m.world);
+  const int auto_blocks = auto_blocks_env > 0 ? auto_blocks_env : uncoupled ? kWsMaxBlocks : kWsAutoBlocks;
   const int auto_q = std::min(ws_q, kWsMaxAll / auto_blocks) & ~1;
   const bool blocks_auto = m.p.ws_blocks == 0;
   const int want_blocks = !blocks_auto ? m.p.ws_blocks
@@ -801,8 +813,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       // a row sample: covtype-shape 0.85, synthetic-2m 0.85 -> WSS2 converges
       // covtype-200k in 21.2 s vs 27.7 s; MNIST-shape 0.0000, adult 0.0002 ->
       // WSS2 only adds ~0.25 us per pair step; profiles/r3_wss2_*.txt)
-      const double k = mean_offdiag_kernel(xh, n_x_rows, d, m.gamma);
-      w.wss = m.all_agree(k > kWsW2Coupling, m.comm, m.world) ? 2 : 1;
+      w.wss = m.all_agree(coupling > kWsW2Coupling, m.comm, m.world) ? 2 : 1;
     }
     m.info.ws_wss = w.wss;
     DPSVM_CHECK(m.p.ws_t_halve >= 0.f && m.p.ws_t_halve <= 1.f, "ws_t_halve must be in [0, 1]");
