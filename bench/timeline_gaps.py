@@ -33,6 +33,15 @@ def main(root):
               f"gaps {tot_gap / 1e6:.3f} ms")
         for g in gaps[:6]:
             print(f"   gap {g[0] / 1e3:8.1f} us  {g[1]} -> {g[2]}")
+    # per-kernel totals of the last solve
+    agg = {}
+    for r in solves[-1]:
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dpsvm::dev::", "")
+        c, t = agg.get(k, (0, 0))
+        agg[k] = (c + 1, t + int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    print("last solve, per kernel:")
+    for k, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
+        print(f"   {k[:52]:52s} {c:4d} x  {t / 1e6:7.3f} ms  ({t / 1e3 / c:8.1f} us each)")
 
 
 if __name__ == "__main__":
