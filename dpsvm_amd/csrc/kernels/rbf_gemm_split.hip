@@ -298,7 +298,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void rbf_gemm_split_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(ash_r[r] + bsh));
-      H[j][r] = rbf_from_dot(asq_r[r], bsq, dot, gamma);
+      H[j][r] = rbf_split_value(asq_r[r], bsq, dot, gamma);
     }
   }
   const bool interior = m0 + TM <= M && n0 + TN <= N;
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
     for (int r = 0; r < 16; ++r) {
       const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
       const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_sh[lr] + bsh));
-      H[j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
+      H[j][r] = rbf_split_value(s_sq[lr], bsq, dot, gamma);
     }
   }
   const bool interior = m0 + TM <= M && n0 + TN <= N;
@@ -637,7 +637,7 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
     for (int r = 0; r < 16; ++r) {
       const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
       const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
-      H[j][r] = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+      H[j][r] = rbf_split_value(s_asq[lr], bsq, dot, gamma);
     }
   }
   const bool interior = n0 + TN <= N;
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
       for (int r = 0; r < 16; ++r) {
         const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
         const float dot = ldexpf(H[r] + (P[r] + Q[r]), -(s_ash[lr] + bsh));
-        const float v = rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+        const float v = rbf_split_value(s_asq[lr], bsq, dot, gamma);
         const int32_t orow = s_orow[lr];
         // exactly 16 stores per lane (the vmcnt(16) above): rows past M and
         // columns past N go to the scratch line
@@ -952,7 +952,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e, lr = lr0 + 8 * g + e;
           const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(ash[e] + bsh));
-          H[i][j][r] = rbf_from_dot(asq[e], bsq, dot, gamma);
+          H[i][j][r] = rbf_split_value(asq[e], bsq, dot, gamma);
           if (NT == 2 && !(H[i][j][r] != H[i][j][r])) continue;
           if (okc && lr < rlim) {
             float* dst = ob + ((uint32_t)lr * ld + (uint32_t)cl);
@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_persist_k
       for (int r = 0; r < 16; ++r) {
         const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
         const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_sh[lr] + bsh));
-        H[j][r] = rbf_from_dot(s_sq[lr], bsq, dot, gamma);
+        H[j][r] = rbf_split_value(s_sq[lr], bsq, dot, gamma);
       }
     }
     if (has_next && tid < ROWS) {
@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_predict_split_kernel(
         for (int r = 0; r < 16; ++r) {
           const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
           const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
-          acc[r] += cf * rbf_from_dot(s_asq[lr], bsq, dot, gamma);
+          acc[r] += cf * rbf_split_value(s_asq[lr], bsq, dot, gamma);
           H[j][r] = P[j][r] = Q[j][r] = 0.f;
         }
       }

@@ -15,6 +15,18 @@ namespace dev {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 
+// K from a split GEMM's dot product — the epilogue of EVERY split kernel (the
+// Gram, its indexed rows, the predictions, the recompute rounds), so they all
+// agree bit for bit: the clamped |x|^2 expansion as rbf_from_dot, then exp on
+// the hardware v_exp_f32 (__expf: a multiply by log2 e and one transcendental)
+// instead of libm expf's ~10-instruction range reduction (~1 ulp apart)
+__device__ __forceinline__ float rbf_split_value(float sq_a, float sq_b, float dot, float gamma) {
+#pragma clang fp contract(off)
+  float d2 = sq_a + sq_b - 2.0f * dot;
+  d2 = d2 > 0.f ? d2 : 0.f;
+  return __expf(-gamma * d2);
+}
+
 __device__ __forceinline__ f16v mfma32_f16(h8 a, h8 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }

@@ -19,12 +19,11 @@
 //
 // The cache path of the same round (ws_merge line assignment, the miss-row GEMM
 // writing ~44 rows x 581k columns, the f update re-reading ~58 cached rows)
-// moves ~250 MB per covtype round; this one streams X once (~150 MB).  The dot
-// products are the split GEMMs' bits (same MFMA order); K takes the hardware
-// exp (~1 ulp from libm's expf: the epilogue's ~10 instructions of expf were
-// a fifth of the pass), and the f update sums per column over the rows instead
-// of per row over the list, so the trajectory matches the cache path to
-// rounding, not bit for bit.
+// moves ~250 MB per covtype round; this one streams X once (~150 MB).  The K
+// values are the split GEMMs' bits (same MFMA order, the same epilogue:
+// rbf_split_value); the f update sums them per column over the rows instead of
+// per row over the list, so the trajectory matches the cache path to rounding,
+// not bit for bit.
 // Reference: svmTrain.cu:98-137 (the f update), svmTrain.cu:212-249 (kernel rows).
 #include <hip/hip_runtime.h>
 
@@ -40,25 +39,10 @@
 namespace dpsvm {
 namespace dev {
 
-// K from the dot product: the Gram kernels' epilogue (rbf_from_dot: libm expf,
-// the same bits as the resident Gram), or (FAST) the hardware exp (__expf:
-// v_exp_f32 on a pre-scaled argument, 2 instructions instead of ~10; ~1 ulp)
-template <bool FAST>
-__device__ __forceinline__ float rc_kernel_value(float sq_a, float sq_b, float dot, float gamma) {
-  if constexpr (!FAST) {
-    return rbf_from_dot(sq_a, sq_b, dot, gamma);
-  } else {
-#pragma clang fp contract(off)
-    float d2 = sq_a + sq_b - 2.0f * dot;
-    d2 = d2 > 0.f ? d2 : 0.f;
-    return __expf(-gamma * d2);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // merge + one 64 x 64 tile of the sub-Gram (4 waves of 32 x 32)
 // ---------------------------------------------------------------------------
-template <int NKB, bool FAST>
+template <int NKB>
 __global__ __launch_bounds__(kWsGatherThreads) void ws_subgram_split_kernel(WsArgs a, const u4* __restrict__ xs,
                                                                             const int32_t* __restrict__ xsh,
                                                                             const float* __restrict__ xsq,
@@ -133,7 +117,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_subgram_split_kernel(WsAr
     const int lr_t = wr + (r & 3) + 8 * (r >> 2) + 4 * hl;  // the value's row inside the tile
     const int row = tx * 64 + lr_t;
     const float dot = ldexpf(H[r] + (P[r] + Q[r]), -(s_sh[0][lr_t] + bsh));
-    const float v = rc_kernel_value<FAST>(s_sq[0][lr_t], bsq, dot, gamma);
+    const float v = rbf_split_value(s_sq[0][lr_t], bsq, dot, gamma);
     if (row < q && col < a.q_max) a.subg[(int64_t)row * a.q_max + col] = col < q ? v : 0.f;
   }
   if (lead) WS_STAMP(8);
@@ -164,7 +148,7 @@ __device__ __forceinline__ void top4_insert(uint64_t (&l)[kWsCand1], uint64_t k)
   }
 }
 
-template <int NKB, bool FAST>
+template <int NKB>
 __global__ __launch_bounds__(kFupdThreads) void ws_fupdate_split_kernel(WsArgs a, const u4* __restrict__ xs,
                                                                         const int32_t* __restrict__ xsh,
                                                                         const float* __restrict__ xsq, float gamma) {
@@ -248,7 +232,7 @@ __global__ __launch_bounds__(kFupdThreads) void ws_fupdate_split_kernel(WsArgs a
       for (int r = 0; r < 16; ++r) {
         const int lr = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
         const float dot = ldexpf(H[r] + (P[r] + Q[r]), -(s_ash[lr] + o.sh));
-        const float v = rc_kernel_value<FAST>(s_asq[lr], o.sq, dot, gamma);
+        const float v = rbf_split_value(s_asq[lr], o.sq, dot, gamma);
         {
 #pragma clang fp contract(off)
           acc = acc + s_coef[lr] * v;
@@ -331,18 +315,6 @@ __global__ __launch_bounds__(kFupdThreads) void ws_fupdate_split_kernel(WsArgs a
 
 namespace launch {
 
-// the hardware exp in both recompute kernels (default: the fused selection pass
-// 46.5 -> 36.6 us a covtype round, covtype box 38.19 -> 37.34 s;
-// profiles/r5_ws_recompute_ab.txt); A/B: DPSVM_RECOMPUTE_EXP=libm keeps the
-// Gram kernels' expf (their bits)
-static bool rc_fast_exp() {
-  static const bool v = [] {
-    const char* e = std::getenv("DPSVM_RECOMPUTE_EXP");
-    return !(e && std::string(e) == "libm");
-  }();
-  return v;
-}
-
 // (one-block rounds only: a multi-block ws-cache engine runs its multi-block
 // rounds on the row cache and its one-block rounds — after the adaptive count
 // reached 1 — without it)
@@ -354,8 +326,7 @@ void ws_subgram_split(const WsArgs& a, const void* xs, const int32_t* xsh, const
                       hipStream_t s) {
   const int tn = (a.q_max + 63) / 64;
   const dim3 grid((unsigned)(tn * tn));
-  auto fn = (dp + 31) / 32 <= 1 ? (rc_fast_exp() ? dev::ws_subgram_split_kernel<1, true> : dev::ws_subgram_split_kernel<1, false>)
-                                : (rc_fast_exp() ? dev::ws_subgram_split_kernel<2, true> : dev::ws_subgram_split_kernel<2, false>);
+  auto fn = (dp + 31) / 32 <= 1 ? dev::ws_subgram_split_kernel<1> : dev::ws_subgram_split_kernel<2>;
   fn<<<grid, dev::kWsGatherThreads, 0, s>>>(a, (const dev::u4*)xs, xsh, xsq, gamma);
   post_launch("ws_subgram_split", s);
 }
@@ -372,8 +343,7 @@ void ws_fupdate_split(const WsArgs& a, const void* xs, const int32_t* xsh, const
   // group's 8 waves walk its 32-column blocks
   (void)cus;
   const int64_t grid = a.G;
-  auto fn = (dp + 31) / 32 <= 1 ? (rc_fast_exp() ? dev::ws_fupdate_split_kernel<1, true> : dev::ws_fupdate_split_kernel<1, false>)
-                                : (rc_fast_exp() ? dev::ws_fupdate_split_kernel<2, true> : dev::ws_fupdate_split_kernel<2, false>);
+  auto fn = (dp + 31) / 32 <= 1 ? dev::ws_fupdate_split_kernel<1> : dev::ws_fupdate_split_kernel<2>;
   fn<<<dim3((unsigned)grid), dev::kFupdThreads, 0, s>>>(a, (const dev::u4*)xs, xsh, xsq, gamma);
   post_launch("ws_fupdate_split", s);
 }
