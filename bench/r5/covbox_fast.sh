@@ -1,3 +1,4 @@
+# (historical: the A/B switch / code this script exercised was removed after its measurement; see profiles/)
 # covtype box end to end with the hardware exp in the recompute rounds
 set -o pipefail
 mkdir -p gpurun_out

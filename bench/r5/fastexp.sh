@@ -1,3 +1,4 @@
+# (historical: the A/B switch / code this script exercised was removed after its measurement; see profiles/)
 # recompute rounds: libm expf (the Gram's bits) vs the hardware exp, covtype 581k x 54 one block, 1M pair steps
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,3 +1,4 @@
+# (historical: the A/B switch / code this script exercised was removed after its measurement; see profiles/)
 # split Gram epilogue: hardware exp (default) vs libm expf (DPSVM_GRAM_NT=4), then the headline
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,3 +1,4 @@
+# (historical: the A/B switch / code this script exercised was removed after its measurement; see profiles/)
 # progressive Gram: equivalence test, then headline / mnist-parity A/B (DPSVM_GRAM_OVERLAP=0: Gram first)
 set -o pipefail
 mkdir -p gpurun_out
