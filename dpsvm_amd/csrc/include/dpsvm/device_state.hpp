@@ -278,7 +278,8 @@ constexpr int kXchGranules = 4;  // per workgroup entry: per side {key bits 63..
 // candidates.  ~10^5 dependent pair steps then cost an LDS round trip each
 // instead of a grid-wide exchange.
 constexpr int kWsMax = 192;          // working-set capacity: q x q fp32 sub-Gram in LDS (147 KiB)
-constexpr int kWsCand = 8;           // candidates per side per selection workgroup (list capacity)
+constexpr int kWsCand = 16;          // candidates per side per selection workgroup (list capacity)
+constexpr int kWsCandStd = 8;        // ... written by rounds of unions <= kWsAutoUnion (WsArgs::ncand)
 constexpr int kWsCand1 = 4;          // ... of them read by the one-block merge and the peer exchange
 constexpr int kWsSelThreads = 256;   // selection / f-update workgroup
 constexpr int kWsMaxGroups = 256;    // selection workgroups per rank
@@ -290,9 +291,10 @@ constexpr int64_t kWsAutoRows = 50000;   // solver auto: working-set engines fro
 // up to P x q_max rows and solves P disjoint q-row sub-problems at once on P
 // workgroups; the combined step is scaled by the exact line-search factor
 // t = min(1, g'd / d'Qd) of the dual (ws_*.hip "multi-block rounds")
-constexpr int kWsMaxBlocks = 64;                  // blocks per round (P x q_max <= kWsMaxAll)
-constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto: P (blocks of kWsMaxAll / P rows)
-constexpr int kWsMaxAll = 16 * kWsMax;            // union capacity (3072 rows: the top 1536 of each side)
+constexpr int kWsMaxBlocks = 128;                 // blocks per round (P x q_max <= kWsMaxAll)
+constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto, coupled kernels: 32 blocks of kWsAutoUnion / 32 rows
+constexpr int kWsAutoUnion = 16 * kWsMax;         // 3072 rows (the top 1536 of each side): coupled, ws-cache, world > 1
+constexpr int kWsMaxAll = 32 * kWsMax;            // union capacity (6144 rows): uncoupled ws-dense rounds at world 1
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 constexpr int kWsMaxPass1Splits = 16;             // multi-block f-update pass 1: list slices over workgroups
 constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
@@ -399,7 +401,11 @@ struct WsArgs {
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
   int32_t* psync;      // persistent rounds (ws_persist.hip): [0] selection arrivals, [1] rounds released,
                        // [2..3] census, [4] gather arrivals (8 words)
+  int32_t ncand;       // multi-block selection: keys per side a list holds (kWsCandStd for unions of <=
+                       // kWsAutoUnion rows, kWsCand beyond; 0 = kWsCand); the tail of a list is kKeyNone
 };
+// keys per side and list of the multi-block selection (ws_select pass 2, the peer exchange)
+constexpr int ws_ncand(int ncand) { return ncand > 0 && ncand < kWsCand ? ncand : kWsCand; }
 // u64 words of the working-set exchange region (both parities): one-block
 // engine
 constexpr int64_t ws_xch_words(int64_t G_all, int64_t q_max) {

@@ -249,25 +249,27 @@ __device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
 // newest rows of the previous union.  Union position i goes to block
 // ((i / 2) mod P): each block gets up / low pairs, block 0 the global extremes
 // (so a round always holds the maximal violating pair and makes progress).
-constexpr int kMH = 4096;  // merge hash slots per side (load <= 0.38)
+constexpr int kMH = 8192;  // merge hash slots per side (load <= 0.19 at 3,072-row unions, <= 0.38 at 6,144)
 constexpr int kWsWindowMulti = 8192;  // cache mode: CLOCK victim window of the multi-block merge
-__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 20; }
-__device__ __forceinline__ void mh_insert(int32_t* keys, int32_t* vals, int32_t idx, int32_t v) {
+static_assert(kMH == 8192, "13-bit Fibonacci hash");
+__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 19; }
+// keys: row indices (-1 empty); values: 16-bit ranks (< kWsMaxGroups * kWsCand)
+__device__ __forceinline__ void mh_insert(int32_t* keys, uint16_t* vals, int32_t idx, int32_t v) {
   uint32_t h = mh_hash(idx);
   while (true) {
     const int32_t old = atomicCAS(keys + h, -1, idx);
     if (old == -1) {
-      vals[h] = v;
+      vals[h] = (uint16_t)v;
       return;
     }
     h = (h + 1) & (kMH - 1);
   }
 }
-__device__ __forceinline__ int32_t mh_find(const int32_t* keys, const int32_t* vals, int32_t idx) {
+__device__ __forceinline__ int32_t mh_find(const int32_t* keys, const uint16_t* vals, int32_t idx) {
   uint32_t h = mh_hash(idx);
   for (int probe = 0; probe < kMH; ++probe) {
     const int32_t k = keys[h];
-    if (k == idx) return vals[h];
+    if (k == idx) return (int32_t)vals[h];
     if (k == -1) return -1;
     h = (h + 1) & (kMH - 1);
   }
@@ -285,10 +287,10 @@ __global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsAr
   if (c->done != kRunning) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(15);
   const int e = (int)(blockIdx.x * kXCollectThreads + threadIdx.x);  // (list, side, rank) key
-  // keys per side the previous round's selection pushed: kWsCand by pass 2 of a
+  // keys per side the previous round's selection pushed: ws_ncand by pass 2 of a
   // multi-block round (and the seed), kWsCand1 by a one-block round — also in the
   // one-block rounds of a multi-block engine, whose slots stay kWsCand wide
-  const int nk = a.blocks > 1 ? kWsCand : kWsCand1;
+  const int nk = a.blocks > 1 ? ws_ncand(a.ncand) : kWsCand1;
   bool ok = true;
   if (e < a.G_all * 2 * kWsCand) {
     const int l = e / (2 * kWsCand), side = (e / kWsCand) & 1, r = e % kWsCand;
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsAr
 // lanes of one key read 16 consecutive 16-B pairs: no bank conflict, broadcast
 // over keys).
 constexpr int kRankThreads = 512;
-constexpr int kRankChunks = 64;
+constexpr int kRankChunks = kWsMaxGroups * kWsCand / 32;  // 32 keys per workgroup, 16 threads per key
 __global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
   constexpr int NK = kWsMaxGroups * kWsCand;
   constexpr int KPW = NK / kRankChunks, SUB = kRankThreads / KPW, PAIRS = NK / (2 * SUB);
@@ -360,12 +362,13 @@ __global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
 __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
   constexpr int T = kWsMergeThreads;
   constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
+  constexpr int X = NK / T;                   // keys per thread and side: elements tid + x T
   constexpr int U = kWsMaxAll / T;            // previous-union rows per thread
-  static_assert(NK == 2 * T, "two keys per thread and side: elements tid and tid + T");
-  static_assert(kWsMaxAll % T == 0 && U <= 3, "previous union: <= 3 rows per thread (scan counts <= 3)");
-  static_assert(kMH >= kWsMaxAll && kWsWindowMulti == 8 * T, "cache-mode aliases of the hash tables / sort keys");
-  __shared__ uint64_t s_k[2][NK];
-  __shared__ int32_t s_hash[4][kMH];
+  static_assert(NK % T == 0 && kWsMaxAll % T == 0 && U <= 7, "previous union: <= 7 rows per thread (3-bit scans)");
+  static_assert(kMH == kWsWindowMulti && kWsWindowMulti == 8 * T && NK <= 65536,
+                "cache mode: the CLOCK window's pins alias the low side's key table; 16-bit ranks");
+  __shared__ int32_t s_hk[2][kMH];   // [side] hash keys (row indices)
+  __shared__ uint16_t s_hv[2][kMH];  // [side] their ranks
   __shared__ int32_t s_keep[kWsMaxAll + 2];
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ int s_wsum[T / 64];
@@ -378,7 +381,6 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     return;
   }
   if (lead) WS_STAMP(1);
-  const int G = a.G_all;
   const int par = (int)(c->outer & 1);
   const int P = max(1, min(c->p_act, a.blocks)), Qmax = P * a.q_max;
   const int q_prev = c->uq[par ^ 1];
@@ -387,24 +389,19 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   int32_t pidx[U];
 #pragma unroll
   for (int h = 0; h < U; ++h) pidx[h] = U * tid + h < q_prev ? c->uidx[par ^ 1][U * tid + h] : -1;
-  // keys e = tid and e = tid + T of each side, in ascending order (ws_rank)
-  uint64_t v[2][2];  // [side][element]
+  // keys e = tid + x T of each side, in ascending order (ws_rank)
+  uint64_t v[2][X];  // [side][element]
 #pragma unroll
-  for (int x = 0; x < 2; ++x) {
+  for (int x = 0; x < X; ++x) {
     v[0][x] = a.sorted[tid + x * T];
     v[1][x] = a.sorted[NK + tid + x * T];
   }
+  const uint64_t gu = a.sorted[0], gl = a.sorted[NK];  // each side's smallest key
   if (tid < kWsMaxBlocks) s_qb[tid] = 0;
-  for (int t = tid; t < 4 * kMH; t += T) (&s_hash[0][0])[t] = -1;
+  for (int t = tid; t < 2 * kMH; t += T) (&s_hk[0][0])[t] = -1;
   if (lead) WS_STAMP(20);
-#pragma unroll
-  for (int sd = 0; sd < 2; ++sd) {
-    s_k[sd][tid] = v[sd][0];
-    s_k[sd][tid + T] = v[sd][1];
-  }
   __syncthreads();
   if (lead) WS_STAMP(11);
-  const uint64_t gu = s_k[0][0], gl = s_k[1][0];
   const float b_hi = key_value(gu), b_lo = -key_value(gl);
   const int64_t it0 = c->iter;
   int stop = kRunning;
@@ -423,14 +420,15 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     }
     return;
   }
-  int32_t* hk_u = s_hash[0];
-  int32_t* hv_u = s_hash[1];
-  int32_t* hk_l = s_hash[2];
-  int32_t* hv_l = s_hash[3];
-  const int half = (want + 1) / 2;  // <= kWsMaxAll / 2 = T + T / 2 ranks per side
-  uint64_t ku[2], kl[2];
+  int32_t* hk_u = s_hk[0];
+  uint16_t* hv_u = s_hv[0];
+  int32_t* hk_l = s_hk[1];
+  uint16_t* hv_l = s_hv[1];
+  int32_t* const s_line = s_hk[0] + kMH / 2;  // cache mode, once the tables are dead: the union's lines
+  const int half = (want + 1) / 2;  // <= kWsMaxAll / 2 ranks per side
+  uint64_t ku[X], kl[X];
 #pragma unroll
-  for (int x = 0; x < 2; ++x) {
+  for (int x = 0; x < X; ++x) {
     const int e = tid + x * T;
     ku[x] = e < half ? v[0][x] : kKeyNone;
     kl[x] = e < half ? v[1][x] : kKeyNone;
@@ -441,10 +439,11 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   if (lead) WS_STAMP(12);
   // rank e keeps its up row unless the low side has it at a smaller rank, its
   // low row unless the up side has it at a rank <= e (the up copy comes first)
-  bool kpu[2] = {false, false}, kpl[2] = {false, false};
+  bool kpu[X], kpl[X];
 #pragma unroll
-  for (int x = 0; x < 2; ++x) {
+  for (int x = 0; x < X; ++x) {
     const int e = tid + x * T;
+    kpu[x] = kpl[x] = false;
     if (ku[x] != kKeyNone) {
       const int rl = mh_find(hk_l, hv_l, (int32_t)key_index(ku[x]));
       kpu[x] = !(rl >= 0 && rl < e);
@@ -455,17 +454,24 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     }
   }
   // union order: ranks 0 .. T - 1 (element 0 of threads in order), then ranks
-  // T .. (element 1): two scans
-  int tot0 = 0, tot1 = 0;
-  const int slot0 = block_scan_merge((int)kpu[0] + (int)kpl[0], s_wsum, &tot0);
-  const int slot1 = tot0 + block_scan_merge((int)kpu[1] + (int)kpl[1], s_wsum, &tot1);
-  const int kept = tot0 + tot1;
+  // T .. 2 T - 1 (element 1), ...: one scan per element row that holds ranks
+  // below half (uniform)
+  int slot[X], kept = 0;
+#pragma unroll
+  for (int x = 0; x < X; ++x) {
+    slot[x] = kept;
+    if (x * T < half) {
+      int tot = 0;
+      slot[x] = kept + block_scan_merge((int)kpu[x] + (int)kpl[x], s_wsum, &tot);
+      kept += tot;
+    }
+  }
   const int n_chosen = min(kept, want);
 #pragma unroll
-  for (int x = 0; x < 2; ++x) {
+  for (int x = 0; x < X; ++x) {
     const int e = tid + x * T;
     if (e < half) {
-      const int su = x == 0 ? slot0 : slot1, sl = su + (int)kpu[x];
+      const int su = slot[x], sl = su + (int)kpu[x];
       const bool cu = kpu[x] && su < want, cl = kpl[x] && sl < want;
       s_keep[2 * e] = cu ? su : -1;
       s_keep[2 * e + 1] = cl ? sl : -1;
@@ -490,7 +496,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   }
   int ptotal = 0;
   if (n_chosen < Qmax) {  // uniform
-    int at = n_chosen + block_scan_merge(npk, s_wsum, &ptotal);
+    int at = n_chosen + block_scan_merge<3>(npk, s_wsum, &ptotal);
 #pragma unroll
     for (int h = 0; h < U; ++h) {
       if (pk[h]) {
@@ -509,9 +515,10 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     // while the round uses them); all misses at once (prefix scans), their
     // rows computed next by one row GEMM.  Setup guarantees
     // L >= 2 Qmax + kWsWindowMulti, so the window holds >= n_miss free lines. ----
-    int32_t* s_pin = (int32_t*)&s_k[0][0];  // the sort keys are dead: 8192 words
-    int32_t* s_victim = s_hash[0];         // the hash tables too: kMH words each
-    int32_t* s_line = s_hash[1];
+    // the hash tables are dead: the pins take the low side's key table (kMH
+    // words), victims and lines halves of the up side's (launch: Qmax <= kMH / 2)
+    int32_t* s_pin = s_hk[1];
+    int32_t* s_victim = s_hk[0];
     const int L = a.L, hand = c->hand;
     const int W = min(L, kWsWindowMulti);
     for (int w = tid; w < kWsWindowMulti; w += T) s_pin[w] = 0;
@@ -535,10 +542,13 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     int mrank[U], n_miss = 0;
 #pragma unroll
     for (int h = 0; h < U; ++h) {
-      const bool mh = tid + h * T < Q && ln[h] < 0;
-      int tot = 0;
-      mrank[h] = n_miss + block_scan_merge<1>((int)mh, s_wsum, &tot);
-      n_miss += tot;
+      mrank[h] = n_miss;
+      if (h * T < Q) {  // uniform
+        const bool mh = tid + h * T < Q && ln[h] < 0;
+        int tot = 0;
+        mrank[h] = n_miss + block_scan_merge<1>((int)mh, s_wsum, &tot);
+        n_miss += tot;
+      }
     }
     // free window slots SPT t .. SPT t + SPT - 1 in window order
     constexpr int SPT = kWsWindowMulti / T;
@@ -593,7 +603,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     c->uidx[par][u] = row;
     const int pi = u >> 1, b = pi % P, la = 2 * (pi / P) + (u & 1);
     c->idx[par][b * a.q_max + la] = row;
-    c->line[par][b * a.q_max + la] = a.cache ? s_hash[1][u] : row;  // cache: s_line; dense: line i is row i
+    c->line[par][b * a.q_max + la] = a.cache ? s_line[u] : row;  // dense: line i is row i
     atomicMax(&s_qb[b], la + 1);
   }
   __syncthreads();
@@ -683,9 +693,9 @@ void ws_xcollect_cand(const WsArgs& a, hipStream_t s) {
 
 void ws_merge_multi(const WsArgs& a, hipStream_t s) {
   DPSVM_CHECK(a.blocks > 1 && a.blocks <= kWsMaxBlocks && a.blocks * a.q_max <= kWsMaxAll && a.G_all <= kWsMaxGroups && a.q_max % 2 == 0 &&
-                  (!a.cache || ws_cache_multi_supported(a.L, a.blocks, a.q_max)),
+                  (!a.cache || (ws_cache_multi_supported(a.L, a.blocks, a.q_max) && a.blocks * a.q_max <= dev::kMH / 2)),
               "ws_merge_multi: multi-block rounds need <= 256 candidate lists, an even q_max and "
-              "(cache mode) L >= 2 P q_max + 4096 lines");
+              "(cache mode) <= 4096 union rows and L >= 2 P q_max + 4096 lines");
   DPSVM_CHECK(a.sorted != nullptr, "ws_merge_multi: no sort buffer");
   DPSVM_CHECK(!a.xpeer || a.xcw >= 4 * kWsCand, "ws_merge_multi: peer exchange slots too narrow");
   dev::ws_rank_kernel<<<2 * dev::kRankChunks, dev::kRankThreads, 0, s>>>(a);

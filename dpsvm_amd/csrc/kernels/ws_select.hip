@@ -264,9 +264,11 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
   // wave 0 merges the four lists; the owner of a winner drops it (keys are
   // unique: the global index is in the low bits)
   const int lane = tid & 63, wave = tid >> 6;
-  // multi-block merges read kWsCand keys per list (MODE 2: every multi-block
-  // round, the seed included), the one-block merge kWsCand1 (MODE 0)
-  constexpr int nc = MODE == 0 ? kWsCand1 : kWsCand;
+  // multi-block merges read ws_ncand keys per list (MODE 2: every multi-block
+  // round, the seed included; the list's tail is kKeyNone), the one-block
+  // merge kWsCand1 (MODE 0)
+  constexpr int NC = MODE == 0 ? kWsCand1 : kWsCand;  // register capacity
+  const int nc = MODE == 0 ? kWsCand1 : ws_ncand(a.ncand);
   for (int round = 0; round < nc && part == 0; ++round) {
     uint64_t mu = kKeyNone, ml = kKeyNone;
 #pragma unroll
@@ -293,17 +295,21 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
     uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
     uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
     uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
-    uint64_t pu[nc], pl[nc];  // uniform: every lane holds the list
-    for (int round = 0; round < nc; ++round) {
-      const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
-      if (lane == 0) {
-        out[round] = mu;
-        out[kWsCand + round] = ml;
+    uint64_t pu[NC], pl[NC];  // uniform: every lane holds the list
+#pragma unroll
+    for (int round = 0; round < NC; ++round) {
+      pu[round] = pl[round] = kKeyNone;
+      if (round < nc) {  // uniform
+        const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
+        pu[round] = mu;
+        pl[round] = ml;
+        if (eu == mu) eu = kKeyNone;
+        if (el == ml) el = kKeyNone;
       }
-      pu[round] = mu;
-      pl[round] = ml;
-      if (eu == mu) eu = kKeyNone;
-      if (el == ml) el = kKeyNone;
+      if (lane == 0 && (MODE != 0 || round < nc)) {  // multi-block lists: the tail past nc is kKeyNone
+        out[round] = pu[round];
+        out[kWsCand + round] = pl[round];
+      }
     }
     if (a.xpeer != nullptr && lane < a.world) {
       // lane p publishes to rank p: the nc keys per side the merge of this
@@ -312,9 +318,11 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
       const uint64_t t = xtag((uint32_t)c->outer + 1u);
       const int lo = a.xcw / 2;
 #pragma unroll
-      for (int r = 0; r < nc; ++r) {
-        ws_put64(dst + 2 * r, t, pu[r]);
-        ws_put64(dst + lo + 2 * r, t, pl[r]);
+      for (int r = 0; r < NC; ++r) {
+        if (r < nc) {
+          ws_put64(dst + 2 * r, t, pu[r]);
+          ws_put64(dst + lo + 2 * r, t, pl[r]);
+        }
       }
     }
   }

@@ -637,17 +637,31 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // region; read by the auto choices below and by the pair choice): where the
   // kernel is numerically diagonal at working-set scale (MNIST-shape at gamma
   // 0.25: 1.7e-9; the structured mnist-parity: 4.3e-3; covtype-shape 0.85) the
-  // blocks of a round do not interact, so kWsMaxBlocks blocks of 48 rows (one
+  // blocks of a round do not interact, so blocks of 48 rows (one
   // row per solve lane: cheaper pair steps) beat 32 of 96 (headline
   // 0.0238-0.0240 vs 0.0241-0.0242 s); coupled data keeps 32 (mnist-parity
   // 0.0206 s with 32, 0.0422 s with 64: damped rounds; profiles/r5_blocks_64_vs_32_ab.txt)
   const double coupling = (ws_cand || wsc_cand) ? mean_offdiag_kernel(xh, n_x_rows, d, m.gamma) : 1.0;
   const bool uncoupled = m.all_agree(coupling < kWsUncoupled, m.comm, m.world);
-  const int auto_blocks = auto_blocks_env > 0 ? auto_blocks_env : uncoupled ? kWsMaxBlocks : kWsAutoBlocks;
-  const int auto_q = std::min(ws_q, kWsMaxAll / auto_blocks) & ~1;
+  // the round's union: the rounds touch ~3.4 n rows in all whatever the union
+  // (headline: 254 / 128 / 67 rounds at 768 / 1,536 / 3,072 rows), so a wider
+  // union divides the rounds' fixed cost (~50 us: selection, rank, merge, launch
+  // gaps) — uncoupled ws-dense rounds at world 1 take kWsMaxAll rows (128 blocks
+  // of 48; profiles/r5_union6144_ab.txt), everything else kWsAutoUnion
+  static const int union_env = [] {  // A/B: DPSVM_WS_UNION (kWsAutoUnion or kWsMaxAll)
+    const char* e = std::getenv("DPSVM_WS_UNION");
+    const int v = e ? atoi(e) : 0;
+    return v == kWsAutoUnion || v == kWsMaxAll ? v : 0;
+  }();
+  const bool wide_ok = uncoupled && ws_cand && m.world == 1;
+  const int auto_union = union_env > 0 ? (wide_ok ? union_env : kWsAutoUnion) : wide_ok ? kWsMaxAll : kWsAutoUnion;
+  const int auto_blocks = auto_blocks_env > 0 ? auto_blocks_env
+                          : uncoupled         ? auto_union / 48
+                                              : kWsAutoBlocks;
+  const int auto_q = std::min(ws_q, auto_union / auto_blocks) & ~1;
   const bool blocks_auto = m.p.ws_blocks == 0;
   const int want_blocks = !blocks_auto ? m.p.ws_blocks
-                                       : (n >= kWsAutoBlocksRows ? std::min(auto_blocks, kWsMaxAll / auto_q) : 1);
+                                       : (n >= kWsAutoBlocksRows ? std::min(auto_blocks, auto_union / auto_q) : 1);
   const int mb_q = blocks_auto ? auto_q : ws_q;  // rows per block of the multi-block rounds
   // (only where working-set rounds can run: solver=smo or a small problem ignores ws_blocks)
   DPSVM_CHECK(!(ws_cand || wsc_cand) || want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
@@ -655,8 +669,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // ws-cache takes them too when its cache holds the union's lines plus the
   // victim window (L >= 2 P q_max + 4096; agreed: L follows each device's free memory)
   const bool wsc_multi = wsc_fits_pre && launch::ws_cache_multi_supported(m.L, want_blocks, mb_q);
+  // (unions past kWsAutoUnion: ws-dense at world 1 only — the cache merge's
+  // line tables and the rehearsed peer exchange hold kWsAutoUnion rows)
   bool multi_elig = want_blocks > 1 && (ws_cand || wsc_multi) && mb_q % 2 == 0 &&
-                    (int64_t)ws_G * m.world <= kWsMaxGroups;
+                    (int64_t)ws_G * m.world <= kWsMaxGroups &&
+                    (want_blocks * mb_q <= kWsAutoUnion || (ws_cand && m.world == 1));
   if (m.world > 1) multi_elig = m.all_agree(multi_elig, m.comm, m.world);
   // Residency of the ws peer exchange with ranks sharing a device (rehearsals;
   // on distinct devices share = 1).  No producer ever waits: selection, gather
@@ -846,6 +863,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // multi-block rounds replace the whole union each round by default (measured on the
     // headline at P = 8: 3/4 q new 0.0506 s, all new 0.0493 s; profiles/r2_ws_blocks_sweep.txt)
     if (w.blocks > 1 && m.p.ws_new <= 0) w.n_new = w.q_max;
+    // keys per selection list: the union's half per side over the lists with
+    // room to spare (8 cover 3,072-row unions: 1,880 a side on the headline's 235)
+    w.ncand = w.blocks * w.q_max > kWsAutoUnion ? kWsCand : kWsCandStd;
     w.rank = m.rank;
     w.aux_stride = w.blocks * kWsMax;
     // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)

@@ -67,9 +67,9 @@ WsMergeProbe ws_merge_multi_probe(const std::vector<uint64_t>& cand, int G, int 
                                   int n_new, float eps, const std::vector<int32_t>& prev_union, int64_t iter,
                                   int64_t max_iter) {
   DPSVM_CHECK(G >= 1 && G <= kWsMaxGroups && (int64_t)cand.size() == (int64_t)G * 2 * kWsCand,
-              "ws_merge_multi_probe: cand must be [G][2][kWsCand = 8] with G <= 256");
+              "ws_merge_multi_probe: cand must be [G][2][kWsCand = 16] with G <= 256");
   DPSVM_CHECK(blocks >= 2 && blocks <= kWsMaxBlocks && q_max >= 2 && q_max <= kWsMax && q_max % 2 == 0,
-              "ws_merge_multi_probe: 2 <= blocks <= 16, even q_max <= 192");
+              "ws_merge_multi_probe: 2 <= blocks <= 128, blocks x q_max <= 6144, even q_max <= 192");
   DPSVM_CHECK((int64_t)prev_union.size() <= (int64_t)blocks * q_max, "ws_merge_multi_probe: previous union too long");
   Stream st;
   auto c = blank_ctrl();
@@ -114,7 +114,7 @@ WsSolveProbe ws_solve_probe(const std::vector<float>& K, const std::vector<float
                             int p_round, float C, int clip, float eps, float rel, float eps_floor, float tau,
                             float b_hi, float b_lo, int inner_max, int64_t iter0, int64_t max_iter, int wss) {
   DPSVM_CHECK(blocks >= 1 && blocks <= kWsMaxBlocks && (int)qb.size() == blocks && q_max >= 2 && q_max <= kWsMax,
-              "ws_solve_probe: 1 <= blocks <= 16, qb per block, q_max <= 192");
+              "ws_solve_probe: 1 <= blocks <= 128, qb per block, q_max <= 192");
   const size_t nq = (size_t)blocks * q_max;
   DPSVM_CHECK(K.size() == nq * q_max && f.size() == nq && alpha.size() == nq && y.size() == nq,
               "ws_solve_probe: K [P][q_max][q_max], f / alpha / y [P][q_max]");

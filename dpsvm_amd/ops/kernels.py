@@ -181,7 +181,7 @@ def rbf_rows_indexed(x: torch.Tensor, rows, gamma: float, out_lines=None, n_line
 
 
 KEY_NONE = (1 << 64) - 1
-WS_CAND = 8  # candidates per side per selection workgroup (device_state.hpp kWsCand)
+WS_CAND = 16  # candidates per side per selection workgroup (device_state.hpp kWsCand)
 
 
 def ws_merge_multi(cand, blocks: int, q_max: int, n_new: int, eps: float, prev_union=(), p_act: int | None = None,

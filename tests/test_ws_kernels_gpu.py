@@ -14,7 +14,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 NONE = np.uint64((1 << 64) - 1)
-KC = 8   # candidates per side per selection workgroup (device_state.hpp kWsCand)
+KC = 16  # candidates per side per selection workgroup (device_state.hpp kWsCand)
 KC1 = 4  # ... produced for (and read by) the one-block rounds (kWsCand1)
 
 
@@ -114,11 +114,15 @@ def crafted_candidates(rng, G, n_rows, ties=True):
 @pytest.mark.parametrize("G,blocks,p_act,n_prev,n_new", [(256, 8, 8, 0, 192), (256, 8, 4, 300, 96),
                                                         (37, 8, 8, 1000, 192), (200, 4, 1, 150, 144),
                                                         (256, 2, 2, 64, 40), (256, 32, 32, 0, 96),
-                                                        (256, 32, 16, 2500, 48), (240, 16, 16, 900, 96)])
+                                                        (256, 32, 16, 2500, 48), (240, 16, 16, 900, 96),
+                                                        (256, 128, 128, 0, 48), (256, 128, 64, 4000, 24),
+                                                        (235, 128, 128, 6000, 48)])
 def test_ws_merge_multi_matches_model(K, G, blocks, p_act, n_prev, n_new):
+    """128 x 48: the 6,144-row union (3,072 ranks a side over 4,096 keys, hash
+    tables three-quarters full)."""
     rng = np.random.default_rng(G * 31 + blocks + p_act + n_prev)
-    q_max = 192 if blocks == 8 else 96
-    cand, rows = crafted_candidates(rng, G, 3000 if blocks <= 8 else 12000)
+    q_max = 192 if blocks == 8 else 48 if blocks > 64 else 96
+    cand, rows = crafted_candidates(rng, G, 3000 if blocks <= 8 else 12000 if blocks <= 64 else 30000)
     # previous union: half of it rows the merge picks again (dropped from the
     # retained tail), half rows it does not
     prev = np.concatenate([rng.choice(rows, size=n_prev // 2, replace=False),
