@@ -646,14 +646,14 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // the round's union: the rounds touch ~3.4 n rows in all whatever the union
   // (headline: 254 / 128 / 67 rounds at 768 / 1,536 / 3,072 rows), so a wider
   // union divides the rounds' fixed cost (~50 us: selection, rank, merge, launch
-  // gaps) — uncoupled ws-dense rounds at world 1 take kWsMaxAll rows (128 blocks
-  // of 48; profiles/r5_union6144_ab.txt), everything else kWsAutoUnion
+  // gaps) — uncoupled ws-dense rounds take kWsMaxAll rows (128 blocks of 48;
+  // profiles/r5_union6144_ab.txt), everything else kWsAutoUnion
   static const int union_env = [] {  // A/B: DPSVM_WS_UNION (kWsAutoUnion or kWsMaxAll)
     const char* e = std::getenv("DPSVM_WS_UNION");
     const int v = e ? atoi(e) : 0;
     return v == kWsAutoUnion || v == kWsMaxAll ? v : 0;
   }();
-  const bool wide_ok = uncoupled && ws_cand && m.world == 1;
+  const bool wide_ok = uncoupled && ws_cand;
   const int auto_union = union_env > 0 ? (wide_ok ? union_env : kWsAutoUnion) : wide_ok ? kWsMaxAll : kWsAutoUnion;
   const int auto_blocks = auto_blocks_env > 0 ? auto_blocks_env
                           : uncoupled         ? auto_union / 48
@@ -669,11 +669,10 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // ws-cache takes them too when its cache holds the union's lines plus the
   // victim window (L >= 2 P q_max + 4096; agreed: L follows each device's free memory)
   const bool wsc_multi = wsc_fits_pre && launch::ws_cache_multi_supported(m.L, want_blocks, mb_q);
-  // (unions past kWsAutoUnion: ws-dense at world 1 only — the cache merge's
-  // line tables and the rehearsed peer exchange hold kWsAutoUnion rows)
+  // (unions past kWsAutoUnion: ws-dense only — the cache merge's line tables
+  // hold kWsAutoUnion rows)
   bool multi_elig = want_blocks > 1 && (ws_cand || wsc_multi) && mb_q % 2 == 0 &&
-                    (int64_t)ws_G * m.world <= kWsMaxGroups &&
-                    (want_blocks * mb_q <= kWsAutoUnion || (ws_cand && m.world == 1));
+                    (int64_t)ws_G * m.world <= kWsMaxGroups && (want_blocks * mb_q <= kWsAutoUnion || ws_cand);
   if (m.world > 1) multi_elig = m.all_agree(multi_elig, m.comm, m.world);
   // Residency of the ws peer exchange with ranks sharing a device (rehearsals;
   // on distinct devices share = 1).  No producer ever waits: selection, gather

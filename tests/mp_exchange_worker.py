@@ -17,7 +17,10 @@ def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
 
     ctx = init_distributed(device="cuda")
     comm = make_comm(ctx, "gloo")
-    X, y = synthetic("covtype", n=n, seed=2)
+    knobs = json.loads(extra_json)
+    data = knobs.pop("_data", "covtype")  # "mnist": the uncoupled headline shape (C 10, gamma 0.25)
+    X, y = synthetic(data, n=n, seed=2)
+    hp = dict(C=10.0, gamma=0.25) if data == "mnist" else dict(C=4.0, gamma=0.5)
     extra = {"cache_lines": 256, "engines": "all"} if engine == "persistent-cache" else {}
     if engine.startswith("ws"):  # working-set rounds, rows sharded (candidates + sub-Gram rows in-kernel)
         extra = {"solver": "ws", "dp": "shard"}
@@ -25,8 +28,8 @@ def main(out: str, engine: str, n: int, extra_json: str = "{}") -> int:
             extra.update(force_cache=True, cache_lines=1500)
     else:
         extra.update(persist="off" if engine == "fused" else "on", persist_block=257)
-    extra.update(json.loads(extra_json))  # SVCConfig knobs (geometry, poll batch, ...)
-    clf = SVC(C=4.0, gamma=0.5, eps=1e-3, device=ctx.device, exchange="peer", xch_timeout_s=30.0,
+    extra.update(knobs)  # SVCConfig knobs (geometry, poll batch, ...)
+    clf = SVC(eps=1e-3, device=ctx.device, exchange="peer", xch_timeout_s=30.0, **hp,
               **extra).fit(X, y, comm=comm)
     rec = {"exchange": clf.setup_info_["exchange"], "iteration": clf.setup_info_["iteration"],
            "exchange_mem": clf.setup_info_["exchange_mem"],

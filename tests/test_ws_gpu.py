@@ -445,6 +445,43 @@ def test_ws_multi_block_peer_exchange_processes_one_gpu(tmp_path, world, clip):
         assert res[k]["alpha_sha"] == sha
 
 
+def test_ws_wide_union_peer_exchange_two_processes_one_gpu(tmp_path):
+    """Sharded rounds of 128 blocks of 48 rows (the 6,144-row union the
+    uncoupled headline takes) over the in-kernel peer exchange, two ranks as
+    processes sharing the GPU: 16 candidate keys a side per list pushed and
+    collected, 128 sub-problems' entries polled by the solve — bit-identical to
+    the same two ranks over host-staged collectives (thread ranks)."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from dpsvm_amd._native import load
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DPSVM_FORCE_DEVICE="0")
+    out = tmp_path / "wide2"
+    knobs = {"ws_blocks": 128, "ws_size": 48, "_data": "mnist"}
+    n = 14000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29761",
+           os.path.join(root, "tests", "mp_exchange_worker.py"), str(out), "ws", str(n), json.dumps(knobs)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    errs = "".join(open(f"{out}.rank{k}.err").read()[-1500:] for k in range(2) if os.path.exists(f"{out}.rank{k}.err"))
+    assert r.returncode == 0, errs + r.stderr[-2000:]
+    res = [json.load(open(f"{out}.rank{k}.json")) for k in range(2)]
+    X, y = synthetic("mnist", n=n, seed=2)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws", dp="shard", ws_blocks=128, ws_size=48)
+    ref = _fit_threads(load(), 2, X, y, exchange="allreduce", **kw)
+    sha = hashlib.sha256(ref[0].alpha_.tobytes()).hexdigest()
+    assert ref[0].stats_["ws_blocks"] == 128 and ref[0].converged_
+    for k in range(2):
+        assert res[k]["exchange"] == "peer" and res[k]["ws_blocks"] == 128, res[k]
+        assert res[k]["iters"] == ref[0].n_iter_ and res[k]["rounds"] == ref[0].n_rounds_
+        assert res[k]["alpha_sha"] == sha
+
+
 @pytest.mark.parametrize("clip", ["independent", "box"])
 @pytest.mark.parametrize("knobs", [{"ws_blocks": 4}, {"ws_blocks": 1}])
 def test_ws_peer_exchange_eight_processes_one_gpu(tmp_path, clip, knobs):
