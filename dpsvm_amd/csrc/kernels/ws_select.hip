@@ -35,6 +35,8 @@ constexpr int ws_parts() {
 // t = min(1, g'd / d'Qd) from the partials (fixed order: every workgroup the
 // same t), applies f += t d_f and alpha = alpha_new - (1 - t) d_alpha, then
 // selects the candidates.  Pass 2 walks no list: one partition, 256 threads.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 template <int RPT, int MODE>
 constexpr int ws_sel_parts() {
   return MODE == 2 ? 1 : ws_parts<RPT>();
@@ -260,57 +262,91 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
       if (in_low(av, yv, a.C)) kl[r] = make_key(-f[r], (uint32_t)gj);
     }
   }
-  // each wave's kWsCand smallest keys per side (DPP minima, no barrier), then
-  // wave 0 merges the four lists; the owner of a winner drops it (keys are
-  // unique: the global index is in the low bits)
+  // each wave's nc smallest keys per side, then wave 0 merges the four lists.
+  // Keys are unique (the global index is in the low bits) except kKeyNone, the
+  // largest: a key's place is the count of smaller keys, kKeyNone's the real
+  // keys' count plus its order among the lanes holding kKeyNone — a
+  // permutation, so every place is written once.  One row per thread (RPT 1,
+  // every rank of up to 60,160 rows): each lane counts over its wave's 64 keys
+  // (broadcast LDS reads, no barrier) instead of nc rounds of wave minima
   const int lane = tid & 63, wave = tid >> 6;
   // multi-block merges read ws_ncand keys per list (MODE 2: every multi-block
   // round, the seed included; the list's tail is kKeyNone), the one-block
   // merge kWsCand1 (MODE 0)
   constexpr int NC = MODE == 0 ? kWsCand1 : kWsCand;  // register capacity
   const int nc = MODE == 0 ? kWsCand1 : ws_ncand(a.ncand);
-  for (int round = 0; round < nc && part == 0; ++round) {
-    uint64_t mu = kKeyNone, ml = kKeyNone;
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      mu = ku[r] < mu ? ku[r] : mu;
-      ml = kl[r] < ml ? kl[r] : ml;
+  constexpr int W = kWsSelThreads / 64;
+  const uint64_t below = (1ull << lane) - 1ull;
+  // place of key k among the wave's keys, given the count of smaller ones
+  auto place = [&](uint64_t k, int smaller) {
+    const uint64_t none = __ballot(k == kKeyNone);
+    return k == kKeyNone ? 64 - __popcll(none) + __popcll(none & below) : smaller;
+  };
+  if constexpr (RPT == 1) {
+    __shared__ u64x2 s_kk[W][2][32];  // [wave][side] the wave's 64 keys
+    if (part == 0) {
+      const uint64_t mu = ku[0], ml = kl[0];
+      ((uint64_t*)s_kk[wave][0])[lane] = mu;
+      ((uint64_t*)s_kk[wave][1])[lane] = ml;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own stores, read by its lanes
+      int cu = 0, cl = 0;
+#pragma unroll 8
+      for (int m = 0; m < 32; ++m) {
+        const u64x2 vu = s_kk[wave][0][m], vl = s_kk[wave][1][m];
+        cu += (vu.x < mu ? 1 : 0) + (vu.y < mu ? 1 : 0);
+        cl += (vl.x < ml ? 1 : 0) + (vl.y < ml ? 1 : 0);
+      }
+      const int pu = place(mu, cu), pl = place(ml, cl);
+      if (pu < nc) s_wc[wave][0][pu] = mu;
+      if (pl < nc) s_wc[wave][1][pl] = ml;
     }
-    mu = wave_min_u64(mu);
-    ml = wave_min_u64(ml);
-    if (lane == 0) {
-      s_wc[wave][0][round] = mu;
-      s_wc[wave][1][round] = ml;
-    }
+  } else {
+    for (int round = 0; round < nc && part == 0; ++round) {
+      uint64_t mu = kKeyNone, ml = kKeyNone;
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      if (ku[r] == mu) ku[r] = kKeyNone;
-      if (kl[r] == ml) kl[r] = kKeyNone;
+      for (int r = 0; r < RPT; ++r) {
+        mu = ku[r] < mu ? ku[r] : mu;
+        ml = kl[r] < ml ? kl[r] : ml;
+      }
+      mu = wave_min_u64(mu);
+      ml = wave_min_u64(ml);
+      if (lane == 0) {
+        s_wc[wave][0][round] = mu;
+        s_wc[wave][1][round] = ml;
+      }
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        if (ku[r] == mu) ku[r] = kKeyNone;
+        if (kl[r] == ml) kl[r] = kKeyNone;
+      }
     }
   }
   __syncthreads();
   if (threadIdx.x < 64) {
-    constexpr int W = kWsSelThreads / 64;
-    const bool have = lane < W * kWsCand && (nc == kWsCand || lane % kWsCand < nc);  // the waves' nc entries
-    uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
-    uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
-    uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
-    uint64_t pu[NC], pl[NC];  // uniform: every lane holds the list
+    // lane l: entry l % kWsCand of wave l / kWsCand's list (W x kWsCand = 64)
+    static_assert(W * kWsCand == 64, "one merge entry per lane");
+    __shared__ uint64_t s_top[2][NC];
+    const bool have = lane % kWsCand < nc;  // the waves' nc entries
+    const uint64_t eu = have ? s_wc[lane / kWsCand][0][lane % kWsCand] : kKeyNone;
+    const uint64_t el = have ? s_wc[lane / kWsCand][1][lane % kWsCand] : kKeyNone;
+    int cu = 0, cl = 0;
 #pragma unroll
-    for (int round = 0; round < NC; ++round) {
-      pu[round] = pl[round] = kKeyNone;
-      if (round < nc) {  // uniform
-        const uint64_t mu = wave_min_u64(eu), ml = wave_min_u64(el);
-        pu[round] = mu;
-        pl[round] = ml;
-        if (eu == mu) eu = kKeyNone;
-        if (el == ml) el = kKeyNone;
-      }
-      if (lane == 0 && (MODE != 0 || round < nc)) {  // multi-block lists: the tail past nc is kKeyNone
-        out[round] = pu[round];
-        out[kWsCand + round] = pl[round];
+    for (int w = 0; w < W; ++w) {
+#pragma unroll
+      for (int r = 0; r < NC; ++r) {
+        if (r < nc) {  // uniform
+          cu += s_wc[w][0][r] < eu ? 1 : 0;
+          cl += s_wc[w][1][r] < el ? 1 : 0;
+        }
       }
     }
+    const int pu = place(eu, cu), pl = place(el, cl);
+    if (pu < NC) s_top[0][pu] = pu < nc ? eu : kKeyNone;  // multi-block lists: the tail past nc is kKeyNone
+    if (pl < NC) s_top[1][pl] = pl < nc ? el : kKeyNone;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint64_t* out = a.cand_out + (size_t)blockIdx.x * 2 * kWsCand;
+    if (lane < NC) out[lane] = s_top[0][lane];
+    else if (lane >= 32 && lane < 32 + NC) out[kWsCand + lane - 32] = s_top[1][lane - 32];
     if (a.xpeer != nullptr && lane < a.world) {
       // lane p publishes to rank p: the nc keys per side the merge of this
       // engine reads (slot width a.xcw: up keys at 0, low keys at a.xcw / 2)
@@ -320,8 +356,8 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
 #pragma unroll
       for (int r = 0; r < NC; ++r) {
         if (r < nc) {
-          ws_put64(dst + 2 * r, t, pu[r]);
-          ws_put64(dst + lo + 2 * r, t, pl[r]);
+          ws_put64(dst + 2 * r, t, s_top[0][r]);
+          ws_put64(dst + lo + 2 * r, t, s_top[1][r]);
         }
       }
     }
