@@ -243,6 +243,50 @@ __device__ __forceinline__ int block_scan_merge(int v, int* wsum, int* total) {
   return off + pre;
 }
 
+// X exclusive scans of per-thread counts (each < 4) behind ONE barrier: the
+// union's slots in scan order — slot[x] = the totals of scans 0 .. x - 1 plus
+// this thread's prefix in scan x; scans x >= nact (uniform) are skipped.
+// Returns the grand total.  msum: [X][kWsMergeThreads / 64], used once.
+template <int X>
+__device__ __forceinline__ int multi_scan_merge(const int (&v)[X], int (&slot)[X], int* msum, int nact) {
+  constexpr int NW = kWsMergeThreads / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  int pre[X];
+#pragma unroll
+  for (int x = 0; x < X; ++x) {
+    pre[x] = 0;
+    if (x < nact) {
+      int wt = 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const uint64_t m = __ballot((v[x] >> b) & 1);
+        pre[x] += __popcll(m & below) << b;
+        wt += __popcll(m) << b;
+      }
+      if (lane == 0) msum[x * NW + wave] = wt;
+    }
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int x = 0; x < X; ++x) {
+    slot[x] = base;
+    if (x < nact) {
+      int off = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int t = msum[x * NW + w];
+        off += w < wave ? t : 0;
+        tot += t;
+      }
+      slot[x] = base + off + pre[x];
+      base += tot;
+    }
+  }
+  return base;
+}
+
 // ONE workgroup: every candidate key of both sides sorted (bitonic, 2048 per
 // side, two per thread), the stop test, then the union: up rank r / low rank r
 // interleaved (most violating first, a row's first position wins), then the
@@ -372,6 +416,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   __shared__ int32_t s_keep[kWsMaxAll + 2];
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ int s_wsum[T / 64];
+  __shared__ int s_msum[X * (T / 64)];
   __shared__ int s_qb[kWsMaxBlocks];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x;
@@ -455,17 +500,11 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   }
   // union order: ranks 0 .. T - 1 (element 0 of threads in order), then ranks
   // T .. 2 T - 1 (element 1), ...: one scan per element row that holds ranks
-  // below half (uniform)
-  int slot[X], kept = 0;
+  // below half, all behind one barrier
+  int cnt[X], slot[X];
 #pragma unroll
-  for (int x = 0; x < X; ++x) {
-    slot[x] = kept;
-    if (x * T < half) {
-      int tot = 0;
-      slot[x] = kept + block_scan_merge((int)kpu[x] + (int)kpl[x], s_wsum, &tot);
-      kept += tot;
-    }
-  }
+  for (int x = 0; x < X; ++x) cnt[x] = (int)kpu[x] + (int)kpl[x];
+  const int kept = multi_scan_merge<X>(cnt, slot, s_msum, min(X, (half + T - 1) / T));
   const int n_chosen = min(kept, want);
 #pragma unroll
   for (int x = 0; x < X; ++x) {
