@@ -85,6 +85,11 @@ def main() -> int:
     if clf.setup_info_.get("ws_rounds") == "persistent":
         return persistent_report(a, clf, raw, rounds)
     s = raw[2:rounds]
+    # direct sub-Gram loads (blocks of <= 64 rows at world 1): no ws_gather launch, so no stamp 8
+    direct = not (s[:, 8] > 0).any()
+    if direct:
+        s = s.copy()
+        s[:, 8] = s[:, 2]  # "gather end" = merged: gather_end_to_solve becomes merged-to-solve
     ok = (s[:, [0, 1, 2, 3, 4, 6, 7, 8]] > 0).all(axis=1)
     us = lambda v: np.round(np.median(v) * 0.01, 2)  # noqa: E731  (10 ns ticks -> us)
     s = s[ok]
@@ -112,6 +117,7 @@ def main() -> int:
            if (s[:, 9] > 0).all() else {}),
         "gather_end_to_solve_us": us(s[:, 0] - s[:, 8]),
         "load_subgram_us": us(s[:, 3] - s[:, 0]),
+        **({"subgram": "direct (ws_solve loads its block; gather_* = merged -> solve)"} if direct else {}),
         "solve_us": us(s[:, 4] - s[:, 3]),
         "solve_per_step_us": float(np.round(np.median((s[:, 4] - s[:, 3]) / np.maximum(1, s[:, 5])) * 0.01, 3)),
         "solve_end_to_next_select_us": us(nxt - s[:, 4]),

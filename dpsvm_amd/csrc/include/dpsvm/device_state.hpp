@@ -401,6 +401,8 @@ struct WsArgs {
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
   int32_t* psync;      // persistent rounds (ws_persist.hip): [0] selection arrivals, [1] rounds released,
                        // [2..3] census, [4] gather arrivals (8 words)
+  int32_t direct_sub;  // multi-block solve loads its sub-Gram / f / alpha / y straight from the resident Gram
+                       // (world 1, dense, blocks of <= 64 rows: no ws_gather launch)
   int32_t ncand;       // multi-block selection: keys per side a list holds (kWsCandStd for unions of <=
                        // kWsAutoUnion rows, kWsCand beyond; 0 = kWsCand); the tail of a list is kKeyNone
 };

@@ -92,6 +92,42 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
       s_idx[tid] = c->idx[par][ib + tid];
       s_line[tid] = c->line[par][ib + tid];
     }
+  } else if (a.direct_sub) {
+    // blocks of <= 64 rows at world 1 (dense): the entries straight from the
+    // resident Gram (K(i, j) at gram[i ldg + j]) instead of a ws_gather launch
+    // of P q workgroups, its launch gap and a second copy through global
+    // memory.  Each entry is a random 128-B line of HBM, so only the upper
+    // triangle is loaded (the split Gram is bitwise symmetric) and mirrored in
+    // LDS: 1,176 loads for a 48-row block, all in flight at once
+    if (tid < q) {
+      const int32_t gi = c->idx[par][ib + tid];
+      s_idx[tid] = gi;
+      s_line[tid] = c->line[par][ib + tid];
+      s_f[tid] = a.f[gi];  // one rank: local row = global row
+      s_a[tid] = a.alpha[gi];
+      s_y[tid] = a.y[gi];
+    }
+    __syncthreads();
+    const int n = q * ldk;
+    constexpr int U = 4;
+    for (int e0 = tid; e0 < n; e0 += U * kWsSolveThreads) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * kWsSolveThreads;
+        const int ra = e / ldk, col = e - ra * ldk;
+        v[u] = e < n && ra <= col && col < q ? a.gram[(int64_t)s_idx[ra] * a.ldg + s_idx[col]] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * kWsSolveThreads;
+        const int ra = e / ldk, col = e - ra * ldk;
+        if (e < n && ra <= col) {
+          K[e] = v[u];                                    // columns q .. q_max - 1: zeros
+          if (col < q && col != ra) K[col * ldk + ra] = v[u];  // the mirrored entry
+        }
+      }
+    }
   } else {
     // q rows of the q_max-stride sub-Gram into LDS (147 KiB at q = 192): 16-B
     // loads, four in flight per thread before their stores

@@ -299,6 +299,7 @@ struct WsRounds : Base {
     // the one-block engine's set turnover (multi-block rounds replace the
     // whole union): ws_new_auto (device_state.hpp)
     w.n_new = ws_new_auto(m.p.ws_new, w.q_max, m.dp);
+    w.direct_sub = 0;  // the one-block rounds merge inside ws_gather
     return w;
   }
   // cache mode: the kernel rows of the round's misses (<= blocks x q_max rows), one GEMM
@@ -350,7 +351,7 @@ struct WsRounds : Base {
     if (w.blocks > 1) launch::ws_merge_multi(w, m.stream);
     else if (kCache) launch::ws_merge(w, m.stream);  // ws-dense one-block rounds merge inside ws_gather
     if (kCache) miss_rows(m, w);
-    launch::ws_gather(w, m.stream);
+    if (!w.direct_sub) launch::ws_gather(w, m.stream);  // else ws_solve loads its block itself
     ws_allreduce_sub(m, w);
     launch::ws_solve(w, m.stream);
     if (w.blocks > 1) {

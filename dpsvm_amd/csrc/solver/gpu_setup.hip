@@ -865,6 +865,15 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // keys per selection list: the union's half per side over the lists with
     // room to spare (8 cover 3,072-row unions: 1,880 a side on the headline's 235)
     w.ncand = w.blocks * w.q_max > kWsAutoUnion ? kWsCand : kWsCandStd;
+    // blocks of <= 64 rows at world 1 on the resident Gram: the solve loads its
+    // q x q block itself (A/B: DPSVM_WS_DIRECT_SUB=0; 96-row blocks measured
+    // slower that way in round 4: 9,216 loads a workgroup, profiles/r4_direct_subgram_ab.txt)
+    static const int direct_env = [] {  // 0 off, 1 blocks of <= 64 rows (default), 2 <= 96 (A/B)
+      const char* e = std::getenv("DPSVM_WS_DIRECT_SUB");
+      return e ? atoi(e) : 1;
+    }();
+    const int direct_q = direct_env == 2 ? 96 : direct_env == 1 ? 64 : 0;
+    w.direct_sub = w.blocks > 1 && w.q_max <= direct_q && m.world == 1 && !w.cache && !m.xch ? 1 : 0;
     w.rank = m.rank;
     w.aux_stride = w.blocks * kWsMax;
     // candidate lists: [world][G][2][kWsCand] (this rank's block is the all-gather source)
