@@ -306,24 +306,40 @@ __device__ __forceinline__ void ws_solve_run(const WsArgs& a, WsCtrl* c, const f
     }
     ws_status(a.status, c);
   }
-  if (lane == 0 && kMulti) {
+  if (kMulti) {
     // publish this block's counts; the last block to finish commits the round
     // (threadfence + counter: no workgroup waits for another)
-    c->nab[blk] = n_apply;
-    c->inb[blk] = inner;
-    c->badb[blk] = bad ? 1 : 0;
-    c->clipb[blk] = clipped_any ? 1 : 0;
-    __threadfence();
-    const int prev = atomicAdd(&c->solve_cnt, 1);
-    if (prev == a.blocks - 1) {
+    int prev = 0;
+    if (lane == 0) {
+      c->nab[blk] = n_apply;
+      c->inb[blk] = inner;
+      c->badb[blk] = bad ? 1 : 0;
+      c->clipb[blk] = clipped_any ? 1 : 0;
       __threadfence();
-      int tot_a = 0, tot_i = 0, any_bad = 0, any_clip = 0;
-      for (int p = 0; p < a.blocks; ++p) {
+      prev = atomicAdd(&c->solve_cnt, 1);
+    }
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    int tot_a = 0, tot_i = 0, any_bad = 0, any_clip = 0;
+    if (prev == a.blocks - 1) {  // uniform
+      __threadfence();
+      // the P blocks' counts: every lane loads its blocks' (all loads in flight;
+      // one lane walking 128 blocks' agent-scope loads serialised them), then
+      // wave sums
+      for (int p = lane; p < a.blocks; p += 64) {
         tot_a += __hip_atomic_load(&c->nab[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         tot_i += __hip_atomic_load(&c->inb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         any_bad |= __hip_atomic_load(&c->badb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         any_clip |= __hip_atomic_load(&c->clipb[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        tot_a += __shfl_xor(tot_a, o);
+        tot_i += __shfl_xor(tot_i, o);
+        any_bad |= __shfl_xor(any_bad, o);
+        any_clip |= __shfl_xor(any_clip, o);
+      }
+    }
+    if (lane == 0 && prev == a.blocks - 1) {
       c->solve_cnt = 0;
       // the reference's independent clipping does not keep sum(alpha y) = 0: once
       // a clip broke it, the blocks' combined steps drift it further (measured:
