@@ -295,27 +295,39 @@ __device__ __forceinline__ int multi_scan_merge(const int (&v)[X], int (&slot)[X
 // (so a round always holds the maximal violating pair and makes progress).
 constexpr int kMH = 8192;  // merge hash slots per side (load <= 0.19 at 3,072-row unions, <= 0.38 at 6,144)
 constexpr int kWsWindowMulti = 8192;  // cache mode: CLOCK victim window of the multi-block merge
-static_assert(kMH == 8192, "13-bit Fibonacci hash");
-__device__ __forceinline__ uint32_t mh_hash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 19; }
-// keys: row indices (-1 empty); values: 16-bit ranks (< kWsMaxGroups * kWsCand)
+static_assert(kMH == 8192, "11-bit bucket hash");
+// keys: row indices (-1 empty) in buckets of four slots read as one 16-B LDS
+// word (a bucket fills left to right: no holes, so a free last slot ends a
+// search); values: 16-bit ranks (< kWsMaxGroups * kWsCand).  At the 6,144-row
+// union's 0.38 load a search is one bucket read; linear probing of single
+// slots took a dependent LDS trip per probe.
+constexpr int kMHB = kMH / 4;  // buckets per side
+typedef int mh_i4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t mh_bucket(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> 21; }
 __device__ __forceinline__ void mh_insert(int32_t* keys, uint16_t* vals, int32_t idx, int32_t v) {
-  uint32_t h = mh_hash(idx);
+  uint32_t b = mh_bucket(idx);
   while (true) {
-    const int32_t old = atomicCAS(keys + h, -1, idx);
-    if (old == -1) {
-      vals[h] = (uint16_t)v;
+    const mh_i4 kb = *(const mh_i4*)(keys + 4 * b);
+    const int s = kb.x == -1 ? 0 : kb.y == -1 ? 1 : kb.z == -1 ? 2 : kb.w == -1 ? 3 : 4;
+    if (s == 4) {
+      b = (b + 1) & (kMHB - 1);
+      continue;
+    }
+    if (atomicCAS(keys + 4 * b + s, -1, idx) == -1) {
+      vals[4 * b + s] = (uint16_t)v;
       return;
     }
-    h = (h + 1) & (kMH - 1);
+    // another row took that slot first: read the bucket again
   }
 }
 __device__ __forceinline__ int32_t mh_find(const int32_t* keys, const uint16_t* vals, int32_t idx) {
-  uint32_t h = mh_hash(idx);
-  for (int probe = 0; probe < kMH; ++probe) {
-    const int32_t k = keys[h];
-    if (k == idx) return (int32_t)vals[h];
-    if (k == -1) return -1;
-    h = (h + 1) & (kMH - 1);
+  uint32_t b = mh_bucket(idx);
+  for (int probe = 0; probe < kMHB; ++probe) {
+    const mh_i4 kb = *(const mh_i4*)(keys + 4 * b);
+    const int s = kb.x == idx ? 0 : kb.y == idx ? 1 : kb.z == idx ? 2 : kb.w == idx ? 3 : -1;
+    if (s >= 0) return (int32_t)vals[4 * b + s];
+    if (kb.w == -1) return -1;
+    b = (b + 1) & (kMHB - 1);
   }
   return -1;
 }
@@ -411,7 +423,7 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   static_assert(NK % T == 0 && kWsMaxAll % T == 0 && U <= 7, "previous union: <= 7 rows per thread (3-bit scans)");
   static_assert(kMH == kWsWindowMulti && kWsWindowMulti == 8 * T && NK <= 65536,
                 "cache mode: the CLOCK window's pins alias the low side's key table; 16-bit ranks");
-  __shared__ int32_t s_hk[2][kMH];   // [side] hash keys (row indices)
+  __shared__ __attribute__((aligned(16))) int32_t s_hk[2][kMH];  // [side] hash keys (row indices), 4-slot buckets
   __shared__ uint16_t s_hv[2][kMH];  // [side] their ranks
   __shared__ int32_t s_keep[kWsMaxAll + 2];
   __shared__ int32_t s_idx[kWsMaxAll];

@@ -205,14 +205,16 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
       if (a.world > 1 && blockIdx.x == 0) {
         // alpha is global on every rank: the changed rows this rank does not own
         // (its threads below fix the owned ones before classifying them)
-        for (int p = 0; p < a.blocks; ++p) {
-          const int nb = c->nab[p];
-          for (int k = threadIdx.x; k < nb; k += kWsSelThreads * PARTS) {
-            const int64_t gi = c->apply_idx[p * a.q_max + k];
-            if (gi >= a.off && gi < a.off + a.nl) continue;
-            if (t < 1.f) a.alpha[gi] = clip01(a.alpha[gi] - (1.f - t) * a.dalpha[gi], 0.f, a.C);
-            a.dalpha[gi] = 0.f;
-          }
+        // (the P segments' slots flat over the threads: every count and row load
+        // in flight at once, not one block's count after another)
+        const int slots = a.blocks * a.q_max;
+        for (int i = threadIdx.x; i < slots; i += kWsSelThreads * PARTS) {
+          const int p = i / a.q_max, k = i - p * a.q_max;
+          if (k >= c->nab[p]) continue;
+          const int64_t gi = c->apply_idx[i];
+          if (gi >= a.off && gi < a.off + a.nl) continue;
+          if (t < 1.f) a.alpha[gi] = clip01(a.alpha[gi] - (1.f - t) * a.dalpha[gi], 0.f, a.C);
+          a.dalpha[gi] = 0.f;
         }
       }
 #pragma unroll
@@ -378,6 +380,7 @@ __global__ __launch_bounds__(4 * kWsSelThreads) void ws_pass1_v4_kernel(WsArgs a
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ float s_coef[kWsMaxAll];
   __shared__ f4 s_part[PARTS - 1][kWsSelThreads];
+  __shared__ int s_off[kWsMaxBlocks];
   __shared__ double s_red[2][4 * kWsSelThreads / 64];
   __shared__ double s_red_tot[2];
   WsCtrl* c = a.ctrl;
@@ -390,15 +393,33 @@ __global__ __launch_bounds__(4 * kWsSelThreads) void ws_pass1_v4_kernel(WsArgs a
   {  // this workgroup's slice [e_lo, e_hi) of the blocks' concatenated apply segments
     const int per_wg = PARTS * ((na + PARTS * KS - 1) / (PARTS * KS));
     const int e_lo = min(na, ksi * per_wg), e_hi = min(na, e_lo + per_wg);
-    int at = 0;
-    for (int p = 0; p < a.blocks && at < e_hi; ++p) {
-      const int nb = c->nab[p];
-      const int k0 = max(0, e_lo - at), k1 = min(nb, e_hi - at);
-      for (int k = k0 + threadIdx.x; k < k1; k += 4 * kWsSelThreads) {
-        s_idx[at + k] = c->apply_line[p * a.q_max + k];
-        s_coef[at + k] = c->apply_coef[p * a.q_max + k];
+    // the segments' offsets: one wave's prefix scan of the P counts (two blocks
+    // a lane) — a walk over 128 blocks' counts, one dependent load after another,
+    // held up every workgroup's first row load by ~10 us
+    static_assert(kWsMaxBlocks <= 128, "two blocks per lane");
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x, P = a.blocks;
+      const int n0 = 2 * l < P ? c->nab[2 * l] : 0, n1 = 2 * l + 1 < P ? c->nab[2 * l + 1] : 0;
+      int inc = n0 + n1;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o);
+        if (l >= o) inc += v;
       }
-      at += nb;
+      s_off[2 * l] = inc - n0 - n1;  // exclusive: block 2 l starts here
+      s_off[2 * l + 1] = inc - n1;
+    }
+    __syncthreads();
+    for (int e = e_lo + (int)threadIdx.x; e < e_hi; e += 4 * kWsSelThreads) {
+      int lo = 0, hi = a.blocks - 1;  // the last block whose segment starts at or before e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      const int k = e - s_off[lo];
+      s_idx[e] = c->apply_line[lo * a.q_max + k];
+      s_coef[e] = c->apply_coef[lo * a.q_max + k];
     }
   }
   __syncthreads();
