@@ -429,7 +429,6 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ int s_wsum[T / 64];
   __shared__ int s_msum[X * (T / 64)];
-  __shared__ int s_qb[kWsMaxBlocks];
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x;
   const bool lead = tid == 0;
@@ -454,7 +453,6 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     v[1][x] = a.sorted[NK + tid + x * T];
   }
   const uint64_t gu = a.sorted[0], gl = a.sorted[NK];  // each side's smallest key
-  if (tid < kWsMaxBlocks) s_qb[tid] = 0;
   for (int t = tid; t < 2 * kMH; t += T) (&s_hk[0][0])[t] = -1;
   if (lead) WS_STAMP(20);
   __syncthreads();
@@ -649,16 +647,27 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
     }
     __syncthreads();
   }
+  // union position u -> block (u / 2) mod P, row 2 ((u / 2) / P) + (u & 1) of it
+  // (shifts for the power-of-two block counts the engine uses; integer
+  // division by a runtime P costs ~40 instructions)
+  const bool pow2 = (P & (P - 1)) == 0;
+  const int lg = pow2 ? __ffs(P) - 1 : 0;
   for (int u = tid; u < Q; u += T) {
     const int32_t row = s_idx[u];
     c->uidx[par][u] = row;
-    const int pi = u >> 1, b = pi % P, la = 2 * (pi / P) + (u & 1);
+    const int pi = u >> 1;
+    const int b = pow2 ? pi & (P - 1) : pi % P, la = 2 * (pow2 ? pi >> lg : pi / P) + (u & 1);
     c->idx[par][b * a.q_max + la] = row;
     c->line[par][b * a.q_max + la] = a.cache ? s_line[u] : row;  // dense: line i is row i
-    atomicMax(&s_qb[b], la + 1);
   }
-  __syncthreads();
-  if (tid < a.blocks) c->qb[par][tid] = s_qb[tid];  // inactive blocks: 0 rows
+  if (tid < a.blocks) {
+    // rows per block from the layout: block b holds pairs b, b + P, ... of the
+    // NP = ceil(Q / 2) pairs; the last pair is one row when Q is odd
+    const int NP = (Q + 1) >> 1, b = tid;
+    const int cnt = b < P && b < NP ? (NP - 1 - b) / P + 1 : 0;
+    const int last = b + P * (cnt - 1);
+    c->qb[par][b] = cnt == 0 ? 0 : 2 * (cnt - 1) + ((last == NP - 1 && (Q & 1)) ? 1 : 2);  // inactive blocks: 0 rows
+  }
   if (lead) {
     c->uq[par] = Q;
     c->q[par] = Q;
