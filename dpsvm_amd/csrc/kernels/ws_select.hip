@@ -374,17 +374,22 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
 // thread 4 adjacent ones (16-B row loads): each wave reads 1 KiB of a changed
 // Gram row per load instead of 256 B (HBM row-buffer locality of the scattered
 // rows), and p1G = ceil(nl_max / 1024) groups x ks list slices fill the device.
-constexpr int kP1Cols = 4 * kWsSelThreads;  // columns per workgroup
-__global__ __launch_bounds__(4 * kWsSelThreads) void ws_pass1_v4_kernel(WsArgs a) {
-  constexpr int PARTS = 4, CH = 12;  // 12 rows x 16 B in flight per thread
+// TPP threads per partition x PARTS partitions = 1024 threads; a workgroup owns
+// 4 TPP columns (TPP 256: 1024 columns, four partitions — the default; TPP 512:
+// 2048 columns, two partitions — A/B, DPSVM_P1_COLS=2048)
+constexpr int kP1Threads = 4 * kWsSelThreads;
+template <int TPP>
+__global__ __launch_bounds__(kP1Threads) void ws_pass1_v4_kernel(WsArgs a) {
+  constexpr int PARTS = kP1Threads / TPP, CH = 12;  // 12 rows x 16 B in flight per thread
+  constexpr int kP1Cols = 4 * TPP;                  // columns per workgroup
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ float s_coef[kWsMaxAll];
-  __shared__ f4 s_part[PARTS - 1][kWsSelThreads];
+  __shared__ f4 s_part[PARTS - 1][TPP];
   __shared__ int s_off[kWsMaxBlocks];
-  __shared__ double s_red[2][4 * kWsSelThreads / 64];
+  __shared__ double s_red[2][kP1Threads / 64];
   __shared__ double s_red_tot[2];
   WsCtrl* c = a.ctrl;
-  const int tid = threadIdx.x & (kWsSelThreads - 1), part = threadIdx.x / kWsSelThreads;
+  const int tid = threadIdx.x & (TPP - 1), part = threadIdx.x / TPP;
   if (blockIdx.x == 0 && threadIdx.x == 0) WS_STAMP(22);
   const int na = c->n_apply;
   if (na == 0) return;
@@ -410,7 +415,7 @@ __global__ __launch_bounds__(4 * kWsSelThreads) void ws_pass1_v4_kernel(WsArgs a
       s_off[2 * l + 1] = inc - n1;
     }
     __syncthreads();
-    for (int e = e_lo + (int)threadIdx.x; e < e_hi; e += 4 * kWsSelThreads) {
+    for (int e = e_lo + (int)threadIdx.x; e < e_hi; e += kP1Threads) {
       int lo = 0, hi = a.blocks - 1;  // the last block whose segment starts at or before e
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -485,7 +490,7 @@ __global__ __launch_bounds__(4 * kWsSelThreads) void ws_pass1_v4_kernel(WsArgs a
   __syncthreads();
   if (threadIdx.x == 0) {
     double tq = 0.0, tg = 0.0;
-    for (int k = 0; k < 4 * kWsSelThreads / 64; ++k) {
+    for (int k = 0; k < kP1Threads / 64; ++k) {
       tq += s_red[0][k];
       tg += s_red[1][k];
     }
@@ -590,9 +595,21 @@ void ws_select(const WsArgs& a, hipStream_t s) {
   }
 }
 
+// columns per wide pass-1 workgroup (A/B: DPSVM_P1_COLS=2048)
+int ws_pass1_v4_cols() {
+  static const int cols = [] {
+    const char* e = std::getenv("DPSVM_P1_COLS");
+    return e && atoi(e) == 2048 ? 2048 : 1024;
+  }();
+  return cols;
+}
+
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
   if (pass == 1 && a.p1v4) {
-    dev::ws_pass1_v4_kernel<<<dim3(a.p1G * std::max(1, a.ks)), 4 * kWsSelThreads, 0, s>>>(a);
+    if (ws_pass1_v4_cols() == 2048)
+      dev::ws_pass1_v4_kernel<512><<<dim3(a.p1G * std::max(1, a.ks)), dev::kP1Threads, 0, s>>>(a);
+    else
+      dev::ws_pass1_v4_kernel<256><<<dim3(a.p1G * std::max(1, a.ks)), dev::kP1Threads, 0, s>>>(a);
     post_launch("ws_pass1_v4", s);
   } else if (pass == 1) {
     ws_select_mode<1>(a, s);
@@ -601,7 +618,10 @@ void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
   }
 }
 
-int ws_pass1_v4_groups(int64_t nl_max) { return (int)std::max<int64_t>(1, (nl_max + dev::kP1Cols - 1) / dev::kP1Cols); }
+int ws_pass1_v4_groups(int64_t nl_max) {
+  const int64_t cols = ws_pass1_v4_cols();
+  return (int)std::max<int64_t>(1, (nl_max + cols - 1) / cols);
+}
 
 // the wide pass 1's list slices: about one workgroup per CU (the headline at one
 // rank: 59 groups x 4 slices; a rank of 8: 8 groups x 32 slices)
