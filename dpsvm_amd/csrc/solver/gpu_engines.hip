@@ -383,13 +383,14 @@ struct WsRounds : Base {
     }
     if (ws_graphs(m) && !m.gexec) capture_rounds(m, this->block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });
   }
-  void observe(GpuSolver::Impl& m, const SmoStatus& st, int64_t blocks_done) override {
+  bool shortens() const override { return true; }
+  void observe(GpuSolver::Impl& m, const SmoStatus& st, int64_t launched) override {
     if (single || m.wsa.blocks <= 1 || st.ws_p1_round <= 0) return;
     // the switch to the one-block graph happens on kWsSwitchRounds boundaries
     // only, with what the host knew one such span earlier — the rounds the
     // 32-round graph blocks switched at, whatever the graph block size (short
     // blocks end a solve sooner after convergence without moving a trajectory)
-    const int64_t B = this->block(m.p), next = (blocks_done + 1) * B;  // first round after the block in flight
+    const int64_t B = this->block(m.p), next = launched;  // first round after the launch in flight
     const int64_t span = std::max<int64_t>(B, kWsSwitchRounds);
     if (next % span != 0) return;
     if (st.ws_p1_round > next - span) return;  // set by a later round: next boundary
@@ -404,7 +405,7 @@ struct WsRounds : Base {
       return;
     }
     hipGraphExec_t g = single ? m.gexec1 : m.gexec;
-    if (g) {
+    if (g && B == this->block(m.p)) {  // a shorter launch (rounds before a predicted convergence): plain launches
       HIP_CHECK(hipGraphLaunch(g, m.stream));
     } else {
       const WsArgs w = single ? one_block(m) : m.wsa;

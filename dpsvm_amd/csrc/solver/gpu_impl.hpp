@@ -202,10 +202,15 @@ struct Engine {
   virtual void prepare(GpuSolver::Impl&) {}  // per-solve state reset, before the timed region
   virtual void seed(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo, SolveResult& res) = 0;
   virtual void run_block(GpuSolver::Impl& m, int B) = 0;
-  // the status after `blocks_done` completed blocks (the next block not yet
-  // enqueued): engines may change what they enqueue next — identically on every
-  // rank, so only from values that completed blocks wrote
-  virtual void observe(GpuSolver::Impl&, const SmoStatus&, int64_t /*blocks_done*/) {}
+  // run_block(m, B) also takes B < block(): the last rounds before a predicted
+  // convergence go one at a time (the host polls one launch behind, so the
+  // rounds after convergence in the launches already queued are early exits)
+  virtual bool shortens() const { return false; }
+  // the status of the completed launches, `launched` iterations / rounds
+  // enqueued so far (the one in flight included): engines may change what they
+  // enqueue next — identically on every rank, so only from values that
+  // completed launches wrote
+  virtual void observe(GpuSolver::Impl&, const SmoStatus&, int64_t /*launched*/) {}
   virtual Pending pending(GpuSolver::Impl&) { return {}; }
   virtual double gram_seconds() { return 0.0; }
 };
