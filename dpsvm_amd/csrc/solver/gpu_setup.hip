@@ -660,9 +660,24 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
                                               : kWsAutoBlocks;
   const int auto_q = std::min(ws_q, auto_union / auto_blocks) & ~1;
   const bool blocks_auto = m.p.ws_blocks == 0;
-  const int want_blocks = !blocks_auto ? m.p.ws_blocks
-                                       : (n >= kWsAutoBlocksRows ? std::min(auto_blocks, auto_union / auto_q) : 1);
+  int want_blocks = !blocks_auto ? m.p.ws_blocks
+                                 : (n >= kWsAutoBlocksRows ? std::min(auto_blocks, auto_union / auto_q) : 1);
   const int mb_q = blocks_auto ? auto_q : ws_q;  // rows per block of the multi-block rounds
+  // ranks sharing one device (rehearsals; 1 on distinct devices) and the wave
+  // slots the peer exchange's spinning consumers may take (below)
+  int xch_share = 1, xch_cus = 0;
+  if (m.world > 1) {
+    xch_share = max_device_sharing(m);  // collective
+    HIP_CHECK(hipDeviceGetAttribute(&xch_cus, hipDeviceAttributeMultiprocessorCount, m.device));
+  }
+  auto xch_waves = [&](int blocks) { return (int64_t)xch_share * (64 + 16 * std::max(1, blocks)) + 1024; };
+  // a wide auto union whose 128 spinning solve workgroups per rank would not
+  // leave the ranks sharing a device room for their producers: the
+  // kWsAutoUnion union instead (4 ranks on one GPU: 64 blocks over the peer
+  // exchange rather than one block per round over host collectives)
+  if (m.world > 1 && blocks_auto && want_blocks * mb_q > kWsAutoUnion &&
+      !m.all_agree(xch_waves(want_blocks) <= (int64_t)xch_cus * 32, m.comm, m.world))
+    want_blocks = kWsAutoUnion / mb_q;
   // (only where working-set rounds can run: solver=smo or a small problem ignores ws_blocks)
   DPSVM_CHECK(!(ws_cand || wsc_cand) || want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
               "ws_blocks x ws_size must be <= " + std::to_string(kWsMaxAll) + " (the round's union capacity)");
@@ -684,14 +699,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // one-block and multi-block rounds alike.
   bool xch_resident = true;
   if (m.world > 1) {
-    const int share = max_device_sharing(m);  // collective
-    int cus = 0;
-    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m.device));
-    const int64_t waves = (int64_t)share * (64 + 16 * std::max(1, want_blocks)) + 1024;
-    xch_resident = m.all_agree(waves <= (int64_t)cus * 32, m.comm, m.world);
+    const int64_t waves = xch_waves(want_blocks);
+    xch_resident = m.all_agree(waves <= (int64_t)xch_cus * 32, m.comm, m.world);
     if (!xch_resident && m.p.exchange != 2 && (ws_cand || wsc_fits_pre))
-      m.info.engine_note = "ws peer exchange refused: " + std::to_string(share) + " ranks share a device (" +
-                           std::to_string(waves) + " spinning + producer waves > " + std::to_string(cus * 32) +
+      m.info.engine_note = "ws peer exchange refused: " + std::to_string(xch_share) + " ranks share a device (" +
+                           std::to_string(waves) + " spinning + producer waves > " + std::to_string(xch_cus * 32) +
                            " wave slots): collectives";
   }
   const bool ws_peer_base = (ws_cand || wsc_fits_pre) && m.p.exchange != 1 && !m.p.force_collectives &&
