@@ -1417,9 +1417,9 @@ void split_rows_f16(const float* x, int64_t rows, int dp, int ldx, void* out, in
 
 namespace {
 // The symmetric Gram's upper tiles of the 256 x 128 wide-wave kernel (tile
-// (tx, ty) is needed when ty >= 2 tx) as a compact table in the XCD order of
-// xcd_tile_of (chunks of 64 tiles of 8 tile rows dealt round-robin to the 8
-// XCDs): built once per shape on the host, kept on the device.  The full grid
+// (tx, ty) is needed when ty >= 2 tx) as a compact table in an XCD order
+// (chunks of CH tiles of GM tile rows dealt round-robin to the 8 XCDs, as
+// xcd_tile_of does with 64 / 8): built once per shape on the host, kept on the device.  The full grid
 // launched tm x tn workgroups of which half exited at once (55k of 110k on
 // the headline).
 struct TileTable {
@@ -1432,10 +1432,22 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find({tm, tn});
   if (it != cache.end()) return it->second;
-  // the needed tiles in the order xcd_tile_of's bijection visits them: groups of
-  // 8 tile rows, column by column, rows inside a column
+  // the needed tiles in groups of GM tile rows, column by column, rows inside a
+  // column; chunks of CH consecutive tiles dealt round-robin to the 8 XCDs.
+  // GM 4 / CH 32 (an XCD's chunk: 4 A panels x 8 B panels) 9.34-9.45 ms vs
+  // 9.47-9.50 for GM 8 / CH 64 (profiles/r5_gram_tile_order_ab.txt; bit-identical
+  // output).  A/B: DPSVM_GRAM_GM / DPSVM_GRAM_CH
   std::vector<uint32_t> order;
-  constexpr int64_t GM = 8, CH = 64;
+  static const int64_t GM = [] {
+    const char* e = std::getenv("DPSVM_GRAM_GM");
+    const int v = e ? atoi(e) : 4;
+    return (int64_t)(v >= 1 && v <= 64 ? v : 4);
+  }();
+  static const int64_t CH = [] {
+    const char* e = std::getenv("DPSVM_GRAM_CH");
+    const int v = e ? atoi(e) : 32;
+    return (int64_t)(v >= 8 && v <= 1024 ? v : 32);
+  }();
   for (int64_t g0 = 0; g0 < tm; g0 += GM) {
     const int64_t gm = std::min(GM, tm - g0);
     for (int64_t ty = 0; ty < tn; ++ty)
