@@ -172,6 +172,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   }();
   const bool can_short = tail_env && m.engine->shortens() && B > 1;
   bool near = false;
+  int near_left = 0;
   double prev_gap = -1.0;
   int64_t launched = 0;
   while (true) {
@@ -199,9 +200,19 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
         progress(Progress{st.iter, st.b_hi, st.b_lo, secs_since(t0), st.hits, st.misses});
       }
       if (st.done != kRunning) break;
-      if (can_short && !near) {
-        const double gap = (double)st.b_lo - (double)st.b_hi;
-        if (prev_gap > 0.0 && gap > 0.0 && gap < prev_gap) near = gap * (gap / prev_gap) <= 4.0 * (double)m.p.eps;
+      if (can_short) {
+        // on when the gap times its last decay is within 2 x the stop gap
+        // (2 eps), for at most kShortRun single-round launches — a noisy drop on
+        // a slowly converging problem costs that many, not the rest of the
+        // solve in single rounds — then re-armed by the same test
+        constexpr int kShortRun = 32;
+        const double gap = (double)st.b_lo - (double)st.b_hi, eps = (double)m.p.eps;
+        if (near_left > 0) {
+          --near_left;
+        } else if (prev_gap > 0.0 && gap > 0.0 && gap < prev_gap && gap * (gap / prev_gap) <= 4.0 * eps) {
+          near_left = kShortRun;
+        }
+        near = near_left > 0;
         prev_gap = gap;
       }
       m.engine->observe(m, st, launched);  // launches 0 .. blocks - 1 completed, launch `blocks` in flight
