@@ -7,10 +7,7 @@ export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
 timeout -k 10 120 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 || true
-# dense headline: Gram GEMM (MFMA 32x32x2 f32) + persistent SMO kernel
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+# headline (ws-dense): split Gram GEMM (f16 MFMA) + the working-set round kernels
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
   -d "$OUT/dense_mfma" -o pmc --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-accuracy || exit $?
-# cache mode: fused cache kernel (X pass on MFMA 16x16x4), bounded run
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES \
-  -d "$OUT/lru" -o pmc --output-format csv -- python3 bench/lru_profile_run.py 14 3000 || exit $?
 python3 bench/pmc_summary.py "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

@@ -18,40 +18,6 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def persistent_report(a, clf, raw, rounds) -> int:
-    """persistent rounds (ws_persist.hip, workgroup 0): [0] round start, [1]
-    arrivals seen, [2] merged, [8] gather arrivals seen, [3] sub-Gram in LDS,
-    [4] solved, then — in the
-    next slot — [6] release seen, [10] f updated, [7] candidates published"""
-    s = raw[2:rounds - 1]
-    nx = raw[3:rounds]  # the select phase that follows round r sits in slot r + 1
-    ok = (s[:, [0, 1, 2, 3, 4, 8]] > 0).all(axis=1) & (nx[:, [6, 7, 10]] > 0).all(axis=1)
-    s, nx = s[ok], nx[ok]
-    us = lambda v: np.round(np.median(v) * 0.01, 2)  # noqa: E731
-    res = {
-        "rounds": clf.n_rounds_, "pair_steps": clf.n_iter_, "fit_time_s": round(clf.fit_time_, 4),
-        "b": float(clf.b_), "n_sv": int(clf.n_support_), "engine": clf.setup_info_["iteration"],
-        "ws_rounds": "persistent", "steps_per_round_median": float(np.median(s[:, 5])),
-        "arrival_wait_us": us(s[:, 1] - s[:, 0]),
-        "merge_us": us(s[:, 2] - s[:, 1]),
-        "gather_and_arrivals_us": us(s[:, 8] - s[:, 2]),
-        "subgram_to_lds_us": us(s[:, 3] - s[:, 8]),
-        "solve_us": us(s[:, 4] - s[:, 3]),
-        "solve_per_step_us": float(np.round(np.median((s[:, 4] - s[:, 3]) / np.maximum(1, s[:, 5])) * 0.01, 3)),
-        "commit_to_release_seen_us": us(nx[:, 6] - s[:, 4]),
-        "select_fupdate_us": us(nx[:, 10] - nx[:, 6]),
-        "select_candidates_us": us(nx[:, 7] - nx[:, 10]),
-        "round_period_us": us(np.diff(s[:, 0])),
-    }
-    res["outside_solve_us"] = round(res["round_period_us"] - res["solve_us"], 2)
-    line = json.dumps(res)
-    print(line)
-    if a.out:
-        with open(a.out, "w") as f:
-            f.write(line + "\n")
-    return 0
-
-
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--data", default="mnist")
@@ -68,7 +34,6 @@ def main() -> int:
     ap.add_argument("--force-cache", action="store_true")
     ap.add_argument("--exchange", default="auto", help="peer: the in-kernel exchange at world 1 (loopback)")
     ap.add_argument("--clip", default="independent", choices=["independent", "box"])
-    ap.add_argument("--ws-persist", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "ws_stamps")
@@ -79,11 +44,9 @@ def main() -> int:
     X, y = synthetic(a.data, n=a.samples, d=a.features)
     clf = SVC(C=a.C, gamma=a.gamma, eps=1e-3, device="cuda", solver="ws", ws_size=a.ws_size, ws_new=a.ws_new,
               ws_rel=a.ws_rel, ws_blocks=a.ws_blocks, max_iter=a.max_iter, cache_lines=a.cache_lines, force_cache=a.force_cache,
-              exchange=a.exchange, xch_timeout_s=60.0, clip=a.clip, shrink="off", ws_persist=a.ws_persist).fit(X, y)
+              exchange=a.exchange, xch_timeout_s=60.0, clip=a.clip, shrink="off").fit(X, y)
     raw = np.fromfile(path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
     rounds = min(clf.n_rounds_, 4096)
-    if clf.setup_info_.get("ws_rounds") == "persistent":
-        return persistent_report(a, clf, raw, rounds)
     s = raw[2:rounds]
     # direct sub-Gram loads (blocks of <= 64 rows at world 1): no ws_gather launch, so no stamp 8
     direct = not (s[:, 8] > 0).any()

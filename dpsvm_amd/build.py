@@ -3,11 +3,13 @@
 Products (all git-ignored, shipped to the GPU box with the snapshot):
   dpsvm_amd/_C<EXT_SUFFIX>   pybind11 module (solver, kernels, comm, I/O): the production engines
   dpsvm_amd/libdpsvm_pairq.so  plugin: the quarantined pair-at-a-time cache / partitioned-X
-                             engines (loaded for engines="all"; linked into the CLIs)
+                             engines (loaded for engines="all"; linked into bin/svmTrainPairq
+                             and bin/dpsvm_unit only)
   bin/svmTrain               distributed trainer CLI  (reference: svmTrainMain.cpp)
   bin/svmTest                predictor CLI            (reference: seq_test.cpp / Makefile:104)
   bin/svmSeq                 CPU trainer CLI          (reference: seq.cpp)
   bin/dpsvm_unit             native unit tests (CTest-style, run by pytest)
+  bin/svmTrainPairq          svmTrain with the quarantined engines linked in (--engines all)
 
 Usage:  python -m dpsvm_amd.build [-j N] [--force] [--debug] [--asan]
 Everything is compiled by hipcc (ROCm 7.2) with --offload-arch=gfx950; .cpp files
@@ -58,7 +60,6 @@ LIB_SOURCES = [
     "kernels/ws_select.hip",
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
-    "kernels/ws_persist.hip",
     "kernels/ws_recompute.hip",
 ]
 # the quarantined engines (solver/gpu_engines_pairq.hip registers them): a plugin
@@ -74,7 +75,11 @@ CLI = {
     "svmTest": "cli/svm_test.cpp",
     "svmSeq": "cli/svm_seq.cpp",
     "dpsvm_unit": "cli/unit_tests.cpp",
+    "svmTrainPairq": "cli/svm_train.cpp",
 }
+# the CLIs that link the quarantined engines in: the native unit tests and a
+# separate trainer for `--engines all`; the default CLIs are production-only
+CLI_WITH_PLUGIN = {"dpsvm_unit", "svmTrainPairq"}
 BINDINGS = "python/bindings.cpp"
 
 
@@ -157,7 +162,7 @@ def build(jobs: int | None = None, force: bool = False, debug: bool = False, asa
     tasks = [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in LIB_SOURCES + PLUGIN_SOURCES]
     tasks.append((CSRC / BINDINGS, objdir / "bindings.o", py_inc + ["-fvisibility=hidden"]))
     if clis:
-        tasks += [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in CLI.values()]
+        tasks += [(CSRC / s, objdir / (s.replace("/", "_") + ".o"), []) for s in sorted(set(CLI.values()))]
     with ThreadPoolExecutor(jobs) as ex:
         futs = [ex.submit(_compile, s, o, flags, e, force, hdr_m) for s, o, e in tasks]
         for f in futs:
@@ -184,8 +189,9 @@ def build(jobs: int | None = None, force: bool = False, debug: bool = False, asa
         for name, src in CLI.items():
             o = objdir / (src.replace("/", "_") + ".o")
             out = bindir / name
+            extra = plug_objs if name in CLI_WITH_PLUGIN else []
             if force or not out.exists() or out.stat().st_mtime < max(newest, newest_p, o.stat().st_mtime):
-                _link(out, lib_objs + plug_objs + [o], False, flags)
+                _link(out, lib_objs + extra + [o], False, flags)
                 if verbose:
                     print(f"linked {out}")
     return mod

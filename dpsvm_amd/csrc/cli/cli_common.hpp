@@ -352,7 +352,7 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           "\"iters_per_s\": %.3f, \"cache_lines\": %lld, \"cache_hits\": %lld, \"cache_misses\": %lld, "
           "\"rows_computed\": %lld, \"x_passes\": %lld, \"spec_rows\": %lld, \"data\": \"%s\", "
           "\"exchange_mem\": \"%s\", \"dp_policy\": \"%s\", \"rows_per_group\": %lld, \"groups\": %lld, "
-          "\"poll_batch\": %d, \"cus\": %d, \"blocks_per_cu\": %d, \"census\": \"%s\", \"engine_note\": \"%s\", "
+          "\"poll_batch\": %d, \"cus\": %d, \"blocks_per_cu\": %d, \"census\": \"%s\", \"engine_note\": \"%s\", \"cache_note\": \"%s\", "
           "\"rounds\": %lld, \"ws_blocks\": %d, \"ws_blocks_end\": %d, \"ws_one_block_from_round\": %lld, "
           "\"ws_damped_rounds\": %lld, \"gram\": \"%s\", \"params\": %s}\n",
           backend.c_str(), json_escape(device).c_str(), r.world, (long long)n, d, o.p.C, o.p.gamma, o.p.eps,
@@ -365,7 +365,8 @@ inline void write_metrics(const std::string& path, const Options& o, const Solve
           json_escape(o.synthetic.empty() ? o.file : "synthetic:" + o.synthetic).c_str(),
           x.setup.exchange_mem.c_str(), x.setup.dp_policy.c_str(), (long long)x.setup.rows_per_group,
           (long long)x.setup.groups, x.setup.poll_batch, x.setup.cus, x.setup.blocks_per_cu,
-          x.setup.census.c_str(), json_escape(x.setup.engine_note).c_str(), (long long)r.outer, r.ws_blocks,
+          x.setup.census.c_str(), json_escape(x.setup.engine_note).c_str(),
+          json_escape(x.setup.cache_note).c_str(), (long long)r.outer, r.ws_blocks,
           r.ws_blocks_end, (long long)r.ws_p1_round, (long long)r.ws_damped, x.setup.gram.c_str(),
           params_json(o.p).c_str());
   fclose(fp);

@@ -126,15 +126,15 @@ struct SolverParams {
   int ws_size = 192;          // working-set rows q (<= 192: the q x q sub-Gram lives in LDS)
   int ws_new = 0;             // rows replaced per one-block round (0: auto, ws_new_auto in device_state.hpp)
   float ws_rel = 0.3f;        // sub-problem tolerance: max(eps, ws_rel * global gap / 2), < 1
-  int ws_blocks = 0;          // working-set engines: up to P disjoint q-row sub-problems per round (1..32,
-                              // P x ws_size <= 3072; 0 auto = 32 blocks of 96 rows from 50k rows, else 1).  Adaptive: halved after every damped round (coupled blocks), 1 after an
-                              // independent-clip event, then the one-block round kernels (ws_*.hip)
+  int ws_blocks = 0;          // working-set engines: up to P disjoint q-row sub-problems per round (1..128,
+                              // P x ws_size <= 6144; 0 auto from 50k rows: 128 x 48 rows on numerically diagonal
+                              // ws-dense kernels, else 32 x 96 (3072 rows); below 50k rows 1).  Adaptive: halved
+                              // after every damped round (coupled blocks), 1 after an independent-clip event,
+                              // then the one-block round kernels (ws_*.hip)
   int ws_inner = 0;           // pair steps per round at most (0: 4 * ws_size)
   int ws_wss = 0;             // sub-problem pair choice: 1 the reference's first-order rule (max f over I_low),
                               // 2 second order (WSS2: max (f_lo - b_hi)^2 / eta); the stop test is unchanged;
                               // 0 auto: second order when a row sample's mean off-diagonal K > 0.1
-  int ws_persist = 0;         // persistent one-block rounds (ws_persist.hip: one rank, resident Gram): 1 on where
-                              // supported; 0 auto and 2 off keep the graph of launches (measured faster)
   int ws_recompute = 0;       // ws-cache rounds without the row cache (ws_recompute.hip: kernel rows recomputed,
                               // fused into the f update): 0 auto (one rank, one block, d <= 64 padded), 1 on, 2 off
   int ws_block = 8;           // rounds per hipGraph block (the host stops at most ~2 blocks past convergence;

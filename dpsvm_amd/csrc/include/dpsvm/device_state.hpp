@@ -295,6 +295,22 @@ constexpr int kWsMaxBlocks = 128;                 // blocks per round (P x q_max
 constexpr int kWsAutoBlocks = 32;                 // ws_blocks auto, coupled kernels: 32 blocks of kWsAutoUnion / 32 rows
 constexpr int kWsAutoUnion = 16 * kWsMax;         // 3072 rows (the top 1536 of each side): coupled, ws-cache, world > 1
 constexpr int kWsMaxAll = 32 * kWsMax;            // union capacity (6144 rows): uncoupled ws-dense rounds at world 1
+constexpr int kWsCacheWindow = 512;               // ws-cache: victim lines searched after the CLOCK hand (ws_merge.hip)
+
+// ws-cache needs the round's rows (2 q_max: this round's and last round's
+// members are pinned) plus the victim window
+inline int64_t ws_cache_min_lines(int q_max) { return 2 * (int64_t)q_max + kWsCacheWindow; }
+
+// -s N (cache_lines > 0) on the engines a setup may choose: the reference takes
+// any count (svmTrainMain.cpp:71, default 10; cache.cu:49-60, 82-105).  The
+// production engines (engines = 0) raise a count below the working-set cache's
+// minimum to that minimum; engines = 1 (the quarantined pair-at-a-time cache
+// engines, which take any >= 2) keep it.  0 = no user cap.
+inline int64_t production_line_cap(int64_t cache_lines, int ws_q, int engines) {
+  if (cache_lines <= 0 || engines != 0) return cache_lines;
+  const int64_t lo = ws_cache_min_lines(ws_q);
+  return cache_lines < lo ? lo : cache_lines;
+}
 constexpr int kWsMergeThreads = 1024;             // multi-block merge: one workgroup
 constexpr int kWsMaxPass1Splits = 16;             // multi-block f-update pass 1: list slices over workgroups
 constexpr int64_t kWsAutoBlocksRows = 50000;      // ws_blocks auto: multi-block rounds from this many rows on
@@ -399,8 +415,6 @@ struct WsArgs {
   int32_t p1G;         // multi-block pass 1: column groups per rank (= G; the wide pass 1: ceil(nl_max / 1024))
   int32_t p1v4;        // multi-block pass 1: 1 = wide column groups, 4 columns (16-B loads) per thread
   uint64_t* sorted;    // multi-block: [2][kWsMaxGroups * kWsCand] every candidate key per side, ascending (ws_rank)
-  int32_t* psync;      // persistent rounds (ws_persist.hip): [0] selection arrivals, [1] rounds released,
-                       // [2..3] census, [4] gather arrivals (8 words)
   int32_t direct_sub;  // multi-block solve loads its sub-Gram / f / alpha / y straight from the resident Gram
                        // (world 1, dense, blocks of <= 64 rows: no ws_gather launch)
   int32_t ncand;       // multi-block selection: keys per side a list holds (kWsCandStd for unions of <=

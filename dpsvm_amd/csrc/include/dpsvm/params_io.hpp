@@ -61,7 +61,6 @@ void for_each_param(SolverParams& p, F&& f) {
   f("ws_t_halve", p.ws_t_halve);
   f("ws_clip_fallback", p.ws_clip_fallback);
   f("ws_block", p.ws_block);
-  f("ws_persist", p.ws_persist);
   f("ws_recompute", p.ws_recompute);
   f("eta", p.eta);
   f("gram_precision", p.gram_precision);

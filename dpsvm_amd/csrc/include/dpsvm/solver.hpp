@@ -64,7 +64,7 @@ struct GpuSetupInfo {
   bool x_replicated = true;
   int64_t cache_lines = 0, host_cache_lines = 0;
   int blocks = 0;
-  size_t bytes_device = 0;
+  size_t bytes_device = 0;  // device memory held now (lines lent out by release_cache() do not count)
   std::string iteration;  // engine: "persistent-dense" | "fused-dense" | "persistent-cache" | "fused-cache" | "chain"
   std::string exchange;   // per-iteration key exchange: "none" | "allreduce" | "peer" | "loopback" (1 rank)
   std::string exchange_mem = "none";  // peer exchange receive buffer: "uncached" (across devices) | "coarse"
@@ -78,6 +78,7 @@ struct GpuSetupInfo {
   int cus = 0, blocks_per_cu = 0;     // residency of the persistent kernel (occupancy API)
   std::string census = "n/a";         // residency census of the persistent grid: "ok" | "failed" | "n/a"
   std::string engine_note;            // why the engine was chosen / refused (fallbacks)
+  std::string cache_note;             // cache_lines (-s N) raised to the working-set cache's minimum
   int ws_wss = 0;                     // working-set engines: sub-problem pair choice (1 first, 2 second order)
   std::string ws_rounds = "none";     // working-set engines: "graph" (launches per round) or "persistent"
   std::string ws_rows = "none";       // ws engines' kernel rows: "gram" (resident), "cache" (row cache), "recompute"

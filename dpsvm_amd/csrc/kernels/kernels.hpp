@@ -79,9 +79,6 @@ void ws_select(const WsArgs& a, hipStream_t s);
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s);
 void ws_gather(const WsArgs& a, hipStream_t s);
 void ws_solve(const WsArgs& a, hipStream_t s);
-// persistent small-problem rounds (ws_persist.hip): `rounds` one-block rounds in
-// one launch of a.G co-resident workgroups; census: rounds = -1 on a.psync + 2
-bool ws_persist_supported(const WsArgs& a);
 // ws-cache without the cache (ws_recompute.hip): merge + sub-Gram from the split
 // X rows, and the round's f update with the kernel rows recomputed (d <= 64)
 bool ws_recompute_supported(const WsArgs& a, int dp);
@@ -89,10 +86,6 @@ void ws_subgram_split(const WsArgs& a, const void* xs, const int32_t* xsh, const
                       hipStream_t s);
 void ws_fupdate_split(const WsArgs& a, const void* xs, const int32_t* xsh, const float* xsq, int dp, float gamma,
                       hipStream_t s);
-size_t ws_persist_lds(const WsArgs& a);
-int ws_persist_blocks_per_cu(const WsArgs& a);
-void ws_persist_census(const WsArgs& a, hipStream_t s);
-void ws_persist(const WsArgs& a, int rounds, hipStream_t s);
 // cache mode: the merge + line assignment (one workgroup) runs before the
 // row GEMM; ws_gather then reads the sub-Gram from the members' lines
 void ws_merge(const WsArgs& a, hipStream_t s);

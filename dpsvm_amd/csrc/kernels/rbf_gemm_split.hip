@@ -39,6 +39,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "dpsvm/common.hpp"
@@ -1426,11 +1427,14 @@ struct TileTable {
   uint32_t* dev = nullptr;
   int64_t count = 0;
 };
+// Keyed by (device, tm, tn): the table lives in the memory of the device that
+// launches the GEMM (svmTrain -p N: one rank per device, threads of one process).
 const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
   static std::mutex mu;
-  static std::map<std::pair<int64_t, int64_t>, TileTable> cache;
+  static std::map<std::tuple<int, int64_t, int64_t>, TileTable> cache;
+  const int device = current_device();
   std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find({tm, tn});
+  auto it = cache.find({device, tm, tn});
   if (it != cache.end()) return it->second;
   // the needed tiles in groups of GM tile rows, column by column, rows inside a
   // column; chunks of CH consecutive tiles dealt round-robin to the 8 XCDs.
@@ -1469,7 +1473,7 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
   HIP_CHECK(hipMalloc((void**)&t.dev, (size_t)total * sizeof(uint32_t)));
   HIP_CHECK(hipMemcpyAsync(t.dev, tab.data(), (size_t)total * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  return cache.emplace(std::make_pair(tm, tn), t).first->second;
+  return cache.emplace(std::make_tuple(device, tm, tn), t).first->second;
 }
 }  // namespace
 
@@ -1578,11 +1582,16 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
       HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
       return std::max(1, n);
     }();
-    static float* trash = [] {  // the scratch line of the fixed-count stores (64 floats, never read)
-      float* t = nullptr;
-      HIP_CHECK(hipMalloc((void**)&t, 64 * sizeof(float)));
-      return t;
-    }();
+    // the scratch line of the fixed-count stores (64 floats, never read), one per device
+    static std::mutex trash_mu;
+    static float* trash_of[kMaxDevices] = {};
+    float* trash = nullptr;
+    {
+      const int device = current_device();
+      std::lock_guard<std::mutex> lk(trash_mu);
+      if (!trash_of[device]) HIP_CHECK(hipMalloc((void**)&trash_of[device], 64 * sizeof(float)));
+      trash = trash_of[device];
+    }
     const int64_t grid = std::min<int64_t>(tm * tn, cus);
     if (nkb == 1)
       dev::rbf_rows_split_persist_kernel<1><<<dim3((unsigned)grid), dev::kRowsPersistThreads, 0, s>>>(

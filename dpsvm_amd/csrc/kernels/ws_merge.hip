@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kWsGatherThreads) void ws_gather_kernel(WsArgs a) {
 // lines that hold a member (pinned while the round uses them); all misses are
 // assigned at once (one prefix scan), their rows computed next by one GEMM.
 // ---------------------------------------------------------------------------
-constexpr int kWsWindow = 512;
+constexpr int kWsWindow = kWsCacheWindow;
 
 __global__ __launch_bounds__(kWsGatherThreads) void ws_merge_kernel(WsArgs a) {
   __shared__ int32_t s_idx[kWsMax];
@@ -794,7 +794,7 @@ void ws_pack_rows(const float* x, int64_t off, int64_t nl, int dp, const float* 
   post_launch("ws_pack_rows", s);
 }
 
-bool ws_cache_supported(int64_t L, int q_max) { return L >= 2 * (int64_t)q_max + dev::kWsWindow; }
+bool ws_cache_supported(int64_t L, int q_max) { return L >= ws_cache_min_lines(q_max); }
 
 bool ws_cache_multi_supported(int64_t L, int blocks, int q_max) {
   return L >= 2 * (int64_t)blocks * q_max + dev::kWsWindowMulti;

@@ -1,7 +1,7 @@
 // Working-set engine: the one-block merge (stop test and the next working set
-// from every selection workgroup's candidate lists), shared by the round
-// kernels of ws_merge.hip and the persistent small-problem rounds
-// (ws_persist.hip).  Round structure and helpers: ws_common.hpp.
+// from every selection workgroup's candidate lists), used by the round
+// kernels of ws_merge.hip and ws_recompute.hip.  Round structure and helpers:
+// ws_common.hpp.
 #pragma once
 
 #include "ws_common.hpp"

@@ -4,6 +4,8 @@
 // shared helpers: ws_common.hpp.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "dpsvm/common.hpp"
 #include "dpsvm/device_state.hpp"
 #include "device_util.hpp"
@@ -202,15 +204,16 @@ void ws_solve(const WsArgs& a, hipStream_t s) {
   const int v2 = (w2 ? 4 : 0) + (multi ? 2 : 0) + (box ? 1 : 0);
   const bool one = a.q_max <= 64, two = !one && a.q_max <= 128;
   const Fn fn = one ? fns1[v2] : two ? fns2[v2] : fns[v];
-  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950)
-  static size_t attr[16] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024,
-                            64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
-  static size_t attr2[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
-  static size_t attr1[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
-  size_t& at = one ? attr1[v2] : two ? attr2[v2] : attr[v];
-  if (lds > at) {
+  // dynamic LDS above 64 KiB needs the attribute (160 KiB on gfx950); the
+  // largest size set so far per device and kernel (rank threads of one process
+  // launch on different devices concurrently)
+  static std::atomic<size_t> attr[kMaxDevices][32];
+  std::atomic<size_t>& at = attr[current_device()][one ? 24 + v2 : two ? 16 + v2 : v];
+  size_t cur = at.load(std::memory_order_relaxed);
+  if (lds > 64 * 1024 && lds > cur) {
     HIP_CHECK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    at = lds;
+    while (lds > cur && !at.compare_exchange_weak(cur, lds)) {
+    }
   }
   fn<<<multi ? a.blocks : 1, kWsSolveThreads, lds, s>>>(a);
   post_launch("ws_solve", s);

@@ -1,7 +1,7 @@
 // Working-set engine: the LDS sub-problem solve on one wave (the reference's
-// pair rule, svmTrainMain.cpp:255-299) and the round's commit — shared by
-// ws_solve.hip (one launch per round) and the persistent small-problem rounds
-// (ws_persist.hip).  Round structure and helpers: ws_common.hpp.
+// pair rule, svmTrainMain.cpp:255-299) and the round's commit, run by
+// ws_solve.hip (one launch per round).  Round structure and helpers:
+// ws_common.hpp.
 #pragma once
 
 #include "ws_common.hpp"

@@ -155,6 +155,7 @@ py::dict setup_dict(const GpuSetupInfo& i) {
   d["blocks_per_cu"] = i.blocks_per_cu;
   d["census"] = i.census;
   d["engine_note"] = i.engine_note;
+  d["cache_note"] = i.cache_note;
   d["ws_wss"] = i.ws_wss;
   d["ws_rounds"] = i.ws_rounds;
   d["ws_rows"] = i.ws_rows;
@@ -232,7 +233,6 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_t_halve", &SolverParams::ws_t_halve)
       .def_readwrite("ws_clip_fallback", &SolverParams::ws_clip_fallback)
       .def_readwrite("ws_block", &SolverParams::ws_block)
-      .def_readwrite("ws_persist", &SolverParams::ws_persist)
       .def_readwrite("ws_recompute", &SolverParams::ws_recompute)
       .def_readwrite("gram_precision", &SolverParams::gram_precision)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
@@ -644,6 +644,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lines"), py::arg("coef"), py::arg("nab"), py::arg("blocks"), py::arg("p_round"), py::arg("p_act"),
         py::arg("q_max"), py::arg("C"), py::arg("outer"), py::arg("ks") = 0, py::arg("reps") = 0,
         py::arg("wide") = false);
+  m.def("production_line_cap", &production_line_cap, py::arg("cache_lines"), py::arg("ws_size"),
+        py::arg("engines") = 0, "-s N on the engines a setup may choose (device_state.hpp)");
+  m.def("ws_cache_min_lines", &ws_cache_min_lines, py::arg("ws_size"));
   m.def("make_key", [](float f, uint32_t idx) { return make_key(f, idx); });
   m.def("key_value", [](uint64_t k) { return key_value(k); });
   m.def("key_index", [](uint64_t k) { return key_index(k); });

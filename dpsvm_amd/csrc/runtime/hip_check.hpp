@@ -26,6 +26,17 @@ inline bool sync_debug_env() {
   }();
   return v;
 }
+// Launch-side caches that hold device pointers or per-device state are keyed by
+// the calling thread's current device: svmTrain -p N runs one rank per device
+// as threads of ONE process, so a process-wide cache filled by device 0 would
+// hand device 0's memory to ranks 1..N-1.
+constexpr int kMaxDevices = 64;
+inline int current_device() {
+  int d = 0;
+  HIP_CHECK(hipGetDevice(&d));
+  if (d < 0 || d >= kMaxDevices) fail("current_device: device id out of range");
+  return d;
+}
 inline void post_launch(const char* what, hipStream_t s, bool force_sync = false) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e));

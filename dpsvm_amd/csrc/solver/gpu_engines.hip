@@ -285,6 +285,7 @@ void capture_rounds(GpuSolver::Impl& m, int B, hipGraph_t* graph, hipGraphExec_t
 template <class Base, bool kCache>
 struct WsRounds : Base {
   bool single = false;  // multi-block engine now running one-block rounds
+  int64_t prev_launched = 0;  // `launched` at the previous observe() (the switch boundary test)
   int block(const SolverParams& p) const override { return std::max(1, p.ws_block); }
   // the one-block view of a multi-block engine's buffers: sub-Gram at the start
   // of wssub, its f / alpha / y right after it (one contiguous sum all-reduce)
@@ -366,6 +367,7 @@ struct WsRounds : Base {
   }
   void seed_rounds(GpuSolver::Impl& m, int64_t iter0, float b_hi, float b_lo) {
     single = false;
+    prev_launched = 0;
     if (m.wsa.blocks > 1) HIP_CHECK(hipMemsetAsync(m.wsa.dalpha, 0, (size_t)m.n * 4, m.stream));
     WsCtrl c;
     memset(&c, 0, sizeof(c));
@@ -377,10 +379,6 @@ struct WsRounds : Base {
     HIP_CHECK(hipMemcpyAsync(m.wsctrl, &c, sizeof(c), hipMemcpyHostToDevice, m.stream));
     launch::ws_select(m.wsa, m.stream);
     ws_allgather_cand(m);
-    if (m.ws_persist) {  // persistent rounds (ws_persist.hip): no graph; arrivals == G x released rounds
-      HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 32, m.stream));
-      return;
-    }
     if (ws_graphs(m) && !m.gexec) capture_rounds(m, this->block(m.p), &m.graph, &m.gexec, [&] { round(m, m.wsa); });
   }
   bool shortens() const override { return true; }
@@ -392,18 +390,20 @@ struct WsRounds : Base {
     // blocks end a solve sooner after convergence without moving a trajectory)
     const int64_t B = this->block(m.p), next = launched;  // first round after the launch in flight
     const int64_t span = std::max<int64_t>(B, kWsSwitchRounds);
-    if (next % span != 0) return;
-    if (st.ws_p1_round > next - span) return;  // set by a later round: next boundary
+    // the last span boundary at or before `next`; it must lie inside the launch
+    // in flight (a short tail's single-round launches can leave `launched` off
+    // the boundaries: a modulo test would then never switch)
+    const int64_t prev = prev_launched;
+    prev_launched = next;
+    const int64_t bnd = next / span * span;
+    if (bnd <= prev) return;
+    if (st.ws_p1_round > bnd - span) return;  // set by a later round: next boundary
     single = true;
     const WsArgs w = one_block(m);
     launch::ws_to_single(w, m.stream);
     if (ws_graphs(m) && !m.gexec1) capture_rounds(m, this->block(m.p), &m.graph1, &m.gexec1, [&] { round(m, w); });
   }
   void run_block(GpuSolver::Impl& m, int B) override {
-    if (m.ws_persist && !single) {
-      launch::ws_persist(m.wsa, B, m.stream);
-      return;
-    }
     hipGraphExec_t g = single ? m.gexec1 : m.gexec;
     if (g && B == this->block(m.p)) {  // a shorter launch (rounds before a predicted convergence): plain launches
       HIP_CHECK(hipGraphLaunch(g, m.stream));

@@ -135,9 +135,6 @@ struct GpuSolver::Impl {
   // switches to once the adaptive block count reached 1 (built on first use)
   hipGraphExec_t gexec1 = nullptr;
   hipGraph_t graph1 = nullptr;
-  // persistent small-problem rounds (ws_persist.hip): on after a passed census
-  bool ws_persist = false;
-  int32_t* wspsync = nullptr;
   // ws-cache rounds with the kernel rows recomputed (ws_recompute.hip)
   bool ws_recompute = false;
 

@@ -37,7 +37,7 @@ GpuSolver::Impl::~Impl() {
   for (void* ptr : {(void*)x, (void*)xsq, (void*)y, (void*)alpha, (void*)f, (void*)lines, (void*)slot_of,
                     (void*)key_of, (void*)ref, (void*)hslot_of, (void*)hkey_of, (void*)partials, (void*)ctrl,
                     (void*)records, (void*)my_record, (void*)pf, (void*)rf, (void*)rcf, (void*)stamps,
-                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wspsync, (void*)wsdfs, (void*)wsdalpha, (void*)wspart, (void*)wssorted,
+                    (void*)plru_meta, (void*)plru_stats, (void*)wsctrl, (void*)wscand, (void*)wssub, (void*)wsdfs, (void*)wsdalpha, (void*)wspart, (void*)wssorted,
                     (void*)wsxq, (void*)wsxqsq, (void*)wsiota, xs, (void*)xsh, wsxs, (void*)wsxsh})
     if (ptr) (void)hipFree(ptr);
   if (status_h) (void)hipHostFree(status_h);
@@ -147,6 +147,9 @@ void GpuSolver::release_cache() {
   m.lines = nullptr;
   m.args.lines = nullptr;
   m.wsa.gram = nullptr;
+  // bytes_device is what the solver holds now (the lines are lent out)
+  m.bytes -= (size_t)m.L * m.ldl * sizeof(float);
+  m.info.bytes_device = m.bytes;
 }
 
 namespace {
@@ -214,58 +217,6 @@ int max_device_sharing(GpuSolver::Impl& m) {
     most = std::max(most, k);
   }
   return most;
-}
-
-// Persistent small-problem rounds (ws_persist.hip): ws-dense at one rank with
-// one block per round, on request (ws_persist = 1; auto keeps the graph: on the
-// covtype-shape 7.5k-row sub-problem a persistent round measured 88.3 us vs
-// 73.2 us for the graph of launches — an agent-scope signal costs what a
-// launch gap in a graph does, and a 256-thread workgroup per CU has a quarter
-// of the memory parallelism of the launches' 1024-thread workgroups for the
-// f update and the sub-Gram load; profiles/r5_ws_persist_ab.txt).  Its grid
-// spins on its own workgroups, so a census of the kernel's own grid and
-// resources comes first; a failed census keeps the graph.
-void ws_persist_setup(GpuSolver::Impl& m) {
-  WsArgs& w = m.wsa;
-  m.ws_persist = false;
-  w.psync = nullptr;
-  m.info.ws_rounds = "graph";
-  int mode = m.p.ws_persist;  // 0 auto, 1 on, 2 off
-  if (const char* e = std::getenv("DPSVM_WS_PERSIST")) mode = std::atoi(e);  // A/B runs
-  if (mode == 2 || m.kind != EngineKind::WsDense || m.world != 1 || w.blocks != 1 || w.off != 0) return;
-  if (mode == 0) return;  // auto: the graph (measured faster, see above)
-  if (w.G > kWsMaxGroups) return;
-  if (!m.wspsync) m.wspsync = dmalloc<int32_t>(8, &m.bytes);
-  w.psync = m.wspsync;
-  if (!launch::ws_persist_supported(w)) {
-    w.psync = nullptr;
-    return;
-  }
-  int cus = 0;
-  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, m.device));
-  const int per_cu = launch::ws_persist_blocks_per_cu(w);
-  bool ok = per_cu >= 1 && w.G <= cus;
-  int32_t h[4] = {0, 0, 0, 0};
-  if (ok) {
-    HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 32, m.stream));
-    w.xtimeout_ticks = (int64_t)(2.0 * 1e8);  // census: 2 s
-    launch::ws_persist_census(w, m.stream);
-    HIP_CHECK(hipMemcpyAsync(h, m.wspsync, 16, hipMemcpyDeviceToHost, m.stream));
-    HIP_CHECK(hipStreamSynchronize(m.stream));
-    ok = h[3] == 0 && h[2] == w.G;
-  }
-  HIP_CHECK(hipMemsetAsync(m.wspsync, 0, 32, m.stream));
-  if (!ok) {
-    m.info.engine_note += std::string(m.info.engine_note.empty() ? "" : "; ") + "ws persistent rounds: census " +
-                          std::to_string(h[2]) + "/" + std::to_string(w.G) + " workgroups co-resident (" +
-                          std::to_string(per_cu) + " per CU): graph rounds";
-    w.psync = nullptr;
-    return;
-  }
-  // a round boundary waits microseconds; 10 s means the grid lost residency
-  w.xtimeout_ticks = (int64_t)(10.0 * 1e8);
-  m.ws_persist = true;
-  m.info.ws_rounds = "persistent";
 }
 
 // ws-cache without the cache (ws_recompute.hip): with short rows (d <= 64
@@ -463,6 +414,23 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // ws-cache packs the misses' X rows and sums them over ranks each round —
   // no engine step after the Gram reads a non-owned X row)
   const int ws_q = std::max(2, std::min(m.p.ws_size, kWsMax));
+  // -s N: the reference takes any line count (default 10 lines,
+  // svmTrainMain.cpp:71; cache.cu:49-60, 82-105), a pure speed knob.  The
+  // production engines cap their lines at N; where the cap lies below the
+  // working-set cache's minimum (the round's 2 x ws_size rows + the victim
+  // window: production_line_cap, device_state.hpp) it is raised to that minimum, so a
+  // reference command line runs instead of failing.  engines=all keeps the
+  // count as given (the quarantined pair-at-a-time cache engines take any >= 2).
+  {
+    const int64_t cap = production_line_cap(m.p.cache_lines, ws_q, m.p.engines);
+    if (cap > m.p.cache_lines && want_lines < cap) {
+      want_lines = std::min<int64_t>(cap, (int64_t)(budget / line_bytes));
+      m.info.cache_note = "cache_lines " + std::to_string(m.p.cache_lines) + " raised to " +
+                          std::to_string(want_lines) + " (the working-set cache's minimum: 2 x ws_size + " +
+                          std::to_string(kWsCacheWindow) + " lines)";
+      if (m.outer_rank == 0) fprintf(stderr, "[dpsvm] note: %s\n", m.info.cache_note.c_str());
+    }
+  }
   // solver auto: the working-set engines from kWsAutoRows rows on (the pair-at-a-time
   // engines follow the reference's trajectory exactly and win on small problems;
   // on 500k-2M rows ws is 5-10x faster: profiles/r2_*_converged.json)
@@ -482,7 +450,8 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
   // only when loaded (engines=all): production setups never pick them
   const gpu::QuarantineOps* qo = gpu::quarantine();
   DPSVM_CHECK(m.p.engines == 0 || qo != nullptr,
-              "engines=all needs the quarantined pair-cache plugin (dpsvm_amd._native.load_quarantine())");
+              "engines=all needs the quarantined pair-cache plugin (Python: dpsvm_amd._native.load_quarantine(); CLI: "
+              "bin/svmTrainPairq)");
   const bool dp16 = m.dp >= 16 && m.dp % 16 == 0;  // the cache-mode X pass / row GEMM operand width
   const bool fused_lru_ok = !m.dense && m.replicated && qo && qo->fused_lru_supported(m.dp) && m.p.cache_engine == 0;
   // working-set engines: the resident Gram (ws-dense), or a kernel-row cache
@@ -949,7 +918,7 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
       HIP_CHECK(hipMemcpyAsync(m.wsiota, io.data(), io.size() * 4, hipMemcpyHostToDevice, m.stream));
       HIP_CHECK(hipStreamSynchronize(m.stream));
     }
-    ws_persist_setup(m);
+    m.info.ws_rounds = "graph";
     ws_recompute_setup(m);
   }
   m.engine = gpu::make_engine(m.kind);

@@ -89,8 +89,8 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   auto ts0 = Clock::now();
 
   if (!m.lines) {  // released (release_cache): the same L lines again, empty
-    size_t tb = 0;
-    m.lines = gpu::dmalloc<float>((size_t)m.L * m.ldl, &tb);
+    m.lines = gpu::dmalloc<float>((size_t)m.L * m.ldl, &m.bytes);
+    m.info.bytes_device = m.bytes;
     m.args.lines = m.lines;
     m.wsa.gram = m.lines;
   }
@@ -205,7 +205,8 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
         // (2 eps), for at most kShortRun single-round launches — a noisy drop on
         // a slowly converging problem costs that many, not the rest of the
         // solve in single rounds — then re-armed by the same test
-        constexpr int kShortRun = 32;
+        // a multiple of the launch size, so launches stay on the engines' span boundaries
+        const int kShortRun = (32 + B - 1) / B * B;
         const double gap = (double)st.b_lo - (double)st.b_hi, eps = (double)m.p.eps;
         if (near_left > 0) {
           --near_left;

@@ -113,16 +113,16 @@ class SVCConfig:
     ws_size: int = 192              # working-set rows (<= 192)
     ws_new: int = 0                 # rows replaced per one-block round (0: auto, ws_size from 128 padded features, else 3/4)
     ws_rel: float = 0.3             # sub-problem tolerance relative to the global gap (< 1)
-    # working-set engines: up to P sub-problems per round (1..32, P x ws_size <= 3072; 0 auto = 32 blocks of
-    # 96 rows from 50k rows, else 1); adaptive — halved
-    # after every damped round (coupled blocks), then the one-block round kernels (ws_*.hip)
+    # working-set engines: up to P sub-problems per round (1..128, P x ws_size <= 6144).  0 auto, from 50k rows:
+    # uncoupled (numerically diagonal) ws-dense kernels 128 blocks of 48 rows (6144-row union; 64 x 48 = 3072
+    # when ranks sharing one device would not leave room for the peer exchange's producers), coupled kernels
+    # and ws-cache 32 blocks of 96 (3072-row union); below 50k rows 1.  Adaptive —
+    # halved after every damped round (coupled blocks), then the one-block round kernels (ws_*.hip;
+    # kWsMaxBlocks / kWsMaxAll in include/dpsvm/device_state.hpp)
     ws_blocks: int = 0
     ws_inner: int = 0               # pair steps per round at most (0: 4 * ws_size)
     ws_wss: int = 0                 # sub-problem pair choice: 0 auto (second order on coupled kernels), 1 first, 2 second
     ws_block: int = 8               # rounds per hipGraph block (or per persistent-round launch)
-    # persistent one-block rounds (one launch per ws_block rounds, ws_persist.hip; one GPU, resident Gram):
-    # on | auto / off (a graph of launches per round: measured faster, profiles/r5_ws_persist_ab.txt)
-    ws_persist: str = "auto"
     # ws-cache rounds without the kernel-row cache (ws_recompute.hip: the round's kernel rows recomputed inside
     # the f update, the sub-Gram straight from X): auto (one GPU, one block, d <= 64) | on | off
     ws_recompute: str = "auto"
@@ -209,7 +209,6 @@ class SVCConfig:
         p.ws_t_halve = float(self.ws_t_halve)
         p.ws_clip_fallback = int(bool(self.ws_clip_fallback))
         p.ws_block = int(self.ws_block)
-        p.ws_persist = _pick({"auto": 0, "on": 1, "off": 2}, self.ws_persist, "ws_persist")
         p.ws_recompute = _pick({"auto": 0, "on": 1, "off": 2}, self.ws_recompute, "ws_recompute")
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         p.gram_precision = _pick({"auto": 0, "f32": 1, "split": 2}, self.gram, "gram")

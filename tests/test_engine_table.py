@@ -61,7 +61,8 @@ def test_quarantined_engines_are_a_plugin_not_the_production_module():
     """The production module carries no code of the quarantined pair-at-a-time
     cache / partitioned-X engines: their kernels and
     engine classes live in libdpsvm_pairq.so, which registers them when loaded
-    (engines="all"); the CLIs link them in."""
+    (engines="all"); of the CLIs only bin/svmTrainPairq and the native unit
+    tests link them in (hygiene)."""
     import subprocess
 
     from dpsvm_amd import build
@@ -72,6 +73,11 @@ def test_quarantined_engines_are_a_plugin_not_the_production_module():
         assert out.returncode == 0, out.stderr
         return out.stdout
 
+    def defined_all(path):  # executables: the static symbol table
+        out = subprocess.run(["nm", "--defined-only", "-C", str(path)], capture_output=True, text=True)
+        assert out.returncode == 0, out.stderr
+        return out.stdout
+
     prod = defined(build.module_path())
     for sym in ("smo_fused_lru_kernel", "smo_persist_lru_kernel", "smo_rows_kernel", "smo_finalize_kernel",
                 "launch::smo_fused_lru(", "launch::smo_persist_lru(", "launch::smo_rows("):
@@ -79,5 +85,30 @@ def test_quarantined_engines_are_a_plugin_not_the_production_module():
     plug = defined(build.plugin_path())
     for sym in ("launch::smo_fused_lru(", "launch::smo_persist_lru(", "launch::smo_rows("):
         assert sym in plug
+    for cli in ("svmTrain", "svmTest", "svmSeq"):
+        exe = os.path.join(ROOT, "bin", cli)
+        if os.path.exists(exe):
+            assert "smo_fused_lru_kernel" not in defined_all(exe), f"{cli} links the quarantined engines"
+    exe = os.path.join(ROOT, "bin", "svmTrainPairq")
+    if os.path.exists(exe):
+        assert "smo_fused_lru_kernel" in defined_all(exe)
     load_quarantine()
     assert C.quarantine_loaded()
+
+
+def test_reference_cache_size_floor_on_production_engines():
+    """-s N: the reference runs any line count (svmTrainMain.cpp:71, default 10).
+    The production engines raise a count below the working-set cache's minimum
+    (2 ws_size + 512 lines) to that minimum (the setup prints a note and records
+    it as setup_info_["cache_note"]); engines=all keeps it for the pair cache
+    engines; 0 (no cap) and counts above the minimum pass through."""
+    lo = C.ws_cache_min_lines(192)
+    assert lo == 2 * 192 + 512
+    assert C.production_line_cap(10, 192) == lo
+    assert C.production_line_cap(10, 48) == 2 * 48 + 512
+    assert C.production_line_cap(lo - 1, 192) == lo
+    assert C.production_line_cap(5000, 192) == 5000
+    assert C.production_line_cap(0, 192) == 0
+    assert C.production_line_cap(10, 192, engines=1) == 10
+    with open(os.path.join(ROOT, "README.md")) as fh:
+        assert "2 x ws_size + 512" in fh.read()  # the deviation list states the rule

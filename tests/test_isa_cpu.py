@@ -25,7 +25,6 @@ SPILL_FREE = [
     "kernels/ws_select.hip",
     "kernels/ws_merge.hip",
     "kernels/ws_solve.hip",
-    "kernels/ws_persist.hip",
     "kernels/ws_recompute.hip",
     "kernels/smo_persist.hip",
     "kernels/compact.hip",

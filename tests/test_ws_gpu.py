@@ -7,12 +7,16 @@ engines; what must agree is the optimum it stops at: the reference's stop test
 intercept, the support set and the decision function — checked here against
 the float64 numpy model of the reference (tests/ref_smo.py) and against the
 persistent SMO engine."""
+import os
+
 import numpy as np
 import pytest
 import torch
 
 from dpsvm_amd import SVC
 from dpsvm_amd.utils.datasets import synthetic
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -128,17 +132,46 @@ def test_ws_cache_engine_bit_identical_to_resident_gram(case):
     assert cache.stats_["rows_computed"] > lines  # more rows than lines: evictions happened
 
 
-def test_ws_cache_engine_small_cache_refused_cleanly():
-    """A cache below ws-cache's 2 q + 512 lines: the production engines refuse
-    it with the reason; engines=all falls back to the (quarantined) pair cache
-    engines."""
+def test_ws_cache_engine_small_cache_raised_to_its_minimum():
+    """A cache below ws-cache's 2 q + 512 lines (the reference's -s N takes any
+    count, svmTrainMain.cpp:71): the production engines raise it to that
+    minimum with a note and run; engines=all keeps the count for the
+    (quarantined) pair cache engines."""
     X, y = synthetic("adult", n=3000, seed=1)
     kw = dict(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300)
-    with pytest.raises(Exception, match="ws-cache needs .*engines=all"):
-        SVC(**kw).fit(X, y)
-    s = SVC(engines="all", **kw).fit(X, y)
-    assert s.setup_info_["iteration"] in ("persistent-cache", "fused-cache")
-    assert "ws-cache needs" in s.setup_info_["engine_note"]
+    s = SVC(**kw).fit(X, y)
+    assert s.setup_info_["iteration"] == "ws-cache" and s.converged_
+    assert s.setup_info_["cache_lines"] == 2 * 192 + 512
+    assert "raised to 896" in s.setup_info_["cache_note"]
+    p = SVC(engines="all", **kw).fit(X, y)
+    assert p.setup_info_["iteration"] in ("persistent-cache", "fused-cache")
+    assert p.setup_info_["cache_lines"] == 300 and p.setup_info_["cache_note"] == ""
+    assert "ws-cache needs" in p.setup_info_["engine_note"]
+    assert abs(p.b_ - s.b_) < 2e-2
+
+
+def test_cli_reference_cache_size_10_lines_production_engines():
+    """svmTrain -s 10 (the reference's default cache: 10 kernel-row lines) on a
+    50k-row problem whose Gram is therefore not resident: the production
+    engines run it (ws-cache at its minimum line count, with a note on stderr)
+    to convergence."""
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(ROOT, "bin", "svmTrain")
+    if not os.path.exists(exe):
+        pytest.skip("bin/svmTrain not built")
+    with tempfile.TemporaryDirectory() as td:
+        model = os.path.join(td, "m.txt")
+        cmd = [exe, "-a", "32", "-x", "50000", "--synthetic", "blobs", "--seed", "5", "-c", "1", "-g", "0.05",
+               "-e", "0.001", "-s", "10", "-m", model, "--metrics-json", os.path.join(td, "m.json")]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        assert "cache_lines 10 raised to 896" in r.stderr
+        assert "Converged at iteration number" in r.stdout, r.stdout[-2000:]
+        import json
+        mj = json.load(open(os.path.join(td, "m.json")))
+        assert mj["engine"] == "ws-cache" and mj["cache_lines"] == 896 and "raised to 896" in mj["cache_note"], mj
 
 
 def test_production_engines_route_small_cache_problems_to_ws():
