@@ -359,6 +359,7 @@ def main(argv=None) -> int:
     shard_check = None
     dp_choice = None
     s_solver = s_comm = None
+    s_info = None
     if on_gpu and n_ranks > 1 and info.get("dp_policy") == "replicate" and a.shard_check == "auto":
         # the replicated policy (every rank solves it all) was chosen from the
         # problem's shape; prove the sharded, cross-device path on this node too
@@ -475,6 +476,26 @@ def main(argv=None) -> int:
                      "train_accuracy": float(sp_solver.train_accuracy(s_alpha, sres["b"]))}
         del sp_solver
 
+    def rank_diag(inf):
+        """this rank's setup as the timed solver ran it (N > 1: gathered to rank 0)"""
+        if not isinstance(inf, dict):
+            return None
+        return {"rank": ctx.rank, "device": inf.get("device"), "comm": inf.get("comm_kind"),
+                "n_local": inf.get("n_local"), "dp_policy": inf.get("dp_policy"), "engine": inf.get("iteration"),
+                "exchange": inf.get("exchange"), "ws_exchange": inf.get("ws_exchange"),
+                "exchange_mem": inf.get("exchange_mem"), "xch_selftest": inf.get("xch_selftest", ""),
+                "union": f"{inf.get('ws_blocks', 0)}x{inf.get('ws_q_max', 0)}",
+                "bytes_device": inf.get("bytes_device"), "engine_note": inf.get("engine_note", "")}
+
+    rank_setup = None
+    if n_ranks > 1:
+        # per-rank setup diagnostics (exchange self test, uncached receive buffer,
+        # union, communicator): a first multi-GPU failure is readable from the line
+        rank_setup = [None] * n_ranks
+        from dpsvm_amd.parallel.dist import _host_group
+
+        dist.all_gather_object(rank_setup, {"timed": rank_diag(info), "shard_check": rank_diag(s_info)},
+                               group=_host_group())
     policy = info.get("dp_policy", "shard")
     if n_ranks > 1 and dp_choice is None:
         # always both data-parallel policies' times at N > 1 where measured: the
@@ -557,6 +578,7 @@ def main(argv=None) -> int:
                        "phase_log": res.get("phase_log", "")},
             "shard_check": shard_check,
             "dp_autotune": dp_choice,
+            "rank_setup": rank_setup,
             "reference_check": ref_check,
             "secondary": secondary,
             "ws_rounds": info.get("ws_rounds", "none"),

@@ -82,6 +82,9 @@ struct GpuSetupInfo {
   int ws_wss = 0;                     // working-set engines: sub-problem pair choice (1 first, 2 second order)
   std::string ws_rounds = "none";     // working-set engines: "graph" (launches per round) or "persistent"
   std::string ws_rows = "none";       // ws engines' kernel rows: "gram" (resident), "cache" (row cache), "recompute"
+  std::string xch_selftest;            // peer exchange setup self test: "rank r: mapped=1 ping=1" or why refused
+  std::string comm_kind;               // communicator backend: local | rccl | thread | callback
+  int ws_blocks = 0, ws_q_max = 0;     // working-set rounds: blocks per round x rows per block (the union)
   std::string gram = "f32";           // Gram / kernel-row GEMM arithmetic: "f32" or "split-f16" (rbf_gemm_split.hip)
 };
 
@@ -176,6 +179,8 @@ class GpuPredictor {
 // Low-level kernel entry points exposed for unit tests (device pointers).
 namespace kernels {
 void row_sqnorm(const float* x, int64_t n, int d, int ld, float* out, void* stream);
+// known-bytes 16-B streaming read (FETCH_SIZE probe, bench/fetch_probe.py)
+void stream_read(const void* x, int64_t bytes, float* out, int blocks, void* stream);
 // K[q][j] = exp(-gamma * max(|x_j|^2 + |w_q|^2 - 2 x_j.w_q, 0)) for q < nq <= 16
 void rbf_rows(const float* x, const float* xsq, int64_t n, int ld, const float* w, const float* wsq,
               int nq, float gamma, float* out, int64_t out_ld, void* stream);

@@ -170,5 +170,7 @@ namespace dpsvm {
 namespace launch {
 // microsecond cost per kernel of a graph-replayed chain of dependent empty kernels
 double launch_floor_us(int blocks, int threads, int chain, int reps);
+// known-bytes 16-B streaming read (FETCH_SIZE probe); out[blocks] per-workgroup sums
+void stream_read(const void* x, int64_t bytes, float* out, int blocks, hipStream_t s);
 }  // namespace launch
 }  // namespace dpsvm

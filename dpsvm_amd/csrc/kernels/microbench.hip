@@ -7,6 +7,7 @@
 #include <chrono>
 
 #include "../runtime/hip_check.hpp"
+#include "device_util.hpp"
 #include "kernels.hpp"
 
 namespace dpsvm {
@@ -18,9 +19,39 @@ __global__ void chain_kernel(const int* __restrict__ in, int* __restrict__ out) 
   if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = v + 1;
 }
 
+// Known-bytes stream for pinning FETCH_SIZE (bench/fetch_probe.py): every 16-B
+// chunk of x read exactly once by 16-B loads (full 128-B lines per 8 lanes, the
+// access shape of the wide pass 1 and of the GEMMs' LDS-DMA), four loads in
+// flight per lane, a per-workgroup sum written so nothing is dead code.
+__global__ __launch_bounds__(256) void stream_read_kernel(const float4* __restrict__ x, int64_t n16,
+                                                          float* __restrict__ out) {
+  float acc = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const float4 a = x[i], b = x[i + stride], c = x[i + 2 * stride], d = x[i + 3 * stride];
+    acc += (a.x + a.y + a.z + a.w) + (b.x + b.y + b.z + b.w) + (c.x + c.y + c.z + c.w) + (d.x + d.y + d.z + d.w);
+  }
+  for (; i < n16; i += stride) {
+    const float4 a = x[i];
+    acc += a.x + a.y + a.z + a.w;
+  }
+  acc = wave_sum(acc);
+  __shared__ float s_w[4];
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
 }  // namespace dev
 
 namespace launch {
+
+void stream_read(const void* x, int64_t bytes, float* out, int blocks, hipStream_t s) {
+  DPSVM_CHECK(bytes % 16 == 0 && ((uintptr_t)x & 15) == 0, "stream_read: 16-B aligned whole chunks");
+  dev::stream_read_kernel<<<dim3((unsigned)blocks), 256, 0, s>>>((const float4*)x, bytes / 16, out);
+  post_launch("stream_read", s);
+}
 
 double launch_floor_us(int blocks, int threads, int chain, int reps) {
   hipStream_t s;

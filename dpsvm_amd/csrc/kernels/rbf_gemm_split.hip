@@ -821,7 +821,10 @@ constexpr int kW64Threads = 512;
 // tiles: nullptr = the whole tm x tn grid in the XCD order; else a compact
 // table of the tiles to compute (the symmetric Gram's upper tiles, host-built
 // in the XCD order: no workgroup is launched only to exit)
-template <int NT>
+// SP 1: the next-but-one block's six LDS-DMA pieces are issued one after each
+// group of four MFMAs instead of all six right after the k-block barrier (all
+// eight waves then stall on the load path at once while the MFMA pipe idles)
+template <int NT, int SP = 0>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
@@ -864,12 +867,14 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     base[i] = g < TM ? A + (m0 + g) * rstride : B + (n0 + (g - TM)) * rstride;
     off[i] = (uint32_t)((lane >> 3) * rstride + c);
   }
-  auto dma = [&](int kb) {
+  auto dma_piece = [&](int kb, int i) {
     u4* dst = lds + (kb % NB) * BUF + 48 * wave * CPR;
+    __builtin_amdgcn_global_load_lds((const void*)(base[i] + (int64_t)kb * 8 + off[i]),
+                                     (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+  };
+  auto dma = [&](int kb) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(base[i] + (int64_t)kb * 8 + off[i]),
-                                       (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+    for (int i = 0; i < 6; ++i) dma_piece(kb, i);
   };
   __syncthreads();  // row data written (no DMA in flight yet)
   dma(0);
@@ -892,7 +897,16 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kb + 2 < nkb) dma(kb + 2);  // into the buffer of block kb - 1 (every wave is past it)
+    // block kb + 2 goes into the buffer of block kb - 1 (every wave is past it)
+    if (SP == 0 && kb + 2 < nkb) dma(kb + 2);
+    const bool spread = SP != 0 && kb + 2 < nkb;  // uniform
+    auto piece = [&](int i) {
+      if (spread) {
+        __builtin_amdgcn_sched_barrier(0);
+        dma_piece(kb + 2, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
     const u4* buf = lds + (kb % NB) * BUF;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -907,18 +921,21 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
       H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
       H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
       H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
+      piece(3 * ks);
       const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
       const h8 bl1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + cl]);
       P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
       P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
       P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
       P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(3 * ks + 1);
       const h8 al0 = __builtin_bit_cast(h8, buf[ra0 + cl]);
       const h8 al1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + cl]);
       Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
       Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
       Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
       Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
+      piece(3 * ks + 2);
     }
   }
 
@@ -1498,14 +1515,23 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   // (32-bit store offsets inside a 256 x 128 tile: ldo < 2^24)
-  if ((variant == 5 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 && ldo < (1ll << 24)) {
+  if ((variant == 5 || variant == 6 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 && ldo < (1ll << 24)) {
     static const int nt = [] {
       const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
       return e ? atoi(e) : 0;
     }();
     const int64_t tm2 = (M + 255) / 256;
+    // the LDS-DMA issue spread over the MFMA groups (default): 9.41 -> 9.27 ms
+    // symmetric, 2.65 -> 2.56 ms for the P = 8 slab, bit-identical
+    // (profiles/r6_gram_dma_spread_ab.json; A/B: DPSVM_GRAM_SPREAD=0 or variant 5 vs 6)
+    static const int spread = [] {
+      const char* e = std::getenv("DPSVM_GRAM_SPREAD");
+      return e ? atoi(e) : 1;
+    }();
     auto kern = nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
-                : nt ? dev::rbf_gemm_split_w64_kernel<1> : dev::rbf_gemm_split_w64_kernel<0>;
+                : nt ? dev::rbf_gemm_split_w64_kernel<1>
+                : ((spread && variant != 5) || variant == 6) ? dev::rbf_gemm_split_w64_kernel<0, 1>
+                                                              : dev::rbf_gemm_split_w64_kernel<0>;
     static const bool compact = [] {  // A/B: DPSVM_GRAM_COMPACT=0 launches the full grid (half exit at once)
       const char* e = std::getenv("DPSVM_GRAM_COMPACT");
       return !(e && e[0] == '0');

@@ -160,6 +160,10 @@ py::dict setup_dict(const GpuSetupInfo& i) {
   d["ws_rounds"] = i.ws_rounds;
   d["ws_rows"] = i.ws_rows;
   d["gram"] = i.gram;
+  d["xch_selftest"] = i.xch_selftest;
+  d["comm_kind"] = i.comm_kind;
+  d["ws_blocks"] = i.ws_blocks;
+  d["ws_q_max"] = i.ws_q_max;
   return d;
 }
 
@@ -654,6 +658,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("shard_of", [](int64_t n, int rank, int world) {
     Shard s = shard_of(n, rank, world);
     return py::make_tuple(s.offset, s.size);
+  });
+  m.def("k_stream_read", [](uintptr_t x, int64_t bytes, uintptr_t out, int blocks, uintptr_t stream) {
+    kernels::stream_read((const void*)x, bytes, (float*)out, blocks, (void*)stream);
   });
   m.def("launch_floor_us", &launch::launch_floor_us, py::arg("blocks") = 256, py::arg("threads") = 256,
         py::arg("chain") = 64, py::arg("reps") = 50, py::call_guard<py::gil_scoped_release>());

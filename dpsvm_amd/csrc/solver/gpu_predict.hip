@@ -310,6 +310,10 @@ void row_sqnorm(const float* x, int64_t n, int d, int ld, float* out, void* stre
   launch::row_sqnorm(x, n, d, ld, out, (hipStream_t)stream);
 }
 
+void stream_read(const void* x, int64_t bytes, float* out, int blocks, void* stream) {
+  launch::stream_read(x, bytes, out, blocks, (hipStream_t)stream);
+}
+
 void rbf_rows(const float* x, const float* xsq, int64_t n, int ld, const float* w, const float* wsq, int nq,
               float gamma, float* out, int64_t out_ld, void* stream) {
   DPSVM_CHECK(nq >= 1 && nq <= kNQ, "rbf_rows: 1 <= nq <= 16");

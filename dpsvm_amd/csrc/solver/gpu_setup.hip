@@ -640,13 +640,16 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     HIP_CHECK(hipDeviceGetAttribute(&xch_cus, hipDeviceAttributeMultiprocessorCount, m.device));
   }
   auto xch_waves = [&](int blocks) { return (int64_t)xch_share * (64 + 16 * std::max(1, blocks)) + 1024; };
-  // a wide auto union whose 128 spinning solve workgroups per rank would not
-  // leave the ranks sharing a device room for their producers: the
-  // kWsAutoUnion union instead (4 ranks on one GPU: 64 blocks over the peer
-  // exchange rather than one block per round over host collectives)
-  if (m.world > 1 && blocks_auto && want_blocks * mb_q > kWsAutoUnion &&
-      !m.all_agree(xch_waves(want_blocks) <= (int64_t)xch_cus * 32, m.comm, m.world))
-    want_blocks = kWsAutoUnion / mb_q;
+  // an auto union whose spinning solve workgroups (one per block, every rank)
+  // would not leave the ranks sharing a device room for their producers: halve
+  // the block count until they fit (4 ranks on one GPU: 64 blocks, 8 ranks: 32,
+  // over the peer exchange, rather than one block per round over host
+  // collectives).  Distinct devices (share 1) always fit 128 blocks.
+  // (collectives — exchange=allreduce, force_collectives — spin on nothing: the wide union stays)
+  if (m.world > 1 && blocks_auto && want_blocks > 1 && m.p.exchange != 1 && !m.p.force_collectives) {
+    while (want_blocks > 8 && !m.all_agree(xch_waves(want_blocks) <= (int64_t)xch_cus * 32, m.comm, m.world))
+      want_blocks /= 2;
+  }
   // (only where working-set rounds can run: solver=smo or a small problem ignores ws_blocks)
   DPSVM_CHECK(!(ws_cand || wsc_cand) || want_blocks <= 1 || want_blocks * mb_q <= kWsMaxAll,
               "ws_blocks x ws_size must be <= " + std::to_string(kWsMaxAll) + " (the round's union capacity)");
@@ -932,6 +935,12 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     // partitioned X in cache mode also sums each round's packed miss rows
     if (m.wsa.xpeer && m.ws_round_collectives()) m.info.ws_exchange += "+rows-allreduce";
   }
+  if (m.working_set()) {
+    m.info.ws_blocks = m.wsa.blocks;
+    m.info.ws_q_max = m.wsa.q_max;
+  }
+  m.info.xch_selftest = m.xch_diag;
+  m.info.comm_kind = m.comm ? m.comm->name() : "local";
   m.info.rows_per_group = m.working_set() ? (int64_t)m.wsa.rpt * kWsSelThreads : m.fused() ? m.RBf : kStepRows;
   m.info.groups = m.working_set() ? m.wsa.G : m.fused() ? m.Gf : m.G;
   m.info.poll_batch = m.xch && !m.working_set() ? launch::poll_batch(a) : 0;

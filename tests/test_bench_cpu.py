@@ -48,6 +48,10 @@ def test_bench_multirank_launch_contract():
     assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4-shard" and out["converged"]
     assert out["dp_autotune"]["shard_s"] == out["value"] and out["dp_autotune"]["chosen"] == "shard"
     assert out["steps"] == 1 and out["warmup"] == 1 and out["value"] > 0
+    # per-rank setup diagnostics at N > 1 (exchange self test, union, communicator)
+    assert [d["timed"]["rank"] for d in out["rank_setup"]] == [0, 1, 2, 3]
+    for d in out["rank_setup"]:
+        assert {"comm", "exchange", "xch_selftest", "union", "n_local"} <= set(d["timed"])
 
 
 def test_bench_spawns_its_own_ranks():

@@ -138,7 +138,8 @@ def test_ws_cache_engine_small_cache_raised_to_its_minimum():
     minimum with a note and run; engines=all keeps the count for the
     (quarantined) pair cache engines."""
     X, y = synthetic("adult", n=3000, seed=1)
-    kw = dict(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300)
+    # box clipping: one optimum for both engine families (independent clipping's depends on the trajectory)
+    kw = dict(C=1.0, gamma=0.05, device="cuda", solver="ws", force_cache=True, cache_lines=300, clip="box")
     s = SVC(**kw).fit(X, y)
     assert s.setup_info_["iteration"] == "ws-cache" and s.converged_
     assert s.setup_info_["cache_lines"] == 2 * 192 + 512
@@ -642,6 +643,40 @@ def test_ws_multi_block_sharded_ranks(world):
     assert _kkt_gap(X, y, out[0].alpha_, 1.0, 0.05) < 2.2e-3
     assert abs(out[0].b_ - ref.b_) < 1e-2
     assert abs(out[0].n_support_ - ref.n_support_) <= max(3, ref.n_support_ // 50)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_ws_wide_union_sharded_thread_ranks_host_collectives(world):
+    """The default 8-GPU path's round shape, rehearsed with thread ranks over
+    host collectives: mnist-shape rows sharded over
+    4 / 8 ranks in rounds of 128 blocks of 48 rows (a 6,144-row union: what
+    ws_blocks auto picks from 50k rows on numerically diagonal data at every
+    rank count), candidate lists / sub-Grams / line-search partials through the
+    communicator each round.  Every rank converges with the same alphas.  The
+    trajectory is not the one-rank one bit for bit: the line search's double
+    partial sums are reduced per 1,024-column group of each rank's shard, so
+    their rounding depends on the partition (4 and 8 ranks land within 1e-8 of
+    each other in b, 2.4e-4 from one rank) — both stop inside the same
+    2 eps band, with the same support set and decision signs."""
+    from dpsvm_amd._native import load
+
+    X, y = synthetic("mnist", n=16000, seed=21)
+    kw = dict(C=10.0, gamma=0.25, eps=1e-3, device="cuda", solver="ws", ws_blocks=128, ws_size=48)
+    ref = SVC(**kw).fit(X, y)
+    assert ref.setup_info_["iteration"] == "ws-dense" and ref.converged_
+    assert ref.stats_["ws_blocks"] == 128, ref.stats_
+    out = _fit_threads(load(), world, X, y, exchange="allreduce", dp="shard", **kw)
+    for r in range(world):
+        assert out[r].setup_info_["iteration"] == "ws-dense" and out[r].setup_info_["n_local"] <= 16000 // world + 1
+        assert out[r].setup_info_["exchange"] == "allreduce"
+        assert out[r].stats_["ws_blocks"] == 128, out[r].stats_  # the 6,144-row union at every rank count
+        assert out[r].converged_
+        assert np.array_equal(out[r].alpha_, out[0].alpha_)
+    assert abs(out[0].b_ - ref.b_) < 1e-3, (out[0].b_, ref.b_)  # eps: inside the stop band
+    assert out[0].n_support_ == ref.n_support_
+    d_ref = ref.decision_function(X[:4000])
+    d_out = out[0].decision_function(X[:4000])
+    assert np.mean(np.sign(d_ref) == np.sign(d_out)) > 0.999
 
 
 def test_ws_multi_block_rccl_one_rank_collective_path():
