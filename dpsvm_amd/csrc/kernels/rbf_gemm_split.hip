@@ -817,7 +817,10 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 // ---------------------------------------------------------------------------
 constexpr int kW64Threads = 512;
 // NT 1: non-temporal Gram stores (measured slower, profiles/r4_gram_nt_store_ab.txt);
-// NT 2: diagnostics only — stores skipped unless a value is NaN (the store-free time)
+// NT 2: diagnostics only — stores skipped unless a value is NaN (the store-free time);
+// NT 3: diagnostics only — plain stores plus per-workgroup s_memtime stamps
+// (entry, first k block landed, k loop done, stores issued, stores done) and
+// s_memrealtime at entry / end into stamps[8 blockIdx.x ..] (bench/gram_stamps.py)
 // tiles: nullptr = the whole tm x tn grid in the XCD order; else a compact
 // table of the tiles to compute (the symmetric Gram's upper tiles, host-built
 // in the XCD order: no workgroup is launched only to exit)
@@ -828,8 +831,14 @@ template <int NT, int SP = 0>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
-    float gamma, float* __restrict__ out, int64_t ldo, int sym, const uint32_t* __restrict__ tiles) {
+    float gamma, float* __restrict__ out, int64_t ldo, int sym, const uint32_t* __restrict__ tiles,
+    uint64_t* __restrict__ stamps) {
   constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
+  uint64_t st[5] = {0, 0, 0, 0, 0}, rt0 = 0;
+  if constexpr (NT == 3) {
+    st[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   int64_t tx, ty;
   if (tiles) {
     const uint32_t t = tiles[blockIdx.x];  // (tx << 16) | ty
@@ -897,6 +906,9 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (NT == 3) {
+      if (kb == 0) st[1] = __builtin_amdgcn_s_memtime();
+    }
     // block kb + 2 goes into the buffer of block kb - 1 (every wave is past it)
     if (SP == 0 && kb + 2 < nkb) dma(kb + 2);
     const bool spread = SP != 0 && kb + 2 < nkb;  // uniform
@@ -939,6 +951,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     }
   }
 
+  if constexpr (NT == 3) st[2] = __builtin_amdgcn_s_memtime();
   // ---- epilogue, one 32 x 32 MFMA tile at a time: values, direct stores,
   // transposed stores.  ONE code path for interior and edge tiles: a second,
   // interior-only copy (round 4) made the compiler spill 396 B of the live
@@ -1001,7 +1014,282 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
       }
     }
   }
+  if constexpr (NT == 3) {
+    st[3] = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[4] = __builtin_amdgcn_s_memtime();
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      uint64_t* o = stamps + (size_t)blockIdx.x * 8;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] = st[i];
+      o[5] = rt0;
+      o[6] = rt1;
+      o[7] = ((uint64_t)tx << 32) | (uint64_t)ty;
+    }
+  }
 }
+
+// ---------------------------------------------------------------------------
+// Persistent wide-wave STORE GEMM (the default from round 6): the w64 kernel's
+// tile, k loop and epilogue, one workgroup per CU walking tiles L = b, b + G,
+// ... of the same table.  In-kernel stamps of the w64 kernel (NT 3,
+// profiles/r6_gram_stamps.json) put 11% of a tile in its prologue (row data,
+// then the first LDS-DMA block's latency) and 14% in the epilogue, with the
+// MFMA pipe idle in both.  Here the LDS-DMA ring runs on across tiles: during
+// the last two k blocks of tile t the prefetch slots load blocks 0 and 1 of
+// tile t + 1 (a block counter g over all tiles picks the buffer, g mod 3), and
+// the next tile's |x|^2 and shifts arrive by LDS-DMA into the other parity of
+// a row-data area (issued at tile t's first block), so tile t + 1 starts with
+// its first blocks landed.  The
+// epilogue's stores are younger than those DMAs: the next tile's first k
+// block waits vmcnt(0) (they drain in ~1k cycles, measured).  Same MFMA
+// sequence per output: bit-identical to the w64 kernel.
+// NT 3: per-tile stamps (first wait, first block landed, k loop done, stores
+// issued) and s_memrealtime at the tile's start / end into stamps[8 L ..].
+// ---------------------------------------------------------------------------
+// LDS-DMA piece i of k block kb of the tile at (m0, n0) into ring buffer buf:
+// wave w fills stage rows 48 w + 8 i + (lane >> 3), lane position p = lane & 7
+// taking global chunk p ^ ((row >> 1) & 7) (the w64 kernel's geometry)
+__device__ __forceinline__ void w64p_dma_piece(const u4* __restrict__ A, const u4* __restrict__ B, u4* lds,
+                                               uint32_t rs, int wave, int lane, int m0, int n0, int kb, int buf,
+                                               int i) {
+  constexpr int TM = 256, BUF = 384 * 8;
+  const int g = __builtin_amdgcn_readfirstlane(48 * wave + 8 * i);  // first row of the group (uniform)
+  const int r = g + (lane >> 3);
+  const uint32_t off = (uint32_t)(lane >> 3) * rs + (uint32_t)((lane & 7) ^ ((r >> 1) & 7));
+  const u4* base = g < TM ? A : B;
+  const uint32_t row = g < TM ? (uint32_t)(m0 + g) : (uint32_t)(n0 + g - TM);
+  u4* dst = lds + buf * BUF + 48 * wave * 8 + 8 * i * 8;
+  __builtin_amdgcn_global_load_lds((const void*)(base + (row * rs + (uint32_t)kb * 8 + off)),
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// a tile's |x|^2 and shifts into row-data parity par: dwords d = 64 (2 wave +
+// i) + lane (two 4-B LDS-DMA instructions a wave, every wave: a uniform count
+// for the waits; ROWS = 384 and TM = 256 are multiples of 64, so the array an
+// instruction reads is wave-uniform); rows past M / N clamp as the w64 kernel's
+// loads do
+__device__ __forceinline__ void w64p_row_dma(const float* __restrict__ Asq, const float* __restrict__ Bsq,
+                                             const int32_t* __restrict__ Ash, const int32_t* __restrict__ Bsh, int M,
+                                             int N, uint32_t* s_rows, int wave, int lane, int m0, int n0, int par) {
+  constexpr int TM = 256, ROWS = 384, RD = 1024;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d0 = __builtin_amdgcn_readfirstlane(64 * (2 * wave + i));
+    const int r0 = d0 < ROWS ? d0 : d0 - ROWS;    // uniform
+    const bool a_rows = r0 < TM, sq = d0 < ROWS;  // uniform
+    const uint32_t* arr = sq ? (a_rows ? (const uint32_t*)Asq : (const uint32_t*)Bsq)
+                             : (a_rows ? (const uint32_t*)Ash : (const uint32_t*)Bsh);
+    const int r = r0 + lane;
+    const int ri = a_rows ? min(m0 + r, M - 1) : min(n0 + (r - TM), N - 1);
+    const uint32_t* src = d0 >= 2 * ROWS ? arr : arr + ri;  // padding: any valid address
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(s_rows + par * RD + d0),
+                                     4, 0, 0);
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int M,
+    const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int N, int nkb,
+    float gamma, float* __restrict__ out, int ldo, int sym, const uint32_t* __restrict__ tiles, int ntiles,
+    int tm, int tn, uint64_t* __restrict__ stamps) {
+  // 32-bit indices throughout (launcher: M, N, ldo and (M + 512) x nkb x 8 < 2^31):
+  // the loop-carried tile state must fit the scalar registers beside the
+  // k loop's, or the 192 accumulators spill
+  constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
+  constexpr int RD = 1024;  // row-data dwords per parity: |x|^2 [ROWS], shifts [ROWS], DMA padding
+  __shared__ u4 lds[NB * BUF + 2 * RD / 4];  // 3 operand buffers, then row data [2][RD]
+  uint32_t* const s_rows = (uint32_t*)(lds + NB * BUF);
+  const int G = gridDim.x;
+  int L = blockIdx.x;
+  if (L >= ntiles) return;  // uniform: no barrier reached
+  uint32_t t = tiles[L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const uint32_t rs = (uint32_t)nkb * 8;  // u4 per split row
+  // the per-lane DMA offsets are recomputed per piece (a few VALU ops) rather
+  // than held in six registers across the loop (w64p_dma_piece)
+#define DMA_PIECE(m0_, n0_, kb_, buf_, i_) w64p_dma_piece(A, B, lds, rs, wave, lane, m0_, n0_, kb_, buf_, i_)
+#define ROW_DMA(m0_, n0_, par_) w64p_row_dma(Asq, Bsq, Ash, Bsh, M, N, s_rows, wave, lane, m0_, n0_, par_)
+  int Ln = L + G;
+  uint32_t tn_next = Ln < ntiles ? tiles[Ln] : 0u;
+  int par = 0;
+  uint32_t g = 0;  // k blocks started over all of this workgroup's tiles: ring buffer g % NB
+  {
+    const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
+    ROW_DMA(m0, n0, 0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) DMA_PIECE(m0, n0, 0, 0, i);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) DMA_PIECE(m0, n0, 1, 1, i);  // launcher: nkb >= 3
+  }
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra0 = (wm * 64 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
+  while (true) {
+    uint64_t st[4] = {0, 0, 0, 0}, rt0 = 0;
+    if constexpr (NT == 3) {
+      st[0] = __builtin_amdgcn_s_memtime();
+      rt0 = __builtin_amdgcn_s_memrealtime();
+    }
+    const bool has_next = Ln < ntiles;  // uniform
+    const int tx = (int)(t >> 16), ty = (int)(t & 0xffffu);
+    const int m0 = tx * TM, n0 = ty * TN;
+    const int nm0 = (int)(tn_next >> 16) * TM, nn0 = (int)(tn_next & 0xffffu) * TN;
+    f16v H[2][2], P[2][2], Q[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) H[i][j][r] = P[i][j][r] = Q[i][j][r] = 0.f;
+#pragma clang loop unroll(disable)
+    for (int kb = 0; kb < nkb; ++kb) {
+      // retire block kb's DMA: at a tile's first block everything (the previous
+      // epilogue's stores are younger than this tile's first blocks); in the
+      // last block the next tile's block 0 and row data (8 a wave) may stay in flight
+      if (kb == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (kb == 1 && has_next) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // + the next row data
+      else if (kb + 1 < nkb || has_next) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if constexpr (NT == 3) {
+        if (kb == 0) st[1] = __builtin_amdgcn_s_memtime();
+      }
+      // the next tile's row data into the other parity (last read by the
+      // previous tile's epilogue, before this barrier), ahead of block 2's DMA
+      if (kb == 0 && has_next) ROW_DMA(nm0, nn0, par ^ 1);
+      // the prefetch slot: block kb + 2 of this tile, or block kb + 2 - nkb of
+      // the next one, into the buffer of block g - 1 (every wave is past it)
+      const bool own = kb + 2 < nkb;
+      const bool pf = own || has_next;  // uniform
+      const int pkb = own ? kb + 2 : kb + 2 - nkb;
+      const int pm0 = own ? m0 : nm0, pn0 = own ? n0 : nn0;
+      const int pbuf = (int)((g + 2) % NB);
+      auto piece = [&](int i) {
+        if (pf) {
+          __builtin_amdgcn_sched_barrier(0);
+          DMA_PIECE(pm0, pn0, pkb, pbuf, i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      const u4* buf = lds + (g % NB) * BUF;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+        const h8 ah0 = __builtin_bit_cast(h8, buf[ra0 + ch]);
+        const h8 ah1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + ch]);
+        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
+        const h8 bh1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + ch]);
+        H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
+        H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
+        H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
+        H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
+        piece(3 * ks);
+        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
+        const h8 bl1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + cl]);
+        P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+        P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+        P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+        P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+        piece(3 * ks + 1);
+        const h8 al0 = __builtin_bit_cast(h8, buf[ra0 + cl]);
+        const h8 al1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + cl]);
+        Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
+        Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
+        Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
+        Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
+        piece(3 * ks + 2);
+      }
+      ++g;
+    }
+    if constexpr (NT == 3) st[2] = __builtin_amdgcn_s_memtime();
+
+    // ---- epilogue of the w64 kernel (row data from parity `par`) ----
+    // (the per-lane epilogue addresses are recomputed per tile from a
+    // laundered lane id: hoisted out of the tile loop they would hold ~64
+    // registers across the k loop)
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int ewn = wn, ewm = wm, ehl = el >> 5;
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const float* s_sq = (const float*)(s_rows + par * RD);
+    const int32_t* s_sh = (const int32_t*)(s_rows + par * RD + ROWS);
+    const bool mirror = sym && ty > 2 * tx + (ewm >> 1);
+    float* const ob = out + ((uint32_t)m0 * (uint32_t)ldo + (uint32_t)n0);
+    float* const mb = out + ((uint32_t)n0 * (uint32_t)ldo + (uint32_t)m0);
+    const uint32_t ld = (uint32_t)ldo;
+    const int rlim = min(M - m0, TM);
+    const int clim = min(N - n0, TN);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = ewn * 64 + 32 * j + (el & 31);
+      const bool okc = cl < clim;
+      const float bsq = s_sq[TM + cl];
+      const int bsh = s_sh[TM + cl];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int lr0 = ewm * 64 + 32 * i + 4 * ehl;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const f4 asq = *(const f4*)(s_sq + lr0 + 8 * q4);
+          const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * q4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * q4 + e, lr = lr0 + 8 * q4 + e;
+            const float dot = ldexpf(H[i][j][r] + (P[i][j][r] + Q[i][j][r]), -(ash[e] + bsh));
+            H[i][j][r] = rbf_split_value(asq[e], bsq, dot, gamma);
+            if (okc && lr < rlim) ob[(uint32_t)lr * ld + (uint32_t)cl] = H[i][j][r];
+          }
+        }
+        if (mirror) {
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const int lr = lr0 + 8 * q4;
+            float* dst = mb + ((uint32_t)cl * ld + (uint32_t)lr);
+            f4 v;
+            v.x = H[i][j][4 * q4 + 0];
+            v.y = H[i][j][4 * q4 + 1];
+            v.z = H[i][j][4 * q4 + 2];
+            v.w = H[i][j][4 * q4 + 3];
+            if (okc && lr + 3 < rlim) {
+              *(f4*)dst = v;
+            } else if (okc) {
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                if (lr + c < rlim) dst[c] = v[c];
+            }
+          }
+        }
+      }
+    }
+    if constexpr (NT == 3) {
+      st[3] = __builtin_amdgcn_s_memtime();
+      const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+      if (tid == 0) {
+        uint64_t* o = stamps + (size_t)L * 8;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = st[i];
+        o[4] = st[3];
+        o[5] = rt0;
+        o[6] = rt1;
+        o[7] = t;
+      }
+    }
+    if (!has_next) break;
+    L = Ln;
+    t = tn_next;
+    par ^= 1;
+    Ln = L + G;
+    if (Ln < ntiles) tn_next = tiles[Ln];
+  }
+}
+#undef DMA_PIECE
+#undef ROW_DMA
 
 // ---------------------------------------------------------------------------
 // Persistent LDS-DMA STORE GEMM: the LDS-DMA kernel's k loop, one 512-thread
@@ -1386,6 +1674,10 @@ int split_gemm_variant() {
 
 void set_split_gemm_variant(int v) { g_split_variant = v; }
 
+// diagnostics: non-null = the wide-wave Gram kernel writes per-workgroup stamps here
+uint64_t* g_gram_stamps = nullptr;
+void set_gram_stamps(uint64_t* p) { g_gram_stamps = p; }
+
 int64_t split_row_u4(int dp) { return (int64_t)((dp + 31) / 32) * 8; }
 
 void rbf_predict_split(const float* A, const float* Asq, int64_t M, int lda, const float* B, const float* Bsq,
@@ -1446,12 +1738,12 @@ struct TileTable {
 };
 // Keyed by (device, tm, tn): the table lives in the memory of the device that
 // launches the GEMM (svmTrain -p N: one rank per device, threads of one process).
-const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
+const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym = true) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int64_t, int64_t>, TileTable> cache;
+  static std::map<std::tuple<int, int64_t, int64_t, bool>, TileTable> cache;
   const int device = current_device();
   std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find({device, tm, tn});
+  auto it = cache.find({device, tm, tn, sym});
   if (it != cache.end()) return it->second;
   // the needed tiles in groups of GM tile rows, column by column, rows inside a
   // column; chunks of CH consecutive tiles dealt round-robin to the 8 XCDs.
@@ -1473,7 +1765,7 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
     const int64_t gm = std::min(GM, tm - g0);
     for (int64_t ty = 0; ty < tn; ++ty)
       for (int64_t tx = g0; tx < g0 + gm; ++tx)
-        if (ty >= 2 * tx) order.push_back((uint32_t)((tx << 16) | ty));
+        if (!sym || ty >= 2 * tx) order.push_back((uint32_t)((tx << 16) | ty));
   }
   const int64_t total = (int64_t)order.size(), full = total / (8 * CH) * (8 * CH);
   std::vector<uint32_t> tab((size_t)total);
@@ -1490,7 +1782,7 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s) {
   HIP_CHECK(hipMalloc((void**)&t.dev, (size_t)total * sizeof(uint32_t)));
   HIP_CHECK(hipMemcpyAsync(t.dev, tab.data(), (size_t)total * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  return cache.emplace(std::make_tuple(device, tm, tn), t).first->second;
+  return cache.emplace(std::make_tuple(device, tm, tn, sym), t).first->second;
 }
 }  // namespace
 
@@ -1515,7 +1807,8 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   // (32-bit store offsets inside a 256 x 128 tile: ldo < 2^24)
-  if ((variant == 5 || variant == 6 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 && ldo < (1ll << 24)) {
+  if ((variant == 5 || variant == 6 || variant == 7 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
+      ldo < (1ll << 24)) {
     static const int nt = [] {
       const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
       return e ? atoi(e) : 0;
@@ -1528,7 +1821,8 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const char* e = std::getenv("DPSVM_GRAM_SPREAD");
       return e ? atoi(e) : 1;
     }();
-    auto kern = nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
+    auto kern = g_gram_stamps ? dev::rbf_gemm_split_w64_kernel<3, 1>
+                : nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
                 : nt ? dev::rbf_gemm_split_w64_kernel<1>
                 : ((spread && variant != 5) || variant == 6) ? dev::rbf_gemm_split_w64_kernel<0, 1>
                                                               : dev::rbf_gemm_split_w64_kernel<0>;
@@ -1536,14 +1830,45 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const char* e = std::getenv("DPSVM_GRAM_COMPACT");
       return !(e && e[0] == '0');
     }();
+    // persistent over the tiles (variant 7; A/B: DPSVM_GRAM_PERSIST=0|1): one
+    // workgroup per CU, the LDS-DMA ring running on across tiles
+    static const int persist_env = [] {
+      const char* e = std::getenv("DPSVM_GRAM_PERSIST");
+      return e ? atoi(e) : 0;
+    }();
+    const int nkb = (dp + 31) / 32;
+    // (32-bit indices: the split operand buffers hold (rows + 512) x nkb x 8 u4, the output M x ldo floats)
+    const bool idx32 = (M + 512) * (int64_t)nkb * 8 < (1ll << 31) && (N + 512) * (int64_t)nkb * 8 < (1ll << 31) &&
+                       M * ldo < (1ll << 32) && N * ldo < (1ll << 32);
+    const bool persist = (variant == 7 || (variant == 0 && persist_env == 1)) && nkb >= 3 && nt == 0 && idx32 &&
+                         tm2 < 65536 && tn < 65536 && (!symmetric || compact);
+    if (persist) {
+      const int cus = [] {
+        int n = 0;
+        HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, current_device()));
+        return std::max(8, n);
+      }();
+      const auto& t = sym_tile_table(tm2, tn, s, symmetric);  // non-symmetric: every tile, same XCD order
+      const uint32_t* tab = t.dev;
+      const int64_t ntiles = t.count;
+      const int64_t grid = std::min<int64_t>(ntiles, cus);
+      auto pk = g_gram_stamps ? dev::rbf_gemm_split_w64p_kernel<3> : dev::rbf_gemm_split_w64p_kernel<0>;
+      pk<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>((const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B,
+                                                          Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
+                                                          symmetric ? 1 : 0, tab, (int)ntiles, (int)tm2, (int)tn,
+                                                          g_gram_stamps);
+      post_launch("rbf_gemm_split_w64p", s);
+      return;
+    }
     if (symmetric && compact && tm2 < 65536 && tn < 65536) {
       const auto& tab = sym_tile_table(tm2, tn, s);
       kern<<<dim3((unsigned)tab.count), dev::kW64Threads, 0, s>>>(
-          (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo, 1, tab.dev);
+          (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo, 1, tab.dev,
+          g_gram_stamps);
     } else {
       kern<<<dim3((unsigned)tm2, (unsigned)tn), dev::kW64Threads, 0, s>>>(
           (const dev::u4*)A, Ash, Asq, M, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, out, ldo,
-          symmetric ? 1 : 0, nullptr);
+          symmetric ? 1 : 0, nullptr, g_gram_stamps);
     }
     post_launch("rbf_gemm_split_w64", s);
     return;

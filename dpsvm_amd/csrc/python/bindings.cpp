@@ -567,6 +567,8 @@ PYBIND11_MODULE(_C, m) {
                               out_ld, (const int*)out_rows, (void*)stream, split);
   }, py::arg("x"), py::arg("xsq"), py::arg("n"), py::arg("ld"), py::arg("rows"), py::arg("m"), py::arg("gamma"),
         py::arg("out"), py::arg("out_ld"), py::arg("out_rows"), py::arg("stream"), py::arg("split") = false);
+  m.def("k_set_gram_stamps", [](uintptr_t p) { launch::set_gram_stamps((uint64_t*)p); },
+        "diagnostics: the wide-wave Gram kernel writes 8 u64 stamps per workgroup at p (0: off)");
   m.def("k_set_split_gemm_variant", [](int v) { launch::set_split_gemm_variant(v); },
         "split STORE GEMM: 0 auto (4, or 3 when dp <= 128), 1 register-staged tile per workgroup, 3 LDS-DMA, 4 persistent LDS-DMA (tests / A/B)");
   m.def("k_split_gemm_variant", []() { return launch::split_gemm_variant(); });
