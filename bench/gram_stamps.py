@@ -37,7 +37,17 @@ def analyse(st, nkb, kernel_ms):
     span_us = (st[:, 6].max() - st[:, 5].min()) / 100.0
     busy_us = (st[:, 6] - st[:, 5]).sum() / 100.0
     med = lambda v: float(np.median(v))  # noqa: E731
+    # persistent kernel: tile L is step L // 256 of its workgroup (drift check:
+    # do later steps run slower k loops?)
+    idx = np.nonzero(ok)[0]
+    step = idx // 256
+    by_step = {}
+    for lo, hi in ((0, 1), (1, 10), (10, 100), (100, 10**9)):
+        m = (step >= lo) & (step < hi)
+        if m.any():
+            by_step[f"{lo}-{hi if hi < 10**9 else 'end'}"] = med(loop[m])
     return {
+        "k_loop_cycles_by_step": by_step,
         "workgroups": int(len(st)), "clock_ghz_median": round(clk_ghz, 3),
         "cycles_median": {"prologue": med(pro), "k_loop": med(loop), "epilogue_store_issue": med(epi),
                           "store_drain": med(drain), "total": med(total)},

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Pass-1 (multi-block f update) kernel time at the per-rank shapes of the
 sharded headline: a rank of P owns n = 60000 / P columns of every Gram row and
-a round changes ~3,072 rows (32 blocks x 96).  Times ws_select pass 1 alone
+a round changes up to 6,144 rows (the default union: 128 blocks x 48).  Times ws_select pass 1 alone
 (event-timed, repeated: it only reads the state) on crafted state through the
 ws_select probe, for several list-slice counts ks (pass-1 workgroups per
 selection group), to see whether the G = ceil(n / 256) workgroups of the
@@ -24,7 +24,8 @@ def main() -> int:
     ap.add_argument("--rows", type=int, default=60000, help="Gram rows (lines) of the shard")
     ap.add_argument("--cols", default="7500,15000,30000", help="columns per rank (60000 / P)")
     ap.add_argument("--ks", default="1,2,4,8,16")
-    ap.add_argument("--changed", type=int, default=3072)
+    ap.add_argument("--changed", type=int, default=6144)
+    ap.add_argument("--blocks", type=int, default=128)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--wide", action="store_true", help="the wide pass 1 (ws_pass1_v4_kernel, the default)")
     ap.add_argument("--out", default=None)
@@ -33,7 +34,7 @@ def main() -> int:
 
     C = load()
     rng = np.random.default_rng(0)
-    blocks, q = 32, a.changed // 32
+    blocks, q = a.blocks, a.changed // a.blocks
     out = []
     for n in [int(v) for v in a.cols.split(",")]:
         L = a.rows

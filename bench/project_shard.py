@@ -29,7 +29,7 @@ import json
 import sys
 
 PASS1_US = 50.0   # f-update pass 1 at P = 1 when the inputs carry no stamp of it (round-2 value)
-UNION = 3072      # rows per round (device_state.hpp kWsMaxAll); blocks of UNION / P rows, <= 192
+UNION = 6144      # rows per round (device_state.hpp kWsMaxAll); blocks of UNION / blocks rows, <= 192
 
 
 def pass1_splits(G: int) -> int:

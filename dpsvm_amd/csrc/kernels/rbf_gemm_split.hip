@@ -827,6 +827,11 @@ constexpr int kW64Threads = 512;
 // SP 1: the next-but-one block's six LDS-DMA pieces are issued one after each
 // group of four MFMAs instead of all six right after the k-block barrier (all
 // eight waves then stall on the load path at once while the MFMA pipe idles)
+// the 32-bit LDS byte address of a __shared__ pointer (asm ds_read operands)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 template <int NT, int SP = 0>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
@@ -899,7 +904,92 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
   const int sw = ((lane & 31) >> 1) & 7;
   const int ra0 = (wm * 64 + (lane & 31)) * CPR;
   const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
-  for (int kb = 0; kb < nkb; ++kb) {
+  if constexpr (SP == 3) {
+    // SP 2's read-ahead carried across k blocks: block kb + 1's barrier sits
+    // before block kb's last MFMA group, so its first fragments are read while
+    // that group runs.  Before the barrier every read of block kb has landed
+    // (lgkmcnt(0)), so the DMA into block kb's buffer (block kb + 3, issued
+    // during block kb + 1) cannot overtake a read; block kb + 1's DMA is
+    // retired by vmcnt(5) (block kb + 2's first five pieces may stay in flight)
+    auto rd2 = [&](uint32_t base, int c, h8& x0, h8& x1) {
+      const uint32_t a0 = base + 16u * (uint32_t)c;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(x0) : "v"(a0) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(x1) : "v"(a0) : "memory");  // + 32 rows
+    };
+    const int ch0 = hl ^ sw, cl0 = (4 + hl) ^ sw, ch1 = (2 + hl) ^ sw, cl1 = (6 + hl) ^ sw;
+    h8 ah0, ah1, bh0, bh1, bl0, bl1, al0, al1, bh0n, bh1n;
+    if (nkb > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    rd2(lds_addr(lds + ra0), ch0, ah0, ah1);
+    rd2(lds_addr(lds + rb0), ch0, bh0, bh1);
+    if constexpr (NT == 3) st[1] = __builtin_amdgcn_s_memtime();
+    for (int kb = 0; kb < nkb; ++kb) {
+      const bool spread = kb + 2 < nkb;  // uniform: block kb + 2 is DMA'd over this block's groups
+      auto piece = [&](int i) {
+        if (spread) {
+          __builtin_amdgcn_sched_barrier(0);
+          dma_piece(kb + 2, i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      const u4* buf = lds + (kb % NB) * BUF;
+      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
+      rd2(bbase, cl0, bl0, bl1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0), "+v"(bh1));
+      H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
+      piece(0);
+      rd2(abase, cl0, al0, al1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(1);
+      rd2(abase, ch1, ah0, ah1);
+      rd2(bbase, ch1, bh0n, bh1n);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(al0), "+v"(al1));
+      Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
+      piece(2);
+      rd2(bbase, cl1, bl0, bl1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0n), "+v"(bh1n));
+      H[0][0] = mfma32_f16(ah0, bh0n, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1n, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0n, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1n, H[1][1]);
+      piece(3);
+      rd2(abase, cl1, al0, al1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(4);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al0), "+v"(al1));
+      if (kb + 1 < nkb) {  // uniform
+        if (spread) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const u4* nbuf = lds + ((kb + 1) % NB) * BUF;
+        rd2(lds_addr(nbuf + ra0), ch0, ah0, ah1);  // (A hi of this block is dead after P)
+        rd2(lds_addr(nbuf + rb0), ch0, bh0, bh1);
+      }
+      Q[0][0] = mfma32_f16(al0, bh0n, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1n, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0n, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1n, Q[1][1]);
+      piece(5);
+    }
+  }
+  for (int kb = 0; kb < (SP == 3 ? 0 : nkb); ++kb) {
     // retire block kb's DMA (block kb + 1 may stay in flight)
     if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -920,6 +1010,66 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
       }
     };
     const u4* buf = lds + (kb % NB) * BUF;
+    if constexpr (SP == 2) {
+      // LDS reads issued one MFMA group ahead, in asm with counted waits (the
+      // compiler drains lgkmcnt to 0 around the LDS-DMA): a group's fragments
+      // land while the previous group's MFMAs run, except the block's first.
+      // Eight fragments live at most.  A wait names the fragments it retires
+      // ("+v"), so no MFMA can move above it
+      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
+      auto rd2 = [&](uint32_t base, int c, h8& x0, h8& x1) {
+        const uint32_t a0 = base + 16u * (uint32_t)c;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(x0) : "v"(a0) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(x1) : "v"(a0) : "memory");  // + 32 rows
+      };
+      const int ch0 = hl ^ sw, cl0 = (4 + hl) ^ sw, ch1 = (2 + hl) ^ sw, cl1 = (6 + hl) ^ sw;
+      h8 ah0, ah1, bh0, bh1, bl0, bl1, al0, al1, bh0n, bh1n;
+      rd2(abase, ch0, ah0, ah1);
+      rd2(bbase, ch0, bh0, bh1);
+      rd2(bbase, cl0, bl0, bl1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0), "+v"(bh1));
+      H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
+      piece(0);
+      rd2(abase, cl0, al0, al1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(1);
+      rd2(abase, ch1, ah0, ah1);  // k step 1 (A hi of step 0 is dead)
+      rd2(bbase, ch1, bh0n, bh1n);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(al0), "+v"(al1));
+      Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
+      piece(2);
+      rd2(bbase, cl1, bl0, bl1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0n), "+v"(bh1n));
+      H[0][0] = mfma32_f16(ah0, bh0n, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1n, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0n, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1n, H[1][1]);
+      piece(3);
+      rd2(abase, cl1, al0, al1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(4);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al0), "+v"(al1));
+      Q[0][0] = mfma32_f16(al0, bh0n, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1n, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0n, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1n, Q[1][1]);
+      piece(5);
+      continue;
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
@@ -1048,20 +1198,23 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
 // NT 3: per-tile stamps (first wait, first block landed, k loop done, stores
 // issued) and s_memrealtime at the tile's start / end into stamps[8 L ..].
 // ---------------------------------------------------------------------------
-// LDS-DMA piece i of k block kb of the tile at (m0, n0) into ring buffer buf:
-// wave w fills stage rows 48 w + 8 i + (lane >> 3), lane position p = lane & 7
-// taking global chunk p ^ ((row >> 1) & 7) (the w64 kernel's geometry)
-__device__ __forceinline__ void w64p_dma_piece(const u4* __restrict__ A, const u4* __restrict__ B, u4* lds,
-                                               uint32_t rs, int wave, int lane, int m0, int n0, int kb, int buf,
-                                               int i) {
-  constexpr int TM = 256, BUF = 384 * 8;
-  const int g = __builtin_amdgcn_readfirstlane(48 * wave + 8 * i);  // first row of the group (uniform)
-  const int r = g + (lane >> 3);
-  const uint32_t off = (uint32_t)(lane >> 3) * rs + (uint32_t)((lane & 7) ^ ((r >> 1) & 7));
-  const u4* base = g < TM ? A : B;
-  const uint32_t row = g < TM ? (uint32_t)(m0 + g) : (uint32_t)(n0 + g - TM);
-  u4* dst = lds + buf * BUF + 48 * wave * 8 + 8 * i * 8;
-  __builtin_amdgcn_global_load_lds((const void*)(base + (row * rs + (uint32_t)kb * 8 + off)),
+// LDS-DMA piece of a k block into ring buffer buf.  The persistent kernel
+// gives every wave four pieces of A rows (wave w: rows 32 w + 8 i) and two of B
+// rows (rows 256 + 16 w + 8 i): six pieces a wave as in the w64 kernel (one
+// uniform vmcnt), with two fixed source pointers and row bases, so a piece is
+// one scalar add and two vector ops (u: the k block's row offset, uniform).
+// Lane position p = lane & 7 takes global chunk p ^ ((row >> 1) & 7), the w64
+// kernel's swizzle; for these rows that is p ^ (((lane >> 4) + 4 (i & 1)) & 7):
+// two lane offsets for all pieces (off_e / off_o).
+// The address is a uniform base plus the lane's byte offset (laundered by the
+// caller, so it is not re-derived per piece): the saddr form of the DMA, no
+// vector math per piece.
+__device__ __forceinline__ void w64p_piece(const u4* __restrict__ src, u4* lds, uint32_t u, uint32_t step,
+                                           int dst_row8, uint32_t off_e, uint32_t off_o, int buf, int i) {
+  constexpr int BUF = 384 * 8;
+  u4* dst = lds + buf * BUF + dst_row8 + i * 64;
+  const char* base = (const char*)(src + (u + (uint32_t)i * step));  // uniform
+  __builtin_amdgcn_global_load_lds((const void*)(base + ((i & 1) ? off_o : off_e)),
                                    (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
@@ -1109,9 +1262,16 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
   const uint32_t rs = (uint32_t)nkb * 8;  // u4 per split row
-  // the per-lane DMA offsets are recomputed per piece (a few VALU ops) rather
-  // than held in six registers across the loop (w64p_dma_piece)
-#define DMA_PIECE(m0_, n0_, kb_, buf_, i_) w64p_dma_piece(A, B, lds, rs, wave, lane, m0_, n0_, kb_, buf_, i_)
+  // every wave: 4 pieces of A rows, 2 of B rows a k block (w64p_piece)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t step = 8 * rs;
+  // the lanes' byte offsets within a piece (even / odd pieces)
+  uint32_t off_e = 16u * ((uint32_t)(lane >> 3) * rs + (uint32_t)((lane & 7) ^ (lane >> 4)));
+  uint32_t off_o = 16u * ((uint32_t)(lane >> 3) * rs + (uint32_t)((lane & 7) ^ ((lane >> 4) + 4)));
+  asm volatile("" : "+v"(off_e), "+v"(off_o));
+  const int dstA = 32 * wv * 8, dstB = (TM + 16 * wv) * 8;
+#define PIECE_A(uA_, buf_, i_) w64p_piece(A, lds, uA_, step, dstA, off_e, off_o, buf_, i_)
+#define PIECE_B(uB_, buf_, i_) w64p_piece(B, lds, uB_, step, dstB, off_e, off_o, buf_, i_)
 #define ROW_DMA(m0_, n0_, par_) w64p_row_dma(Asq, Bsq, Ash, Bsh, M, N, s_rows, wave, lane, m0_, n0_, par_)
   int Ln = L + G;
   uint32_t tn_next = Ln < ntiles ? tiles[Ln] : 0u;
@@ -1121,9 +1281,15 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
     ROW_DMA(m0, n0, 0);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) DMA_PIECE(m0, n0, 0, 0, i);
+    for (int b = 0; b < 2; ++b) {  // blocks 0 and 1 (launcher: nkb >= 3)
+      const uint32_t uA = (uint32_t)(m0 + 32 * wv) * rs + (uint32_t)b * 8;
+      const uint32_t uB = (uint32_t)(n0 + 16 * wv) * rs + (uint32_t)b * 8;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) DMA_PIECE(m0, n0, 1, 1, i);  // launcher: nkb >= 3
+      for (int i = 0; i < 4; ++i) PIECE_A(uA, b, i);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) PIECE_B(uB, b, i);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the loop's first wait counts 6 younger: tile 0 starts landed
   }
   const int sw = ((lane & 31) >> 1) & 7;
   const int ra0 = (wm * 64 + (lane & 31)) * CPR;
@@ -1137,7 +1303,9 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     const bool has_next = Ln < ntiles;  // uniform
     const int tx = (int)(t >> 16), ty = (int)(t & 0xffffu);
     const int m0 = tx * TM, n0 = ty * TN;
-    const int nm0 = (int)(tn_next >> 16) * TM, nn0 = (int)(tn_next & 0xffffu) * TN;
+    // (the last tile prefetches its own blocks 0 / 1 into dead buffers: no branch in the loop)
+    const uint32_t tp = has_next ? tn_next : t;
+    const int nm0 = (int)(tp >> 16) * TM, nn0 = (int)(tp & 0xffffu) * TN;
     f16v H[2][2], P[2][2], Q[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1147,35 +1315,30 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
         for (int r = 0; r < 16; ++r) H[i][j][r] = P[i][j][r] = Q[i][j][r] = 0.f;
 #pragma clang loop unroll(disable)
     for (int kb = 0; kb < nkb; ++kb) {
-      // retire block kb's DMA: at a tile's first block everything (the previous
-      // epilogue's stores are younger than this tile's first blocks); in the
-      // last block the next tile's block 0 and row data (8 a wave) may stay in flight
-      if (kb == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (kb == 1 && has_next) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // + the next row data
-      else if (kb + 1 < nkb || has_next) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // retire block kb's DMA: block kb + 1 (6 pieces a wave) may stay in flight.
+      // Every k block prefetches (the last tile's last two re-load blocks 0 / 1
+      // of itself into dead buffers) and every epilogue ends with vmcnt(0): one
+      // wait, no branch (a taken branch a piece cost ~10% of the loop)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if constexpr (NT == 3) {
         if (kb == 0) st[1] = __builtin_amdgcn_s_memtime();
       }
-      // the next tile's row data into the other parity (last read by the
-      // previous tile's epilogue, before this barrier), ahead of block 2's DMA
-      if (kb == 0 && has_next) ROW_DMA(nm0, nn0, par ^ 1);
       // the prefetch slot: block kb + 2 of this tile, or block kb + 2 - nkb of
       // the next one, into the buffer of block g - 1 (every wave is past it)
       const bool own = kb + 2 < nkb;
-      const bool pf = own || has_next;  // uniform
       const int pkb = own ? kb + 2 : kb + 2 - nkb;
-      const int pm0 = own ? m0 : nm0, pn0 = own ? n0 : nn0;
+      const uint32_t uA = (uint32_t)((own ? m0 : nm0) + 32 * wv) * rs + (uint32_t)pkb * 8;
+      const uint32_t uB = (uint32_t)((own ? n0 : nn0) + 16 * wv) * rs + (uint32_t)pkb * 8;
       const int pbuf = (int)((g + 2) % NB);
-      auto piece = [&](int i) {
-        if (pf) {
-          __builtin_amdgcn_sched_barrier(0);
-          DMA_PIECE(pm0, pn0, pkb, pbuf, i);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      // after MFMA group j (0..5) of the block: A0, A1, B0, A2, A3, B1
+      auto piece = [&](int j) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (j == 2 || j == 5) PIECE_B(uB, pbuf, j == 2 ? 0 : 1);
+        else PIECE_A(uA, pbuf, j < 2 ? j : j - 1);
+        __builtin_amdgcn_sched_barrier(0);
       };
       const u4* buf = lds + (g % NB) * BUF;
 #pragma unroll
@@ -1208,6 +1371,9 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
       ++g;
     }
     if constexpr (NT == 3) st[2] = __builtin_amdgcn_s_memtime();
+    // the next tile's row data into the other parity (last read by the previous
+    // tile's epilogue, before this tile's first barrier)
+    if (has_next) ROW_DMA(nm0, nn0, par ^ 1);
 
     // ---- epilogue of the w64 kernel (row data from parity `par`) ----
     // (the per-lane epilogue addresses are recomputed per tile from a
@@ -1267,6 +1433,10 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
         }
       }
     }
+    // the stores, the next tile's blocks 0 / 1 and its row data retired here:
+    // the loop's uniform vmcnt(6) then holds at the next tile's first block (and
+    // no DMA is in flight when the kernel ends)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (NT == 3) {
       st[3] = __builtin_amdgcn_s_memtime();
       const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
@@ -1288,7 +1458,8 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     if (Ln < ntiles) tn_next = tiles[Ln];
   }
 }
-#undef DMA_PIECE
+#undef PIECE_A
+#undef PIECE_B
 #undef ROW_DMA
 
 // ---------------------------------------------------------------------------
@@ -1807,7 +1978,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   // (32-bit store offsets inside a 256 x 128 tile: ldo < 2^24)
-  if ((variant == 5 || variant == 6 || variant == 7 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
+  if ((variant == 5 || variant == 6 || variant == 7 || variant == 8 || variant == 9 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
       ldo < (1ll << 24)) {
     static const int nt = [] {
       const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
@@ -1821,7 +1992,11 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const char* e = std::getenv("DPSVM_GRAM_SPREAD");
       return e ? atoi(e) : 1;
     }();
-    auto kern = g_gram_stamps ? dev::rbf_gemm_split_w64_kernel<3, 1>
+    auto kern = g_gram_stamps ? (variant == 8   ? dev::rbf_gemm_split_w64_kernel<3, 2>
+                                 : variant == 9 ? dev::rbf_gemm_split_w64_kernel<3, 3>
+                                                : dev::rbf_gemm_split_w64_kernel<3, 1>)
+                : variant == 8 ? dev::rbf_gemm_split_w64_kernel<0, 2>
+                : variant == 9 ? dev::rbf_gemm_split_w64_kernel<0, 3>
                 : nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
                 : nt ? dev::rbf_gemm_split_w64_kernel<1>
                 : ((spread && variant != 5) || variant == 6) ? dev::rbf_gemm_split_w64_kernel<0, 1>
