@@ -827,6 +827,10 @@ constexpr int kW64Threads = 512;
 // SP 1: the next-but-one block's six LDS-DMA pieces are issued one after each
 // group of four MFMAs instead of all six right after the k-block barrier (all
 // eight waves then stall on the load path at once while the MFMA pipe idles)
+// SP 2 (default): SP 1 plus the operand fragments read from LDS one MFMA group
+// ahead with counted lgkmcnt waits, so only the block's first group waits on
+// LDS latency (k loop 63.8k -> 59.1k cycles a tile, bench/gram_stamps.py)
+
 // the 32-bit LDS byte address of a __shared__ pointer (asm ds_read operands)
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -904,92 +908,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
   const int sw = ((lane & 31) >> 1) & 7;
   const int ra0 = (wm * 64 + (lane & 31)) * CPR;
   const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
-  if constexpr (SP == 3) {
-    // SP 2's read-ahead carried across k blocks: block kb + 1's barrier sits
-    // before block kb's last MFMA group, so its first fragments are read while
-    // that group runs.  Before the barrier every read of block kb has landed
-    // (lgkmcnt(0)), so the DMA into block kb's buffer (block kb + 3, issued
-    // during block kb + 1) cannot overtake a read; block kb + 1's DMA is
-    // retired by vmcnt(5) (block kb + 2's first five pieces may stay in flight)
-    auto rd2 = [&](uint32_t base, int c, h8& x0, h8& x1) {
-      const uint32_t a0 = base + 16u * (uint32_t)c;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(x0) : "v"(a0) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(x1) : "v"(a0) : "memory");  // + 32 rows
-    };
-    const int ch0 = hl ^ sw, cl0 = (4 + hl) ^ sw, ch1 = (2 + hl) ^ sw, cl1 = (6 + hl) ^ sw;
-    h8 ah0, ah1, bh0, bh1, bl0, bl1, al0, al1, bh0n, bh1n;
-    if (nkb > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    rd2(lds_addr(lds + ra0), ch0, ah0, ah1);
-    rd2(lds_addr(lds + rb0), ch0, bh0, bh1);
-    if constexpr (NT == 3) st[1] = __builtin_amdgcn_s_memtime();
-    for (int kb = 0; kb < nkb; ++kb) {
-      const bool spread = kb + 2 < nkb;  // uniform: block kb + 2 is DMA'd over this block's groups
-      auto piece = [&](int i) {
-        if (spread) {
-          __builtin_amdgcn_sched_barrier(0);
-          dma_piece(kb + 2, i);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      };
-      const u4* buf = lds + (kb % NB) * BUF;
-      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
-      rd2(bbase, cl0, bl0, bl1);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0), "+v"(bh1));
-      H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
-      H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
-      H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
-      H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
-      piece(0);
-      rd2(abase, cl0, al0, al1);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
-      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
-      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
-      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
-      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
-      piece(1);
-      rd2(abase, ch1, ah0, ah1);
-      rd2(bbase, ch1, bh0n, bh1n);
-      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(al0), "+v"(al1));
-      Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
-      Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
-      Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
-      Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
-      piece(2);
-      rd2(bbase, cl1, bl0, bl1);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0n), "+v"(bh1n));
-      H[0][0] = mfma32_f16(ah0, bh0n, H[0][0]);
-      H[0][1] = mfma32_f16(ah0, bh1n, H[0][1]);
-      H[1][0] = mfma32_f16(ah1, bh0n, H[1][0]);
-      H[1][1] = mfma32_f16(ah1, bh1n, H[1][1]);
-      piece(3);
-      rd2(abase, cl1, al0, al1);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
-      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
-      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
-      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
-      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
-      piece(4);
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al0), "+v"(al1));
-      if (kb + 1 < nkb) {  // uniform
-        if (spread) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const u4* nbuf = lds + ((kb + 1) % NB) * BUF;
-        rd2(lds_addr(nbuf + ra0), ch0, ah0, ah1);  // (A hi of this block is dead after P)
-        rd2(lds_addr(nbuf + rb0), ch0, bh0, bh1);
-      }
-      Q[0][0] = mfma32_f16(al0, bh0n, Q[0][0]);
-      Q[0][1] = mfma32_f16(al0, bh1n, Q[0][1]);
-      Q[1][0] = mfma32_f16(al1, bh0n, Q[1][0]);
-      Q[1][1] = mfma32_f16(al1, bh1n, Q[1][1]);
-      piece(5);
-    }
-  }
-  for (int kb = 0; kb < (SP == 3 ? 0 : nkb); ++kb) {
+  for (int kb = 0; kb < nkb; ++kb) {
     // retire block kb's DMA (block kb + 1 may stay in flight)
     if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1978,29 +1897,29 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   // (32-bit store offsets inside a 256 x 128 tile: ldo < 2^24)
-  if ((variant == 5 || variant == 6 || variant == 7 || variant == 8 || variant == 9 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
+  if ((variant == 5 || variant == 6 || variant == 7 || variant == 8 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
       ldo < (1ll << 24)) {
     static const int nt = [] {
       const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
       return e ? atoi(e) : 0;
     }();
     const int64_t tm2 = (M + 255) / 256;
-    // the LDS-DMA issue spread over the MFMA groups (default): 9.41 -> 9.27 ms
-    // symmetric, 2.65 -> 2.56 ms for the P = 8 slab, bit-identical
-    // (profiles/r6_gram_dma_spread_ab.json; A/B: DPSVM_GRAM_SPREAD=0 or variant 5 vs 6)
+    // the LDS-DMA issue spread over the MFMA groups: 9.41 -> 9.27 ms symmetric,
+    // 2.65 -> 2.56 ms for the P = 8 slab (profiles/r6_gram_dma_spread_ab.json);
+    // with the LDS reads one MFMA group ahead (default): 9.22-9.27 -> 8.81-8.93
+    // ms, 2.56-2.70 -> 2.41-2.55 ms; all bit-identical (profiles/r6_gram_lds_readahead_ab.json).
+    // A/B: DPSVM_GRAM_SPREAD=0 (neither) or variants 5 (neither), 6 (spread), 8 (both)
     static const int spread = [] {
       const char* e = std::getenv("DPSVM_GRAM_SPREAD");
       return e ? atoi(e) : 1;
     }();
-    auto kern = g_gram_stamps ? (variant == 8   ? dev::rbf_gemm_split_w64_kernel<3, 2>
-                                 : variant == 9 ? dev::rbf_gemm_split_w64_kernel<3, 3>
-                                                : dev::rbf_gemm_split_w64_kernel<3, 1>)
-                : variant == 8 ? dev::rbf_gemm_split_w64_kernel<0, 2>
-                : variant == 9 ? dev::rbf_gemm_split_w64_kernel<0, 3>
-                : nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
-                : nt ? dev::rbf_gemm_split_w64_kernel<1>
-                : ((spread && variant != 5) || variant == 6) ? dev::rbf_gemm_split_w64_kernel<0, 1>
-                                                              : dev::rbf_gemm_split_w64_kernel<0>;
+    const int sp = variant == 5 ? 0 : variant == 6 ? 1 : variant == 8 ? 2 : spread ? 2 : 0;
+    auto kern = g_gram_stamps ? (sp == 2 ? dev::rbf_gemm_split_w64_kernel<3, 2> : dev::rbf_gemm_split_w64_kernel<3, 1>)
+                : nt == 2     ? dev::rbf_gemm_split_w64_kernel<2>
+                : nt          ? dev::rbf_gemm_split_w64_kernel<1>
+                : sp == 2     ? dev::rbf_gemm_split_w64_kernel<0, 2>
+                : sp == 1     ? dev::rbf_gemm_split_w64_kernel<0, 1>
+                              : dev::rbf_gemm_split_w64_kernel<0>;
     static const bool compact = [] {  // A/B: DPSVM_GRAM_COMPACT=0 launches the full grid (half exit at once)
       const char* e = std::getenv("DPSVM_GRAM_COMPACT");
       return !(e && e[0] == '0');
