@@ -1259,34 +1259,60 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
         else PIECE_A(uA, pbuf, j < 2 ? j : j - 1);
         __builtin_amdgcn_sched_barrier(0);
       };
+      // operand fragments read one MFMA group ahead (the w64 kernel's SP 2)
       const u4* buf = lds + (g % NB) * BUF;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
-        const h8 ah0 = __builtin_bit_cast(h8, buf[ra0 + ch]);
-        const h8 ah1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + ch]);
-        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
-        const h8 bh1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + ch]);
-        H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
-        H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
-        H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
-        H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
-        piece(3 * ks);
-        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
-        const h8 bl1 = __builtin_bit_cast(h8, buf[rb0 + 32 * CPR + cl]);
-        P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
-        P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
-        P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
-        P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
-        piece(3 * ks + 1);
-        const h8 al0 = __builtin_bit_cast(h8, buf[ra0 + cl]);
-        const h8 al1 = __builtin_bit_cast(h8, buf[ra0 + 32 * CPR + cl]);
-        Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
-        Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
-        Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
-        Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
-        piece(3 * ks + 2);
-      }
+      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
+      auto rd2 = [&](uint32_t base, int c, h8& x0, h8& x1) {
+        const uint32_t a0 = base + 16u * (uint32_t)c;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(x0) : "v"(a0) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(x1) : "v"(a0) : "memory");  // + 32 rows
+      };
+      const int ch0 = hl ^ sw, cl0 = (4 + hl) ^ sw, ch1 = (2 + hl) ^ sw, cl1 = (6 + hl) ^ sw;
+      h8 ah0, ah1, bh0, bh1, bl0, bl1, al0, al1, bh0n, bh1n;
+      rd2(abase, ch0, ah0, ah1);
+      rd2(bbase, ch0, bh0, bh1);
+      rd2(bbase, cl0, bl0, bl1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0), "+v"(bh1));
+      H[0][0] = mfma32_f16(ah0, bh0, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1, H[1][1]);
+      piece(0);
+      rd2(abase, cl0, al0, al1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(1);
+      rd2(abase, ch1, ah0, ah1);
+      rd2(bbase, ch1, bh0n, bh1n);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(al0), "+v"(al1));
+      Q[0][0] = mfma32_f16(al0, bh0, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1, Q[1][1]);
+      piece(2);
+      rd2(bbase, cl1, bl0, bl1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ah0), "+v"(ah1), "+v"(bh0n), "+v"(bh1n));
+      H[0][0] = mfma32_f16(ah0, bh0n, H[0][0]);
+      H[0][1] = mfma32_f16(ah0, bh1n, H[0][1]);
+      H[1][0] = mfma32_f16(ah1, bh0n, H[1][0]);
+      H[1][1] = mfma32_f16(ah1, bh1n, H[1][1]);
+      piece(3);
+      rd2(abase, cl1, al0, al1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bl0), "+v"(bl1));
+      P[0][0] = mfma32_f16(ah0, bl0, P[0][0]);
+      P[0][1] = mfma32_f16(ah0, bl1, P[0][1]);
+      P[1][0] = mfma32_f16(ah1, bl0, P[1][0]);
+      P[1][1] = mfma32_f16(ah1, bl1, P[1][1]);
+      piece(4);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al0), "+v"(al1));
+      Q[0][0] = mfma32_f16(al0, bh0n, Q[0][0]);
+      Q[0][1] = mfma32_f16(al0, bh1n, Q[0][1]);
+      Q[1][0] = mfma32_f16(al1, bh0n, Q[1][0]);
+      Q[1][1] = mfma32_f16(al1, bh1n, Q[1][1]);
+      piece(5);
       ++g;
     }
     if constexpr (NT == 3) st[2] = __builtin_amdgcn_s_memtime();
