@@ -1100,19 +1100,19 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Persistent wide-wave STORE GEMM (the default from round 6): the w64 kernel's
-// tile, k loop and epilogue, one workgroup per CU walking tiles L = b, b + G,
-// ... of the same table.  In-kernel stamps of the w64 kernel (NT 3,
-// profiles/r6_gram_stamps.json) put 11% of a tile in its prologue (row data,
-// then the first LDS-DMA block's latency) and 14% in the epilogue, with the
-// MFMA pipe idle in both.  Here the LDS-DMA ring runs on across tiles: during
-// the last two k blocks of tile t the prefetch slots load blocks 0 and 1 of
-// tile t + 1 (a block counter g over all tiles picks the buffer, g mod 3), and
-// the next tile's |x|^2 and shifts arrive by LDS-DMA into the other parity of
-// a row-data area (issued at tile t's first block), so tile t + 1 starts with
-// its first blocks landed.  The
-// epilogue's stores are younger than those DMAs: the next tile's first k
-// block waits vmcnt(0) (they drain in ~1k cycles, measured).  Same MFMA
+// Persistent wide-wave STORE GEMM (variant 7, opt-in: DPSVM_GRAM_PERSIST=1):
+// the w64 kernel's tile, k loop (with SP 2's read-ahead) and epilogue, one
+// workgroup per CU walking tiles L = b, b + G, ... of the same table.  The
+// w64 kernel's stamps put ~11% of a tile in its prologue (row data, then the
+// first LDS-DMA block's latency) with the MFMA pipe idle.  Here the LDS-DMA
+// ring runs on across tiles: during the last two k blocks of tile t the
+// prefetch slots load blocks 0 and 1 of tile t + 1 (a block counter g over all
+// tiles picks the buffer, g mod 3), and the next tile's |x|^2 and shifts arrive
+// by LDS-DMA into the other parity of a row-data area (issued after tile t's k
+// loop); every epilogue ends with vmcnt(0), so the loop's one uniform wait
+// holds at the next tile's first block.  80.3k vs 84.5k cycles a tile, but the
+// clock the chip holds drops with it: 8.97 vs 9.01 ms symmetric, 2.48 vs 2.52
+// ms for the P = 8 slab (profiles/r6_gram_lds_readahead_ab.json).  Same MFMA
 // sequence per output: bit-identical to the w64 kernel.
 // NT 3: per-tile stamps (first wait, first block landed, k loop done, stores
 // issued) and s_memrealtime at the tile's start / end into stamps[8 L ..].

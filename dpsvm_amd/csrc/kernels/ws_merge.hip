@@ -320,8 +320,37 @@ __device__ __forceinline__ void mh_insert(int32_t* keys, uint16_t* vals, int32_t
     // another row took that slot first: read the bucket again
   }
 }
-__device__ __forceinline__ int32_t mh_find(const int32_t* keys, const uint16_t* vals, int32_t idx) {
-  uint32_t b = mh_bucket(idx);
+// N inserts of one thread with every first bucket read, then every claim, in
+// flight together (one LDS round trip each instead of two per key in
+// sequence); a claim another row won first, or a full first bucket (rare at
+// the 0.38 load), takes the one-at-a-time path.  idx < 0: nothing to insert
+template <int N>
+__device__ __forceinline__ void mh_insert_n(int32_t* keys, uint16_t* vals, const int32_t (&idx)[N],
+                                            const int32_t (&v)[N]) {
+  uint32_t b[N];
+  mh_i4 kb[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    b[j] = mh_bucket(idx[j] < 0 ? 0 : idx[j]);
+    if (idx[j] >= 0) kb[j] = *(const mh_i4*)(keys + 4 * b[j]);
+  }
+  int sl[N];
+  bool won[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    sl[j] = kb[j].x == -1 ? 0 : kb[j].y == -1 ? 1 : kb[j].z == -1 ? 2 : kb[j].w == -1 ? 3 : 4;
+    won[j] = false;
+    if (idx[j] >= 0 && sl[j] < 4) won[j] = atomicCAS(keys + 4 * b[j] + sl[j], -1, idx[j]) == -1;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (idx[j] < 0) continue;
+    if (won[j]) vals[4 * b[j] + sl[j]] = (uint16_t)v[j];
+    else mh_insert(keys, vals, idx[j], v[j]);
+  }
+}
+
+__device__ __forceinline__ int32_t mh_find_from(const int32_t* keys, const uint16_t* vals, int32_t idx, uint32_t b) {
   for (int probe = 0; probe < kMHB; ++probe) {
     const mh_i4 kb = *(const mh_i4*)(keys + 4 * b);
     const int s = kb.x == idx ? 0 : kb.y == idx ? 1 : kb.z == idx ? 2 : kb.w == idx ? 3 : -1;
@@ -330,6 +359,32 @@ __device__ __forceinline__ int32_t mh_find(const int32_t* keys, const uint16_t* 
     b = (b + 1) & (kMHB - 1);
   }
   return -1;
+}
+__device__ __forceinline__ int32_t mh_find(const int32_t* keys, const uint16_t* vals, int32_t idx) {
+  return mh_find_from(keys, vals, idx, mh_bucket(idx));
+}
+
+// N lookups of one thread with every first bucket read in flight together; a
+// key not in a full first bucket probes on one at a time.  idx < 0: -1
+template <int N>
+__device__ __forceinline__ void mh_find_n(const int32_t* keys, const uint16_t* vals, const int32_t (&idx)[N],
+                                          int32_t (&out)[N]) {
+  uint32_t b[N];
+  mh_i4 kb[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    b[j] = mh_bucket(idx[j] < 0 ? 0 : idx[j]);
+    if (idx[j] >= 0) kb[j] = *(const mh_i4*)(keys + 4 * b[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    out[j] = -1;
+    if (idx[j] < 0) continue;
+    const int32_t k = idx[j];
+    const int s = kb[j].x == k ? 0 : kb[j].y == k ? 1 : kb[j].z == k ? 2 : kb[j].w == k ? 3 : -1;
+    if (s >= 0) out[j] = (int32_t)vals[4 * b[j] + s];
+    else if (kb[j].w != -1) out[j] = mh_find_from(keys, vals, k, (b[j] + 1) & (kMHB - 1));
+  }
 }
 
 // Multi-block rounds over the peer exchange: every rank's candidate lists
@@ -387,11 +442,22 @@ __global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
   if (blockIdx.x == 0 && tid == 0) WS_STAMP(21);
   const int G = a.G_all;
   int real = 0;
-  for (int e = tid; e < NK; e += kRankThreads) {
-    const int l = e / kWsCand, r = e % kWsCand;
-    const uint64_t k = l < G ? a.cand[(size_t)l * 2 * kWsCand + side * kWsCand + r] : kKeyNone;
-    s_k[e] = k;
-    real += k != kKeyNone ? 1 : 0;
+  {
+    // all NK / threads loads in flight before the LDS stores (a rolled loop
+    // paid one L2 round trip per key: ~5 of the kernel's 8 us)
+    constexpr int PER = NK / kRankThreads;
+    static_assert(NK % kRankThreads == 0, "rank load geometry");
+    uint64_t kk[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + j * kRankThreads, l = e / kWsCand, r = e % kWsCand;
+      kk[j] = l < G ? a.cand[(size_t)l * 2 * kWsCand + side * kWsCand + r] : kKeyNone;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      s_k[tid + j * kRankThreads] = kk[j];
+      real += kk[j] != kKeyNone ? 1 : 0;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) real += __shfl_xor(real, o);
@@ -482,30 +548,32 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   int32_t* const s_line = s_hk[0] + kMH / 2;  // cache mode, once the tables are dead: the union's lines
   const int half = (want + 1) / 2;  // <= kWsMaxAll / 2 ranks per side
   uint64_t ku[X], kl[X];
+  int32_t iu[X], il[X], er[X];  // the keys' rows (-1: none), their ranks
 #pragma unroll
   for (int x = 0; x < X; ++x) {
     const int e = tid + x * T;
     ku[x] = e < half ? v[0][x] : kKeyNone;
     kl[x] = e < half ? v[1][x] : kKeyNone;
-    if (ku[x] != kKeyNone) mh_insert(hk_u, hv_u, (int32_t)key_index(ku[x]), e);
-    if (kl[x] != kKeyNone) mh_insert(hk_l, hv_l, (int32_t)key_index(kl[x]), e);
+    iu[x] = ku[x] != kKeyNone ? (int32_t)key_index(ku[x]) : -1;
+    il[x] = kl[x] != kKeyNone ? (int32_t)key_index(kl[x]) : -1;
+    er[x] = e;
   }
+  mh_insert_n<X>(hk_u, hv_u, iu, er);
+  mh_insert_n<X>(hk_l, hv_l, il, er);
   __syncthreads();
   if (lead) WS_STAMP(12);
   // rank e keeps its up row unless the low side has it at a smaller rank, its
   // low row unless the up side has it at a rank <= e (the up copy comes first)
   bool kpu[X], kpl[X];
+  {
+    int32_t rl[X], ru[X];
+    mh_find_n<X>(hk_l, hv_l, iu, rl);
+    mh_find_n<X>(hk_u, hv_u, il, ru);
 #pragma unroll
-  for (int x = 0; x < X; ++x) {
-    const int e = tid + x * T;
-    kpu[x] = kpl[x] = false;
-    if (ku[x] != kKeyNone) {
-      const int rl = mh_find(hk_l, hv_l, (int32_t)key_index(ku[x]));
-      kpu[x] = !(rl >= 0 && rl < e);
-    }
-    if (kl[x] != kKeyNone) {
-      const int ru = mh_find(hk_u, hv_u, (int32_t)key_index(kl[x]));
-      kpl[x] = !(ru >= 0 && ru <= e);
+    for (int x = 0; x < X; ++x) {
+      const int e = tid + x * T;
+      kpu[x] = iu[x] >= 0 && !(rl[x] >= 0 && rl[x] < e);
+      kpl[x] = il[x] >= 0 && !(ru[x] >= 0 && ru[x] <= e);
     }
   }
   // union order: ranks 0 .. T - 1 (element 0 of threads in order), then ranks
@@ -535,14 +603,17 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   bool pk[U];
   int npk = 0;
 #pragma unroll
-  for (int h = 0; h < U; ++h) {
-    pk[h] = false;
-    if (n_chosen < Qmax && pidx[h] >= 0) {
-      const int ru = mh_find(hk_u, hv_u, pidx[h]), rl = mh_find(hk_l, hv_l, pidx[h]);
-      pk[h] = !((ru >= 0 && s_keep[2 * ru] >= 0) || (rl >= 0 && s_keep[2 * rl + 1] >= 0));
-    }
-    npk += (int)pk[h];
+  for (int h = 0; h < U; ++h) pk[h] = false;
+  if (n_chosen < Qmax) {  // uniform
+    int32_t ru[U], rl[U];
+    mh_find_n<U>(hk_u, hv_u, pidx, ru);
+    mh_find_n<U>(hk_l, hv_l, pidx, rl);
+#pragma unroll
+    for (int h = 0; h < U; ++h)
+      pk[h] = pidx[h] >= 0 && !((ru[h] >= 0 && s_keep[2 * ru[h]] >= 0) || (rl[h] >= 0 && s_keep[2 * rl[h] + 1] >= 0));
   }
+#pragma unroll
+  for (int h = 0; h < U; ++h) npk += (int)pk[h];
   int ptotal = 0;
   if (n_chosen < Qmax) {  // uniform
     int at = n_chosen + block_scan_merge<3>(npk, s_wsum, &ptotal);

@@ -101,17 +101,23 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
     // memory.  Each entry is a random 128-B line of HBM, so only the upper
     // triangle is loaded (the split Gram is bitwise symmetric) and mirrored in
     // LDS: 1,176 loads for a 48-row block, all in flight at once
+    int32_t gi = 0;
     if (tid < q) {
-      const int32_t gi = c->idx[par][ib + tid];
+      gi = c->idx[par][ib + tid];
       s_idx[tid] = gi;
       s_line[tid] = c->line[par][ib + tid];
-      s_f[tid] = a.f[gi];  // one rank: local row = global row
-      s_a[tid] = a.alpha[gi];
-      s_y[tid] = a.y[gi];
     }
     __syncthreads();
+    // the rows' f / alpha / y in flight with the entries (one memory round trip
+    // for both, stored after)
+    float fv = 0.f, av = 0.f, yv = 0.f;
+    if (tid < q) {
+      fv = a.f[gi];  // one rank: local row = global row
+      av = a.alpha[gi];
+      yv = a.y[gi];
+    }
     const int n = q * ldk;
-    constexpr int U = 4;
+    constexpr int U = 4;  // n <= 64 x 64 = U x threads: one pass
     for (int e0 = tid; e0 < n; e0 += U * kWsSolveThreads) {
       float v[U];
 #pragma unroll
@@ -129,6 +135,11 @@ __global__ __launch_bounds__(kWsSolveThreads) void ws_solve_kernel(WsArgs a) {
           if (col < q && col != ra) K[col * ldk + ra] = v[u];  // the mirrored entry
         }
       }
+    }
+    if (tid < q) {
+      s_f[tid] = fv;
+      s_a[tid] = av;
+      s_y[tid] = yv;
     }
   } else {
     // q rows of the q_max-stride sub-Gram into LDS (147 KiB at q = 192): 16-B
