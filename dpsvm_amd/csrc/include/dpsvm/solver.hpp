@@ -199,6 +199,11 @@ void rbf_gram(const float* a, const float* asq, int64_t m, const float* b, const
 // the working-set cache engine's row GEMM: out[out_rows[i]][j] = K(x[rows[i]], x_j), i < m, j < n
 void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const int* rows, int m, float gamma,
                       float* out, int64_t out_ld, const int* out_rows, void* stream, bool split = false);
+// diagnostics: the split row GEMM alone (operands split once), reps launches
+// event-timed; returns ms per launch (bench/rows_probe.py)
+std::vector<float> rbf_rows_indexed_split_bench(const float* x, const float* xsq, int64_t n, int ld, const int* rows,
+                                                int m, float gamma, float* out, int64_t out_ld, const int* out_rows,
+                                                int reps, void* stream);
 // the same two GEMMs on fp16 MFMA over split operands (rbf_gemm_split.hip)
 void rbf_gram_split(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
                     float gamma, float* out, int64_t out_ld, bool symmetric, void* stream);

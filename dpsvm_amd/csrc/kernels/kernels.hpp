@@ -132,6 +132,7 @@ int split_gemm_variant();
 void set_split_gemm_variant(int v);
 // diagnostics: per-workgroup s_memtime stamps of the wide-wave Gram kernel (nullptr: off)
 void set_gram_stamps(uint64_t* p);
+void set_rows_stamps(uint64_t* p);  // diagnostics: the LDS-DMA rows kernel's per-workgroup stamps (0: off)
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
                           int64_t ldo, hipStream_t s, bool symmetric = false);

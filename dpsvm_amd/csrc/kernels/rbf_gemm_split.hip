@@ -505,6 +505,11 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
   }
 }
 
+// the 32-bit LDS byte address of a __shared__ pointer (asm ds_read operands)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // ---------------------------------------------------------------------------
 // LDS-DMA ROWS GEMM: a working-set round's cache misses (up to 192 indexed A
 // rows, a_rows[0 .. *m_dev)) against all of this rank's B rows, K written to
@@ -522,20 +527,39 @@ __global__ __launch_bounds__(kGldsThreads, 1) void rbf_gemm_split_glds_kernel(
 constexpr int kRowsGldsThreads = 768;
 // BAUX: cache policy of the B operand's DMA (2 = nt: streamed once per round,
 // kept from evicting the A rows every tile re-reads from L2)
-template <int BAUX>
+// NBR: B ring depth.  A and B have separate rings: A three deep (block kb + 2
+// issued at block kb), B NBR deep (block kb + NBR - 1 issued at kb); the waves
+// that stage A (0-5) and B (6-9) wait on their own DMA counts.  Measured at the
+// synthetic-2m round shape (bench/rows_probe.py, profiles/r6_rows_kernel.txt):
+// NBR 5 does not beat 3, B read from L2 instead of HBM saves only ~10%, and
+// the operand reads one MFMA group ahead (the Gram's SP 2) change nothing —
+// the k loop runs at ~46% MFMA with the chip at ~1.57 GHz.
+// ST: diagnostics build with per-workgroup stamps (entry, first block landed,
+// k loop done, stores issued, stores done; s_memrealtime at entry / end) at
+// stamps[8 (blockIdx.y gridDim.x + blockIdx.x) ..] (bench/rows_probe.py --stamps)
+template <int BAUX, int NBR = 3, bool ST = false>
 __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
     const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
     const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb, float gamma,
-    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
-  constexpr int WN = 2, TM = 192, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
-  constexpr int DMA_WAVES = ROWS / 32;  // 10: each fills 32 rows (4 instructions of 8 rows)
+    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows, uint64_t* __restrict__ stamps) {
+  uint64_t st[5] = {0, 0, 0, 0, 0}, rt0 = 0;
+  if constexpr (ST) {
+    st[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+  constexpr int WN = 2, TM = 192, TN = 128, CPR = 8, NA = 3;
+  constexpr int BUFA = TM * CPR, BUFB = TN * CPR;
+  constexpr int DMA_WAVES = (TM + TN) / 32;  // 10: each fills 32 rows (4 instructions of 8 rows)
+  static_assert(NA * BUFA * 16 + NBR * BUFB * 16 + (3 * TM + 2 * TN) * 4 <= 160 * 1024, "LDS");
   int64_t tx, ty;
   xcd_tile(tx, ty);
   const int M = *m_dev;
   if (tx * TM >= M) return;  // uniform: no barrier reached
-  __shared__ u4 lds[NB * BUF + (3 * TM + 2 * TN) / 4];
-  float* s_asq = (float*)(lds + NB * BUF);
+  __shared__ u4 lds[NA * BUFA + NBR * BUFB + (3 * TM + 2 * TN) / 4];
+  u4* const ldsA = lds;
+  u4* const ldsB = lds + NA * BUFA;
+  float* s_asq = (float*)(lds + NA * BUFA + NBR * BUFB);
   int32_t* s_ash = (int32_t*)(s_asq + TM);
   int32_t* s_orow = s_ash + TM;
   float* s_bsq = (float*)(s_orow + TM);
@@ -556,13 +580,15 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
     s_bsq[tid - TM] = Bsq[cc];
     s_bsh[tid - TM] = Bsh[cc];
   }
-  // DMA sources: wave w < 10 fills stage rows 32 w + 8 i + (lane >> 3); lane
-  // position p = lane & 7 takes global chunk p ^ ((row >> 1) & 7) (the read
-  // swizzle); A rows past M re-read a valid row (never stored)
+  // DMA sources: wave w < 10 fills stage rows 32 w + 8 i + (lane >> 3) (rows
+  // >= TM: B row r - TM of its own ring); lane position p = lane & 7 takes
+  // global chunk p ^ ((row >> 1) & 7) (the read swizzle; TM is a multiple of
+  // 16, so B rows keep it re-based at 0); A rows past M re-read a valid row
+  // (never stored)
   const u4* src[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int r = min(32 * wave + 8 * i + (lane >> 3), ROWS - 1);
+    const int r = min(32 * wave + 8 * i + (lane >> 3), TM + TN - 1);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int64_t grow = r < TM ? (int64_t)a_rows[min(m0 + r, (int64_t)M - 1)] : n0 + (r - TM);
     src[i] = (r < TM ? A : B) + grow * rstride + c;
@@ -570,23 +596,24 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
   const bool dma_wave = wave < DMA_WAVES;
   const bool b_wave = 32 * wave >= TM;  // waves 6 .. 9 stage B rows only (TM = 192 = 6 x 32)
   auto dma = [&](int kb) {
-    u4* dst = lds + (kb % NB) * BUF + 32 * wave * CPR;
     if (b_wave) {
+      u4* dst = ldsB + (kb % NBR) * BUFB + (32 * wave - TM) * CPR;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
                                          (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, BAUX);
     } else {
+      u4* dst = ldsA + (kb % NA) * BUFA + 32 * wave * CPR;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(src[i] + (int64_t)kb * 8),
                                          (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
     }
   };
+  const int ahead = b_wave ? NBR - 1 : NA - 1;  // blocks a staging wave keeps issued past the current one
   __syncthreads();  // row data written (no DMA in flight yet)
   if (dma_wave) {
-    dma(0);
-    if (nkb > 1) dma(1);
+    for (int b = 0; b < ahead && b < nkb; ++b) dma(b);
   }
 
   f16v H[2], P[2], Q[2];
@@ -596,27 +623,37 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
     for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
   const int sw = ((lane & 31) >> 1) & 7;
   const int ra = (wm * 32 + (lane & 31)) * CPR;
-  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  const int rb0 = (wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
   const bool live = m0 + wm * 32 < M;  // a wave whose rows all lie past M only stages
   for (int kb = 0; kb < nkb; ++kb) {
-    // retire block kb's DMA (block kb + 1 may stay in flight)
-    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // retire block kb's DMA: a staging wave's younger blocks kb + 1 .. (4
+    // pieces each) may stay in flight (uniform per wave)
+    const int younger = min(ahead - 1, nkb - 1 - kb);
+    if (younger >= 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (dma_wave && kb + 2 < nkb) dma(kb + 2);  // into the buffer of block kb - 1 (every wave is past it)
+    if constexpr (ST) {
+      if (kb == 0) st[1] = __builtin_amdgcn_s_memtime();
+    }
+    // block kb + ahead into its ring's buffer of block kb - 1 (every wave is past it)
+    if (dma_wave && kb + ahead < nkb) dma(kb + ahead);
     if (live) {
-      const u4* buf = lds + (kb % NB) * BUF;
+      const u4* bufa = ldsA + (kb % NA) * BUFA;
+      const u4* bufb = ldsB + (kb % NBR) * BUFB;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
-        const h8 ah = __builtin_bit_cast(h8, buf[ra + ch]);
-        const h8 al = __builtin_bit_cast(h8, buf[ra + cl]);
-        const h8 bh0 = __builtin_bit_cast(h8, buf[rb0 + ch]);
-        const h8 bl0 = __builtin_bit_cast(h8, buf[rb0 + cl]);
-        const h8 bh1 = __builtin_bit_cast(h8, buf[rb1 + ch]);
-        const h8 bl1 = __builtin_bit_cast(h8, buf[rb1 + cl]);
+        const h8 ah = __builtin_bit_cast(h8, bufa[ra + ch]);
+        const h8 al = __builtin_bit_cast(h8, bufa[ra + cl]);
+        const h8 bh0 = __builtin_bit_cast(h8, bufb[rb0 + ch]);
+        const h8 bl0 = __builtin_bit_cast(h8, bufb[rb0 + cl]);
+        const h8 bh1 = __builtin_bit_cast(h8, bufb[rb1 + ch]);
+        const h8 bl1 = __builtin_bit_cast(h8, bufb[rb1 + cl]);
         H[0] = mfma32_f16(ah, bh0, H[0]);
         H[1] = mfma32_f16(ah, bh1, H[1]);
         P[0] = mfma32_f16(ah, bl0, P[0]);
@@ -627,6 +664,7 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
     }
   }
   if (!live) return;
+  if constexpr (ST) st[2] = __builtin_amdgcn_s_memtime();
 
   // ---- epilogue (the ROWS kernel's): K = exp(-g max(|a|^2 + |b|^2 - 2 dot, 0)) ----
 #pragma unroll
@@ -649,6 +687,20 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
     for (int j = 0; j < 2; ++j) {
       const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
       if (orow >= 0 && (interior || col < N)) out[(int64_t)orow * ldo + col] = H[j][r];
+    }
+  }
+  if constexpr (ST) {
+    st[3] = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[4] = __builtin_amdgcn_s_memtime();
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      uint64_t* o = stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] = st[i];
+      o[5] = rt0;
+      o[6] = rt1;
+      o[7] = 0;
     }
   }
 }
@@ -831,10 +883,6 @@ constexpr int kW64Threads = 512;
 // ahead with counted lgkmcnt waits, so only the block's first group waits on
 // LDS latency (k loop 63.8k -> 59.1k cycles a tile, bench/gram_stamps.py)
 
-// the 32-bit LDS byte address of a __shared__ pointer (asm ds_read operands)
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
 
 template <int NT, int SP = 0>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
@@ -1792,6 +1840,10 @@ void set_split_gemm_variant(int v) { g_split_variant = v; }
 
 // diagnostics: non-null = the wide-wave Gram kernel writes per-workgroup stamps here
 uint64_t* g_gram_stamps = nullptr;
+// diagnostics: non-null = the LDS-DMA rows kernel writes per-workgroup stamps here
+uint64_t* g_rows_stamps = nullptr;
+void set_rows_stamps(uint64_t* p) { g_rows_stamps = p; }
+
 void set_gram_stamps(uint64_t* p) { g_gram_stamps = p; }
 
 int64_t split_row_u4(int dp) { return (int64_t)((dp + 31) / 32) * 8; }
@@ -2081,14 +2133,19 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
       const char* e = std::getenv("DPSVM_ROWS_BNT");
       return e && std::string(e) == "0";
     }();
-    if (b_cached)
-      dev::rbf_rows_split_glds_kernel<0><<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
-          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
-          ldl, out_rows);
-    else
-      dev::rbf_rows_split_glds_kernel<2><<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
-          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
-          ldl, out_rows);
+    // B ring depth: 3 (A/B: DPSVM_ROWS_BRING=5 — 3.42 vs 3.26-3.28 ms at the
+    // synthetic-2m round shape: the kernel is not bound by the B stream's
+    // latency; profiles/r6_rows_kernel.txt)
+    static const int bring = [] {
+      const char* e = std::getenv("DPSVM_ROWS_BRING");
+      return e && atoi(e) == 5 ? 5 : 3;
+    }();
+    auto k = g_rows_stamps ? dev::rbf_rows_split_glds_kernel<2, 3, true>
+             : b_cached ? (bring == 5 ? dev::rbf_rows_split_glds_kernel<0, 5> : dev::rbf_rows_split_glds_kernel<0, 3>)
+                        : (bring == 5 ? dev::rbf_rows_split_glds_kernel<2, 5> : dev::rbf_rows_split_glds_kernel<2, 3>);
+    k<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
+        (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl,
+        out_rows, g_rows_stamps);
   }
   post_launch("rbf_rows_indexed_split", s);
 }

@@ -567,6 +567,15 @@ PYBIND11_MODULE(_C, m) {
                               out_ld, (const int*)out_rows, (void*)stream, split);
   }, py::arg("x"), py::arg("xsq"), py::arg("n"), py::arg("ld"), py::arg("rows"), py::arg("m"), py::arg("gamma"),
         py::arg("out"), py::arg("out_ld"), py::arg("out_rows"), py::arg("stream"), py::arg("split") = false);
+  m.def("k_rows_split_bench", [](uintptr_t x, uintptr_t xsq, int64_t n, int ld, uintptr_t rows, int m_, float gamma,
+                                 uintptr_t out, int64_t out_ld, uintptr_t out_rows, int reps, uintptr_t stream) {
+    py::gil_scoped_release rel;
+    return kernels::rbf_rows_indexed_split_bench((const float*)x, (const float*)xsq, n, ld, (const int*)rows, m_,
+                                                 gamma, (float*)out, out_ld, (const int*)out_rows, reps,
+                                                 (void*)stream);
+  }, "diagnostics: the split row GEMM alone, ms per launch");
+  m.def("k_set_rows_stamps", [](uintptr_t p) { launch::set_rows_stamps((uint64_t*)p); },
+        "diagnostics: the LDS-DMA rows kernel writes 8 u64 stamps per workgroup at p (0: off)");
   m.def("k_set_gram_stamps", [](uintptr_t p) { launch::set_gram_stamps((uint64_t*)p); },
         "diagnostics: the wide-wave Gram kernel writes 8 u64 stamps per workgroup at p (0: off)");
   m.def("k_set_split_gemm_variant", [](int v) { launch::set_split_gemm_variant(v); },

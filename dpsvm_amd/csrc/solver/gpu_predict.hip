@@ -452,6 +452,35 @@ void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const
   (void)hipFree(md);
 }
 
+std::vector<float> rbf_rows_indexed_split_bench(const float* x, const float* xsq, int64_t n, int ld, const int* rows,
+                                                int m, float gamma, float* out, int64_t out_ld, const int* out_rows,
+                                                int reps, void* stream) {
+  DPSVM_CHECK(ld % 16 == 0 && m >= 0 && m <= 4096 && reps > 0, "rbf_rows_indexed_split_bench: arguments");
+  hipStream_t s = (hipStream_t)stream;
+  size_t tb = 0;
+  int32_t* md = dmalloc<int32_t>(1, &tb);
+  HIP_CHECK(hipMemcpyAsync(md, &m, 4, hipMemcpyHostToDevice, s));
+  SplitRows sx(x, n, ld, s);
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  std::vector<float> ms;
+  for (int r = 0; r < reps; ++r) {
+    HIP_CHECK(hipEventRecord(e0, s));
+    launch::rbf_rows_indexed_split(sx.planes, sx.shift, xsq, rows, md, m, sx.planes, sx.shift, xsq, n, ld, gamma, out,
+                                   out_rows, out_ld, s);
+    HIP_CHECK(hipEventRecord(e1, s));
+    HIP_CHECK(hipEventSynchronize(e1));
+    float t = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+    ms.push_back(t);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(md);
+  return ms;
+}
+
 void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* keys, int nq, float gamma,
                 float* out, int64_t out_ld, int rows_per_group, void* stream) {
   DPSVM_CHECK(ld % 16 == 0 && rows_per_group > 0 && rows_per_group % kFusedThreads == 0,
