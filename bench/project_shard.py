@@ -44,16 +44,21 @@ def probe_pass1(path):
     """{P: pass-1 us} at the shard shapes of the probe, with the solver's split:
     the wide pass 1 (the default since round 5) when the probe holds it, else
     the selection-geometry pass 1"""
-    wide, sel = {}, {}
+    wide, sel = {}, {}  # P -> (|ks - the solver's split|, us): the probed split nearest the solver's
     for line in open(path):
         r = json.loads(line)
         if r["rows"] != 60000:
             continue
-        if r.get("wide") and r["ks"] == pass1_v4_splits(r["p1G"]):
-            wide[60000 // r["cols"]] = r["pass1_us_median"]
-        elif not r.get("wide") and r["ks"] == pass1_splits(r["G"]):
-            sel[60000 // r["cols"]] = r["pass1_us_median"]
-    return wide or sel
+        P = 60000 // r["cols"]
+        if r.get("wide"):
+            d = abs(r["ks"] - pass1_v4_splits(r["p1G"]))
+            if P not in wide or d < wide[P][0]:
+                wide[P] = (d, r["pass1_us_median"])
+        else:
+            d = abs(r["ks"] - pass1_splits(r["G"]))
+            if P not in sel or d < sel[P][0]:
+                sel[P] = (d, r["pass1_us_median"])
+    return {P: v[1] for P, v in (wide or sel).items()}
 
 
 def main() -> int:

@@ -102,13 +102,15 @@ def main() -> int:
     raw = np.fromfile(stamp_path + ".rank0", dtype=np.uint64).reshape(4096, 24).astype(np.int64)
     R = min(st.n_rounds_, 4096)
     s = raw[2:R]
-    s = s[(s[:, [0, 1, 2, 3, 4, 6, 7, 8]] > 0).all(axis=1)]
+    # (stamp 8, the gather kernel's exit, is absent when the solve loads its
+    # block itself: direct sub-Gram at world 1)
+    s = s[(s[:, [0, 1, 2, 3, 4, 6, 7]] > 0).all(axis=1)]
     us = lambda v: float(np.round(np.median(v) * 0.01, 2))  # noqa: E731
     out["round_us"] = {
         "period": us(np.diff(s[:, 6])),
         # the candidate rank kernel (stamp 21) + the merge: redundant on every rank
         "merge": us(s[:, 2] - s[:, 21]) if (s[:, 21] > 0).all() else us(s[:, 2] - s[:, 1]),
-        "gather": us(s[:, 8] - s[:, 2]),
+        "gather": us(s[:, 8] - s[:, 2]) if (s[:, 8] > 0).all() else 0.0,
         "load_subgram": us(s[:, 3] - s[:, 0]),
         "solve": us(s[:, 4] - s[:, 3]),
         "select_pass2": us(s[:, 7] - s[:, 6]),
