@@ -852,6 +852,112 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
   }
 }
 
+// The w64 kernels' epilogue (PE, the default): the values two at a time in
+// packed f32 (v_pk_add / v_pk_mul; the same IEEE operations per value, so the
+// same bits as rbf_split_value), stores through buffer descriptors: a lane
+// outside the tile's columns gets an out-of-range offset and rows past M fall
+// beyond the descriptor's size, so the hardware drops them — one address add
+// per store and no exec-mask branch.  The scalar epilogue was ~20 VALU and ~13
+// SALU per value, VALU-issue-bound: 13.4k -> 10.0k cycles a tile
+// (profiles/r6_gram_lds_readahead_ab.json).  Host: the last row tile's
+// (M - m0) x ldo floats < 2^31 bytes.  lane: the caller's (laundered) lane id.
+typedef int i4v_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void w64_epilogue_pe(f16v (&H)[2][2], const f16v (&P)[2][2], const f16v (&Q)[2][2],
+                                                const float* s_sq, const int32_t* s_sh, int lane, int wm, int wn,
+                                                bool mirror, float* out, int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                                int64_t ldo, float gamma) {
+  constexpr int TM = 256, TN = 128;
+  typedef i4v_t i4v;
+  const int hl = lane >> 5;
+  float* const ob = out + m0 * ldo + n0;  // direct block
+  float* const mb = out + n0 * ldo + m0;  // mirrored block (symmetric: M == N)
+  const uint32_t ld = (uint32_t)ldo;
+  const int rlim = (int)min<int64_t>(M - m0, TM);  // tile rows inside [0, M)
+  const int clim = (int)min<int64_t>(N - n0, TN);  // tile columns inside [0, N)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr uint32_t OOB = 0x80000000u;
+  const int64_t ob_bytes = min<int64_t>((M - m0) * ldo * 4 - n0 * 4, (int64_t)OOB);
+  const int64_t mb_bytes = min<int64_t>((N - n0) * ldo * 4 - m0 * 4, (int64_t)OOB);
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, (int)ob_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mb, 0, (int)mb_bytes, 0x00020000);
+  const float ng = -gamma, l2e = 1.4426950408889634f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cl = wn * 64 + 32 * j + (lane & 31);
+    const bool okc = cl < clim;
+    const float bsq = s_sq[TM + cl];
+    const int nbsh = -s_sh[TM + cl];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int lr0 = wm * 64 + 32 * i + 4 * hl;  // value r sits on row lr0 + 8 (r >> 2) + (r & 3)
+      const uint32_t vo = okc ? ((uint32_t)lr0 * ld + (uint32_t)cl) * 4u : OOB;  // value 0's byte offset
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
+        const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int r = 4 * g + e;
+          f2 h, pp, qq;
+          h.x = H[i][j][r];
+          h.y = H[i][j][r + 1];
+          pp.x = P[i][j][r];
+          pp.y = P[i][j][r + 1];
+          qq.x = Q[i][j][r];
+          qq.y = Q[i][j][r + 1];
+          f2 dot, sq, d2, t;
+          {
+#pragma clang fp contract(off)
+            const f2 sum = h + (pp + qq);
+            dot.x = ldexpf(sum.x, nbsh - ash[e]);
+            dot.y = ldexpf(sum.y, nbsh - ash[e + 1]);
+            sq.x = asq[e];
+            sq.y = asq[e + 1];
+            d2 = (sq + bsq) - (dot + dot);  // |a|^2 + |b|^2 - 2 dot (rbf_split_value)
+            d2.x = d2.x > 0.f ? d2.x : 0.f;
+            d2.y = d2.y > 0.f ? d2.y : 0.f;
+            t = (ng * d2) * l2e;  // __expf(-gamma d2) = exp2((-gamma d2) log2 e)
+          }
+          H[i][j][r] = __builtin_amdgcn_exp2f(t.x);
+          H[i][j][r + 1] = __builtin_amdgcn_exp2f(t.y);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          // (a float local first: __builtin_bit_cast of a vector element
+          // subscript reads element 0 in this hipcc)
+          const float hv = H[i][j][r];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hv), rs_o, (int)(vo + (uint32_t)(8 * g + e) * ld * 4u),
+                                                0, 0);
+        }
+      }
+      if (mirror) {
+        // transposed: lane (column cl) writes rows lr .. lr + 3 of mirrored row cl
+        const uint32_t vm = okc ? ((uint32_t)cl * ld + (uint32_t)lr0) * 4u : OOB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int lr = lr0 + 8 * q;
+          f4 v;
+          v.x = H[i][j][4 * q + 0];
+          v.y = H[i][j][4 * q + 1];
+          v.z = H[i][j][4 * q + 2];
+          v.w = H[i][j][4 * q + 3];
+          const uint32_t o = lr + 3 < rlim ? vm + 32u * q : OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v), rs_m, (int)o, 0, 0);
+          if (rlim < TM) {  // uniform: the last row tile — the values of a partial quad one at a time
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t oc = (lr + 3 >= rlim && lr + c < rlim) ? vm + 32u * q + 4u * c : OOB;
+              const float vc = v[c];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vc), rs_m, (int)oc, 0, 0);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Wide-wave LDS-DMA STORE GEMM (variant 5): 256 x 128 tiles, 8 waves of
 // 64 x 64 (2 x 2 MFMA tiles, three accumulators each: 192 accumulator
@@ -884,7 +990,7 @@ constexpr int kW64Threads = 512;
 // LDS latency (k loop 63.8k -> 59.1k cycles a tile, bench/gram_stamps.py)
 
 
-template <int NT, int SP = 0>
+template <int NT, int SP = 0, bool PE = false>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int64_t M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb,
@@ -1083,8 +1189,9 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
   const uint32_t ld = (uint32_t)ldo;
   const int rlim = (int)min<int64_t>(M - m0, TM);  // tile rows inside [0, M)
   const int clim = (int)min<int64_t>(N - n0, TN);  // tile columns inside [0, N)
+  if constexpr (PE) w64_epilogue_pe(H, P, Q, s_sq, s_sh, lane, wm, wn, mirror, out, m0, n0, M, N, ldo, gamma);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < (PE ? 0 : 2); ++j) {
     const int cl = wn * 64 + 32 * j + (lane & 31);
     const bool okc = cl < clim;
     const float bsq = s_sq[TM + cl];
@@ -1209,7 +1316,7 @@ __device__ __forceinline__ void w64p_row_dma(const float* __restrict__ Asq, cons
   }
 }
 
-template <int NT>
+template <int NT, bool PE = false>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int N, int nkb,
@@ -1369,6 +1476,12 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     if (has_next) ROW_DMA(nm0, nn0, par ^ 1);
 
     // ---- epilogue of the w64 kernel (row data from parity `par`) ----
+    if constexpr (PE) {
+      int el = lane;
+      asm volatile("" : "+v"(el));
+      w64_epilogue_pe(H, P, Q, (const float*)(s_rows + par * RD), (const int32_t*)(s_rows + par * RD + ROWS), el, wm,
+                      wn, sym && ty > 2 * tx + (wm >> 1), out, m0, n0, M, N, ldo, gamma);
+    }
     // (the per-lane epilogue addresses are recomputed per tile from a
     // laundered lane id: hoisted out of the tile loop they would hold ~64
     // registers across the k loop)
@@ -1385,7 +1498,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     const int rlim = min(M - m0, TM);
     const int clim = min(N - n0, TN);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < (PE ? 0 : 2); ++j) {
       const int cl = ewn * 64 + 32 * j + (el & 31);
       const bool okc = cl < clim;
       const float bsq = s_sq[TM + cl];
@@ -1975,7 +2088,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
   // symmetric: 10.1-10.8 ms vs 10.9-11.1 for the persistent LDS-DMA kernel,
   // bit-identical; profiles/r4_w64_gram_ab.txt)
   // (32-bit store offsets inside a 256 x 128 tile: ldo < 2^24)
-  if ((variant == 5 || variant == 6 || variant == 7 || variant == 8 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
+  if ((variant == 5 || variant == 6 || variant == 7 || variant == 8 || variant == 11 || variant == 12 || (variant == 0 && (dp + 31) / 32 >= 5)) && ablate == 0 &&
       ldo < (1ll << 24)) {
     static const int nt = [] {
       const char* e = std::getenv("DPSVM_GRAM_NT");  // A/B: 0 plain Gram stores, 1 non-temporal, 2 none (diagnostics)
@@ -1992,7 +2105,10 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       return e ? atoi(e) : 1;
     }();
     const int sp = variant == 5 ? 0 : variant == 6 ? 1 : variant == 8 ? 2 : spread ? 2 : 0;
-    auto kern = g_gram_stamps ? (sp == 2 ? dev::rbf_gemm_split_w64_kernel<3, 2> : dev::rbf_gemm_split_w64_kernel<3, 1>)
+    auto kern = g_gram_stamps ? (variant == 11 ? dev::rbf_gemm_split_w64_kernel<3, 2, true>
+                                 : sp == 2     ? dev::rbf_gemm_split_w64_kernel<3, 2>
+                                               : dev::rbf_gemm_split_w64_kernel<3, 1>)
+                : variant == 11 ? dev::rbf_gemm_split_w64_kernel<0, 2, true>
                 : nt == 2     ? dev::rbf_gemm_split_w64_kernel<2>
                 : nt          ? dev::rbf_gemm_split_w64_kernel<1>
                 : sp == 2     ? dev::rbf_gemm_split_w64_kernel<0, 2>
@@ -2012,7 +2128,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
     // (32-bit indices: the split operand buffers hold (rows + 512) x nkb x 8 u4, the output M x ldo floats)
     const bool idx32 = (M + 512) * (int64_t)nkb * 8 < (1ll << 31) && (N + 512) * (int64_t)nkb * 8 < (1ll << 31) &&
                        M * ldo < (1ll << 32) && N * ldo < (1ll << 32);
-    const bool persist = (variant == 7 || (variant == 0 && persist_env == 1)) && nkb >= 3 && nt == 0 && idx32 &&
+    const bool persist = (variant == 7 || variant == 12 || (variant == 0 && persist_env == 1)) && nkb >= 3 && nt == 0 && idx32 &&
                          tm2 < 65536 && tn < 65536 && (!symmetric || compact);
     if (persist) {
       const int cus = [] {
@@ -2024,7 +2140,8 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const uint32_t* tab = t.dev;
       const int64_t ntiles = t.count;
       const int64_t grid = std::min<int64_t>(ntiles, cus);
-      auto pk = g_gram_stamps ? dev::rbf_gemm_split_w64p_kernel<3> : dev::rbf_gemm_split_w64p_kernel<0>;
+      auto pk = g_gram_stamps ? (variant == 12 ? dev::rbf_gemm_split_w64p_kernel<3, true> : dev::rbf_gemm_split_w64p_kernel<3>)
+                : variant == 12 ? dev::rbf_gemm_split_w64p_kernel<0, true> : dev::rbf_gemm_split_w64p_kernel<0>;
       pk<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>((const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B,
                                                           Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
                                                           symmetric ? 1 : 0, tab, (int)ntiles, (int)tm2, (int)tn,
