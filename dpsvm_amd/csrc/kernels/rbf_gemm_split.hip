@@ -1255,19 +1255,21 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Persistent wide-wave STORE GEMM (variant 7, opt-in: DPSVM_GRAM_PERSIST=1):
-// the w64 kernel's tile, k loop (with SP 2's read-ahead) and epilogue, one
-// workgroup per CU walking tiles L = b, b + G, ... of the same table.  The
-// w64 kernel's stamps put ~11% of a tile in its prologue (row data, then the
-// first LDS-DMA block's latency) with the MFMA pipe idle.  Here the LDS-DMA
-// ring runs on across tiles: during the last two k blocks of tile t the
-// prefetch slots load blocks 0 and 1 of tile t + 1 (a block counter g over all
-// tiles picks the buffer, g mod 3), and the next tile's |x|^2 and shifts arrive
-// by LDS-DMA into the other parity of a row-data area (issued after tile t's k
-// loop); every epilogue ends with vmcnt(0), so the loop's one uniform wait
-// holds at the next tile's first block.  80.3k vs 84.5k cycles a tile, but the
-// clock the chip holds drops with it: 8.97 vs 9.01 ms symmetric, 2.48 vs 2.52
-// ms for the P = 8 slab (profiles/r6_gram_lds_readahead_ab.json).  Same MFMA
+// Persistent wide-wave STORE GEMM (the default; PE: the packed epilogue,
+// variant 12; variant 7 without it; DPSVM_GRAM_PERSIST=0 for the tile-per-
+// workgroup kernel): the w64 kernel's tile, k loop (with SP 2's read-ahead)
+// and epilogue, one workgroup per CU walking tiles L = b, b + G, ... of the
+// same table.  The w64 kernel's stamps put ~12% of a tile in its prologue (row
+// data, then the first LDS-DMA block's latency) with the MFMA pipe idle, and
+// ~7% of the CU time between workgroups (237.5 of 256 in flight).  Here the
+// LDS-DMA ring runs on across tiles: during the last two k blocks of tile t
+// the prefetch slots load blocks 0 and 1 of tile t + 1 (a block counter g
+// over all tiles picks the buffer, g mod 3), and the next tile's |x|^2 and
+// shifts arrive by LDS-DMA into the other parity of a row-data area (issued
+// after tile t's k loop); every epilogue ends with vmcnt(0), so the loop's one
+// uniform wait holds at the next tile's first block.  With the packed
+// epilogue: 8.86 vs 9.01 ms symmetric, 2.30 vs 2.47 ms for the P = 8 slab
+// against the w64 kernel (profiles/r6_gram_lds_readahead_ab.json).  Same MFMA
 // sequence per output: bit-identical to the w64 kernel.
 // NT 3: per-tile stamps (first wait, first block landed, k loop done, stores
 // issued) and s_memrealtime at the tile's start / end into stamps[8 L ..].
@@ -2095,40 +2097,45 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       return e ? atoi(e) : 0;
     }();
     const int64_t tm2 = (M + 255) / 256;
-    // the LDS-DMA issue spread over the MFMA groups: 9.41 -> 9.27 ms symmetric,
-    // 2.65 -> 2.56 ms for the P = 8 slab (profiles/r6_gram_dma_spread_ab.json);
-    // with the LDS reads one MFMA group ahead (default): 9.22-9.27 -> 8.81-8.93
-    // ms, 2.56-2.70 -> 2.41-2.55 ms; all bit-identical (profiles/r6_gram_lds_readahead_ab.json).
-    // A/B: DPSVM_GRAM_SPREAD=0 (neither) or variants 5 (neither), 6 (spread), 8 (both)
+    // Defaults, each bit-identical to the others (profiles/r6_gram_lds_readahead_ab.json):
+    //  - the LDS-DMA issue spread over the MFMA groups (9.41 -> 9.27 ms symmetric)
+    //    with the operand reads one MFMA group ahead (-> 8.81-8.93 ms);
+    //  - the packed-f32 / buffer-store epilogue (13.4k -> 10.0k cycles a tile);
+    //  - persistent over the tiles (below): 9.01 -> 8.86 ms symmetric, 2.47 -> 2.30 ms
+    //    for the P = 8 slab against the tile-per-workgroup kernel of the same tree.
+    // A/B: variants 5 (no spread), 6 (spread), 8 (spread + read-ahead), 11 (+ PE),
+    // 7 / 12 persistent without / with PE; DPSVM_GRAM_SPREAD=0, DPSVM_GRAM_PERSIST=0
     static const int spread = [] {
       const char* e = std::getenv("DPSVM_GRAM_SPREAD");
       return e ? atoi(e) : 1;
     }();
-    const int sp = variant == 5 ? 0 : variant == 6 ? 1 : variant == 8 ? 2 : spread ? 2 : 0;
-    auto kern = g_gram_stamps ? (variant == 11 ? dev::rbf_gemm_split_w64_kernel<3, 2, true>
-                                 : sp == 2     ? dev::rbf_gemm_split_w64_kernel<3, 2>
-                                               : dev::rbf_gemm_split_w64_kernel<3, 1>)
-                : variant == 11 ? dev::rbf_gemm_split_w64_kernel<0, 2, true>
-                : nt == 2     ? dev::rbf_gemm_split_w64_kernel<2>
-                : nt          ? dev::rbf_gemm_split_w64_kernel<1>
-                : sp == 2     ? dev::rbf_gemm_split_w64_kernel<0, 2>
-                : sp == 1     ? dev::rbf_gemm_split_w64_kernel<0, 1>
-                              : dev::rbf_gemm_split_w64_kernel<0>;
+    const int sp = variant == 5 ? 0 : variant == 6 ? 1 : variant == 8 || variant == 11 ? 2 : spread ? 2 : 0;
+    const bool pe = variant == 11 || variant == 12 || (variant == 0 && spread);
+    auto kern = g_gram_stamps ? (pe        ? dev::rbf_gemm_split_w64_kernel<3, 2, true>
+                                 : sp == 2 ? dev::rbf_gemm_split_w64_kernel<3, 2>
+                                           : dev::rbf_gemm_split_w64_kernel<3, 1>)
+                : nt == 2 ? dev::rbf_gemm_split_w64_kernel<2>
+                : nt      ? dev::rbf_gemm_split_w64_kernel<1>
+                : pe      ? dev::rbf_gemm_split_w64_kernel<0, 2, true>
+                : sp == 2 ? dev::rbf_gemm_split_w64_kernel<0, 2>
+                : sp == 1 ? dev::rbf_gemm_split_w64_kernel<0, 1>
+                          : dev::rbf_gemm_split_w64_kernel<0>;
     static const bool compact = [] {  // A/B: DPSVM_GRAM_COMPACT=0 launches the full grid (half exit at once)
       const char* e = std::getenv("DPSVM_GRAM_COMPACT");
       return !(e && e[0] == '0');
     }();
-    // persistent over the tiles (variant 7; A/B: DPSVM_GRAM_PERSIST=0|1): one
-    // workgroup per CU, the LDS-DMA ring running on across tiles
+    // persistent over the tiles (the default; variants 7 / 12; A/B:
+    // DPSVM_GRAM_PERSIST=0): one workgroup per CU, the LDS-DMA ring running on
+    // across tiles
     static const int persist_env = [] {
       const char* e = std::getenv("DPSVM_GRAM_PERSIST");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 1;
     }();
     const int nkb = (dp + 31) / 32;
     // (32-bit indices: the split operand buffers hold (rows + 512) x nkb x 8 u4, the output M x ldo floats)
     const bool idx32 = (M + 512) * (int64_t)nkb * 8 < (1ll << 31) && (N + 512) * (int64_t)nkb * 8 < (1ll << 31) &&
                        M * ldo < (1ll << 32) && N * ldo < (1ll << 32);
-    const bool persist = (variant == 7 || variant == 12 || (variant == 0 && persist_env == 1)) && nkb >= 3 && nt == 0 && idx32 &&
+    const bool persist = (variant == 7 || variant == 12 || (variant == 0 && persist_env == 1 && spread)) && nkb >= 3 && nt == 0 && idx32 &&
                          tm2 < 65536 && tn < 65536 && (!symmetric || compact);
     if (persist) {
       const int cus = [] {
@@ -2140,8 +2147,8 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const uint32_t* tab = t.dev;
       const int64_t ntiles = t.count;
       const int64_t grid = std::min<int64_t>(ntiles, cus);
-      auto pk = g_gram_stamps ? (variant == 12 ? dev::rbf_gemm_split_w64p_kernel<3, true> : dev::rbf_gemm_split_w64p_kernel<3>)
-                : variant == 12 ? dev::rbf_gemm_split_w64p_kernel<0, true> : dev::rbf_gemm_split_w64p_kernel<0>;
+      auto pk = g_gram_stamps ? (pe ? dev::rbf_gemm_split_w64p_kernel<3, true> : dev::rbf_gemm_split_w64p_kernel<3>)
+                : pe ? dev::rbf_gemm_split_w64p_kernel<0, true> : dev::rbf_gemm_split_w64p_kernel<0>;
       pk<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>((const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B,
                                                           Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
                                                           symmetric ? 1 : 0, tab, (int)ntiles, (int)tm2, (int)tn,
