@@ -327,7 +327,8 @@ struct alignas(16) WsCtrl {
   int32_t n_miss;    // cache mode: rows of the current set without a line (computed this round)
   int32_t hand;      // cache mode: next line the victim window starts at
   int32_t solve_cnt; // multi-block: solve workgroups finished this round (the last one commits)
-  int32_t pad[2];
+  int32_t rank_cnt;  // multi-block: rank workgroups finished this round (the last one merges)
+  int32_t pad[1];
   // block p's rows at [p * q_max, p * q_max + qb[par][p]) (one block: idx[par][0..q))
   int32_t idx[2][kWsMaxAll];     // working set per round parity (global rows), newest first
   int32_t line[2][kWsMaxAll];    // the line holding each member's kernel row (dense mode: the row itself)

@@ -5,6 +5,9 @@
 // Round structure and shared helpers: ws_common.hpp.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
+
 #include "dpsvm/common.hpp"
 #include "dpsvm/device_state.hpp"
 #include "device_util.hpp"
@@ -430,15 +433,25 @@ __global__ __launch_bounds__(kXCollectThreads) void ws_xcollect_cand_kernel(WsAr
 // over keys).
 constexpr int kRankThreads = 512;
 constexpr int kRankChunks = kWsMaxGroups * kWsCand / 32;  // 32 keys per workgroup, 16 threads per key
-__global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
-  constexpr int NK = kWsMaxGroups * kWsCand;
-  constexpr int KPW = NK / kRankChunks, SUB = kRankThreads / KPW, PAIRS = NK / (2 * SUB);
-  static_assert(NK % kRankChunks == 0 && kRankThreads % KPW == 0 && SUB == 16 && NK % (2 * SUB) == 0, "rank geometry");
-  __shared__ uint64_t s_k[NK];
-  __shared__ int s_real[kRankThreads / 64];
+template <int T>
+struct RankLds {
+  uint64_t k[kWsMaxGroups * kWsCand];
+  int real[T / 64];
+};
+// one rank workgroup's work (the caller checked c->done): T threads rank T /
+// 16 keys of one side, 16 threads per key; 2 x NK x 16 / T workgroups
+template <int T>
+constexpr int rank_chunks() { return kWsMaxGroups * kWsCand * 16 / T; }
+template <int T, bool kCoherent = false>
+__device__ __forceinline__ void ws_rank_body(const WsArgs& a, RankLds<T>& L) {
+  constexpr int NK = kWsMaxGroups * kWsCand, CH = rank_chunks<T>();
+  constexpr int KPW = NK / CH, SUB = T / KPW, PAIRS = NK / (2 * SUB);
+  static_assert(NK % CH == 0 && T % KPW == 0 && SUB == 16 && NK % (2 * SUB) == 0, "rank geometry");
+  constexpr int kRankThreads = T;
+  uint64_t* const s_k = L.k;
+  int* const s_real = L.real;
   const WsCtrl* c = a.ctrl;
-  if (c->done != kRunning) return;
-  const int side = blockIdx.x / kRankChunks, chunk = blockIdx.x % kRankChunks, tid = threadIdx.x;
+  const int side = blockIdx.x / CH, chunk = blockIdx.x % CH, tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) WS_STAMP(21);
   const int G = a.G_all;
   int real = 0;
@@ -477,11 +490,36 @@ __global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
 #pragma unroll
   for (int o = 1; o < SUB; o <<= 1) cnt += __shfl_xor(cnt, o);
   uint64_t* out = a.sorted + (size_t)side * NK;
-  if (sub == 0 && k != kKeyNone) out[cnt] = k;
-  if (tid < KPW && chunk * KPW + tid >= n_real) out[chunk * KPW + tid] = kKeyNone;
+  // coherent (the fused rank + merge): agent-scope (sc1) stores, read by
+  // another workgroup of the same launch with sc1 loads — no L2 write-back
+  auto put = [&](int i, uint64_t v) {
+    if constexpr (kCoherent) __hip_atomic_store(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else out[i] = v;
+  };
+  if (sub == 0 && k != kKeyNone) put(cnt, k);
+  if (tid < KPW && chunk * KPW + tid >= n_real) put(chunk * KPW + tid, kKeyNone);
 }
 
-__global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
+__global__ __launch_bounds__(kRankThreads) void ws_rank_kernel(WsArgs a) {
+  static_assert(rank_chunks<kRankThreads>() == kRankChunks, "rank grid");
+  __shared__ RankLds<kRankThreads> L;
+  if (a.ctrl->done != kRunning) return;
+  ws_rank_body<kRankThreads>(a, L);
+}
+
+struct MergeLds {
+  __attribute__((aligned(16))) int32_t hk[2][kMH];  // [side] hash keys (row indices), 4-slot buckets
+  uint16_t hv[2][kMH];                               // [side] their ranks
+  int32_t keep[kWsMaxAll + 2];
+  int32_t idx[kWsMaxAll];
+  int wsum[kWsMergeThreads / 64];
+  int msum[(kWsMaxGroups * kWsCand / kWsMergeThreads) * (kWsMergeThreads / 64)];
+};
+// the merge on one workgroup (the caller checked c->done).  coherent: the
+// ranked keys were written by other workgroups of the same launch (the fused
+// rank + merge): read them with agent-scope loads, not through this XCD's L2
+template <bool kCoherent>
+__device__ __forceinline__ void ws_merge_multi_body(const WsArgs& a, MergeLds& L) {
   constexpr int T = kWsMergeThreads;
   constexpr int NK = kWsMaxGroups * kWsCand;  // keys per side
   constexpr int X = NK / T;                   // keys per thread and side: elements tid + x T
@@ -489,19 +527,15 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   static_assert(NK % T == 0 && kWsMaxAll % T == 0 && U <= 7, "previous union: <= 7 rows per thread (3-bit scans)");
   static_assert(kMH == kWsWindowMulti && kWsWindowMulti == 8 * T && NK <= 65536,
                 "cache mode: the CLOCK window's pins alias the low side's key table; 16-bit ranks");
-  __shared__ __attribute__((aligned(16))) int32_t s_hk[2][kMH];  // [side] hash keys (row indices), 4-slot buckets
-  __shared__ uint16_t s_hv[2][kMH];  // [side] their ranks
-  __shared__ int32_t s_keep[kWsMaxAll + 2];
-  __shared__ int32_t s_idx[kWsMaxAll];
-  __shared__ int s_wsum[T / 64];
-  __shared__ int s_msum[X * (T / 64)];
+  auto& s_hk = L.hk;
+  auto& s_hv = L.hv;
+  int32_t* const s_keep = L.keep;
+  int32_t* const s_idx = L.idx;
+  int* const s_wsum = L.wsum;
+  int* const s_msum = L.msum;
   WsCtrl* c = a.ctrl;
   const int tid = threadIdx.x;
   const bool lead = tid == 0;
-  if (c->done != kRunning) {
-    if (lead) c->n_apply = 0;  // applied by the last ws_select already
-    return;
-  }
   if (lead) WS_STAMP(1);
   const int par = (int)(c->outer & 1);
   const int P = max(1, min(c->p_act, a.blocks)), Qmax = P * a.q_max;
@@ -513,12 +547,16 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   for (int h = 0; h < U; ++h) pidx[h] = U * tid + h < q_prev ? c->uidx[par ^ 1][U * tid + h] : -1;
   // keys e = tid + x T of each side, in ascending order (ws_rank)
   uint64_t v[2][X];  // [side][element]
+  auto ld_sorted = [&](int i) -> uint64_t {
+    if constexpr (kCoherent) return __hip_atomic_load(a.sorted + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return a.sorted[i];
+  };
 #pragma unroll
   for (int x = 0; x < X; ++x) {
-    v[0][x] = a.sorted[tid + x * T];
-    v[1][x] = a.sorted[NK + tid + x * T];
+    v[0][x] = ld_sorted(tid + x * T);
+    v[1][x] = ld_sorted(NK + tid + x * T);
   }
-  const uint64_t gu = a.sorted[0], gl = a.sorted[NK];  // each side's smallest key
+  const uint64_t gu = ld_sorted(0), gl = ld_sorted(NK);  // each side's smallest key
   for (int t = tid; t < 2 * kMH; t += T) (&s_hk[0][0])[t] = -1;
   if (lead) WS_STAMP(20);
   __syncthreads();
@@ -749,6 +787,47 @@ __global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs 
   }
 }
 
+__global__ __launch_bounds__(kWsMergeThreads) void ws_merge_multi_kernel(WsArgs a) {
+  __shared__ MergeLds L;
+  if (a.ctrl->done != kRunning) {
+    if (threadIdx.x == 0) a.ctrl->n_apply = 0;  // applied by the last ws_select already
+    return;
+  }
+  ws_merge_multi_body<false>(a, L);
+}
+
+// rank + merge in one launch: the rank workgroups publish their keys with
+// agent-scope (sc1) stores, every storing wave waits for them, then one lane a
+// workgroup takes a ticket (agent-scope add); the workgroup whose add comes
+// last runs the merge, reading the keys with sc1 loads — the hand-off form of
+// MI355X_MICROARCH.md that needs no L2 write-back or invalidate (a
+// __threadfence in each of the 128 workgroups cost ~30 us a round, measured)
+// — one launch gap and its dispatch less per round.
+// LDS: the merge's tables, the rank's key copy aliased onto them; the merge's
+// workgroup shape (1,024 threads: 2 x 64 rank workgroups of 64 keys).
+__global__ __launch_bounds__(kWsMergeThreads) void ws_rank_merge_kernel(WsArgs a) {
+  __shared__ union {
+    RankLds<kWsMergeThreads> r;
+    MergeLds m;
+  } L;
+  __shared__ int s_last;
+  WsCtrl* c = a.ctrl;
+  if (c->done != kRunning) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) c->n_apply = 0;  // (the merge's early exit)
+    return;
+  }
+  ws_rank_body<kWsMergeThreads, true>(a, L.r);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores done
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(&c->rank_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (int)gridDim.x - 1 ? 1 : 0;
+  __syncthreads();
+  if (!s_last) return;  // uniform
+  if (threadIdx.x == 0) c->rank_cnt = 0;  // the next round's tickets (a later launch)
+  ws_merge_multi_body<true>(a, L.m);
+}
+
 
 // P x q_max workgroups: workgroup p q_max + a gathers row a of block p's
 // sub-Gram (block p's columns) and the row's f / alpha / y
@@ -829,10 +908,19 @@ void ws_merge_multi(const WsArgs& a, hipStream_t s) {
               "(cache mode) <= 4096 union rows and L >= 2 P q_max + 4096 lines");
   DPSVM_CHECK(a.sorted != nullptr, "ws_merge_multi: no sort buffer");
   DPSVM_CHECK(!a.xpeer || a.xcw >= 4 * kWsCand, "ws_merge_multi: peer exchange slots too narrow");
-  dev::ws_rank_kernel<<<2 * dev::kRankChunks, dev::kRankThreads, 0, s>>>(a);
-  post_launch("ws_rank", s);
-  dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
-  post_launch("ws_merge_multi", s);
+  static const bool split = [] {  // A/B: DPSVM_WS_RANK_MERGE=split, the two launches of round 5
+    const char* e = std::getenv("DPSVM_WS_RANK_MERGE");
+    return e && std::string(e) == "split";
+  }();
+  if (split) {
+    dev::ws_rank_kernel<<<2 * dev::kRankChunks, dev::kRankThreads, 0, s>>>(a);
+    post_launch("ws_rank", s);
+    dev::ws_merge_multi_kernel<<<1, kWsMergeThreads, 0, s>>>(a);
+    post_launch("ws_merge_multi", s);
+  } else {
+    dev::ws_rank_merge_kernel<<<2 * dev::rank_chunks<kWsMergeThreads>(), kWsMergeThreads, 0, s>>>(a);
+    post_launch("ws_rank_merge", s);
+  }
 }
 
 void ws_gather(const WsArgs& a, hipStream_t s) {
