@@ -56,7 +56,7 @@ def main():
     cols = torch.arange(0, n, max(1, n // 4096), device="cuda")[:4096]
     ref = torch.exp(-(1.0 / d) * torch.cdist(xr[sel].double(), xr[cols].double()) ** 2)
     err = float((out[:4, cols].double() - ref).abs().max())
-    res = {"n": n, "d": d, "m": m, "ring": os.environ.get("DPSVM_ROWS_BRING", "5"), "ms_median": round(med, 4),
+    res = {"n": n, "d": d, "m": m, "ring": os.environ.get("DPSVM_ROWS_BRING", "3"), "persist": os.environ.get("DPSVM_ROWS_PERSIST", "1"), "ms_median": round(med, 4),
            "ms_min": round(float(min(ms)), 4), "b_stream_TBps": round(b_bytes / med / 1e9, 2),
            "split_peak_share": round(flops / (med * 1e-3) / 2.5e15, 3), "max_abs_err_vs_f64": err}
     if a.stamps:

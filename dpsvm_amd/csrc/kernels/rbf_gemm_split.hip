@@ -706,6 +706,200 @@ __global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_kerne
 }
 
 // ---------------------------------------------------------------------------
+// Persistent LDS-DMA ROWS GEMM (the default for one tile row, M <= 192, and
+// nkb >= 3: a one-block ws-cache round's misses against all of this rank's B
+// rows — synthetic-2m's round).  The tile-per-workgroup kernel above spends
+// ~8% of a tile in its prologue (the miss rows' data and DMA sources, the
+// first blocks' latency) and the device runs ~239 of 256 workgroups at a time
+// (stamps, profiles/r6_rows_kernel.txt).  Here one workgroup per CU walks
+// column tiles ty = b, b + G, ...: the A side (the misses' |x|^2, shifts,
+// output lines and DMA sources) is set up once, and the DMA rings run on
+// across tiles — during a tile's last two k blocks the prefetch slots load
+// blocks 0 and 1 of the next (A's are the same blocks, B's the next tile's
+// rows), the next tile's B row data is loaded into registers during the k
+// loop and stored into the other parity of a row-data area after it.  Every
+// DMA wave issues 4 pieces every k block (the last tile re-loads its own
+// blocks 0 / 1 into dead buffers), so one uniform vmcnt(4) retires a block;
+// each epilogue ends with vmcnt(0).  Same MFMA sequence and epilogue per tile:
+// bit-identical to the kernel above.
+// ---------------------------------------------------------------------------
+template <int BAUX>
+__global__ __launch_bounds__(kRowsGldsThreads, 1) void rbf_rows_split_glds_persist_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
+    const int32_t* __restrict__ a_rows, const int32_t* __restrict__ m_dev, const u4* __restrict__ B,
+    const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int64_t N, int nkb, float gamma,
+    float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows, int ntiles) {
+  constexpr int WN = 2, TM = 192, TN = 128, CPR = 8, NBUF = 3;
+  constexpr int BUFA = TM * CPR, BUFB = TN * CPR;
+  constexpr int DMA_WAVES = (TM + TN) / 32;  // 10: waves 0-5 stage A rows, 6-9 B rows (4 pieces of 8 rows each)
+  __shared__ u4 lds[NBUF * BUFA + NBUF * BUFB + (3 * TM + 4 * TN) / 4];
+  u4* const ldsA = lds;
+  u4* const ldsB = lds + NBUF * BUFA;
+  float* const s_asq = (float*)(lds + NBUF * (BUFA + BUFB));
+  int32_t* const s_ash = (int32_t*)(s_asq + TM);
+  int32_t* const s_orow = s_ash + TM;
+  float* const s_bsq = (float*)(s_orow + TM);    // [2][TN] by parity
+  int32_t* const s_bsh = (int32_t*)(s_bsq + 2 * TN);  // [2][TN]
+  const int M = *m_dev;
+  const int G = gridDim.x;
+  int ty = blockIdx.x;
+  if (ty >= ntiles || M <= 0) return;  // uniform
+  // (the wave index in an SGPR: the epilogue's row addresses stay scalar
+  // instead of 16 VGPRs hoisted across the tile loop)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int64_t rstride = (int64_t)nkb * 8;  // u4 per split row
+  if (tid < TM) {
+    const int64_t ar = a_rows[min(tid, M - 1)];
+    s_asq[tid] = Asq[ar];
+    s_ash[tid] = Ash[ar];
+    s_orow[tid] = tid < M ? out_rows[tid] : -1;
+  } else if (tid < TM + TN) {
+    const int64_t cc = min((int64_t)ty * TN + (tid - TM), N - 1);
+    s_bsq[tid - TM] = Bsq[cc];
+    s_bsh[tid - TM] = Bsh[cc];
+  }
+  // DMA sources: the kernel above's geometry; A's fixed for the launch, B's as
+  // a per-lane offset from the tile's first row (a uniform base per tile)
+  const bool dma_wave = wave < DMA_WAVES;
+  const bool b_wave = 32 * wave >= TM;
+  // (32-bit u4 offsets: launcher, (N + 512) x nkb x 8 < 2^32; registers are
+  // what the 96 accumulators leave at three waves per SIMD)
+  uint32_t off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = min(32 * wave + 8 * i + (lane >> 3), TM + TN - 1);
+    const uint32_t c = (uint32_t)((lane & 7) ^ ((r >> 1) & 7));
+    off[i] = r < TM ? (uint32_t)a_rows[min(r, M - 1)] * (uint32_t)rstride + c : (uint32_t)(r - TM) * (uint32_t)rstride + c;
+  }
+  // piece set of global block g (kb of tile tt): into ring buffer g % 3
+  auto dma = [&](uint32_t g, int kb, int tt) {
+    const u4* base = b_wave ? B + (int64_t)tt * TN * rstride + (int64_t)kb * 8 : A + (int64_t)kb * 8;  // uniform
+    u4* dst = b_wave ? ldsB + (g % NBUF) * BUFB + (32 * wave - TM) * CPR : ldsA + (g % NBUF) * BUFA + 32 * wave * CPR;
+    if (b_wave) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[i]),
+                                         (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, BAUX);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[i]),
+                                         (__attribute__((address_space(3))) void*)(dst + 8 * i * CPR), 16, 0, 0);
+    }
+  };
+  __syncthreads();  // row data written (no DMA in flight yet)
+  uint32_t g = 0;   // k blocks started over all of this workgroup's tiles
+  if (dma_wave) {
+    dma(0, 0, ty);
+    dma(1, 1, ty);  // (launcher: nkb >= 3)
+  }
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra = (wm * 32 + (lane & 31)) * CPR;
+  const int rb0 = (wn * 64 + (lane & 31)) * CPR, rb1 = rb0 + 32 * CPR;
+  const bool live = wm * 32 < M;  // a wave whose rows all lie past M only stages
+  int par = 0;
+  while (true) {
+    const int tn_next = ty + G;
+    const bool has_next = tn_next < ntiles;  // uniform
+    const int tp = has_next ? tn_next : ty;  // the last tile prefetches itself into dead buffers
+    // the next tile's B row data, in flight across the k loop
+    float nbsq = 0.f;
+    int32_t nbsh = 0;
+    if (has_next && tid >= TM && tid < TM + TN) {
+      const int64_t cc = min((int64_t)tn_next * TN + (tid - TM), N - 1);
+      nbsq = Bsq[cc];
+      nbsh = Bsh[cc];
+    }
+    f16v H[2], P[2], Q[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) H[j][r] = P[j][r] = Q[j][r] = 0.f;
+    for (int kb = 0; kb < nkb; ++kb) {
+      // block kb landed: only block kb + 1's 4 pieces may stay in flight
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // block kb + 2 of this tile, or block kb + 2 - nkb of the next, into the
+      // buffer of block g - 1 (every wave is past it)
+      if (dma_wave) {
+        const bool own = kb + 2 < nkb;
+        dma(g + 2, own ? kb + 2 : kb + 2 - nkb, own ? ty : tp);
+      }
+      if (live) {
+        const u4* bufa = ldsA + (g % NBUF) * BUFA;
+        const u4* bufb = ldsB + (g % NBUF) * BUFB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int ch = (2 * ks + hl) ^ sw, cl = (4 + 2 * ks + hl) ^ sw;
+          const h8 ah = __builtin_bit_cast(h8, bufa[ra + ch]);
+          const h8 al = __builtin_bit_cast(h8, bufa[ra + cl]);
+          const h8 bh0 = __builtin_bit_cast(h8, bufb[rb0 + ch]);
+          const h8 bl0 = __builtin_bit_cast(h8, bufb[rb0 + cl]);
+          const h8 bh1 = __builtin_bit_cast(h8, bufb[rb1 + ch]);
+          const h8 bl1 = __builtin_bit_cast(h8, bufb[rb1 + cl]);
+          H[0] = mfma32_f16(ah, bh0, H[0]);
+          H[1] = mfma32_f16(ah, bh1, H[1]);
+          P[0] = mfma32_f16(ah, bl0, P[0]);
+          P[1] = mfma32_f16(ah, bl1, P[1]);
+          Q[0] = mfma32_f16(al, bh0, Q[0]);
+          Q[1] = mfma32_f16(al, bh1, Q[1]);
+        }
+      }
+      ++g;
+    }
+    // the next tile's B row data into the other parity (last read by the
+    // previous tile's epilogue, before this tile's first barrier)
+    if (has_next && tid >= TM && tid < TM + TN) {
+      s_bsq[(par ^ 1) * TN + (tid - TM)] = nbsq;
+      s_bsh[(par ^ 1) * TN + (tid - TM)] = nbsh;
+    }
+    if (live) {
+      // ---- epilogue (the kernel above's) ----
+      // (per-lane addresses from a laundered lane id: hoisted out of the tile
+      // loop they would hold registers across the k loop and spill)
+      int el = lane;
+      asm volatile("" : "+v"(el));
+      const int ehl = el >> 5;
+      const int64_t n0 = (int64_t)ty * TN;
+      const float* bq = s_bsq + par * TN;
+      const int32_t* bs = s_bsh + par * TN;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cb = wn * 64 + 32 * j + (el & 31);
+        const float bsq = bq[cb];
+        const int bsh = bs[cb];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * ehl;
+          const float dot = ldexpf(H[j][r] + (P[j][r] + Q[j][r]), -(s_ash[lr] + bsh));
+          H[j][r] = rbf_split_value(s_asq[lr], bsq, dot, gamma);
+        }
+      }
+      const bool interior = n0 + TN <= N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int32_t orow = s_orow[wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * ehl];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t col = n0 + wn * 64 + 32 * j + (el & 31);
+          if (orow >= 0 && (interior || col < N)) out[(int64_t)orow * ldo + col] = H[j][r];
+        }
+      }
+    }
+    // the stores and the next tile's blocks 0 / 1 retired: the loop's uniform
+    // vmcnt(4) holds at the next tile's first block (and no DMA is in flight
+    // when the kernel ends)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!has_next) break;
+    ty = tn_next;
+    par ^= 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent small-K ROWS GEMM (nkb <= 2 k blocks: d <= 64, covtype's 54
 // features).  There a tile is two k blocks of MFMA work against 24-98 KiB of
 // operand and store traffic, so a tile-per-workgroup grid is a chain of
@@ -2267,9 +2461,28 @@ void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq,
     auto k = g_rows_stamps ? dev::rbf_rows_split_glds_kernel<2, 3, true>
              : b_cached ? (bring == 5 ? dev::rbf_rows_split_glds_kernel<0, 5> : dev::rbf_rows_split_glds_kernel<0, 3>)
                         : (bring == 5 ? dev::rbf_rows_split_glds_kernel<2, 5> : dev::rbf_rows_split_glds_kernel<2, 3>);
-    k<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
-        (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines, ldl,
-        out_rows, g_rows_stamps);
+    // persistent over the column tiles (one tile row, nkb >= 3; A/B:
+    // DPSVM_ROWS_PERSIST=0)
+    static const bool persist = [] {
+      const char* e = std::getenv("DPSVM_ROWS_PERSIST");
+      return !(e && e[0] == '0');
+    }();
+    if (persist && tm == 1 && nkb >= 3 && !g_rows_stamps && bring == 3 && (N + 512) * (int64_t)nkb * 8 < (1ll << 32)) {
+      static const int cus = [] {
+        int n = 0;
+        HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, current_device()));
+        return std::max(8, n);
+      }();
+      const int64_t grid = std::min<int64_t>(tn, cus);
+      auto kp = b_cached ? dev::rbf_rows_split_glds_persist_kernel<0> : dev::rbf_rows_split_glds_persist_kernel<2>;
+      kp<<<dim3((unsigned)grid), dev::kRowsGldsThreads, 0, s>>>((const dev::u4*)X, Xsh, Xsq, a_rows, m_dev,
+                                                                (const dev::u4*)B, Bsh, Bsq, N, nkb, gamma, lines, ldl,
+                                                                out_rows, (int)tn);
+    } else {
+      k<<<dim3((unsigned)tm, (unsigned)tn), dev::kRowsGldsThreads, 0, s>>>(
+          (const dev::u4*)X, Xsh, Xsq, a_rows, m_dev, (const dev::u4*)B, Bsh, Bsq, N, (dp + 31) / 32, gamma, lines,
+          ldl, out_rows, g_rows_stamps);
+    }
   }
   post_launch("rbf_rows_indexed_split", s);
 }
