@@ -126,6 +126,10 @@ def parse(argv=None):
     ap.add_argument("--gram", default="auto", choices=["auto", "f32", "split"],
                     help="Gram / kernel-row GEMMs: f32-input MFMA or fp16 MFMA over hi/lo split operands (fp32 "
                          "accuracy); auto = split for the working-set engines")
+    ap.add_argument("--gram-adapt", default="auto", choices=["auto", "on", "off"],
+                    help="resident ws-dense Gram: one-product tiles where every value is provably within 2^-22 of "
+                         "the three-product split value, the rest recomputed (docs/DESIGN.md §13); auto = on when "
+                         "a row sample passes the bound")
     ap.add_argument("--rows-per-group", type=int, default=0, help="engine geometry override (multiple of 256)")
     ap.add_argument("--cache-groups", type=int, default=256)
     ap.add_argument("--force-cache", action="store_true")
@@ -283,7 +287,7 @@ def main(argv=None) -> int:
                     rows_per_group=a.rows_per_group, cache_groups=a.cache_groups, force_cache=a.force_cache, engines=a.engines,
                     xch_poll_batch=a.xch_poll_batch, xch_mem=a.xch_mem, solver=a.solver, ws_size=a.ws_size,
                     ws_new=a.ws_new, ws_rel=a.ws_rel, ws_block=a.ws_block, ws_blocks=a.ws_blocks, ws_inner=a.ws_inner, eta=a.eta,
-                    gram=a.gram,
+                    gram=a.gram, gram_adapt=a.gram_adapt,
                     **({} if a.ws_wss is None else {"ws_wss": a.ws_wss}),
                     **({} if a.ws_t_halve is None else {"ws_t_halve": a.ws_t_halve}),
                     **({"ws_clip_fallback": False} if a.ws_no_clip_fallback else {}),
@@ -562,6 +566,9 @@ def main(argv=None) -> int:
             "x_replicated": bool(info.get("x_replicated", True)),
             "iteration": info.get("iteration", "cpu"),
             "gram": info.get("gram", "f32"),
+            # adaptive Gram: one-product tiles and the hot ones recomputed with three products (-1: not adaptive)
+            "gram_tiles": int(res.get("gram_tiles", -1)),
+            "gram_hot_tiles": int(res.get("gram_hot_tiles", -1)),
             "cache_lines": int(info.get("cache_lines", 0)),
             "comm": getattr(comm, "name", "local"),
             "exchange": info.get("exchange", "none"),

@@ -97,6 +97,9 @@ inline void usage_train(const char* prog, bool seq) {
                "   --eta x|gram        :  pair engines' K(hi, lo): from the X rows (default) | the resident Gram\n"
                "   --gram auto|f32|split :  Gram / kernel-row GEMMs: f32-input MFMA, or fp16 MFMA over hi/lo split\n"
                "                          operands (fp32 accuracy); auto = split for the ws engines\n"
+               "   --gram-adapt auto|on|off : resident ws-dense Gram: one-product tiles where every value is provably\n"
+               "                          within 2^-22 of the three-product one, the rest recomputed (auto: on when a\n"
+               "                          row sample passes the bound)\n"
                "   --params-json PATH  :  solver parameters from a --metrics-json run summary\n"
                "   --checkpoint PATH --checkpoint-every N --resume PATH\n"
                "   --metrics-json PATH :  run summary\n"
@@ -115,7 +118,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
     OPT_LEGG, OPT_QUIET, OPT_SKIPACC, OPT_VERBOSE, OPT_HOSTC, OPT_PERSIST, OPT_PBLOCK, OPT_XCH,
     OPT_DP, OPT_FCACHE, OPT_CENG, OPT_CGROUPS, OPT_ROWS, OPT_XKB, OPT_XSLEEP, OPT_XSTRIDE, OPT_XMEM,
     OPT_XTMO, OPT_WDOG, OPT_CENSUS, OPT_NOVR, OPT_PJSON, OPT_SOLVER, OPT_WSSIZE, OPT_WSNEW, OPT_WSREL, OPT_WSBLOCKS,
-    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM, OPT_SHRINK, OPT_ENGINES
+    OPT_WSINNER, OPT_WSBLOCK, OPT_ETA, OPT_WSWSS, OPT_GRAM, OPT_SHRINK, OPT_ENGINES, OPT_GRAM_ADAPT
   };
   static struct option longopts[] = {
       {"num-att", required_argument, 0, 'a'},     {"num-ex", required_argument, 0, 'x'},
@@ -149,6 +152,7 @@ inline Options parse_train(int argc, char** argv, bool seq) {
       {"ws-blocks", required_argument, 0, OPT_WSBLOCKS},
       {"ws-inner", required_argument, 0, OPT_WSINNER}, {"ws-block", required_argument, 0, OPT_WSBLOCK},
       {"ws-wss", required_argument, 0, OPT_WSWSS}, {"gram", required_argument, 0, OPT_GRAM},
+      {"gram-adapt", required_argument, 0, OPT_GRAM_ADAPT},
       {"shrink", optional_argument, 0, OPT_SHRINK}, {"engines", required_argument, 0, OPT_ENGINES},
       {0, 0, 0, 0}};
   while (true) {
@@ -267,6 +271,12 @@ inline Options parse_train(int argc, char** argv, bool seq) {
         const std::string v = optarg;
         if (v != "x" && v != "gram") usage_train(argv[0], seq);
         o.p.eta = v == "gram" ? 1 : 0;
+        break;
+      }
+      case OPT_GRAM_ADAPT: {
+        const std::string v = optarg;
+        if (v != "auto" && v != "on" && v != "off") usage_train(argv[0], seq);
+        o.p.gram_adapt = v == "on" ? 1 : v == "off" ? 2 : 0;
         break;
       }
       case OPT_GRAM: {

@@ -151,6 +151,11 @@ struct SolverParams {
   // the MFMA time), 0 auto = split for the working-set engines, f32 for the
   // pair-at-a-time engines (the reference's trajectory)
   int gram_precision = 0;
+  // adaptive split Gram (ws-dense resident Gram, docs/DESIGN.md §13): one-product tiles where every element is
+  // provably within gram_cold_tau of the three-product value, the rest recomputed: 0 auto (on when a row
+  // sample's elements all pass the bound), 1 on, 2 off
+  int gram_adapt = 0;
+  float gram_cold_tau = 0x1p-22f;
 };
 
 
@@ -162,6 +167,9 @@ struct SolveResult {
   int status = 0;             // 1 converged, 2 max_iter, 3 no violating pair, 4 non-finite
   double t_setup = 0.0, t_solve = 0.0;
   double t_gram = 0.0;  // device time of the resident Gram GEMM inside t_solve (dense mode)
+  // adaptive split Gram (gram_adapt, docs/DESIGN.md §13): tiles of the one-product pass and how many of them
+  // held an element the error bound rejected (recomputed with all three products); -1: not adaptive
+  int64_t gram_tiles = -1, gram_hot_tiles = -1;
   int64_t cache_hits = 0, cache_misses = 0, rows_computed = 0, x_passes = 0;
   int64_t host_hits = 0, spec_rows = 0;
   int64_t cache_lines = 0, host_cache_lines = 0;

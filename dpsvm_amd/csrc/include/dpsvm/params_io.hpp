@@ -64,6 +64,8 @@ void for_each_param(SolverParams& p, F&& f) {
   f("ws_recompute", p.ws_recompute);
   f("eta", p.eta);
   f("gram_precision", p.gram_precision);
+  f("gram_adapt", p.gram_adapt);
+  f("gram_cold_tau", p.gram_cold_tau);
 }
 
 inline std::string num(double v) {

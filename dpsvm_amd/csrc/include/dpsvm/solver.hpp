@@ -7,6 +7,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dpsvm/comm.hpp"
@@ -206,7 +207,10 @@ std::vector<float> rbf_rows_indexed_split_bench(const float* x, const float* xsq
                                                 int reps, void* stream);
 // the same two GEMMs on fp16 MFMA over split operands (rbf_gemm_split.hip)
 void rbf_gram_split(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
-                    float gamma, float* out, int64_t out_ld, bool symmetric, void* stream);
+                    float gamma, float* out, int64_t out_ld, bool symmetric, void* stream,
+                    float cold_tau = 0.f);
+// the adaptive Gram of the calling thread's last rbf_gram_split / solve: (one-product tiles, hot tiles) or (-1, -1)
+std::pair<int64_t, int64_t> gram_adapt_last();
 void xpass_rows(const float* x, const float* xsq, int64_t n, int ld, const int* keys, int nq, float gamma,
                 float* out, int64_t out_ld, int rows_per_group, void* stream);
 // the fused / persistent engines' selection: per workgroup of rows_per_group rows

@@ -133,9 +133,15 @@ void set_split_gemm_variant(int v);
 // diagnostics: per-workgroup s_memtime stamps of the wide-wave Gram kernel (nullptr: off)
 void set_gram_stamps(uint64_t* p);
 void set_rows_stamps(uint64_t* p);  // diagnostics: the LDS-DMA rows kernel's per-workgroup stamps (0: off)
+// cold_tau > 0: the adaptive Gram (docs/DESIGN.md §13) — a one-product pass, then the tiles holding an element
+// split_cold rejects recomputed with all three products; every stored value within cold_tau of the three-product
+// one.  Falls back to the three-product kernel where the persistent wide-wave path does not apply.
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
-                          int64_t ldo, hipStream_t s, bool symmetric = false);
+                          int64_t ldo, hipStream_t s, bool symmetric = false, float cold_tau = 0.f);
+// the calling thread's last adaptive Gram: tiles of the one-product pass and the hot ones recomputed (valid once
+// the stream passed the GEMM; -1 / -1 when the last Gram was not adaptive)
+void gram_adapt_last(int64_t* tiles, int64_t* hot);
 void rbf_rows_indexed_split(const void* X, const int32_t* Xsh, const float* Xsq, const int32_t* a_rows,
                             const int32_t* m_dev, int64_t M_max, const void* B, const int32_t* Bsh, const float* Bsq,
                             int64_t N, int dp, float gamma, float* lines, const int32_t* out_rows, int64_t ldl,

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -1055,11 +1056,16 @@ __global__ __launch_bounds__(kRowsPersistThreads, 1) void rbf_rows_split_persist
 // SALU per value, VALU-issue-bound: 13.4k -> 10.0k cycles a tile
 // (profiles/r6_gram_lds_readahead_ab.json).  Host: the last row tile's
 // (M - m0) x ldo floats < 2^31 bytes.  lane: the caller's (laundered) lane id.
+// AD: the adaptive Gram's hot-tile pass — every element takes the one-product
+// value where split_cold allows it (R = log2 |x| from Ar / Br, global loads:
+// this pass runs only the few tiles the one-product pass reported).
 typedef int i4v_t __attribute__((ext_vector_type(4)));
+template <bool AD = false>
 __device__ __forceinline__ void w64_epilogue_pe(f16v (&H)[2][2], const f16v (&P)[2][2], const f16v (&Q)[2][2],
                                                 const float* s_sq, const int32_t* s_sh, int lane, int wm, int wn,
                                                 bool mirror, float* out, int64_t m0, int64_t n0, int64_t M, int64_t N,
-                                                int64_t ldo, float gamma) {
+                                                int64_t ldo, float gamma, const float* Ar = nullptr,
+                                                const float* Br = nullptr, float c0 = 0.f, float c1 = 0.f) {
   constexpr int TM = 256, TN = 128;
   typedef i4v_t i4v;
   const int hl = lane >> 5;
@@ -1081,6 +1087,7 @@ __device__ __forceinline__ void w64_epilogue_pe(f16v (&H)[2][2], const f16v (&P)
     const bool okc = cl < clim;
     const float bsq = s_sq[TM + cl];
     const int nbsh = -s_sh[TM + cl];
+    const float rb = AD ? Br[min<int64_t>(n0 + cl, N - 1)] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int lr0 = wm * 64 + 32 * i + 4 * hl;  // value r sits on row lr0 + 8 (r >> 2) + (r & 3)
@@ -1089,6 +1096,11 @@ __device__ __forceinline__ void w64_epilogue_pe(f16v (&H)[2][2], const f16v (&P)
       for (int g = 0; g < 4; ++g) {
         const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
         const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * g);
+        f4 ar = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (AD) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ar[c] = Ar[min<int64_t>(m0 + lr0 + 8 * g + c, M - 1)];
+        }
 #pragma unroll
         for (int e = 0; e < 4; e += 2) {
           const int r = 4 * g + e;
@@ -1111,6 +1123,17 @@ __device__ __forceinline__ void w64_epilogue_pe(f16v (&H)[2][2], const f16v (&P)
             d2.x = d2.x > 0.f ? d2.x : 0.f;
             d2.y = d2.y > 0.f ? d2.y : 0.f;
             t = (ng * d2) * l2e;  // __expf(-gamma d2) = exp2((-gamma d2) log2 e)
+            if constexpr (AD) {  // the one-product pass's value where it is within tau (split_cold)
+              f2 dot1, d21, t1;
+              dot1.x = ldexpf(h.x, nbsh - ash[e]);
+              dot1.y = ldexpf(h.y, nbsh - ash[e + 1]);
+              d21 = (sq + bsq) - (dot1 + dot1);
+              d21.x = d21.x > 0.f ? d21.x : 0.f;
+              d21.y = d21.y > 0.f ? d21.y : 0.f;
+              t1 = (ng * d21) * l2e;
+              if (split_cold(t1.x, ar[e] + rb, c0, c1)) t.x = t1.x;
+              if (split_cold(t1.y, ar[e + 1] + rb, c0, c1)) t.y = t1.y;
+            }
           }
           H[i][j][r] = __builtin_amdgcn_exp2f(t.x);
           H[i][j][r + 1] = __builtin_amdgcn_exp2f(t.y);
@@ -1512,12 +1535,17 @@ __device__ __forceinline__ void w64p_row_dma(const float* __restrict__ Asq, cons
   }
 }
 
-template <int NT, bool PE = false>
+// AD (with PE): the adaptive Gram's hot-tile pass — the tile count is read from
+// ntiles_dev (written by the one-product pass) and the epilogue applies
+// split_cold with Ar / Br, c0, c1.
+template <int NT, bool PE = false, bool AD = false>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq, int M,
     const u4* __restrict__ B, const int32_t* __restrict__ Bsh, const float* __restrict__ Bsq, int N, int nkb,
     float gamma, float* __restrict__ out, int ldo, int sym, const uint32_t* __restrict__ tiles, int ntiles,
-    int tm, int tn, uint64_t* __restrict__ stamps) {
+    int tm, int tn, uint64_t* __restrict__ stamps, const float* __restrict__ Ar = nullptr,
+    const float* __restrict__ Br = nullptr, float c0 = 0.f, float c1 = 0.f,
+    const uint32_t* __restrict__ ntiles_dev = nullptr) {
   // 32-bit indices throughout (launcher: M, N, ldo and (M + 512) x nkb x 8 < 2^31):
   // the loop-carried tile state must fit the scalar registers beside the
   // k loop's, or the 192 accumulators spill
@@ -1527,6 +1555,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
   uint32_t* const s_rows = (uint32_t*)(lds + NB * BUF);
   const int G = gridDim.x;
   int L = blockIdx.x;
+  if constexpr (AD) ntiles = (int)__builtin_amdgcn_readfirstlane(*ntiles_dev);
   if (L >= ntiles) return;  // uniform: no barrier reached
   uint32_t t = tiles[L];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1675,8 +1704,9 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
     if constexpr (PE) {
       int el = lane;
       asm volatile("" : "+v"(el));
-      w64_epilogue_pe(H, P, Q, (const float*)(s_rows + par * RD), (const int32_t*)(s_rows + par * RD + ROWS), el, wm,
-                      wn, sym && ty > 2 * tx + (wm >> 1), out, m0, n0, M, N, ldo, gamma);
+      w64_epilogue_pe<AD>(H, P, Q, (const float*)(s_rows + par * RD), (const int32_t*)(s_rows + par * RD + ROWS),
+                          el, wm, wn, sym && ty > 2 * tx + (wm >> 1), out, m0, n0, M, N, ldo, gamma, Ar, Br, c0,
+                          c1);
     }
     // (the per-lane epilogue addresses are recomputed per tile from a
     // laundered lane id: hoisted out of the tile loop they would hold ~64
@@ -1763,6 +1793,314 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
 #undef PIECE_A
 #undef PIECE_B
 #undef ROW_DMA
+
+// ---------------------------------------------------------------------------
+// Adaptive split Gram, pass 1: the one-product (h_a . h_b) Gram with per-tile
+// hot reports (docs/DESIGN.md §13).  Where the kernel is far from the identity
+// only near the diagonal (the headline: every off-diagonal K < 3e-6), the two
+// correction products change no stored value by more than tau = 2^-22 — 45x
+// below the three-product Gram's own error vs float64 — and split_cold proves
+// it element by element.  This pass multiplies the h planes only (1/3 of the
+// MFMAs, half the operand bytes), stores K1 everywhere and appends every tile
+// holding an element split_cold rejects to a list; pass 2 (w64p, AD) recomputes
+// those tiles with all three products.  The H accumulator's MFMA sequence is
+// the three-product kernels' (same k order), so K1 and the rule's inputs are
+// the same bits in both passes.
+// Tiles, waves and the persistent LDS-DMA ring are the w64p kernel's; a ring
+// stage is 64 k of h planes (split blocks 2 s and 2 s + 1: LDS row chunk p
+// holds virtual chunk v = p ^ swizzle, the h chunk v & 3 of block 2 s + (v >> 2));
+// an odd block count's last stage loads block 2 s twice and multiplies its
+// first two k steps only.  64 accumulator registers instead of 192.
+// tile_hot [ntiles] (zeroed): per-tile report counts; hot[0] (zeroed) the
+// list's length, hot[1 ..] the reported tiles' table entries.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void h1_row_dma(const float* __restrict__ Asq, const float* __restrict__ Bsq,
+                                           const int32_t* __restrict__ Ash, const int32_t* __restrict__ Bsh,
+                                           const float* __restrict__ Ar, const float* __restrict__ Br, int M, int N,
+                                           uint32_t* s_rows, int wave, int lane, int m0, int n0, int par) {
+  constexpr int TM = 256, ROWS = 384, RD = 1536;  // |x|^2 [ROWS], shifts [ROWS], log2 |x| [ROWS], padding
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int d0 = __builtin_amdgcn_readfirstlane(64 * (3 * wave + i));
+    const int kind = d0 / ROWS;  // uniform: 0 |x|^2, 1 shifts, 2 log2 |x|, 3 padding
+    const int r0 = d0 - (kind < 3 ? kind : 0) * ROWS;
+    const bool a_rows = r0 < TM;
+    const uint32_t* arr = kind == 0   ? (a_rows ? (const uint32_t*)Asq : (const uint32_t*)Bsq)
+                          : kind == 1 ? (a_rows ? (const uint32_t*)Ash : (const uint32_t*)Bsh)
+                                      : (a_rows ? (const uint32_t*)Ar : (const uint32_t*)Br);
+    const int r = r0 + lane;
+    const int ri = a_rows ? min(m0 + r, M - 1) : min(n0 + (r - TM), N - 1);
+    const uint32_t* src = kind == 3 ? (const uint32_t*)Asq : arr + ri;  // padding: any valid address
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(s_rows + par * RD + d0),
+                                     4, 0, 0);
+  }
+}
+
+// the one-product epilogue: K1 = exp2(t1) stored as the PE epilogue stores;
+// returns (wave-uniform) whether any of the wave's elements is hot.
+// ABL (diagnostics, DPSVM_H1_ABLATE): 1 every store dropped (out-of-range
+// offsets: issued, no memory traffic), 2 the mirrored stores dropped, 3 no
+// MFMAs in the k loop
+template <int ABL = 0>
+__device__ __forceinline__ bool h1_epilogue(f16v (&H)[2][2], const float* s_sq, const int32_t* s_sh,
+                                            const float* s_r, int lane, int wm, int wn, bool mirror, float* out,
+                                            int64_t m0, int64_t n0, int64_t M, int64_t N, int64_t ldo, float gamma,
+                                            float c0, float c1) {
+  constexpr int TM = 256, TN = 128;
+  typedef i4v_t i4v;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int hl = lane >> 5;
+  float* const ob = out + m0 * ldo + n0;
+  float* const mb = out + n0 * ldo + m0;
+  const uint32_t ld = (uint32_t)ldo;
+  const int rlim = (int)min<int64_t>(M - m0, TM);
+  const int clim = (int)min<int64_t>(N - n0, TN);
+  constexpr uint32_t OOB = 0x80000000u;
+  const int64_t ob_bytes = min<int64_t>((M - m0) * ldo * 4 - n0 * 4, (int64_t)OOB);
+  const int64_t mb_bytes = min<int64_t>((N - n0) * ldo * 4 - m0 * 4, (int64_t)OOB);
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, (int)ob_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mb, 0, (int)mb_bytes, 0x00020000);
+  const float ng = -gamma, l2e = 1.4426950408889634f;
+  bool hot = false;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cl = wn * 64 + 32 * j + (lane & 31);
+    const bool okc = cl < clim;
+    const float bsq = s_sq[TM + cl];
+    const int nbsh = -s_sh[TM + cl];
+    const float rb = s_r[TM + cl];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int lr0 = wm * 64 + 32 * i + 4 * hl;
+      const uint32_t vo = okc && ABL != 1 ? ((uint32_t)lr0 * ld + (uint32_t)cl) * 4u : OOB;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
+        const i4v ash = *(const i4v*)(s_sh + lr0 + 8 * g);
+        const f4 ar = *(const f4*)(s_r + lr0 + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int r = 4 * g + e;
+          f2 h, dot, sq, d2, t;
+          h.x = H[i][j][r];
+          h.y = H[i][j][r + 1];
+          {
+#pragma clang fp contract(off)
+            dot.x = ldexpf(h.x, nbsh - ash[e]);
+            dot.y = ldexpf(h.y, nbsh - ash[e + 1]);
+            sq.x = asq[e];
+            sq.y = asq[e + 1];
+            d2 = (sq + bsq) - (dot + dot);
+            d2.x = d2.x > 0.f ? d2.x : 0.f;
+            d2.y = d2.y > 0.f ? d2.y : 0.f;
+            t = (ng * d2) * l2e;
+            hot |= !split_cold(t.x, ar[e] + rb, c0, c1);
+            hot |= !split_cold(t.y, ar[e + 1] + rb, c0, c1);
+          }
+          H[i][j][r] = __builtin_amdgcn_exp2f(t.x);
+          H[i][j][r + 1] = __builtin_amdgcn_exp2f(t.y);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float hv = H[i][j][4 * g + e];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hv), rs_o, (int)(vo + (uint32_t)(8 * g + e) * ld * 4u),
+                                                0, 0);
+        }
+      }
+      if (mirror) {
+        const uint32_t vm = okc && ABL != 1 && ABL != 2 ? ((uint32_t)cl * ld + (uint32_t)lr0) * 4u : OOB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int lr = lr0 + 8 * q;
+          f4 v;
+          v.x = H[i][j][4 * q + 0];
+          v.y = H[i][j][4 * q + 1];
+          v.z = H[i][j][4 * q + 2];
+          v.w = H[i][j][4 * q + 3];
+          const uint32_t o = lr + 3 < rlim && vm != OOB ? vm + 32u * q : OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v), rs_m, (int)o, 0, 0);
+          if (rlim < TM) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t oc = (lr + 3 >= rlim && lr + c < rlim) ? vm + 32u * q + 4u * c : OOB;
+              const float vc = v[c];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vc), rs_m, (int)oc, 0, 0);
+            }
+          }
+        }
+      }
+    }
+  }
+  return __builtin_amdgcn_ballot_w64(hot) != 0;
+}
+
+template <int ABL = 0>
+__global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
+    const float* __restrict__ Ar, int M, const u4* __restrict__ B, const int32_t* __restrict__ Bsh,
+    const float* __restrict__ Bsq, const float* __restrict__ Br, int N, int nkb, float gamma, float c0, float c1,
+    float* __restrict__ out, int ldo, int sym, const uint32_t* __restrict__ tiles, int ntiles,
+    uint32_t* __restrict__ tile_hot, uint32_t* __restrict__ hot) {
+  constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
+  constexpr int RD = 1536;
+  __shared__ u4 lds[NB * BUF + 2 * RD / 4];  // 3 operand buffers, then row data [2][RD]
+  uint32_t* const s_rows = (uint32_t*)(lds + NB * BUF);
+  const int G = gridDim.x;
+  int L = blockIdx.x;
+  if (L >= ntiles) return;  // uniform
+  uint32_t t = tiles[L];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const uint32_t rs = (uint32_t)nkb * 8;  // u4 per split row
+  const int nst = (nkb + 1) >> 1;         // ring stages a tile (launcher: nkb >= 5)
+  const bool odd = (nkb & 1) != 0;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t step = 8 * rs;
+  // lane byte offsets of a piece (even / odd pieces: swizzle lane >> 4 / (lane >> 4) + 4, as w64p);
+  // _t: an odd block count's last stage (virtual chunks 4..7 re-read block 2 s)
+  const int p = lane & 7, ve = p ^ (lane >> 4), vd = p ^ ((lane >> 4) + 4);
+  const uint32_t rowb = (uint32_t)(lane >> 3) * rs;
+  uint32_t off_e = 16u * (rowb + (uint32_t)((ve >> 2) * 8 + (ve & 3)));
+  uint32_t off_o = 16u * (rowb + (uint32_t)((vd >> 2) * 8 + (vd & 3)));
+  uint32_t off_et = 16u * (rowb + (uint32_t)(ve & 3));
+  uint32_t off_ot = 16u * (rowb + (uint32_t)(vd & 3));
+  asm volatile("" : "+v"(off_e), "+v"(off_o), "+v"(off_et), "+v"(off_ot));
+  const int dstA = 32 * wv * 8, dstB = (TM + 16 * wv) * 8;
+  int Ln = L + G;
+  uint32_t tn_next = Ln < ntiles ? tiles[Ln] : 0u;
+  int par = 0;
+  uint32_t g = 0;  // stages started over all of this workgroup's tiles: ring buffer g % NB
+  {
+    const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
+    h1_row_dma(Asq, Bsq, Ash, Bsh, Ar, Br, M, N, s_rows, wave, lane, m0, n0, 0);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {  // stages 0 and 1 (never an odd tail: nst >= 3)
+      const uint32_t uA = (uint32_t)(m0 + 32 * wv) * rs + (uint32_t)b * 16;
+      const uint32_t uB = (uint32_t)(n0 + 16 * wv) * rs + (uint32_t)b * 16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w64p_piece(A, lds, uA, step, dstA, off_e, off_o, b, i);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) w64p_piece(B, lds, uB, step, dstB, off_e, off_o, b, i);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra0 = (wm * 64 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
+  while (true) {
+    const bool has_next = Ln < ntiles;  // uniform
+    const int tx = (int)(t >> 16), ty = (int)(t & 0xffffu);
+    const int m0 = tx * TM, n0 = ty * TN;
+    const uint32_t tp = has_next ? tn_next : t;
+    const int nm0 = (int)(tp >> 16) * TM, nn0 = (int)(tp & 0xffffu) * TN;
+    f16v H[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) H[i][j][r] = 0.f;
+#pragma clang loop unroll(disable)
+    for (int s = 0; s < nst; ++s) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // the prefetch slot: stage s + 2 of this tile or stage s + 2 - nst of the next
+      const bool own = s + 2 < nst;
+      const int ps = own ? s + 2 : s + 2 - nst;
+      const bool ptail = odd && ps == nst - 1;  // uniform
+      const uint32_t pe_ = ptail ? off_et : off_e, po_ = ptail ? off_ot : off_o;
+      const uint32_t uA = (uint32_t)((own ? m0 : nm0) + 32 * wv) * rs + (uint32_t)ps * 16;
+      const uint32_t uB = (uint32_t)((own ? n0 : nn0) + 16 * wv) * rs + (uint32_t)ps * 16;
+      const int pbuf = (int)((g + 2) % NB);
+      auto piece = [&](int j) {  // A0, A1, B0, A2, A3, B1
+        __builtin_amdgcn_sched_barrier(0);
+        if (j == 2 || j == 5) w64p_piece(B, lds, uB, step, dstB, pe_, po_, pbuf, j == 2 ? 0 : 1);
+        else w64p_piece(A, lds, uA, step, dstA, pe_, po_, pbuf, j < 2 ? j : j - 1);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      const u4* buf = lds + (g % NB) * BUF;
+      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
+      // k step q's fragments: A rows (+ 32), B rows (+ 32) of virtual chunk 2 q + hl
+      auto rd = [&](int q, h8& a0, h8& a1, h8& b0, h8& b1) {
+        const uint32_t c = 16u * (uint32_t)((2 * q + hl) ^ sw);
+        const uint32_t pa = abase + c, pb = bbase + c;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(a0) : "v"(pa) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(a1) : "v"(pa) : "memory");
+        asm volatile("ds_read_b128 %0, %1" : "=v"(b0) : "v"(pb) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(b1) : "v"(pb) : "memory");
+      };
+      auto mma = [&](const h8& a0, const h8& a1, const h8& b0, const h8& b1) {
+        if (ABL == 3) return;
+        H[0][0] = mfma32_f16(a0, b0, H[0][0]);
+        H[0][1] = mfma32_f16(a0, b1, H[0][1]);
+        H[1][0] = mfma32_f16(a1, b0, H[1][0]);
+        H[1][1] = mfma32_f16(a1, b1, H[1][1]);
+      };
+      h8 x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
+      const bool tail = odd && s == nst - 1;  // uniform
+      rd(0, x0, x1, x2, x3);
+      rd(1, y0, y1, y2, y3);
+      if (!tail) {
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+        mma(x0, x1, x2, x3);
+        piece(0);
+        piece(1);
+        rd(2, z0, z1, z2, z3);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
+        mma(y0, y1, y2, y3);
+        piece(2);
+        piece(3);
+        rd(3, x0, x1, x2, x3);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+        mma(z0, z1, z2, z3);
+        piece(4);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+        mma(x0, x1, x2, x3);
+        piece(5);
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+        mma(x0, x1, x2, x3);
+        piece(0);
+        piece(1);
+        piece(2);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
+        mma(y0, y1, y2, y3);
+        piece(3);
+        piece(4);
+        piece(5);
+      }
+      ++g;
+    }
+    if (has_next) h1_row_dma(Asq, Bsq, Ash, Bsh, Ar, Br, M, N, s_rows, wave, lane, nm0, nn0, par ^ 1);
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const float* rows = (const float*)(s_rows + par * RD);
+    const bool hotw = h1_epilogue<ABL>(H, rows, (const int32_t*)(rows + ROWS), rows + 2 * ROWS, el, wm, wn,
+                                  sym && ty > 2 * tx + (wm >> 1), out, m0, n0, M, N, ldo, gamma, c0, c1);
+    if (hotw && lane == 0) {  // the tile's first report appends it to the list
+      if (atomicAdd(tile_hot + L, 1u) == 0u) {
+        const uint32_t k = atomicAdd(hot, 1u);
+        hot[1 + k] = t;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!has_next) break;
+    L = Ln;
+    t = tn_next;
+    par ^= 1;
+    Ln = L + G;
+    if (Ln < ntiles) tn_next = tiles[Ln];
+  }
+}
+
+// R = log2 |x| = split_log2norm(|x|^2) of n rows (the adaptive Gram's rule input)
+__global__ __launch_bounds__(256) void split_log2norm_kernel(const float* __restrict__ sq, int n,
+                                                             float* __restrict__ r) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) r[i] = split_log2norm(sq[i]);
+}
 
 // ---------------------------------------------------------------------------
 // Persistent LDS-DMA STORE GEMM: the LDS-DMA kernel's k loop, one 512-thread
@@ -2263,9 +2601,21 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym 
 }
 }  // namespace
 
+namespace {
+// the calling thread's last adaptive Gram (svmTrain -p N: one rank per thread)
+thread_local int64_t t_adapt_tiles = -1;
+thread_local uint32_t* t_adapt_hot = nullptr;  // pinned: the hot-tile count, copied after pass 1
+}  // namespace
+
+void gram_adapt_last(int64_t* tiles, int64_t* hot) {
+  *tiles = t_adapt_tiles;
+  *hot = t_adapt_tiles >= 0 && t_adapt_hot ? (int64_t)*(volatile uint32_t*)t_adapt_hot : -1;
+}
+
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
-                          int64_t ldo, hipStream_t s, bool symmetric) {
+                          int64_t ldo, hipStream_t s, bool symmetric, float cold_tau) {
+  t_adapt_tiles = -1;
   if (M <= 0 || N <= 0) return;
   DPSVM_CHECK(!symmetric || (A == B && Asq == Bsq && Ash == Bsh && M == N && ldo % 4 == 0),
               "rbf_gemm_store_split: symmetric mode needs B == A, N == M");
@@ -2341,12 +2691,53 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const uint32_t* tab = t.dev;
       const int64_t ntiles = t.count;
       const int64_t grid = std::min<int64_t>(ntiles, cus);
+      if (pe && cold_tau > 0.f && gamma > 0.f && nkb >= 5 && !g_gram_stamps) {
+        // adaptive: pass 1 one-product over every tile, pass 2 three products over the reported ones
+        const double e = 4.5 * std::ldexp(1.0, -11) * (double)gamma;  // E = e |a| |b| (split_cold)
+        const float c1 = (float)(-std::log2(e));
+        const float c0 = (float)(std::log2((double)cold_tau) - std::log2(1.72 * e) - 0.01);
+        const int64_t nr = symmetric ? M : M + N;
+        float* r = nullptr;
+        uint32_t* hb = nullptr;  // [ntiles] per-tile reports, then the list's length and entries
+        HIP_CHECK(hipMallocAsync((void**)&r, (size_t)nr * 4, s));
+        HIP_CHECK(hipMallocAsync((void**)&hb, (size_t)(2 * ntiles + 1) * 4, s));
+        HIP_CHECK(hipMemsetAsync(hb, 0, (size_t)(ntiles + 1) * 4, s));
+        dev::split_log2norm_kernel<<<dim3((unsigned)((M + 255) / 256)), 256, 0, s>>>(Asq, (int)M, r);
+        float* br = r;
+        if (!symmetric) {
+          br = r + M;
+          dev::split_log2norm_kernel<<<dim3((unsigned)((N + 255) / 256)), 256, 0, s>>>(Bsq, (int)N, br);
+        }
+        post_launch("split_log2norm", s);
+        static const int h1_abl = [] {  // diagnostics (bench/gram_adapt_probe.py): h1 pass ablations
+          const char* e = std::getenv("DPSVM_H1_ABLATE");
+          return e ? atoi(e) : 0;
+        }();
+        auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1>
+                   : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2>
+                   : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3>
+                                 : dev::rbf_gemm_split_h1_kernel<0>;
+        h1k<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
+            (const dev::u4*)A, Ash, Asq, r, (int)M, (const dev::u4*)B, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1, out,
+            (int)ldo, symmetric ? 1 : 0, tab, (int)ntiles, hb, hb + ntiles);
+        post_launch("rbf_gemm_split_h1", s);
+        dev::rbf_gemm_split_w64p_kernel<0, true, true><<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
+            (const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B, Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
+            symmetric ? 1 : 0, hb + ntiles + 1, 0, (int)tm2, (int)tn, nullptr, r, br, c0, c1, hb + ntiles);
+        post_launch("rbf_gemm_split_w64p_hot", s);
+        if (!t_adapt_hot) HIP_CHECK(hipHostMalloc((void**)&t_adapt_hot, 4, hipHostMallocDefault));
+        HIP_CHECK(hipMemcpyAsync(t_adapt_hot, hb + ntiles, 4, hipMemcpyDeviceToHost, s));
+        t_adapt_tiles = ntiles;
+        HIP_CHECK(hipFreeAsync(r, s));
+        HIP_CHECK(hipFreeAsync(hb, s));
+        return;
+      }
       auto pk = g_gram_stamps ? (pe ? dev::rbf_gemm_split_w64p_kernel<3, true> : dev::rbf_gemm_split_w64p_kernel<3>)
                 : pe ? dev::rbf_gemm_split_w64p_kernel<0, true> : dev::rbf_gemm_split_w64p_kernel<0>;
       pk<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>((const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B,
                                                           Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
                                                           symmetric ? 1 : 0, tab, (int)ntiles, (int)tm2, (int)tn,
-                                                          g_gram_stamps);
+                                                          g_gram_stamps, nullptr, nullptr, 0.f, 0.f, nullptr);
       post_launch("rbf_gemm_split_w64p", s);
       return;
     }

@@ -27,6 +27,26 @@ __device__ __forceinline__ float rbf_split_value(float sq_a, float sq_b, float d
   return __expf(-gamma * d2);
 }
 
+// Error-bounded one-product Gram (the adaptive split Gram, docs/DESIGN.md §13).
+// The one-product dot product h_a.h_b differs from the three-product one by
+// |h_a.l_b + l_a.h_b| <= 2u(1 + u)|a||b| (u = 2^-11, the fp16 rounding of the
+// scaled rows, plus fp32 rounding far below it), so the two d^2 differ by at
+// most D = 4.5 u |a||b| and the two K by at most K1 (e^{gamma D} - 1) <=
+// 1.72 K1 E for E = gamma D <= 1.  Element (i, j) keeps the one-product value
+// K1 when
+//     s = R_i + R_j <= c1            (E <= 1)
+//     t1 <= c0 - s                   (1.72 K1 E <= tau)
+// with R = log2 |x| = split_log2norm(|x|^2), t1 the one-product exp2
+// argument and c0 / c1 from split_cold_consts (host); every other element gets
+// the three-product value.  The test reads only symmetric quantities (R_i + R_j
+// commutes, t1 is the same expression as K's), so the choice is the same for
+// (i, j) and (j, i) and in every tiling: the symmetric Gram, the sharded slabs
+// and a hot-tile recompute store the same bits.
+__device__ __forceinline__ float split_log2norm(float sq) { return 0.5f * __builtin_amdgcn_logf(sq); }
+__device__ __forceinline__ bool split_cold(float t1, float s, float c0, float c1) {
+  return (s <= c1) & (t1 <= c0 - s);
+}
+
 __device__ __forceinline__ f16v mfma32_f16(h8 a, h8 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }

@@ -110,6 +110,8 @@ py::dict result_dict(const SolveResult& r) {
   d["t_setup"] = r.t_setup;
   d["t_solve"] = r.t_solve;
   d["t_gram"] = r.t_gram;
+  d["gram_tiles"] = r.gram_tiles;
+  d["gram_hot_tiles"] = r.gram_hot_tiles;
   d["verify_f_err"] = r.verify_f_err;
   d["cache_hits"] = r.cache_hits;
   d["cache_misses"] = r.cache_misses;
@@ -239,6 +241,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("ws_block", &SolverParams::ws_block)
       .def_readwrite("ws_recompute", &SolverParams::ws_recompute)
       .def_readwrite("gram_precision", &SolverParams::gram_precision)
+      .def_readwrite("gram_adapt", &SolverParams::gram_adapt)
+      .def_readwrite("gram_cold_tau", &SolverParams::gram_cold_tau)
       .def("to_json", [](const SolverParams& p) { return params_json(p); })
       .def("update_from_json", [](SolverParams& p, const std::string& t) { apply_params_json(t, p); });
 
@@ -586,10 +590,14 @@ PYBIND11_MODULE(_C, m) {
     launch::split_rows_f16((const float*)x, rows, dp, ldx, (void*)out, (int32_t*)shift, (hipStream_t)stream);
   });
   m.def("k_rbf_gram_split", [](uintptr_t a, uintptr_t asq, int64_t m_, uintptr_t b, uintptr_t bsq, int64_t n, int ld,
-                               float gamma, uintptr_t out, int64_t out_ld, bool sym, uintptr_t stream) {
+                               float gamma, uintptr_t out, int64_t out_ld, bool sym, uintptr_t stream,
+                               float cold_tau) {
     kernels::rbf_gram_split((const float*)a, (const float*)asq, m_, (const float*)b, (const float*)bsq, n, ld, gamma,
-                            (float*)out, out_ld, sym, (void*)stream);
-  });
+                            (float*)out, out_ld, sym, (void*)stream, cold_tau);
+  }, py::arg("a"), py::arg("asq"), py::arg("m"), py::arg("b"), py::arg("bsq"), py::arg("n"), py::arg("ld"),
+     py::arg("gamma"), py::arg("out"), py::arg("out_ld"), py::arg("sym"), py::arg("stream"), py::arg("cold_tau") = 0.f);
+  m.def("k_gram_adapt_last", []() { return kernels::gram_adapt_last(); },
+        "(one-product tiles, hot tiles) of the calling thread's last adaptive split Gram, or (-1, -1)");
   m.def("k_fused_select", [](uintptr_t f, uintptr_t alpha, uintptr_t y, int64_t n, float C, int rows, uintptr_t out,
                              uintptr_t stream) {
     kernels::fused_select((const float*)f, (const float*)alpha, (const float*)y, n, C, rows, (uint64_t*)out,

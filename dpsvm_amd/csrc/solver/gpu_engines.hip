@@ -80,7 +80,8 @@ struct DenseBase : Engine {
       const bool sym = m.off == 0 && m.nl == m.n;
       const size_t ru = (size_t)launch::split_row_u4(m.dp) * 16;
       launch::rbf_gemm_store_split(m.xs, m.xsh, m.xsq, m.n, (const uint8_t*)m.xs + (size_t)m.off * ru, m.xsh + m.off,
-                                   m.xsq + m.off, m.nl, m.dp, m.gamma, m.lines, m.ldl, m.stream, sym);
+                                   m.xsq + m.off, m.nl, m.dp, m.gamma, m.lines, m.ldl, m.stream, sym,
+                                   m.gram_cold_tau);
     } else {
       // one rank holds the whole (symmetric) Gram: compute half, mirror the rest
       const bool sym = m.off == 0 && m.nl == m.n;
@@ -123,7 +124,8 @@ struct DenseBase : Engine {
       if (m.gram_split) {
         launch::split_rows_f16(panel, prow, m.dp, m.dp, pxs, pxsh, m.stream);
         launch::rbf_gemm_store_split(pxs, pxsh, m.xsq + s.offset, s.size, m.xs, m.xsh, m.xsq + m.off, m.nl, m.dp,
-                                     m.gamma, m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);
+                                     m.gamma, m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false,
+                                     m.gram_cold_tau);
       } else {
         launch::rbf_gemm_store(panel, m.xsq + s.offset, s.size, m.dp, m.x, m.xsq + m.off, m.nl, m.dp, m.dp, m.gamma,
                                m.lines + (size_t)s.offset * m.ldl, m.ldl, m.stream, false);

@@ -108,6 +108,7 @@ struct GpuSolver::Impl {
   // solve inside the timed region: xs / xsh = the x_rows rows of x; wsxs /
   // wsxsh = the packed misses of partitioned ws-cache rounds
   bool gram_split = false;
+  float gram_cold_tau = 0.f;  // > 0: the resident split Gram is adaptive (gram_adapt, docs/DESIGN.md §13)
   void* xs = nullptr;
   int32_t* xsh = nullptr;
   void* wsxs = nullptr;

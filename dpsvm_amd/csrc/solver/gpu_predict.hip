@@ -418,19 +418,25 @@ struct SplitRows {
 }  // namespace
 
 void rbf_gram_split(const float* a, const float* asq, int64_t m, const float* b, const float* bsq, int64_t n, int ld,
-                    float gamma, float* out, int64_t out_ld, bool symmetric, void* stream) {
+                    float gamma, float* out, int64_t out_ld, bool symmetric, void* stream, float cold_tau) {
   hipStream_t s = (hipStream_t)stream;
   SplitRows sa(a, m, ld, s);
   if (symmetric) {
     launch::rbf_gemm_store_split(sa.planes, sa.shift, asq, m, sa.planes, sa.shift, asq, n, ld, gamma, out, out_ld, s,
-                                 true);
+                                 true, cold_tau);
     HIP_CHECK(hipStreamSynchronize(s));
     return;
   }
   SplitRows sb(b, n, ld, s);
   launch::rbf_gemm_store_split(sa.planes, sa.shift, asq, m, sb.planes, sb.shift, bsq, n, ld, gamma, out, out_ld, s,
-                               false);
+                               false, cold_tau);
   HIP_CHECK(hipStreamSynchronize(s));
+}
+
+std::pair<int64_t, int64_t> gram_adapt_last() {
+  int64_t t = -1, h = -1;
+  launch::gram_adapt_last(&t, &h);
+  return {t, h};
 }
 
 void rbf_rows_indexed(const float* x, const float* xsq, int64_t n, int ld, const int* rows, int m, float gamma,

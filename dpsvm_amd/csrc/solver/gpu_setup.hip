@@ -199,6 +199,39 @@ double mean_offdiag_kernel(const float* xh, int64_t rows, int d, float gamma) {
   return acc / (double)(s * (s - 1) / 2);
 }
 
+// adaptive split Gram (gram_adapt auto, docs/DESIGN.md §13): true when every
+// off-diagonal pair of the coupling sample (96 rows, float64) passes the
+// one-product error bound with a 4x margin — K (e^E - 1) <= tau / 4 with
+// E = gamma 4.5 2^-11 |a| |b| <= 1 — so that few tiles of the Gram hold an
+// element the bound rejects (each costs a three-product recompute).  Any
+// rejected element is still recomputed: this only predicts the cost.
+bool gram_cold_sample_ok(const float* xh, int64_t rows, int d, float gamma, float tau) {
+  const int64_t s = std::min<int64_t>(96, rows);
+  if (s < 2 || !(gamma > 0.f) || !(tau > 0.f)) return false;
+  const int64_t stride = rows / s;
+  const double e = 4.5 * std::ldexp(1.0, -11) * (double)gamma;
+  std::vector<double> nrm((size_t)s);
+  for (int64_t a = 0; a < s; ++a) {
+    const float* xa = xh + (size_t)(a * stride) * d;
+    double q = 0.0;
+    for (int k = 0; k < d; ++k) q += (double)xa[k] * (double)xa[k];
+    nrm[(size_t)a] = std::sqrt(q);
+  }
+  for (int64_t a = 0; a < s; ++a)
+    for (int64_t b = a + 1; b < s; ++b) {
+      const float* xa = xh + (size_t)(a * stride) * d;
+      const float* xb = xh + (size_t)(b * stride) * d;
+      double d2 = 0.0;
+      for (int k = 0; k < d; ++k) {
+        const double t = (double)xa[k] - (double)xb[k];
+        d2 += t * t;
+      }
+      const double E = e * nrm[(size_t)a] * nrm[(size_t)b];
+      if (!(E <= 1.0) || std::exp(-(double)gamma * d2) * std::expm1(E) > 0.25 * (double)tau) return false;
+    }
+  return true;
+}
+
 // the most ranks any one device carries (collective: every rank calls it)
 int max_device_sharing(GpuSolver::Impl& m) {
   struct Id {
@@ -779,6 +812,21 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     m.xsh = nullptr;
   }
   m.info.gram = m.gram_split ? "split-f16" : "f32";
+  {
+    // adaptive split Gram for the resident ws-dense Gram (gram_adapt: 0 auto, 1 on, 2 off;
+    // A/B: DPSVM_GRAM_ADAPT overrides)
+    static const int adapt_env = [] {
+      const char* e = std::getenv("DPSVM_GRAM_ADAPT");
+      return e ? atoi(e) : -1;
+    }();
+    const int mode = adapt_env >= 0 ? adapt_env : m.p.gram_adapt;
+    DPSVM_CHECK(mode >= 0 && mode <= 2, "gram_adapt must be 0 (auto), 1 (on) or 2 (off)");
+    DPSVM_CHECK(m.p.gram_cold_tau > 0.f && m.p.gram_cold_tau <= 1e-3f, "gram_cold_tau must be in (0, 1e-3]");
+    const bool cand = m.gram_split && m.kind == EngineKind::WsDense && mode != 2 && m.gamma > 0.f;
+    const bool ok = cand && (mode == 1 || gram_cold_sample_ok(xh, n_x_rows, d, m.gamma, m.p.gram_cold_tau));
+    m.gram_cold_tau = m.all_agree(ok, m.comm, m.world) ? m.p.gram_cold_tau : 0.f;
+    if (m.gram_cold_tau > 0.f) m.info.gram = "split-f16-adaptive";
+  }
   if (m.working_set()) {
     WsArgs& w = m.wsa;
     w = WsArgs{};

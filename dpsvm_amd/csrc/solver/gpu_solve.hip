@@ -254,6 +254,7 @@ SolveResult GpuSolver::solve(const Checkpoint* resume, const ProgressFn& progres
   HIP_CHECK(hipStreamSynchronize(m.stream));
   res.t_solve = secs_since(t0);
   res.t_gram = m.engine->gram_seconds();
+  if (m.gram_cold_tau > 0.f) launch::gram_adapt_last(&res.gram_tiles, &res.gram_hot_tiles);
   if (m.p.checkpoint_every > 0 && !m.p.checkpoint_path.empty()) {
     st = m.read_status();
     if (st.done == kMaxIter) m.snapshot(st);  // resumable continuation point

@@ -136,6 +136,11 @@ class SVCConfig:
     # Gram / kernel-row GEMM arithmetic: auto (split for the working-set engines, f32 for the pair engines),
     # f32 (f32-input MFMA), split (fp16 MFMA over hi/lo split operands: fp32 accuracy, 3/16 of the MFMA time)
     gram: str = "auto"
+    # adaptive resident split Gram (ws-dense, docs/DESIGN.md §13): one-product tiles where every element is
+    # provably within gram_cold_tau of the three-product value, the rest recomputed — auto (on when a row
+    # sample passes the bound) | on | off
+    gram_adapt: str = "auto"
+    gram_cold_tau: float = 2.0 ** -22
 
     def shrink_mode(self) -> str:
         s = self.shrink
@@ -212,6 +217,8 @@ class SVCConfig:
         p.ws_recompute = _pick({"auto": 0, "on": 1, "off": 2}, self.ws_recompute, "ws_recompute")
         p.eta = _pick({"x": 0, "gram": 1}, self.eta, "eta")
         p.gram_precision = _pick({"auto": 0, "f32": 1, "split": 2}, self.gram, "gram")
+        p.gram_adapt = _pick({"auto": 0, "on": 1, "off": 2}, self.gram_adapt, "gram_adapt")
+        p.gram_cold_tau = float(self.gram_cold_tau)
         return p
 
     def device_kind(self) -> tuple[str, int]:

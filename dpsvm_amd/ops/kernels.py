@@ -37,11 +37,15 @@ def row_sqnorm(x: torch.Tensor) -> torch.Tensor:
     return out[: x.shape[0]]
 
 
-def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0, split: bool = False) -> torch.Tensor:
+def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0, split: bool = False,
+             cold_tau: float = 0.0) -> torch.Tensor:
     """Gram block K[i, j] = exp(-gamma |a_i - b_j|^2) with the dense-mode MFMA
     GEMM (32x32x2 f32, fused exp; split=True: fp16 MFMA over hi/lo split
     operands, rbf_gemm_split.hip).  b=None: the symmetric Gram of a, computed
-    as upper-triangle tiles plus their mirrored transposes."""
+    as upper-triangle tiles plus their mirrored transposes.  cold_tau > 0
+    (split only): the adaptive Gram — one-product values where they are
+    provably within cold_tau of the three-product ones (docs/DESIGN.md §13);
+    gram_adapt_last() then reports its tile counts."""
     C = load()
     sym = b is None
     ap, dp = _pad_rows_cols(a)
@@ -57,10 +61,21 @@ def rbf_gram(a: torch.Tensor, b: torch.Tensor | None = None, gamma: float = 1.0,
     n = m if sym else b.shape[0]
     ld = (n + 127) // 128 * 128
     out = torch.full((m, ld), float("nan"), device=a.device)
-    fn = C.k_rbf_gram_split if split else C.k_rbf_gram
-    fn(ap.data_ptr(), asq.data_ptr(), m, bp.data_ptr(), bsq.data_ptr(), n, dp, float(gamma), out.data_ptr(), ld, sym,
-       _stream(a))
+    if split:
+        C.k_rbf_gram_split(ap.data_ptr(), asq.data_ptr(), m, bp.data_ptr(), bsq.data_ptr(), n, dp, float(gamma),
+                           out.data_ptr(), ld, sym, _stream(a), float(cold_tau))
+    else:
+        if cold_tau:
+            raise ValueError("cold_tau needs split=True")
+        C.k_rbf_gram(ap.data_ptr(), asq.data_ptr(), m, bp.data_ptr(), bsq.data_ptr(), n, dp, float(gamma),
+                     out.data_ptr(), ld, sym, _stream(a))
     return out[:, :n]
+
+
+def gram_adapt_last() -> tuple[int, int]:
+    """(one-product tiles, hot tiles recomputed) of this thread's last adaptive
+    split Gram, or (-1, -1) when it was not adaptive."""
+    return tuple(load().k_gram_adapt_last())
 
 
 def rbf_rows(x: torch.Tensor, w: torch.Tensor, gamma: float) -> torch.Tensor:
