@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--slab", type=int, default=7500)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cases", default="sym,slab")
+    ap.add_argument("--adaptive-only", action="store_true", help="skip the three-product Gram (A/B sweeps)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     X, _ = synthetic(args.data, n=args.n, seed=1)
@@ -55,9 +56,13 @@ def main():
     a64 = X[sub].astype(np.float64)
     for case in args.cases.split(","):
         b = None if case == "sym" else x[: args.slab].contiguous()
-        t3, k3 = timed(lambda: K.rbf_gram(x, b, args.gamma, split=True), args.reps)
         ta, ka = timed(lambda: K.rbf_gram(x, b, args.gamma, split=True, cold_tau=args.tau), args.reps)
         tiles, hot = K.gram_adapt_last()
+        if args.adaptive_only:
+            res[case] = {"ms_adaptive": ta, "tiles": tiles, "hot_tiles": hot}
+            print(case, json.dumps(res[case]), flush=True)
+            continue
+        t3, k3 = timed(lambda: K.rbf_gram(x, b, args.gamma, split=True), args.reps)
         diff = (ka - k3).abs().max().item()
         bx = X if case == "sym" else X[: args.slab]
         b64 = bx.astype(np.float64)

@@ -1836,43 +1836,25 @@ __device__ __forceinline__ void h1_row_dma(const float* __restrict__ Asq, const 
   }
 }
 
-// the one-product epilogue: K1 = exp2(t1) stored as the PE epilogue stores;
-// returns (wave-uniform) whether any of the wave's elements is hot.
-// ABL (diagnostics, DPSVM_H1_ABLATE): 1 every store dropped (out-of-range
-// offsets: issued, no memory traffic), 2 the mirrored stores dropped, 3 no
-// MFMAs in the k loop
-template <int ABL = 0>
-__device__ __forceinline__ bool h1_epilogue(f16v (&H)[2][2], const float* s_sq, const int32_t* s_sh,
-                                            const float* s_r, int lane, int wm, int wn, bool mirror, float* out,
-                                            int64_t m0, int64_t n0, int64_t M, int64_t N, int64_t ldo, float gamma,
-                                            float c0, float c1) {
-  constexpr int TM = 256, TN = 128;
+// the one-product epilogue's math: H becomes K1 = exp2(t1) in place; returns
+// (wave-uniform) whether any of the wave's elements is hot
+__device__ __forceinline__ bool h1_values(f16v (&H)[2][2], const float* s_sq, const int32_t* s_sh, const float* s_r,
+                                          int lane, int wm, int wn, float gamma, float c0, float c1) {
+  constexpr int TM = 256;
   typedef i4v_t i4v;
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int hl = lane >> 5;
-  float* const ob = out + m0 * ldo + n0;
-  float* const mb = out + n0 * ldo + m0;
-  const uint32_t ld = (uint32_t)ldo;
-  const int rlim = (int)min<int64_t>(M - m0, TM);
-  const int clim = (int)min<int64_t>(N - n0, TN);
-  constexpr uint32_t OOB = 0x80000000u;
-  const int64_t ob_bytes = min<int64_t>((M - m0) * ldo * 4 - n0 * 4, (int64_t)OOB);
-  const int64_t mb_bytes = min<int64_t>((N - n0) * ldo * 4 - m0 * 4, (int64_t)OOB);
-  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, (int)ob_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mb, 0, (int)mb_bytes, 0x00020000);
   const float ng = -gamma, l2e = 1.4426950408889634f;
   bool hot = false;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int cl = wn * 64 + 32 * j + (lane & 31);
-    const bool okc = cl < clim;
     const float bsq = s_sq[TM + cl];
     const int nbsh = -s_sh[TM + cl];
     const float rb = s_r[TM + cl];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int lr0 = wm * 64 + 32 * i + 4 * hl;
-      const uint32_t vo = okc && ABL != 1 ? ((uint32_t)lr0 * ld + (uint32_t)cl) * 4u : OOB;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f4 asq = *(const f4*)(s_sq + lr0 + 8 * g);
@@ -1900,40 +1882,74 @@ __device__ __forceinline__ bool h1_epilogue(f16v (&H)[2][2], const float* s_sq, 
           H[i][j][r] = __builtin_amdgcn_exp2f(t.x);
           H[i][j][r + 1] = __builtin_amdgcn_exp2f(t.y);
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float hv = H[i][j][4 * g + e];
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hv), rs_o, (int)(vo + (uint32_t)(8 * g + e) * ld * 4u),
-                                                0, 0);
-        }
-      }
-      if (mirror) {
-        const uint32_t vm = okc && ABL != 1 && ABL != 2 ? ((uint32_t)cl * ld + (uint32_t)lr0) * 4u : OOB;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int lr = lr0 + 8 * q;
-          f4 v;
-          v.x = H[i][j][4 * q + 0];
-          v.y = H[i][j][4 * q + 1];
-          v.z = H[i][j][4 * q + 2];
-          v.w = H[i][j][4 * q + 3];
-          const uint32_t o = lr + 3 < rlim && vm != OOB ? vm + 32u * q : OOB;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v), rs_m, (int)o, 0, 0);
-          if (rlim < TM) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              const uint32_t oc = (lr + 3 >= rlim && lr + c < rlim) ? vm + 32u * q + 4u * c : OOB;
-              const float vc = v[c];
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vc), rs_m, (int)oc, 0, 0);
-            }
-          }
-        }
       }
     }
   }
   return __builtin_amdgcn_ballot_w64(hot) != 0;
 }
 
+// the stores of one 32 x 32 MFMA block (i, j) of a wave's values v: 16 direct
+// 4-B stores per lane, and for a mirroring wave 4 transposed 16-B ones (plus,
+// on the last row tile, a partial quad's values one at a time); out-of-range
+// offsets where a value has no place (the hardware drops those).  ABL
+// (diagnostics): 1 every store dropped, 2 the mirrored ones.
+template <int ABL = 0>
+__device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int lane, int wm, int wn, bool mirror,
+                                               bool valid, float* out, int m0, int n0, int M, int N, int ldo) {
+  constexpr int TM = 256, TN = 128;
+  typedef i4v_t i4v;
+  constexpr uint32_t OOB = 0x80000000u;
+  const int hl = lane >> 5;
+  float* const ob = out + ((int64_t)m0 * ldo + n0);
+  float* const mb = out + ((int64_t)n0 * ldo + m0);
+  const uint32_t ld = (uint32_t)ldo;
+  const int rlim = min(M - m0, TM);
+  const int clim = min(N - n0, TN);
+  const int64_t ob_bytes = min<int64_t>((int64_t)(M - m0) * ldo * 4 - (int64_t)n0 * 4, (int64_t)OOB);
+  const int64_t mb_bytes = min<int64_t>((int64_t)(N - n0) * ldo * 4 - (int64_t)m0 * 4, (int64_t)OOB);
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, (int)ob_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mb, 0, (int)mb_bytes, 0x00020000);
+  const int cl = wn * 64 + 32 * j + (lane & 31);
+  const bool okc = valid && cl < clim && ABL != 1;
+  const int lr0 = wm * 64 + 32 * i + 4 * hl;
+  const uint32_t vo = okc ? ((uint32_t)lr0 * ld + (uint32_t)cl) * 4u : OOB;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float hv = v[r];
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hv), rs_o,
+                                          (int)(vo + (uint32_t)(8 * (r >> 2) + (r & 3)) * ld * 4u), 0, 0);
+  }
+  if (!(mirror && valid) || ABL == 2) return;  // uniform
+  const bool okm = okc;
+  const uint32_t vm = okm ? ((uint32_t)cl * ld + (uint32_t)lr0) * 4u : OOB;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int lr = lr0 + 8 * q;
+    f4 w;
+    w.x = v[4 * q + 0];
+    w.y = v[4 * q + 1];
+    w.z = v[4 * q + 2];
+    w.w = v[4 * q + 3];
+    const uint32_t o = lr + 3 < rlim && okm ? vm + 32u * q : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, w), rs_m, (int)o, 0, 0);
+    if (rlim < TM) {  // uniform: the last row tile — a partial quad's values one at a time
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t oc = (okm && lr + 3 >= rlim && lr + c < rlim) ? vm + 32u * q + 4u * c : OOB;
+        const float vc = w[c];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vc), rs_m, (int)oc, 0, 0);
+      }
+    }
+  }
+}
+
+// The one-product pass: every tile's stores, then vmcnt(0).  (Measured and
+// dropped: the values held in registers and stored in four 20-store chunks
+// behind the next tile's ring stages 0..3, the waits counting them — 10.3 vs
+// 7.2 ms: 33 dwords spilled and the interleaved stores slowed the ring; and
+// two workgroups per CU of four 128 x 64 waves over a ring of 32-k stages,
+// 78 KiB of LDS each — 8.5 vs 7.2 ms: the same bytes in flight per CU and
+// twice the barriers; profiles/r6_gram_adapt/h1_ablation_kernels.txt.)
 template <int ABL = 0>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
@@ -1972,7 +1988,6 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
   uint32_t g = 0;  // stages started over all of this workgroup's tiles: ring buffer g % NB
   {
     const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
-    h1_row_dma(Asq, Bsq, Ash, Bsh, Ar, Br, M, N, s_rows, wave, lane, m0, n0, 0);
 #pragma unroll
     for (int b = 0; b < 2; ++b) {  // stages 0 and 1 (never an odd tail: nst >= 3)
       const uint32_t uA = (uint32_t)(m0 + 32 * wv) * rs + (uint32_t)b * 16;
@@ -1982,6 +1997,7 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
 #pragma unroll
       for (int i = 0; i < 2; ++i) w64p_piece(B, lds, uB, step, dstB, off_e, off_o, b, i);
     }
+    h1_row_dma(Asq, Bsq, Ash, Bsh, Ar, Br, M, N, s_rows, wave, lane, m0, n0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   const int sw = ((lane & 31) >> 1) & 7;
@@ -2038,7 +2054,8 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
         H[1][0] = mfma32_f16(a1, b0, H[1][0]);
         H[1][1] = mfma32_f16(a1, b1, H[1][1]);
       };
-      h8 x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
+      // two fragment sets: a set is re-read right after the MFMAs that read it
+      h8 x0, x1, x2, x3, y0, y1, y2, y3;
       const bool tail = odd && s == nst - 1;  // uniform
       rd(0, x0, x1, x2, x3);
       rd(1, y0, y1, y2, y3);
@@ -2047,17 +2064,17 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
         mma(x0, x1, x2, x3);
         piece(0);
         piece(1);
-        rd(2, z0, z1, z2, z3);
+        rd(2, x0, x1, x2, x3);
         asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
         mma(y0, y1, y2, y3);
         piece(2);
         piece(3);
-        rd(3, x0, x1, x2, x3);
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
-        mma(z0, z1, z2, z3);
-        piece(4);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+        rd(3, y0, y1, y2, y3);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
         mma(x0, x1, x2, x3);
+        piece(4);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
+        mma(y0, y1, y2, y3);
         piece(5);
       } else {
         asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
@@ -2077,14 +2094,18 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
     int el = lane;
     asm volatile("" : "+v"(el));
     const float* rows = (const float*)(s_rows + par * RD);
-    const bool hotw = h1_epilogue<ABL>(H, rows, (const int32_t*)(rows + ROWS), rows + 2 * ROWS, el, wm, wn,
-                                  sym && ty > 2 * tx + (wm >> 1), out, m0, n0, M, N, ldo, gamma, c0, c1);
+    const bool hotw = h1_values(H, rows, (const int32_t*)(rows + ROWS), rows + 2 * ROWS, el, wm, wn, gamma, c0, c1);
     if (hotw && lane == 0) {  // the tile's first report appends it to the list
       if (atomicAdd(tile_hot + L, 1u) == 0u) {
         const uint32_t k = atomicAdd(hot, 1u);
         hot[1 + k] = t;
       }
     }
+    const bool mirror = sym && ty > 2 * tx + (wm >> 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) h1_store_block<ABL>(H[i][j], i, j, el, wm, wn, mirror, true, out, m0, n0, M, N, ldo);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!has_next) break;
     L = Ln;
