@@ -1949,7 +1949,9 @@ __device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int 
 // 7.2 ms: 33 dwords spilled and the interleaved stores slowed the ring; and
 // two workgroups per CU of four 128 x 64 waves over a ring of 32-k stages,
 // 78 KiB of LDS each — 8.5 vs 7.2 ms: the same bytes in flight per CU and
-// twice the barriers; profiles/r6_gram_adapt/h1_ablation_kernels.txt.)
+// twice the barriers; odd workgroups started 4-12 us late so half the CUs
+// multiply while the others store — no change, 6.95-7.00 ms;
+// profiles/r6_gram_adapt/h1_ablation_kernels.txt.)
 template <int ABL = 0>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
@@ -2574,12 +2576,14 @@ struct TileTable {
 };
 // Keyed by (device, tm, tn): the table lives in the memory of the device that
 // launches the GEMM (svmTrain -p N: one rank per device, threads of one process).
-const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym = true) {
+// gm / ch > 0: that grouping instead of the default (the one-product pass: 8 / 64,
+// 6.73-6.93 vs 7.03-7.10 ms for 4 / 32, profiles/r6_gram_adapt/h1_tile_order_sweep.txt)
+const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym = true, int gm = 0, int ch = 0) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int64_t, int64_t, bool>, TileTable> cache;
+  static std::map<std::tuple<int, int64_t, int64_t, bool, int, int>, TileTable> cache;
   const int device = current_device();
   std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find({device, tm, tn, sym});
+  auto it = cache.find({device, tm, tn, sym, gm, ch});
   if (it != cache.end()) return it->second;
   // the needed tiles in groups of GM tile rows, column by column, rows inside a
   // column; chunks of CH consecutive tiles dealt round-robin to the 8 XCDs.
@@ -2587,16 +2591,17 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym 
   // 9.47-9.50 for GM 8 / CH 64 (profiles/r5_gram_tile_order_ab.txt; bit-identical
   // output).  A/B: DPSVM_GRAM_GM / DPSVM_GRAM_CH
   std::vector<uint32_t> order;
-  static const int64_t GM = [] {
+  static const int64_t GM_env = [] {
     const char* e = std::getenv("DPSVM_GRAM_GM");
     const int v = e ? atoi(e) : 4;
     return (int64_t)(v >= 1 && v <= 64 ? v : 4);
   }();
-  static const int64_t CH = [] {
+  static const int64_t CH_env = [] {
     const char* e = std::getenv("DPSVM_GRAM_CH");
     const int v = e ? atoi(e) : 32;
     return (int64_t)(v >= 8 && v <= 1024 ? v : 32);
   }();
+  const int64_t GM = gm > 0 ? gm : GM_env, CH = ch > 0 ? ch : CH_env;
   for (int64_t g0 = 0; g0 < tm; g0 += GM) {
     const int64_t gm = std::min(GM, tm - g0);
     for (int64_t ty = 0; ty < tn; ++ty)
@@ -2618,7 +2623,7 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym 
   HIP_CHECK(hipMalloc((void**)&t.dev, (size_t)total * sizeof(uint32_t)));
   HIP_CHECK(hipMemcpyAsync(t.dev, tab.data(), (size_t)total * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  return cache.emplace(std::make_tuple(device, tm, tn, sym), t).first->second;
+  return cache.emplace(std::make_tuple(device, tm, tn, sym, gm, ch), t).first->second;
 }
 }  // namespace
 
@@ -2713,6 +2718,11 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const int64_t ntiles = t.count;
       const int64_t grid = std::min<int64_t>(ntiles, cus);
       if (pe && cold_tau > 0.f && gamma > 0.f && nkb >= 5 && !g_gram_stamps) {
+        static const bool h1_order = [] {  // A/B: DPSVM_H1_ORDER=0 keeps the three-product kernel's grouping
+          const char* e = std::getenv("DPSVM_H1_ORDER");
+          return !(e && e[0] == '0') && !std::getenv("DPSVM_GRAM_GM") && !std::getenv("DPSVM_GRAM_CH");
+        }();
+        const auto& t1 = h1_order ? sym_tile_table(tm2, tn, s, symmetric, 8, 64) : t;
         // adaptive: pass 1 one-product over every tile, pass 2 three products over the reported ones
         const double e = 4.5 * std::ldexp(1.0, -11) * (double)gamma;  // E = e |a| |b| (split_cold)
         const float c1 = (float)(-std::log2(e));
@@ -2740,7 +2750,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
                                  : dev::rbf_gemm_split_h1_kernel<0>;
         h1k<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
             (const dev::u4*)A, Ash, Asq, r, (int)M, (const dev::u4*)B, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1, out,
-            (int)ldo, symmetric ? 1 : 0, tab, (int)ntiles, hb, hb + ntiles);
+            (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
         post_launch("rbf_gemm_split_h1", s);
         dev::rbf_gemm_split_w64p_kernel<0, true, true><<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
             (const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B, Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
