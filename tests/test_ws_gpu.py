@@ -118,11 +118,13 @@ def test_ws_cache_engine_bit_identical_to_resident_gram(case):
     """ws-cache (kernel-row cache, the set's missing rows by one indexed MFMA
     GEMM per round, CLOCK-window victims) follows the ws-dense trajectory bit
     for bit: the same K values (same GEMM arithmetic), the same merge, the same
-    f-update order.  A cache of ~900-2000 lines forces evictions."""
+    f-update order.  A cache of ~900-2000 lines forces evictions.  (The
+    resident Gram three-product, gram_adapt off: the rows GEMM has no
+    one-product pass, docs/DESIGN.md §13.)"""
     name, n, C_, g, lines = case
     X, y = synthetic(name, n=n, seed=5)
     kw = dict(C=C_, gamma=g, eps=1e-3, device="cuda", solver="ws")
-    dense = SVC(**kw).fit(X, y)
+    dense = SVC(gram_adapt="off", **kw).fit(X, y)
     cache = SVC(force_cache=True, cache_lines=lines, ws_recompute="off", **kw).fit(X, y)
     assert dense.setup_info_["iteration"] == "ws-dense"
     assert cache.setup_info_["iteration"] == "ws-cache" and cache.setup_info_["cache_lines"] == lines
@@ -745,10 +747,11 @@ def test_ws_cache_multi_block_bit_identical_to_resident_gram(clip):
     an 8192-line CLOCK window (misses computed by one row GEMM per round).  The
     K values and the round arithmetic are the dense engine's, so the trajectory
     — including the adaptive block count — is bit-identical to ws-dense with the
-    same blocks, with a cache small enough to evict."""
+    same blocks (its Gram three-product: gram_adapt off), with a cache small
+    enough to evict."""
     X, y = synthetic("mnist", n=14000, seed=12)
     kw = dict(C=10.0, gamma=0.25, eps=1e-3, clip=clip, device="cuda", solver="ws", ws_blocks=4, ws_size=64)
-    dense = SVC(**kw).fit(X, y)
+    dense = SVC(gram_adapt="off", **kw).fit(X, y)
     cache = SVC(force_cache=True, cache_lines=9000, **kw).fit(X, y)
     assert dense.setup_info_["iteration"] == "ws-dense" and cache.setup_info_["iteration"] == "ws-cache"
     assert "ws_blocks" not in cache.setup_info_.get("engine_note", "")
