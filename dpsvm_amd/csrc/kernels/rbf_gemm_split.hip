@@ -1952,7 +1952,11 @@ __device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int 
 // twice the barriers; odd workgroups started 4-12 us late so half the CUs
 // multiply while the others store — no change, 6.95-7.00 ms;
 // profiles/r6_gram_adapt/h1_ablation_kernels.txt.)
-template <int ABL = 0>
+// HP: A / B are h planes (split_hplane: the h halves of a row's split blocks
+// back to back, padded to an even block count with zeros) — a ring stage is one
+// whole 128-B line per row, where the split rows give every line's h half only
+// (half of each L2 line fetched unused).
+template <int ABL = 0, bool HP = false>
 __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
     const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
     const float* __restrict__ Ar, int M, const u4* __restrict__ B, const int32_t* __restrict__ Bsh,
@@ -1969,19 +1973,20 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
   uint32_t t = tiles[L];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
-  const uint32_t rs = (uint32_t)nkb * 8;  // u4 per split row
-  const int nst = (nkb + 1) >> 1;         // ring stages a tile (launcher: nkb >= 5)
+  const int nst = (nkb + 1) >> 1;  // ring stages a tile (launcher: nkb >= 5)
+  const uint32_t rs = HP ? (uint32_t)nst * 8 : (uint32_t)nkb * 8;  // u4 per operand row
   const bool odd = (nkb & 1) != 0;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t step = 8 * rs;
   // lane byte offsets of a piece (even / odd pieces: swizzle lane >> 4 / (lane >> 4) + 4, as w64p);
-  // _t: an odd block count's last stage (virtual chunks 4..7 re-read block 2 s)
+  // _t: an odd block count's last stage (split rows: virtual chunks 4..7 re-read block 2 s; h planes:
+  // the zero pad)
   const int p = lane & 7, ve = p ^ (lane >> 4), vd = p ^ ((lane >> 4) + 4);
   const uint32_t rowb = (uint32_t)(lane >> 3) * rs;
-  uint32_t off_e = 16u * (rowb + (uint32_t)((ve >> 2) * 8 + (ve & 3)));
-  uint32_t off_o = 16u * (rowb + (uint32_t)((vd >> 2) * 8 + (vd & 3)));
-  uint32_t off_et = 16u * (rowb + (uint32_t)(ve & 3));
-  uint32_t off_ot = 16u * (rowb + (uint32_t)(vd & 3));
+  uint32_t off_e = 16u * (rowb + (uint32_t)(HP ? ve : (ve >> 2) * 8 + (ve & 3)));
+  uint32_t off_o = 16u * (rowb + (uint32_t)(HP ? vd : (vd >> 2) * 8 + (vd & 3)));
+  uint32_t off_et = HP ? off_e : 16u * (rowb + (uint32_t)(ve & 3));
+  uint32_t off_ot = HP ? off_o : 16u * (rowb + (uint32_t)(vd & 3));
   asm volatile("" : "+v"(off_e), "+v"(off_o), "+v"(off_et), "+v"(off_ot));
   const int dstA = 32 * wv * 8, dstB = (TM + 16 * wv) * 8;
   int Ln = L + G;
@@ -1992,8 +1997,8 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
     const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {  // stages 0 and 1 (never an odd tail: nst >= 3)
-      const uint32_t uA = (uint32_t)(m0 + 32 * wv) * rs + (uint32_t)b * 16;
-      const uint32_t uB = (uint32_t)(n0 + 16 * wv) * rs + (uint32_t)b * 16;
+      const uint32_t uA = (uint32_t)(m0 + 32 * wv) * rs + (uint32_t)b * (HP ? 8 : 16);
+      const uint32_t uB = (uint32_t)(n0 + 16 * wv) * rs + (uint32_t)b * (HP ? 8 : 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) w64p_piece(A, lds, uA, step, dstA, off_e, off_o, b, i);
 #pragma unroll
@@ -2029,8 +2034,8 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
       const int ps = own ? s + 2 : s + 2 - nst;
       const bool ptail = odd && ps == nst - 1;  // uniform
       const uint32_t pe_ = ptail ? off_et : off_e, po_ = ptail ? off_ot : off_o;
-      const uint32_t uA = (uint32_t)((own ? m0 : nm0) + 32 * wv) * rs + (uint32_t)ps * 16;
-      const uint32_t uB = (uint32_t)((own ? n0 : nn0) + 16 * wv) * rs + (uint32_t)ps * 16;
+      const uint32_t uA = (uint32_t)((own ? m0 : nm0) + 32 * wv) * rs + (uint32_t)ps * (HP ? 8 : 16);
+      const uint32_t uB = (uint32_t)((own ? n0 : nn0) + 16 * wv) * rs + (uint32_t)ps * (HP ? 8 : 16);
       const int pbuf = (int)((g + 2) % NB);
       auto piece = [&](int j) {  // A0, A1, B0, A2, A3, B1
         __builtin_amdgcn_sched_barrier(0);
@@ -2116,6 +2121,18 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
     Ln = L + G;
     if (Ln < ntiles) tn_next = tiles[Ln];
   }
+}
+
+// h planes of split rows (the one-product pass's operands): row r holds the h
+// halves of its nkb split blocks back to back, then zeros to an even count
+__global__ __launch_bounds__(256) void split_hplane_kernel(const u4* __restrict__ src, int64_t rows, int nkb,
+                                                          u4* __restrict__ dst) {
+  const int nq = ((nkb + 1) >> 1) * 8;  // u4 per plane row
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * nq) return;
+  const int64_t r = e / nq;
+  const int q = (int)(e - r * nq), b = q >> 2, c = q & 3;
+  dst[e] = b < nkb ? src[r * nkb * 8 + b * 8 + c] : u4{0u, 0u, 0u, 0u};
 }
 
 // R = log2 |x| = split_log2norm(|x|^2) of n rows (the adaptive Gram's rule input)
@@ -2744,13 +2761,37 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
           const char* e = std::getenv("DPSVM_H1_ABLATE");
           return e ? atoi(e) : 0;
         }();
-        auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1>
-                   : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2>
-                   : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3>
-                                 : dev::rbf_gemm_split_h1_kernel<0>;
+        static const bool h1_planes = [] {  // A/B: DPSVM_H1_PLANES=0 reads the split rows' h halves
+          const char* e = std::getenv("DPSVM_H1_PLANES");
+          return !(e && e[0] == '0');
+        }();
+        const void *hA = A, *hB = B;
+        dev::u4* planes = nullptr;
+        if (h1_planes) {  // the h planes of the rows the tiles read (whole 256 / 128-row tiles)
+          const int64_t nq = (int64_t)((nkb + 1) / 2) * 8, ra = tm2 * 256, rb = symmetric ? 0 : tn * 128;
+          HIP_CHECK(hipMallocAsync((void**)&planes, (size_t)(ra + rb) * nq * 16, s));
+          dev::split_hplane_kernel<<<dim3((unsigned)((ra * nq + 255) / 256)), 256, 0, s>>>((const dev::u4*)A, ra,
+                                                                                            nkb, planes);
+          hA = hB = planes;
+          if (!symmetric) {
+            dev::split_hplane_kernel<<<dim3((unsigned)((rb * nq + 255) / 256)), 256, 0, s>>>((const dev::u4*)B, rb,
+                                                                                              nkb, planes + ra * nq);
+            hB = planes + ra * nq;
+          }
+          post_launch("split_hplane", s);
+        }
+        auto h1k = h1_planes ? (h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1, true>
+                                : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2, true>
+                                : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3, true>
+                                              : dev::rbf_gemm_split_h1_kernel<0, true>)
+                             : (h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1>
+                                : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2>
+                                : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3>
+                                              : dev::rbf_gemm_split_h1_kernel<0>);
         h1k<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
-            (const dev::u4*)A, Ash, Asq, r, (int)M, (const dev::u4*)B, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1, out,
-            (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
+            (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1,
+            out, (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
+        if (planes) HIP_CHECK(hipFreeAsync(planes, s));
         post_launch("rbf_gemm_split_h1", s);
         dev::rbf_gemm_split_w64p_kernel<0, true, true><<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
             (const dev::u4*)A, Ash, Asq, (int)M, (const dev::u4*)B, Bsh, Bsq, (int)N, nkb, gamma, out, (int)ldo,
