@@ -2123,6 +2123,207 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// One-product pass with specialised waves (h1s, the default): the h1 kernel's
+// eight 64 x 64 compute waves plus four DMA waves (768 threads).  In h1 every
+// wave both feeds the LDS-DMA ring and stores its tile, and gfx950 counts
+// both in one in-order vmcnt: each tile ends waiting on its own stores before
+// the ring can go on.  Here only the DMA waves issue loads and wait on vmcnt
+// (h1s_dma, a function of its own so its addressing does not crowd the
+// compute waves' scalar registers); the compute waves never wait on a load,
+// so a tile's stores drain while the next tile multiplies.  The two meet at
+// one barrier per ring stage: the DMA waves have waited for stage s, the
+// compute waves have read stage s - 1, whose buffer the DMA waves then refill
+// with stage s + 2; row data of tile t + 1 is loaded during tile t's stage 0.
+// Operands: h planes.  6.10 vs 6.32 ms symmetric, 1.11 vs 1.13 ms slab
+// (profiles/r6_gram_adapt/h1_ablation_kernels.txt): the stores' cost is their
+// bytes more than their latency.  Same H sequence per element.
+// ---------------------------------------------------------------------------
+// the h1s kernel's DMA waves (a function of its own: its uniform addressing
+// does not share the compute waves' scalar registers)
+__device__ __noinline__ void h1s_dma(const u4* __restrict__ A, const int32_t* __restrict__ Ash,
+                                     const float* __restrict__ Asq, const float* __restrict__ Ar, int M,
+                                     const u4* __restrict__ B, const int32_t* __restrict__ Bsh,
+                                     const float* __restrict__ Bsq, const float* __restrict__ Br, int N, int nst,
+                                     const uint32_t* __restrict__ tiles, int ntiles, int L, int dwave, int lane,
+                                     u4* lds, uint32_t* s_rows) {
+  constexpr int TM = 256, TN = 128, ROWS = TM + TN, NB = 3, RD = 1536;
+  const int G = gridDim.x;
+  const uint32_t rs = (uint32_t)nst * 8;
+  uint32_t t = tiles[L];
+  int Ln = L + G;
+  uint32_t tn_next = Ln < ntiles ? tiles[Ln] : 0u;
+  uint32_t g = 0;
+  const int dw = __builtin_amdgcn_readfirstlane(dwave);
+    const int p = lane & 7;
+    uint32_t off_e = 16u * ((uint32_t)(lane >> 3) * rs + (uint32_t)(p ^ (lane >> 4)));
+    uint32_t off_o = 16u * ((uint32_t)(lane >> 3) * rs + (uint32_t)(p ^ ((lane >> 4) + 4)));
+    asm volatile("" : "+v"(off_e), "+v"(off_o));
+    auto stage = [&](int m0_, int n0_, int st, int buf) {
+      const uint32_t uA = (uint32_t)(m0_ + 64 * dw) * rs + (uint32_t)st * 8;
+      const uint32_t uB = (uint32_t)(n0_ + 32 * dw) * rs + (uint32_t)st * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w64p_piece(A, lds, uA, 8 * rs, 64 * dw * 8, off_e, off_o, buf, i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w64p_piece(B, lds, uB, 8 * rs, (TM + 32 * dw) * 8, off_e, off_o, buf, i);
+    };
+    // row data: DMA wave dw = 0 / 1 / 2 loads |x|^2 / shifts / log2 |x| of the 384 rows (six chunks of 64:
+    // A rows for i < 4); wave 3 loads a valid word into the padding (every stage wait counts 6)
+    const uint32_t* const rd_a =
+        dw == 0 ? (const uint32_t*)Asq : dw == 1 ? (const uint32_t*)Ash : (const uint32_t*)Ar;
+    const uint32_t* const rd_b =
+        dw == 0 ? (const uint32_t*)Bsq : dw == 1 ? (const uint32_t*)Bsh : (const uint32_t*)Br;
+    auto rowdata = [&](int m0_, int n0_, int par_) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int r = 64 * i + lane;
+        const int ri = i < 4 ? min(m0_ + r, M - 1) : min(n0_ + (r - TM), N - 1);
+        const uint32_t* src = dw == 3 ? (const uint32_t*)Asq : (i < 4 ? rd_a : rd_b) + ri;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)src, (__attribute__((address_space(3))) void*)(s_rows + par_ * RD + 64 * (6 * dw + i)),
+            4, 0, 0);
+      }
+    };
+    {
+      const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
+      stage(m0, n0, 0, 0);
+      stage(m0, n0, 1, 1);
+      rowdata(m0, n0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    int par = 0;
+    while (true) {
+      const bool has_next = Ln < ntiles;  // uniform
+      const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
+      const uint32_t tp = has_next ? tn_next : t;
+      const int nm0 = (int)(tp >> 16) * TM, nn0 = (int)(tp & 0xffffu) * TN;
+#pragma clang loop unroll(disable)
+      for (int s = 0; s < nst; ++s) {
+        // stage s landed: younger are stage s + 1 (12 pieces) and, at s == 1, the next tile's row data (6)
+        if (s == 1) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const bool own = s + 2 < nst;
+        stage(own ? m0 : nm0, own ? n0 : nn0, own ? s + 2 : s + 2 - nst, (int)((g + 2) % NB));
+        // the next tile's row data (the last tile reloads its own into the unused parity: the count stays 6)
+        if (s == 0) rowdata(nm0, nn0, par ^ 1);
+        ++g;
+      }
+      if (!has_next) break;
+      L = Ln;
+      t = tn_next;
+      par ^= 1;
+      Ln = L + G;
+      if (Ln < ntiles) tn_next = tiles[Ln];
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+constexpr int kH1sThreads = 768;  // 8 compute waves + 4 DMA waves
+template <int ABL = 0>
+__global__ __launch_bounds__(kH1sThreads, 1) void rbf_gemm_split_h1s_kernel(
+    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
+    const float* __restrict__ Ar, int M, const u4* __restrict__ B, const int32_t* __restrict__ Bsh,
+    const float* __restrict__ Bsq, const float* __restrict__ Br, int N, int nkb, float gamma, float c0, float c1,
+    float* __restrict__ out, int ldo, int sym, const uint32_t* __restrict__ tiles, int ntiles,
+    uint32_t* __restrict__ tile_hot, uint32_t* __restrict__ hot) {
+  constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3, RD = 1536;
+  __shared__ u4 lds[NB * BUF + 2 * RD / 4];  // 3 operand buffers, then row data [2][RD]
+  uint32_t* const s_rows = (uint32_t*)(lds + NB * BUF);
+  const int G = gridDim.x;
+  int L = blockIdx.x;
+  if (L >= ntiles) return;  // uniform
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nst = (nkb + 1) >> 1;  // ring stages a tile (launcher: nkb >= 5)
+  if (__builtin_amdgcn_readfirstlane(wave) >= 8) {
+    h1s_dma(A, Ash, Asq, Ar, M, B, Bsh, Bsq, Br, N, nst, tiles, ntiles, L, wave - 8, lane, lds, s_rows);
+    return;
+  }
+  // ---- compute waves: the h1 kernel's 64 x 64 waves; never a load, so their stores drain unwaited ----
+  uint32_t t = tiles[L];
+  int Ln = L + G;
+  uint32_t tn_next = Ln < ntiles ? tiles[Ln] : 0u;
+  uint32_t g = 0;
+  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int ra0 = (wm * 64 + (lane & 31)) * CPR;
+  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
+  int par = 0;
+  while (true) {
+    const bool has_next = Ln < ntiles;  // uniform
+    const int tx = (int)(t >> 16), ty = (int)(t & 0xffffu);
+    const int m0 = tx * TM, n0 = ty * TN;
+    f16v H[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) H[i][j][r] = 0.f;
+#pragma clang loop unroll(disable)
+    for (int s = 0; s < nst; ++s) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const u4* buf = lds + (g % NB) * BUF;
+      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
+      auto rd = [&](int q, h8& a0, h8& a1, h8& b0, h8& b1) {
+        const uint32_t c = 16u * (uint32_t)((2 * q + hl) ^ sw);
+        const uint32_t pa = abase + c, pb = bbase + c;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(a0) : "v"(pa) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(a1) : "v"(pa) : "memory");
+        asm volatile("ds_read_b128 %0, %1" : "=v"(b0) : "v"(pb) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(b1) : "v"(pb) : "memory");
+      };
+      auto mma = [&](const h8& a0, const h8& a1, const h8& b0, const h8& b1) {
+        if (ABL == 3) return;
+        H[0][0] = mfma32_f16(a0, b0, H[0][0]);
+        H[0][1] = mfma32_f16(a0, b1, H[0][1]);
+        H[1][0] = mfma32_f16(a1, b0, H[1][0]);
+        H[1][1] = mfma32_f16(a1, b1, H[1][1]);
+      };
+      // (an odd block count's last stage multiplies the h plane's zero pad: H + 0 is H, bit for bit)
+      h8 x0, x1, x2, x3, y0, y1, y2, y3;
+      rd(0, x0, x1, x2, x3);
+      rd(1, y0, y1, y2, y3);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+      mma(x0, x1, x2, x3);
+      rd(2, x0, x1, x2, x3);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
+      mma(y0, y1, y2, y3);
+      rd(3, y0, y1, y2, y3);
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+      mma(x0, x1, x2, x3);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
+      mma(y0, y1, y2, y3);
+      ++g;
+    }
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const float* rows = (const float*)(s_rows + par * RD);
+    const bool hotw = h1_values(H, rows, (const int32_t*)(rows + ROWS), rows + 2 * ROWS, el, wm, wn, gamma, c0, c1);
+    const bool mirror = sym && ty > 2 * tx + (wm >> 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) h1_store_block<ABL>(H[i][j], i, j, el, wm, wn, mirror, true, out, m0, n0, M, N, ldo);
+    if (hotw && lane == 0) {  // the tile's first report appends it to the list
+      if (atomicAdd(tile_hot + L, 1u) == 0u) {
+        const uint32_t k = atomicAdd(hot, 1u);
+        hot[1 + k] = t;
+      }
+    }
+    if (!has_next) break;
+    L = Ln;
+    t = tn_next;
+    par ^= 1;
+    Ln = L + G;
+    if (Ln < ntiles) tn_next = tiles[Ln];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // h planes of split rows (the one-product pass's operands): row r holds the h
 // halves of its nkb split blocks back to back, then zeros to an even count
 __global__ __launch_bounds__(256) void split_hplane_kernel(const u4* __restrict__ src, int64_t rows, int nkb,
@@ -2761,13 +2962,9 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
           const char* e = std::getenv("DPSVM_H1_ABLATE");
           return e ? atoi(e) : 0;
         }();
-        static const bool h1_planes = [] {  // A/B: DPSVM_H1_PLANES=0 reads the split rows' h halves
-          const char* e = std::getenv("DPSVM_H1_PLANES");
-          return !(e && e[0] == '0');
-        }();
         const void *hA = A, *hB = B;
         dev::u4* planes = nullptr;
-        if (h1_planes) {  // the h planes of the rows the tiles read (whole 256 / 128-row tiles)
+        {  // the h planes of the rows the tiles read (whole 256 / 128-row tiles)
           const int64_t nq = (int64_t)((nkb + 1) / 2) * 8, ra = tm2 * 256, rb = symmetric ? 0 : tn * 128;
           HIP_CHECK(hipMallocAsync((void**)&planes, (size_t)(ra + rb) * nq * 16, s));
           dev::split_hplane_kernel<<<dim3((unsigned)((ra * nq + 255) / 256)), 256, 0, s>>>((const dev::u4*)A, ra,
@@ -2780,17 +2977,27 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
           }
           post_launch("split_hplane", s);
         }
-        auto h1k = h1_planes ? (h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1, true>
-                                : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2, true>
-                                : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3, true>
-                                              : dev::rbf_gemm_split_h1_kernel<0, true>)
-                             : (h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1>
-                                : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2>
-                                : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3>
-                                              : dev::rbf_gemm_split_h1_kernel<0>);
-        h1k<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
-            (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1,
-            out, (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
+        static const bool h1_spec = [] {  // A/B: DPSVM_H1_SPEC=0 the h1 kernel (every wave loads and stores)
+          const char* e = std::getenv("DPSVM_H1_SPEC");
+          return !(e && e[0] == '0');
+        }();
+        if (h1_spec) {
+          auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1s_kernel<1>
+                     : h1_abl == 2 ? dev::rbf_gemm_split_h1s_kernel<2>
+                     : h1_abl == 3 ? dev::rbf_gemm_split_h1s_kernel<3>
+                                   : dev::rbf_gemm_split_h1s_kernel<0>;
+          h1k<<<dim3((unsigned)grid), dev::kH1sThreads, 0, s>>>(
+              (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1,
+              out, (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
+        } else {
+          auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1, true>
+                     : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2, true>
+                     : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3, true>
+                                   : dev::rbf_gemm_split_h1_kernel<0, true>;
+          h1k<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
+              (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1,
+              out, (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
+        }
         if (planes) HIP_CHECK(hipFreeAsync(planes, s));
         post_launch("rbf_gemm_split_h1", s);
         dev::rbf_gemm_split_w64p_kernel<0, true, true><<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
