@@ -139,6 +139,8 @@ void set_rows_stamps(uint64_t* p);  // diagnostics: the LDS-DMA rows kernel's pe
 void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, int64_t M, const void* B,
                           const int32_t* Bsh, const float* Bsq, int64_t N, int dp, float gamma, float* out,
                           int64_t ldo, hipStream_t s, bool symmetric = false, float cold_tau = 0.f);
+// split_cold's constants c0, c1 for gamma, tau (host; docs/DESIGN.md §13)
+void split_cold_consts(float gamma, float tau, float* c0, float* c1);
 // the calling thread's last adaptive Gram: tiles of the one-product pass and the hot ones recomputed (valid once
 // the stream passed the GEMM; -1 / -1 when the last Gram was not adaptive)
 void gram_adapt_last(int64_t* tiles, int64_t* hot);

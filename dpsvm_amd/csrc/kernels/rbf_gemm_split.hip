@@ -2845,6 +2845,15 @@ const TileTable& sym_tile_table(int64_t tm, int64_t tn, hipStream_t s, bool sym 
 }
 }  // namespace
 
+// split_cold's constants: E = e |a| |b| with e = 4.5 2^-11 gamma bounds gamma times the one- vs
+// three-product d^2 difference; cold iff R_i + R_j <= c1 (E <= 1) and t1 <= c0 - (R_i + R_j)
+// (1.72 K1 E <= tau, e^E - 1 <= 1.72 E for E <= 1), c0 with a 0.01 (0.7%) margin in log2
+void split_cold_consts(float gamma, float tau, float* c0, float* c1) {
+  const double e = 4.5 * std::ldexp(1.0, -11) * (double)gamma;
+  *c1 = (float)(-std::log2(e));
+  *c0 = (float)(std::log2((double)tau) - std::log2(1.72 * e) - 0.01);
+}
+
 namespace {
 // the calling thread's last adaptive Gram (svmTrain -p N: one rank per thread)
 thread_local int64_t t_adapt_tiles = -1;
@@ -2942,9 +2951,8 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
         }();
         const auto& t1 = h1_order ? sym_tile_table(tm2, tn, s, symmetric, 8, 64) : t;
         // adaptive: pass 1 one-product over every tile, pass 2 three products over the reported ones
-        const double e = 4.5 * std::ldexp(1.0, -11) * (double)gamma;  // E = e |a| |b| (split_cold)
-        const float c1 = (float)(-std::log2(e));
-        const float c0 = (float)(std::log2((double)cold_tau) - std::log2(1.72 * e) - 0.01);
+        float c0 = 0.f, c1 = 0.f;
+        split_cold_consts(gamma, cold_tau, &c0, &c1);
         const int64_t nr = symmetric ? M : M + N;
         float* r = nullptr;
         uint32_t* hb = nullptr;  // [ntiles] per-tile reports, then the list's length and entries

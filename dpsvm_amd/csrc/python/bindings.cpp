@@ -596,6 +596,11 @@ PYBIND11_MODULE(_C, m) {
                             (float*)out, out_ld, sym, (void*)stream, cold_tau);
   }, py::arg("a"), py::arg("asq"), py::arg("m"), py::arg("b"), py::arg("bsq"), py::arg("n"), py::arg("ld"),
      py::arg("gamma"), py::arg("out"), py::arg("out_ld"), py::arg("sym"), py::arg("stream"), py::arg("cold_tau") = 0.f);
+  m.def("split_cold_consts", [](float gamma, float tau) {
+    float c0 = 0.f, c1 = 0.f;
+    launch::split_cold_consts(gamma, tau, &c0, &c1);
+    return py::make_tuple(c0, c1);
+  }, "the adaptive Gram's element rule constants (c0, c1): cold iff R_i + R_j <= c1 and t1 <= c0 - (R_i + R_j)");
   m.def("k_gram_adapt_last", []() { return kernels::gram_adapt_last(); },
         "(one-product tiles, hot tiles) of the calling thread's last adaptive split Gram, or (-1, -1)");
   m.def("k_fused_select", [](uintptr_t f, uintptr_t alpha, uintptr_t y, int64_t n, float C, int rows, uintptr_t out,
