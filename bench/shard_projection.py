@@ -79,16 +79,19 @@ def main() -> int:
                             "extra_us_per_round": round(1e6 * (t_px - t_loc) / max(1, px.n_rounds_), 2)}
 
     # one rank's Gram slab: K(all rows, n / P columns), non-symmetric GEMM
+    # (the adaptive Gram when the local solve ran it, docs/DESIGN.md §13: every rank applies the same rule)
     xt = torch.tensor(X, device="cuda")
+    tau = 2.0 ** -22 if loc.setup_info_.get("gram") == "split-f16-adaptive" else 0.0
+    out["gram_slab_mode"] = "adaptive" if tau else "three-product"
     slabs = {}
     for P in (1, 2, 4, 8):
         cols = xt[: (a.samples + P - 1) // P]
-        K.rbf_gram(xt, cols, 0.25, split=True)  # warm
+        K.rbf_gram(xt, cols, 0.25, split=True, cold_tau=tau)  # warm
         torch.cuda.synchronize()
         ts = []
         for _ in range(a.reps):
             t0 = time.perf_counter()
-            K.rbf_gram(xt, cols, 0.25, split=True)
+            K.rbf_gram(xt, cols, 0.25, split=True, cold_tau=tau)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         slabs[P] = round(min(ts), 6)
