@@ -869,6 +869,11 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     w.clip_fallback = m.p.ws_clip_fallback ? 1 : 0;
     DPSVM_CHECK(m.p.ws_rel >= 0.f && m.p.ws_rel < 1.f, "ws_rel must be in [0, 1)");
     w.rel_local = m.p.ws_rel;
+    static const float rel_local_env = [] {  // A/B: DPSVM_WS_REL_LOCAL (the gap fraction only; the floor keeps ws_rel)
+      const char* e = std::getenv("DPSVM_WS_REL_LOCAL");
+      return e ? (float)atof(e) : -1.f;
+    }();
+    if (rel_local_env > 0.f && rel_local_env < 1.f) w.rel_local = rel_local_env;
     // sub-problem tolerance ws_rel * max(eps, gap / 2): floored at ws_rel * eps
     // rather than eps, rounds near the end keep taking steps (adult-shape:
     // 0.230 -> 0.206 s; headline unchanged; profiles/r2_ws_param_sweep2.txt)
