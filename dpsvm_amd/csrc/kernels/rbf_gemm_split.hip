@@ -1854,6 +1854,9 @@ __device__ __forceinline__ bool h1_values(f16v (&H)[2][2], const float* s_sq, co
     const float rb = s_r[TM + cl];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      // one 32 x 32 block's row data at a time (the scheduler hoisting every
+      // block's LDS reads ahead made the specialised kernel spill)
+      __builtin_amdgcn_sched_barrier(0);
       const int lr0 = wm * 64 + 32 * i + 4 * hl;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -2307,7 +2310,10 @@ __global__ __launch_bounds__(kH1sThreads, 1) void rbf_gemm_split_h1s_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) h1_store_block<ABL>(H[i][j], i, j, el, wm, wn, mirror, true, out, m0, n0, M, N, ldo);
+      for (int j = 0; j < 2; ++j) {
+        __builtin_amdgcn_sched_barrier(0);
+        h1_store_block<ABL>(H[i][j], i, j, el, wm, wn, mirror, true, out, m0, n0, M, N, ldo);
+      }
     if (hotw && lane == 0) {  // the tile's first report appends it to the list
       if (atomicAdd(tile_hot + L, 1u) == 0u) {
         const uint32_t k = atomicAdd(hot, 1u);
