@@ -2940,7 +2940,15 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
                        M * ldo < (1ll << 32) && N * ldo < (1ll << 32);
     const bool persist = (variant == 7 || variant == 12 || (variant == 0 && persist_env == 1 && spread)) && nkb >= 3 && nt == 0 && idx32 &&
                          tm2 < 65536 && tn < 65536 && (!symmetric || compact);
-    if (persist) {
+    // the adaptive Gram's kernels (h1s, w64p with the packed epilogue) index a tile's stores from
+    // 64-bit tile bases with 32-bit offsets (256 rows x ldo x 4 B < 2^32) and the operand rows in
+    // 32 bits: they also take Grams of more than 2^32 elements (200k rows: 160 GB)
+    const bool idx_adapt = (M + 512) * (int64_t)nkb * 8 < (1ll << 31) && (N + 512) * (int64_t)nkb * 8 < (1ll << 31) &&
+                           ldo < (1ll << 22);
+    const bool adapt = pe && cold_tau > 0.f && gamma > 0.f && nkb >= 5 && !g_gram_stamps && nt == 0 && idx_adapt &&
+                       tm2 < 65536 && tn < 65536 && (!symmetric || compact) &&
+                       (variant == 0 || variant == 7 || variant == 12);
+    if (persist || adapt) {
       const int cus = [] {
         int n = 0;
         HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, current_device()));
@@ -2950,7 +2958,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
       const uint32_t* tab = t.dev;
       const int64_t ntiles = t.count;
       const int64_t grid = std::min<int64_t>(ntiles, cus);
-      if (pe && cold_tau > 0.f && gamma > 0.f && nkb >= 5 && !g_gram_stamps) {
+      if (adapt) {
         static const bool h1_order = [] {  // A/B: DPSVM_H1_ORDER=0 keeps the three-product kernel's grouping
           const char* e = std::getenv("DPSVM_H1_ORDER");
           return !(e && e[0] == '0') && !std::getenv("DPSVM_GRAM_GM") && !std::getenv("DPSVM_GRAM_CH");

@@ -823,9 +823,9 @@ GpuSetupInfo GpuSolver::setup(const float* xh, int64_t n_x_rows, int64_t n, int 
     DPSVM_CHECK(mode >= 0 && mode <= 2, "gram_adapt must be 0 (auto), 1 (on) or 2 (off)");
     DPSVM_CHECK(m.p.gram_cold_tau > 0.f && m.p.gram_cold_tau <= 1e-3f, "gram_cold_tau must be in (0, 1e-3]");
     // (the one-product pass needs >= 5 split blocks a row: dp > 128; shorter rows keep the three-product Gram)
-    // and 32-bit tile indexing of the persistent kernels (rbf_gemm_store_split's idx32: n x ldl < 2^32)
+    // and the adaptive kernels' indexing (rbf_gemm_store_split's idx_adapt)
     const bool cand = m.gram_split && m.kind == EngineKind::WsDense && mode != 2 && m.gamma > 0.f && m.dp > 128 &&
-                      (int64_t)n * m.ldl < (1ll << 32) && m.ldl < (1ll << 24);
+                      (int64_t)(n + 512) * ((m.dp + 31) / 32) * 8 < (1ll << 31) && m.ldl < (1ll << 22);
     const bool ok = cand && (mode == 1 || gram_cold_sample_ok(xh, n_x_rows, d, m.gamma, m.p.gram_cold_tau));
     m.gram_cold_tau = m.all_agree(ok, m.comm, m.world) ? m.p.gram_cold_tau : 0.f;
     if (m.gram_cold_tau > 0.f) m.info.gram = "split-f16-adaptive";
