@@ -1806,36 +1806,20 @@ __global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_w64p_kernel(
 // those tiles with all three products.  The H accumulator's MFMA sequence is
 // the three-product kernels' (same k order), so K1 and the rule's inputs are
 // the same bits in both passes.
-// Tiles, waves and the persistent LDS-DMA ring are the w64p kernel's; a ring
-// stage is 64 k of h planes (split blocks 2 s and 2 s + 1: LDS row chunk p
-// holds virtual chunk v = p ^ swizzle, the h chunk v & 3 of block 2 s + (v >> 2));
-// an odd block count's last stage loads block 2 s twice and multiplies its
-// first two k steps only.  64 accumulator registers instead of 192.
+// Tiles and the persistent LDS-DMA ring are the w64p kernel's; the operands are
+// h planes (split_hplane_kernel: a row's h halves back to back, zero-padded to an
+// even block count), so a ring stage is 64 k = one whole 128-B line a row; an
+// odd block count's last stage multiplies the zero pad (H + 0 is H).  64
+// accumulator registers instead of 192.  Measured and dropped on the way
+// (profiles/r6_gram_adapt/h1_ablation_kernels.txt): one workgroup whose waves
+// both feed the ring and store (each tile then waits on its own stores:
+// 6.32 ms), the split rows' h halves as operands (half of every fetched line
+// unused: 7.32 ms), deferring a tile's stores into the next tile's ring (spills,
+// 10.3 ms), two workgroups per CU of 128 x 64 waves over 32-k stages (8.5 ms),
+// staggered workgroup starts (no change).
 // tile_hot [ntiles] (zeroed): per-tile report counts; hot[0] (zeroed) the
 // list's length, hot[1 ..] the reported tiles' table entries.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void h1_row_dma(const float* __restrict__ Asq, const float* __restrict__ Bsq,
-                                           const int32_t* __restrict__ Ash, const int32_t* __restrict__ Bsh,
-                                           const float* __restrict__ Ar, const float* __restrict__ Br, int M, int N,
-                                           uint32_t* s_rows, int wave, int lane, int m0, int n0, int par) {
-  constexpr int TM = 256, ROWS = 384, RD = 1536;  // |x|^2 [ROWS], shifts [ROWS], log2 |x| [ROWS], padding
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int d0 = __builtin_amdgcn_readfirstlane(64 * (3 * wave + i));
-    const int kind = d0 / ROWS;  // uniform: 0 |x|^2, 1 shifts, 2 log2 |x|, 3 padding
-    const int r0 = d0 - (kind < 3 ? kind : 0) * ROWS;
-    const bool a_rows = r0 < TM;
-    const uint32_t* arr = kind == 0   ? (a_rows ? (const uint32_t*)Asq : (const uint32_t*)Bsq)
-                          : kind == 1 ? (a_rows ? (const uint32_t*)Ash : (const uint32_t*)Bsh)
-                                      : (a_rows ? (const uint32_t*)Ar : (const uint32_t*)Br);
-    const int r = r0 + lane;
-    const int ri = a_rows ? min(m0 + r, M - 1) : min(n0 + (r - TM), N - 1);
-    const uint32_t* src = kind == 3 ? (const uint32_t*)Asq : arr + ri;  // padding: any valid address
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(s_rows + par * RD + d0),
-                                     4, 0, 0);
-  }
-}
-
 // the one-product epilogue's math: H becomes K1 = exp2(t1) in place; returns
 // (wave-uniform) whether any of the wave's elements is hot
 __device__ __forceinline__ bool h1_values(f16v (&H)[2][2], const float* s_sq, const int32_t* s_sh, const float* s_r,
@@ -1946,202 +1930,6 @@ __device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int 
   }
 }
 
-// The one-product pass: every tile's stores, then vmcnt(0).  (Measured and
-// dropped: the values held in registers and stored in four 20-store chunks
-// behind the next tile's ring stages 0..3, the waits counting them — 10.3 vs
-// 7.2 ms: 33 dwords spilled and the interleaved stores slowed the ring; and
-// two workgroups per CU of four 128 x 64 waves over a ring of 32-k stages,
-// 78 KiB of LDS each — 8.5 vs 7.2 ms: the same bytes in flight per CU and
-// twice the barriers; odd workgroups started 4-12 us late so half the CUs
-// multiply while the others store — no change, 6.95-7.00 ms;
-// profiles/r6_gram_adapt/h1_ablation_kernels.txt.)
-// HP: A / B are h planes (split_hplane: the h halves of a row's split blocks
-// back to back, padded to an even block count with zeros) — a ring stage is one
-// whole 128-B line per row, where the split rows give every line's h half only
-// (half of each L2 line fetched unused).
-template <int ABL = 0, bool HP = false>
-__global__ __launch_bounds__(kW64Threads, 1) void rbf_gemm_split_h1_kernel(
-    const u4* __restrict__ A, const int32_t* __restrict__ Ash, const float* __restrict__ Asq,
-    const float* __restrict__ Ar, int M, const u4* __restrict__ B, const int32_t* __restrict__ Bsh,
-    const float* __restrict__ Bsq, const float* __restrict__ Br, int N, int nkb, float gamma, float c0, float c1,
-    float* __restrict__ out, int ldo, int sym, const uint32_t* __restrict__ tiles, int ntiles,
-    uint32_t* __restrict__ tile_hot, uint32_t* __restrict__ hot) {
-  constexpr int WN = 2, TM = 256, TN = 128, ROWS = TM + TN, CPR = 8, BUF = ROWS * CPR, NB = 3;
-  constexpr int RD = 1536;
-  __shared__ u4 lds[NB * BUF + 2 * RD / 4];  // 3 operand buffers, then row data [2][RD]
-  uint32_t* const s_rows = (uint32_t*)(lds + NB * BUF);
-  const int G = gridDim.x;
-  int L = blockIdx.x;
-  if (L >= ntiles) return;  // uniform
-  uint32_t t = tiles[L];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN, hl = lane >> 5;
-  const int nst = (nkb + 1) >> 1;  // ring stages a tile (launcher: nkb >= 5)
-  const uint32_t rs = HP ? (uint32_t)nst * 8 : (uint32_t)nkb * 8;  // u4 per operand row
-  const bool odd = (nkb & 1) != 0;
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  const uint32_t step = 8 * rs;
-  // lane byte offsets of a piece (even / odd pieces: swizzle lane >> 4 / (lane >> 4) + 4, as w64p);
-  // _t: an odd block count's last stage (split rows: virtual chunks 4..7 re-read block 2 s; h planes:
-  // the zero pad)
-  const int p = lane & 7, ve = p ^ (lane >> 4), vd = p ^ ((lane >> 4) + 4);
-  const uint32_t rowb = (uint32_t)(lane >> 3) * rs;
-  uint32_t off_e = 16u * (rowb + (uint32_t)(HP ? ve : (ve >> 2) * 8 + (ve & 3)));
-  uint32_t off_o = 16u * (rowb + (uint32_t)(HP ? vd : (vd >> 2) * 8 + (vd & 3)));
-  uint32_t off_et = HP ? off_e : 16u * (rowb + (uint32_t)(ve & 3));
-  uint32_t off_ot = HP ? off_o : 16u * (rowb + (uint32_t)(vd & 3));
-  asm volatile("" : "+v"(off_e), "+v"(off_o), "+v"(off_et), "+v"(off_ot));
-  const int dstA = 32 * wv * 8, dstB = (TM + 16 * wv) * 8;
-  int Ln = L + G;
-  uint32_t tn_next = Ln < ntiles ? tiles[Ln] : 0u;
-  int par = 0;
-  uint32_t g = 0;  // stages started over all of this workgroup's tiles: ring buffer g % NB
-  {
-    const int m0 = (int)(t >> 16) * TM, n0 = (int)(t & 0xffffu) * TN;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {  // stages 0 and 1 (never an odd tail: nst >= 3)
-      const uint32_t uA = (uint32_t)(m0 + 32 * wv) * rs + (uint32_t)b * (HP ? 8 : 16);
-      const uint32_t uB = (uint32_t)(n0 + 16 * wv) * rs + (uint32_t)b * (HP ? 8 : 16);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) w64p_piece(A, lds, uA, step, dstA, off_e, off_o, b, i);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) w64p_piece(B, lds, uB, step, dstB, off_e, off_o, b, i);
-    }
-    h1_row_dma(Asq, Bsq, Ash, Bsh, Ar, Br, M, N, s_rows, wave, lane, m0, n0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  const int sw = ((lane & 31) >> 1) & 7;
-  const int ra0 = (wm * 64 + (lane & 31)) * CPR;
-  const int rb0 = (TM + wn * 64 + (lane & 31)) * CPR;
-  while (true) {
-    const bool has_next = Ln < ntiles;  // uniform
-    const int tx = (int)(t >> 16), ty = (int)(t & 0xffffu);
-    const int m0 = tx * TM, n0 = ty * TN;
-    const uint32_t tp = has_next ? tn_next : t;
-    const int nm0 = (int)(tp >> 16) * TM, nn0 = (int)(tp & 0xffffu) * TN;
-    f16v H[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) H[i][j][r] = 0.f;
-#pragma clang loop unroll(disable)
-    for (int s = 0; s < nst; ++s) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      // the prefetch slot: stage s + 2 of this tile or stage s + 2 - nst of the next
-      const bool own = s + 2 < nst;
-      const int ps = own ? s + 2 : s + 2 - nst;
-      const bool ptail = odd && ps == nst - 1;  // uniform
-      const uint32_t pe_ = ptail ? off_et : off_e, po_ = ptail ? off_ot : off_o;
-      const uint32_t uA = (uint32_t)((own ? m0 : nm0) + 32 * wv) * rs + (uint32_t)ps * (HP ? 8 : 16);
-      const uint32_t uB = (uint32_t)((own ? n0 : nn0) + 16 * wv) * rs + (uint32_t)ps * (HP ? 8 : 16);
-      const int pbuf = (int)((g + 2) % NB);
-      auto piece = [&](int j) {  // A0, A1, B0, A2, A3, B1
-        __builtin_amdgcn_sched_barrier(0);
-        if (j == 2 || j == 5) w64p_piece(B, lds, uB, step, dstB, pe_, po_, pbuf, j == 2 ? 0 : 1);
-        else w64p_piece(A, lds, uA, step, dstA, pe_, po_, pbuf, j < 2 ? j : j - 1);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      const u4* buf = lds + (g % NB) * BUF;
-      const uint32_t abase = lds_addr(buf + ra0), bbase = lds_addr(buf + rb0);
-      // k step q's fragments: A rows (+ 32), B rows (+ 32) of virtual chunk 2 q + hl
-      auto rd = [&](int q, h8& a0, h8& a1, h8& b0, h8& b1) {
-        const uint32_t c = 16u * (uint32_t)((2 * q + hl) ^ sw);
-        const uint32_t pa = abase + c, pb = bbase + c;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(a0) : "v"(pa) : "memory");
-        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(a1) : "v"(pa) : "memory");
-        asm volatile("ds_read_b128 %0, %1" : "=v"(b0) : "v"(pb) : "memory");
-        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(b1) : "v"(pb) : "memory");
-      };
-      auto mma = [&](const h8& a0, const h8& a1, const h8& b0, const h8& b1) {
-        if (ABL == 3) return;
-        H[0][0] = mfma32_f16(a0, b0, H[0][0]);
-        H[0][1] = mfma32_f16(a0, b1, H[0][1]);
-        H[1][0] = mfma32_f16(a1, b0, H[1][0]);
-        H[1][1] = mfma32_f16(a1, b1, H[1][1]);
-      };
-      // two fragment sets: a set is re-read right after the MFMAs that read it
-      h8 x0, x1, x2, x3, y0, y1, y2, y3;
-      const bool tail = odd && s == nst - 1;  // uniform
-      rd(0, x0, x1, x2, x3);
-      rd(1, y0, y1, y2, y3);
-      if (!tail) {
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
-        mma(x0, x1, x2, x3);
-        piece(0);
-        piece(1);
-        rd(2, x0, x1, x2, x3);
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
-        mma(y0, y1, y2, y3);
-        piece(2);
-        piece(3);
-        rd(3, y0, y1, y2, y3);
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
-        mma(x0, x1, x2, x3);
-        piece(4);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
-        mma(y0, y1, y2, y3);
-        piece(5);
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
-        mma(x0, x1, x2, x3);
-        piece(0);
-        piece(1);
-        piece(2);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
-        mma(y0, y1, y2, y3);
-        piece(3);
-        piece(4);
-        piece(5);
-      }
-      ++g;
-    }
-    if (has_next) h1_row_dma(Asq, Bsq, Ash, Bsh, Ar, Br, M, N, s_rows, wave, lane, nm0, nn0, par ^ 1);
-    int el = lane;
-    asm volatile("" : "+v"(el));
-    const float* rows = (const float*)(s_rows + par * RD);
-    const bool hotw = h1_values(H, rows, (const int32_t*)(rows + ROWS), rows + 2 * ROWS, el, wm, wn, gamma, c0, c1);
-    if (hotw && lane == 0) {  // the tile's first report appends it to the list
-      if (atomicAdd(tile_hot + L, 1u) == 0u) {
-        const uint32_t k = atomicAdd(hot, 1u);
-        hot[1 + k] = t;
-      }
-    }
-    const bool mirror = sym && ty > 2 * tx + (wm >> 1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) h1_store_block<ABL>(H[i][j], i, j, el, wm, wn, mirror, true, out, m0, n0, M, N, ldo);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!has_next) break;
-    L = Ln;
-    t = tn_next;
-    par ^= 1;
-    Ln = L + G;
-    if (Ln < ntiles) tn_next = tiles[Ln];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// One-product pass with specialised waves (h1s, the default): the h1 kernel's
-// eight 64 x 64 compute waves plus four DMA waves (768 threads).  In h1 every
-// wave both feeds the LDS-DMA ring and stores its tile, and gfx950 counts
-// both in one in-order vmcnt: each tile ends waiting on its own stores before
-// the ring can go on.  Here only the DMA waves issue loads and wait on vmcnt
-// (h1s_dma, a function of its own so its addressing does not crowd the
-// compute waves' scalar registers); the compute waves never wait on a load,
-// so a tile's stores drain while the next tile multiplies.  The two meet at
-// one barrier per ring stage: the DMA waves have waited for stage s, the
-// compute waves have read stage s - 1, whose buffer the DMA waves then refill
-// with stage s + 2; row data of tile t + 1 is loaded during tile t's stage 0.
-// Operands: h planes.  6.10 vs 6.32 ms symmetric, 1.11 vs 1.13 ms slab
-// (profiles/r6_gram_adapt/h1_ablation_kernels.txt): the stores' cost is their
-// bytes more than their latency.  Same H sequence per element.
-// ---------------------------------------------------------------------------
 // the h1s kernel's DMA waves (a function of its own: its uniform addressing
 // does not share the compute waves' scalar registers)
 __device__ __noinline__ void h1s_dma(const u4* __restrict__ A, const int32_t* __restrict__ Ash,
@@ -2999,27 +2787,13 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
           }
           post_launch("split_hplane", s);
         }
-        static const bool h1_spec = [] {  // A/B: DPSVM_H1_SPEC=0 the h1 kernel (every wave loads and stores)
-          const char* e = std::getenv("DPSVM_H1_SPEC");
-          return !(e && e[0] == '0');
-        }();
-        if (h1_spec) {
-          auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1s_kernel<1>
-                     : h1_abl == 2 ? dev::rbf_gemm_split_h1s_kernel<2>
-                     : h1_abl == 3 ? dev::rbf_gemm_split_h1s_kernel<3>
-                                   : dev::rbf_gemm_split_h1s_kernel<0>;
-          h1k<<<dim3((unsigned)grid), dev::kH1sThreads, 0, s>>>(
-              (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1,
-              out, (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
-        } else {
-          auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1_kernel<1, true>
-                     : h1_abl == 2 ? dev::rbf_gemm_split_h1_kernel<2, true>
-                     : h1_abl == 3 ? dev::rbf_gemm_split_h1_kernel<3, true>
-                                   : dev::rbf_gemm_split_h1_kernel<0, true>;
-          h1k<<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
-              (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1,
-              out, (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
-        }
+        auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1s_kernel<1>
+                   : h1_abl == 2 ? dev::rbf_gemm_split_h1s_kernel<2>
+                   : h1_abl == 3 ? dev::rbf_gemm_split_h1s_kernel<3>
+                                 : dev::rbf_gemm_split_h1s_kernel<0>;
+        h1k<<<dim3((unsigned)grid), dev::kH1sThreads, 0, s>>>(
+            (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1, out,
+            (int)ldo, symmetric ? 1 : 0, t1.dev, (int)ntiles, hb, hb + ntiles);
         if (planes) HIP_CHECK(hipFreeAsync(planes, s));
         post_launch("rbf_gemm_split_h1", s);
         dev::rbf_gemm_split_w64p_kernel<0, true, true><<<dim3((unsigned)grid), dev::kW64Threads, 0, s>>>(
