@@ -1,4 +1,4 @@
-"""Adaptive split Gram (rbf_gemm_split.hip: rbf_gemm_split_h1_kernel + the
+"""Adaptive split Gram (rbf_gemm_split.hip: rbf_gemm_split_h1s_kernel + the
 w64p hot-tile pass; docs/DESIGN.md §13): the one-product value where
 split_cold proves it within tau of the three-product one, the three-product
 value elsewhere.  Checked here against the three-product kernel (every element
