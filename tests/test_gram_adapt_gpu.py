@@ -124,3 +124,25 @@ def test_adaptive_gram_in_ws_solve_matches_three_product():
     assert abs(on.b_ - off.b_) <= 2e-3
     Xt, _ = synthetic("mnist", n=2000, seed=8)
     assert (np.sign(on.decision_function(Xt)) == np.sign(off.decision_function(Xt))).mean() >= 0.999
+
+
+def test_adaptive_gram_beyond_2_32_elements(K):
+    """More than 2^32 Gram elements (66,000 rows: 17.4 GB): the adaptive
+    kernels index tiles from 64-bit bases (rbf_gemm_store_split's idx_adapt).
+    Rows past element 2^32 match the three-product Gram within tau."""
+    free, _ = torch.cuda.mem_get_info()
+    if free < 48 << 30:
+        pytest.skip("needs ~40 GB of free device memory")
+    n = 66000
+    X, _ = synthetic("mnist", n=n, seed=9)
+    x = torch.from_numpy(X).cuda()
+    ka = K.rbf_gram(x, None, 0.25, split=True, cold_tau=TAU)
+    tiles, hot = K.gram_adapt_last()
+    assert tiles > 0 and 0 < hot < tiles
+    rows = torch.arange(n - 2048, n, device="cuda")  # past row 2^32 / ld ~ 65,000
+    top = ka[rows].clone()
+    del ka
+    torch.cuda.empty_cache()
+    k3 = K.rbf_gram(x, None, 0.25, split=True)
+    assert (top - k3[rows]).abs().max().item() <= TAU
+    assert torch.isfinite(top).all()
