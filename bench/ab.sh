@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B runner: one bench.py run per line of a spec file, "label | bench.py args",
+# A/B runner: one bench.py run per line of a spec file, "label | bench.py args"
+# or "label | bench.py args | VAR=value ..." (DPSVM_* A/B switches for that run),
 # each under its own time limit; a one-line digest per run goes to
 # gpurun_out/ab_$TAG.txt (full JSON lines to gpurun_out/ab_$TAG.jsonl).
 # Stops at the first failing run.
@@ -14,13 +15,13 @@ SPEC=$1
 out=gpurun_out/ab_$TAG.txt
 : > "$out"
 : > "gpurun_out/ab_$TAG.jsonl"
-while IFS='|' read -r label args; do
+while IFS='|' read -r label args envs; do
   label=$(echo "$label" | xargs)
   [ -z "$label" ] && continue
   case "$label" in \#*) continue ;; esac
   log="gpurun_out/ab_${TAG}_${label}.log"
   # shellcheck disable=SC2086
-  timeout -k 10 "$LIMIT" python -u bench.py $args > "$log" 2>&1
+  timeout -k 10 "$LIMIT" env $envs python -u bench.py $args > "$log" 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then
     echo "$label FAILED rc=$rc" | tee -a "$out"

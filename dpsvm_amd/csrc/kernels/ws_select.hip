@@ -376,9 +376,11 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
 // rows), and p1G = ceil(nl_max / 1024) groups x ks list slices fill the device.
 // TPP threads per partition x PARTS partitions = 1024 threads; a workgroup owns
 // 4 TPP columns (TPP 256: 1024 columns, four partitions — the default; TPP 512:
-// 2048 columns, two partitions — A/B, DPSVM_P1_COLS=2048)
+// 2048 columns, two partitions — A/B, DPSVM_P1_COLS=2048).  NT: the Gram rows
+// by non-temporal loads (each changed row is read once a round: no L2 / MALL
+// reuse to keep) — A/B, DPSVM_P1_NT
 constexpr int kP1Threads = 4 * kWsSelThreads;
-template <int TPP>
+template <int TPP, bool NT>
 __global__ __launch_bounds__(kP1Threads) void ws_pass1_v4_kernel(WsArgs a) {
   constexpr int PARTS = kP1Threads / TPP, CH = 12;  // 12 rows x 16 B in flight per thread
   constexpr int kP1Cols = 4 * TPP;                  // columns per workgroup
@@ -439,7 +441,10 @@ __global__ __launch_bounds__(kP1Threads) void ws_pass1_v4_kernel(WsArgs a) {
     for (int u = 0; u < CH; ++u) {
       const int kk = min(k0 + u, k_hi - 1);
       const float* row = a.gram + (int64_t)s_idx[kk] * a.ldg;
-      kv[u] = has ? *(const f4*)(row + j0) : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (NT)
+        kv[u] = has ? __builtin_nontemporal_load((const f4*)(row + j0)) : f4{0.f, 0.f, 0.f, 0.f};
+      else
+        kv[u] = has ? *(const f4*)(row + j0) : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
@@ -604,12 +609,24 @@ int ws_pass1_v4_cols() {
   return cols;
 }
 
+// the wide pass 1's Gram row loads: non-temporal (DPSVM_P1_NT=1) or default policy
+static bool ws_pass1_nt() {
+  static const bool nt = [] {
+    const char* e = std::getenv("DPSVM_P1_NT");
+    return e && atoi(e) == 1;
+  }();
+  return nt;
+}
+
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
   if (pass == 1 && a.p1v4) {
+    const dim3 g(a.p1G * std::max(1, a.ks));
     if (ws_pass1_v4_cols() == 2048)
-      dev::ws_pass1_v4_kernel<512><<<dim3(a.p1G * std::max(1, a.ks)), dev::kP1Threads, 0, s>>>(a);
+      dev::ws_pass1_v4_kernel<512, false><<<g, dev::kP1Threads, 0, s>>>(a);
+    else if (ws_pass1_nt())
+      dev::ws_pass1_v4_kernel<256, true><<<g, dev::kP1Threads, 0, s>>>(a);
     else
-      dev::ws_pass1_v4_kernel<256><<<dim3(a.p1G * std::max(1, a.ks)), dev::kP1Threads, 0, s>>>(a);
+      dev::ws_pass1_v4_kernel<256, false><<<g, dev::kP1Threads, 0, s>>>(a);
     post_launch("ws_pass1_v4", s);
   } else if (pass == 1) {
     ws_select_mode<1>(a, s);
