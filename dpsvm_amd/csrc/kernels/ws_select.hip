@@ -378,7 +378,7 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
 // 4 TPP columns (TPP 256: 1024 columns, four partitions — the default; TPP 512:
 // 2048 columns, two partitions — A/B, DPSVM_P1_COLS=2048).  NT: the Gram rows
 // by non-temporal loads (each changed row is read once a round: no L2 / MALL
-// reuse to keep) — A/B, DPSVM_P1_NT
+// reuse to keep; ws_pass1_nt picks it)
 constexpr int kP1Threads = 4 * kWsSelThreads;
 template <int TPP, bool NT>
 __global__ __launch_bounds__(kP1Threads) void ws_pass1_v4_kernel(WsArgs a) {
@@ -609,13 +609,19 @@ int ws_pass1_v4_cols() {
   return cols;
 }
 
-// the wide pass 1's Gram row loads: non-temporal (DPSVM_P1_NT=1) or default policy
-static bool ws_pass1_nt() {
-  static const bool nt = [] {
+// the wide pass 1's Gram row loads: non-temporal where the Gram is far larger
+// than the 256 MB MALL (> 1 GiB: the rows of a round are not read again before
+// they would be evicted) — headline 0.0170 -> 0.0160 s, same trajectory
+// (profiles/r6_p1_nt_ab.txt); default policy below, where a small Gram's rows
+// stay MALL-resident from round to round.  DPSVM_P1_NT=0 / 1 forces it.
+static bool ws_pass1_nt(const WsArgs& a) {
+  static const int env = [] {
     const char* e = std::getenv("DPSVM_P1_NT");
-    return e && atoi(e) == 1;
+    return e ? atoi(e) : -1;
   }();
-  return nt;
+  if (env == 0 || env == 1) return env == 1;
+  const int64_t lines = a.cache ? (int64_t)a.L : a.n;
+  return lines * a.ldg * (int64_t)sizeof(float) > (int64_t(1) << 30);
 }
 
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
@@ -623,7 +629,7 @@ void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
     const dim3 g(a.p1G * std::max(1, a.ks));
     if (ws_pass1_v4_cols() == 2048)
       dev::ws_pass1_v4_kernel<512, false><<<g, dev::kP1Threads, 0, s>>>(a);
-    else if (ws_pass1_nt())
+    else if (ws_pass1_nt(a))
       dev::ws_pass1_v4_kernel<256, true><<<g, dev::kP1Threads, 0, s>>>(a);
     else
       dev::ws_pass1_v4_kernel<256, false><<<g, dev::kP1Threads, 0, s>>>(a);
