@@ -1879,7 +1879,8 @@ __device__ __forceinline__ bool h1_values(f16v (&H)[2][2], const float* s_sq, co
 // 4-B stores per lane, and for a mirroring wave 4 transposed 16-B ones (plus,
 // on the last row tile, a partial quad's values one at a time); out-of-range
 // offsets where a value has no place (the hardware drops those).  ABL
-// (diagnostics): 1 every store dropped, 2 the mirrored ones.
+// (diagnostics): 1 every store dropped, 2 the mirrored ones; 4 (A/B): every
+// store with the non-temporal cache policy.
 template <int ABL = 0>
 __device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int lane, int wm, int wn, bool mirror,
                                                bool valid, float* out, int m0, int n0, int M, int N, int ldo) {
@@ -1898,13 +1899,14 @@ __device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int 
   const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mb, 0, (int)mb_bytes, 0x00020000);
   const int cl = wn * 64 + 32 * j + (lane & 31);
   const bool okc = valid && cl < clim && ABL != 1;
+  constexpr int CP = ABL == 4 ? 2 : 0;  // buffer-store cache policy: nt
   const int lr0 = wm * 64 + 32 * i + 4 * hl;
   const uint32_t vo = okc ? ((uint32_t)lr0 * ld + (uint32_t)cl) * 4u : OOB;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const float hv = v[r];
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hv), rs_o,
-                                          (int)(vo + (uint32_t)(8 * (r >> 2) + (r & 3)) * ld * 4u), 0, 0);
+                                          (int)(vo + (uint32_t)(8 * (r >> 2) + (r & 3)) * ld * 4u), 0, CP);
   }
   if (!(mirror && valid) || ABL == 2) return;  // uniform
   const bool okm = okc;
@@ -1918,13 +1920,13 @@ __device__ __forceinline__ void h1_store_block(const f16v& v, int i, int j, int 
     w.z = v[4 * q + 2];
     w.w = v[4 * q + 3];
     const uint32_t o = lr + 3 < rlim && okm ? vm + 32u * q : OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, w), rs_m, (int)o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, w), rs_m, (int)o, 0, CP);
     if (rlim < TM) {  // uniform: the last row tile — a partial quad's values one at a time
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const uint32_t oc = (okm && lr + 3 >= rlim && lr + c < rlim) ? vm + 32u * q + 4u * c : OOB;
         const float vc = w[c];
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vc), rs_m, (int)oc, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vc), rs_m, (int)oc, 0, CP);
       }
     }
   }
@@ -2790,6 +2792,7 @@ void rbf_gemm_store_split(const void* A, const int32_t* Ash, const float* Asq, i
         auto h1k = h1_abl == 1   ? dev::rbf_gemm_split_h1s_kernel<1>
                    : h1_abl == 2 ? dev::rbf_gemm_split_h1s_kernel<2>
                    : h1_abl == 3 ? dev::rbf_gemm_split_h1s_kernel<3>
+                   : h1_abl == 4 ? dev::rbf_gemm_split_h1s_kernel<4>
                                  : dev::rbf_gemm_split_h1s_kernel<0>;
         h1k<<<dim3((unsigned)grid), dev::kH1sThreads, 0, s>>>(
             (const dev::u4*)hA, Ash, Asq, r, (int)M, (const dev::u4*)hB, Bsh, Bsq, br, (int)N, nkb, gamma, c0, c1, out,

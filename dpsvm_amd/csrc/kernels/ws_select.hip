@@ -380,9 +380,9 @@ __global__ __launch_bounds__((kWsSelThreads * ws_sel_parts<RPT, MODE>())) void w
 // by non-temporal loads (each changed row is read once a round: no L2 / MALL
 // reuse to keep; ws_pass1_nt picks it)
 constexpr int kP1Threads = 4 * kWsSelThreads;
-template <int TPP, bool NT>
+template <int TPP, bool NT, int CH = 12>  // CH rows x 16 B in flight per thread
 __global__ __launch_bounds__(kP1Threads) void ws_pass1_v4_kernel(WsArgs a) {
-  constexpr int PARTS = kP1Threads / TPP, CH = 12;  // 12 rows x 16 B in flight per thread
+  constexpr int PARTS = kP1Threads / TPP;
   constexpr int kP1Cols = 4 * TPP;                  // columns per workgroup
   __shared__ int32_t s_idx[kWsMaxAll];
   __shared__ float s_coef[kWsMaxAll];
@@ -624,11 +624,25 @@ static bool ws_pass1_nt(const WsArgs& a) {
   return lines * a.ldg * (int64_t)sizeof(float) > (int64_t(1) << 30);
 }
 
+// rows in flight per thread of the non-temporal wide pass 1 (A/B: DPSVM_P1_CH=8 / 16)
+static int ws_pass1_ch() {
+  static const int ch = [] {
+    const char* e = std::getenv("DPSVM_P1_CH");
+    const int v = e ? atoi(e) : 12;
+    return v == 8 || v == 16 ? v : 12;
+  }();
+  return ch;
+}
+
 void ws_select_pass(const WsArgs& a, int pass, hipStream_t s) {
   if (pass == 1 && a.p1v4) {
     const dim3 g(a.p1G * std::max(1, a.ks));
     if (ws_pass1_v4_cols() == 2048)
       dev::ws_pass1_v4_kernel<512, false><<<g, dev::kP1Threads, 0, s>>>(a);
+    else if (ws_pass1_nt(a) && ws_pass1_ch() == 16)
+      dev::ws_pass1_v4_kernel<256, true, 16><<<g, dev::kP1Threads, 0, s>>>(a);
+    else if (ws_pass1_nt(a) && ws_pass1_ch() == 8)
+      dev::ws_pass1_v4_kernel<256, true, 8><<<g, dev::kP1Threads, 0, s>>>(a);
     else if (ws_pass1_nt(a))
       dev::ws_pass1_v4_kernel<256, true><<<g, dev::kP1Threads, 0, s>>>(a);
     else
